@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""FrameTiling throughput on MI355X (BASELINE.json metric), one process per GPU.
+
+A step = DoFrameTiling (main.pas:3992-4047) over one keyframe batch of synthetic 1080p frames:
+query PsyV descriptors (fp64 Haar -> fp32) + exact NN against the keyframe's 262,144 mirror
+candidates of a 64k tileset + tilemap items, all inputs resident in HBM before timing starts.
+Weak scaling: every rank tiles its own keyframe (keyframes are independent, main.pas:4005-4011);
+there is no data-path collective.  The tileset is broadcast once from rank 0 (RCCL) before timing.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline` for the
+dominant kernel (nn_shortlist: MFMA) and a bounded `cpu_baseline` of the oracle on the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "FrameTiling Mtiles/sec @1080p 8×8, 64k tileset; % HBM roofline at 1/2/4/8 GPU"
+PEAK_F16_TFLOPS = 2500.0   # MI355X dense fp16 MFMA (MI355X_MICROARCH.md; sparsity excluded)
+PEAK_HBM_GBS = 8000.0
+
+CONFIGS = {
+    # name: (width, height, frames per keyframe step, tileset size)
+    "c3": (1920, 1080, 24, 65536),
+    "c2": (1280, 720, 24, 16384),
+    "c5": (3840, 2160, 24, 262144),
+    "tiny": (320, 240, 4, 2048),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (rank 0)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, visible cores)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    import tiler_amd
+    from tiler_amd import synth
+    from tiler_amd._lib import check
+
+    lib = tiler_amd.load()
+    check(lib.tiler_init(local), "tiler_init")
+
+    W, H, F, TS = CONFIGS[args.config]
+    Q = (W // 8) * (H // 8)
+    P = 128
+
+    # ---- global tileset + palettes: generated on rank 0, all-gathered (broadcast) over RCCL ----
+    rng0 = np.random.default_rng(args.seed)
+    if rank == 0:
+        pals = synth.palettes(rng0, P)
+        tiles, thm, tvm = synth.tileset(rng0, TS)
+        tile_pal = rng0.integers(0, P, TS).astype(np.int32)
+        packed = np.concatenate([tiles.reshape(-1).astype(np.int32), thm.astype(np.int32), tvm.astype(np.int32),
+                                 tile_pal, pals.reshape(-1)])
+        t_packed = torch.from_numpy(packed).to(dev)
+    else:
+        t_packed = torch.empty(TS * 64 + 3 * TS + P * 16, dtype=torch.int32, device=dev)
+    if world > 1:
+        dist.broadcast(t_packed, 0)
+    packed = t_packed.cpu().numpy()
+    o = 0
+    tiles = packed[o:o + TS * 64].astype(np.uint8).reshape(TS, 64); o += TS * 64
+    thm = packed[o:o + TS].astype(np.uint8); o += TS
+    tvm = packed[o:o + TS].astype(np.uint8); o += TS
+    tile_pal = packed[o:o + TS].astype(np.int32); o += TS
+    pals = packed[o:o + P * 16].astype(np.int32).reshape(P, 16)
+    ds = synth.ft_dataset_from_used(synth.used_one_palette(tile_pal, P), thm, tvm)
+    M = ds.tile_of.size
+
+    # ---- this rank's keyframe (independent seed per rank) ----
+    rng = np.random.default_rng(args.seed + 1 + rank)
+    frames = synth.keyframe_frames(rng, F, Q)
+    d_rgb = torch.from_numpy(frames.reshape(-1, 64)).to(dev)
+    QK = d_rgb.shape[0]
+
+    # ---- keyframe dataset in HBM: candidate descriptors on the GPU (DoPsyV) + index ----
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    d_tiles = torch.from_numpy(tiles).to(dev)
+    d_pals = torch.from_numpy(pals).to(dev)
+    d_to = torch.from_numpy(ds.tile_of).to(dev)
+    d_po = torch.from_numpy(ds.pal_of).to(dev)
+    d_fl = torch.from_numpy(ds.psyv_flags).to(dev)
+    d_rows = torch.empty((M, 192), dtype=torch.float32, device=dev)
+    tiler_amd.psyv_batch_dev(M, palpix=d_tiles.data_ptr(), tile_of=d_to.data_ptr(), palettes=d_pals.data_ptr(),
+                             pal_of=d_po.data_ptr(), flags_per=d_fl.data_ptr(), flags=1 | 2, gamma=-1,
+                             out32=d_rows.data_ptr(), stream=stream)
+    torch.cuda.synchronize(dev)
+    kdt = tiler_amd.KDTree(dev_ptr=d_rows.data_ptr(), n=M, dd=192, stream=stream)
+    import ctypes
+    vp = ctypes.c_void_p
+    check(lib.tiler_ft_set_maps(kdt.handle, ds.tile_of.ctypes.data_as(vp), ds.pal_of.ctypes.data_as(vp),
+                                ds.attrs.ctypes.data_as(vp)), "tiler_ft_set_maps")
+    torch.cuda.synchronize(dev)
+
+    out_tile = torch.empty(QK, dtype=torch.int32, device=dev)
+    out_pal = torch.empty(QK, dtype=torch.int32, device=dev)
+    out_hm = torch.empty(QK, dtype=torch.uint8, device=dev)
+    out_vm = torch.empty(QK, dtype=torch.uint8, device=dev)
+    out_err = torch.empty(QK, dtype=torch.float32, device=dev)
+
+    def step():
+        check(lib.tiler_frame_tiling_dev(kdt.handle, vp(d_rgb.data_ptr()), QK, 1, -1, vp(out_tile.data_ptr()),
+                                         vp(out_pal.data_ptr()), vp(out_hm.data_ptr()), vp(out_vm.data_ptr()),
+                                         vp(out_err.data_ptr()), vp(stream)), "tiler_frame_tiling_dev")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    lib.tiler_timing_reset()
+    lib.tiler_timing_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lib.tiler_timing_enable(0)
+    kernels = {}
+    for name in ("psyv", "nn_prep", "nn_shortlist", "nn_rescore", "nn_exact"):
+        n = ctypes.c_int(0)
+        ms = lib.tiler_timing_get(name.encode(), ctypes.byref(n))
+        kernels[name] = {"ms_total": round(ms, 4), "launches": n.value,
+                         "ms_avg": round(ms / n.value, 4) if n.value else None}
+    stats = kdt.stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_tiles = QK * args.steps * world
+    value = total_tiles / elapsed / 1e6
+
+    # ---- roofline of the dominant kernel (MFMA shortlist), per launch ----
+    sl = kernels["nn_shortlist"]
+    flops_launch = 2.0 * M * 192 * QK            # 2*M*D per matched tile
+    achieved = flops_launch / (sl["ms_avg"] * 1e-3) / 1e12 if sl["ms_avg"] else None
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None, "peak": PEAK_F16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
+                "traffic": None, "kernel": "nn_shortlist_kernel<12,4,2>",
+                "note": "algorithmic 2*M*D per tile vs dense fp16 MFMA peak; 1 fp16 product per pair"}
+
+    # ---- CPU baseline (rank 0, N=1): the oracle restatement, bounded sample, same workload ----
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out_hm, out_vm, out_err)
+
+    if rank == 0:
+        res = {
+            "metric": METRIC, "value": round(value, 4), "unit": "Mtiles/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded, SURVEY.md 8(d))",
+            "config": {"workload": f"{args.config.upper()}: {W}x{H} 8x8 tiles ({Q} tiles/frame), keyframe of {F} "
+                                   f"frames per GPU per step, {TS} tileset x 4 mirrors = {M} candidates (P_eff=1)",
+                       "tiles_per_step_per_gpu": QK, "candidates": M, "descriptor": "PsyV Haar 192-d",
+                       "parallelism": f"keyframes sharded, {world} GPU(s)"},
+            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "search_stats": stats,
+        }
+        print(json.dumps(res))
+    kdt.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out_hm, out_vm, out_err):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    P, T = pals.shape[0], tiles.shape[0]
+    used = np.zeros((P, T, 4), np.uint8)
+    used[ds.pal_of, ds.tile_of, ds.attrs] = 1
+    ods, ot, op, oa = pyoracle.build_ft_dataset(used, tiles, thm, tvm, pals)
+    q0 = frames.reshape(-1, 64)
+    g = [t.cpu().numpy() for t in (out_tile, out_pal, out_hm, out_vm, out_err)]
+    done, chunk, spent = 0, 4 * threads, 0.0
+    mism = 0
+    while spent < args.cpu_seconds and done < q0.shape[0]:
+        sl = slice(done, min(done + chunk, q0.shape[0]))
+        t0 = time.perf_counter()
+        o = pyoracle.frame_tiling(q0[sl], ods, ot, op, oa, threads=threads)
+        spent += time.perf_counter() - t0
+        for a, b in zip(g, o):
+            mism += int(np.count_nonzero(np.asarray(a[sl]).view(np.uint8) != np.asarray(b).view(np.uint8)))
+        done = sl.stop
+    return {"value": round(done / spent / 1e6, 6), "unit": "Mtiles/s", "cores": threads, "kind": "port",
+            "sample": f"first {done} query tiles of the keyframe vs the full {ods.shape[0]}-candidate set "
+                      f"(oracle/tiler_oracle.c exhaustive fp32 scan with ANN's early break, {threads} threads)",
+            "parity_mismatches_vs_gpu": mism}
+
+
+if __name__ == "__main__":
+    main()

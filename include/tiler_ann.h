@@ -1,0 +1,118 @@
+/*
+ * tiler_ann.h -- C-ABI of libANN.so, the MI355X-native drop-in for the reference's ANN.dll
+ * boundary plus batched/device extensions for the FrameTiling, Smooth and GlobalTiling hot path.
+ *
+ * Reference interface replaced (b0nefish/tiler, /root/reference):
+ *   extern.pas:63  function ann_kdtree_create(pa: PPANNFloat; n, dd, bs: Integer; split: TANNsplitRule): PANNkdtree; cdecl;
+ *   extern.pas:64  procedure ann_kdtree_destroy(akd: PANNkdtree); cdecl;
+ *   extern.pas:65  function ann_kdtree_search(akd: PANNkdtree; q: PANNFloat; eps: TANNFloat; err: PANNFloat): Integer; cdecl;
+ *   extern.pas:66  function ann_kdtree_pri_search(akd: PANNkdtree; q: PANNFloat; eps: TANNFloat; err: PANNFloat): Integer; cdecl;
+ *   extern.pas:67  function ann_kdtree_search_multi(akd: PANNkdtree; idxs: PInteger; errs: PANNFloat; cnt: Integer;
+ *                                                    q: PANNFloat; eps: TANNFloat): Integer; cdecl;
+ * Types: TANNFloat = Single (extern.pas:30), Integer = int32, TANNsplitRule = int32 enum (extern.pas:21-28).
+ *
+ * Semantics kept from ANN 1.1.2: exact nearest neighbours of the fp32
+ * squared distance accumulated in dimension order with every operation rounded (no FMA); err =
+ * squared distance (no sqrt); k results ascending.  Differences (superset behaviour):
+ *   - equal distances resolve to the LOWEST dataset index (ANN: first found in kd-tree order,
+ *     which no reference fixture pins: "parity unpinned" for ties);
+ *   - eps > 0 is accepted and ignored: the exact answer satisfies every eps bound;
+ *   - the dataset rows are copied to device memory at create (ANN borrows pa until destroy);
+ *   - no process abort: errors return -1 (or NULL) and tiler_last_error() explains;
+ *   - every entry point is thread-safe; concurrent calls on one handle are serialised.
+ * The search runs on the GPU only.  There is no CPU fallback: if the HIP runtime or a gfx950
+ * device is missing every call fails with -1 / NULL.
+ */
+#ifndef TILER_ANN_H
+#define TILER_ANN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ann_kdtree ann_kdtree; /* opaque */
+
+/* ---- the reference ANN.dll surface (extern.pas:63-67), symbol- and ABI-identical ---- */
+ann_kdtree *ann_kdtree_create(float **pa, int n, int dd, int bs, int split);
+void ann_kdtree_destroy(ann_kdtree *akd);
+int ann_kdtree_search(ann_kdtree *akd, float *q, float eps, float *err);
+int ann_kdtree_pri_search(ann_kdtree *akd, float *q, float eps, float *err);
+int ann_kdtree_search_multi(ann_kdtree *akd, int *idxs, float *errs, int cnt, float *q, float eps);
+
+/* Create from fp32 rows already in HBM (d_rows[n][dd], copied); e.g. descriptors made by tiler_psyv_batch_dev. */
+ann_kdtree *ann_kdtree_create_dev(const float *d_rows, int n, int dd, void *stream);
+
+/* ---- batched extensions; host buffers, row-major q[nq][dd] ---- */
+/* k = 1 for every query: idx[nq], err[nq].  Returns 0 or -1. */
+int ann_kdtree_search_batch(ann_kdtree *akd, const float *q, int nq, float eps, int *idx, float *err);
+/* k results per query, ascending by (err, index): idxs[nq][k], errs[nq][k] (missing: -1 / FLT_MAX). k <= 32. */
+int ann_kdtree_search_multi_batch(ann_kdtree *akd, const float *q, int nq, int k, float eps, int *idxs, float *errs);
+/* Same with device-resident buffers (HBM) on a HIP stream (NULL = default stream); asynchronous. */
+int ann_kdtree_search_batch_dev(ann_kdtree *akd, const float *d_q, int nq, int k, int *d_idx, float *d_err,
+                                void *stream);
+
+/* Search statistics of the last call on this handle (shortlist sizes, exact fallbacks). */
+typedef struct {
+    int64_t queries;
+    int64_t fallback_queries; /* queries rescanned exactly because the MFMA shortlist overflowed */
+    int32_t exact_integer;    /* 1 when the dataset is small integers: MFMA keys are exact */
+    int32_t splits;           /* candidate splits used by the last launch */
+} tiler_search_stats;
+int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
+
+/* ---- runtime ---- */
+int tiler_init(int device);         /* optional; first call of any entry point initialises device 0 */
+int tiler_shutdown(void);
+const char *tiler_last_error(void); /* thread-local message of the last failure */
+int tiler_set_gamma(double g0, double g1); /* gGamma main.pas:586 / 1441-1447; rebuilds gGammaCorLut */
+/* Kernel timing with HIP events on the launching stream (bench/profiling): enable, then read the
+ * summed milliseconds and launch count of one kernel family ("psyv", "nn_prep", "nn_shortlist",
+ * "nn_rescore", "nn_exact", "smooth", "kmodes").  Reading synchronises the recorded events. */
+int tiler_timing_enable(int on);
+double tiler_timing_get(const char *kernel, int *launches);
+int tiler_timing_reset(void);
+
+/* ---- PsyV descriptor (ComputeTilePsyVisFeatures main.pas:2997-3177) ----
+ * flags: 1 FromPal, 2 UseWavelets, 8 QWeighting, 16 HMirror, 32 VMirror (UseLAB unsupported: off on the hot path).
+ * RGB mode: rgb[n][64] (0x00BBGGRR).  Pal mode: palpix[*][64] indexed by tile_of[i] (or i when NULL),
+ * palettes[*][16] indexed by pal_of[i] (or 0), per-item extra flags flags_per[i] (or NULL).
+ * gamma: -1 (r/255) or 0/1 (gGammaCorLut).  Outputs: out64[n][192] and/or out32[n][192]. */
+int tiler_psyv_batch(int n, const int32_t *rgb, int n_tiles, const uint8_t *palpix, const int32_t *tile_of, int n_palettes,
+                     const int32_t *palettes,
+                     const int32_t *pal_of, const uint8_t *flags_per, int flags, int gamma, double *out64, float *out32);
+/* device-pointer variant (every pointer in HBM); asynchronous on stream */
+int tiler_psyv_batch_dev(int n, const int32_t *rgb, const uint8_t *palpix, const int32_t *tile_of,
+                         const int32_t *palettes, const int32_t *pal_of, const uint8_t *flags_per, int flags, int gamma,
+                         double *out64, float *out32, void *stream);
+
+/* ---- FrameTiling (DoFrameTiling main.pas:3992-4047) ----
+ * Attach the keyframe dataset's row -> (tile, palette, attrs) maps (TTilingDataset.TRTo*, main.pas:181-189)
+ * to a handle created over the keyframe's candidate descriptors. */
+int tiler_ft_set_maps(ann_kdtree *akd, const int32_t *tr_tile, const int32_t *tr_pal, const uint8_t *tr_attr);
+/* For Q frame tiles (RGB): query descriptor (UseWavelets, gamma, no mirror) -> fp32 -> exact NN ->
+ * tilemap item {GlobalTileIndex, PalIdx, HMirror = attr&1, VMirror = attr&2} + err. Host buffers. */
+int tiler_frame_tiling(ann_kdtree *akd, const int32_t *rgb, int Q, int use_wavelets, int gamma, int32_t *out_tile,
+                       int32_t *out_pal, uint8_t *out_hm, uint8_t *out_vm, float *out_err);
+/* Same, every buffer in HBM, asynchronous on stream (the benchmarked path). */
+int tiler_frame_tiling_dev(ann_kdtree *akd, const int32_t *d_rgb, int Q, int use_wavelets, int gamma,
+                           int32_t *d_tile, int32_t *d_pal, uint8_t *d_hm, uint8_t *d_vm, float *d_err, void *stream);
+
+/* ---- Smooth (DoTemporalSmoothing main.pas:4071-4119 over one keyframe) ----
+ * Items are [F][Q] arrays (F frames of one keyframe, Q tilemap positions), updated in place exactly
+ * as btnSmoothClick does after SmoothedTileMap := TileMap.  palpix[T][64], palettes[P][16]. */
+int tiler_smooth_keyframe(int F, int Q, int32_t *tile, int32_t *tmpidx, int32_t *pal, uint8_t *hm, uint8_t *vm,
+                          uint8_t *smoothed, int T, const uint8_t *palpix, int P, const int32_t *palettes,
+                          double strength);
+
+/* ---- GlobalTiling K-Modes (TKModes.ComputeKModes kmodes.pas:917-1060) ----
+ * X[n][nattr] bytes; k clusters; start_point = -ANumInit (the DoKModes call, main.pas:4218); labels[n]
+ * (0-based), centroids[k][nattr].  Returns k or -1.  n_iter / cost optional. */
+int tiler_kmodes_compute(const uint8_t *X, int n, int nattr, int k, int start_point, int n_modalities,
+                         int32_t *labels, uint8_t *centroids, int *n_iter, uint64_t *cost);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,218 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of oracle/liboracle.so (the CPU restatement).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and only
+as the checker.  The product (tiler_amd / libANN.so) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+REF_LIB = os.path.join(HERE, "_ref", "libkmodes_ref.so")
+
+_o = None
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def lib():
+    global _o
+    if _o is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"{LIB} missing: run `make -C oracle` (or __graft_entry__.build())")
+        _o = ctypes.CDLL(LIB)
+        _o.or_km_dissim.restype = ctypes.c_uint64
+        _o.or_km_dissim_generic.restype = ctypes.c_uint64
+        _o.or_randint.restype = ctypes.c_uint32
+        _o.or_palette_corr.restype = ctypes.c_double
+        _o.or_dist.restype = ctypes.c_float
+        _o.or_set_gamma.argtypes = [ctypes.c_double, ctypes.c_double]
+        _o.or_smooth.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 8 + [ctypes.c_double]
+        _o.or_eqtc.argtypes = [ctypes.c_double]
+        _o.or_init()
+    return _o
+
+
+def psyv(rgb=None, palpix=None, pal=None, flags=0, gamma=-1):
+    out = np.zeros(192, np.float64)
+    rgb = None if rgb is None else np.ascontiguousarray(rgb, np.int32)
+    palpix = None if palpix is None else np.ascontiguousarray(palpix, np.uint8)
+    pal = None if pal is None else np.ascontiguousarray(pal, np.int32)
+    lib().or_psyv(_p(rgb), _p(palpix), _p(pal), flags, gamma, _p(out))
+    return out
+
+
+def psyv_batch(n, rgb=None, palpix=None, pals=None, pal_of=None, flags_per=None, flags=0, gamma=-1):
+    """pal mode: palpix is [n,64] (already gathered per item)."""
+    out = np.zeros((n, 192), np.float64)
+    a = [None if x is None else np.ascontiguousarray(x) for x in (rgb, palpix, pals, pal_of, flags_per)]
+    if a[0] is not None:
+        a[0] = a[0].astype(np.int32)
+    if a[1] is not None:
+        a[1] = a[1].astype(np.uint8)
+    if a[2] is not None:
+        a[2] = a[2].astype(np.int32)
+    if a[3] is not None:
+        a[3] = a[3].astype(np.int32)
+    if a[4] is not None:
+        a[4] = a[4].astype(np.uint8)
+    lib().or_psyv_batch(n, *[_p(x) for x in a], flags, gamma, _p(out))
+    return out
+
+
+def nn(data, q):
+    data = np.ascontiguousarray(data, np.float32)
+    q = np.ascontiguousarray(q, np.float32)
+    err = np.zeros(1, np.float32)
+    i = lib().or_nn(_p(data), data.shape[0], data.shape[1], _p(q), _p(err))
+    return i, float(err[0])
+
+
+def knn(data, q, k):
+    data = np.ascontiguousarray(data, np.float32)
+    q = np.ascontiguousarray(q, np.float32)
+    idx = np.zeros(k, np.int32)
+    err = np.zeros(k, np.float32)
+    lib().or_knn(_p(data), data.shape[0], data.shape[1], _p(q), k, _p(idx), _p(err))
+    return idx, err
+
+
+def nn_batch(data, qs, threads=None):
+    data = np.ascontiguousarray(data, np.float32)
+    qs = np.ascontiguousarray(qs, np.float32).reshape(-1, data.shape[1])
+    idx = np.zeros(qs.shape[0], np.int32)
+    err = np.zeros(qs.shape[0], np.float32)
+    lib().or_nn_batch(_p(data), data.shape[0], data.shape[1], _p(qs), qs.shape[0], _p(idx), _p(err),
+                      threads or (os.cpu_count() or 1))
+    return idx, err
+
+
+def build_ft_dataset(used, palpix, thm, tvm, palettes, use_wavelets=True, gamma=-1):
+    used = np.ascontiguousarray(used, np.uint8)
+    P, T, _ = used.shape
+    cnt = int(used.sum())
+    ds = np.zeros((max(cnt, 1), 192), np.float32)
+    tidx = np.zeros(max(cnt, 1), np.int32)
+    pidx = np.zeros(max(cnt, 1), np.int32)
+    attrs = np.zeros(max(cnt, 1), np.uint8)
+    n = lib().or_build_ft_dataset(_p(used), P, T, _p(np.ascontiguousarray(palpix, np.uint8)),
+                                  _p(np.ascontiguousarray(thm, np.uint8)), _p(np.ascontiguousarray(tvm, np.uint8)),
+                                  _p(np.ascontiguousarray(palettes, np.int32)), int(use_wavelets), gamma, _p(ds),
+                                  _p(tidx), _p(pidx), _p(attrs))
+    return ds[:n], tidx[:n], pidx[:n], attrs[:n]
+
+
+def frame_tiling(frame_rgb, ds, tidx, pidx, attrs, use_wavelets=True, gamma=-1, threads=None):
+    rgb = np.ascontiguousarray(frame_rgb, np.int32).reshape(-1, 64)
+    Q = rgb.shape[0]
+    out = [np.zeros(Q, np.int32), np.zeros(Q, np.int32), np.zeros(Q, np.uint8), np.zeros(Q, np.uint8),
+           np.zeros(Q, np.float32)]
+    lib().or_frame_tiling(_p(rgb), Q, _p(np.ascontiguousarray(ds, np.float32)), ds.shape[0], _p(tidx), _p(pidx),
+                          _p(attrs), int(use_wavelets), gamma, threads or (os.cpu_count() or 1), *[_p(o) for o in out])
+    return tuple(out)
+
+
+def prepare_global_ds(palpix, active=None):
+    palpix = np.ascontiguousarray(palpix, np.uint8)
+    T = palpix.shape[0]
+    active = np.ones(T, np.uint8) if active is None else np.ascontiguousarray(active, np.uint8)
+    ds = np.zeros((4 * T, 64), np.float32)
+    ti = np.zeros(4 * T, np.int32)
+    at = np.zeros(4 * T, np.uint8)
+    n = lib().or_prepare_global_ds(_p(palpix), _p(active), T, _p(ds), _p(ti), _p(at))
+    return ds[:n], ti[:n], at[:n]
+
+
+def palette_corr(centroids):
+    c = np.ascontiguousarray(centroids, np.float64)
+    P = c.shape[0]
+    corr = np.zeros((P, P), np.float64)
+    hi = lib().or_palette_corr(_p(c), P, _p(corr))
+    return corr, hi
+
+
+def mark_used(gds, g_tile, g_attr, item_pal, item_tile, palpix, P, quality, corrs=None, highest=0.0, paltol=0.05):
+    palpix = np.ascontiguousarray(palpix, np.uint8)
+    T = palpix.shape[0]
+    used = np.zeros((P, T, 4), np.uint8)
+    corrs = np.zeros((P, P)) if corrs is None else np.ascontiguousarray(corrs, np.float64)
+    item_pal = np.ascontiguousarray(item_pal, np.int32)
+    item_tile = np.ascontiguousarray(item_tile, np.int32)
+    f = lib().or_mark_used
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                  ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+    f(_p(np.ascontiguousarray(gds, np.float32)), gds.shape[0], _p(np.ascontiguousarray(g_tile, np.int32)),
+      _p(np.ascontiguousarray(g_attr, np.uint8)), _p(item_pal), _p(item_tile), item_pal.size, _p(palpix), T, P,
+      quality, _p(corrs), highest, paltol, _p(used))
+    return used
+
+
+def smooth(tile, pal, hm, vm, smoothed, palpix, palettes, strength=0.02, tmpidx=None):
+    """In place on copies; arrays [F, Q]."""
+    tile = np.array(tile, np.int32, copy=True)
+    pal = np.array(pal, np.int32, copy=True)
+    hm = np.array(hm, np.uint8, copy=True)
+    vm = np.array(vm, np.uint8, copy=True)
+    smoothed = np.array(smoothed, np.uint8, copy=True)
+    tmp = None if tmpidx is None else np.array(tmpidx, np.int32, copy=True)
+    F, Q = tile.shape
+    lib().or_smooth(F, Q, _p(tile), _p(tmp), _p(pal), _p(hm), _p(vm), _p(smoothed),
+                    _p(np.ascontiguousarray(palpix, np.uint8)), _p(np.ascontiguousarray(palettes, np.int32)),
+                    strength)
+    return tile, pal, hm, vm, smoothed, tmp
+
+
+def km_dissim(row, item):
+    return int(lib().or_km_dissim(_p(np.ascontiguousarray(row, np.uint8)), _p(np.ascontiguousarray(item, np.uint8))))
+
+
+def km_get_min(rows, item):
+    rows = np.ascontiguousarray(rows, np.uint8)
+    best = ctypes.c_uint64()
+    i = lib().or_km_get_min(_p(rows), rows.shape[0], _p(np.ascontiguousarray(item, np.uint8)), ctypes.byref(best))
+    return i, best.value
+
+
+def kmodes(X, k, start, modalities=16):
+    X = np.ascontiguousarray(X, np.uint8)
+    n, a = X.shape
+    labels = np.zeros(n, np.int32)
+    cent = np.zeros((k, a), np.uint8)
+    it = ctypes.c_int()
+    cost = ctypes.c_uint64()
+    lib().or_kmodes(_p(X), n, a, k, start, modalities, _p(labels), _p(cent), ctypes.byref(it), ctypes.byref(cost))
+    return labels, cent, it.value, cost.value
+
+
+def randint(rng_range, seed):
+    s = ctypes.c_uint32(seed)
+    r = lib().or_randint(ctypes.c_uint32(rng_range), ctypes.byref(s))
+    return r, s.value
+
+
+def global_tiling(palpix, dith_pal, P, desired, palsize=16, restart=7, use_count=None):
+    palpix = np.array(palpix, np.uint8, copy=True)
+    T = palpix.shape[0]
+    active = np.ones(T, np.uint8)
+    uc = np.ones(T, np.int32) if use_count is None else np.array(use_count, np.int32, copy=True)
+    mi = np.full(T, -1, np.int32)
+    kpb = np.zeros(P, np.int32)
+    lib().or_global_tiling(T, _p(palpix), _p(active), _p(uc), _p(mi), _p(np.ascontiguousarray(dith_pal, np.int32)), P,
+                           palsize, desired, restart, _p(kpb))
+    return palpix, active, uc, mi, kpb
+
+
+def ref_kmodes_lib():
+    """The reference's own asm (kmodes.pas:316-596) if oracle/_ref was built here; else None."""
+    if not os.path.exists(REF_LIB):
+        return None
+    r = ctypes.CDLL(REF_LIB)
+    r.ref_get_min.restype = ctypes.c_int64
+    return r

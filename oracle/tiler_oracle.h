@@ -1,0 +1,88 @@
+/*
+ * tiler_oracle.h -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * CPU restatement of the b0nefish/tiler tile-search hot path (FrameTiling, Smooth,
+ * GlobalTiling K-Modes).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library.  The product path (libANN.so) never links it.
+ *
+ * Every function cites the reference file:line it restates.  Numeric rules:
+ *   - fp64 descriptor math in source order, no FMA contraction (-ffp-contract=off);
+ *   - fp32 ANN distances: t = q-c; dist = dist + t*t, each op rounded (ANN.dll leaf scan);
+ *   - K-Modes dissimilarity as the x86-64 asm actually computes it (kmodes.pas:316-453).
+ *
+ * Parity pins: the K-Modes dissimilarity / argmin / min-distance update are pinned against
+ * the reference's own asm assembled from kmodes.pas (oracle/build_ref_asm.sh -> oracle/_ref).
+ * The descriptor, FT and Smooth paths have no reference fixture (no FPC, ANN.dll is a PE):
+ * they are pinned by known-answer tests (tests/golden) derived from the formulas; tie order
+ * of ANN's kd-tree is "parity unpinned" (canonical rule: lowest candidate index).
+ */
+#ifndef TILER_ORACLE_H
+#define TILER_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OR_TILE_W 8
+#define OR_DESC_D 192
+#define OR_KM_ATTRS 80
+
+/* flags for or_psyv (ComputeTilePsyVisFeatures arguments, main.pas:2997) */
+#define OR_FROM_PAL 1
+#define OR_WAVELETS 2
+#define OR_QWEIGHT 8
+#define OR_HMIRROR 16
+#define OR_VMIRROR 32
+
+void or_init(void);
+void or_set_gamma(double g0, double g1);
+const double *or_dct_lut(void);
+const double *or_gamma_lut(void); /* [3][256], row g+1 for g = -1..1 */
+
+void or_psyv(const int32_t *rgb, const uint8_t *palpix, const int32_t *pal, int flags, int gamma, double *out);
+void or_psyv_batch(int n, const int32_t *rgb, const uint8_t *palpix, const int32_t *pals, const int32_t *pal_of,
+                   const uint8_t *flags_per, int flags, int gamma, double *out);
+
+float or_dist(const float *a, const float *b, int d);
+int or_nn(const float *data, int n, int d, const float *q, float *err);
+void or_knn(const float *data, int n, int d, const float *q, int k, int *idx, float *err);
+void or_nn_batch(const float *data, int n, int d, const float *q, int nq, int *idx, float *err, int threads);
+
+int or_prepare_global_ds(const uint8_t *palpix, const uint8_t *active, int T, float *ds, int32_t *tile_idx,
+                         uint8_t *attrs);
+double or_palette_corr(const double *centroids, int P, double *corrs);
+void or_mark_used(const float *gds, int gn, const int32_t *g_tile, const uint8_t *g_attr, const int32_t *item_pal,
+                  const int32_t *item_tile, int nitems, const uint8_t *palpix, int T, int P, int quality,
+                  const double *corrs, double highest, double paltol, uint8_t *used);
+int or_count_used(const uint8_t *used, int P, int T);
+int or_build_ft_dataset(const uint8_t *used, int P, int T, const uint8_t *palpix, const uint8_t *thm,
+                        const uint8_t *tvm, const int32_t *palettes, int use_wavelets, int gamma, float *ds,
+                        int32_t *tidx, int32_t *pidx, uint8_t *attrs);
+void or_frame_tiling(const int32_t *frame_rgb, int Q, const float *ds, int M, const int32_t *tidx,
+                     const int32_t *pidx, const uint8_t *attrs, int use_wavelets, int gamma, int threads,
+                     int32_t *out_tile, int32_t *out_pal, uint8_t *out_h, uint8_t *out_v, float *out_err);
+
+void or_smooth(int F, int Q, int32_t *tile, int32_t *tmpidx, int32_t *pal, uint8_t *hm, uint8_t *vm,
+               uint8_t *smoothed, const uint8_t *palpix, const int32_t *palettes, double strength);
+
+uint64_t or_km_dissim(const uint8_t *row, const uint8_t *item);
+uint64_t or_km_dissim_generic(const uint8_t *row, const uint8_t *item, int n);
+int or_km_get_min(const uint8_t *rows, int count, const uint8_t *item, uint64_t *best);
+void or_km_update_min_distance(const uint8_t *item, const uint8_t *rows, int count, uint64_t *mindist);
+uint32_t or_randint(uint32_t range, uint32_t *seed);
+int or_kmodes(const uint8_t *X, int N, int A, int K, int start, int modalities, int32_t *labels,
+              uint8_t *centroids, int *n_iter, uint64_t *cost);
+
+int or_eqtc(double n);
+int or_tile_dataset_line(const uint8_t *palpix64, int palsize, uint8_t *line80);
+int or_global_tiling(int T, uint8_t *palpix, uint8_t *active, int32_t *use_count, int32_t *merge_index,
+                     const int32_t *dith_pal, int P, int palsize, int desired, int restart, int32_t *k_per_bin);
+void or_make_tiles_unique(int T, uint8_t *palpix, uint8_t *active, int32_t *use_count, int32_t *merge_index);
+int or_reindex(int T, const uint8_t *active, const int32_t *use_count, int32_t *idx_map);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

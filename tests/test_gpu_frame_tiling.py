@@ -1,0 +1,173 @@
+"""GPU parity: libANN.so (HIP, gfx950) against the CPU restatement (oracle/) on seeded inputs.
+
+Bar: descriptors fp64 bit-exact; distances fp32 bit-exact; tile / palette / mirror
+indices bit-exact under the canonical tie rule (lowest candidate index).
+"""
+import numpy as np
+import pytest
+
+from tiler_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+PSYV_FLAG_SETS = [2, 0, 8, 2 | 16, 2 | 32, 2 | 48, 8 | 16 | 32, 1 | 2, 1 | 8, 1 | 2 | 16 | 32, 1 | 8 | 48]
+
+
+def _rgb_tiles(rng, n):
+    t = synth.frame_tiles(rng, n)
+    # extremes: black, white, pure primaries, single-pixel impulses
+    t[:6] = np.array([0, 0xFFFFFF, 0xFF, 0xFF00, 0xFF0000, 0x808080], np.int32)[:, None]
+    t[6, 17] = 0xFFFFFF
+    return t
+
+
+@pytest.mark.parametrize("gamma", [-1, 0, 1])
+def test_psyv_rgb_bit_exact(gpu, oracle, gamma):
+    rng = np.random.default_rng(100 + gamma)
+    n = 600
+    rgb = _rgb_tiles(rng, n)
+    for flags in [f for f in PSYV_FLAG_SETS if not f & 1]:
+        g64, g32 = gpu.psyv_batch(rgb=rgb, flags=flags, gamma=gamma, want64=True, want32=True)
+        o64 = oracle.psyv_batch(n, rgb=rgb, flags=flags, gamma=gamma)
+        assert np.array_equal(g64.view(np.uint64), o64.view(np.uint64)), f"flags={flags}"
+        assert np.array_equal(g32.view(np.uint32), o64.astype(np.float32).view(np.uint32))
+
+
+def test_psyv_palette_bit_exact(gpu, oracle):
+    rng = np.random.default_rng(7)
+    T, P, n = 300, 9, 900
+    pp = rng.integers(0, 16, (T, 64)).astype(np.uint8)
+    pals = synth.palettes(rng, P)
+    tile_of = rng.integers(0, T, n).astype(np.int32)
+    pal_of = rng.integers(0, P, n).astype(np.int32)
+    fper = (rng.integers(0, 4, n) * 16).astype(np.uint8)
+    for flags in (1 | 2, 1 | 8, 1):
+        g64, _ = gpu.psyv_batch(palpix=pp, tile_of=tile_of, palettes=pals, pal_of=pal_of, flags_per=fper,
+                                flags=flags, gamma=-1)
+        o64 = oracle.psyv_batch(n, palpix=pp[tile_of], pals=pals, pal_of=pal_of, flags_per=fper, flags=flags)
+        assert np.array_equal(g64.view(np.uint64), o64.view(np.uint64)), f"flags={flags}"
+
+
+def _check_nn(gpu, oracle, data, qs):
+    with gpu.KDTree(data) as kdt:
+        gi, ge = kdt.search_batch(qs)
+        st = kdt.stats()
+    oi, oe = oracle.nn_batch(data, qs)
+    assert np.array_equal(gi, oi), f"{np.count_nonzero(gi != oi)} index mismatches"
+    assert np.array_equal(ge.view(np.uint32), oe.view(np.uint32))
+    return st
+
+
+def test_nn_random_descriptors(gpu, oracle):
+    rng = np.random.default_rng(1)
+    wl = synth.make_workload(11, 160, 80, 2, 2000, n_palettes=8)
+    _, data = gpu.psyv_batch(palpix=wl.tiles, tile_of=wl.ds.tile_of, palettes=wl.palettes, pal_of=wl.ds.pal_of,
+                             flags_per=wl.ds.psyv_flags, flags=3, want64=False, want32=True)
+    _, qs = gpu.psyv_batch(rgb=wl.frame_rgb.reshape(-1, 64), flags=2, want64=False, want32=True)
+    st = _check_nn(gpu, oracle, data, qs)
+    assert st["queries"] == qs.shape[0]
+    # near-duplicate queries: a candidate row itself plus tiny perturbations (tight shortlists)
+    q2 = data[rng.integers(0, data.shape[0], 300)].copy()
+    q2[100:] += rng.normal(0, 1e-4, q2[100:].shape).astype(np.float32)
+    _check_nn(gpu, oracle, data, q2)
+
+
+def test_nn_ties_lowest_index(gpu, oracle):
+    rng = np.random.default_rng(2)
+    base = rng.normal(0, 1, (500, 192)).astype(np.float32)
+    data = np.concatenate([base, base[::-1], base[:50]])  # every row duplicated, some three times
+    qs = np.concatenate([base[:100], rng.normal(0, 1, (100, 192)).astype(np.float32)])
+    _check_nn(gpu, oracle, data, qs)
+
+
+def test_nn_overflow_fallback(gpu, oracle):
+    # 300 identical candidates: every lane list overflows below the threshold -> exact rescan path
+    rng = np.random.default_rng(3)
+    data = np.repeat(rng.normal(0, 1, (1, 192)).astype(np.float32), 300, 0)
+    data = np.concatenate([rng.normal(0, 1, (700, 192)).astype(np.float32), data])
+    qs = data[[0, 5, 700, 950]] + np.float32(1e-3)
+    st = _check_nn(gpu, oracle, data, qs)
+    assert st["fallback_queries"] >= 1
+
+
+def test_nn_generic_dims(gpu, oracle):
+    rng = np.random.default_rng(4)
+    for d in (3, 17, 64, 100, 256, 300):
+        data = rng.normal(0, 3, (3000, d)).astype(np.float32)
+        qs = rng.normal(0, 3, (257, d)).astype(np.float32)
+        _check_nn(gpu, oracle, data, qs)
+
+
+def test_knn_palette_index_preselection(gpu, oracle):
+    """k=8 on 64-d palette-index rows (PrepareGlobalFT dataset, main.pas:3779/3830): exact integer keys."""
+    rng = np.random.default_rng(5)
+    tiles, _, _ = synth.tileset(rng, 1500)
+    gds, gt, ga = oracle.prepare_global_ds(tiles)
+    qs = tiles[rng.integers(0, 1500, 400)].astype(np.float32)
+    qs[200:] = rng.integers(0, 16, (200, 64))
+    with gpu.KDTree(gds) as kdt:
+        gi, ge = kdt.search_batch(qs, k=8)
+        assert kdt.stats()["exact_integer"] == 1
+    for i in range(qs.shape[0]):
+        oi, oe = oracle.knn(gds, qs[i], 8)
+        assert np.array_equal(gi[i], oi) and np.array_equal(ge[i], oe), i
+
+
+def test_reference_call_shapes(gpu, oracle):
+    """ann_kdtree_search / search_multi one query at a time, as main.pas:4027 and 3830 call them."""
+    rng = np.random.default_rng(6)
+    data = rng.normal(0, 1, (4000, 192)).astype(np.float32)
+    with gpu.KDTree(data) as kdt:
+        for j in range(5):
+            q = rng.normal(0, 1, 192).astype(np.float32)
+            i, e = kdt.search(q)
+            oi, oe = oracle.nn(data, q)
+            assert (i, np.float32(e)) == (oi, np.float32(oe))
+            for k in (1, 8, 20):
+                ii, ee = kdt.search_multi(q, k)
+                oi2, oe2 = oracle.knn(data, q, k)
+                assert np.array_equal(ii, oi2) and np.array_equal(ee, oe2)
+    with gpu.KDTree(np.zeros((0, 192), np.float32)) as empty:
+        idx, err = empty.search_batch(np.zeros((2, 192), np.float32))
+        assert (idx == -1).all()
+
+
+def test_frame_tiling_end_to_end_c1(gpu, oracle):
+    """C1 shape (320x240, 8x8) with a 1k tileset: DoFrameTiling tilemap items bit-exact."""
+    from tiler_amd.frame_tiling import KeyframeTiler
+    wl = synth.make_workload(21, 320, 240, 3, 1000, n_palettes=16)
+    kt = KeyframeTiler(wl.tiles, wl.thm, wl.tvm, wl.palettes, wl.ds)
+    used = synth.used_one_palette(wl.tile_pal, 16)
+    ods, otile, opal, oattr = oracle.build_ft_dataset(used, wl.tiles, wl.thm, wl.tvm, wl.palettes)
+    assert np.array_equal(kt.rows.view(np.uint32), ods.view(np.uint32))
+    assert np.array_equal(otile, wl.ds.tile_of) and np.array_equal(opal, wl.ds.pal_of)
+    assert np.array_equal(oattr, wl.ds.attrs)
+    for f in range(wl.frames):
+        g = kt.do_frame_tiling(wl.frame_rgb[f])
+        o = oracle.frame_tiling(wl.frame_rgb[f], ods, otile, opal, oattr)
+        for a, b in zip(g[:4], o[:4]):
+            assert np.array_equal(a, b)
+        assert np.array_equal(g[4].view(np.uint32), o[4].view(np.uint32))
+    kt.finish_frame_tiling()
+
+
+def test_prepare_frame_tiling_used_table(gpu, oracle):
+    """UseOne (k=8 preselection + distinct-err walk) for Fast / Medium / Slow, main.pas:3802-3853."""
+    from tiler_amd import frame_tiling as ft
+    rng = np.random.default_rng(8)
+    P, T = 6, 400
+    tiles, thm, tvm = synth.tileset(rng, T)
+    cent = rng.normal(0, 1, (P, 192))
+    cent[3] = cent[2] + 1e-3  # a close palette pair for Medium
+    items_t = rng.integers(0, T, 2000).astype(np.int32)
+    items_p = rng.integers(0, P, 2000).astype(np.int32)
+    gds = ft.prepare_global_ft(tiles)
+    ogds, ogt, oga = oracle.prepare_global_ds(tiles)
+    assert np.array_equal(gds.tr_tile, ogt) and np.array_equal(gds.tr_attrs, oga)
+    corr_o, hi_o = oracle.palette_corr(cent)
+    corr_g, hi_g = ft.palette_corr(cent)
+    assert np.array_equal(corr_o, corr_g) and hi_o == hi_g
+    for q in (ft.FT_FAST, ft.FT_MEDIUM, ft.FT_SLOW):
+        ug = ft.mark_used(gds, tiles, items_p, items_t, P, q, corr_g, hi_g)
+        uo = oracle.mark_used(ogds, ogt, oga, items_p, items_t, tiles, P, q, corr_o, hi_o)
+        assert np.array_equal(ug, uo), q

@@ -1,0 +1,100 @@
+"""ctypes binding of libANN.so (include/tiler_ann.h).
+
+The shared library is built in-tree (tiler_amd/lib/libANN.so, `python -c "import __graft_entry__ as g; g.build()"`).
+There is no CPU fallback: if the library or a gfx950 device is missing, calls raise TilerError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libANN.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tiler_ann.h")
+
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_double = ctypes.c_double
+c_void_p = ctypes.c_void_p
+c_char_p = ctypes.c_char_p
+P = ctypes.POINTER
+
+
+class TilerError(RuntimeError):
+    pass
+
+
+class SearchStats(ctypes.Structure):
+    _fields_ = [("queries", ctypes.c_int64), ("fallback_queries", ctypes.c_int64),
+                ("exact_integer", ctypes.c_int32), ("splits", ctypes.c_int32)]
+
+
+_SIGS = {
+    "ann_kdtree_create": (c_void_p, [P(P(c_float)), c_int, c_int, c_int, c_int]),
+    "ann_kdtree_create_dev": (c_void_p, [c_void_p, c_int, c_int, c_void_p]),
+    "ann_kdtree_destroy": (None, [c_void_p]),
+    "ann_kdtree_search": (c_int, [c_void_p, c_void_p, c_float, c_void_p]),
+    "ann_kdtree_pri_search": (c_int, [c_void_p, c_void_p, c_float, c_void_p]),
+    "ann_kdtree_search_multi": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_float]),
+    "ann_kdtree_search_batch": (c_int, [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p]),
+    "ann_kdtree_search_multi_batch": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p]),
+    "ann_kdtree_search_batch_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "ann_kdtree_get_stats": (c_int, [c_void_p, P(SearchStats)]),
+    "tiler_init": (c_int, [c_int]),
+    "tiler_shutdown": (c_int, []),
+    "tiler_last_error": (c_char_p, []),
+    "tiler_set_gamma": (c_int, [c_double, c_double]),
+    "tiler_timing_enable": (c_int, [c_int]),
+    "tiler_timing_get": (c_double, [c_char_p, P(c_int)]),
+    "tiler_timing_reset": (c_int, []),
+    "tiler_psyv_batch": (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                 c_int, c_int, c_void_p, c_void_p]),
+    "tiler_psyv_batch_dev": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                     c_void_p, c_void_p, c_void_p]),
+    "tiler_ft_set_maps": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "tiler_frame_tiling": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p]),
+    "tiler_frame_tiling_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p]),
+    "tiler_smooth_keyframe": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                      c_void_p, c_int, c_void_p, c_double]),
+    "tiler_kmodes_compute": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]),
+}
+
+_lib = None
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Every function name declared in include/tiler_ann.h."""
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b((?:ann|tiler)_[a-z_0-9]+)\s*\(", txt)))
+
+
+def load() -> ctypes.CDLL:
+    """Load the in-tree libANN.so; raise TilerError when it is absent (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise TilerError(f"{LIB_PATH} missing: build it with __graft_entry__.build() (no CPU fallback exists)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    msg = load().tiler_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc, what: str):
+    if rc is None or (isinstance(rc, int) and rc < 0):
+        raise TilerError(f"{what} failed: {last_error()}")
+    return rc

@@ -1,0 +1,98 @@
+"""Python mirror of the reference's ANN usage (extern.pas:63-67 -> libANN.so).
+
+`KDTree` keeps the reference call shape (create over rows, search / search_multi per query) and adds
+the batched and HBM-resident forms the MI355X path is built around.  Every call runs on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import SearchStats, TilerError, check, load
+
+FLT_MAX = np.float32(3.4028234663852886e38)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class KDTree:
+    """ann_kdtree_create(pa, n, dd, bs=1, split=ANN_KD_STD) ... ann_kdtree_destroy."""
+
+    def __init__(self, data=None, *, dev_ptr: int | None = None, n: int | None = None, dd: int | None = None,
+                 stream: int = 0, bs: int = 1, split: int = 0):
+        lib = load()
+        self._lib = lib
+        if dev_ptr is not None:
+            self.n, self.dd = int(n), int(dd)
+            h = lib.ann_kdtree_create_dev(ctypes.c_void_p(dev_ptr), self.n, self.dd, ctypes.c_void_p(stream))
+        else:
+            data = np.ascontiguousarray(data, dtype=np.float32)
+            if data.ndim != 2:
+                raise ValueError("dataset must be [n, dd]")
+            self.n, self.dd = data.shape
+            self._rows = data
+            rowp = (ctypes.POINTER(ctypes.c_float) * max(1, self.n))()
+            base = data.ctypes.data
+            for i in range(self.n):
+                rowp[i] = ctypes.cast(base + 4 * self.dd * i, ctypes.POINTER(ctypes.c_float))
+            h = lib.ann_kdtree_create(rowp, self.n, self.dd, bs, split)
+        if not h:
+            raise TilerError("ann_kdtree_create failed: " + lib.tiler_last_error().decode())
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.ann_kdtree_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- reference-shaped single-query calls (main.pas:4027, 3830) --
+    def search(self, q, eps: float = 0.0):
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        err = np.zeros(1, np.float32)
+        idx = self._lib.ann_kdtree_search(self.handle, _ptr(q), eps, _ptr(err))
+        check(idx if idx >= 0 or self.n == 0 else -1, "ann_kdtree_search")
+        return int(idx), float(err[0])
+
+    def search_multi(self, q, cnt: int, eps: float = 0.0):
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        idxs = np.zeros(cnt, np.int32)
+        errs = np.zeros(cnt, np.float32)
+        check(self._lib.ann_kdtree_search_multi(self.handle, _ptr(idxs), _ptr(errs), cnt, _ptr(q), eps),
+              "ann_kdtree_search_multi")
+        return idxs, errs
+
+    # -- batched --
+    def search_batch(self, qs, k: int = 1, eps: float = 0.0):
+        qs = np.ascontiguousarray(qs, dtype=np.float32).reshape(-1, self.dd)
+        nq = qs.shape[0]
+        idx = np.zeros((nq, k), np.int32)
+        err = np.zeros((nq, k), np.float32)
+        check(self._lib.ann_kdtree_search_multi_batch(self.handle, _ptr(qs), nq, k, eps, _ptr(idx), _ptr(err)),
+              "ann_kdtree_search_multi_batch")
+        return (idx[:, 0], err[:, 0]) if k == 1 else (idx, err)
+
+    def search_batch_dev(self, q_ptr: int, nq: int, k: int, idx_ptr: int, err_ptr: int, stream: int = 0):
+        check(self._lib.ann_kdtree_search_batch_dev(self.handle, ctypes.c_void_p(q_ptr), nq, k,
+                                                    ctypes.c_void_p(idx_ptr), ctypes.c_void_p(err_ptr),
+                                                    ctypes.c_void_p(stream)), "ann_kdtree_search_batch_dev")
+
+    def stats(self) -> dict:
+        s = SearchStats()
+        check(self._lib.ann_kdtree_get_stats(self.handle, ctypes.byref(s)), "ann_kdtree_get_stats")
+        return {"queries": s.queries, "fallback_queries": s.fallback_queries, "exact_integer": s.exact_integer,
+                "splits": s.splits}

@@ -1,0 +1,528 @@
+// ann_api.hip -- extern "C" entry points of libANN.so (include/tiler_ann.h).
+//
+// The ANN.dll surface (extern.pas:63-67) plus batched / device-resident extensions.  Host-buffer
+// entry points stage through a per-handle HIP stream; *_dev entry points run on the caller's
+// stream with HBM pointers (the benchmarked path).  No CPU compute path exists: without a gfx950
+// device every entry point fails with -1 / NULL and tiler_last_error().
+#include <float.h>
+#include <math.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/tiler_ann.h"
+#include "kmodes.hpp"
+#include "nn_search.hpp"
+#include "psyv.hpp"
+#include "smooth.hpp"
+
+namespace tiler {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+const char *last_error() { return g_err.c_str(); }
+
+static std::mutex g_init_mu;
+static bool g_ready = false;
+static int g_device = 0;
+static Luts g_luts;
+static double g_gamma[2] = {2.0, 0.6};
+
+const Luts &luts() { return g_luts; }
+
+// ---- kernel timing --------------------------------------------------------------------------
+struct TimedPair {
+    std::string name;
+    hipEvent_t a, b;
+};
+static std::mutex g_time_mu;
+static std::vector<TimedPair> g_times;
+static bool g_timing = false;
+bool timing_enabled() { return g_timing; }
+KTimer::KTimer(const char *n, hipStream_t s) : name(n), stream(s) {
+    if (!g_timing) return;
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess) return;
+    if (hipEventCreate(&b) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        return;
+    }
+    ev_a = a;
+    ev_b = b;
+    (void)hipEventRecord(a, s);
+}
+KTimer::~KTimer() {
+    if (!ev_a) return;
+    (void)hipEventRecord((hipEvent_t)ev_b, stream);
+    std::lock_guard<std::mutex> lk(g_time_mu);
+    g_times.push_back({name, (hipEvent_t)ev_a, (hipEvent_t)ev_b});
+}
+
+// InitLuts main.pas:592-642; constants main.pas:63-98, 2675-2676, 2816, 3000-3009 -- all on the host,
+// identical expressions to the CPU restatement, so device and oracle share the same bits.
+static int upload_gamma_lut() {
+    std::vector<double> g(3 * 256);
+    for (int gi = -1; gi <= 1; gi++)
+        for (int i = 0; i < 256; i++) g[(gi + 1) * 256 + i] = (gi >= 0) ? pow(i / 255.0, g_gamma[gi]) : i / 255.0;
+    TILER_HIP_CHECK(hipMemcpy(g_luts.d_gamma, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int build_luts() {
+    static const int qden[3][64] = {
+        {16, 11, 10, 16, 24, 40, 51, 61, 12, 12, 14, 19, 26, 58, 60, 55, 14, 13, 16, 24, 40, 57, 69, 56,
+         14, 17, 22, 29, 51, 87, 80, 62, 18, 22, 37, 56, 68, 109, 103, 77, 24, 35, 55, 64, 81, 104, 113, 92,
+         49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99},
+        {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 112, 24, 26, 56, 99, 99, 99, 112, 128,
+         47, 66, 99, 99, 99, 112, 128, 144, 99, 99, 99, 99, 112, 128, 144, 160, 99, 99, 99, 112, 128, 144, 160, 176,
+         99, 99, 112, 128, 144, 160, 176, 192, 99, 112, 128, 144, 160, 176, 192, 208},
+        {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 112, 24, 26, 56, 99, 99, 99, 112, 128,
+         47, 66, 99, 99, 99, 112, 128, 144, 99, 99, 99, 99, 112, 128, 144, 160, 99, 99, 99, 112, 128, 144, 160, 176,
+         99, 99, 112, 128, 144, 160, 176, 192, 99, 112, 128, 144, 160, 176, 192, 208}};
+    std::vector<double> dct(4096), qm(192), ratio(64);
+    int i = 0;
+    for (int v = 0; v < 8; v++)
+        for (int u = 0; u < 8; u++)
+            for (int y = 0; y < 8; y++)
+                for (int x = 0; x < 8; x++) {
+                    double a = (((double)x + 0.5) * (double)u) * M_PI / 16.0;
+                    double b = (((double)y + 0.5) * (double)v) * M_PI / 16.0;
+                    dct[i++] = cos(a) * cos(b);
+                }
+    for (int c = 0; c < 3; c++)
+        for (int k = 0; k < 64; k++) qm[c * 64 + k] = 4.0 / sqrt((double)qden[c][k]);
+    const double sh = sqrt(0.5);
+    for (int v = 0; v < 8; v++)
+        for (int u = 0; u < 8; u++) ratio[v * 8 + u] = (u == 0 && v == 0) ? 0.5 : ((u == 0 || v == 0) ? sh : 1.0);
+    TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_gamma, 3 * 256 * sizeof(double)));
+    TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_dct, 4096 * sizeof(double)));
+    TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_qmul, 192 * sizeof(double)));
+    TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_ratio, 64 * sizeof(double)));
+    TILER_HIP_CHECK(hipMemcpy(g_luts.d_dct, dct.data(), 4096 * sizeof(double), hipMemcpyHostToDevice));
+    TILER_HIP_CHECK(hipMemcpy(g_luts.d_qmul, qm.data(), 192 * sizeof(double), hipMemcpyHostToDevice));
+    TILER_HIP_CHECK(hipMemcpy(g_luts.d_ratio, ratio.data(), 64 * sizeof(double), hipMemcpyHostToDevice));
+    g_luts.haar_f = 1.0 / sqrt(2.0);
+    g_luts.u_mul = 0.5 / (1.0 - 722.0 / 10000.0);
+    g_luts.v_mul = 0.5 / (1.0 - 2126.0 / 10000.0);
+    return upload_gamma_lut();
+}
+
+static int init_locked(int device) {
+    if (g_ready) return 0;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        set_error("tiler: no HIP device visible (libANN.so runs on MI355X / gfx950 only, no CPU path)");
+        return -1;
+    }
+    if (device < 0 || device >= count) {
+        set_error("tiler: device index out of range");
+        return -1;
+    }
+    hipDeviceProp_t prop;
+    TILER_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error(std::string("tiler: device is ") + prop.gcnArchName + ", libANN.so is built for gfx950 only");
+        return -1;
+    }
+    TILER_HIP_CHECK(hipSetDevice(device));
+    g_device = device;
+    if (build_luts()) return -1;
+    g_ready = true;
+    return 0;
+}
+
+bool ensure_init() {
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    if (!g_ready && init_locked(0)) return false;
+    return hipSetDevice(g_device) == hipSuccess;
+}
+
+}  // namespace tiler
+
+using namespace tiler;
+
+struct ann_kdtree {
+    NNIndex *ix = nullptr;
+    hipStream_t stream = nullptr;
+    float *d_q = nullptr;
+    int *d_idx = nullptr;
+    float *d_err = nullptr;
+    size_t cap = 0;
+    int32_t *d_rgb = nullptr, *d_mt = nullptr, *d_mp = nullptr;
+    uint8_t *d_mh = nullptr, *d_mv = nullptr;
+    size_t cap_ft = 0;
+};
+
+static int ensure_io(ann_kdtree *t, size_t nq, int d, int k) {
+    const size_t need = nq * (size_t)std::max(d, k);
+    if (need <= t->cap) return 0;
+    hipFree(t->d_q);
+    hipFree(t->d_idx);
+    hipFree(t->d_err);
+    TILER_HIP_CHECK(hipMalloc((void **)&t->d_q, need * sizeof(float)));
+    TILER_HIP_CHECK(hipMalloc((void **)&t->d_idx, need * sizeof(int)));
+    TILER_HIP_CHECK(hipMalloc((void **)&t->d_err, need * sizeof(float)));
+    t->cap = need;
+    return 0;
+}
+
+extern "C" {
+
+int tiler_init(int device) {
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    return init_locked(device);
+}
+
+int tiler_shutdown(void) { return 0; }
+
+int tiler_timing_enable(int on) {
+    g_timing = on != 0;
+    return 0;
+}
+
+double tiler_timing_get(const char *kernel, int *launches) {
+    std::lock_guard<std::mutex> lk(g_time_mu);
+    double ms = 0.0;
+    int cnt = 0;
+    for (auto &p : g_times) {
+        if (p.name != kernel) continue;
+        float e = 0.0f;
+        if (hipEventSynchronize(p.b) != hipSuccess || hipEventElapsedTime(&e, p.a, p.b) != hipSuccess) {
+            set_error("tiler_timing_get: event query failed");
+            return -1.0;
+        }
+        ms += e;
+        cnt++;
+    }
+    if (launches) *launches = cnt;
+    return ms;
+}
+
+int tiler_timing_reset(void) {
+    std::lock_guard<std::mutex> lk(g_time_mu);
+    for (auto &p : g_times) {
+        (void)hipEventSynchronize(p.b);
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    g_times.clear();
+    return 0;
+}
+
+const char *tiler_last_error(void) { return tiler::last_error(); }
+
+int tiler_set_gamma(double g0, double g1) {
+    if (!ensure_init()) return -1;
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    g_gamma[0] = g0;
+    g_gamma[1] = g1;
+    return upload_gamma_lut();
+}
+
+ann_kdtree *ann_kdtree_create(float **pa, int n, int dd, int bs, int split) {
+    (void)bs;
+    (void)split;  // bucket size / split rule only shape ANN's tree; the exhaustive search has none
+    if (!ensure_init()) return nullptr;
+    if (n < 0 || dd <= 0 || (n > 0 && !pa)) {
+        set_error("ann_kdtree_create: invalid arguments");
+        return nullptr;
+    }
+    std::vector<float> h((size_t)n * dd);
+    for (int i = 0; i < n; i++) {
+        if (!pa[i]) {
+            set_error("ann_kdtree_create: null row pointer");
+            return nullptr;
+        }
+        memcpy(&h[(size_t)i * dd], pa[i], sizeof(float) * dd);
+    }
+    ann_kdtree *t = new ann_kdtree();
+    TILER_HIP_CHECK_NULL(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+    float *d_rows = nullptr;
+    TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_rows, std::max<size_t>(1, h.size()) * sizeof(float)));
+    if (n > 0)
+        TILER_HIP_CHECK_NULL(hipMemcpyAsync(d_rows, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, t->stream));
+    t->ix = nn_index_create_dev(d_rows, n, dd, t->stream);
+    if (!t->ix) {
+        hipStreamDestroy(t->stream);
+        delete t;
+        return nullptr;
+    }
+    return t;
+}
+
+ann_kdtree *ann_kdtree_create_dev(const float *d_rows_in, int n, int dd, void *stream) {
+    if (!ensure_init()) return nullptr;
+    if (n < 0 || dd <= 0 || (n > 0 && !d_rows_in)) {
+        set_error("ann_kdtree_create_dev: invalid arguments");
+        return nullptr;
+    }
+    ann_kdtree *t = new ann_kdtree();
+    TILER_HIP_CHECK_NULL(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+    hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+    float *d_rows = nullptr;
+    const size_t bytes = (size_t)n * dd * sizeof(float);
+    TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_rows, std::max<size_t>(4, bytes)));
+    if (n > 0) TILER_HIP_CHECK_NULL(hipMemcpyAsync(d_rows, d_rows_in, bytes, hipMemcpyDeviceToDevice, s));
+    t->ix = nn_index_create_dev(d_rows, n, dd, s);
+    if (!t->ix) {
+        (void)hipStreamDestroy(t->stream);
+        delete t;
+        return nullptr;
+    }
+    return t;
+}
+
+void ann_kdtree_destroy(ann_kdtree *t) {
+    if (!t) return;
+    if (t->stream) hipStreamSynchronize(t->stream);
+    nn_index_destroy(t->ix);
+    hipFree(t->d_q);
+    hipFree(t->d_idx);
+    hipFree(t->d_err);
+    hipFree(t->d_rgb);
+    hipFree(t->d_mt);
+    hipFree(t->d_mp);
+    hipFree(t->d_mh);
+    hipFree(t->d_mv);
+    if (t->stream) hipStreamDestroy(t->stream);
+    delete t;
+}
+
+int ann_kdtree_search_multi_batch(ann_kdtree *t, const float *q, int nq, int k, float eps, int *idxs, float *errs) {
+    (void)eps;
+    if (!t || !t->ix || nq < 0 || (nq > 0 && (!q || !idxs || !errs))) {
+        set_error("ann_kdtree_search: invalid arguments");
+        return -1;
+    }
+    if (k < 1 || k > 32) {
+        set_error("ann_kdtree_search: k must be in 1..32");
+        return -1;
+    }
+    if (!ensure_init()) return -1;
+    std::lock_guard<std::mutex> lk(t->ix->mu);
+    if (nq == 0) return 0;
+    NNIndex *ix = t->ix;
+    if (ix->n == 0) {
+        for (long i = 0; i < (long)nq * k; i++) {
+            idxs[i] = -1;
+            errs[i] = FLT_MAX;
+        }
+        return 0;
+    }
+    if (ensure_io(t, nq, ix->d, k)) return -1;
+    TILER_HIP_CHECK(hipMemcpyAsync(t->d_q, q, (size_t)nq * ix->d * sizeof(float), hipMemcpyHostToDevice, t->stream));
+    if (nn_search_dev(ix, t->d_q, nq, k, t->d_idx, t->d_err, nullptr, t->stream)) return -1;
+    TILER_HIP_CHECK(hipMemcpyAsync(idxs, t->d_idx, (size_t)nq * k * sizeof(int), hipMemcpyDeviceToHost, t->stream));
+    TILER_HIP_CHECK(hipMemcpyAsync(errs, t->d_err, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, t->stream));
+    TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
+    return 0;
+}
+
+int ann_kdtree_search_batch(ann_kdtree *t, const float *q, int nq, float eps, int *idx, float *err) {
+    return ann_kdtree_search_multi_batch(t, q, nq, 1, eps, idx, err);
+}
+
+int ann_kdtree_search(ann_kdtree *t, float *q, float eps, float *err) {
+    int idx = -1;
+    float e = 0.0f;
+    if (ann_kdtree_search_multi_batch(t, q, 1, 1, eps, &idx, &e)) return -1;
+    if (err) *err = e;
+    return idx;
+}
+
+int ann_kdtree_pri_search(ann_kdtree *t, float *q, float eps, float *err) { return ann_kdtree_search(t, q, eps, err); }
+
+int ann_kdtree_search_multi(ann_kdtree *t, int *idxs, float *errs, int cnt, float *q, float eps) {
+    return ann_kdtree_search_multi_batch(t, q, 1, cnt, eps, idxs, errs);
+}
+
+int ann_kdtree_search_batch_dev(ann_kdtree *t, const float *d_q, int nq, int k, int *d_idx, float *d_err,
+                                void *stream) {
+    if (!t || !t->ix) {
+        set_error("ann_kdtree_search_batch_dev: null handle");
+        return -1;
+    }
+    if (!ensure_init()) return -1;
+    std::lock_guard<std::mutex> lk(t->ix->mu);
+    return nn_search_dev(t->ix, d_q, nq, k, d_idx, d_err, nullptr, (hipStream_t)stream);
+}
+
+int ann_kdtree_get_stats(ann_kdtree *t, tiler_search_stats *out) {
+    if (!t || !t->ix || !out) {
+        set_error("ann_kdtree_get_stats: invalid arguments");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(t->ix->mu);
+    out->queries = t->ix->last_queries;
+    out->fallback_queries = t->ix->last_splits > 0 ? *t->ix->h_fb_count : t->ix->last_fallback;
+    out->exact_integer = t->ix->exact_int ? 1 : 0;
+    out->splits = t->ix->last_splits;
+    return 0;
+}
+
+int tiler_psyv_batch_dev(int n, const int32_t *rgb, const uint8_t *palpix, const int32_t *tile_of,
+                         const int32_t *palettes, const int32_t *pal_of, const uint8_t *flags_per, int flags, int gamma,
+                         double *out64, float *out32, void *stream) {
+    if (!ensure_init()) return -1;
+    if ((flags & 4) != 0) {
+        set_error("psyv: UseLAB is not on the hot path and is not supported");
+        return -1;
+    }
+    PsyvArgs a;
+    a.n = n;
+    a.rgb = rgb;
+    a.palpix = palpix;
+    a.tile_of = tile_of;
+    a.palettes = palettes;
+    a.pal_of = pal_of;
+    a.flags_per = flags_per;
+    a.flags = flags;
+    a.gamma = gamma;
+    a.out64 = out64;
+    a.out32 = out32;
+    return launch_psyv(a, (hipStream_t)stream);
+}
+
+int tiler_psyv_batch(int n, const int32_t *rgb, int n_tiles, const uint8_t *palpix, const int32_t *tile_of,
+                     int n_palettes, const int32_t *palettes, const int32_t *pal_of, const uint8_t *flags_per,
+                     int flags, int gamma, double *out64, float *out32) {
+    if (!ensure_init()) return -1;
+    if (n < 0) {
+        set_error("psyv: n < 0");
+        return -1;
+    }
+    if (n == 0) return 0;
+    const bool from_pal = (flags & 1) != 0 || (flags_per != nullptr);
+    std::vector<void *> bufs;
+    auto up = [&](const void *h, size_t bytes) -> void * {
+        if (!h || bytes == 0) return nullptr;
+        void *d = nullptr;
+        if (hipMalloc(&d, bytes) != hipSuccess) return nullptr;
+        bufs.push_back(d);
+        hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
+        return d;
+    };
+    auto cleanup = [&]() {
+        for (void *p : bufs) hipFree(p);
+    };
+    int32_t *d_rgb = (int32_t *)up(rgb, rgb ? (size_t)n * 64 * 4 : 0);
+    uint8_t *d_pp = from_pal ? (uint8_t *)up(palpix, (size_t)std::max(n_tiles, 0) * 64) : nullptr;
+    int32_t *d_to = (int32_t *)up(tile_of, tile_of ? (size_t)n * 4 : 0);
+    int32_t *d_pal = from_pal ? (int32_t *)up(palettes, (size_t)std::max(n_palettes, 0) * 16 * 4) : nullptr;
+    int32_t *d_po = (int32_t *)up(pal_of, pal_of ? (size_t)n * 4 : 0);
+    uint8_t *d_fp = (uint8_t *)up(flags_per, flags_per ? (size_t)n : 0);
+    double *d_o64 = nullptr;
+    float *d_o32 = nullptr;
+    if (out64 && hipMalloc((void **)&d_o64, (size_t)n * 192 * 8) == hipSuccess) bufs.push_back(d_o64);
+    if (out32 && hipMalloc((void **)&d_o32, (size_t)n * 192 * 4) == hipSuccess) bufs.push_back(d_o32);
+    if ((!rgb && !from_pal) || (rgb && !d_rgb) || (from_pal && (!d_pp || !d_pal)) || (out64 && !d_o64) ||
+        (out32 && !d_o32)) {
+        cleanup();
+        set_error("psyv: missing input buffer or device allocation failed");
+        return -1;
+    }
+    int rc = tiler_psyv_batch_dev(n, d_rgb, d_pp, d_to, d_pal, d_po, d_fp, flags, gamma, d_o64, d_o32, nullptr);
+    if (rc == 0) {
+        if (out64) hipMemcpy(out64, d_o64, (size_t)n * 192 * 8, hipMemcpyDeviceToHost);
+        if (out32) hipMemcpy(out32, d_o32, (size_t)n * 192 * 4, hipMemcpyDeviceToHost);
+        if (hipDeviceSynchronize() != hipSuccess) {
+            set_error("psyv: kernel failed");
+            rc = -1;
+        }
+    }
+    cleanup();
+    return rc;
+}
+
+int tiler_ft_set_maps(ann_kdtree *t, const int32_t *tr_tile, const int32_t *tr_pal, const uint8_t *tr_attr) {
+    if (!t || !t->ix || !tr_tile || !tr_pal || !tr_attr) {
+        set_error("tiler_ft_set_maps: invalid arguments");
+        return -1;
+    }
+    if (!ensure_init()) return -1;
+    NNIndex *ix = t->ix;
+    std::lock_guard<std::mutex> lk(ix->mu);
+    const size_t n = std::max(1, ix->n);
+    hipFree(ix->d_tr_tile);
+    hipFree(ix->d_tr_pal);
+    hipFree(ix->d_tr_attr);
+    TILER_HIP_CHECK(hipMalloc((void **)&ix->d_tr_tile, n * 4));
+    TILER_HIP_CHECK(hipMalloc((void **)&ix->d_tr_pal, n * 4));
+    TILER_HIP_CHECK(hipMalloc((void **)&ix->d_tr_attr, n));
+    TILER_HIP_CHECK(hipMemcpy(ix->d_tr_tile, tr_tile, (size_t)ix->n * 4, hipMemcpyHostToDevice));
+    TILER_HIP_CHECK(hipMemcpy(ix->d_tr_pal, tr_pal, (size_t)ix->n * 4, hipMemcpyHostToDevice));
+    TILER_HIP_CHECK(hipMemcpy(ix->d_tr_attr, tr_attr, (size_t)ix->n, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int tiler_frame_tiling_dev(ann_kdtree *t, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int32_t *d_tile,
+                           int32_t *d_pal, uint8_t *d_hm, uint8_t *d_vm, float *d_err, void *stream) {
+    if (!t || !t->ix) {
+        set_error("tiler_frame_tiling: null handle");
+        return -1;
+    }
+    if (!t->ix->d_tr_tile) {
+        set_error("tiler_frame_tiling: call tiler_ft_set_maps first");
+        return -1;
+    }
+    if (!ensure_init()) return -1;
+    std::lock_guard<std::mutex> lk(t->ix->mu);
+    if (ensure_io(t, Q, 1, 1)) return -1;
+    FtMaps m{d_tile, d_pal, d_hm, d_vm};
+    return nn_frame_tiling_dev(t->ix, d_rgb, Q, use_wavelets, gamma, t->d_idx, d_err, &m, (hipStream_t)stream);
+}
+
+int tiler_frame_tiling(ann_kdtree *t, const int32_t *rgb, int Q, int use_wavelets, int gamma, int32_t *out_tile,
+                       int32_t *out_pal, uint8_t *out_hm, uint8_t *out_vm, float *out_err) {
+    if (!t || !t->ix || Q < 0 || (Q > 0 && (!rgb || !out_tile || !out_pal || !out_hm || !out_vm || !out_err))) {
+        set_error("tiler_frame_tiling: invalid arguments");
+        return -1;
+    }
+    if (Q == 0) return 0;
+    if (!ensure_init()) return -1;
+    if ((size_t)Q > t->cap_ft) {
+        hipFree(t->d_rgb);
+        hipFree(t->d_mt);
+        hipFree(t->d_mp);
+        hipFree(t->d_mh);
+        hipFree(t->d_mv);
+        TILER_HIP_CHECK(hipMalloc((void **)&t->d_rgb, (size_t)Q * 256));
+        TILER_HIP_CHECK(hipMalloc((void **)&t->d_mt, (size_t)Q * 4));
+        TILER_HIP_CHECK(hipMalloc((void **)&t->d_mp, (size_t)Q * 4));
+        TILER_HIP_CHECK(hipMalloc((void **)&t->d_mh, (size_t)Q));
+        TILER_HIP_CHECK(hipMalloc((void **)&t->d_mv, (size_t)Q));
+        t->cap_ft = Q;
+    }
+    {
+        std::lock_guard<std::mutex> lk(t->ix->mu);
+        if (ensure_io(t, Q, 1, 1)) return -1;
+    }
+    TILER_HIP_CHECK(hipMemcpyAsync(t->d_rgb, rgb, (size_t)Q * 256, hipMemcpyHostToDevice, t->stream));
+    if (tiler_frame_tiling_dev(t, t->d_rgb, Q, use_wavelets, gamma, t->d_mt, t->d_mp, t->d_mh, t->d_mv, t->d_err,
+                               t->stream))
+        return -1;
+    TILER_HIP_CHECK(hipMemcpyAsync(out_tile, t->d_mt, (size_t)Q * 4, hipMemcpyDeviceToHost, t->stream));
+    TILER_HIP_CHECK(hipMemcpyAsync(out_pal, t->d_mp, (size_t)Q * 4, hipMemcpyDeviceToHost, t->stream));
+    TILER_HIP_CHECK(hipMemcpyAsync(out_hm, t->d_mh, (size_t)Q, hipMemcpyDeviceToHost, t->stream));
+    TILER_HIP_CHECK(hipMemcpyAsync(out_vm, t->d_mv, (size_t)Q, hipMemcpyDeviceToHost, t->stream));
+    TILER_HIP_CHECK(hipMemcpyAsync(out_err, t->d_err, (size_t)Q * 4, hipMemcpyDeviceToHost, t->stream));
+    TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
+    return 0;
+}
+
+int tiler_smooth_keyframe(int F, int Q, int32_t *tile, int32_t *tmpidx, int32_t *pal, uint8_t *hm, uint8_t *vm,
+                          uint8_t *smoothed, int T, const uint8_t *palpix, int P, const int32_t *palettes,
+                          double strength) {
+    if (!ensure_init()) return -1;
+    return smooth_keyframe_host(F, Q, tile, tmpidx, pal, hm, vm, smoothed, T, palpix, P, palettes, strength);
+}
+
+int tiler_kmodes_compute(const uint8_t *X, int n, int nattr, int k, int start_point, int n_modalities,
+                         int32_t *labels, uint8_t *centroids, int *n_iter, uint64_t *cost) {
+    if (!ensure_init()) return -1;
+    return kmodes_compute_host(X, n, nattr, k, start_point, n_modalities, labels, centroids, n_iter, cost);
+}
+
+}  // extern "C"

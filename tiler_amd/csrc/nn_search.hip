@@ -1,0 +1,755 @@
+// nn_search.hip -- exact nearest-neighbour search over fp32 descriptors on gfx950 (MI355X).
+//
+// Replaces ANN.dll's kd-tree search (called at main.pas:3830 and 4027).  The
+// result must equal an exhaustive scan of the reference distance
+//     dist(q, c) = fp32 sum over d of (q_d - c_d)^2, dimension order, every op rounded, no FMA
+// with equal distances resolved to the lowest dataset index.  That sum is not a GEMM, so the
+// search runs in three kernels:
+//   1. nn_shortlist_kernel: keys = ||c||^2 - 2 q.c on the matrix cores (v_mfma_f32_32x32x16_f16 on
+//      fp16-rounded operands, fp32 accumulate).  Every lane keeps the L smallest keys of its
+//      query column; nothing Q x M ever reaches HBM.
+//   2. nn_rescore_kernel: per query, a rigorous bound E on |key - exact key| (norms of the fp16
+//      residuals + accumulation and rounding terms, DESIGN.md "Exactness argument") gives a
+//      threshold T >= the key of the exact winner; every kept candidate with key <= T is rescored
+//      with the reference fp32 sequential distance and the winner picked by (dist, index).
+//      If a lane's list was full below T (a candidate might have been dropped) the query is queued.
+//   3. nn_exact_kernel: exhaustive reference-order scan for queued queries (and k > 8).
+// Small-integer datasets (the 64-d palette-index preselection, main.pas:3779/3830) make the MFMA
+// keys exact; the same kernels then return exact (key, index) order with no margin.
+#include <float.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "nn_search.hpp"
+#include "psyv.hpp"
+
+#pragma clang fp contract(off)
+
+namespace tiler {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+enum { QF_INT = 1, QF_BAD = 2 };
+
+// ------------------------------------------------------------------------------------------
+// prep: fp32 rows -> fp16 MFMA fragments [blk][s][lane][8] + norms + bounds
+//   lane l of block b holds row b*32 + (l & 31), k = s*16 + 8*(l >> 5) + j   (A and B maps coincide)
+// ------------------------------------------------------------------------------------------
+struct PrepArgs {
+    const float *rows;
+    long n;
+    int d, S;
+    float scale;
+    half8 *frag;
+    float *nc;      // dataset only: accumulator-row order
+    QStat *qstat;   // queries only
+    DsStat *ds;     // dataset only
+};
+
+__device__ __forceinline__ double wave_max_d(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void prep_rows_kernel(PrepArgs a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+    const long nblk = (a.n + 31) / 32;
+    for (long blk = (long)blockIdx.x * 4 + wave; blk < nblk; blk += (long)gridDim.x * 4) {
+        const long r = blk * 32 + (lane & 31);
+        const bool valid = r < a.n;
+        double s2 = 0, sh = 0, se = 0, mabs = 0;
+        int notint = 0, bad = 0;
+        for (int s = 0; s < a.S; s++) {
+            half8 hv;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int k = s * 16 + 8 * h + j;
+                const float v = (valid && k < a.d) ? a.rows[r * a.d + k] : 0.0f;
+                const float vs = v * a.scale;
+                _Float16 vh = (_Float16)vs;
+                if (fabsf((float)vh) < 6.103515625e-05f) vh = (_Float16)0.0f;  // no fp16 subnormal operands
+                hv[j] = vh;
+                const double dv = vs, dh = (double)(float)vh;
+                s2 += dv * dv;
+                sh += dh * dh;
+                se += (dv - dh) * (dv - dh);
+                mabs = fmax(mabs, fabs((double)v));
+                if (!(v == rintf(v)) || fabsf(v) > 2048.0f) notint = 1;
+                if (!isfinite(vs) || fabsf(vs) > 65000.0f) bad = 1;
+            }
+            a.frag[(blk * a.S + s) * 64 + lane] = hv;
+        }
+        s2 += __shfl_xor(s2, 32, 64);
+        sh += __shfl_xor(sh, 32, 64);
+        se += __shfl_xor(se, 32, 64);
+        mabs = fmax(mabs, __shfl_xor(mabs, 32, 64));
+        notint |= __shfl_xor(notint, 32, 64);
+        bad |= __shfl_xor(bad, 32, 64);
+        if (a.qstat && h == 0 && valid) {
+            QStat q;
+            q.n2 = s2;
+            q.hn = sqrt(sh);
+            q.en = sqrt(se);
+            q.flags = (notint ? 0 : QF_INT) | (bad ? QF_BAD : 0);
+            q.pad = (int)fmin(mabs, 2e9);
+            a.qstat[r] = q;
+        }
+        if (a.nc && h == 0) {
+            const int rr = lane & 31;
+            const int pos = ((rr >> 2) & 1) * 16 + ((rr & 3) | ((rr >> 3) << 2));
+            a.nc[blk * 32 + pos] = valid ? (float)s2 : INFINITY;
+        }
+        if (a.ds) {
+            double m2 = wave_max_d(valid ? s2 : 0.0), mh = wave_max_d(valid ? sh : 0.0);
+            double me = wave_max_d(valid ? se : 0.0), ma = wave_max_d(valid ? mabs : 0.0);
+            int ni = __any(valid && notint), bd = __any(valid && bad);
+            if (lane == 0) {
+                atomicMax(&a.ds->max_n2_bits, (unsigned long long)__double_as_longlong(m2));
+                atomicMax(&a.ds->max_h2_bits, (unsigned long long)__double_as_longlong(mh));
+                atomicMax(&a.ds->max_e2_bits, (unsigned long long)__double_as_longlong(me));
+                atomicMax(&a.ds->max_abs_bits, (unsigned long long)__double_as_longlong(ma));
+                if (ni) atomicOr(&a.ds->not_int, 1u);
+                if (bd) atomicOr(&a.ds->bad, 1u);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void maxabs_kernel(const float *rows, long total, unsigned int *out) {
+    float m = 0.0f;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        float v = fabsf(rows[i]);
+        m = isfinite(v) ? fmaxf(m, v) : m;
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// ------------------------------------------------------------------------------------------
+// 1. MFMA shortlist.  Workgroup = 4 waves; wave = 2 query blocks of 32 (64 queries); the
+// candidate blocks of this split stream through a double-buffered LDS ring (CB blocks/stage).
+// ------------------------------------------------------------------------------------------
+template <int L>
+__device__ __forceinline__ void list_insert(float (&k)[L], int (&id)[L], float x, int ix) {
+#pragma unroll
+    for (int i = L - 1; i > 0; --i) {
+        const bool gp = k[i - 1] > x, gc = k[i] > x;
+        const float nk = gp ? k[i - 1] : (gc ? x : k[i]);
+        const int ni = gp ? id[i - 1] : (gc ? ix : id[i]);
+        k[i] = nk;
+        id[i] = ni;
+    }
+    if (k[0] > x) {
+        k[0] = x;
+        id[0] = ix;
+    }
+}
+
+template <int L>
+__device__ __forceinline__ void scan_keys(const floatx16 &acc, const float (&nc)[16], int base, float (&lk)[L],
+                                          int (&li)[L]) {
+    float key[16];
+    float mn = INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        key[r] = fmaf(-2.0f, acc[r], nc[r]);
+        mn = fminf(mn, key[r]);
+    }
+    if (mn < lk[L - 1]) {
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+            if (key[r] < lk[L - 1]) list_insert<L>(lk, li, key[r], base + (r & 3) + 8 * (r >> 2));
+    }
+}
+
+template <int S, int L, int CB>
+__global__ __launch_bounds__(256, 2) void nn_shortlist_kernel(const half8 *__restrict__ cfrag,
+                                                              const float *__restrict__ cnc, int nblk,
+                                                              const half8 *__restrict__ qfrag, int nq,
+                                                              int blk_per_split, int nsplit,
+                                                              float *__restrict__ out_key, int *__restrict__ out_idx) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int FRAG_BYTES = CB * S * 1024;
+    constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
+    constexpr int PER_T = CB * S * 64 / 256;
+    static_assert((CB * S * 64) % 256 == 0, "stage must split evenly over 256 threads");
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int nqblk = (nq + 31) / 32;
+    const int qb0 = (blockIdx.x * 4 + w) * 2;
+    const int split = blockIdx.y;
+    const int b_begin = split * blk_per_split;
+    const int b_end = min(nblk, b_begin + blk_per_split);
+
+    half8 bq0[S], bq1[S];
+    const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        bq0[s] = (qb0 < nqblk) ? qfrag[((long)qb0 * S + s) * 64 + lane] : zero8;
+        bq1[s] = (qb0 + 1 < nqblk) ? qfrag[((long)(qb0 + 1) * S + s) * 64 + lane] : zero8;
+    }
+    float lk0[L], lk1[L];
+    int li0[L], li1[L];
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+        lk0[i] = lk1[i] = INFINITY;
+        li0[i] = li1[i] = -1;
+    }
+
+    const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
+    uint4 stg[PER_T];
+    uint4 stg_nc = make_uint4(0, 0, 0, 0);
+    const uint4 inf4 = make_uint4(0x7f800000u, 0x7f800000u, 0x7f800000u, 0x7f800000u);
+    auto gload = [&](int st) {
+        const int blk0 = b_begin + st * CB;
+        const int avail = min(CB, b_end - blk0) * S * 64;
+        const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64;
+#pragma unroll
+        for (int j = 0; j < PER_T; j++) {
+            const int c = tid + j * 256;
+            stg[j] = (c < avail) ? src[c] : make_uint4(0, 0, 0, 0);
+        }
+        if (tid < CB * 8) {
+            const int bb = tid >> 3;
+            stg_nc = (blk0 + bb < b_end) ? reinterpret_cast<const uint4 *>(cnc)[(long)blk0 * 8 + tid] : inf4;
+        }
+    };
+    auto swrite = [&](int buf) {
+        uint4 *dst = reinterpret_cast<uint4 *>(smem + buf * BUF_BYTES);
+#pragma unroll
+        for (int j = 0; j < PER_T; j++) dst[tid + j * 256] = stg[j];
+        if (tid < CB * 8) reinterpret_cast<uint4 *>(smem + buf * BUF_BYTES + FRAG_BYTES)[tid] = stg_nc;
+    };
+
+    if (nstage > 0) {
+        gload(0);
+        swrite(0);
+    }
+    __syncthreads();
+    for (int st = 0; st < nstage; st++) {
+        if (st + 1 < nstage) gload(st + 1);
+        const char *B = smem + (st & 1) * BUF_BYTES;
+#pragma unroll
+        for (int cb = 0; cb < CB; cb++) {
+            const int blk = b_begin + st * CB + cb;
+            if (blk < b_end) {
+                floatx16 acc0 = {0}, acc1 = {0};
+#pragma unroll
+                for (int s = 0; s < S; s++) {
+                    const half8 av = reinterpret_cast<const half8 *>(B)[(cb * S + s) * 64 + lane];
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq0[s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq1[s], acc1, 0, 0, 0);
+                }
+                const float4 *np = reinterpret_cast<const float4 *>(B + FRAG_BYTES) + cb * 8 + h * 4;
+                const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
+                const float nc[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w,
+                                      n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
+                const int base = blk * 32 + 4 * h;
+                scan_keys<L>(acc0, nc, base, lk0, li0);
+                scan_keys<L>(acc1, nc, base, lk1, li1);
+            }
+        }
+        if (st + 1 < nstage) swrite((st + 1) & 1);
+        __syncthreads();
+    }
+    // partial lists: [q][split][h][L]
+#pragma unroll
+    for (int qb = 0; qb < 2; qb++) {
+        const int q = (qb0 + qb) * 32 + (lane & 31);
+        if (q < nq) {
+            const long o = (((long)q * nsplit + split) * 2 + h) * L;
+#pragma unroll
+            for (int i = 0; i < L; i++) {
+                out_key[o + i] = qb ? lk1[i] : lk0[i];
+                out_idx[o + i] = qb ? li1[i] : li0[i];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// 2. rescore: one wave per query.
+// ------------------------------------------------------------------------------------------
+struct RescoreArgs {
+    const float *rows;   // [n][d]
+    const float *q;      // [nq][d]
+    const QStat *qstat;
+    const float *key;
+    const int *idx;
+    int n, d, nq, k, L, nsplit;
+    double N, H, Ec, max_abs_c;
+    int ds_int;
+    int *out_idx;
+    float *out_err;
+    int *fb_list;
+    int *fb_count;
+    const int32_t *tr_tile, *tr_pal;
+    const uint8_t *tr_attr;
+    int32_t *m_tile, *m_pal;
+    uint8_t *m_hm, *m_vm;
+};
+
+__device__ __forceinline__ float exact_dist(const float *__restrict__ q, const float *__restrict__ c, int d) {
+    float dist = 0.0f;
+    int i = 0;
+    if ((d & 3) == 0) {
+        const float4 *q4 = reinterpret_cast<const float4 *>(q), *c4 = reinterpret_cast<const float4 *>(c);
+        for (; i < d / 4; i++) {
+            const float4 a = q4[i], b = c4[i];
+            float t;
+            t = a.x - b.x; dist = dist + t * t;
+            t = a.y - b.y; dist = dist + t * t;
+            t = a.z - b.z; dist = dist + t * t;
+            t = a.w - b.w; dist = dist + t * t;
+        }
+        return dist;
+    }
+    for (; i < d; i++) {
+        const float t = q[i] - c[i];
+        dist = dist + t * t;
+    }
+    return dist;
+}
+
+// lexicographic (v, i) wave minimum
+__device__ __forceinline__ void wave_argmin(float &v, int &i) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(v, o, 64);
+        const int oi = __shfl_xor(i, o, 64);
+        const bool take = (ov < v) || (ov == v && (unsigned)oi < (unsigned)i);
+        v = take ? ov : v;
+        i = take ? oi : i;
+    }
+}
+
+__device__ __forceinline__ void write_map(const RescoreArgs &a, long q, int best) {
+    if (!a.m_tile) return;
+    a.m_tile[q] = best >= 0 ? a.tr_tile[best] : -1;
+    a.m_pal[q] = best >= 0 ? a.tr_pal[best] : -1;
+    const int at = best >= 0 ? a.tr_attr[best] : 0;
+    a.m_hm[q] = (at & 1) != 0;
+    a.m_vm[q] = (at & 2) != 0;
+}
+
+__global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
+    const int lane = threadIdx.x & 63;
+    const long q = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= a.nq) return;
+    const int E = a.nsplit * 2 * a.L;
+    float key = INFINITY;
+    int idx = -1;
+    if (lane < E) {
+        key = a.key[q * E + lane];
+        idx = a.idx[q * E + lane];
+    }
+    const QStat st = a.qstat[q];
+    bool fallback = (st.flags & QF_BAD) != 0;
+    // k-th smallest key (lexicographic by (key, lane) so duplicates count separately)
+    float kk = INFINITY;
+    {
+        float v = (idx >= 0) ? key : INFINITY;
+        int who = lane;
+        bool taken = false;
+        for (int r = 0; r < a.k; r++) {
+            float mv = taken ? INFINITY : v;
+            int mi = taken ? 0x7fffffff : who;
+            wave_argmin(mv, mi);
+            kk = mv;
+            if (lane == mi) taken = true;
+        }
+    }
+    // threshold T (DESIGN.md "Exactness argument")
+    double T;
+    const double u = 5.9604644775390625e-08;  // 2^-24
+    const bool exact = a.ds_int && (st.flags & QF_INT) &&
+                       (double)a.d * a.max_abs_c * (double)st.pad * 4.0 < 16777216.0 &&
+                       (double)a.d * a.max_abs_c * a.max_abs_c < 16777216.0;
+    if (exact) {
+        T = kk;
+    } else {
+        const double nq = sqrt(st.n2);
+        const double gam = 2.0 * a.d * u;  // >= 2x gamma_d: MFMA accumulation, conservative
+        const double E = 1.05 * (2.0 * u * a.N * a.N + 2.0 * u * st.hn * a.H +
+                                 2.0 * (gam * st.hn * a.H + st.en * a.N + st.hn * a.Ec)) + 1e-30;
+        const double g = (double)(a.d + 4) * u / (1.0 - (double)(a.d + 4) * u) * 1.05;
+        T = ((st.n2 + (double)kk + E) * (1.0 + g) / (1.0 - g)) - st.n2 + E;
+        T += 1e-12 * (st.n2 + fabs((double)kk)) + 1e-30;
+        (void)nq;
+    }
+    if (!isfinite(kk)) T = INFINITY;
+    // overflow: a full list whose last kept key is <= T may have dropped a needed candidate
+    if (!exact || a.L < a.k) {
+        const bool last = lane < E && (lane % a.L) == a.L - 1;
+        if (__any(last && idx >= 0 && (double)key <= T)) fallback = true;
+    }
+    const bool cand = (idx >= 0) && ((double)key <= T);
+    float dist = INFINITY;
+    int di = 0x7fffffff;
+    if (!fallback && cand) {
+        dist = exact_dist(a.q + q * a.d, a.rows + (long)idx * a.d, a.d);
+        di = idx;
+    }
+    if (fallback) {
+        if (lane == 0) {
+            const int p = atomicAdd(a.fb_count, 1);
+            a.fb_list[p] = (int)q;
+        }
+        return;
+    }
+    // top-k by (dist, idx)
+    bool taken = false;
+    for (int r = 0; r < a.k; r++) {
+        float mv = taken ? INFINITY : dist;
+        int mi = taken ? 0x7fffffff : di;
+        wave_argmin(mv, mi);
+        if (!taken && di == mi && mi != 0x7fffffff) taken = true;
+        if (lane == 0) {
+            const bool ok = mi != 0x7fffffff;
+            a.out_idx[q * a.k + r] = ok ? mi : -1;
+            a.out_err[q * a.k + r] = ok ? mv : FLT_MAX;
+            if (r == 0) write_map(a, q, ok ? mi : -1);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// 3. exhaustive exact scan (queued queries, k > 8): one workgroup per query, grid-stride list.
+// ------------------------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256) void nn_exact_kernel(RescoreArgs a, int list_n) {
+    __shared__ float sq[1024];
+    __shared__ float sd[256 * K];
+    __shared__ int si[256 * K];
+    const int tid = threadIdx.x;
+    const int count = a.fb_list ? *a.fb_count : list_n;
+    for (int qi = blockIdx.x; qi < count; qi += gridDim.x) {
+        const long q = a.fb_list ? a.fb_list[qi] : qi;
+        __syncthreads();
+        for (int i = tid; i < a.d; i += 256) sq[i] = a.q[q * a.d + i];
+        __syncthreads();
+        float bd[K];
+        int bi[K];
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            bd[i] = FLT_MAX;
+            bi[i] = -1;
+        }
+        int cnt = 0;
+        for (int j = tid; j < a.n; j += 256) {
+            const float *c = a.rows + (long)j * a.d;
+            float dist = 0.0f;
+            const float lim = (cnt < K) ? INFINITY : bd[K - 1];
+            int i = 0;
+            for (; i < a.d; i++) {
+                const float t = sq[i] - c[i];
+                dist = dist + t * t;
+                if (dist > lim) break;
+            }
+            if (i < a.d) continue;
+            if (cnt == K && !(dist < bd[K - 1])) continue;  // equal keeps the earlier index
+            list_insert<K>(bd, bi, dist, j);
+            if (cnt < K) cnt++;
+        }
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            sd[tid * K + i] = (i < cnt) ? bd[i] : INFINITY;
+            si[tid * K + i] = (i < cnt) ? bi[i] : 0x7fffffff;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            // each lane holds 4 thread lists; extract the k best by (dist, idx)
+            int ptr[4] = {0, 0, 0, 0};
+            for (int r = 0; r < a.k; r++) {
+                float lv = INFINITY;
+                int li = 0x7fffffff, lt = -1;
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const int th = tid * 4 + t;
+                    if (ptr[t] < K) {
+                        const float v = sd[th * K + ptr[t]];
+                        const int ii = si[th * K + ptr[t]];
+                        if (v < lv || (v == lv && (unsigned)ii < (unsigned)li)) {
+                            lv = v;
+                            li = ii;
+                            lt = t;
+                        }
+                    }
+                }
+                float mv = lv;
+                int mi = li;
+                wave_argmin(mv, mi);
+                if (lt >= 0 && li == mi && mi != 0x7fffffff) ptr[lt]++;
+                if (tid == 0) {
+                    const bool ok = mi != 0x7fffffff;
+                    a.out_idx[q * a.k + r] = ok ? mi : -1;
+                    a.out_err[q * a.k + r] = ok ? mv : FLT_MAX;
+                    if (r == 0) write_map(a, q, ok ? mi : -1);
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+static int pick_S(int d) {
+    const int s = (d + 15) / 16;
+    if (s <= 4) return 4;
+    if (s <= 8) return 8;
+    if (s <= 12) return 12;
+    if (s <= 16) return 16;
+    return 0;  // exact kernel only
+}
+
+NNIndex *nn_index_create_dev(float *d_rows, int n, int d, hipStream_t stream) {
+    NNIndex *ix = new NNIndex();
+    ix->n = n;
+    ix->d = d;
+    ix->d_rows = d_rows;
+    ix->S = pick_S(d);
+    ix->nblk = (n + 31) / 32;
+    TILER_HIP_CHECK_NULL(hipHostMalloc((void **)&ix->h_fb_count, sizeof(int) * 2, hipHostMallocDefault));
+    if (ix->S == 0 || n == 0) return ix;
+    // scale: power of two so that max|v| * scale <= 16384
+    unsigned int *d_m = nullptr;
+    DsStat *d_ds = nullptr;
+    TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_m, sizeof(unsigned int)));
+    TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_ds, sizeof(DsStat)));
+    TILER_HIP_CHECK_NULL(hipMemsetAsync(d_m, 0, sizeof(unsigned int), stream));
+    TILER_HIP_CHECK_NULL(hipMemsetAsync(d_ds, 0, sizeof(DsStat), stream));
+    const long total = (long)n * d;
+    hipLaunchKernelGGL(maxabs_kernel, dim3((unsigned)std::min<long>(2048, (total + 255) / 256)), dim3(256), 0, stream,
+                       d_rows, total, d_m);
+    unsigned int mbits = 0;
+    TILER_HIP_CHECK_NULL(hipMemcpyAsync(&mbits, d_m, sizeof(mbits), hipMemcpyDeviceToHost, stream));
+    TILER_HIP_CHECK_NULL(hipStreamSynchronize(stream));
+    float mabs;
+    memcpy(&mabs, &mbits, 4);
+    float scale = 1.0f;
+    if (mabs > 0.0f) {
+        int e;
+        frexpf(16384.0f / mabs, &e);
+        scale = ldexpf(1.0f, e - 1);
+        if (scale > 1.0f && mabs == rintf(mabs)) scale = 1.0f;  // keep small integers exact
+    }
+    ix->scale = scale;
+    TILER_HIP_CHECK_NULL(hipMalloc(&ix->d_frag, (size_t)ix->nblk * ix->S * 64 * 16));
+    TILER_HIP_CHECK_NULL(hipMalloc((void **)&ix->d_nc, (size_t)ix->nblk * 32 * sizeof(float)));
+    PrepArgs pa{d_rows, n, d, ix->S, scale, (half8 *)ix->d_frag, ix->d_nc, nullptr, d_ds};
+    hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)std::min<long>(4096, (ix->nblk + 3) / 4)), dim3(256), 0,
+                       stream, pa);
+    TILER_HIP_CHECK_NULL(hipGetLastError());
+    DsStat ds;
+    TILER_HIP_CHECK_NULL(hipMemcpyAsync(&ds, d_ds, sizeof(ds), hipMemcpyDeviceToHost, stream));
+    TILER_HIP_CHECK_NULL(hipStreamSynchronize(stream));
+    hipFree(d_m);
+    hipFree(d_ds);
+    auto bits2d = [](unsigned long long b) {
+        double v;
+        memcpy(&v, &b, 8);
+        return v;
+    };
+    ix->maxN = sqrt(bits2d(ds.max_n2_bits));
+    ix->maxH = sqrt(bits2d(ds.max_h2_bits));
+    ix->maxE = sqrt(bits2d(ds.max_e2_bits));
+    const double maxabs = bits2d(ds.max_abs_bits);
+    ix->max_abs = maxabs;
+    ix->exact_int = (ds.not_int == 0) && scale == 1.0f && maxabs <= 2048.0;
+    if (ds.bad) ix->S = 0;  // non-finite / out-of-range data: exhaustive path only
+    return ix;
+}
+
+void nn_index_destroy(NNIndex *ix) {
+    if (!ix) return;
+    hipFree(ix->d_rows);
+    hipFree(ix->d_frag);
+    hipFree(ix->d_nc);
+    hipFree(ix->d_tr_tile);
+    hipFree(ix->d_tr_pal);
+    hipFree(ix->d_tr_attr);
+    SearchScratch &s = ix->scratch;
+    hipFree(s.qfrag);
+    hipFree(s.qstat);
+    hipFree(s.key);
+    hipFree(s.idx);
+    hipFree(s.fb_list);
+    hipFree(s.fb_count);
+    hipFree(s.qrows);
+    hipHostFree(ix->h_fb_count);
+    delete ix;
+}
+
+static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
+    SearchScratch &s = ix->scratch;
+    if ((size_t)nq > s.cap_q) {
+        hipFree(s.qfrag);
+        hipFree(s.qstat);
+        hipFree(s.fb_list);
+        hipFree(s.fb_count);
+        const long nqblk = (nq + 31) / 32 + 2;
+        TILER_HIP_CHECK(hipMalloc(&s.qfrag, (size_t)nqblk * 16 * 64 * 16));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.qstat, (size_t)nq * sizeof(QStat)));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.fb_list, (size_t)nq * sizeof(int)));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.fb_count, 16));
+        s.cap_q = nq;
+    }
+    if ((size_t)nkeys > s.cap_keys) {
+        hipFree(s.key);
+        hipFree(s.idx);
+        TILER_HIP_CHECK(hipMalloc((void **)&s.key, (size_t)nkeys * sizeof(float)));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.idx, (size_t)nkeys * sizeof(int)));
+        s.cap_keys = nkeys;
+    }
+    return 0;
+}
+
+template <int S, int L, int CB>
+static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
+    const int nqblk = (nq + 31) / 32;
+    const dim3 grid((nqblk + 7) / 8, nsplit);
+    const size_t lds = 2 * (CB * S * 1024 + CB * 128);
+    KTimer tm("nn_shortlist", stream);
+    hipLaunchKernelGGL((nn_shortlist_kernel<S, L, CB>), grid, dim3(256), lds, stream, (const half8 *)ix->d_frag,
+                       ix->d_nc, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps, nsplit, ix->scratch.key,
+                       ix->scratch.idx);
+}
+
+template <int L>
+static int dispatch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
+    switch (ix->S) {
+        case 4: launch_shortlist<4, L, 6>(ix, nq, nsplit, bps, stream); break;
+        case 8: launch_shortlist<8, L, 3>(ix, nq, nsplit, bps, stream); break;
+        case 12: launch_shortlist<12, L, 2>(ix, nq, nsplit, bps, stream); break;
+        case 16: launch_shortlist<16, L, 2>(ix, nq, nsplit, bps, stream); break;
+        default: set_error("nn: unsupported fragment depth"); return -1;
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+static int launch_exact(RescoreArgs ra, int list_n, int grid, hipStream_t stream) {
+    if (ra.d > 1024) {
+        set_error("nn: dimension > 1024 unsupported");
+        return -1;
+    }
+    KTimer tm("nn_exact", stream);
+    if (ra.k <= 1)
+        hipLaunchKernelGGL(nn_exact_kernel<1>, dim3(grid), dim3(256), 0, stream, ra, list_n);
+    else if (ra.k <= 8)
+        hipLaunchKernelGGL(nn_exact_kernel<8>, dim3(grid), dim3(256), 0, stream, ra, list_n);
+    else if (ra.k <= 32)
+        hipLaunchKernelGGL(nn_exact_kernel<32>, dim3(grid), dim3(256), 0, stream, ra, list_n);
+    else {
+        set_error("nn: k > 32 unsupported");
+        return -1;
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
+                  hipStream_t stream) {
+    if (nq <= 0) return 0;
+    if (k < 1 || k > 32) {
+        set_error("nn: k must be in 1..32");
+        return -1;
+    }
+    RescoreArgs ra{};
+    ra.rows = ix->d_rows;
+    ra.q = d_q;
+    ra.n = ix->n;
+    ra.d = ix->d;
+    ra.nq = nq;
+    ra.k = k;
+    ra.N = ix->maxN;
+    ra.H = ix->maxH;
+    ra.Ec = ix->maxE;
+    ra.ds_int = ix->exact_int ? 1 : 0;
+    ra.max_abs_c = ix->max_abs;
+    ra.out_idx = d_idx;
+    ra.out_err = d_err;
+    if (maps && k == 1 && ix->d_tr_tile) {
+        ra.tr_tile = ix->d_tr_tile;
+        ra.tr_pal = ix->d_tr_pal;
+        ra.tr_attr = ix->d_tr_attr;
+        ra.m_tile = maps->tile;
+        ra.m_pal = maps->pal;
+        ra.m_hm = maps->hm;
+        ra.m_vm = maps->vm;
+    }
+    ix->last_queries = nq;
+    const bool mfma = ix->S > 0 && k <= 8;
+    if (!mfma) {
+        ix->last_splits = 0;
+        ix->last_fallback = nq;
+        ra.fb_list = nullptr;
+        return launch_exact(ra, nq, std::min(nq, 4096), stream);
+    }
+    const int L = (k == 1) ? 4 : 8;
+    const int max_split = 64 / (2 * L);
+    const int wgs = ((nq + 31) / 32 + 7) / 8;
+    int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
+    nsplit = std::min(nsplit, ix->nblk);
+    const int bps = (ix->nblk + nsplit - 1) / nsplit;
+    nsplit = (ix->nblk + bps - 1) / bps;
+    ix->last_splits = nsplit;
+    if (ensure_scratch(ix, nq, (long)nq * nsplit * 2 * L)) return -1;
+    SearchScratch &s = ix->scratch;
+    TILER_HIP_CHECK(hipMemsetAsync(s.fb_count, 0, 16, stream));
+    // queries -> fragments (same layout and scale as the dataset)
+    const long nqblk = (nq + 31) / 32;
+    PrepArgs pa{d_q, nq, ix->d, ix->S, ix->scale, (half8 *)s.qfrag, nullptr, s.qstat, nullptr};
+    {
+        KTimer t_prep("nn_prep", stream);
+        hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)std::min<long>(4096, (nqblk + 3) / 4)), dim3(256), 0,
+                           stream, pa);
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    if ((L == 4 ? dispatch_shortlist<4>(ix, nq, nsplit, bps, stream)
+                : dispatch_shortlist<8>(ix, nq, nsplit, bps, stream)))
+        return -1;
+    ra.qstat = s.qstat;
+    ra.key = s.key;
+    ra.idx = s.idx;
+    ra.L = L;
+    ra.nsplit = nsplit;
+    ra.fb_list = s.fb_list;
+    ra.fb_count = s.fb_count;
+    {
+        KTimer t_rs("nn_rescore", stream);
+        hipLaunchKernelGGL(nn_rescore_kernel, dim3((nq + 3) / 4), dim3(256), 0, stream, ra);
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    // queued queries: a fixed grid that reads the device-side count (no host round trip)
+    if (launch_exact(ra, 0, std::min(nq, 512), stream)) return -1;
+    TILER_HIP_CHECK(hipMemcpyAsync(ix->h_fb_count, s.fb_count, sizeof(int), hipMemcpyDeviceToHost, stream));
+    return 0;
+}
+
+int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int *d_idx,
+                        float *d_err, const FtMaps *maps, hipStream_t stream) {
+    if (Q <= 0) return 0;
+    if (ix->d != 192) {
+        set_error("frame tiling: dataset dimension must be 192 (cTileDCTSize)");
+        return -1;
+    }
+    SearchScratch &s = ix->scratch;
+    if ((size_t)Q > s.cap_rows) {
+        hipFree(s.qrows);
+        TILER_HIP_CHECK(hipMalloc((void **)&s.qrows, (size_t)Q * 192 * sizeof(float)));
+        s.cap_rows = Q;
+    }
+    PsyvArgs pa;
+    pa.n = Q;
+    pa.rgb = d_rgb;
+    pa.flags = use_wavelets ? PSYV_WAVELETS : 0;
+    pa.gamma = gamma;
+    pa.out32 = s.qrows;
+    if (launch_psyv(pa, stream)) return -1;
+    return nn_search_dev(ix, s.qrows, Q, 1, d_idx, d_err, maps, stream);
+}
+
+}  // namespace tiler

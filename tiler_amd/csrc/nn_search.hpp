@@ -1,0 +1,76 @@
+// nn_search.hpp -- exact nearest-neighbour search on gfx950 (internal interface).
+#pragma once
+#include <mutex>
+#include <vector>
+
+#include "tiler_common.hpp"
+
+namespace tiler {
+
+// dataset statistics reduced on device (norm bounds in the scaled space, see nn_search.hip)
+struct DsStat {
+    unsigned long long max_n2_bits;  // max ||c||^2 (double bits; positive doubles order like u64)
+    unsigned long long max_h2_bits;  // max ||fp16(c)||^2
+    unsigned long long max_e2_bits;  // max ||c - fp16(c)||^2
+    unsigned long long max_abs_bits; // max |c| (double bits)
+    unsigned int not_int;            // any value not a small integer (|v| <= 2048)
+    unsigned int bad;                // any non-finite value or fp16 overflow
+    unsigned int pad[2];
+};
+
+// per-query statistics (written by the query prep kernel)
+struct QStat {
+    double n2;     // ||q||^2 (scaled space)
+    double hn;     // ||fp16(q)||
+    double en;     // ||q - fp16(q)||
+    int flags;     // bit0: integer query, bit1: bad (non-finite / fp16 overflow) -> exact path
+    int pad;
+};
+
+struct SearchScratch {
+    void *qfrag = nullptr;
+    QStat *qstat = nullptr;
+    float *key = nullptr;
+    int *idx = nullptr;
+    int *fb_list = nullptr;
+    int *fb_count = nullptr;  // [2]: count, pad
+    float *qrows = nullptr;   // fp32 query rows (frame-tiling path: descriptors)
+    size_t cap_q = 0, cap_keys = 0, cap_rows = 0;
+};
+
+struct NNIndex {
+    int n = 0, d = 0, S = 0, nblk = 0;
+    float scale = 1.0f;         // power of two applied before the fp16 split (keeps |v| <= 16384)
+    double maxN = 0, maxH = 0, maxE = 0, max_abs = 0;
+    bool exact_int = false;
+    float *d_rows = nullptr;    // [n][d] fp32 (exact rescoring)
+    void *d_frag = nullptr;     // [nblk][S][64][8] fp16, MFMA A-operand fragment order
+    float *d_nc = nullptr;      // [nblk][32] ||c||^2 in accumulator-row order (+inf on padding rows)
+    int32_t *d_tr_tile = nullptr, *d_tr_pal = nullptr;
+    uint8_t *d_tr_attr = nullptr;
+    SearchScratch scratch;
+    std::mutex mu;
+    long long last_queries = 0, last_fallback = 0;
+    int last_splits = 0;
+    int *h_fb_count = nullptr;  // pinned
+};
+
+// build the device index from fp32 rows already in HBM (takes ownership of d_rows)
+NNIndex *nn_index_create_dev(float *d_rows, int n, int d, hipStream_t stream);
+void nn_index_destroy(NNIndex *ix);
+
+struct FtMaps {
+    int32_t *tile = nullptr, *pal = nullptr;
+    uint8_t *hm = nullptr, *vm = nullptr;
+};
+
+// k nearest neighbours of nq fp32 query rows in HBM; results [nq][k] in HBM; async on stream.
+// If maps is non-null (k == 1) the FrameTiling tilemap items are written too.
+int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
+                  hipStream_t stream);
+
+// frame tiling: RGB tiles -> descriptors (fp32) -> search -> tilemap items
+int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int *d_idx,
+                        float *d_err, const FtMaps *maps, hipStream_t stream);
+
+}  // namespace tiler

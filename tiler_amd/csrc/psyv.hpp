@@ -1,0 +1,28 @@
+// psyv.hpp -- descriptor kernel interface (internal).
+#pragma once
+#include "tiler_common.hpp"
+
+namespace tiler {
+
+enum { PSYV_FROM_PAL = 1, PSYV_WAVELETS = 2, PSYV_QWEIGHT = 8, PSYV_HMIRROR = 16, PSYV_VMIRROR = 32 };
+
+struct PsyvArgs {
+    long n = 0;
+    const int32_t *rgb = nullptr;       // [n][64]
+    const uint8_t *palpix = nullptr;    // [T][64]
+    const int32_t *tile_of = nullptr;   // [n] or null (identity)
+    const int32_t *palettes = nullptr;  // [P][16]
+    const int32_t *pal_of = nullptr;    // [n] or null (palette 0)
+    const uint8_t *flags_per = nullptr; // [n] or null
+    int flags = 0;
+    int gamma = -1;
+    double *out64 = nullptr;            // [n][192]
+    float *out32 = nullptr;             // [n][192]
+    // filled by launch_psyv from the shared LUTs
+    const double *gamma_lut = nullptr, *dct_lut = nullptr, *qmul = nullptr, *ratio = nullptr;
+    double haar_f = 0, u_mul = 0, v_mul = 0;
+};
+
+int launch_psyv(PsyvArgs args, hipStream_t stream);
+
+}  // namespace tiler

@@ -1,0 +1,163 @@
+"""Seeded synthetic inputs for the tile-search hot path.
+
+There is no video (ffmpeg.exe / Load step are out of scope), so frames, palettes and the global
+tileset are generated with numpy's PCG64 from a recorded seed:
+  - frame tiles: 50 % smooth gradients, 30 % textured (uniform +-32 around a per-tile mean), 20 % flat;
+    frames of one keyframe evolve from the first (a share of tiles re-drawn per frame) so Smooth has work;
+  - palettes: P x 16 uniform RGB (0x00BBGGRR, main.pas:566-569);
+  - tileset: T random 4-bit index tiles, 20 % made H- and/or V-symmetric (exact mirror ties), then
+    canonicalised like PrepareTileMirrors (main.pas:4049-4069); one palette per tile (P_eff = 1).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+TILE = 8
+
+
+def rgb_pack(r, g, b):
+    return (np.asarray(b, np.int32) << 16) | (np.asarray(g, np.int32) << 8) | np.asarray(r, np.int32)
+
+
+def frame_tiles(rng: np.random.Generator, n: int) -> np.ndarray:
+    """n RGB tiles [n, 64] int32 (0x00BBGGRR)."""
+    kind = rng.random(n)
+    out = np.empty((n, 64, 3), np.float64)
+    yy, xx = np.mgrid[0:8, 0:8]
+    yy = yy.reshape(64) / 7.0
+    xx = xx.reshape(64) / 7.0
+    grad = kind < 0.5
+    tex = (kind >= 0.5) & (kind < 0.8)
+    flat = kind >= 0.8
+    ng = int(grad.sum())
+    c0 = rng.integers(0, 256, (ng, 1, 3)).astype(np.float64)
+    c1 = rng.integers(0, 256, (ng, 1, 3)).astype(np.float64)
+    ang = rng.random((ng, 1, 1)) * 2 * np.pi
+    t = (np.cos(ang) * xx[None, :, None] + np.sin(ang) * yy[None, :, None])
+    t = (t - t.min(axis=1, keepdims=True)) / np.maximum(np.ptp(t, axis=1, keepdims=True), 1e-9)
+    out[grad] = c0 + (c1 - c0) * t
+    nt = int(tex.sum())
+    mean = rng.integers(32, 224, (nt, 1, 3)).astype(np.float64)
+    out[tex] = mean + rng.integers(-32, 33, (nt, 64, 3))
+    nf = int(flat.sum())
+    out[flat] = rng.integers(0, 256, (nf, 1, 3)).astype(np.float64)
+    px = np.clip(np.rint(out), 0, 255).astype(np.int32)
+    return rgb_pack(px[..., 0], px[..., 1], px[..., 2])
+
+
+def keyframe_frames(rng: np.random.Generator, frames: int, tiles_per_frame: int, change: float = 0.3) -> np.ndarray:
+    """[frames, Q, 64] int32; each frame re-draws `change` of the previous frame's tiles."""
+    out = np.empty((frames, tiles_per_frame, 64), np.int32)
+    out[0] = frame_tiles(rng, tiles_per_frame)
+    for f in range(1, frames):
+        out[f] = out[f - 1]
+        sel = np.nonzero(rng.random(tiles_per_frame) < change)[0]
+        if sel.size:
+            out[f, sel] = frame_tiles(rng, sel.size)
+    return out
+
+
+def palettes(rng: np.random.Generator, count: int, size: int = 16) -> np.ndarray:
+    c = rng.integers(0, 256, (count, size, 3))
+    return rgb_pack(c[..., 0], c[..., 1], c[..., 2])
+
+
+def hflip(t: np.ndarray) -> np.ndarray:
+    return t.reshape(-1, 8, 8)[:, :, ::-1].reshape(t.shape)
+
+
+def vflip(t: np.ndarray) -> np.ndarray:
+    return t.reshape(-1, 8, 8)[:, ::-1, :].reshape(t.shape)
+
+
+def prepare_tile_mirrors(pal_tiles: np.ndarray):
+    """PrepareTileMirrors main.pas:4049-4069: pick the quadrant (v-outer, h-inner, first max) with the
+    largest palette-index sum, flip it to the top-left; returns (tiles, HMirror, VMirror)."""
+    t = pal_tiles.reshape(-1, 8, 8).astype(np.int64)
+    sums = np.stack([t[:, 0:4, 0:4].sum((1, 2)), t[:, 0:4, 4:8].sum((1, 2)),
+                     t[:, 4:8, 0:4].sum((1, 2)), t[:, 4:8, 4:8].sum((1, 2))], 1)  # order (vf,hf)=FF,FT,TF,TT
+    best = np.argmax(sums, axis=1)  # first max == strict '>' scan in the reference
+    hm = (best & 1).astype(np.uint8)
+    vm = (best >> 1).astype(np.uint8)
+    out = pal_tiles.copy()
+    out[hm == 1] = hflip(out[hm == 1])
+    out[vm == 1] = vflip(out[vm == 1])
+    return out, hm, vm
+
+
+def tileset(rng: np.random.Generator, count: int, palsize: int = 16, sym_share: float = 0.2):
+    """[count, 64] uint8 palette-index tiles (canonical orientation) + HMirror/VMirror flags."""
+    t = rng.integers(0, palsize, (count, 64)).astype(np.uint8).reshape(-1, 8, 8)
+    kind = rng.random(count)
+    hs = kind < sym_share * 0.4
+    vs = (kind >= sym_share * 0.4) & (kind < sym_share * 0.8)
+    hv = (kind >= sym_share * 0.8) & (kind < sym_share)
+    t[hs, :, 4:] = t[hs, :, 3::-1]
+    t[vs, 4:, :] = t[vs, 3::-1, :]
+    t[hv, :, 4:] = t[hv, :, 3::-1]
+    t[hv, 4:, :] = t[hv, 3::-1, :]
+    tiles = t.reshape(count, 64)
+    return prepare_tile_mirrors(tiles)
+
+
+@dataclass
+class FTDataset:
+    """The keyframe search dataset of PrepareFrameTiling.DoPsyV (main.pas:3883-3919) as index arrays:
+    candidate r = descriptor of tile_of[r] in palette pal_of[r] with attrs (H=1, V=2); psyv_flags[r] is
+    the mirror actually applied (attrs xor the tile's canonical flags, main.pas:3912)."""
+    tile_of: np.ndarray
+    pal_of: np.ndarray
+    attrs: np.ndarray
+    psyv_flags: np.ndarray
+
+
+def ft_dataset_from_used(used: np.ndarray, thm: np.ndarray, tvm: np.ndarray) -> FTDataset:
+    """Emission order of DoPsyV: palette asc, tile asc, vmir F/T, hmir F/T (used[p, i, vm<<1|hm])."""
+    P, T, _ = used.shape
+    p, i, a = np.nonzero(used)  # row-major: p, then i, then a = (vm<<1)|hm ascending == vmir outer, hmir inner
+    hm = (a & 1).astype(np.uint8)
+    vm = ((a >> 1) & 1).astype(np.uint8)
+    fl = (((hm ^ thm[i]) * 16) | ((vm ^ tvm[i]) * 32)).astype(np.uint8)
+    return FTDataset(i.astype(np.int32), p.astype(np.int32), (hm | (vm << 1)).astype(np.uint8), fl)
+
+
+def used_one_palette(tile_pal: np.ndarray, P: int) -> np.ndarray:
+    """P_eff = 1 benchmark shape: every tile's 4 orientations used in its own palette only."""
+    T = tile_pal.shape[0]
+    used = np.zeros((P, T, 4), np.uint8)
+    used[tile_pal, np.arange(T), :] = 1
+    return used
+
+
+@dataclass
+class Workload:
+    seed: int
+    width: int
+    height: int
+    frames: int
+    tileset_size: int
+    palettes: np.ndarray
+    tiles: np.ndarray
+    thm: np.ndarray
+    tvm: np.ndarray
+    tile_pal: np.ndarray
+    frame_rgb: np.ndarray  # [frames, Q, 64]
+    ds: FTDataset
+
+    @property
+    def tiles_per_frame(self) -> int:
+        return (self.width // TILE) * (self.height // TILE)
+
+
+def make_workload(seed: int, width: int, height: int, frames: int, tileset_size: int, n_palettes: int = 128,
+                  palsize: int = 16) -> Workload:
+    rng = np.random.default_rng(seed)
+    pals = palettes(rng, n_palettes, palsize)
+    tiles, thm, tvm = tileset(rng, tileset_size, palsize)
+    tile_pal = rng.integers(0, n_palettes, tileset_size).astype(np.int32)
+    q = (width // TILE) * (height // TILE)
+    fr = keyframe_frames(rng, frames, q)
+    ds = ft_dataset_from_used(used_one_palette(tile_pal, n_palettes), thm, tvm)
+    return Workload(seed, width, height, frames, tileset_size, pals, tiles, thm, tvm, tile_pal, fr, ds)

@@ -105,6 +105,10 @@ int tiler_frame_tiling_dev(ann_kdtree *akd, const int32_t *d_rgb, int Q, int use
 int tiler_smooth_keyframe(int F, int Q, int32_t *tile, int32_t *tmpidx, int32_t *pal, uint8_t *hm, uint8_t *vm,
                           uint8_t *smoothed, int T, const uint8_t *palpix, int P, const int32_t *palettes,
                           double strength);
+/* Same with every array in HBM (tmpidx may be NULL); asynchronous on stream. */
+int tiler_smooth_keyframe_dev(int F, int Q, int32_t *d_tile, int32_t *d_tmpidx, int32_t *d_pal, uint8_t *d_hm,
+                              uint8_t *d_vm, uint8_t *d_smoothed, const uint8_t *d_palpix, const int32_t *d_palettes,
+                              double strength, void *stream);
 
 /* ---- GlobalTiling K-Modes (TKModes.ComputeKModes kmodes.pas:917-1060) ----
  * X[n][nattr] bytes; k clusters; start_point = -ANumInit (the DoKModes call, main.pas:4218); labels[n]

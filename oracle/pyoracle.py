@@ -32,6 +32,8 @@ def lib():
         _o.or_randint.restype = ctypes.c_uint32
         _o.or_palette_corr.restype = ctypes.c_double
         _o.or_dist.restype = ctypes.c_float
+        _o.or_dct_lut.restype = ctypes.c_void_p
+        _o.or_gamma_lut.restype = ctypes.c_void_p
         _o.or_set_gamma.argtypes = [ctypes.c_double, ctypes.c_double]
         _o.or_smooth.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 8 + [ctypes.c_double]
         _o.or_eqtc.argtypes = [ctypes.c_double]

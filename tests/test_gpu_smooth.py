@@ -1,0 +1,69 @@
+"""GPU parity of Smooth (DoTemporalSmoothing main.pas:4071-4119) against the CPU restatement: items and
+Smoothed flags bit-exact, including the 'PrevTMI^ := TMI^' branch that rewrites frame i-1."""
+import numpy as np
+import pytest
+
+from tiler_amd import synth
+from tiler_amd.smooth import smooth_keyframe
+
+pytestmark = pytest.mark.gpu
+
+
+def _tilemaps(rng, F, Q, T, P, repeat=0.6):
+    """Tilemaps with temporal coherence: most positions keep (or nearly keep) the previous item."""
+    tile = np.zeros((F, Q), np.int32)
+    pal = np.zeros((F, Q), np.int32)
+    hm = np.zeros((F, Q), np.uint8)
+    vm = np.zeros((F, Q), np.uint8)
+    tile[0] = rng.integers(0, T, Q)
+    pal[0] = rng.integers(0, P, Q)
+    hm[0] = rng.integers(0, 2, Q)
+    vm[0] = rng.integers(0, 2, Q)
+    for f in range(1, F):
+        r = rng.random(Q)
+        keep = r < repeat
+        near = (r >= repeat) & (r < repeat + (1 - repeat) * 0.6)
+        tile[f] = np.where(keep, tile[f - 1], rng.integers(0, T, Q))
+        pal[f] = np.where(keep, pal[f - 1], rng.integers(0, P, Q))
+        hm[f] = np.where(keep, hm[f - 1], rng.integers(0, 2, Q))
+        vm[f] = np.where(keep, vm[f - 1], rng.integers(0, 2, Q))
+        # near variants: the twin tile (T/2 apart, one pixel differs) or the twin palette (0 <-> 1)
+        twin_t = (tile[f - 1] + T // 2) % T
+        tile[f] = np.where(near & (r < repeat + 0.12), twin_t, tile[f])
+        pal[f] = np.where(near & (r < repeat + 0.12), pal[f - 1], pal[f])
+        other = near & (r >= repeat + 0.12)
+        tile[f] = np.where(other, tile[f - 1], tile[f])
+        pal[f] = np.where(other, np.where(pal[f - 1] == 0, 1, 0), pal[f])
+        hm[f] = np.where(near, hm[f - 1], hm[f])
+        vm[f] = np.where(near, vm[f - 1], vm[f])
+    return tile, pal, hm, vm
+
+
+@pytest.mark.parametrize("strength", [0.02, 0.08, 0.0])
+def test_smooth_bit_exact(gpu, oracle, strength):
+    rng = np.random.default_rng(31)
+    F, Q, T, P = 12, 700, 120, 5
+    palpix = rng.integers(0, 16, (T, 64)).astype(np.uint8)
+    # near-duplicate tiles (one pixel index apart) so |cmp| lands on both sides of Strength
+    palpix[60:] = palpix[:60]
+    palpix[60:, 5] = (palpix[60:, 5] + 1) % 16
+    pals = synth.palettes(rng, P)
+    pals[1] = pals[0] + 1
+    tile, pal, hm, vm = _tilemaps(rng, F, Q, T, P)
+    sm = np.zeros((F, Q), np.uint8)
+    tmp = rng.integers(-1, 100, (F, Q)).astype(np.int32)
+    g = smooth_keyframe(tile, pal, hm, vm, sm, palpix, pals, strength, tmpidx=tmp)
+    o = oracle.smooth(tile, pal, hm, vm, sm, palpix, pals, strength, tmpidx=tmp)
+    for a, b in zip(g, o):
+        assert np.array_equal(a, b)
+    changed = int(np.count_nonzero(g[0] != tile))
+    if strength > 0:
+        assert g[4].sum() > 0 and changed > 0  # both branches exercised
+
+
+def test_smooth_single_frame_is_identity(gpu):
+    rng = np.random.default_rng(1)
+    tile = rng.integers(0, 10, (1, 50)).astype(np.int32)
+    z = np.zeros((1, 50), np.uint8)
+    g = smooth_keyframe(tile, np.zeros_like(tile), z, z, z, rng.integers(0, 16, (10, 64)), synth.palettes(rng, 1))
+    assert np.array_equal(g[0], tile)

@@ -519,6 +519,14 @@ int tiler_smooth_keyframe(int F, int Q, int32_t *tile, int32_t *tmpidx, int32_t 
     return smooth_keyframe_host(F, Q, tile, tmpidx, pal, hm, vm, smoothed, T, palpix, P, palettes, strength);
 }
 
+int tiler_smooth_keyframe_dev(int F, int Q, int32_t *d_tile, int32_t *d_tmpidx, int32_t *d_pal, uint8_t *d_hm,
+                              uint8_t *d_vm, uint8_t *d_smoothed, const uint8_t *d_palpix, const int32_t *d_palettes,
+                              double strength, void *stream) {
+    if (!ensure_init()) return -1;
+    return smooth_keyframe_dev(F, Q, d_tile, d_tmpidx, d_pal, d_hm, d_vm, d_smoothed, d_palpix, d_palettes, strength,
+                               (hipStream_t)stream);
+}
+
 int tiler_kmodes_compute(const uint8_t *X, int n, int nattr, int k, int start_point, int n_modalities,
                          int32_t *labels, uint8_t *centroids, int *n_iter, uint64_t *cost) {
     if (!ensure_init()) return -1;

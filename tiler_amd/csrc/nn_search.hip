@@ -47,7 +47,14 @@ struct PrepArgs {
     float *nc;      // dataset only: accumulator-row order
     QStat *qstat;   // queries only
     DsStat *ds;     // dataset only
+    int perm;       // dataset only: A-operand row i holds candidate blk*32 + row_perm(i)
 };
+
+// Candidate -> A-operand row permutation (swap bits 0 and 2 of the row).  The 4 mirror candidates of
+// one tile are consecutive indices; unpermuted they all land in the same accumulator lane (rows
+// 4h..4h+3), so a 4-way near-tie fills that lane's list.  Swapping bits 0 and 2 spreads them 2+2 over
+// the two half-waves.  Involution; identity for exact-integer datasets (arrival order = index order).
+__device__ __forceinline__ int row_perm(int i) { return (i & ~5) | ((i & 1) << 2) | ((i >> 2) & 1); }
 
 __device__ __forceinline__ double wave_max_d(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
@@ -58,7 +65,7 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(PrepArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
     const long nblk = (a.n + 31) / 32;
     for (long blk = (long)blockIdx.x * 4 + wave; blk < nblk; blk += (long)gridDim.x * 4) {
-        const long r = blk * 32 + (lane & 31);
+        const long r = blk * 32 + (a.perm ? row_perm(lane & 31) : (lane & 31));
         const bool valid = r < a.n;
         double s2 = 0, sh = 0, se = 0, mabs = 0;
         int notint = 0, bad = 0;
@@ -118,14 +125,22 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(PrepArgs a) {
     }
 }
 
+// out[0] = max |v| (float bits), out[1] |= 1 if any value is not an integer
 __global__ __launch_bounds__(256) void maxabs_kernel(const float *rows, long total, unsigned int *out) {
     float m = 0.0f;
+    int ni = 0;
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        float v = fabsf(rows[i]);
+        const float x = rows[i];
+        float v = fabsf(x);
         m = isfinite(v) ? fmaxf(m, v) : m;
+        ni |= !(x == rintf(x));
     }
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+    const bool any_ni = __any(ni);
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(out, __float_as_uint(m));
+        if (any_ni) atomicOr(out + 1, 1u);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -149,8 +164,8 @@ __device__ __forceinline__ void list_insert(float (&k)[L], int (&id)[L], float x
 }
 
 template <int L>
-__device__ __forceinline__ void scan_keys(const floatx16 &acc, const float (&nc)[16], int base, float (&lk)[L],
-                                          int (&li)[L]) {
+__device__ __forceinline__ void scan_keys(const floatx16 &acc, const float (&nc)[16], int base, int h, int perm,
+                                          float (&lk)[L], int (&li)[L]) {
     float key[16];
     float mn = INFINITY;
 #pragma unroll
@@ -161,7 +176,10 @@ __device__ __forceinline__ void scan_keys(const floatx16 &acc, const float (&nc)
     if (mn < lk[L - 1]) {
 #pragma unroll
         for (int r = 0; r < 16; r++)
-            if (key[r] < lk[L - 1]) list_insert<L>(lk, li, key[r], base + (r & 3) + 8 * (r >> 2));
+            if (key[r] < lk[L - 1]) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                list_insert<L>(lk, li, key[r], base + (perm ? row_perm(row) : row));
+            }
     }
 }
 
@@ -169,7 +187,7 @@ template <int S, int L, int CB>
 __global__ __launch_bounds__(256, 2) void nn_shortlist_kernel(const half8 *__restrict__ cfrag,
                                                               const float *__restrict__ cnc, int nblk,
                                                               const half8 *__restrict__ qfrag, int nq,
-                                                              int blk_per_split, int nsplit,
+                                                              int blk_per_split, int nsplit, int perm,
                                                               float *__restrict__ out_key, int *__restrict__ out_idx) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * S * 1024;
@@ -246,9 +264,9 @@ __global__ __launch_bounds__(256, 2) void nn_shortlist_kernel(const half8 *__res
                 const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
                 const float nc[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w,
                                       n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
-                const int base = blk * 32 + 4 * h;
-                scan_keys<L>(acc0, nc, base, lk0, li0);
-                scan_keys<L>(acc1, nc, base, lk1, li1);
+                const int base = blk * 32;
+                scan_keys<L>(acc0, nc, base, h, perm, lk0, li0);
+                scan_keys<L>(acc1, nc, base, h, perm, lk1, li1);
             }
         }
         if (st + 1 < nstage) swrite((st + 1) & 1);
@@ -516,29 +534,30 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, hipStream_t stream) {
     // scale: power of two so that max|v| * scale <= 16384
     unsigned int *d_m = nullptr;
     DsStat *d_ds = nullptr;
-    TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_m, sizeof(unsigned int)));
+    TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_m, 2 * sizeof(unsigned int)));
     TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_ds, sizeof(DsStat)));
-    TILER_HIP_CHECK_NULL(hipMemsetAsync(d_m, 0, sizeof(unsigned int), stream));
+    TILER_HIP_CHECK_NULL(hipMemsetAsync(d_m, 0, 2 * sizeof(unsigned int), stream));
     TILER_HIP_CHECK_NULL(hipMemsetAsync(d_ds, 0, sizeof(DsStat), stream));
     const long total = (long)n * d;
     hipLaunchKernelGGL(maxabs_kernel, dim3((unsigned)std::min<long>(2048, (total + 255) / 256)), dim3(256), 0, stream,
                        d_rows, total, d_m);
-    unsigned int mbits = 0;
-    TILER_HIP_CHECK_NULL(hipMemcpyAsync(&mbits, d_m, sizeof(mbits), hipMemcpyDeviceToHost, stream));
+    unsigned int mbits[2] = {0, 0};
+    TILER_HIP_CHECK_NULL(hipMemcpyAsync(mbits, d_m, sizeof(mbits), hipMemcpyDeviceToHost, stream));
     TILER_HIP_CHECK_NULL(hipStreamSynchronize(stream));
     float mabs;
-    memcpy(&mabs, &mbits, 4);
+    memcpy(&mabs, &mbits[0], 4);
+    const bool all_int = mbits[1] == 0 && mabs <= 2048.0f;
     float scale = 1.0f;
-    if (mabs > 0.0f) {
+    if (mabs > 0.0f && !all_int) {
         int e;
         frexpf(16384.0f / mabs, &e);
         scale = ldexpf(1.0f, e - 1);
-        if (scale > 1.0f && mabs == rintf(mabs)) scale = 1.0f;  // keep small integers exact
     }
     ix->scale = scale;
+    ix->perm = all_int ? 0 : 1;
     TILER_HIP_CHECK_NULL(hipMalloc(&ix->d_frag, (size_t)ix->nblk * ix->S * 64 * 16));
     TILER_HIP_CHECK_NULL(hipMalloc((void **)&ix->d_nc, (size_t)ix->nblk * 32 * sizeof(float)));
-    PrepArgs pa{d_rows, n, d, ix->S, scale, (half8 *)ix->d_frag, ix->d_nc, nullptr, d_ds};
+    PrepArgs pa{d_rows, n, d, ix->S, scale, (half8 *)ix->d_frag, ix->d_nc, nullptr, d_ds, ix->perm};
     hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)std::min<long>(4096, (ix->nblk + 3) / 4)), dim3(256), 0,
                        stream, pa);
     TILER_HIP_CHECK_NULL(hipGetLastError());
@@ -613,8 +632,8 @@ static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream
     const size_t lds = 2 * (CB * S * 1024 + CB * 128);
     KTimer tm("nn_shortlist", stream);
     hipLaunchKernelGGL((nn_shortlist_kernel<S, L, CB>), grid, dim3(256), lds, stream, (const half8 *)ix->d_frag,
-                       ix->d_nc, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps, nsplit, ix->scratch.key,
-                       ix->scratch.idx);
+                       ix->d_nc, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps, nsplit, ix->perm,
+                       ix->scratch.key, ix->scratch.idx);
 }
 
 template <int L>
@@ -688,7 +707,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         ra.fb_list = nullptr;
         return launch_exact(ra, nq, std::min(nq, 4096), stream);
     }
-    const int L = (k == 1) ? 4 : 8;
+    const int L = 8;  // >= 2x the 4-way mirror near-ties of one tile per lane (row_perm spreads them 2+2)
     const int max_split = 64 / (2 * L);
     const int wgs = ((nq + 31) / 32 + 7) / 8;
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
@@ -701,16 +720,14 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     TILER_HIP_CHECK(hipMemsetAsync(s.fb_count, 0, 16, stream));
     // queries -> fragments (same layout and scale as the dataset)
     const long nqblk = (nq + 31) / 32;
-    PrepArgs pa{d_q, nq, ix->d, ix->S, ix->scale, (half8 *)s.qfrag, nullptr, s.qstat, nullptr};
+    PrepArgs pa{d_q, nq, ix->d, ix->S, ix->scale, (half8 *)s.qfrag, nullptr, s.qstat, nullptr, 0};
     {
         KTimer t_prep("nn_prep", stream);
         hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)std::min<long>(4096, (nqblk + 3) / 4)), dim3(256), 0,
                            stream, pa);
     }
     TILER_HIP_CHECK(hipGetLastError());
-    if ((L == 4 ? dispatch_shortlist<4>(ix, nq, nsplit, bps, stream)
-                : dispatch_shortlist<8>(ix, nq, nsplit, bps, stream)))
-        return -1;
+    if (dispatch_shortlist<L>(ix, nq, nsplit, bps, stream)) return -1;
     ra.qstat = s.qstat;
     ra.key = s.key;
     ra.idx = s.idx;

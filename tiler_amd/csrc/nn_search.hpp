@@ -43,6 +43,7 @@ struct NNIndex {
     float scale = 1.0f;         // power of two applied before the fp16 split (keeps |v| <= 16384)
     double maxN = 0, maxH = 0, maxE = 0, max_abs = 0;
     bool exact_int = false;
+    int perm = 0;               // 1: candidate rows spread over accumulator lanes (row_perm), float data
     float *d_rows = nullptr;    // [n][d] fp32 (exact rescoring)
     void *d_frag = nullptr;     // [nblk][S][64][8] fp16, MFMA A-operand fragment order
     float *d_nc = nullptr;      // [nblk][32] ||c||^2 in accumulator-row order (+inf on padding rows)

@@ -8,28 +8,11 @@
 //   - DCT branch (main.pas:3075-3175): sequential 64-term sums against the host-built gDCTLut.
 // HBM traffic per tile: 256 B in (RGB) or 64 B + 64 B palette, 768 B (fp32) / 1536 B (fp64) out.
 #include "psyv.hpp"
+#include "psyv_dev.hpp"
 
 #pragma clang fp contract(off)
 
 namespace tiler {
-
-__device__ __forceinline__ double shfl_d(double v, int src) { return __shfl(v, src, 64); }
-
-// one Haar level on the dx x dx top-left block (WaveletGS body, main.pas:2818-2836)
-__device__ __forceinline__ double haar_level(double d, int y, int x, int dx, double f) {
-    const int half = dx >> 1;
-    // rows: tempX[y][x] = (D[y][2x'] +/- D[y][2x'+1]) * f, x' = x mod half
-    const int xs = x & (half - 1);
-    double a = shfl_d(d, y * 8 + 2 * xs);
-    double b = shfl_d(d, y * 8 + 2 * xs + 1);
-    double tx = (x < half) ? (a + b) * f : (a - b) * f;
-    // columns: tempY[y][x] = (tempX[2y'][x] +/- tempX[2y'+1][x]) * f, y' = y mod half
-    const int ys = y & (half - 1);
-    double c = shfl_d(tx, (2 * ys) * 8 + x);
-    double e = shfl_d(tx, (2 * ys + 1) * 8 + x);
-    double ty = (y < half) ? (c + e) * f : (c - e) * f;
-    return (x < dx && y < dx) ? ty : d;
-}
 
 __global__ __launch_bounds__(256) void psyv_kernel(PsyvArgs a) {
     const int lane = threadIdx.x & 63;
@@ -49,33 +32,16 @@ __global__ __launch_bounds__(256) void psyv_kernel(PsyvArgs a) {
         } else {
             col = a.rgb[i * 64 + src];
         }
-        const int r = col & 0xff, g = (col >> 8) & 0xff, b = (col >> 16) & 0xff;
-        // RGBToYUV main.pas:2661-2676 (row 0 of the LUT is i/255.0 exactly as the host computes it)
-        const double fr = glut[r], fg = glut[g], fb = glut[b];
-        double cy = (2126.0 * fr + 7152.0 * fg + 722.0 * fb) / 10000.0;
-        double cu = (fb - cy) * a.u_mul;
-        double cv = (fr - cy) * a.v_mul;
-        double cp[3] = {cy, cu, cv};
+        double cp[3];
+        yuv_of(col, glut, a.u_mul, a.v_mul, cp[0], cp[1], cp[2]);
         double out[3];
         if (f & PSYV_WAVELETS) {
 #pragma unroll
-            for (int c = 0; c < 3; c++) {
-                double d = cp[c];
-                d = haar_level(d, y, x, 8, a.haar_f);
-                d = haar_level(d, y, x, 4, a.haar_f);
-                d = haar_level(d, y, x, 2, a.haar_f);
-                out[c] = d;
-            }
+            for (int c = 0; c < 3; c++) out[c] = haar3(cp[c], y, x, a.haar_f);
         } else {
-            // lane = (v, u); z = sum_k cpn[k] * gDCTLut[(v*8+u)*64 + k], sequential (main.pas:3092-3167)
-            const double *__restrict__ lut = a.dct_lut + lane * 64;
+            const PsyvConst k{a.gamma_lut, a.dct_lut, a.qmul, a.ratio, a.haar_f, a.u_mul, a.v_mul};
 #pragma unroll
-            for (int c = 0; c < 3; c++) {
-                double z = 0.0;
-                for (int k = 0; k < 64; k++) z += shfl_d(cp[c], k) * lut[k];
-                if (f & PSYV_QWEIGHT) z *= a.qmul[c * 64 + lane];
-                out[c] = z * a.ratio[lane];
-            }
+            for (int c = 0; c < 3; c++) out[c] = dct_lane(cp[c], lane, c, (f & PSYV_QWEIGHT) != 0, k);
         }
 #pragma unroll
         for (int c = 0; c < 3; c++) {

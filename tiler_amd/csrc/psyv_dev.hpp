@@ -1,0 +1,59 @@
+// psyv_dev.hpp -- wave64 device helpers for the PsyV descriptor (shared by psyv.hip and smooth.hip).
+// Lane = pixel (y*8+x) for the colour conversion, = output coefficient for the transform.
+// fp64 throughout in the reference's source order; the including file sets fp contract(off).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tiler {
+
+struct PsyvConst {
+    const double *gamma_lut;  // [3][256]
+    const double *dct_lut;    // [4096]
+    const double *qmul;       // [192]
+    const double *ratio;      // [64]
+    double haar_f, u_mul, v_mul;
+};
+
+__device__ __forceinline__ double shfl_d(double v, int src) { return __shfl(v, src, 64); }
+
+// RGBToYUV main.pas:2656-2679; glut = gGammaCorLut row (row 0 = i/255.0 exactly as the host computes it)
+__device__ __forceinline__ void yuv_of(int32_t col, const double *__restrict__ glut, double u_mul, double v_mul,
+                                       double &cy, double &cu, double &cv) {
+    const int r = col & 0xff, g = (col >> 8) & 0xff, b = (col >> 16) & 0xff;
+    const double fr = glut[r], fg = glut[g], fb = glut[b];
+    cy = (2126.0 * fr + 7152.0 * fg + 722.0 * fb) / 10000.0;
+    cu = (fb - cy) * u_mul;
+    cv = (fr - cy) * v_mul;
+}
+
+// one WaveletGS level on the dx x dx top-left block (main.pas:2818-2836)
+__device__ __forceinline__ double haar_level(double d, int y, int x, int dx, double f) {
+    const int half = dx >> 1;
+    const int xs = x & (half - 1);
+    const double a = shfl_d(d, y * 8 + 2 * xs);
+    const double b = shfl_d(d, y * 8 + 2 * xs + 1);
+    const double tx = (x < half) ? (a + b) * f : (a - b) * f;
+    const int ys = y & (half - 1);
+    const double c = shfl_d(tx, (2 * ys) * 8 + x);
+    const double e = shfl_d(tx, (2 * ys + 1) * 8 + x);
+    const double ty = (y < half) ? (c + e) * f : (c - e) * f;
+    return (x < dx && y < dx) ? ty : d;
+}
+
+__device__ __forceinline__ double haar3(double d, int y, int x, double f) {
+    d = haar_level(d, y, x, 8, f);
+    d = haar_level(d, y, x, 4, f);
+    return haar_level(d, y, x, 2, f);
+}
+
+// DCT branch main.pas:3075-3175 for output (v,u) = lane of component c: sequential 64-term sum
+__device__ __forceinline__ double dct_lane(double cp, int lane, int c, bool qweight, const PsyvConst &k) {
+    const double *__restrict__ lut = k.dct_lut + lane * 64;
+    double z = 0.0;
+    for (int i = 0; i < 64; i++) z += shfl_d(cp, i) * lut[i];
+    if (qweight) z *= k.qmul[c * 64 + lane];
+    return z * k.ratio[lane];
+}
+
+}  // namespace tiler

@@ -146,7 +146,7 @@ def main():
     elapsed = time.perf_counter() - t0
     lib.tiler_timing_enable(0)
     kernels = {}
-    for name in ("psyv", "nn_prep", "nn_shortlist", "nn_rescore", "nn_exact"):
+    for name in ("psyv", "nn_prep", "nn_shortlist", "nn_rescore", "nn_collect", "nn_rescore2", "nn_exact"):
         n = ctypes.c_int(0)
         ms = lib.tiler_timing_get(name.encode(), ctypes.byref(n))
         kernels[name] = {"ms_total": round(ms, 4), "launches": n.value,
@@ -165,7 +165,8 @@ def main():
     achieved = flops_launch / (sl["ms_avg"] * 1e-3) / 1e12 if sl["ms_avg"] else None
     roofline = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None, "peak": PEAK_F16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
-                "traffic": None, "kernel": "nn_shortlist_kernel<12,4,2>",
+                "traffic": None,
+                "kernel": f"nn_shortlist_kernel<S=12,L=8,CB=2,NW={os.environ.get('TILER_SHORTLIST_WAVES', '8')}>",
                 "note": "algorithmic 2*M*D per tile vs dense fp16 MFMA peak; 1 fp16 product per pair"}
 
     # ---- CPU baseline (rank 0, N=1): the oracle restatement, bounded sample, same workload ----

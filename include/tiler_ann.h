@@ -56,7 +56,8 @@ int ann_kdtree_search_batch_dev(ann_kdtree *akd, const float *d_q, int nq, int k
 /* Search statistics of the last call on this handle (shortlist sizes, exact fallbacks). */
 typedef struct {
     int64_t queries;
-    int64_t fallback_queries; /* queries rescanned exactly because the MFMA shortlist overflowed */
+    int64_t fallback_queries;   /* tier 2: shortlist overflowed -> MFMA collect pass + exact rescoring */
+    int64_t exhaustive_queries; /* tier 3: exhaustive reference-order scan (k > 8, bad data, collect overflow) */
     int32_t exact_integer;    /* 1 when the dataset is small integers: MFMA keys are exact */
     int32_t splits;           /* candidate splits used by the last launch */
 } tiler_search_stats;

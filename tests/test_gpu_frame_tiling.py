@@ -87,7 +87,12 @@ def test_nn_overflow_fallback(gpu, oracle):
     data = np.concatenate([rng.normal(0, 1, (700, 192)).astype(np.float32), data])
     qs = data[[0, 5, 700, 950]] + np.float32(1e-3)
     st = _check_nn(gpu, oracle, data, qs)
-    assert st["fallback_queries"] >= 1
+    assert st["fallback_queries"] >= 1  # tier 2 (MFMA collect + exact rescoring)
+    # 1500 identical candidates overflow the tier-2 buffer too -> tier 3 exhaustive scan
+    many = np.repeat(data[700:701], 1500, 0)
+    data3 = np.concatenate([data[:700], many])
+    st3 = _check_nn(gpu, oracle, data3, data3[[3, 800]] + np.float32(1e-3))
+    assert st3["exhaustive_queries"] >= 1
 
 
 def test_nn_generic_dims(gpu, oracle):

@@ -27,7 +27,7 @@ class TilerError(RuntimeError):
 
 class SearchStats(ctypes.Structure):
     _fields_ = [("queries", ctypes.c_int64), ("fallback_queries", ctypes.c_int64),
-                ("exact_integer", ctypes.c_int32), ("splits", ctypes.c_int32)]
+                ("exhaustive_queries", ctypes.c_int64), ("exact_integer", ctypes.c_int32), ("splits", ctypes.c_int32)]
 
 
 _SIGS = {

@@ -94,5 +94,5 @@ class KDTree:
     def stats(self) -> dict:
         s = SearchStats()
         check(self._lib.ann_kdtree_get_stats(self.handle, ctypes.byref(s)), "ann_kdtree_get_stats")
-        return {"queries": s.queries, "fallback_queries": s.fallback_queries, "exact_integer": s.exact_integer,
-                "splits": s.splits}
+        return {"queries": s.queries, "fallback_queries": s.fallback_queries,
+                "exhaustive_queries": s.exhaustive_queries, "exact_integer": s.exact_integer, "splits": s.splits}

@@ -356,7 +356,8 @@ int ann_kdtree_get_stats(ann_kdtree *t, tiler_search_stats *out) {
     }
     std::lock_guard<std::mutex> lk(t->ix->mu);
     out->queries = t->ix->last_queries;
-    out->fallback_queries = t->ix->last_splits > 0 ? *t->ix->h_fb_count : t->ix->last_fallback;
+    out->fallback_queries = t->ix->last_splits > 0 ? t->ix->h_fb_count[0] : 0;
+    out->exhaustive_queries = t->ix->last_splits > 0 ? t->ix->h_fb_count[1] : t->ix->last_fallback;
     out->exact_integer = t->ix->exact_int ? 1 : 0;
     out->splits = t->ix->last_splits;
     return 0;

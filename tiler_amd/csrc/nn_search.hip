@@ -18,6 +18,7 @@
 // keys exact; the same kernels then return exact (key, index) order with no margin.
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -183,8 +184,8 @@ __device__ __forceinline__ void scan_keys(const floatx16 &acc, const float (&nc)
     }
 }
 
-template <int S, int L, int CB>
-__global__ __launch_bounds__(256, 2) void nn_shortlist_kernel(const half8 *__restrict__ cfrag,
+template <int S, int L, int CB, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *__restrict__ cfrag,
                                                               const float *__restrict__ cnc, int nblk,
                                                               const half8 *__restrict__ qfrag, int nq,
                                                               int blk_per_split, int nsplit, int perm,
@@ -192,11 +193,12 @@ __global__ __launch_bounds__(256, 2) void nn_shortlist_kernel(const half8 *__res
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * S * 1024;
     constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
-    constexpr int PER_T = CB * S * 64 / 256;
-    static_assert((CB * S * 64) % 256 == 0, "stage must split evenly over 256 threads");
+    constexpr int NT = NW * 64;
+    constexpr int PER_T = CB * S * 64 / NT;
+    static_assert((CB * S * 64) % NT == 0, "stage must split evenly over the workgroup");
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int nqblk = (nq + 31) / 32;
-    const int qb0 = (blockIdx.x * 4 + w) * 2;
+    const int qb0 = (blockIdx.x * NW + w) * 2;
     const int split = blockIdx.y;
     const int b_begin = split * blk_per_split;
     const int b_end = min(nblk, b_begin + blk_per_split);
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(256, 2) void nn_shortlist_kernel(const half8 *__res
         const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64;
 #pragma unroll
         for (int j = 0; j < PER_T; j++) {
-            const int c = tid + j * 256;
+            const int c = tid + j * NT;
             stg[j] = (c < avail) ? src[c] : make_uint4(0, 0, 0, 0);
         }
         if (tid < CB * 8) {
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void nn_shortlist_kernel(const half8 *__res
     auto swrite = [&](int buf) {
         uint4 *dst = reinterpret_cast<uint4 *>(smem + buf * BUF_BYTES);
 #pragma unroll
-        for (int j = 0; j < PER_T; j++) dst[tid + j * 256] = stg[j];
+        for (int j = 0; j < PER_T; j++) dst[tid + j * NT] = stg[j];
         if (tid < CB * 8) reinterpret_cast<uint4 *>(smem + buf * BUF_BYTES + FRAG_BYTES)[tid] = stg_nc;
     };
 
@@ -288,6 +290,100 @@ __global__ __launch_bounds__(256, 2) void nn_shortlist_kernel(const half8 *__res
 }
 
 // ------------------------------------------------------------------------------------------
+// 1b. tier-2 collect: for the queries whose tier-1 lists overflowed, recompute the MFMA keys and append
+// EVERY candidate with key <= T(q) to a per-query buffer (atomic cursor).  Compact query j's B fragment
+// is gathered straight from the tier-1 fragment buffer.  Grid-stride over groups of 256 queries.
+// ------------------------------------------------------------------------------------------
+template <int S, int CB>
+__global__ __launch_bounds__(256, 2) void nn_collect_kernel(const half8 *__restrict__ cfrag,
+                                                            const float *__restrict__ cnc, int nblk,
+                                                            const half8 *__restrict__ qfrag, const int *fb_list,
+                                                            const int *fb_count, int fb_max, const float *thr,
+                                                            int blk_per_split, int perm, int *ccnt, int *cbuf,
+                                                            int cap) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int FRAG_BYTES = CB * S * 1024;
+    constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
+    constexpr int PER_T = CB * S * 64 / 256;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int count = min(*fb_count, fb_max);
+    const int b_begin = blockIdx.y * blk_per_split;
+    const int b_end = min(nblk, b_begin + blk_per_split);
+    const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint4 inf4 = make_uint4(0x7f800000u, 0x7f800000u, 0x7f800000u, 0x7f800000u);
+    for (int g = blockIdx.x; g * 256 < count; g += gridDim.x) {
+        half8 bq0[S], bq1[S];
+        int j0 = (g * 4 + w) * 64 + (lane & 31), j1 = j0 + 32;
+        const int q0 = j0 < count ? fb_list[j0] : -1, q1 = j1 < count ? fb_list[j1] : -1;
+        const float t0 = q0 >= 0 ? thr[q0] : -INFINITY, t1 = q1 >= 0 ? thr[q1] : -INFINITY;
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            bq0[s] = q0 >= 0 ? qfrag[((long)(q0 >> 5) * S + s) * 64 + (q0 & 31) + 32 * h] : zero8;
+            bq1[s] = q1 >= 0 ? qfrag[((long)(q1 >> 5) * S + s) * 64 + (q1 & 31) + 32 * h] : zero8;
+        }
+        const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
+        uint4 stg[PER_T];
+        uint4 stg_nc = make_uint4(0, 0, 0, 0);
+        auto gload = [&](int st) {
+            const int blk0 = b_begin + st * CB;
+            const int avail = min(CB, b_end - blk0) * S * 64;
+            const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64;
+#pragma unroll
+            for (int jj = 0; jj < PER_T; jj++) {
+                const int c = tid + jj * 256;
+                stg[jj] = (c < avail) ? src[c] : make_uint4(0, 0, 0, 0);
+            }
+            if (tid < CB * 8)
+                stg_nc = (blk0 + (tid >> 3) < b_end) ? reinterpret_cast<const uint4 *>(cnc)[(long)blk0 * 8 + tid] : inf4;
+        };
+        auto swrite = [&](int buf) {
+            uint4 *dst = reinterpret_cast<uint4 *>(smem + buf * BUF_BYTES);
+#pragma unroll
+            for (int jj = 0; jj < PER_T; jj++) dst[tid + jj * 256] = stg[jj];
+            if (tid < CB * 8) reinterpret_cast<uint4 *>(smem + buf * BUF_BYTES + FRAG_BYTES)[tid] = stg_nc;
+        };
+        __syncthreads();
+        if (nstage > 0) {
+            gload(0);
+            swrite(0);
+        }
+        __syncthreads();
+        for (int st = 0; st < nstage; st++) {
+            if (st + 1 < nstage) gload(st + 1);
+            const char *B = smem + (st & 1) * BUF_BYTES;
+            for (int cb = 0; cb < CB; cb++) {
+                const int blk = b_begin + st * CB + cb;
+                if (blk >= b_end) break;
+                floatx16 acc0 = {0}, acc1 = {0};
+#pragma unroll
+                for (int s = 0; s < S; s++) {
+                    const half8 av = reinterpret_cast<const half8 *>(B)[(cb * S + s) * 64 + lane];
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq0[s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq1[s], acc1, 0, 0, 0);
+                }
+                const float *np = reinterpret_cast<const float *>(B + FRAG_BYTES) + cb * 32 + h * 16;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const float nc = np[r];
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int idx = blk * 32 + (perm ? row_perm(row) : row);
+                    if (fmaf(-2.0f, acc0[r], nc) <= t0) {
+                        const int p = atomicAdd(&ccnt[j0], 1);
+                        if (p < cap) cbuf[(long)j0 * cap + p] = idx;
+                    }
+                    if (fmaf(-2.0f, acc1[r], nc) <= t1) {
+                        const int p = atomicAdd(&ccnt[j1], 1);
+                        if (p < cap) cbuf[(long)j1 * cap + p] = idx;
+                    }
+                }
+            }
+            if (st + 1 < nstage) swrite((st + 1) & 1);
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // 2. rescore: one wave per query.
 // ------------------------------------------------------------------------------------------
 struct RescoreArgs {
@@ -301,8 +397,14 @@ struct RescoreArgs {
     int ds_int;
     int *out_idx;
     float *out_err;
-    int *fb_list;
+    int *fb_list;        // tier 2: overflowed queries (MFMA collect pass), count in fb_count
     int *fb_count;
+    float *thr;          // [nq] tier-2 threshold T (rounded up to fp32)
+    int *ex_list;        // tier 3: exhaustive scan (bad queries, collect-buffer overflow)
+    int *ex_count;
+    int *ccnt;           // [fb_max] collected candidates per tier-2 query
+    int *cbuf;           // [fb_max][cap]
+    int cap, fb_max;
     const int32_t *tr_tile, *tr_pal;
     const uint8_t *tr_attr;
     int32_t *m_tile, *m_pal;
@@ -363,7 +465,11 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
         idx = a.idx[q * E + lane];
     }
     const QStat st = a.qstat[q];
-    bool fallback = (st.flags & QF_BAD) != 0;
+    if (st.flags & QF_BAD) {  // fp16 overflow / non-finite: no valid MFMA keys -> exhaustive scan
+        if (lane == 0) a.ex_list[atomicAdd(a.ex_count, 1)] = (int)q;
+        return;
+    }
+    bool fallback = false;
     // k-th smallest key (lexicographic by (key, lane) so duplicates count separately)
     float kk = INFINITY;
     {
@@ -411,8 +517,14 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
     }
     if (fallback) {
         if (lane == 0) {
+            float tf = (float)T;
+            if ((double)tf < T) tf = nextafterf(tf, INFINITY);  // keep T an upper bound in fp32
+            a.thr[q] = tf;
             const int p = atomicAdd(a.fb_count, 1);
-            a.fb_list[p] = (int)q;
+            if (p < a.fb_max)
+                a.fb_list[p] = (int)q;
+            else
+                a.ex_list[atomicAdd(a.ex_count, 1)] = (int)q;
         }
         return;
     }
@@ -433,6 +545,68 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// 2b. tier-2 rescore: every collected candidate (key <= T) rescored exactly; top-k by (dist, index).
+// One wave per compact query; a buffer that overflowed its capacity sends the query to tier 3.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool lex_less(float a, int ia, float b, int ib) {
+    return a < b || (a == b && (unsigned)ia < (unsigned)ib);
+}
+
+__global__ __launch_bounds__(256) void nn_rescore2_kernel(RescoreArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int count = min(*a.fb_count, a.fb_max);
+    for (long j = (long)blockIdx.x * 4 + (threadIdx.x >> 6); j < count; j += (long)gridDim.x * 4) {
+        const long q = a.fb_list[j];
+        const int n = a.ccnt[j];
+        if (n > a.cap) {
+            if (lane == 0) a.ex_list[atomicAdd(a.ex_count, 1)] = (int)q;
+            continue;
+        }
+        float bd[8];
+        int bi[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            bd[i] = INFINITY;
+            bi[i] = 0x7fffffff;
+        }
+        for (int e = lane; e < n; e += 64) {
+            const int idx = a.cbuf[j * a.cap + e];
+            const float dist = exact_dist(a.q + q * a.d, a.rows + (long)idx * a.d, a.d);
+            if (!lex_less(dist, idx, bd[7], bi[7])) continue;
+            int p = 7;  // lexicographic insertion (entries arrive in no particular order)
+            while (p > 0 && lex_less(dist, idx, bd[p - 1], bi[p - 1])) {
+                bd[p] = bd[p - 1];
+                bi[p] = bi[p - 1];
+                p--;
+            }
+            bd[p] = dist;
+            bi[p] = idx;
+        }
+        int ptr = 0;
+        for (int r = 0; r < a.k; r++) {
+            float hv = INFINITY;
+            int hi = 0x7fffffff;
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (i == ptr) {
+                    hv = bd[i];
+                    hi = bi[i];
+                }
+            float mv = hv;
+            int mi = hi;
+            wave_argmin(mv, mi);
+            if (hi == mi && mi != 0x7fffffff) ptr++;
+            if (lane == 0) {
+                const bool ok = mi != 0x7fffffff;
+                a.out_idx[q * a.k + r] = ok ? mi : -1;
+                a.out_err[q * a.k + r] = ok ? mv : FLT_MAX;
+                if (r == 0) write_map(a, q, ok ? mi : -1);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // 3. exhaustive exact scan (queued queries, k > 8): one workgroup per query, grid-stride list.
 // ------------------------------------------------------------------------------------------
 template <int K>
@@ -441,9 +615,9 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(RescoreArgs a, int list_n
     __shared__ float sd[256 * K];
     __shared__ int si[256 * K];
     const int tid = threadIdx.x;
-    const int count = a.fb_list ? *a.fb_count : list_n;
+    const int count = a.ex_list ? *a.ex_count : list_n;
     for (int qi = blockIdx.x; qi < count; qi += gridDim.x) {
-        const long q = a.fb_list ? a.fb_list[qi] : qi;
+        const long q = a.ex_list ? a.ex_list[qi] : qi;
         __syncthreads();
         for (int i = tid; i < a.d; i += 256) sq[i] = a.q[q * a.d + i];
         __syncthreads();
@@ -597,9 +771,16 @@ void nn_index_destroy(NNIndex *ix) {
     hipFree(s.fb_list);
     hipFree(s.fb_count);
     hipFree(s.qrows);
+    hipFree(s.thr);
+    hipFree(s.ex_list);
+    hipFree(s.ccnt);
+    hipFree(s.cbuf);
     hipHostFree(ix->h_fb_count);
     delete ix;
 }
+
+static constexpr int TIER2_MAX = 65536;  // queries per call in the tier-2 collect pass
+static constexpr int TIER2_CAP = 1024;   // collected candidates per tier-2 query
 
 static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
     SearchScratch &s = ix->scratch;
@@ -608,12 +789,20 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         hipFree(s.qstat);
         hipFree(s.fb_list);
         hipFree(s.fb_count);
+        hipFree(s.thr);
+        hipFree(s.ex_list);
         const long nqblk = (nq + 31) / 32 + 2;
         TILER_HIP_CHECK(hipMalloc(&s.qfrag, (size_t)nqblk * 16 * 64 * 16));
         TILER_HIP_CHECK(hipMalloc((void **)&s.qstat, (size_t)nq * sizeof(QStat)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.fb_list, (size_t)nq * sizeof(int)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.fb_count, 16));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.thr, (size_t)nq * sizeof(float)));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.ex_list, (size_t)nq * sizeof(int)));
         s.cap_q = nq;
+    }
+    if (!s.ccnt) {
+        TILER_HIP_CHECK(hipMalloc((void **)&s.ccnt, (size_t)TIER2_MAX * sizeof(int)));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.cbuf, (size_t)TIER2_MAX * TIER2_CAP * sizeof(int)));
     }
     if ((size_t)nkeys > s.cap_keys) {
         hipFree(s.key);
@@ -625,24 +814,64 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
     return 0;
 }
 
-template <int S, int L, int CB>
+template <int S, int L, int CB, int NW>
 static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     const int nqblk = (nq + 31) / 32;
-    const dim3 grid((nqblk + 7) / 8, nsplit);
+    const dim3 grid((nqblk + 2 * NW - 1) / (2 * NW), nsplit);
     const size_t lds = 2 * (CB * S * 1024 + CB * 128);
     KTimer tm("nn_shortlist", stream);
-    hipLaunchKernelGGL((nn_shortlist_kernel<S, L, CB>), grid, dim3(256), lds, stream, (const half8 *)ix->d_frag,
+    hipLaunchKernelGGL((nn_shortlist_kernel<S, L, CB, NW>), grid, dim3(NW * 64), lds, stream, (const half8 *)ix->d_frag,
                        ix->d_nc, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps, nsplit, ix->perm,
                        ix->scratch.key, ix->scratch.idx);
+}
+
+// workgroup size of the D=192 shortlist: 8 waves (512 queries share each staged candidate tile)
+// unless TILER_SHORTLIST_WAVES=4 (A/B switch for measurements)
+static int shortlist_waves() {
+    static int w = [] {
+        const char *e = getenv("TILER_SHORTLIST_WAVES");
+        return (e && atoi(e) == 4) ? 4 : 8;
+    }();
+    return w;
 }
 
 template <int L>
 static int dispatch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     switch (ix->S) {
-        case 4: launch_shortlist<4, L, 6>(ix, nq, nsplit, bps, stream); break;
-        case 8: launch_shortlist<8, L, 3>(ix, nq, nsplit, bps, stream); break;
-        case 12: launch_shortlist<12, L, 2>(ix, nq, nsplit, bps, stream); break;
-        case 16: launch_shortlist<16, L, 2>(ix, nq, nsplit, bps, stream); break;
+        case 4: launch_shortlist<4, L, 6, 4>(ix, nq, nsplit, bps, stream); break;
+        case 8: launch_shortlist<8, L, 3, 4>(ix, nq, nsplit, bps, stream); break;
+        case 12:
+            if (shortlist_waves() == 8)
+                launch_shortlist<12, L, 2, 8>(ix, nq, nsplit, bps, stream);
+            else
+                launch_shortlist<12, L, 2, 4>(ix, nq, nsplit, bps, stream);
+            break;
+        case 16: launch_shortlist<16, L, 2, 4>(ix, nq, nsplit, bps, stream); break;
+        default: set_error("nn: unsupported fragment depth"); return -1;
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+template <int S, int CB>
+static void launch_collect(NNIndex *ix, int nq, hipStream_t stream) {
+    const int nsplit = std::min(ix->nblk, 64);
+    const int bps = (ix->nblk + nsplit - 1) / nsplit;
+    const int groups = std::min(64, (std::min(nq, TIER2_MAX) + 255) / 256);
+    const size_t lds = 2 * (CB * S * 1024 + CB * 128);
+    SearchScratch &s = ix->scratch;
+    KTimer tm("nn_collect", stream);
+    hipLaunchKernelGGL((nn_collect_kernel<S, CB>), dim3(groups, (ix->nblk + bps - 1) / bps), dim3(256), lds, stream,
+                       (const half8 *)ix->d_frag, ix->d_nc, ix->nblk, (const half8 *)s.qfrag, s.fb_list, s.fb_count,
+                       TIER2_MAX, s.thr, bps, ix->perm, s.ccnt, s.cbuf, TIER2_CAP);
+}
+
+static int dispatch_collect(NNIndex *ix, int nq, hipStream_t stream) {
+    switch (ix->S) {
+        case 4: launch_collect<4, 6>(ix, nq, stream); break;
+        case 8: launch_collect<8, 3>(ix, nq, stream); break;
+        case 12: launch_collect<12, 2>(ix, nq, stream); break;
+        case 16: launch_collect<16, 2>(ix, nq, stream); break;
         default: set_error("nn: unsupported fragment depth"); return -1;
     }
     TILER_HIP_CHECK(hipGetLastError());
@@ -704,12 +933,12 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     if (!mfma) {
         ix->last_splits = 0;
         ix->last_fallback = nq;
-        ra.fb_list = nullptr;
+        ra.ex_list = nullptr;
         return launch_exact(ra, nq, std::min(nq, 4096), stream);
     }
     const int L = 8;  // >= 2x the 4-way mirror near-ties of one tile per lane (row_perm spreads them 2+2)
     const int max_split = 64 / (2 * L);
-    const int wgs = ((nq + 31) / 32 + 7) / 8;
+    const int wgs = ((nq + 31) / 32 + 15) / 16;
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
     nsplit = std::min(nsplit, ix->nblk);
     const int bps = (ix->nblk + nsplit - 1) / nsplit;
@@ -735,14 +964,29 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     ra.nsplit = nsplit;
     ra.fb_list = s.fb_list;
     ra.fb_count = s.fb_count;
+    ra.ex_list = s.ex_list;
+    ra.ex_count = s.fb_count + 1;
+    ra.thr = s.thr;
+    ra.ccnt = s.ccnt;
+    ra.cbuf = s.cbuf;
+    ra.cap = TIER2_CAP;
+    ra.fb_max = TIER2_MAX;
+    TILER_HIP_CHECK(hipMemsetAsync(s.ccnt, 0, (size_t)std::min(nq, TIER2_MAX) * sizeof(int), stream));
     {
         KTimer t_rs("nn_rescore", stream);
         hipLaunchKernelGGL(nn_rescore_kernel, dim3((nq + 3) / 4), dim3(256), 0, stream, ra);
     }
     TILER_HIP_CHECK(hipGetLastError());
-    // queued queries: a fixed grid that reads the device-side count (no host round trip)
+    // tier 2 and tier 3 read their device-side counts: fixed grids, no host round trip
+    if (dispatch_collect(ix, nq, stream)) return -1;
+    {
+        KTimer t_r2("nn_rescore2", stream);
+        hipLaunchKernelGGL(nn_rescore2_kernel, dim3((unsigned)std::min(1024, (std::min(nq, TIER2_MAX) + 3) / 4)),
+                           dim3(256), 0, stream, ra);
+    }
+    TILER_HIP_CHECK(hipGetLastError());
     if (launch_exact(ra, 0, std::min(nq, 512), stream)) return -1;
-    TILER_HIP_CHECK(hipMemcpyAsync(ix->h_fb_count, s.fb_count, sizeof(int), hipMemcpyDeviceToHost, stream));
+    TILER_HIP_CHECK(hipMemcpyAsync(ix->h_fb_count, s.fb_count, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
     return 0;
 }
 

@@ -35,6 +35,10 @@ struct SearchScratch {
     int *fb_list = nullptr;
     int *fb_count = nullptr;  // [2]: count, pad
     float *qrows = nullptr;   // fp32 query rows (frame-tiling path: descriptors)
+    float *thr = nullptr;     // tier-2 thresholds [nq]
+    int *ex_list = nullptr;   // tier-3 list [nq]
+    int *ccnt = nullptr;      // tier-2 collect counts
+    int *cbuf = nullptr;      // tier-2 collect buffers
     size_t cap_q = 0, cap_keys = 0, cap_rows = 0;
 };
 

@@ -116,6 +116,11 @@ int tiler_smooth_keyframe_dev(int F, int Q, int32_t *d_tile, int32_t *d_tmpidx, 
  * (0-based), centroids[k][nattr].  Returns k or -1.  n_iter / cost optional. */
 int tiler_kmodes_compute(const uint8_t *X, int n, int nattr, int k, int start_point, int n_modalities,
                          int32_t *labels, uint8_t *centroids, int *n_iter, uint64_t *cost);
+/* DoKModes medoids (main.pas:4231-4253): for every cluster j, the member row minimising the K-Modes
+ * dissimilarity to centroid j (ties -> last member, as GetMinMatchingDissim); medoid[j] = -1 and
+ * counts[j] = 0 for empty clusters.  X[n][80], labels[n] in 0..k-1, centroids[k][80]. */
+int tiler_kmodes_medoids(const uint8_t *X, int n, const int32_t *labels, const uint8_t *centroids, int k,
+                         int32_t *medoid, int32_t *counts);
 
 #ifdef __cplusplus
 }

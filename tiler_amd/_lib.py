@@ -61,6 +61,7 @@ _SIGS = {
                                       c_void_p, c_int, c_void_p, c_double]),
     "tiler_smooth_keyframe_dev": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_double, c_void_p]),
+    "tiler_kmodes_medoids": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "tiler_kmodes_compute": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
 }

@@ -528,6 +528,12 @@ int tiler_smooth_keyframe_dev(int F, int Q, int32_t *d_tile, int32_t *d_tmpidx, 
                                (hipStream_t)stream);
 }
 
+int tiler_kmodes_medoids(const uint8_t *X, int n, const int32_t *labels, const uint8_t *centroids, int k,
+                         int32_t *medoid, int32_t *counts) {
+    if (!ensure_init()) return -1;
+    return kmodes_medoids_host(X, n, labels, centroids, k, medoid, counts);
+}
+
 int tiler_kmodes_compute(const uint8_t *X, int n, int nattr, int k, int start_point, int n_modalities,
                          int32_t *labels, uint8_t *centroids, int *n_iter, uint64_t *cost) {
     if (!ensure_init()) return -1;

@@ -464,6 +464,61 @@ int kmodes_compute_dev(const uint8_t *d_X, int n, int k, int start_point, int n_
     return rc;
 }
 
+// ---- DoKModes medoid choice (main.pas:4231-4253): per cluster j with members, the member minimising
+// dissim(member, centroid_j) (GetMinMatchingDissim(ToMerge, LocCentroids[j]) -> ties: last member) ----
+__global__ __launch_bounds__(256) void km_medoid_kernel(const uint8_t *X, int n, const int32_t *labels,
+                                                        const uint8_t *cent, unsigned long long *best,
+                                                        int32_t *counts) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const int j = labels[i];
+        uint32_t row[20], item[20];
+        load_row(X + i * KM_A, row);
+        load_row(cent + (long)j * KM_A, item);
+        const unsigned long long d = km_dissim(row, item);
+        atomicMin(&best[j], (d << 32) | (0xFFFFFFFFu - (unsigned)i));
+        atomicAdd(&counts[j], 1);
+    }
+}
+
+int kmodes_medoids_host(const uint8_t *X, int n, const int32_t *labels, const uint8_t *centroids, int k,
+                        int32_t *medoid, int32_t *counts) {
+    if (n < 0 || k <= 0 || (n > 0 && (!X || !labels)) || !centroids || !medoid || !counts) {
+        set_error("kmodes_medoids: invalid arguments");
+        return -1;
+    }
+    for (int i = 0; i < n; i++)
+        if (labels[i] < 0 || labels[i] >= k) {
+            set_error("kmodes_medoids: label out of range");
+            return -1;
+        }
+    char *buf = nullptr;
+    const size_t oX = 0, oL = ((size_t)n * KM_A + 255) & ~(size_t)255, oC = oL + (((size_t)n * 4 + 255) & ~(size_t)255),
+                 oB = oC + (((size_t)k * KM_A + 255) & ~(size_t)255), oN = oB + (size_t)k * 8, total = oN + (size_t)k * 4;
+    TILER_HIP_CHECK(hipMalloc((void **)&buf, total));
+    int rc = -1;
+    do {
+        if (n > 0 && hipMemcpy(buf + oX, X, (size_t)n * KM_A, hipMemcpyHostToDevice) != hipSuccess) break;
+        if (n > 0 && hipMemcpy(buf + oL, labels, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess) break;
+        if (hipMemcpy(buf + oC, centroids, (size_t)k * KM_A, hipMemcpyHostToDevice) != hipSuccess) break;
+        if (hipMemset(buf + oB, 0xff, (size_t)k * 8) != hipSuccess) break;
+        if (hipMemset(buf + oN, 0, (size_t)k * 4) != hipSuccess) break;
+        if (n > 0)
+            hipLaunchKernelGGL(km_medoid_kernel, dim3(std::min(4096, (n + 255) / 256)), dim3(256), 0, nullptr,
+                               (const uint8_t *)(buf + oX), n, (const int32_t *)(buf + oL),
+                               (const uint8_t *)(buf + oC), (unsigned long long *)(buf + oB), (int32_t *)(buf + oN));
+        if (hipGetLastError() != hipSuccess) break;
+        std::vector<unsigned long long> b(k);
+        if (hipMemcpy(b.data(), buf + oB, (size_t)k * 8, hipMemcpyDeviceToHost) != hipSuccess) break;
+        if (hipMemcpy(counts, buf + oN, (size_t)k * 4, hipMemcpyDeviceToHost) != hipSuccess) break;
+        for (int j = 0; j < k; j++)
+            medoid[j] = counts[j] > 0 ? (int32_t)(0xFFFFFFFFu - (unsigned)(b[j] & 0xFFFFFFFFull)) : -1;
+        rc = 0;
+    } while (0);
+    if (rc) set_error("kmodes_medoids: HIP failure");
+    (void)hipFree(buf);
+    return rc;
+}
+
 int kmodes_compute_host(const uint8_t *X, int n, int nattr, int k, int start_point, int n_modalities,
                         int32_t *labels, uint8_t *centroids, int *n_iter, uint64_t *cost) {
     if (nattr != KM_A) {

@@ -148,6 +148,13 @@ __global__ __launch_bounds__(256) void maxabs_kernel(const float *rows, long tot
 // 1. MFMA shortlist.  Workgroup = 4 waves; wave = 2 query blocks of 32 (64 queries); the
 // candidate blocks of this split stream through a double-buffered LDS ring (CB blocks/stage).
 // ------------------------------------------------------------------------------------------
+// one 16-byte LDS-DMA piece per lane: LDS destination = wave-uniform base + lane * 16
+__device__ __forceinline__ void glds16(const uint4 *gsrc, char *lds_wave_base) {
+    typedef __attribute__((address_space(1))) void gvoid;
+    typedef __attribute__((address_space(3))) void lvoid;
+    __builtin_amdgcn_global_load_lds((gvoid *)(gsrc), (lvoid *)(lds_wave_base), 16, 0, 0);
+}
+
 template <int L>
 __device__ __forceinline__ void list_insert(float (&k)[L], int (&id)[L], float x, int ix) {
 #pragma unroll
@@ -164,22 +171,21 @@ __device__ __forceinline__ void list_insert(float (&k)[L], int (&id)[L], float x
     }
 }
 
+// acc was seeded with -||c||^2/2, so acc = q.c - ||c||^2/2 and key = ||c||^2 - 2 q.c = -2 acc (exact
+// scaling): the epilogue is a max tree plus one compare per 16 values, no per-value FMA.
 template <int L>
-__device__ __forceinline__ void scan_keys(const floatx16 &acc, const float (&nc)[16], int base, int h, int perm,
-                                          float (&lk)[L], int (&li)[L]) {
-    float key[16];
-    float mn = INFINITY;
+__device__ __forceinline__ void scan_keys(const floatx16 &acc, int base, int h, int perm, float (&lk)[L],
+                                          int (&li)[L]) {
+    float mx = acc[0];
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-        key[r] = fmaf(-2.0f, acc[r], nc[r]);
-        mn = fminf(mn, key[r]);
-    }
-    if (mn < lk[L - 1]) {
+    for (int r = 1; r < 16; r++) mx = fmaxf(mx, acc[r]);
+    const float thr = -0.5f * lk[L - 1];  // acc > thr  <=>  key < lk[L-1]
+    if (mx > thr) {
 #pragma unroll
         for (int r = 0; r < 16; r++)
-            if (key[r] < lk[L - 1]) {
+            if (acc[r] > -0.5f * lk[L - 1]) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                list_insert<L>(lk, li, key[r], base + (perm ? row_perm(row) : row));
+                list_insert<L>(lk, li, -2.0f * acc[r], base + (perm ? row_perm(row) : row));
             }
     }
 }
@@ -204,11 +210,12 @@ __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *_
     const int b_end = min(nblk, b_begin + blk_per_split);
 
     half8 bq0[S], bq1[S];
-    const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    // query blocks past the end compute on a clamped duplicate and are never written out
+    const long qa = min(qb0, nqblk - 1), qc = min(qb0 + 1, nqblk - 1);
 #pragma unroll
     for (int s = 0; s < S; s++) {
-        bq0[s] = (qb0 < nqblk) ? qfrag[((long)qb0 * S + s) * 64 + lane] : zero8;
-        bq1[s] = (qb0 + 1 < nqblk) ? qfrag[((long)(qb0 + 1) * S + s) * 64 + lane] : zero8;
+        bq0[s] = qfrag[(qa * S + s) * 64 + lane];
+        bq1[s] = qfrag[(qc * S + s) * 64 + lane];
     }
     float lk0[L], lk1[L];
     int li0[L], li1[L];
@@ -219,60 +226,56 @@ __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *_
     }
 
     const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
-    uint4 stg[PER_T];
-    uint4 stg_nc = make_uint4(0, 0, 0, 0);
-    const uint4 inf4 = make_uint4(0x7f800000u, 0x7f800000u, 0x7f800000u, 0x7f800000u);
-    auto gload = [&](int st) {
+    // LDS-DMA staging (global_load_lds_dwordx4): the fragment image is lane-linear, so each wave
+    // copies 1 KiB pieces straight into LDS; the barrier at the end of a stage drains them.
+    // Sources are clamped: blocks past b_end land in LDS but are never computed on.
+    auto issue = [&](int st, int buf) {
         const int blk0 = b_begin + st * CB;
-        const int avail = min(CB, b_end - blk0) * S * 64;
+        const int nb = min(CB, b_end - blk0);
+        const int last = nb * S * 64 - 1;
         const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64;
+        char *dst = smem + buf * BUF_BYTES;
 #pragma unroll
-        for (int j = 0; j < PER_T; j++) {
-            const int c = tid + j * NT;
-            stg[j] = (c < avail) ? src[c] : make_uint4(0, 0, 0, 0);
-        }
-        if (tid < CB * 8) {
-            const int bb = tid >> 3;
-            stg_nc = (blk0 + bb < b_end) ? reinterpret_cast<const uint4 *>(cnc)[(long)blk0 * 8 + tid] : inf4;
-        }
-    };
-    auto swrite = [&](int buf) {
-        uint4 *dst = reinterpret_cast<uint4 *>(smem + buf * BUF_BYTES);
-#pragma unroll
-        for (int j = 0; j < PER_T; j++) dst[tid + j * NT] = stg[j];
-        if (tid < CB * 8) reinterpret_cast<uint4 *>(smem + buf * BUF_BYTES + FRAG_BYTES)[tid] = stg_nc;
+        for (int j = 0; j < PER_T; j++) glds16(src + min(j * NT + w * 64 + lane, last), dst + (j * NT + w * 64) * 16);
+        if (w == 0 && lane < CB * 8)
+            glds16(reinterpret_cast<const uint4 *>(cnc) + (long)blk0 * 8 + min(lane, nb * 8 - 1), dst + FRAG_BYTES);
     };
 
-    if (nstage > 0) {
-        gload(0);
-        swrite(0);
-    }
+    if (nstage > 0) issue(0, 0);
     __syncthreads();
     for (int st = 0; st < nstage; st++) {
-        if (st + 1 < nstage) gload(st + 1);
         const char *B = smem + (st & 1) * BUF_BYTES;
+        // the stage's norms go to registers BEFORE the next DMA is issued: hipcc otherwise waits
+        // vmcnt(0) (the DMA) at the first norm read, serialising the prefetch behind the compute
+        float4 ncr[CB][4];
+#pragma unroll
+        for (int cb = 0; cb < CB; cb++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) ncr[cb][i] = reinterpret_cast<const float4 *>(B + FRAG_BYTES)[cb * 8 + h * 4 + i];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
 #pragma unroll
         for (int cb = 0; cb < CB; cb++) {
             const int blk = b_begin + st * CB + cb;
             if (blk < b_end) {
-                floatx16 acc0 = {0}, acc1 = {0};
+                const float4 n0 = ncr[cb][0], n1 = ncr[cb][1], n2 = ncr[cb][2], n3 = ncr[cb][3];
+                floatx16 acc0 = {-0.5f * n0.x, -0.5f * n0.y, -0.5f * n0.z, -0.5f * n0.w,
+                                 -0.5f * n1.x, -0.5f * n1.y, -0.5f * n1.z, -0.5f * n1.w,
+                                 -0.5f * n2.x, -0.5f * n2.y, -0.5f * n2.z, -0.5f * n2.w,
+                                 -0.5f * n3.x, -0.5f * n3.y, -0.5f * n3.z, -0.5f * n3.w};
+                floatx16 acc1 = acc0;
 #pragma unroll
                 for (int s = 0; s < S; s++) {
                     const half8 av = reinterpret_cast<const half8 *>(B)[(cb * S + s) * 64 + lane];
                     acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq0[s], acc0, 0, 0, 0);
                     acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq1[s], acc1, 0, 0, 0);
                 }
-                const float4 *np = reinterpret_cast<const float4 *>(B + FRAG_BYTES) + cb * 8 + h * 4;
-                const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
-                const float nc[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w,
-                                      n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
                 const int base = blk * 32;
-                scan_keys<L>(acc0, nc, base, h, perm, lk0, li0);
-                scan_keys<L>(acc1, nc, base, h, perm, lk1, li1);
+                scan_keys<L>(acc0, base, h, perm, lk0, li0);
+                scan_keys<L>(acc1, base, h, perm, lk1, li1);
             }
         }
-        if (st + 1 < nstage) swrite((st + 1) & 1);
-        __syncthreads();
+        __syncthreads();  // vmcnt(0) + s_barrier: next stage's DMA landed, this stage's reads done
     }
     // partial lists: [q][split][h][L]
 #pragma unroll
@@ -310,7 +313,6 @@ __global__ __launch_bounds__(256, 2) void nn_collect_kernel(const half8 *__restr
     const int b_begin = blockIdx.y * blk_per_split;
     const int b_end = min(nblk, b_begin + blk_per_split);
     const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
-    const uint4 inf4 = make_uint4(0x7f800000u, 0x7f800000u, 0x7f800000u, 0x7f800000u);
     for (int g = blockIdx.x; g * 256 < count; g += gridDim.x) {
         half8 bq0[S], bq1[S];
         int j0 = (g * 4 + w) * 64 + (lane & 31), j1 = j0 + 32;
@@ -326,15 +328,11 @@ __global__ __launch_bounds__(256, 2) void nn_collect_kernel(const half8 *__restr
         uint4 stg_nc = make_uint4(0, 0, 0, 0);
         auto gload = [&](int st) {
             const int blk0 = b_begin + st * CB;
-            const int avail = min(CB, b_end - blk0) * S * 64;
+            const int last = min(CB, b_end - blk0) * S * 64 - 1;
             const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64;
 #pragma unroll
-            for (int jj = 0; jj < PER_T; jj++) {
-                const int c = tid + jj * 256;
-                stg[jj] = (c < avail) ? src[c] : make_uint4(0, 0, 0, 0);
-            }
-            if (tid < CB * 8)
-                stg_nc = (blk0 + (tid >> 3) < b_end) ? reinterpret_cast<const uint4 *>(cnc)[(long)blk0 * 8 + tid] : inf4;
+            for (int jj = 0; jj < PER_T; jj++) stg[jj] = src[min(tid + jj * 256, last)];
+            stg_nc = reinterpret_cast<const uint4 *>(cnc)[(long)blk0 * 8 + min(tid, min(CB, b_end - blk0) * 8 - 1)];
         };
         auto swrite = [&](int buf) {
             uint4 *dst = reinterpret_cast<uint4 *>(smem + buf * BUF_BYTES);
@@ -494,9 +492,11 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
         T = kk;
     } else {
         const double nq = sqrt(st.n2);
-        const double gam = 2.0 * a.d * u;  // >= 2x gamma_d: MFMA accumulation, conservative
-        const double E = 1.05 * (2.0 * u * a.N * a.N + 2.0 * u * st.hn * a.H +
-                                 2.0 * (gam * st.hn * a.H + st.en * a.N + st.hn * a.Ec)) + 1e-30;
+        // key error bound: fp32 rounding of ||c||^2, the MFMA accumulation seeded with
+        // -||c||^2/2 (>= 2x gamma_{D+1} over |seed| + sum |q^_d c^_d|), and the fp16 residuals
+        const double gam = 2.0 * (a.d + 1) * u;
+        const double E = 1.05 * (2.0 * u * a.N * a.N + gam * (a.N * a.N + 2.0 * st.hn * a.H) +
+                                 2.0 * (st.en * a.N + st.hn * a.Ec)) + 1e-30;
         const double g = (double)(a.d + 4) * u / (1.0 - (double)(a.d + 4) * u) * 1.05;
         T = ((st.n2 + (double)kk + E) * (1.0 + g) / (1.0 - g)) - st.n2 + E;
         T += 1e-12 * (st.n2 + fabs((double)kk)) + 1e-30;

@@ -1,0 +1,126 @@
+"""GlobalTiling step (btnDoGlobalTilingClick main.pas:837-856 -> DoGlobalTiling main.pas:4256-4370).
+
+Host bookkeeping mirrors the reference procedures by name; the K-Modes reduction and the medoid choice
+run on the GPU (tiler_kmodes_compute / tiler_kmodes_medoids):
+  write_tile_dataset_line  WriteTileDatasetLine main.pas:4167-4183 (+ GetTilePalZoneThres 4142-4165)
+  equal_quality_tile_count EqualQualityTileCount main.pas:722-725
+  do_global_tiling         DoGlobalTiling 4256-4331 + DoKModes 4195-4254 + MergeTiles 3688-3712
+  make_tiles_unique        MakeTilesUnique 2555-2612 (stable order: lowest index represents duplicates)
+  reindex_tiles            ReindexTiles 4483-4527 (UseCount desc, old index asc)
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+
+from ._lib import check, load
+from .kmodes import compute_kmodes
+
+CRANDOM_KMODES_COUNT = 7  # cRandomKModesCount main.pas:19
+
+
+def write_tile_dataset_line(tiles: np.ndarray, palsize: int = 16) -> np.ndarray:
+    """[T, 64] palette indices -> [T, 80] K-Modes rows: 64 indices + 16 zone flags
+    (count(idx*16 div palsize == z) > palsize div 16)."""
+    t = np.asarray(tiles, np.uint8).reshape(-1, 64)
+    zone = (t.astype(np.int64) * 16) // palsize
+    acc = np.stack([(zone == z).sum(1) for z in range(16)], 1)
+    flags = (acc > (palsize // 16)).astype(np.uint8)
+    return np.ascontiguousarray(np.concatenate([t, flags], 1))
+
+
+def equal_quality_tile_count(n: float) -> int:
+    """round(sqrt(n) * log2(1 + n)) with FPC's banker's rounding (Python round is half-even)."""
+    return int(round(math.sqrt(n) * (math.log(1.0 + n) / math.log(2.0))))
+
+
+def kmodes_medoids(X: np.ndarray, labels: np.ndarray, centroids: np.ndarray):
+    lib = load()
+    X = np.ascontiguousarray(X, np.uint8)
+    labels = np.ascontiguousarray(labels, np.int32)
+    centroids = np.ascontiguousarray(centroids, np.uint8)
+    k = centroids.shape[0]
+    medoid = np.zeros(k, np.int32)
+    counts = np.zeros(k, np.int32)
+    v = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    check(lib.tiler_kmodes_medoids(v(X), X.shape[0], v(labels), v(centroids), k, v(medoid), v(counts)),
+          "tiler_kmodes_medoids")
+    return medoid, counts
+
+
+def merge_tiles(idx, best, palpix, active, use_count, merge_index):
+    """MergeTiles main.pas:3688-3712 (NewTile = nil)."""
+    for j in idx:
+        if j == best:
+            continue
+        use_count[best] += use_count[j]
+        active[j] = 0
+        merge_index[j] = best
+        palpix[j] = 0
+
+
+def do_global_tiling(palpix, dith_pal, n_palettes: int, desired: int, palsize: int = 16,
+                     restart: int = CRANDOM_KMODES_COUNT, active=None, use_count=None):
+    """Returns (palpix, active, use_count, merge_index, k_per_bin) after the K-Modes merge pass
+    (the caller applies merge_index to tilemaps: FinishMergeTiles main.pas:3722-3734)."""
+    palpix = np.array(palpix, np.uint8, copy=True).reshape(-1, 64)
+    T = palpix.shape[0]
+    active = np.ones(T, np.uint8) if active is None else np.array(active, np.uint8, copy=True)
+    use_count = np.ones(T, np.int64) if use_count is None else np.array(use_count, np.int64, copy=True)
+    dith_pal = np.asarray(dith_pal, np.int64)
+    merge_index = np.full(T, -1, np.int64)
+    lines = write_tile_dataset_line(palpix, palsize)
+    act = np.nonzero(active)[0]
+    bins = [act[dith_pal[act] == p] for p in range(n_palettes)]
+    # StartingPoint: last row of the bin with minimal byte sum (acc <= best), -restart when empty
+    starts = []
+    for b in bins:
+        if b.size == 0:
+            starts.append(-restart)
+            continue
+        s = lines[b].astype(np.int64).sum(1)
+        starts.append(int(b.size - 1 - np.argmin(s[::-1])))
+    dis_cnt = sum(equal_quality_tile_count(b.size) for b in bins)
+    share = desired / dis_cnt
+    k_per_bin = np.zeros(n_palettes, np.int64)
+    for p, b in enumerate(bins):
+        kc = math.ceil(equal_quality_tile_count(b.size) * share)
+        k = int(round(kc))
+        k_per_bin[p] = k
+        if b.size <= kc:
+            continue
+        X = np.ascontiguousarray(lines[b])
+        labels, cent, _, _ = compute_kmodes(X, k, starts[p], palsize)
+        medoid, counts = kmodes_medoids(X, labels, cent)
+        for j in np.nonzero(counts >= 2)[0]:
+            members = b[labels == j]
+            merge_tiles(members, int(b[medoid[j]]), palpix, active, use_count, merge_index)
+    return palpix, active, use_count, merge_index, k_per_bin
+
+
+def make_tiles_unique(palpix, active, use_count):
+    """MakeTilesUnique main.pas:2555-2612 over all tiles; duplicates merge into the lowest index."""
+    palpix = np.array(palpix, np.uint8, copy=True)
+    active = np.array(active, np.uint8, copy=True)
+    use_count = np.array(use_count, np.int64, copy=True)
+    merge_index = np.full(palpix.shape[0], -1, np.int64)
+    idx = np.nonzero(active)[0]
+    if idx.size:
+        _, inv = np.unique(palpix[idx], axis=0, return_inverse=True)
+        inv = inv.reshape(-1)
+        for g in np.unique(inv):
+            members = idx[inv == g]
+            if members.size >= 2:
+                merge_tiles(members, int(members.min()), palpix, active, use_count, merge_index)
+    return palpix, active, use_count, merge_index
+
+
+def reindex_tiles(active, use_count):
+    """ReindexTiles main.pas:4483-4527: idx_map[old] = new, order (UseCount desc, old index asc)."""
+    act = np.nonzero(active)[0]
+    order = act[np.lexsort((act, -np.asarray(use_count)[act]))]
+    idx_map = np.full(np.asarray(active).shape[0], -1, np.int64)
+    idx_map[order] = np.arange(order.size)
+    return idx_map

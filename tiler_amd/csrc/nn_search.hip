@@ -293,6 +293,179 @@ __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *_
 }
 
 // ------------------------------------------------------------------------------------------
+// 1'. Shortlist, one wave per SIMD (512-register budget): each wave holds 4 query blocks (128 queries)
+// as B fragments, so every A fragment read from LDS feeds 4 MFMAs, and the epilogue of candidate block
+// n-1 (max tree + threshold compare, straight-line VALU) is interleaved with the MFMAs of block n
+// (ping-pong accumulator sets).  List insertion (rare) runs between blocks behind one wave-uniform
+// branch.  Workgroup = 4 waves = 512 queries; candidate tiles by LDS-DMA, double-buffered.
+// ------------------------------------------------------------------------------------------
+template <int L>
+__device__ __forceinline__ void flush_inserts(const floatx16 &acc, float (&lk)[L], int (&li)[L], int base, int h,
+                                              int perm) {
+#pragma unroll
+    for (int r = 0; r < 16; r++)
+        if (acc[r] > -0.5f * lk[L - 1]) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            list_insert<L>(lk, li, -2.0f * acc[r], base + (perm ? row_perm(row) : row));
+        }
+}
+
+__device__ __forceinline__ float max16(const floatx16 &a) {
+    float m0 = fmaxf(fmaxf(a[0], a[1]), a[2]), m1 = fmaxf(fmaxf(a[3], a[4]), a[5]);
+    float m2 = fmaxf(fmaxf(a[6], a[7]), a[8]), m3 = fmaxf(fmaxf(a[9], a[10]), a[11]);
+    float m4 = fmaxf(fmaxf(a[12], a[13]), a[14]);
+    return fmaxf(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)), fmaxf(m4, a[15]));
+}
+
+template <int S, int L, int CB, int QB>
+__global__ __launch_bounds__(256, 1) void nn_shortlist4_kernel(const half8 *__restrict__ cfrag,
+                                                               const float *__restrict__ cnc, int nblk,
+                                                               const half8 *__restrict__ qfrag, int nq,
+                                                               int blk_per_split, int nsplit, int perm,
+                                                               float *__restrict__ out_key, int *__restrict__ out_idx) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int FRAG_BYTES = CB * S * 1024;
+    constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
+    constexpr int PER_T = CB * S * 64 / 256;
+    static_assert((CB * S * 64) % 256 == 0 && CB % 2 == 0, "stage geometry");
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int nqblk = (nq + 31) / 32;
+    const int qb0 = (blockIdx.x * 4 + w) * QB;
+    const int split = blockIdx.y;
+    const int b_begin = split * blk_per_split;
+    const int b_end = min(nblk, b_begin + blk_per_split);
+
+    half8 bq[QB][S];
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+        const long qq = min(qb0 + q, nqblk - 1);  // blocks past the end: clamped duplicate, never written
+#pragma unroll
+        for (int s = 0; s < S; s++) bq[q][s] = qfrag[(qq * S + s) * 64 + lane];
+    }
+    float lk[QB][L];
+    int li[QB][L];
+#pragma unroll
+    for (int q = 0; q < QB; q++)
+#pragma unroll
+        for (int i = 0; i < L; i++) {
+            lk[q][i] = INFINITY;
+            li[q][i] = -1;
+        }
+
+    const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
+    auto issue = [&](int st, int buf) {
+        const int blk0 = b_begin + st * CB;
+        const int nb = min(CB, b_end - blk0);
+        const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64 + w * 64 + lane;
+        char *dst = smem + buf * BUF_BYTES + w * 1024;
+        if (nb == CB) {  // full stage: one lane pointer + immediate offsets (few live registers)
+#pragma unroll
+            for (int j = 0; j < PER_T; j++) glds16(src + j * 256, dst + j * 4096);
+        } else {         // last partial stage: clamp to the valid range
+            const int last = nb * S * 64 - 1 - (w * 64 + lane);
+#pragma unroll
+            for (int j = 0; j < PER_T; j++) glds16(src + min(j * 256, last), dst + j * 4096);
+        }
+        if (w == 0 && lane < CB * 8)
+            glds16(reinterpret_cast<const uint4 *>(cnc) + (long)blk0 * 8 + min(lane, nb * 8 - 1),
+                   smem + buf * BUF_BYTES + FRAG_BYTES);
+    };
+
+    floatx16 accA[QB], accB[QB];
+    int baseA = -1, baseB = -1;  // candidate block of the pending (not yet scanned) accumulator set
+    bool needB = false;
+
+    // one candidate block: MFMAs into `cur` interleaved with the max-scan of `prev`
+    auto block = [&](const char *B, int cb, const float4 (&nc)[4], floatx16 (&cur)[QB], floatx16 (&prev)[QB],
+                     int prev_base, bool &need) {
+        floatx16 seed;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            seed[4 * i] = -0.5f * nc[i].x;
+            seed[4 * i + 1] = -0.5f * nc[i].y;
+            seed[4 * i + 2] = -0.5f * nc[i].z;
+            seed[4 * i + 3] = -0.5f * nc[i].w;
+        }
+        bool nd = false;
+        half8 a_next = reinterpret_cast<const half8 *>(B)[(cb * S) * 64 + lane];
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            const half8 av = a_next;
+            if (s + 1 < S) a_next = reinterpret_cast<const half8 *>(B)[(cb * S + s + 1) * 64 + lane];
+#pragma unroll
+            for (int q = 0; q < QB; q++)
+                cur[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[q][s], s == 0 ? seed : cur[q], 0, 0, 0);
+            // the previous block's epilogue, spread over the k-steps (independent of these MFMAs)
+            if (prev_base >= 0 && s >= 1 && s <= QB) {
+                const int q = s - 1;
+                nd |= max16(prev[q]) > -0.5f * lk[q][L - 1];
+            }
+        }
+        need = nd;
+    };
+    auto drain = [&](floatx16 (&prev)[QB], int prev_base, bool need) {
+        if (prev_base >= 0 && __any(need)) {
+#pragma unroll
+            for (int q = 0; q < QB; q++) flush_inserts<L>(prev[q], lk[q], li[q], prev_base, h, perm);
+        }
+    };
+
+    if (nstage > 0) issue(0, 0);
+    __syncthreads();
+    for (int st = 0; st < nstage; st++) {
+        const char *B = smem + (st & 1) * BUF_BYTES;
+        float4 ncr[CB][4];
+#pragma unroll
+        for (int cb = 0; cb < CB; cb++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) ncr[cb][i] = reinterpret_cast<const float4 *>(B + FRAG_BYTES)[cb * 8 + h * 4 + i];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
+#pragma unroll
+        for (int cb = 0; cb < CB; cb += 2) {
+            const int blk = b_begin + st * CB + cb;
+            if (blk < b_end) {  // block -> accA, scanning accB (previous odd block)
+                bool need = false;
+                block(B, cb, ncr[cb], accA, accB, baseB, need);
+                drain(accB, baseB, need);
+                baseB = -1;
+                baseA = blk * 32;
+            }
+            if (blk + 1 < b_end) {  // block -> accB, scanning accA
+                bool need = false;
+                block(B, cb + 1, ncr[cb + 1], accB, accA, baseA, need);
+                drain(accA, baseA, need);
+                baseA = -1;
+                baseB = (blk + 1) * 32;
+            }
+        }
+        __syncthreads();
+    }
+    // tail: the last block's accumulators
+    if (baseA >= 0) {
+#pragma unroll
+        for (int q = 0; q < QB; q++) flush_inserts<L>(accA[q], lk[q], li[q], baseA, h, perm);
+    }
+    if (baseB >= 0) {
+#pragma unroll
+        for (int q = 0; q < QB; q++) flush_inserts<L>(accB[q], lk[q], li[q], baseB, h, perm);
+    }
+    (void)needB;
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+        const int qq = (qb0 + q) * 32 + (lane & 31);
+        if (qq < nq) {
+            const long o = (((long)qq * nsplit + split) * 2 + h) * L;
+#pragma unroll
+            for (int i = 0; i < L; i++) {
+                out_key[o + i] = lk[q][i];
+                out_idx[o + i] = li[q][i];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // 1b. tier-2 collect: for the queries whose tier-1 lists overflowed, recompute the MFMA keys and append
 // EVERY candidate with key <= T(q) to a per-query buffer (atomic cursor).  Compact query j's B fragment
 // is gathered straight from the tier-1 fragment buffer.  Grid-stride over groups of 256 queries.
@@ -825,14 +998,35 @@ static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream
                        ix->scratch.key, ix->scratch.idx);
 }
 
-// workgroup size of the D=192 shortlist: 8 waves (512 queries share each staged candidate tile)
-// unless TILER_SHORTLIST_WAVES=4 (A/B switch for measurements)
-static int shortlist_waves() {
-    static int w = [] {
-        const char *e = getenv("TILER_SHORTLIST_WAVES");
-        return (e && atoi(e) == 4) ? 4 : 8;
+static constexpr int SL4_QB = 3;  // query blocks per wave in the one-wave-per-SIMD shortlist
+
+template <int S, int L, int CB, int QB>
+static void launch_shortlist4(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
+    const int nqblk = (nq + 31) / 32;
+    const dim3 grid((nqblk + 4 * QB - 1) / (4 * QB), nsplit);
+    const size_t lds = 2 * (CB * S * 1024 + CB * 128);
+    KTimer tm("nn_shortlist", stream);
+    hipLaunchKernelGGL((nn_shortlist4_kernel<S, L, CB, QB>), grid, dim3(256), lds, stream, (const half8 *)ix->d_frag,
+                       ix->d_nc, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps, nsplit, ix->perm,
+                       ix->scratch.key, ix->scratch.idx);
+}
+
+// D=192 shortlist variant (A/B switch TILER_SHORTLIST for measurements):
+//   "w1" (default): one wave per SIMD, 4 query blocks per wave, epilogue interleaved (nn_shortlist4_kernel)
+//   "w8": 8 waves x 2 query blocks, 2 waves per SIMD;  "w4": 4 waves x 2 query blocks
+static int shortlist_variant() {
+    static int v = [] {
+        const char *e = getenv("TILER_SHORTLIST");
+        if (e && !strcmp(e, "w8")) return 8;
+        if (e && !strcmp(e, "w4")) return 4;
+        return 1;
     }();
-    return w;
+    return v;
+}
+
+static int shortlist_queries_per_wg(int S) {
+    if (S != 12) return 256;
+    return shortlist_variant() == 8 ? 512 : shortlist_variant() == 4 ? 256 : 128 * SL4_QB;
 }
 
 template <int L>
@@ -841,10 +1035,12 @@ static int dispatch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
         case 4: launch_shortlist<4, L, 6, 4>(ix, nq, nsplit, bps, stream); break;
         case 8: launch_shortlist<8, L, 3, 4>(ix, nq, nsplit, bps, stream); break;
         case 12:
-            if (shortlist_waves() == 8)
+            if (shortlist_variant() == 8)
                 launch_shortlist<12, L, 2, 8>(ix, nq, nsplit, bps, stream);
-            else
+            else if (shortlist_variant() == 4)
                 launch_shortlist<12, L, 2, 4>(ix, nq, nsplit, bps, stream);
+            else
+                launch_shortlist4<12, L, 2, SL4_QB>(ix, nq, nsplit, bps, stream);
             break;
         case 16: launch_shortlist<16, L, 2, 4>(ix, nq, nsplit, bps, stream); break;
         default: set_error("nn: unsupported fragment depth"); return -1;
@@ -938,7 +1134,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     }
     const int L = 8;  // >= 2x the 4-way mirror near-ties of one tile per lane (row_perm spreads them 2+2)
     const int max_split = 64 / (2 * L);
-    const int wgs = ((nq + 31) / 32 + 15) / 16;
+    const int wgs = (nq + shortlist_queries_per_wg(ix->S) - 1) / shortlist_queries_per_wg(ix->S);
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
     nsplit = std::min(nsplit, ix->nblk);
     const int bps = (ix->nblk + nsplit - 1) / nsplit;

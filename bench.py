@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (rank 0)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, visible cores)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-smooth", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -166,8 +167,27 @@ def main():
     roofline = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None, "peak": PEAK_F16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
                 "traffic": None,
-                "kernel": f"nn_shortlist_kernel<S=12,L=8,CB=2,NW={os.environ.get('TILER_SHORTLIST_WAVES', '8')}>",
+                "kernel": {"w1": "nn_shortlist4_kernel<12,8,2,QB=3>", "w4": "nn_shortlist_kernel<12,8,2,NW=4>"}.get(
+                    os.environ.get("TILER_SHORTLIST", ""), "nn_shortlist_kernel<12,8,2,NW=8>"),
                 "note": "algorithmic 2*M*D per tile vs dense fp16 MFMA peak; 1 fp16 product per pair"}
+
+    # ---- secondary (not the metric): Smooth over this keyframe's FT tilemap (DoTemporalSmoothing) ----
+    smooth = None
+    if rank == 0 and not args.no_smooth:
+        s_tile = out_tile.view(F, Q).clone()
+        s_pal = out_pal.view(F, Q).clone()
+        s_hm, s_vm = out_hm.view(F, Q).clone(), out_vm.view(F, Q).clone()
+        s_sm = torch.zeros((F, Q), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        check(lib.tiler_smooth_keyframe_dev(F, Q, vp(s_tile.data_ptr()), None, vp(s_pal.data_ptr()),
+                                            vp(s_hm.data_ptr()), vp(s_vm.data_ptr()), vp(s_sm.data_ptr()),
+                                            vp(d_tiles.data_ptr()), vp(d_pals.data_ptr()), 0.02, vp(stream)),
+              "tiler_smooth_keyframe_dev")
+        torch.cuda.synchronize(dev)
+        ts = time.perf_counter() - t0
+        smooth = {"value": round((F - 1) * Q / ts / 1e6, 4), "unit": "Msteps/s", "ms": round(ts * 1e3, 3),
+                  "smoothed": int(s_sm.sum().item()), "shape": f"{F} frames x {Q} positions, Strength 0.02"}
 
     # ---- CPU baseline (rank 0, N=1): the oracle restatement, bounded sample, same workload ----
     cpu = None
@@ -184,6 +204,7 @@ def main():
                        "tiles_per_step_per_gpu": QK, "candidates": M, "descriptor": "PsyV Haar 192-d",
                        "parallelism": f"keyframes sharded, {world} GPU(s)"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "search_stats": stats,
+            "secondary": {"smooth": smooth},
         }
         print(json.dumps(res))
     kdt.close()

@@ -194,7 +194,7 @@ template <int S, int L, int CB, int NW>
 __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *__restrict__ cfrag,
                                                               const float *__restrict__ cnc, int nblk,
                                                               const half8 *__restrict__ qfrag, int nq,
-                                                              int blk_per_split, int nsplit, int perm,
+                                                              int blk_per_split, int nsplit, int perm, int prio,
                                                               float *__restrict__ out_key, int *__restrict__ out_idx) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * S * 1024;
@@ -264,12 +264,14 @@ __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *_
                                  -0.5f * n2.x, -0.5f * n2.y, -0.5f * n2.z, -0.5f * n2.w,
                                  -0.5f * n3.x, -0.5f * n3.y, -0.5f * n3.z, -0.5f * n3.w};
                 floatx16 acc1 = acc0;
+                if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int s = 0; s < S; s++) {
                     const half8 av = reinterpret_cast<const half8 *>(B)[(cb * S + s) * 64 + lane];
                     acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq0[s], acc0, 0, 0, 0);
                     acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq1[s], acc1, 0, 0, 0);
                 }
+                if (prio) __builtin_amdgcn_s_setprio(0);
                 const int base = blk * 32;
                 scan_keys<L>(acc0, base, h, perm, lk0, li0);
                 scan_keys<L>(acc1, base, h, perm, lk1, li1);
@@ -987,6 +989,16 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
     return 0;
 }
 
+// s_setprio(1) around the MFMA chain (TILER_SETPRIO=1): lets the wave that reaches its MFMAs keep the
+// matrix pipe while the sibling wave on the SIMD runs its list-update epilogue.
+static int shortlist_prio() {
+    static int v = [] {
+        const char *e = getenv("TILER_SETPRIO");
+        return (e && e[0] == '1') ? 1 : 0;
+    }();
+    return v;
+}
+
 template <int S, int L, int CB, int NW>
 static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     const int nqblk = (nq + 31) / 32;
@@ -995,7 +1007,7 @@ static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream
     KTimer tm("nn_shortlist", stream);
     hipLaunchKernelGGL((nn_shortlist_kernel<S, L, CB, NW>), grid, dim3(NW * 64), lds, stream, (const half8 *)ix->d_frag,
                        ix->d_nc, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps, nsplit, ix->perm,
-                       ix->scratch.key, ix->scratch.idx);
+                       shortlist_prio(), ix->scratch.key, ix->scratch.idx);
 }
 
 static constexpr int SL4_QB = 3;  // query blocks per wave in the one-wave-per-SIMD shortlist
@@ -1012,14 +1024,15 @@ static void launch_shortlist4(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
 }
 
 // D=192 shortlist variant (A/B switch TILER_SHORTLIST for measurements):
-//   "w1" (default): one wave per SIMD, 4 query blocks per wave, epilogue interleaved (nn_shortlist4_kernel)
-//   "w8": 8 waves x 2 query blocks, 2 waves per SIMD;  "w4": 4 waves x 2 query blocks
+//   "w8" (default): 8 waves x 2 query blocks, 2 waves per SIMD (63 ms / C3 keyframe, 49.6 % of peak)
+//   "w4": 4 waves x 2 query blocks (67 ms);  "w1": one wave per SIMD, 3 query blocks per wave with the
+//   epilogue interleaved (nn_shortlist4_kernel, 89 ms: hipcc's schedule of the 512-register body loses)
 static int shortlist_variant() {
     static int v = [] {
         const char *e = getenv("TILER_SHORTLIST");
-        if (e && !strcmp(e, "w8")) return 8;
+        if (e && !strcmp(e, "w1")) return 1;
         if (e && !strcmp(e, "w4")) return 4;
-        return 1;
+        return 8;
     }();
     return v;
 }

@@ -25,6 +25,16 @@ sys.path.insert(0, ROOT)
 
 METRIC = "FrameTiling Mtiles/sec @1080p 8×8, 64k tileset; % HBM roofline at 1/2/4/8 GPU"
 PEAK_F16_TFLOPS = 2500.0   # MI355X dense fp16 MFMA (MI355X_MICROARCH.md; sparsity excluded)
+# dominant kernel per TILER_SHORTLIST variant (tiler_amd/csrc/nn_search.hip, shortlist_variant())
+SHORTLIST_KERNELS = {
+    "q16": "nn_shortlist16_kernel<S=6,L=4,CB=8,NW=8,QB=4>",
+    "q16l6": "nn_shortlist16_kernel<S=6,L=6,CB=8,NW=8,QB=4>",
+    "p4": "nn_shortlist2_kernel<S=12,L=8,CB=4,NW=8>",
+    "p2": "nn_shortlist2_kernel<S=12,L=8,CB=2,NW=8>",
+    "w8": "nn_shortlist_kernel<S=12,L=8,CB=2,NW=8>",
+    "w4": "nn_shortlist_kernel<S=12,L=8,CB=2,NW=4>",
+    "w1": "nn_shortlist4_kernel<S=12,L=8,CB=2,QB=3>",
+}
 PEAK_HBM_GBS = 8000.0
 
 CONFIGS = {
@@ -167,8 +177,7 @@ def main():
     roofline = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None, "peak": PEAK_F16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
                 "traffic": None,
-                "kernel": {"w1": "nn_shortlist4_kernel<12,8,2,QB=3>", "w4": "nn_shortlist_kernel<12,8,2,NW=4>"}.get(
-                    os.environ.get("TILER_SHORTLIST", ""), "nn_shortlist_kernel<12,8,2,NW=8>"),
+                "kernel": SHORTLIST_KERNELS.get(os.environ.get("TILER_SHORTLIST", ""), SHORTLIST_KERNELS["q16"]),
                 "note": "algorithmic 2*M*D per tile vs dense fp16 MFMA peak; 1 fp16 product per pair"}
 
     # ---- secondary (not the metric): Smooth over this keyframe's FT tilemap (DoTemporalSmoothing) ----

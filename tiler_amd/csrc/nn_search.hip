@@ -46,6 +46,7 @@ struct PrepArgs {
     float scale;
     half8 *frag;
     float *nc;      // dataset only: accumulator-row order
+    float *seed;    // dataset only: -||c||^2/2 in accumulator-row order (shortlist accumulator seed)
     QStat *qstat;   // queries only
     DsStat *ds;     // dataset only
     int perm;       // dataset only: A-operand row i holds candidate blk*32 + row_perm(i)
@@ -109,6 +110,7 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(PrepArgs a) {
             const int rr = lane & 31;
             const int pos = ((rr >> 2) & 1) * 16 + ((rr & 3) | ((rr >> 3) << 2));
             a.nc[blk * 32 + pos] = valid ? (float)s2 : INFINITY;
+            if (a.seed) a.seed[blk * 32 + pos] = valid ? -0.5f * (float)s2 : -INFINITY;
         }
         if (a.ds) {
             double m2 = wave_max_d(valid ? s2 : 0.0), mh = wave_max_d(valid ? sh : 0.0);
@@ -154,6 +156,17 @@ __device__ __forceinline__ void glds16(const uint4 *gsrc, char *lds_wave_base) {
     typedef __attribute__((address_space(3))) void lvoid;
     __builtin_amdgcn_global_load_lds((gvoid *)(gsrc), (lvoid *)(lds_wave_base), 16, 0, 0);
 }
+
+// The same DMA as inline asm, invisible to hipcc's waitcnt pass: the compiler counts a pending
+// global_load_lds as an LGKM event of another kind, which makes every later LDS-read wait an
+// lgkmcnt(0) (no read can stay in flight behind an MFMA).  Users drain it themselves: dma_drain()
+// before the barrier that publishes the stage.
+__device__ __forceinline__ void glds16_asm(const uint4 *gsrc, char *lds_wave_base) {
+    const unsigned lds = __builtin_amdgcn_readfirstlane(
+        (unsigned)(size_t)(__attribute__((address_space(3))) char *)lds_wave_base);
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(lds) : "memory");
+}
+__device__ __forceinline__ void dma_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 template <int L>
 __device__ __forceinline__ void list_insert(float (&k)[L], int (&id)[L], float x, int ix) {
@@ -289,6 +302,329 @@ __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *_
             for (int i = 0; i < L; i++) {
                 out_key[o + i] = qb ? lk1[i] : lk0[i];
                 out_idx[o + i] = qb ? li1[i] : li0[i];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// 1''. Shortlist, software-pipelined LDS reads.  Same work split as nn_shortlist_kernel (NW waves x 2
+// query blocks, CB candidate blocks per LDS stage) but: the A fragments of k-step pair s+1 are read
+// while the MFMAs of pair s run (the plain kernel waits on every LDS read), the next block's first
+// pair and seeds are read before the current block's epilogue, and the accumulator seed
+// (-||c||^2/2, cseed) is the first MFMA's C operand, so a block costs no seed arithmetic.
+// ------------------------------------------------------------------------------------------
+template <int S, int L, int CB, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void nn_shortlist2_kernel(const half8 *__restrict__ cfrag,
+                                                               const float *__restrict__ cseed, int nblk,
+                                                               const half8 *__restrict__ qfrag, int nq,
+                                                               int blk_per_split, int nsplit, int perm,
+                                                               float *__restrict__ out_key, int *__restrict__ out_idx) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int FRAG_BYTES = CB * S * 1024;
+    constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
+    constexpr int NT = NW * 64;
+    constexpr int PER_T = CB * S * 64 / NT;
+    static_assert((CB * S * 64) % NT == 0 && S % 2 == 0, "stage must split evenly over the workgroup");
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int nqblk = (nq + 31) / 32;
+    const int qb0 = (blockIdx.x * NW + w) * 2;
+    const int split = blockIdx.y;
+    const int b_begin = split * blk_per_split;
+    const int b_end = min(nblk, b_begin + blk_per_split);
+
+    half8 bq0[S], bq1[S];
+    const long qa = min(qb0, nqblk - 1), qc = min(qb0 + 1, nqblk - 1);
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        bq0[s] = qfrag[(qa * S + s) * 64 + lane];
+        bq1[s] = qfrag[(qc * S + s) * 64 + lane];
+    }
+    // land the query fragments before the loop (a real s_waitcnt the compiler's pass accounts for):
+    // a wait sunk into the loop would also count the hidden DMA pieces and stall on them
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    float lk0[L], lk1[L];
+    int li0[L], li1[L];
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+        lk0[i] = lk1[i] = INFINITY;
+        li0[i] = li1[i] = -1;
+    }
+
+    const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
+    auto issue = [&](int st, int buf) {
+        const int blk0 = b_begin + st * CB;
+        const int nb = min(CB, b_end - blk0);
+        const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64 + w * 64 + lane;
+        char *dst = smem + buf * BUF_BYTES + w * 1024;
+        if (nb == CB) {
+#pragma unroll
+            for (int j = 0; j < PER_T; j++) glds16_asm(src + j * NT, dst + j * NT * 16);
+        } else {
+            const int last = nb * S * 64 - 1 - (w * 64 + lane);
+#pragma unroll
+            for (int j = 0; j < PER_T; j++) glds16_asm(src + min(j * NT, last), dst + j * NT * 16);
+        }
+        if (w == 0 && lane < CB * 8)
+            glds16_asm(reinterpret_cast<const uint4 *>(cseed) + (long)blk0 * 8 + min(lane, nb * 8 - 1),
+                   smem + buf * BUF_BYTES + FRAG_BYTES);
+    };
+
+    if (nstage > 0) issue(0, 0);
+    dma_drain();
+    __syncthreads();
+    for (int st = 0; st < nstage; st++) {
+        const char *B = smem + (st & 1) * BUF_BYTES;
+        const half8 *A = reinterpret_cast<const half8 *>(B) + lane;
+        const float4 *SD = reinterpret_cast<const float4 *>(B + FRAG_BYTES) + h * 4;
+        // every block's seeds and the first k-step pair go to registers before the DMA issue: hipcc
+        // would otherwise put a vmcnt(0) (the DMA) in front of the first seed read
+        float4 sd[CB][4];
+#pragma unroll
+        for (int cb = 0; cb < CB; cb++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) sd[cb][i] = SD[cb * 8 + i];
+        half8 a0 = A[0], a1 = A[64];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
+#pragma unroll
+        for (int cb = 0; cb < CB; cb++) {
+            const int blk = b_begin + st * CB + cb;
+            if (blk < b_end) {
+                const floatx16 seed = {sd[cb][0].x, sd[cb][0].y, sd[cb][0].z, sd[cb][0].w,
+                                       sd[cb][1].x, sd[cb][1].y, sd[cb][1].z, sd[cb][1].w,
+                                       sd[cb][2].x, sd[cb][2].y, sd[cb][2].z, sd[cb][2].w,
+                                       sd[cb][3].x, sd[cb][3].y, sd[cb][3].z, sd[cb][3].w};
+                floatx16 acc0, acc1;
+#pragma unroll
+                for (int s = 0; s < S; s += 2) {
+                    half8 n0, n1;
+                    const bool more = s + 2 < S || cb + 1 < CB;
+                    if (s + 2 < S) {
+                        n0 = A[(cb * S + s + 2) * 64];
+                        n1 = A[(cb * S + s + 3) * 64];
+                    } else if (cb + 1 < CB) {  // next block of this stage: first pair
+                        n0 = A[((cb + 1) * S) * 64];
+                        n1 = A[((cb + 1) * S + 1) * 64];
+                    }
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq0[s], s == 0 ? seed : acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq1[s], s == 0 ? seed : acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bq0[s + 1], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bq1[s + 1], acc1, 0, 0, 0);
+                    // keep the next pair's reads ahead of this pair's MFMAs (hipcc re-clusters them otherwise)
+                    if (more) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                    if (more) {
+                        a0 = n0;
+                        a1 = n1;
+                    }
+                }
+                const int base = blk * 32;
+                scan_keys<L>(acc0, base, h, perm, lk0, li0);
+                scan_keys<L>(acc1, base, h, perm, lk1, li1);
+            }
+        }
+        dma_drain();      // this wave's pieces of the next stage landed
+        __syncthreads();  // everyone's landed; this stage's reads done
+    }
+#pragma unroll
+    for (int qb = 0; qb < 2; qb++) {
+        const int q = (qb0 + qb) * 32 + (lane & 31);
+        if (q < nq) {
+            const long o = (((long)q * nsplit + split) * 2 + h) * L;
+#pragma unroll
+            for (int i = 0; i < L; i++) {
+                out_key[o + i] = qb ? lk1[i] : lk0[i];
+                out_idx[o + i] = qb ? li1[i] : li0[i];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// 1'''. Shortlist on v_mfma_f32_16x16x32_f16.  Under load the chip holds a higher clock on the
+// 16x16x32 shape than on 32x32x16 at equal cycles per flop (MI355X_MICROARCH.md, DVFS item 7), so the
+// D=192 hot path runs on it.  16-row fragment layout (prep16_kernel): lane l of block b holds row
+// b*16 + (l & 15), k = s*32 + 8*(l >> 4) + j; the accumulator of lane l holds rows 4*(l >> 4) + i of
+// query column l & 15, i.e. each query's candidates are spread over 4 lanes (lane groups g = 0..3), and
+// perm16 puts the 4 mirror candidates of a tile into 4 different groups.  Wave = QB query blocks of 16.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int perm16(int r) { return ((r & 3) << 2) | (r >> 2); }
+
+struct Prep16Args {
+    const float *rows;
+    long n;
+    int d, S;       // S = k-steps of 32
+    float scale;
+    half8 *frag;    // [ceil(n/16)][S][64][8]
+    float *seed;    // dataset: [ceil(n/16)][16] -||c||^2/2 by A row (-inf on padding rows); queries: null
+    int perm;
+};
+
+__global__ __launch_bounds__(256) void prep16_kernel(Prep16Args a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
+    const long nblk = (a.n + 15) / 16;
+    for (long blk = (long)blockIdx.x * 4 + wave; blk < nblk; blk += (long)gridDim.x * 4) {
+        const long row = blk * 16 + (a.perm ? perm16(r) : r);
+        const bool valid = row < a.n;
+        double s2 = 0;
+        for (int s = 0; s < a.S; s++) {
+            half8 hv;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int k = s * 32 + 8 * g + j;
+                const float v = (valid && k < a.d) ? a.rows[row * a.d + k] : 0.0f;
+                const float vs = v * a.scale;
+                _Float16 vh = (_Float16)vs;
+                if (fabsf((float)vh) < 6.103515625e-05f) vh = (_Float16)0.0f;  // as prep_rows_kernel
+                hv[j] = vh;
+                s2 += (double)vs * (double)vs;
+            }
+            a.frag[(blk * a.S + s) * 64 + lane] = hv;
+        }
+        if (a.seed) {
+            s2 += __shfl_xor(s2, 16, 64);
+            s2 += __shfl_xor(s2, 32, 64);
+            if (g == 0) a.seed[blk * 16 + r] = valid ? -0.5f * (float)s2 : -INFINITY;
+        }
+    }
+}
+
+template <int S, int L, int CB, int NW, int QB>
+__global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 *__restrict__ cfrag,
+                                                                const float *__restrict__ cseed, int nblk,
+                                                                const half8 *__restrict__ qfrag, int nq,
+                                                                int blk_per_split, int nsplit, int perm,
+                                                                float *__restrict__ out_key,
+                                                                int *__restrict__ out_idx) {
+    typedef float floatx4 __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int FRAG_BYTES = CB * S * 1024;
+    constexpr int BUF_BYTES = FRAG_BYTES + CB * 64;
+    constexpr int NT = NW * 64;
+    constexpr int PER_T = CB * S * 64 / NT;
+    static_assert((CB * S * 64) % NT == 0 && S % 2 == 0, "stage must split evenly over the workgroup");
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+    const int nqblk = (nq + 15) / 16;
+    const int qb0 = (blockIdx.x * NW + w) * QB;
+    const int split = blockIdx.y;
+    const int b_begin = split * blk_per_split;
+    const int b_end = min(nblk, b_begin + blk_per_split);
+
+    half8 bq[QB][S];
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+        const long qq = min(qb0 + q, nqblk - 1);  // blocks past the end: clamped duplicate, never written
+#pragma unroll
+        for (int s = 0; s < S; s++) bq[q][s] = qfrag[(qq * S + s) * 64 + lane];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see nn_shortlist2_kernel
+    float lk[QB][L];
+    int li[QB][L];
+#pragma unroll
+    for (int q = 0; q < QB; q++)
+#pragma unroll
+        for (int i = 0; i < L; i++) {
+            lk[q][i] = INFINITY;
+            li[q][i] = -1;
+        }
+    // candidate index of accumulator element i of this lane, relative to the block
+    int rel[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) rel[i] = perm ? perm16(4 * g + i) : 4 * g + i;
+
+    const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
+    auto issue = [&](int st, int buf) {
+        const int blk0 = b_begin + st * CB;
+        const int nb = min(CB, b_end - blk0);
+        const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64 + w * 64 + lane;
+        char *dst = smem + buf * BUF_BYTES + w * 1024;
+        if (nb == CB) {
+#pragma unroll
+            for (int j = 0; j < PER_T; j++) glds16_asm(src + j * NT, dst + j * NT * 16);
+        } else {
+            const int last = nb * S * 64 - 1 - (w * 64 + lane);
+#pragma unroll
+            for (int j = 0; j < PER_T; j++) glds16_asm(src + min(j * NT, last), dst + j * NT * 16);
+        }
+        if (w == 0 && lane < CB * 4)
+            glds16_asm(reinterpret_cast<const uint4 *>(cseed) + (long)blk0 * 4 + min(lane, nb * 4 - 1),
+                       smem + buf * BUF_BYTES + FRAG_BYTES);
+    };
+
+    if (nstage > 0) issue(0, 0);
+    dma_drain();
+    __syncthreads();
+    for (int st = 0; st < nstage; st++) {
+        const char *B = smem + (st & 1) * BUF_BYTES;
+        const half8 *A = reinterpret_cast<const half8 *>(B) + lane;
+        const floatx4 *SD = reinterpret_cast<const floatx4 *>(B + FRAG_BYTES) + g;
+        floatx4 sd[CB];
+#pragma unroll
+        for (int cb = 0; cb < CB; cb++) sd[cb] = SD[cb * 4];
+        half8 a0 = A[0], a1 = A[64];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
+#pragma unroll
+        for (int cb = 0; cb < CB; cb++) {
+            const int blk = b_begin + st * CB + cb;
+            if (blk < b_end) {
+                floatx4 acc[QB];
+#pragma unroll
+                for (int s = 0; s < S; s += 2) {
+                    half8 n0, n1;
+                    const bool more = s + 2 < S || cb + 1 < CB;
+                    if (s + 2 < S) {
+                        n0 = A[(cb * S + s + 2) * 64];
+                        n1 = A[(cb * S + s + 3) * 64];
+                    } else if (cb + 1 < CB) {
+                        n0 = A[((cb + 1) * S) * 64];
+                        n1 = A[((cb + 1) * S + 1) * 64];
+                    }
+#pragma unroll
+                    for (int q = 0; q < QB; q++)
+                        acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bq[q][s], s == 0 ? sd[cb] : acc[q], 0, 0, 0);
+#pragma unroll
+                    for (int q = 0; q < QB; q++)
+                        acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bq[q][s + 1], acc[q], 0, 0, 0);
+                    if (more) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2 * QB, 0);
+                    if (more) {
+                        a0 = n0;
+                        a1 = n1;
+                    }
+                }
+                // epilogue: acc = q.c - ||c||^2/2, key = -2 acc; one wave-uniform branch per block
+                bool need = false;
+#pragma unroll
+                for (int q = 0; q < QB; q++) {
+                    const float m = fmaxf(fmaxf(acc[q][0], acc[q][1]), fmaxf(acc[q][2], acc[q][3]));
+                    need |= m > -0.5f * lk[q][L - 1];
+                }
+                if (__builtin_expect(__any(need), 0)) {
+                    const int base = blk * 16;
+#pragma unroll
+                    for (int q = 0; q < QB; q++)
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            if (acc[q][i] > -0.5f * lk[q][L - 1])
+                                list_insert<L>(lk[q], li[q], -2.0f * acc[q][i], base + rel[i]);
+                }
+            }
+        }
+        dma_drain();
+        __syncthreads();
+    }
+    // partial lists: [q][split][g][L]
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+        const int qq = (qb0 + q) * 16 + (lane & 15);
+        if (qq < nq) {
+            const long o = (((long)qq * nsplit + split) * 4 + g) * L;
+#pragma unroll
+            for (int i = 0; i < L; i++) {
+                out_key[o + i] = lk[q][i];
+                out_idx[o + i] = li[q][i];
             }
         }
     }
@@ -535,18 +871,28 @@ __global__ __launch_bounds__(256, 2) void nn_collect_kernel(const half8 *__restr
                     acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq1[s], acc1, 0, 0, 0);
                 }
                 const float *np = reinterpret_cast<const float *>(B + FRAG_BYTES) + cb * 32 + h * 16;
+                // one slot reservation per lane and block (not one returning atomic per candidate)
+                unsigned m0 = 0, m1 = 0;
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
                     const float nc = np[r];
-                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const int idx = blk * 32 + (perm ? row_perm(row) : row);
-                    if (fmaf(-2.0f, acc0[r], nc) <= t0) {
-                        const int p = atomicAdd(&ccnt[j0], 1);
-                        if (p < cap) cbuf[(long)j0 * cap + p] = idx;
+                    m0 |= (fmaf(-2.0f, acc0[r], nc) <= t0) ? 1u << r : 0u;
+                    m1 |= (fmaf(-2.0f, acc1[r], nc) <= t1) ? 1u << r : 0u;
+                }
+                int p0 = m0 ? atomicAdd(&ccnt[j0], __popc(m0)) : 0;
+                int p1 = m1 ? atomicAdd(&ccnt[j1], __popc(m1)) : 0;
+                while (m0 | m1) {
+                    if (m0) {
+                        const int r = __ffs(m0) - 1, row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (p0 < cap) cbuf[(long)j0 * cap + p0] = blk * 32 + (perm ? row_perm(row) : row);
+                        p0++;
+                        m0 &= m0 - 1;
                     }
-                    if (fmaf(-2.0f, acc1[r], nc) <= t1) {
-                        const int p = atomicAdd(&ccnt[j1], 1);
-                        if (p < cap) cbuf[(long)j1 * cap + p] = idx;
+                    if (m1) {
+                        const int r = __ffs(m1) - 1, row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (p1 < cap) cbuf[(long)j1 * cap + p1] = blk * 32 + (perm ? row_perm(row) : row);
+                        p1++;
+                        m1 &= m1 - 1;
                     }
                 }
             }
@@ -566,6 +912,7 @@ struct RescoreArgs {
     const float *key;
     const int *idx;
     int n, d, nq, k, L, nsplit;
+    int lpq;             // lanes (partial lists) per query and split: 2 (32x32 shortlist) or 4 (16x16)
     double N, H, Ec, max_abs_c;
     int ds_int;
     int *out_idx;
@@ -584,7 +931,33 @@ struct RescoreArgs {
     uint8_t *m_hm, *m_vm;
 };
 
+// D = 192 (the FrameTiling descriptor): fully unrolled so every load is issued up front and only the
+// reference's dependent add chain remains (the runtime-d loop below waits on a load per 4 terms)
+__device__ __forceinline__ float exact_dist192(const float *__restrict__ q, const float *__restrict__ c) {
+    const float4 *q4 = reinterpret_cast<const float4 *>(q), *c4 = reinterpret_cast<const float4 *>(c);
+    float dist = 0.0f;
+#pragma unroll
+    for (int h = 0; h < 4; h++) {  // 4 chunks of 12 float4 each: loads of a chunk issued together
+        float4 qa[12], ca[12];
+#pragma unroll
+        for (int i = 0; i < 12; i++) {
+            qa[i] = q4[h * 12 + i];
+            ca[i] = c4[h * 12 + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 12; i++) {
+            float t;
+            t = qa[i].x - ca[i].x; dist = dist + t * t;
+            t = qa[i].y - ca[i].y; dist = dist + t * t;
+            t = qa[i].z - ca[i].z; dist = dist + t * t;
+            t = qa[i].w - ca[i].w; dist = dist + t * t;
+        }
+    }
+    return dist;
+}
+
 __device__ __forceinline__ float exact_dist(const float *__restrict__ q, const float *__restrict__ c, int d) {
+    if (d == 192) return exact_dist192(q, c);
     float dist = 0.0f;
     int i = 0;
     if ((d & 3) == 0) {
@@ -630,7 +1003,7 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
     const int lane = threadIdx.x & 63;
     const long q = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= a.nq) return;
-    const int E = a.nsplit * 2 * a.L;
+    const int E = a.nsplit * a.lpq * a.L;  // list entries per query
     float key = INFINITY;
     int idx = -1;
     if (lane < E) {
@@ -670,10 +1043,10 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
         // key error bound: fp32 rounding of ||c||^2, the MFMA accumulation seeded with
         // -||c||^2/2 (>= 2x gamma_{D+1} over |seed| + sum |q^_d c^_d|), and the fp16 residuals
         const double gam = 2.0 * (a.d + 1) * u;
-        const double E = 1.05 * (2.0 * u * a.N * a.N + gam * (a.N * a.N + 2.0 * st.hn * a.H) +
-                                 2.0 * (st.en * a.N + st.hn * a.Ec)) + 1e-30;
+        const double Ek = 1.05 * (2.0 * u * a.N * a.N + gam * (a.N * a.N + 2.0 * st.hn * a.H) +
+                                  2.0 * (st.en * a.N + st.hn * a.Ec)) + 1e-30;
         const double g = (double)(a.d + 4) * u / (1.0 - (double)(a.d + 4) * u) * 1.05;
-        T = ((st.n2 + (double)kk + E) * (1.0 + g) / (1.0 - g)) - st.n2 + E;
+        T = ((st.n2 + (double)kk + Ek) * (1.0 + g) / (1.0 - g)) - st.n2 + Ek;
         T += 1e-12 * (st.n2 + fabs((double)kk)) + 1e-30;
         (void)nq;
     }
@@ -906,7 +1279,8 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, hipStream_t stream) {
     ix->perm = all_int ? 0 : 1;
     TILER_HIP_CHECK_NULL(hipMalloc(&ix->d_frag, (size_t)ix->nblk * ix->S * 64 * 16));
     TILER_HIP_CHECK_NULL(hipMalloc((void **)&ix->d_nc, (size_t)ix->nblk * 32 * sizeof(float)));
-    PrepArgs pa{d_rows, n, d, ix->S, scale, (half8 *)ix->d_frag, ix->d_nc, nullptr, d_ds, ix->perm};
+    TILER_HIP_CHECK_NULL(hipMalloc((void **)&ix->d_seed, (size_t)ix->nblk * 32 * sizeof(float)));
+    PrepArgs pa{d_rows, n, d, ix->S, scale, (half8 *)ix->d_frag, ix->d_nc, ix->d_seed, nullptr, d_ds, ix->perm};
     hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)std::min<long>(4096, (ix->nblk + 3) / 4)), dim3(256), 0,
                        stream, pa);
     TILER_HIP_CHECK_NULL(hipGetLastError());
@@ -927,6 +1301,17 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, hipStream_t stream) {
     ix->max_abs = maxabs;
     ix->exact_int = (ds.not_int == 0) && scale == 1.0f && maxabs <= 2048.0;
     if (ds.bad) ix->S = 0;  // non-finite / out-of-range data: exhaustive path only
+    if (ix->S > 0 && ix->perm && (d + 31) / 32 == 6) {
+        ix->S16 = 6;
+        ix->nblk16 = (int)((n + 15) / 16);
+        TILER_HIP_CHECK_NULL(hipMalloc(&ix->d_frag16, (size_t)ix->nblk16 * ix->S16 * 1024));
+        TILER_HIP_CHECK_NULL(hipMalloc((void **)&ix->d_seed16, (size_t)ix->nblk16 * 16 * sizeof(float)));
+        Prep16Args p16{d_rows, n, d, ix->S16, scale, (half8 *)ix->d_frag16, ix->d_seed16, 1};
+        hipLaunchKernelGGL(prep16_kernel, dim3((unsigned)std::min<long>(4096, (ix->nblk16 + 3) / 4)), dim3(256), 0,
+                           stream, p16);
+        TILER_HIP_CHECK_NULL(hipGetLastError());
+        TILER_HIP_CHECK_NULL(hipStreamSynchronize(stream));
+    }
     return ix;
 }
 
@@ -935,11 +1320,15 @@ void nn_index_destroy(NNIndex *ix) {
     hipFree(ix->d_rows);
     hipFree(ix->d_frag);
     hipFree(ix->d_nc);
+    hipFree(ix->d_seed);
+    hipFree(ix->d_frag16);
+    hipFree(ix->d_seed16);
     hipFree(ix->d_tr_tile);
     hipFree(ix->d_tr_pal);
     hipFree(ix->d_tr_attr);
     SearchScratch &s = ix->scratch;
     hipFree(s.qfrag);
+    hipFree(s.qfrag16);
     hipFree(s.qstat);
     hipFree(s.key);
     hipFree(s.idx);
@@ -961,6 +1350,7 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
     SearchScratch &s = ix->scratch;
     if ((size_t)nq > s.cap_q) {
         hipFree(s.qfrag);
+        hipFree(s.qfrag16);
         hipFree(s.qstat);
         hipFree(s.fb_list);
         hipFree(s.fb_count);
@@ -968,6 +1358,7 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         hipFree(s.ex_list);
         const long nqblk = (nq + 31) / 32 + 2;
         TILER_HIP_CHECK(hipMalloc(&s.qfrag, (size_t)nqblk * 16 * 64 * 16));
+        TILER_HIP_CHECK(hipMalloc(&s.qfrag16, (size_t)((nq + 15) / 16 + 2) * 8 * 64 * 16));
         TILER_HIP_CHECK(hipMalloc((void **)&s.qstat, (size_t)nq * sizeof(QStat)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.fb_list, (size_t)nq * sizeof(int)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.fb_count, 16));
@@ -1023,23 +1414,61 @@ static void launch_shortlist4(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
                        ix->scratch.key, ix->scratch.idx);
 }
 
-// D=192 shortlist variant (A/B switch TILER_SHORTLIST for measurements):
-//   "w8" (default): 8 waves x 2 query blocks, 2 waves per SIMD (63 ms / C3 keyframe, 49.6 % of peak)
-//   "w4": 4 waves x 2 query blocks (67 ms);  "w1": one wave per SIMD, 3 query blocks per wave with the
-//   epilogue interleaved (nn_shortlist4_kernel, 89 ms: hipcc's schedule of the 512-register body loses)
+// D=192 shortlist variant (A/B switch TILER_SHORTLIST for measurements; C3 keyframe, one box):
+//   "q16" (default): nn_shortlist16_kernel, 16x16x32 MFMA, L16 = 4 (51.6 ms); "q16l6": L16 = 6 (53.4 ms,
+//   fewer tier-2 queries); "p4"/"p2": nn_shortlist2_kernel, 32x32x16, pipelined LDS reads, CB = 4/2
+//   (-6 % vs w8); "w8": nn_shortlist_kernel, 8 waves x 2 query blocks (63.9 ms); "w4": 4 waves (+5 %);
+//   "w1": one wave per SIMD, 3 query blocks per wave (nn_shortlist4_kernel, +40 %)
 static int shortlist_variant() {
     static int v = [] {
         const char *e = getenv("TILER_SHORTLIST");
         if (e && !strcmp(e, "w1")) return 1;
         if (e && !strcmp(e, "w4")) return 4;
-        return 8;
+        if (e && !strcmp(e, "p2")) return 102;
+        if (e && !strcmp(e, "p4")) return 104;
+        if (e && !strcmp(e, "w8")) return 8;
+        if (e && !strcmp(e, "q16l6")) return 166;
+        return 16;
     }();
     return v;
 }
 
 static int shortlist_queries_per_wg(int S) {
     if (S != 12) return 256;
-    return shortlist_variant() == 8 ? 512 : shortlist_variant() == 4 ? 256 : 128 * SL4_QB;
+    const int v = shortlist_variant();
+    return (v == 8 || v > 100) ? 512 : v == 4 ? 256 : 128 * SL4_QB;
+}
+
+template <int S, int L, int CB, int NW>
+static void launch_shortlist2(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
+    const int nqblk = (nq + 31) / 32;
+    const dim3 grid((nqblk + 2 * NW - 1) / (2 * NW), nsplit);
+    const size_t lds = 2 * (CB * S * 1024 + CB * 128);
+    KTimer tm("nn_shortlist", stream);
+    hipLaunchKernelGGL((nn_shortlist2_kernel<S, L, CB, NW>), grid, dim3(NW * 64), lds, stream,
+                       (const half8 *)ix->d_frag, ix->d_seed, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps,
+                       nsplit, ix->perm, ix->scratch.key, ix->scratch.idx);
+}
+
+// 16x16x32 shortlist for D = 161..192 float datasets: TILER_SHORTLIST=q16 (L16 = 4) / q16l6 (L16 = 6);
+// returns L16, or 0 for the 32x32x16 kernels
+static constexpr int SL16_NW = 8, SL16_QB = 4, SL16_CB = 8;
+static int shortlist16_L() {
+    const int v = shortlist_variant();
+    return v == 16 ? 4 : v == 166 ? 6 : 0;
+}
+
+template <int S, int L>
+static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
+    const int nqblk = (nq + 15) / 16;
+    const dim3 grid((nqblk + SL16_NW * SL16_QB - 1) / (SL16_NW * SL16_QB), nsplit);
+    const size_t lds = 2 * (SL16_CB * S * 1024 + SL16_CB * 64);
+    KTimer tm("nn_shortlist", stream);
+    hipLaunchKernelGGL((nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB>), grid, dim3(SL16_NW * 64), lds, stream,
+                       (const half8 *)ix->d_frag16, ix->d_seed16, ix->nblk16, (const half8 *)ix->scratch.qfrag16, nq,
+                       bps, nsplit, ix->perm, ix->scratch.key, ix->scratch.idx);
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 template <int L>
@@ -1048,7 +1477,11 @@ static int dispatch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
         case 4: launch_shortlist<4, L, 6, 4>(ix, nq, nsplit, bps, stream); break;
         case 8: launch_shortlist<8, L, 3, 4>(ix, nq, nsplit, bps, stream); break;
         case 12:
-            if (shortlist_variant() == 8)
+            if (shortlist_variant() == 102)
+                launch_shortlist2<12, L, 2, 8>(ix, nq, nsplit, bps, stream);
+            else if (shortlist_variant() == 104)
+                launch_shortlist2<12, L, 4, 8>(ix, nq, nsplit, bps, stream);
+            else if (shortlist_variant() == 8)
                 launch_shortlist<12, L, 2, 8>(ix, nq, nsplit, bps, stream);
             else if (shortlist_variant() == 4)
                 launch_shortlist<12, L, 2, 4>(ix, nq, nsplit, bps, stream);
@@ -1064,9 +1497,11 @@ static int dispatch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
 
 template <int S, int CB>
 static void launch_collect(NNIndex *ix, int nq, hipStream_t stream) {
-    const int nsplit = std::min(ix->nblk, 64);
+    // fixed grid (the overflow count stays on the device): many short splits so that a few hundred
+    // overflowed queries still spread over the whole chip
+    const int nsplit = std::min(ix->nblk, 256);
     const int bps = (ix->nblk + nsplit - 1) / nsplit;
-    const int groups = std::min(64, (std::min(nq, TIER2_MAX) + 255) / 256);
+    const int groups = std::min(32, (std::min(nq, TIER2_MAX) + 255) / 256);
     const size_t lds = 2 * (CB * S * 1024 + CB * 128);
     SearchScratch &s = ix->scratch;
     KTimer tm("nn_collect", stream);
@@ -1145,31 +1580,53 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         ra.ex_list = nullptr;
         return launch_exact(ra, nq, std::min(nq, 4096), stream);
     }
-    const int L = 8;  // >= 2x the 4-way mirror near-ties of one tile per lane (row_perm spreads them 2+2)
-    const int max_split = 64 / (2 * L);
-    const int wgs = (nq + shortlist_queries_per_wg(ix->S) - 1) / shortlist_queries_per_wg(ix->S);
+    // 32x32x16 shortlist: 2 lanes x L = 8 per query (>= 2x the 4-way mirror near-ties of one tile per
+    // lane, row_perm spreads them 2+2); 16x16x32: 4 lanes x L16 (perm16 spreads them 1 per lane)
+    const int v16 = ix->S16 > 0 ? shortlist16_L() : 0;
+    const int L = v16 ? v16 : 8;
+    const int lpq = v16 ? 4 : 2;
+    const int nblk = v16 ? ix->nblk16 : ix->nblk;
+    const int max_split = 64 / (lpq * L);
+    const int qpwg = v16 ? SL16_NW * SL16_QB * 16 : shortlist_queries_per_wg(ix->S);
+    const int wgs = (nq + qpwg - 1) / qpwg;
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
-    nsplit = std::min(nsplit, ix->nblk);
-    const int bps = (ix->nblk + nsplit - 1) / nsplit;
-    nsplit = (ix->nblk + bps - 1) / bps;
+    nsplit = std::min(nsplit, nblk);
+    const int bps = (nblk + nsplit - 1) / nsplit;
+    nsplit = (nblk + bps - 1) / bps;
     ix->last_splits = nsplit;
-    if (ensure_scratch(ix, nq, (long)nq * nsplit * 2 * L)) return -1;
+    if (ensure_scratch(ix, nq, (long)nq * nsplit * lpq * L)) return -1;
     SearchScratch &s = ix->scratch;
     TILER_HIP_CHECK(hipMemsetAsync(s.fb_count, 0, 16, stream));
     // queries -> fragments (same layout and scale as the dataset)
     const long nqblk = (nq + 31) / 32;
-    PrepArgs pa{d_q, nq, ix->d, ix->S, ix->scale, (half8 *)s.qfrag, nullptr, s.qstat, nullptr, 0};
+    PrepArgs pa{d_q, nq, ix->d, ix->S, ix->scale, (half8 *)s.qfrag, nullptr, nullptr, s.qstat, nullptr, 0};
     {
         KTimer t_prep("nn_prep", stream);
         hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)std::min<long>(4096, (nqblk + 3) / 4)), dim3(256), 0,
                            stream, pa);
     }
     TILER_HIP_CHECK(hipGetLastError());
-    if (dispatch_shortlist<L>(ix, nq, nsplit, bps, stream)) return -1;
+    if (v16) {
+        Prep16Args p16{d_q, nq, ix->d, ix->S16, ix->scale, (half8 *)s.qfrag16, nullptr, 0};
+        {
+            KTimer t_prep("nn_prep", stream);
+            hipLaunchKernelGGL(prep16_kernel, dim3((unsigned)std::min<long>(4096, ((nq + 15) / 16 + 3) / 4)),
+                               dim3(256), 0, stream, p16);
+        }
+        TILER_HIP_CHECK(hipGetLastError());
+        if (v16 == 6) {
+            if (launch_shortlist16<6, 6>(ix, nq, nsplit, bps, stream)) return -1;
+        } else {
+            if (launch_shortlist16<6, 4>(ix, nq, nsplit, bps, stream)) return -1;
+        }
+    } else if (dispatch_shortlist<8>(ix, nq, nsplit, bps, stream)) {
+        return -1;
+    }
     ra.qstat = s.qstat;
     ra.key = s.key;
     ra.idx = s.idx;
     ra.L = L;
+    ra.lpq = lpq;
     ra.nsplit = nsplit;
     ra.fb_list = s.fb_list;
     ra.fb_count = s.fb_count;

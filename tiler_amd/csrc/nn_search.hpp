@@ -35,6 +35,7 @@ struct SearchScratch {
     int *fb_list = nullptr;
     int *fb_count = nullptr;  // [2]: count, pad
     float *qrows = nullptr;   // fp32 query rows (frame-tiling path: descriptors)
+    void *qfrag16 = nullptr;  // query fragments, 16-row layout
     float *thr = nullptr;     // tier-2 thresholds [nq]
     int *ex_list = nullptr;   // tier-3 list [nq]
     int *ccnt = nullptr;      // tier-2 collect counts
@@ -51,6 +52,11 @@ struct NNIndex {
     float *d_rows = nullptr;    // [n][d] fp32 (exact rescoring)
     void *d_frag = nullptr;     // [nblk][S][64][8] fp16, MFMA A-operand fragment order
     float *d_nc = nullptr;      // [nblk][32] ||c||^2 in accumulator-row order (+inf on padding rows)
+    float *d_seed = nullptr;    // [nblk][32] -||c||^2/2, same order (-inf on padding rows)
+    // 16-row layout for the 16x16x32 shortlist (float datasets of 161..192 dims; S16 = 0 if absent)
+    int S16 = 0, nblk16 = 0;
+    void *d_frag16 = nullptr;   // [nblk16][S16][64][8] fp16
+    float *d_seed16 = nullptr;  // [nblk16][16] -||c||^2/2 by A row
     int32_t *d_tr_tile = nullptr, *d_tr_pal = nullptr;
     uint8_t *d_tr_attr = nullptr;
     SearchScratch scratch;

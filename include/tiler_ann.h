@@ -60,6 +60,9 @@ typedef struct {
     int64_t exhaustive_queries; /* tier 3: exhaustive reference-order scan (k > 8, bad data, collect overflow) */
     int32_t exact_integer;    /* 1 when the dataset is small integers: MFMA keys are exact */
     int32_t splits;           /* candidate splits used by the last launch */
+    int64_t orbit_groups;     /* mirror orbits found in the dataset (0: mirror-orbit path unavailable) */
+    int32_t orbit_search;     /* 1 when the last search ran the mirror-orbit shortlist */
+    int32_t reserved;
 } tiler_search_stats;
 int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
 

@@ -27,7 +27,8 @@ class TilerError(RuntimeError):
 
 class SearchStats(ctypes.Structure):
     _fields_ = [("queries", ctypes.c_int64), ("fallback_queries", ctypes.c_int64),
-                ("exhaustive_queries", ctypes.c_int64), ("exact_integer", ctypes.c_int32), ("splits", ctypes.c_int32)]
+                ("exhaustive_queries", ctypes.c_int64), ("exact_integer", ctypes.c_int32), ("splits", ctypes.c_int32),
+                ("orbit_groups", ctypes.c_int64), ("orbit_search", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 _SIGS = {

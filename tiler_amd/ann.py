@@ -95,4 +95,5 @@ class KDTree:
         s = SearchStats()
         check(self._lib.ann_kdtree_get_stats(self.handle, ctypes.byref(s)), "ann_kdtree_get_stats")
         return {"queries": s.queries, "fallback_queries": s.fallback_queries,
-                "exhaustive_queries": s.exhaustive_queries, "exact_integer": s.exact_integer, "splits": s.splits}
+                "exhaustive_queries": s.exhaustive_queries, "exact_integer": s.exact_integer, "splits": s.splits,
+                "orbit_groups": s.orbit_groups, "orbit_search": s.orbit_search}

@@ -15,6 +15,7 @@
 #include "../../include/tiler_ann.h"
 #include "kmodes.hpp"
 #include "nn_search.hpp"
+#include "orbit.hpp"
 #include "psyv.hpp"
 #include "smooth.hpp"
 
@@ -360,6 +361,9 @@ int ann_kdtree_get_stats(ann_kdtree *t, tiler_search_stats *out) {
     out->exhaustive_queries = t->ix->last_splits > 0 ? t->ix->h_fb_count[1] : t->ix->last_fallback;
     out->exact_integer = t->ix->exact_int ? 1 : 0;
     out->splits = t->ix->last_splits;
+    out->orbit_groups = t->ix->orbit ? orbit_groups(t->ix) : 0;
+    out->orbit_search = t->ix->last_orbit;
+    out->reserved = 0;
     return 0;
 }
 

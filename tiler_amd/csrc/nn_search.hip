@@ -24,14 +24,13 @@
 #include <algorithm>
 
 #include "nn_search.hpp"
+#include "nn_dev.hpp"
+#include "orbit.hpp"
 #include "psyv.hpp"
 
 #pragma clang fp contract(off)
 
 namespace tiler {
-
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 enum { QF_INT = 1, QF_BAD = 2 };
 
@@ -58,10 +57,6 @@ struct PrepArgs {
 // the two half-waves.  Involution; identity for exact-integer datasets (arrival order = index order).
 __device__ __forceinline__ int row_perm(int i) { return (i & ~5) | ((i & 1) << 2) | ((i >> 2) & 1); }
 
-__device__ __forceinline__ double wave_max_d(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
-}
 
 __global__ __launch_bounds__(256) void prep_rows_kernel(PrepArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
@@ -150,40 +145,6 @@ __global__ __launch_bounds__(256) void maxabs_kernel(const float *rows, long tot
 // 1. MFMA shortlist.  Workgroup = 4 waves; wave = 2 query blocks of 32 (64 queries); the
 // candidate blocks of this split stream through a double-buffered LDS ring (CB blocks/stage).
 // ------------------------------------------------------------------------------------------
-// one 16-byte LDS-DMA piece per lane: LDS destination = wave-uniform base + lane * 16
-__device__ __forceinline__ void glds16(const uint4 *gsrc, char *lds_wave_base) {
-    typedef __attribute__((address_space(1))) void gvoid;
-    typedef __attribute__((address_space(3))) void lvoid;
-    __builtin_amdgcn_global_load_lds((gvoid *)(gsrc), (lvoid *)(lds_wave_base), 16, 0, 0);
-}
-
-// The same DMA as inline asm, invisible to hipcc's waitcnt pass: the compiler counts a pending
-// global_load_lds as an LGKM event of another kind, which makes every later LDS-read wait an
-// lgkmcnt(0) (no read can stay in flight behind an MFMA).  Users drain it themselves: dma_drain()
-// before the barrier that publishes the stage.
-__device__ __forceinline__ void glds16_asm(const uint4 *gsrc, char *lds_wave_base) {
-    const unsigned lds = __builtin_amdgcn_readfirstlane(
-        (unsigned)(size_t)(__attribute__((address_space(3))) char *)lds_wave_base);
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(gsrc), "{m0}"(lds) : "memory");
-}
-__device__ __forceinline__ void dma_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-template <int L>
-__device__ __forceinline__ void list_insert(float (&k)[L], int (&id)[L], float x, int ix) {
-#pragma unroll
-    for (int i = L - 1; i > 0; --i) {
-        const bool gp = k[i - 1] > x, gc = k[i] > x;
-        const float nk = gp ? k[i - 1] : (gc ? x : k[i]);
-        const int ni = gp ? id[i - 1] : (gc ? ix : id[i]);
-        k[i] = nk;
-        id[i] = ni;
-    }
-    if (k[0] > x) {
-        k[0] = x;
-        id[0] = ix;
-    }
-}
-
 // acc was seeded with -||c||^2/2, so acc = q.c - ||c||^2/2 and key = ||c||^2 - 2 q.c = -2 acc (exact
 // scaling): the epilogue is a max tree plus one compare per 16 values, no per-value FMA.
 template <int L>
@@ -931,65 +892,6 @@ struct RescoreArgs {
     uint8_t *m_hm, *m_vm;
 };
 
-// D = 192 (the FrameTiling descriptor): fully unrolled so every load is issued up front and only the
-// reference's dependent add chain remains (the runtime-d loop below waits on a load per 4 terms)
-__device__ __forceinline__ float exact_dist192(const float *__restrict__ q, const float *__restrict__ c) {
-    const float4 *q4 = reinterpret_cast<const float4 *>(q), *c4 = reinterpret_cast<const float4 *>(c);
-    float dist = 0.0f;
-#pragma unroll
-    for (int h = 0; h < 4; h++) {  // 4 chunks of 12 float4 each: loads of a chunk issued together
-        float4 qa[12], ca[12];
-#pragma unroll
-        for (int i = 0; i < 12; i++) {
-            qa[i] = q4[h * 12 + i];
-            ca[i] = c4[h * 12 + i];
-        }
-#pragma unroll
-        for (int i = 0; i < 12; i++) {
-            float t;
-            t = qa[i].x - ca[i].x; dist = dist + t * t;
-            t = qa[i].y - ca[i].y; dist = dist + t * t;
-            t = qa[i].z - ca[i].z; dist = dist + t * t;
-            t = qa[i].w - ca[i].w; dist = dist + t * t;
-        }
-    }
-    return dist;
-}
-
-__device__ __forceinline__ float exact_dist(const float *__restrict__ q, const float *__restrict__ c, int d) {
-    if (d == 192) return exact_dist192(q, c);
-    float dist = 0.0f;
-    int i = 0;
-    if ((d & 3) == 0) {
-        const float4 *q4 = reinterpret_cast<const float4 *>(q), *c4 = reinterpret_cast<const float4 *>(c);
-        for (; i < d / 4; i++) {
-            const float4 a = q4[i], b = c4[i];
-            float t;
-            t = a.x - b.x; dist = dist + t * t;
-            t = a.y - b.y; dist = dist + t * t;
-            t = a.z - b.z; dist = dist + t * t;
-            t = a.w - b.w; dist = dist + t * t;
-        }
-        return dist;
-    }
-    for (; i < d; i++) {
-        const float t = q[i] - c[i];
-        dist = dist + t * t;
-    }
-    return dist;
-}
-
-// lexicographic (v, i) wave minimum
-__device__ __forceinline__ void wave_argmin(float &v, int &i) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(v, o, 64);
-        const int oi = __shfl_xor(i, o, 64);
-        const bool take = (ov < v) || (ov == v && (unsigned)oi < (unsigned)i);
-        v = take ? ov : v;
-        i = take ? oi : i;
-    }
-}
-
 __device__ __forceinline__ void write_map(const RescoreArgs &a, long q, int best) {
     if (!a.m_tile) return;
     a.m_tile[q] = best >= 0 ? a.tr_tile[best] : -1;
@@ -1096,9 +998,6 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
 // 2b. tier-2 rescore: every collected candidate (key <= T) rescored exactly; top-k by (dist, index).
 // One wave per compact query; a buffer that overflowed its capacity sends the query to tier 3.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool lex_less(float a, int ia, float b, int ib) {
-    return a < b || (a == b && (unsigned)ia < (unsigned)ib);
-}
 
 __global__ __launch_bounds__(256) void nn_rescore2_kernel(RescoreArgs a) {
     const int lane = threadIdx.x & 63;
@@ -1312,11 +1211,13 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, hipStream_t stream) {
         TILER_HIP_CHECK_NULL(hipGetLastError());
         TILER_HIP_CHECK_NULL(hipStreamSynchronize(stream));
     }
+    if (ix->S > 0 && orbit_build(ix, stream) < 0) return nullptr;
     return ix;
 }
 
 void nn_index_destroy(NNIndex *ix) {
     if (!ix) return;
+    orbit_destroy(ix->orbit);
     hipFree(ix->d_rows);
     hipFree(ix->d_frag);
     hipFree(ix->d_nc);
@@ -1542,6 +1443,8 @@ static int launch_exact(RescoreArgs ra, int list_n, int grid, hipStream_t stream
     return 0;
 }
 
+static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream);
+
 int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
                   hipStream_t stream) {
     if (nq <= 0) return 0;
@@ -1606,6 +1509,44 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
                            stream, pa);
     }
     TILER_HIP_CHECK(hipGetLastError());
+    ix->last_orbit = 0;
+    if (k == 1 && ix->orbit) {
+        // mirror-orbit path (orbit.hip): the generic query fragments above feed only the tier-2 pass
+        TILER_HIP_CHECK(hipMemsetAsync(s.ccnt, 0, (size_t)std::min(nq, TIER2_MAX) * sizeof(int), stream));
+        OrbitTail t{};
+        t.gqstat = s.qstat;
+        t.gN = ix->maxN;
+        t.gH = ix->maxH;
+        t.gEc = ix->maxE;
+        t.fb_list = s.fb_list;
+        t.fb_count = s.fb_count;
+        t.ex_list = s.ex_list;
+        t.ex_count = s.fb_count + 1;
+        t.fb_max = TIER2_MAX;
+        t.thr = s.thr;
+        t.out_idx = d_idx;
+        t.out_err = d_err;
+        t.tr_tile = ra.tr_tile;
+        t.tr_pal = ra.tr_pal;
+        t.tr_attr = ra.tr_attr;
+        t.m_tile = ra.m_tile;
+        t.m_pal = ra.m_pal;
+        t.m_hm = ra.m_hm;
+        t.m_vm = ra.m_vm;
+        if (orbit_search(ix, d_q, nq, t, stream)) return -1;
+        ix->last_orbit = 1;
+        ra.qstat = s.qstat;
+        ra.fb_list = s.fb_list;
+        ra.fb_count = s.fb_count;
+        ra.ex_list = s.ex_list;
+        ra.ex_count = s.fb_count + 1;
+        ra.thr = s.thr;
+        ra.ccnt = s.ccnt;
+        ra.cbuf = s.cbuf;
+        ra.cap = TIER2_CAP;
+        ra.fb_max = TIER2_MAX;
+        return search_tail(ix, ra, nq, stream);
+    }
     if (v16) {
         Prep16Args p16{d_q, nq, ix->d, ix->S16, ix->scale, (half8 *)s.qfrag16, nullptr, 0};
         {
@@ -1643,7 +1584,12 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         hipLaunchKernelGGL(nn_rescore_kernel, dim3((nq + 3) / 4), dim3(256), 0, stream, ra);
     }
     TILER_HIP_CHECK(hipGetLastError());
-    // tier 2 and tier 3 read their device-side counts: fixed grids, no host round trip
+    return search_tail(ix, ra, nq, stream);
+}
+
+// tiers 2 and 3 read their device-side counts: fixed grids, no host round trip
+static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream) {
+    SearchScratch &s = ix->scratch;
     if (dispatch_collect(ix, nq, stream)) return -1;
     {
         KTimer t_r2("nn_rescore2", stream);

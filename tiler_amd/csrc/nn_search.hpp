@@ -27,6 +27,8 @@ struct QStat {
     int pad;
 };
 
+struct OrbitIndex;  // orbit.hpp
+
 struct SearchScratch {
     void *qfrag = nullptr;
     QStat *qstat = nullptr;
@@ -63,6 +65,8 @@ struct NNIndex {
     std::mutex mu;
     long long last_queries = 0, last_fallback = 0;
     int last_splits = 0;
+    int last_orbit = 0;         // 1: the last search ran the mirror-orbit path
+    OrbitIndex *orbit = nullptr; // mirror-orbit index (orbit.hip), null when not applicable
     int *h_fb_count = nullptr;  // pinned
 };
 

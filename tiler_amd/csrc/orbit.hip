@@ -1,0 +1,906 @@
+// orbit.hip -- mirror-orbit FrameTiling search on gfx950 (see orbit.hpp for the algebra).
+//
+//   orbit_eq_kernel        device check: which of the next 3 candidates equal S_m row_j bit for bit
+//   (host)                 greedy grouping of consecutive candidates into orbits (base + mirror slots)
+//   orbit_prep_kernel      c' = U c_base (dataset) / q' = U' q (queries): fp64 transform -> fp16 MFMA
+//                          fragments + row-major fp16 + norms and rounding-error statistics
+//   nn_orbit_shortlist     v_mfma_f32_32x32x16_f16, 12 k-steps = 4 isotypic blocks of 3: per (query,
+//                          tile) four 48-d partial dots d_x in 4 accumulators (d_0 seeded with
+//                          -||c||^2/2).  u = d_0 + |d_1| + |d_2| + |d_3| bounds the 4 mirror values
+//                          q.(S_m c) - ||c||^2/2 from above; each lane keeps its L best 4-tile
+//                          sub-blocks by max u (key = -2u).
+//   nn_orbit_rescore       per query: re-key the kept sub-blocks from the fp16 rows, derive the exact
+//                          threshold from a real reference distance, rescore every candidate whose key
+//                          can reach it with the reference fp32 sequential distance, pick (dist, index).
+//                          A list that may have dropped a needed entry sends the query to the generic
+//                          tier-2 collect pass (nn_search.hip) with the threshold in its key domain.
+#include <float.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "nn_dev.hpp"
+#include "orbit.hpp"
+
+namespace tiler {
+
+static constexpr int OD = 192;  // descriptor dimension (cTileDCTSize, main.pas:44)
+static constexpr int OS = 12;   // k-steps of 16 (4 isotypic blocks x 3)
+
+// device copy of the transform: output coordinate o (block x = o / 48) = coef[o] * sum_t w[o][t] * v[src[o][t]]
+struct OrbitMap {
+    int16_t src[OD][4];
+    float w[OD][4];      // +-1, 0 beyond cnt
+    float cs[OD], qs[OD]; // dataset / query coefficient (cs * qs = 1 / orbit size)
+    int16_t msrc[3][OD];  // mirror m = 1, 2, 3 (H, V, HV): (S_m v)[i] = msgn[m-1][i] * v[msrc[m-1][i]]
+    float msgn[3][OD];
+};
+
+struct OrbitDsStat {
+    unsigned long long max_n2, max_p2, max_h2, max_e2;  // double bits (non-negative)
+    unsigned int bad, pad;
+};
+
+// ------------------------------------------------------------------------------------------
+// host: the signed permutations of the Haar layout and the isotypic basis
+// ------------------------------------------------------------------------------------------
+// structure replica of WaveletGS (main.pas:2805-2840) on one 8x8 component, dx = dy = 8, depth 2
+static void haar_host(const double *in, double *out) {
+    double cur[64];
+    memcpy(cur, in, sizeof(cur));
+    const double f = 1.0 / sqrt(2.0);
+    for (int dx = 8; dx >= 2; dx >>= 1) {
+        double tx[64], ty[64];
+        memcpy(tx, cur, sizeof(tx));
+        memcpy(ty, cur, sizeof(ty));
+        for (int y = 0; y < dx; y++)
+            for (int x = 0; x < dx / 2; x++) {
+                tx[y * 8 + x] = (cur[y * 8 + 2 * x] + cur[y * 8 + 2 * x + 1]) * f;
+                tx[y * 8 + x + dx / 2] = (cur[y * 8 + 2 * x] - cur[y * 8 + 2 * x + 1]) * f;
+            }
+        for (int x = 0; x < dx; x++)
+            for (int y = 0; y < dx / 2; y++) {
+                ty[y * 8 + x] = (tx[2 * y * 8 + x] + tx[(2 * y + 1) * 8 + x]) * f;
+                ty[(y + dx / 2) * 8 + x] = (tx[2 * y * 8 + x] - tx[(2 * y + 1) * 8 + x]) * f;
+            }
+        for (int y = 0; y < dx; y++)
+            for (int x = 0; x < dx; x++) cur[y * 8 + x] = ty[y * 8 + x];
+    }
+    memcpy(out, cur, sizeof(cur));
+}
+
+struct SPerm {
+    int src[OD];
+    int sgn[OD];
+};
+
+// S = T M T^T for the pixel mirror M (T = the orthonormal 3-level Haar), rounded to a signed permutation
+static bool mirror_sperm(int hm, int vm, SPerm &p) {
+    static double T[64][64];  // T[i][pix]
+    for (int pix = 0; pix < 64; pix++) {
+        double e[64] = {0}, o[64];
+        e[pix] = 1.0;
+        haar_host(e, o);
+        for (int i = 0; i < 64; i++) T[i][pix] = o[i];
+    }
+    for (int i = 0; i < 64; i++) {
+        int found = -1, sg = 0;
+        for (int j = 0; j < 64; j++) {
+            double s = 0;
+            for (int pix = 0; pix < 64; pix++) {
+                const int y = pix >> 3, x = pix & 7;
+                const int mp = (vm ? 7 - y : y) * 8 + (hm ? 7 - x : x);
+                s += T[i][pix] * T[j][mp];
+            }
+            if (fabs(s) > 1e-9) {
+                if (found >= 0 || fabs(fabs(s) - 1.0) > 1e-9) return false;
+                found = j;
+                sg = s > 0 ? 1 : -1;
+            }
+        }
+        if (found < 0) return false;
+        for (int c = 0; c < 3; c++) {
+            p.src[c * 64 + i] = c * 64 + found;
+            p.sgn[c * 64 + i] = sg;
+        }
+    }
+    return true;
+}
+
+static bool build_map(OrbitMap &m) {
+    SPerm g[4];
+    for (int i = 0; i < OD; i++) {
+        g[0].src[i] = i;
+        g[0].sgn[i] = 1;
+    }
+    if (!mirror_sperm(1, 0, g[1]) || !mirror_sperm(0, 1, g[2])) return false;
+    for (int i = 0; i < OD; i++) {  // HV = H o V: (S_H (S_V v))[i] = sH[i] sV[srcH[i]] v[srcV[srcH[i]]]
+        g[3].src[i] = g[2].src[g[1].src[i]];
+        g[3].sgn[i] = g[1].sgn[i] * g[2].sgn[g[1].src[i]];
+    }
+    memset(&m, 0, sizeof(m));
+    for (int mm = 1; mm < 4; mm++)
+        for (int i = 0; i < OD; i++) {
+            m.msrc[mm - 1][i] = (int16_t)g[mm].src[i];
+            m.msgn[mm - 1][i] = (float)g[mm].sgn[i];
+        }
+    int fill[4] = {0, 0, 0, 0};
+    bool seen[OD] = {false};
+    std::vector<int> out_src[4][48], out_w[4][48];
+    int out_size[4][48];
+    for (int i0 = 0; i0 < OD; i0++) {
+        if (seen[i0]) continue;
+        int orb[4], no = 0;
+        for (int gi = 0; gi < 4; gi++) {
+            const int j = g[gi].src[i0];
+            bool dup = false;
+            for (int t = 0; t < no; t++) dup |= orb[t] == j;
+            if (!dup) orb[no++] = j;
+        }
+        for (int t = 0; t < no; t++) seen[orb[t]] = true;
+        for (int x = 0; x < 4; x++) {
+            int w[4] = {0, 0, 0, 0};
+            for (int gi = 0; gi < 4; gi++) {
+                const int chi = (__builtin_popcount(x & gi) & 1) ? -1 : 1;
+                for (int t = 0; t < no; t++)
+                    if (orb[t] == g[gi].src[i0]) w[t] += chi * g[gi].sgn[i0];
+            }
+            bool nz = false;
+            for (int t = 0; t < no; t++) nz |= w[t] != 0;
+            if (!nz) continue;
+            if (fill[x] >= 48) return false;
+            const int o = fill[x]++;
+            out_size[x][o] = no;
+            for (int t = 0; t < no; t++) {
+                if (w[t] == 0) return false;
+                out_src[x][o].push_back(orb[t]);
+                out_w[x][o].push_back(w[t] > 0 ? 1 : -1);
+            }
+        }
+    }
+    for (int x = 0; x < 4; x++)
+        if (fill[x] != 48) return false;
+    for (int x = 0; x < 4; x++)
+        for (int o = 0; o < 48; o++) {
+            const int oo = x * 48 + o, no = out_size[x][o];
+            for (int t = 0; t < 4; t++) {
+                m.src[oo][t] = (int16_t)(t < no ? out_src[x][o][t] : 0);
+                m.w[oo][t] = t < no ? (float)out_w[x][o][t] : 0.0f;
+            }
+            m.cs[oo] = no == 4 ? 0.5f : 1.0f;
+            m.qs[oo] = no == 1 ? 1.0f : 0.5f;
+        }
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------
+// device: orbit detection
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void orbit_eq_kernel(const float *__restrict__ rows, long n,
+                                                       const OrbitMap *__restrict__ mp, uint16_t *bits) {
+    const int lane = threadIdx.x & 63;
+    for (long j = (long)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (long)gridDim.x * 4) {
+        unsigned b = 0;
+        for (int t = 1; t <= 3; t++) {
+            if (j + t >= n) break;
+            for (int m = 0; m < 3; m++) {
+                bool ok = true;
+                for (int i = lane; i < OD; i += 64)
+                    ok &= rows[(j + t) * OD + i] == mp->msgn[m][i] * rows[j * OD + mp->msrc[m][i]];
+                if (__all(ok)) b |= 1u << ((t - 1) * 3 + m);
+            }
+        }
+        if (lane == 0) bits[j] = (uint16_t)b;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// device: transform + fp16 split (dataset rows: member != null, coefficient cs; queries: qs)
+//   lane l of block b holds row b*32 + (l & 31), k = s*16 + 8*(l >> 5) + j  (A and B maps coincide)
+// ------------------------------------------------------------------------------------------
+struct OrbitPrepArgs {
+    const float *rows;     // dataset: candidate rows [n][192]; queries: [nq][192]
+    const int *member;     // dataset: [G][4] (slot 0 = base row); queries: null
+    long count;            // G or nq
+    const OrbitMap *mp;
+    float scale;
+    half8 *frag;           // [ceil(count/32)][12][64]
+    _Float16 *rowh;        // [count][192]
+    float *seed, *nc;      // dataset only
+    OrbitDsStat *ds;       // dataset only
+    OrbitStat *qstat;      // queries only
+};
+
+// One wave per 32 rows: the rows (gathered through member[] for the dataset) and the transform table
+// are staged in LDS (row stride 193 floats: the 32 lanes of a half-wave read 32 rows conflict-free).
+static constexpr int ORB_RS = OD + 1;
+
+__global__ __launch_bounds__(64) void orbit_prep_kernel(OrbitPrepArgs a) {
+    __shared__ float srow[32 * ORB_RS];
+    __shared__ int16_t msrc[OD * 4];
+    __shared__ float mw[OD * 4], mc[OD];
+    const int lane = threadIdx.x, h = lane >> 5;
+    const long nblk = (a.count + 31) / 32;
+    const bool dataset = a.member != nullptr;
+    for (int i = lane; i < OD * 4; i += 64) {
+        msrc[i] = a.mp->src[i >> 2][i & 3];
+        mw[i] = a.mp->w[i >> 2][i & 3];
+    }
+    for (int i = lane; i < OD; i += 64) mc[i] = dataset ? a.mp->cs[i] : a.mp->qs[i];
+    for (long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        __syncthreads();
+        for (int i = lane; i < 32 * (OD / 4); i += 64) {
+            const int rr = i / (OD / 4), c4 = i % (OD / 4);
+            const long r = blk * 32 + rr;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r < a.count) {
+                const long base = dataset ? (long)a.member[r * 4] : r;
+                v = reinterpret_cast<const float4 *>(a.rows + base * OD)[c4];
+            }
+            float *d = srow + rr * ORB_RS + c4 * 4;
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+        __syncthreads();
+        const long r = blk * 32 + (lane & 31);
+        const bool valid = r < a.count;
+        const float *row = srow + (lane & 31) * ORB_RS;
+        double n2 = 0, p2 = 0, h2 = 0, e2 = 0;
+        int bad = 0;
+        for (int s = 0; s < OS; s++) {
+            half8 hv;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int k = s * 16 + 8 * h + j;
+                double v = 0.0;
+                if (valid) {
+                    const double orig = (double)row[k] * (double)a.scale;
+                    n2 += orig * orig;
+#pragma unroll
+                    for (int t = 0; t < 4; t++) v += (double)mw[k * 4 + t] * (double)row[msrc[k * 4 + t]];
+                    v *= (double)mc[k] * (double)a.scale;
+                }
+                _Float16 vh = (_Float16)(float)v;
+                if (fabs((double)(float)vh) < 6.103515625e-05) vh = (_Float16)0.0f;  // no fp16 subnormal operands
+                hv[j] = vh;
+                const double dh = (double)(float)vh;
+                p2 += v * v;
+                h2 += dh * dh;
+                e2 += (v - dh) * (v - dh);
+                if (!isfinite(v) || fabs(v) > 65000.0) bad = 1;
+            }
+            a.frag[(blk * OS + s) * 64 + lane] = hv;
+            if (valid) *reinterpret_cast<half8 *>(a.rowh + r * OD + s * 16 + 8 * h) = hv;
+        }
+        n2 += __shfl_xor(n2, 32, 64);
+        p2 += __shfl_xor(p2, 32, 64);
+        h2 += __shfl_xor(h2, 32, 64);
+        e2 += __shfl_xor(e2, 32, 64);
+        bad |= __shfl_xor(bad, 32, 64);
+        if (!dataset) {
+            if (valid && h == 0) {
+                OrbitStat q;
+                q.n2 = n2;
+                q.hn = sqrt(h2);
+                q.en = sqrt(e2);
+                q.flags = (bad || !isfinite(n2)) ? 2 : 0;
+                q.pad = 0;
+                a.qstat[r] = q;
+            }
+            continue;
+        }
+        if (h == 0) {
+            const int rr = lane & 31;
+            const int pos = ((rr >> 2) & 1) * 16 + ((rr & 3) | ((rr >> 3) << 2));
+            a.seed[blk * 32 + pos] = valid ? -0.5f * (float)n2 : -INFINITY;
+            if (valid) a.nc[r] = (float)n2;
+        }
+        double mn = wave_max_d(valid ? n2 : 0.0), mp2 = wave_max_d(valid ? p2 : 0.0);
+        double mh = wave_max_d(valid ? h2 : 0.0), me = wave_max_d(valid ? e2 : 0.0);
+        const int bd = __any(valid && bad);
+        if (lane == 0) {
+            atomicMax(&a.ds->max_n2, (unsigned long long)__double_as_longlong(mn));
+            atomicMax(&a.ds->max_p2, (unsigned long long)__double_as_longlong(mp2));
+            atomicMax(&a.ds->max_h2, (unsigned long long)__double_as_longlong(mh));
+            atomicMax(&a.ds->max_e2, (unsigned long long)__double_as_longlong(me));
+            if (bd) atomicOr(&a.ds->bad, 1u);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// device: the orbit shortlist.  Workgroup = NW waves x one 32-query block; the 32-tile blocks of this
+// split stream through a double-buffered LDS ring (CB blocks per stage, LDS-DMA).  Accumulator element
+// r of lane l holds tile row (r & 3) + 8 (r >> 2) + 4 h (h = l >> 5) of query column l & 31; sub-block
+// s = r >> 2 = the 4 consecutive tiles 8 s + 4 h + 0..3.  List entry id = blk * 4 + s.
+// ------------------------------------------------------------------------------------------
+template <int L, int CB, int NW, int QB, int MODE>
+__global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_kernel(const half8 *__restrict__ cfrag,
+                                                                    const float *__restrict__ cseed, int nblk,
+                                                                    const half8 *__restrict__ qfrag, int nq,
+                                                                    int blk_per_split, int nsplit,
+                                                                    float *__restrict__ out_key,
+                                                                    int *__restrict__ out_id) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int FRAG_BYTES = CB * OS * 1024;
+    constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
+    constexpr int NT = NW * 64;
+    constexpr int PER_T = CB * OS * 64 / NT;
+    static_assert((CB * OS * 64) % NT == 0, "stage must split evenly over the workgroup");
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int nqblk = (nq + 31) / 32;
+    const int qb0 = (blockIdx.x * NW + w) * QB;
+    const int split = blockIdx.y;
+    const int b_begin = split * blk_per_split;
+    const int b_end = min(nblk, b_begin + blk_per_split);
+
+    // the wave's QB query blocks stay in registers as B fragments; each A fragment read from LDS feeds QB MFMAs
+    half8 bq[QB][OS];
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+        const long qa = min(qb0 + q, nqblk - 1);  // past the end: clamped duplicate, never written
+#pragma unroll
+        for (int s = 0; s < OS; s++) bq[q][s] = qfrag[(qa * OS + s) * 64 + lane];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) before the hidden DMA starts counting
+    float lk[QB][L];
+    int li[QB][L];
+#pragma unroll
+    for (int q = 0; q < QB; q++)
+#pragma unroll
+        for (int i = 0; i < L; i++) {
+            lk[q][i] = INFINITY;
+            li[q][i] = -1;
+        }
+
+    const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
+    auto issue = [&](int st, int buf) {
+        const int blk0 = b_begin + st * CB;
+        const int nb = min(CB, b_end - blk0);
+        const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * OS * 64 + w * 64 + lane;
+        char *dst = smem + buf * BUF_BYTES + w * 1024;
+        if (nb == CB) {
+#pragma unroll
+            for (int j = 0; j < PER_T; j++) glds16_asm(src + j * NT, dst + j * NT * 16);
+        } else {
+            const int last = nb * OS * 64 - 1 - (w * 64 + lane);
+#pragma unroll
+            for (int j = 0; j < PER_T; j++) glds16_asm(src + min(j * NT, last), dst + j * NT * 16);
+        }
+        if (w == 0 && lane < CB * 8)
+            glds16_asm(reinterpret_cast<const uint4 *>(cseed) + (long)blk0 * 8 + min(lane, nb * 8 - 1),
+                       smem + buf * BUF_BYTES + FRAG_BYTES);
+    };
+
+    if (nstage > 0) issue(0, 0);
+    dma_drain();
+    __syncthreads();
+    const floatx16 zero = {0};
+    for (int st = 0; st < nstage; st++) {
+        const char *B = smem + (st & 1) * BUF_BYTES;
+        const half8 *A = reinterpret_cast<const half8 *>(B) + lane;
+        const float4 *SD = reinterpret_cast<const float4 *>(B + FRAG_BYTES) + h * 4;
+        half8 a0 = A[0], a1 = A[64];
+        float4 sd0 = SD[0], sd1 = SD[1], sd2 = SD[2], sd3 = SD[3];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
+#pragma unroll
+        for (int cb = 0; cb < CB; cb++) {
+            const int blk = b_begin + st * CB + cb;
+            if (blk < b_end) {
+                const floatx16 seed = {sd0.x, sd0.y, sd0.z, sd0.w, sd1.x, sd1.y, sd1.z, sd1.w,
+                                       sd2.x, sd2.y, sd2.z, sd2.w, sd3.x, sd3.y, sd3.z, sd3.w};
+                // p = d0 (seeded with -||c||^2/2), then p += |d_x| as each isotypic block x = 1..3 completes;
+                // blocks 1 and 3 accumulate in ta, block 2 in tb (the next block's MFMAs run while p reads the last)
+                floatx16 p[QB], ta[QB], tb[QB];
+#pragma unroll
+                for (int s = 0; s < OS; s += 2) {
+                    half8 n0, n1;
+                    const bool more = s + 2 < OS || cb + 1 < CB;
+                    if (s + 2 < OS) {
+                        n0 = A[(cb * OS + s + 2) * 64];
+                        n1 = A[(cb * OS + s + 3) * 64];
+                    } else if (cb + 1 < CB) {  // next block of this stage: first pair and seeds
+                        n0 = A[((cb + 1) * OS) * 64];
+                        n1 = A[((cb + 1) * OS + 1) * 64];
+                        sd0 = SD[(cb + 1) * 8 + 0];
+                        sd1 = SD[(cb + 1) * 8 + 1];
+                        sd2 = SD[(cb + 1) * 8 + 2];
+                        sd3 = SD[(cb + 1) * 8 + 3];
+                    }
+#pragma unroll
+                    for (int hh = 0; hh < 2; hh++) {
+                        const int ss = s + hh, x = ss / 3;
+                        const half8 av = hh ? a1 : a0;
+#pragma unroll
+                        for (int q = 0; q < QB; q++) {
+                            if (x == 0)
+                                p[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[q][ss], ss == 0 ? seed : p[q], 0, 0, 0);
+                            else if (x == 2)
+                                tb[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[q][ss], ss % 3 == 0 ? zero : tb[q], 0, 0, 0);
+                            else
+                                ta[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[q][ss], ss % 3 == 0 ? zero : ta[q], 0, 0, 0);
+                        }
+                        if (MODE != 3 && x > 0 && ss % 3 == 2) {
+#pragma unroll
+                            for (int q = 0; q < QB; q++)
+#pragma unroll
+                                for (int r = 0; r < 16; r++) p[q][r] = p[q][r] + fabsf(x == 2 ? tb[q][r] : ta[q][r]);
+                        }
+                    }
+                    if (more) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2 * QB, 0);
+                    if (more) {
+                        a0 = n0;
+                        a1 = n1;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < QB; q++) {
+                    if (MODE == 3) {  // timing experiment: MFMA only
+                        lk[q][0] = fmaxf(lk[q][0], p[q][0] + ta[q][1] + tb[q][2]);
+                        continue;
+                    }
+                    // p = u = d0 + |d1| + |d2| + |d3| >= every mirror value q.(S_m c) - ||c||^2/2 (key = -2u)
+                    float m4[4];
+#pragma unroll
+                    for (int sb = 0; sb < 4; sb++)
+                        m4[sb] = fmaxf(fmaxf(p[q][4 * sb], p[q][4 * sb + 1]), fmaxf(p[q][4 * sb + 2], p[q][4 * sb + 3]));
+                    const float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+                    if (MODE == 2) {  // timing experiment: MFMA + bound only
+                        lk[q][0] = fmaxf(lk[q][0], mx);
+                        continue;
+                    }
+                    if (__builtin_expect(__any(mx > -0.5f * lk[q][L - 1]), 0)) {
+                        // insert every sub-block above the lane's current L-th entry, best first
+#pragma unroll
+                        for (int it = 0; it < 4; it++) {
+                            float best = m4[0];
+                            int bs = 0;
+#pragma unroll
+                            for (int sb = 1; sb < 4; sb++)
+                                if (m4[sb] > best) {
+                                    best = m4[sb];
+                                    bs = sb;
+                                }
+                            const bool ins = best > -0.5f * lk[q][L - 1];
+                            if (!__any(ins)) break;
+                            if (ins) {
+                                list_insert<L>(lk[q], li[q], -2.0f * best, blk * 4 + bs);
+#pragma unroll
+                                for (int sb = 0; sb < 4; sb++)
+                                    if (sb == bs) m4[sb] = -INFINITY;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        dma_drain();
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+        const int qq = (qb0 + q) * 32 + (lane & 31);
+        if (qb0 + q < nqblk && qq < nq) {
+            const long o = (((long)qq * nsplit + split) * 2 + h) * L;
+#pragma unroll
+            for (int i = 0; i < L; i++) {
+                out_key[o + i] = lk[q][i];
+                out_id[o + i] = li[q][i];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// device: orbit rescore, one wave per query
+// ------------------------------------------------------------------------------------------
+struct OrbitRescoreArgs {
+    const float *rows, *q;          // fp32 candidate rows [n][192], query rows [nq][192]
+    const _Float16 *rowh, *qrowh;   // fp16 c' [G][192], q' [nq][192]
+    const float *nc;                // [G]
+    const int *member;              // [G][4]
+    const OrbitStat *ostat;
+    const float *key;
+    const int *id;
+    int G, nq, L, nsplit;
+    double scale2;                  // scale^2
+    double N, Np, Hp, Ecp;
+    OrbitTail t;
+};
+
+// the reference distance (sequential fp32, every op rounded) with a short load window: the rescore
+// runs one query per wave and needs occupancy more than load depth
+__device__ __forceinline__ float exact_dist192_lean(const float *__restrict__ q, const float *__restrict__ c) {
+    const float4 *q4 = reinterpret_cast<const float4 *>(q), *c4 = reinterpret_cast<const float4 *>(c);
+    float dist = 0.0f;
+#pragma unroll 8
+    for (int i = 0; i < OD / 4; i++) {
+        const float4 x = q4[i], y = c4[i];
+        float t;
+        t = x.x - y.x; dist = dist + t * t;
+        t = x.y - y.y; dist = dist + t * t;
+        t = x.z - y.z; dist = dist + t * t;
+        t = x.w - y.w; dist = dist + t * t;
+    }
+    return dist;
+}
+
+__device__ __forceinline__ float wave_min_f(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// re-key the 16 candidates of sub-block `id` (half h): lane = (tile j, block x, part p); returns, in lane
+// (j, m = x, p = 0), the candidate index of mirror slot m (or -1) and its fp64 key; other lanes -1
+__device__ __forceinline__ int orbit_expand(const OrbitRescoreArgs &a, long q, int id, int h, double &key) {
+    const int lane = threadIdx.x & 63;
+    const int j = lane >> 4, x = (lane >> 2) & 3, p = lane & 3;
+    const int g = (id >> 2) * 32 + 8 * (id & 3) + 4 * h + j;
+    const bool gv = g < a.G;
+    float part = 0.0f;
+    if (gv) {  // 12 fp16 products, fp32 sums (any order is inside the bound's gamma_{D+1} allowance)
+        typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+        const half2_t *cr = reinterpret_cast<const half2_t *>(a.rowh + (long)g * OD + x * 48 + p * 12);
+        const half2_t *qr = reinterpret_cast<const half2_t *>(a.qrowh + q * OD + x * 48 + p * 12);
+#pragma unroll
+        for (int t = 0; t < 6; t++) part = __builtin_amdgcn_fdot2(cr[t], qr[t], part, false);
+    }
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    const float d0 = __shfl(part, j * 16 + 0, 64), d1 = __shfl(part, j * 16 + 4, 64);
+    const float d2 = __shfl(part, j * 16 + 8, 64), d3 = __shfl(part, j * 16 + 12, 64);
+    key = INFINITY;
+    if (!gv || p != 0) return -1;
+    const int m = x;  // mirror slot: value = sum_y chi_y(m) d_y, chi_y(m) = (-1)^popcount(y & m)
+    const double v = (double)d0 + ((m & 1) ? -(double)d1 : (double)d1) + ((m & 2) ? -(double)d2 : (double)d2) +
+                     ((__builtin_popcount(m & 3) & 1) ? -(double)d3 : (double)d3);
+    const int cand = a.member[(long)g * 4 + m];
+    if (cand < 0) return -1;
+    key = (double)a.nc[g] - 2.0 * v;
+    return cand;
+}
+
+static constexpr int ORB_QCAP = 128;  // rescore queue per wave
+
+__global__ __launch_bounds__(256) void nn_orbit_rescore_kernel(OrbitRescoreArgs a) {
+    const int lane = threadIdx.x & 63;
+    const long q = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= a.nq) return;
+    const OrbitTail &t = a.t;
+    const OrbitStat st = a.ostat[q];
+    if (st.flags & 2) {
+        if (lane == 0) t.ex_list[atomicAdd(t.ex_count, 1)] = (int)q;
+        return;
+    }
+    const int E = a.nsplit * 2 * a.L;
+    float ek = INFINITY;
+    int eid = -1;
+    if (lane < E) {
+        ek = a.key[q * E + lane];
+        eid = a.id[q * E + lane];
+    }
+    const int eh = (lane / a.L) & 1;
+    if (eid < 0) ek = INFINITY;
+    // 1. a real reference distance: expand the best entry, rescore its smallest-key candidate
+    float bk = ek;
+    int bl = lane;
+    wave_argmin(bk, bl);
+    if (!(bk < INFINITY)) {  // empty dataset
+        if (lane == 0) {
+            t.out_idx[q] = -1;
+            t.out_err[q] = FLT_MAX;
+            if (t.m_tile) {
+                t.m_tile[q] = -1;
+                t.m_pal[q] = -1;
+                t.m_hm[q] = 0;
+                t.m_vm[q] = 0;
+            }
+        }
+        return;
+    }
+    const float *qrow = a.q + q * OD;
+    double kx;
+    const int c0 = orbit_expand(a, q, __shfl(eid, bl, 64), __shfl(eh, bl, 64), kx);
+    float kk = c0 >= 0 ? (float)kx : INFINITY;  // rounded: only sets a looser threshold below
+    kk = wave_min_f(kk);
+    // 2. thresholds.  Some candidate has real key <= kk + Eo, so the winner's reference
+    // distance is <= (n2 + kk + Eo)(1 + g); any candidate c that can reach it has real key <= Tr.
+    const double u = 5.9604644775390625e-08;  // 2^-24
+    const double g = (double)(OD + 4) * u / (1.0 - (double)(OD + 4) * u) * 1.05;
+    const double gam = 2.0 * (OD + 1) * u;
+    const double Eo = 1.05 * (2.0 * u * a.N * a.N + gam * (a.N * a.N + 2.0 * st.hn * a.Hp) +
+                              2.0 * (st.en * a.Np + st.hn * a.Ecp)) + 1e-30;
+    const double kd = (double)kk + 1e-6 * fabs((double)kk) + 1e-30;  // covers the fp32 rounding of kk
+    const double Tr = (st.n2 + kd + Eo) * (1.0 + g) / (1.0 - g) - st.n2 + 1e-12 * (st.n2 + fabs(kd)) + 1e-30;
+    const double Tb = Tr + Eo;
+    // 3. overflow: a full lane list whose worst kept entry can still reach the threshold
+    const bool last = lane < E && (lane % a.L) == a.L - 1;
+    if (__any(last && eid >= 0 && (double)ek <= Tb)) {
+        if (lane == 0) {
+            const QStat gs = t.gqstat[q];
+            const double Eg = 1.05 * (2.0 * u * t.gN * t.gN + gam * (t.gN * t.gN + 2.0 * gs.hn * t.gH) +
+                                      2.0 * (gs.en * t.gN + gs.hn * t.gEc)) + 1e-30;
+            const double T = Tr + Eg;
+            float tf = (float)T;
+            if ((double)tf < T) tf = nextafterf(tf, INFINITY);
+            t.thr[q] = tf;
+            const int pidx = atomicAdd(t.fb_count, 1);
+            if (pidx < t.fb_max)
+                t.fb_list[pidx] = (int)q;
+            else
+                t.ex_list[atomicAdd(t.ex_count, 1)] = (int)q;
+        }
+        return;
+    }
+    // 4. expand every entry that can hold such a candidate and queue its candidates that can; then
+    // rescore the queue with the reference distance, one candidate per lane
+    __shared__ int s_cand[4][ORB_QCAP];
+    int *sc = s_cand[threadIdx.x >> 6];
+    float bd = INFINITY;
+    int bi = 0x7fffffff;
+    int cnt = 0, nexp = 0;
+    auto flush = [&]() {
+        for (int i = lane; i < cnt; i += 64) {
+            const int c = sc[i];
+            const float dd = exact_dist192_lean(qrow, a.rows + (long)c * OD);
+            if (lex_less(dd, c, bd, bi)) {
+                bd = dd;
+                bi = c;
+            }
+        }
+        cnt = 0;
+    };
+    unsigned long long todo = __ballot(lane < E && eid >= 0 && (double)ek <= Tb);
+    while (todo) {
+        const int e = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        nexp++;
+        double k;
+        const int c = orbit_expand(a, q, __shfl(eid, e, 64), __shfl(eh, e, 64), k);
+        const bool take = c >= 0 && k <= Tb;
+        const unsigned long long b = __ballot(take);
+        if (take) sc[cnt + __popcll(b & ((1ull << lane) - 1))] = c;
+        cnt += __popcll(b);
+        __builtin_amdgcn_wave_barrier();
+        if (cnt > ORB_QCAP - 16) flush();
+    }
+    __builtin_amdgcn_wave_barrier();
+    flush();
+    wave_argmin(bd, bi);
+    if (lane == 0) {
+        if (t.n_expand) atomicAdd(t.n_expand, nexp);
+        const bool ok = bi != 0x7fffffff;
+        t.out_idx[q] = ok ? bi : -1;
+        t.out_err[q] = ok ? bd : FLT_MAX;
+        if (t.m_tile) {
+            t.m_tile[q] = ok ? t.tr_tile[bi] : -1;
+            t.m_pal[q] = ok ? t.tr_pal[bi] : -1;
+            const int at = ok ? t.tr_attr[bi] : 0;
+            t.m_hm[q] = (at & 1) != 0;
+            t.m_vm[q] = (at & 2) != 0;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// host
+// ------------------------------------------------------------------------------------------
+static double bits2d(unsigned long long b) {
+    double v;
+    memcpy(&v, &b, 8);
+    return v;
+}
+
+void orbit_destroy(OrbitIndex *o) {
+    if (!o) return;
+    hipFree(o->d_frag);
+    hipFree(o->d_rowh);
+    hipFree(o->d_seed);
+    hipFree(o->d_nc);
+    hipFree(o->d_member);
+    hipFree(o->d_map);
+    hipFree(o->qfrag);
+    hipFree(o->qrowh);
+    hipFree(o->qstat);
+    hipFree(o->key);
+    hipFree(o->id);
+    delete o;
+}
+
+static int orbit_enabled() {
+    static int v = [] {
+        const char *e = getenv("TILER_ORBIT");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v;
+}
+
+int orbit_build(NNIndex *ix, hipStream_t stream) {
+    if (!orbit_enabled() || ix->d != OD || ix->S == 0 || ix->exact_int || ix->n < 2) return 1;
+    static OrbitMap hmap;
+    static int map_ok = -1;
+    if (map_ok < 0) map_ok = build_map(hmap) ? 1 : 0;
+    if (!map_ok) return 1;
+    const long n = ix->n;
+    OrbitMap *d_map = nullptr;
+    uint16_t *d_bits = nullptr;
+    TILER_HIP_CHECK(hipMalloc((void **)&d_map, sizeof(OrbitMap)));
+    TILER_HIP_CHECK(hipMemcpyAsync(d_map, &hmap, sizeof(OrbitMap), hipMemcpyHostToDevice, stream));
+    TILER_HIP_CHECK(hipMalloc((void **)&d_bits, n * sizeof(uint16_t)));
+    hipLaunchKernelGGL(orbit_eq_kernel, dim3((unsigned)std::min<long>(8192, (n + 3) / 4)), dim3(256), 0, stream,
+                       ix->d_rows, n, d_map, d_bits);
+    TILER_HIP_CHECK(hipGetLastError());
+    std::vector<uint16_t> bits(n);
+    TILER_HIP_CHECK(hipMemcpyAsync(bits.data(), d_bits, n * sizeof(uint16_t), hipMemcpyDeviceToHost, stream));
+    TILER_HIP_CHECK(hipStreamSynchronize(stream));
+    hipFree(d_bits);
+    // greedy grouping in index order: candidate j joins the open group (base s) in a free mirror slot m
+    // if row_j == S_m row_s (checked on the device above); otherwise it opens a new group
+    std::vector<int> member;
+    member.reserve(n + 4);
+    long start = -1;
+    int used = 0;
+    for (long j = 0; j < n; j++) {
+        bool joined = false;
+        const long tt = j - start;
+        if (start >= 0 && tt >= 1 && tt <= 3) {
+            for (int m = 1; m <= 3 && !joined; m++)
+                if (!((used >> m) & 1) && ((bits[start] >> ((tt - 1) * 3 + m - 1)) & 1)) {
+                    member[member.size() - 4 + m] = (int)j;
+                    used |= 1 << m;
+                    joined = true;
+                }
+        }
+        if (!joined) {
+            member.push_back((int)j);
+            member.push_back(-1);
+            member.push_back(-1);
+            member.push_back(-1);
+            start = j;
+            used = 1;
+        }
+    }
+    const long G = (long)member.size() / 4;
+    if (G * 10 > n * 7) {  // < ~1.43 candidates per orbit: the generic kernels are as fast
+        hipFree(d_map);
+        return 1;
+    }
+    OrbitIndex *o = new OrbitIndex();
+    o->G = (int)G;
+    o->gblk = (int)((G + 31) / 32);
+    o->d_map = d_map;
+    OrbitDsStat *d_ds = nullptr;
+    TILER_HIP_CHECK(hipMalloc((void **)&o->d_member, G * 4 * sizeof(int)));
+    TILER_HIP_CHECK(hipMemcpyAsync(o->d_member, member.data(), G * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
+    TILER_HIP_CHECK(hipMalloc(&o->d_frag, (size_t)o->gblk * OS * 1024));
+    TILER_HIP_CHECK(hipMalloc(&o->d_rowh, (size_t)G * OD * 2));
+    TILER_HIP_CHECK(hipMalloc((void **)&o->d_seed, (size_t)o->gblk * 32 * sizeof(float)));
+    TILER_HIP_CHECK(hipMalloc((void **)&o->d_nc, (size_t)G * sizeof(float)));
+    TILER_HIP_CHECK(hipMalloc((void **)&d_ds, sizeof(OrbitDsStat)));
+    TILER_HIP_CHECK(hipMemsetAsync(d_ds, 0, sizeof(OrbitDsStat), stream));
+    OrbitPrepArgs pa{ix->d_rows, o->d_member, G, (const OrbitMap *)d_map, ix->scale, (half8 *)o->d_frag,
+                     (_Float16 *)o->d_rowh, o->d_seed, o->d_nc, d_ds, nullptr};
+    hipLaunchKernelGGL(orbit_prep_kernel, dim3((unsigned)std::min<long>(8192, o->gblk)), dim3(64), 0,
+                       stream, pa);
+    TILER_HIP_CHECK(hipGetLastError());
+    OrbitDsStat ds;
+    TILER_HIP_CHECK(hipMemcpyAsync(&ds, d_ds, sizeof(ds), hipMemcpyDeviceToHost, stream));
+    TILER_HIP_CHECK(hipStreamSynchronize(stream));
+    hipFree(d_ds);
+    if (ds.bad) {
+        orbit_destroy(o);
+        return 1;
+    }
+    o->N = sqrt(bits2d(ds.max_n2));
+    o->Np = sqrt(bits2d(ds.max_p2));
+    o->Hp = sqrt(bits2d(ds.max_h2));
+    o->Ecp = sqrt(bits2d(ds.max_e2));
+    ix->orbit = o;
+    return 0;
+}
+
+static constexpr int ORB_L = 4, ORB_CB = 4, ORB_NW = 8;
+
+int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, hipStream_t stream) {
+    OrbitIndex *o = ix->orbit;
+    const int nqblk = (nq + 31) / 32;
+    static const int qb = [] {
+        const char *e = getenv("TILER_ORBIT_QB");  // query blocks of 32 per wave: 2 (default) or 1
+        return (e && e[0] == '1') ? 1 : 2;
+    }();
+    const int wgs = (nqblk + ORB_NW * qb - 1) / (ORB_NW * qb);
+    const int max_split = 64 / (2 * ORB_L);
+    int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
+    nsplit = std::min(nsplit, o->gblk);
+    const int bps = (o->gblk + nsplit - 1) / nsplit;
+    nsplit = (o->gblk + bps - 1) / bps;
+    if ((size_t)nq > o->cap_q) {
+        hipFree(o->qfrag);
+        hipFree(o->qrowh);
+        hipFree(o->qstat);
+        TILER_HIP_CHECK(hipMalloc(&o->qfrag, (size_t)(nqblk + 1) * OS * 1024));
+        TILER_HIP_CHECK(hipMalloc(&o->qrowh, (size_t)nq * OD * 2));
+        TILER_HIP_CHECK(hipMalloc((void **)&o->qstat, (size_t)nq * sizeof(OrbitStat)));
+        o->cap_q = nq;
+    }
+    const size_t nkeys = (size_t)nq * nsplit * 2 * ORB_L;
+    if (nkeys > o->cap_keys) {
+        hipFree(o->key);
+        hipFree(o->id);
+        TILER_HIP_CHECK(hipMalloc((void **)&o->key, nkeys * sizeof(float)));
+        TILER_HIP_CHECK(hipMalloc((void **)&o->id, nkeys * sizeof(int)));
+        o->cap_keys = nkeys;
+    }
+    {
+        OrbitPrepArgs pa{d_q, nullptr, nq, (const OrbitMap *)o->d_map, ix->scale, (half8 *)o->qfrag,
+                         (_Float16 *)o->qrowh, nullptr, nullptr, nullptr, o->qstat};
+        KTimer tm("nn_prep", stream);
+        hipLaunchKernelGGL(orbit_prep_kernel, dim3((unsigned)std::min<long>(8192, nqblk)), dim3(64), 0,
+                           stream, pa);
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    {
+        const size_t lds = 2 * (ORB_CB * OS * 1024 + ORB_CB * 128);
+        KTimer tm("nn_orbit", stream);
+        static const int mode = [] {
+            const char *e = getenv("TILER_ORBIT_MODE");  // 2, 3: timing experiments (results invalid)
+            return e ? atoi(e) : 0;
+        }();
+#define ORB_LAUNCH(QB, MD)                                                                                        \
+    hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, ORB_NW, QB, MD>), dim3(wgs, nsplit),               \
+                       dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                \
+                       (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id)
+        if (qb == 1) {
+            if (mode == 2)
+                ORB_LAUNCH(1, 2);
+            else if (mode == 3)
+                ORB_LAUNCH(1, 3);
+            else
+                ORB_LAUNCH(1, 0);
+        } else {
+            if (mode == 2)
+                ORB_LAUNCH(2, 2);
+            else if (mode == 3)
+                ORB_LAUNCH(2, 3);
+            else
+                ORB_LAUNCH(2, 0);
+        }
+#undef ORB_LAUNCH
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    OrbitRescoreArgs ra;
+    ra.rows = ix->d_rows;
+    ra.q = d_q;
+    ra.rowh = (const _Float16 *)o->d_rowh;
+    ra.qrowh = (const _Float16 *)o->qrowh;
+    ra.nc = o->d_nc;
+    ra.member = o->d_member;
+    ra.ostat = o->qstat;
+    ra.key = o->key;
+    ra.id = o->id;
+    ra.G = o->G;
+    ra.nq = nq;
+    ra.L = ORB_L;
+    ra.nsplit = nsplit;
+    ra.scale2 = (double)ix->scale * (double)ix->scale;
+    ra.N = o->N;
+    ra.Np = o->Np;
+    ra.Hp = o->Hp;
+    ra.Ecp = o->Ecp;
+    ra.t = tail;
+    {
+        KTimer tm("nn_rescore", stream);
+        hipLaunchKernelGGL(nn_orbit_rescore_kernel, dim3((nq + 3) / 4), dim3(256), 0, stream, ra);
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    ix->last_splits = nsplit;
+    return 0;
+}
+
+}  // namespace tiler

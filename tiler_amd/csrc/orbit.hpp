@@ -1,0 +1,69 @@
+// orbit.hpp -- mirror-orbit FrameTiling search (gfx950): one MFMA pass scores all 4 H/V mirrors of a tile.
+//
+// The a6 search dataset (PrepareFrameTiling.DoPsyV, main.pas:3883-3919) holds every used tile in up to
+// 4 orientations, emitted consecutively (hmir inner, vmir outer).  For the Haar PsyV descriptor
+// (WaveletGS main.pas:2805-2840, the FrameTiling default `chkUseWL`) a mirrored tile's descriptor is an
+// EXACT signed permutation of the unmirrored one (L = (a+b)*f and H = (a-b)*f are symmetric /
+// antisymmetric in a, b bit for bit), so with S_m the signed permutation of mirror m and the isotypic
+// decomposition of R^192 under {I, H, V, HV} (4 components of 48 dimensions each),
+//     q . (S_m c) = sum_x chi_x(m) (P_x q) . (P_x c),   chi_x(m) = (-1)^popcount(x & m).
+// The shortlist therefore runs one 192-deep MFMA contraction per (query, tile) instead of 4, keeping
+// the 4 partial 48-d dots in separate accumulators; everything downstream stays exact.
+// Grouping is data-driven and verified bit-for-bit on the device, so the path also serves the
+// reference's plain `ann_kdtree_create` + `ann_kdtree_search` calls (extern.pas:63-67).
+#pragma once
+#include "nn_search.hpp"
+
+namespace tiler {
+
+// per-query statistics of the transformed query q' (scaled space)
+struct OrbitStat {
+    double n2;   // ||q||^2
+    double hn;   // ||fp16(q')||
+    double en;   // ||q' - fp16(q')||
+    int flags;   // bit1: bad (non-finite / fp16 overflow) -> exhaustive scan
+    int pad;
+};
+
+struct OrbitIndex {
+    int G = 0, gblk = 0;          // tile groups (orbits of candidates) and 32-group blocks
+    void *d_frag = nullptr;       // [gblk][12][64][8] fp16 MFMA A fragments of c' = U c_base
+    void *d_rowh = nullptr;       // [G][192] fp16 c' row-major (rescore re-keying)
+    float *d_seed = nullptr;      // [gblk][32] -||c||^2/2 in accumulator-row order (-inf padding)
+    float *d_nc = nullptr;        // [G] ||c||^2 (scaled, fp32)
+    int *d_member = nullptr;      // [G][4] candidate index of relative mirror slot m (H = 1, V = 2), -1 absent
+    void *d_map = nullptr;        // OrbitMap
+    double N = 0, Np = 0, Hp = 0, Ecp = 0;  // max ||c||, ||c'||, ||fp16(c')||, ||c' - fp16(c')||
+    // per-call scratch
+    void *qfrag = nullptr, *qrowh = nullptr;
+    OrbitStat *qstat = nullptr;
+    size_t cap_q = 0;
+    float *key = nullptr;
+    int *id = nullptr;
+    size_t cap_keys = 0;
+    long long last_expansions = 0;
+};
+
+// generic tier-2 / tier-3 plumbing the orbit rescore feeds (owned by nn_search.hip)
+struct OrbitTail {
+    const QStat *gqstat;          // generic per-query stats: tier-2 threshold in the generic key domain
+    double gN, gH, gEc;
+    int *fb_list, *fb_count, *ex_list, *ex_count, fb_max;
+    float *thr;
+    int *out_idx;
+    float *out_err;
+    const int32_t *tr_tile, *tr_pal;
+    const uint8_t *tr_attr;
+    int32_t *m_tile, *m_pal;
+    uint8_t *m_hm, *m_vm;
+    int *n_expand;                // optional device counter of block expansions
+};
+
+// 0: orbit index built (ix->orbit), 1: dataset has no exploitable mirror structure, -1: HIP error
+int orbit_build(NNIndex *ix, hipStream_t stream);
+void orbit_destroy(OrbitIndex *o);
+inline long long orbit_groups(const NNIndex *ix) { return ix->orbit ? ((const OrbitIndex *)ix->orbit)->G : 0; }
+// k = 1 search of nq fp32 query rows: query prep, orbit shortlist, orbit rescore (tiers 2/3 by the caller)
+int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, hipStream_t stream);
+
+}  // namespace tiler

@@ -63,6 +63,8 @@ typedef struct {
     int64_t orbit_groups;     /* mirror orbits found in the dataset (0: mirror-orbit path unavailable) */
     int32_t orbit_search;     /* 1 when the last search ran the mirror-orbit shortlist */
     int32_t reserved;
+    int64_t orbit_expansions; /* TILER_ORBIT_STATS=1 only: 4-entry re-key passes of the orbit rescore */
+    int64_t orbit_rescored;   /* TILER_ORBIT_STATS=1 only: candidates rescored with the reference distance */
 } tiler_search_stats;
 int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
 

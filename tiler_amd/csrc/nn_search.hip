@@ -1151,6 +1151,8 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, hipStream_t stream) {
     ix->S = pick_S(d);
     ix->nblk = (n + 31) / 32;
     TILER_HIP_CHECK_NULL(hipHostMalloc((void **)&ix->h_fb_count, sizeof(int) * 2, hipHostMallocDefault));
+    ix->h_fb_count[0] = 1 << 30;  // first call: full tier-2 grid
+    ix->h_fb_count[1] = 0;
     if (ix->S == 0 || n == 0) return ix;
     // scale: power of two so that max|v| * scale <= 16384
     unsigned int *d_m = nullptr;
@@ -1402,7 +1404,11 @@ static void launch_collect(NNIndex *ix, int nq, hipStream_t stream) {
     // overflowed queries still spread over the whole chip
     const int nsplit = std::min(ix->nblk, 256);
     const int bps = (ix->nblk + nsplit - 1) / nsplit;
-    const int groups = std::min(32, (std::min(nq, TIER2_MAX) + 255) / 256);
+    // grid.x = query groups of 256; the kernel strides over the device-side count, so any grid is correct.
+    // Idle workgroups are not free (about 0.18 us each to dispatch and retire at this LDS size), so the
+    // grid follows the previous call's tier-2 count (h_fb_count, copied back at the end of each search)
+    const int prev = ix->h_fb_count ? std::max(0, ix->h_fb_count[0]) : TIER2_MAX;
+    const int groups = std::max(1, std::min({32, (std::min(nq, TIER2_MAX) + 255) / 256, (prev + prev / 4 + 255) / 256 + 1}));
     const size_t lds = 2 * (CB * S * 1024 + CB * 128);
     SearchScratch &s = ix->scratch;
     KTimer tm("nn_collect", stream);
@@ -1500,21 +1506,12 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     if (ensure_scratch(ix, nq, (long)nq * nsplit * lpq * L)) return -1;
     SearchScratch &s = ix->scratch;
     TILER_HIP_CHECK(hipMemsetAsync(s.fb_count, 0, 16, stream));
-    // queries -> fragments (same layout and scale as the dataset)
-    const long nqblk = (nq + 31) / 32;
-    PrepArgs pa{d_q, nq, ix->d, ix->S, ix->scale, (half8 *)s.qfrag, nullptr, nullptr, s.qstat, nullptr, 0};
-    {
-        KTimer t_prep("nn_prep", stream);
-        hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)std::min<long>(4096, (nqblk + 3) / 4)), dim3(256), 0,
-                           stream, pa);
-    }
-    TILER_HIP_CHECK(hipGetLastError());
     ix->last_orbit = 0;
     if (k == 1 && ix->orbit) {
-        // mirror-orbit path (orbit.hip): the generic query fragments above feed only the tier-2 pass
+        // mirror-orbit path (orbit.hip); generic query fragments are built for the tier-2 queries only
         TILER_HIP_CHECK(hipMemsetAsync(s.ccnt, 0, (size_t)std::min(nq, TIER2_MAX) * sizeof(int), stream));
         OrbitTail t{};
-        t.gqstat = s.qstat;
+        t.gqfrag = s.qfrag;
         t.gN = ix->maxN;
         t.gH = ix->maxH;
         t.gEc = ix->maxE;
@@ -1547,6 +1544,15 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         ra.fb_max = TIER2_MAX;
         return search_tail(ix, ra, nq, stream);
     }
+    // queries -> fragments (same layout and scale as the dataset)
+    const long nqblk = (nq + 31) / 32;
+    PrepArgs pa{d_q, nq, ix->d, ix->S, ix->scale, (half8 *)s.qfrag, nullptr, nullptr, s.qstat, nullptr, 0};
+    {
+        KTimer t_prep("nn_prep", stream);
+        hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)std::min<long>(4096, (nqblk + 3) / 4)), dim3(256), 0,
+                           stream, pa);
+    }
+    TILER_HIP_CHECK(hipGetLastError());
     if (v16) {
         Prep16Args p16{d_q, nq, ix->d, ix->S16, ix->scale, (half8 *)s.qfrag16, nullptr, 0};
         {

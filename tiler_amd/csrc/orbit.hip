@@ -28,6 +28,12 @@ namespace tiler {
 
 static constexpr int OD = 192;  // descriptor dimension (cTileDCTSize, main.pas:44)
 static constexpr int OS = 12;   // k-steps of 16 (4 isotypic blocks x 3)
+#ifndef ORB_XBATCH
+#define ORB_XBATCH 3
+#endif
+#ifndef ORB_DU
+#define ORB_DU 4
+#endif
 
 // device copy of the transform: output coordinate o (block x = o / 48) = coef[o] * sum_t w[o][t] * v[src[o][t]]
 struct OrbitMap {
@@ -509,6 +515,7 @@ struct OrbitRescoreArgs {
     const float *key;
     const int *id;
     int G, nq, L, nsplit;
+    int p1;                         // entries re-keyed in the first pass (1..4)
     double scale2;                  // scale^2
     double N, Np, Hp, Ecp;
     OrbitTail t;
@@ -536,39 +543,54 @@ __device__ __forceinline__ float wave_min_f(float v) {
     return v;
 }
 
-// re-key the 16 candidates of sub-block `id` (half h): lane = (tile j, block x, part p); returns, in lane
-// (j, m = x, p = 0), the candidate index of mirror slot m (or -1) and its fp64 key; other lanes -1
-__device__ __forceinline__ int orbit_expand(const OrbitRescoreArgs &a, long q, int id, int h, double &key) {
-    const int lane = threadIdx.x & 63;
-    const int j = lane >> 4, x = (lane >> 2) & 3, p = lane & 3;
+static constexpr int ORB_XB = ORB_XBATCH;  // 16-byte loads in flight per lane in the re-key
+
+// Re-key 4 list entries at once: lane = (slot e, tile j, isotypic block x).  Each lane forms the 48-d partial
+// dot d_x of its tile from the fp16 rows; a 2-stage Walsh-Hadamard butterfly over the 4 lanes of a tile turns
+// (d_0..d_3) into the 4 mirror values V_m = sum_x chi_x(m) d_x, m = x of the lane.  Returns the candidate of
+// mirror slot m (or -1) and its key ||c||^2 - 2 V_m.  `id` / `h`: the entry of this lane's slot (-1: none).
+__device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, int id, int h, double &key) {
+    typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+    const int lane = threadIdx.x & 63, j = (lane >> 2) & 3, x = lane & 3;
     const int g = (id >> 2) * 32 + 8 * (id & 3) + 4 * h + j;
-    const bool gv = g < a.G;
-    float part = 0.0f;
-    if (gv) {  // 12 fp16 products, fp32 sums (any order is inside the bound's gamma_{D+1} allowance)
-        typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
-        const half2_t *cr = reinterpret_cast<const half2_t *>(a.rowh + (long)g * OD + x * 48 + p * 12);
-        const half2_t *qr = reinterpret_cast<const half2_t *>(a.qrowh + q * OD + x * 48 + p * 12);
+    const bool gv = id >= 0 && g < a.G;
+    float d = 0.0f;
+    if (gv) {  // fp16 products, fp32 sums (any order is inside the bound's gamma_{D+1} allowance)
+        const uint4 *cr = reinterpret_cast<const uint4 *>(a.rowh + (long)g * OD + x * 48);
+        const uint4 *qr = reinterpret_cast<const uint4 *>(a.qrowh + q * OD + x * 48);
 #pragma unroll
-        for (int t = 0; t < 6; t++) part = __builtin_amdgcn_fdot2(cr[t], qr[t], part, false);
+        for (int t0 = 0; t0 < 6; t0 += ORB_XB) {
+            uint4 cv[ORB_XB], qv[ORB_XB];
+#pragma unroll
+            for (int t = 0; t < ORB_XB; t++) {
+                cv[t] = cr[t0 + t];
+                qv[t] = qr[t0 + t];
+            }
+#pragma unroll
+            for (int t = 0; t < ORB_XB; t++) {
+                const half2_t *c2 = reinterpret_cast<const half2_t *>(&cv[t]);
+                const half2_t *q2 = reinterpret_cast<const half2_t *>(&qv[t]);
+#pragma unroll
+                for (int u = 0; u < 4; u++) d = __builtin_amdgcn_fdot2(c2[u], q2[u], d, false);
+            }
+        }
     }
-    part += __shfl_xor(part, 1, 64);
-    part += __shfl_xor(part, 2, 64);
-    const float d0 = __shfl(part, j * 16 + 0, 64), d1 = __shfl(part, j * 16 + 4, 64);
-    const float d2 = __shfl(part, j * 16 + 8, 64), d3 = __shfl(part, j * 16 + 12, 64);
+    float o = __shfl_xor(d, 1, 64);
+    d = (x & 1) ? (o - d) : (d + o);
+    o = __shfl_xor(d, 2, 64);
+    d = (x & 2) ? (o - d) : (d + o);
     key = INFINITY;
-    if (!gv || p != 0) return -1;
-    const int m = x;  // mirror slot: value = sum_y chi_y(m) d_y, chi_y(m) = (-1)^popcount(y & m)
-    const double v = (double)d0 + ((m & 1) ? -(double)d1 : (double)d1) + ((m & 2) ? -(double)d2 : (double)d2) +
-                     ((__builtin_popcount(m & 3) & 1) ? -(double)d3 : (double)d3);
-    const int cand = a.member[(long)g * 4 + m];
+    if (!gv) return -1;
+    const int cand = a.member[(long)g * 4 + x];
     if (cand < 0) return -1;
-    key = (double)a.nc[g] - 2.0 * v;
+    key = (double)a.nc[g] - 2.0 * (double)d;
     return cand;
 }
 
 static constexpr int ORB_QCAP = 128;  // rescore queue per wave
+static constexpr int ORB_STG = 8;     // candidate rows staged in LDS per pass
 
-__global__ __launch_bounds__(256) void nn_orbit_rescore_kernel(OrbitRescoreArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void nn_orbit_rescore_kernel(OrbitRescoreArgs a) {
     const int lane = threadIdx.x & 63;
     const long q = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= a.nq) return;
@@ -587,11 +609,22 @@ __global__ __launch_bounds__(256) void nn_orbit_rescore_kernel(OrbitRescoreArgs 
     }
     const int eh = (lane / a.L) & 1;
     if (eid < 0) ek = INFINITY;
-    // 1. a real reference distance: expand the best entry, rescore its smallest-key candidate
-    float bk = ek;
-    int bl = lane;
-    wave_argmin(bk, bl);
-    if (!(bk < INFINITY)) {  // empty dataset
+    const bool last = lane < E && (lane % a.L) == a.L - 1 && eid >= 0;
+    // 1. the 4 entries with the smallest keys, re-keyed together (one round trip)
+    int sel = -1;  // slot e (lane >> 4) <- entry lane
+    bool taken = false;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        if (r >= a.p1) break;
+        float v = (taken || !(ek < INFINITY)) ? INFINITY : ek;
+        int who = lane;
+        wave_argmin(v, who);
+        if (v < INFINITY) {
+            if (lane == who) taken = true;
+            if ((lane >> 4) == r) sel = who;
+        }
+    }
+    if (__shfl(sel, 0, 64) < 0) {  // empty dataset
         if (lane == 0) {
             t.out_idx[q] = -1;
             t.out_err[q] = FLT_MAX;
@@ -604,10 +637,11 @@ __global__ __launch_bounds__(256) void nn_orbit_rescore_kernel(OrbitRescoreArgs 
         }
         return;
     }
-    const float *qrow = a.q + q * OD;
-    double kx;
-    const int c0 = orbit_expand(a, q, __shfl(eid, bl, 64), __shfl(eh, bl, 64), kx);
-    float kk = c0 >= 0 ? (float)kx : INFINITY;  // rounded: only sets a looser threshold below
+    const int sl = sel < 0 ? 0 : sel;
+    const int sid = __shfl(eid, sl, 64), shh = __shfl(eh, sl, 64);
+    double k1;
+    const int c1 = orbit_expand4(a, q, sel < 0 ? -1 : sid, shh, k1);
+    float kk = c1 >= 0 ? (float)k1 : INFINITY;  // rounded: only sets a looser threshold below
     kk = wave_min_f(kk);
     // 2. thresholds.  Some candidate has real key <= kk + Eo, so the winner's reference
     // distance is <= (n2 + kk + Eo)(1 + g); any candidate c that can reach it has real key <= Tr.
@@ -619,17 +653,11 @@ __global__ __launch_bounds__(256) void nn_orbit_rescore_kernel(OrbitRescoreArgs 
     const double kd = (double)kk + 1e-6 * fabs((double)kk) + 1e-30;  // covers the fp32 rounding of kk
     const double Tr = (st.n2 + kd + Eo) * (1.0 + g) / (1.0 - g) - st.n2 + 1e-12 * (st.n2 + fabs(kd)) + 1e-30;
     const double Tb = Tr + Eo;
-    // 3. overflow: a full lane list whose worst kept entry can still reach the threshold
-    const bool last = lane < E && (lane % a.L) == a.L - 1;
-    if (__any(last && eid >= 0 && (double)ek <= Tb)) {
+    // 3. overflow: a full lane list whose worst kept entry can still reach the threshold.  The tier-2
+    // threshold (generic key domain) is completed by orbit_fbprep_kernel.
+    if (__any(last && (double)ek <= Tb)) {
         if (lane == 0) {
-            const QStat gs = t.gqstat[q];
-            const double Eg = 1.05 * (2.0 * u * t.gN * t.gN + gam * (t.gN * t.gN + 2.0 * gs.hn * t.gH) +
-                                      2.0 * (gs.en * t.gN + gs.hn * t.gEc)) + 1e-30;
-            const double T = Tr + Eg;
-            float tf = (float)T;
-            if ((double)tf < T) tf = nextafterf(tf, INFINITY);
-            t.thr[q] = tf;
+            reinterpret_cast<double *>(t.thr_real)[q] = Tr;
             const int pidx = atomicAdd(t.fb_count, 1);
             if (pidx < t.fb_max)
                 t.fb_list[pidx] = (int)q;
@@ -638,43 +666,81 @@ __global__ __launch_bounds__(256) void nn_orbit_rescore_kernel(OrbitRescoreArgs 
         }
         return;
     }
-    // 4. expand every entry that can hold such a candidate and queue its candidates that can; then
-    // rescore the queue with the reference distance, one candidate per lane
+    // 4. queue every candidate that can reach the threshold; entries beyond the first 4 that can hold
+    // one are re-keyed 4 at a time; then the queue is rescored with the reference distance: candidate rows
+    // are staged in LDS by the whole wave (one round trip), then one lane per candidate sums in order
     __shared__ int s_cand[4][ORB_QCAP];
-    int *sc = s_cand[threadIdx.x >> 6];
+    __shared__ float4 s_row[4][ORB_STG][OD / 4];
+    const int wv = threadIdx.x >> 6;
+    int *sc = s_cand[wv];
+    const float *qrow = a.q + q * OD;
     float bd = INFINITY;
     int bi = 0x7fffffff;
-    int cnt = 0, nexp = 0;
+    int cnt = 0, nexp = 1, nres = 0;
     auto flush = [&]() {
-        for (int i = lane; i < cnt; i += 64) {
-            const int c = sc[i];
-            const float dd = exact_dist192_lean(qrow, a.rows + (long)c * OD);
-            if (lex_less(dd, c, bd, bi)) {
-                bd = dd;
-                bi = c;
+        for (int b0 = 0; b0 < cnt; b0 += ORB_STG) {
+            const int nb = min(ORB_STG, cnt - b0);
+            for (int i = lane; i < nb * (OD / 4); i += 64) {
+                const int r = i / (OD / 4), c4 = i - r * (OD / 4);
+                s_row[wv][r][c4] = reinterpret_cast<const float4 *>(a.rows + (long)sc[b0 + r] * OD)[c4];
             }
+            __builtin_amdgcn_wave_barrier();
+            if (lane < nb) {
+                const int c = sc[b0 + lane];
+                const float4 *q4 = reinterpret_cast<const float4 *>(qrow);
+                float dist = 0.0f;
+#pragma unroll ORB_DU
+                for (int i = 0; i < OD / 4; i++) {
+                    const float4 x = q4[i], y = s_row[wv][lane][i];
+                    float tt;
+                    tt = x.x - y.x; dist = dist + tt * tt;
+                    tt = x.y - y.y; dist = dist + tt * tt;
+                    tt = x.z - y.z; dist = dist + tt * tt;
+                    tt = x.w - y.w; dist = dist + tt * tt;
+                }
+                if (lex_less(dist, c, bd, bi)) {
+                    bd = dist;
+                    bi = c;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
         }
+        nres += cnt;
         cnt = 0;
     };
-    unsigned long long todo = __ballot(lane < E && eid >= 0 && (double)ek <= Tb);
-    while (todo) {
-        const int e = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        nexp++;
-        double k;
-        const int c = orbit_expand(a, q, __shfl(eid, e, 64), __shfl(eh, e, 64), k);
+    auto enqueue = [&](int c, double k) {
         const bool take = c >= 0 && k <= Tb;
         const unsigned long long b = __ballot(take);
         if (take) sc[cnt + __popcll(b & ((1ull << lane) - 1))] = c;
         cnt += __popcll(b);
         __builtin_amdgcn_wave_barrier();
-        if (cnt > ORB_QCAP - 16) flush();
+        if (cnt > ORB_QCAP - 64) flush();
+    };
+    enqueue(c1, k1);
+    unsigned long long todo = __ballot(!taken && eid >= 0 && (double)ek <= Tb);
+    while (todo) {
+        int el = -1;  // slot e <- the e-th remaining entry
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int e = todo ? __builtin_ctzll(todo) : -1;
+            if (todo) todo &= todo - 1;
+            if ((lane >> 4) == r) el = e;
+        }
+        nexp++;
+        const int ee = el < 0 ? 0 : el;
+        const int xid = __shfl(eid, ee, 64), xh = __shfl(eh, ee, 64);
+        double k;
+        const int c = orbit_expand4(a, q, el < 0 ? -1 : xid, xh, k);
+        enqueue(c, k);
     }
     __builtin_amdgcn_wave_barrier();
     flush();
     wave_argmin(bd, bi);
     if (lane == 0) {
-        if (t.n_expand) atomicAdd(t.n_expand, nexp);
+        if (t.n_expand) {
+            atomicAdd(t.n_expand, nexp);
+            atomicAdd(t.n_expand + 1, nres);
+        }
         const bool ok = bi != 0x7fffffff;
         t.out_idx[q] = ok ? bi : -1;
         t.out_err[q] = ok ? bd : FLT_MAX;
@@ -684,6 +750,59 @@ __global__ __launch_bounds__(256) void nn_orbit_rescore_kernel(OrbitRescoreArgs 
             const int at = ok ? t.tr_attr[bi] : 0;
             t.m_hm[q] = (at & 1) != 0;
             t.m_vm[q] = (at & 2) != 0;
+        }
+    }
+}
+
+// Tier-2 hand-off for the queries the orbit rescore could not settle: their generic fp16 B fragments
+// (the 32-column layout of nn_search.hip's collect pass, at the query's own column), the generic key
+// error bound, and the tier-2 threshold T = T_real + E_generic rounded up to fp32.  One wave per query.
+struct OrbitFbArgs {
+    const float *q;       // [nq][192]
+    const int *fb_list, *fb_count;
+    int fb_max;
+    const double *thr_real;
+    float *thr;
+    half8 *qfrag;         // generic [nqblk][12][64]
+    float scale;
+    double gN, gH, gEc;
+};
+
+__global__ __launch_bounds__(256) void orbit_fbprep_kernel(OrbitFbArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int count = min(*a.fb_count, a.fb_max);
+    for (int j = blockIdx.x * 4 + (threadIdx.x >> 6); j < count; j += gridDim.x * 4) {
+        const long qq = a.fb_list[j];
+        double n2 = 0, sh = 0, se = 0;
+        if (lane < 2 * OS) {  // lane = (k-step s, half h)
+            const int s = lane >> 1, h = lane & 1;
+            half8 hv;
+#pragma unroll
+            for (int jj = 0; jj < 8; jj++) {
+                const float vs = a.q[qq * OD + s * 16 + 8 * h + jj] * a.scale;
+                _Float16 vh = (_Float16)vs;
+                if (fabsf((float)vh) < 6.103515625e-05f) vh = (_Float16)0.0f;  // as prep_rows_kernel
+                hv[jj] = vh;
+                const double dv = vs, dh = (double)(float)vh;
+                n2 += dv * dv;
+                sh += dh * dh;
+                se += (dv - dh) * (dv - dh);
+            }
+            a.qfrag[((qq >> 5) * OS + s) * 64 + (qq & 31) + 32 * h] = hv;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            sh += __shfl_xor(sh, o, 64);
+            se += __shfl_xor(se, o, 64);
+        }
+        if (lane == 0) {
+            const double u = 5.9604644775390625e-08, gam = 2.0 * (OD + 1) * u;
+            const double hn = sqrt(sh), en = sqrt(se);
+            const double Eg = 1.05 * (2.0 * u * a.gN * a.gN + gam * (a.gN * a.gN + 2.0 * hn * a.gH) +
+                                      2.0 * (en * a.gN + hn * a.gEc)) + 1e-30;
+            const double T = a.thr_real[qq] + Eg;
+            float tf = (float)T;
+            if ((double)tf < T) tf = nextafterf(tf, INFINITY);  // keep T an upper bound in fp32
+            a.thr[qq] = tf;
         }
     }
 }
@@ -708,6 +827,8 @@ void orbit_destroy(OrbitIndex *o) {
     hipFree(o->qfrag);
     hipFree(o->qrowh);
     hipFree(o->qstat);
+    hipFree(o->thr_real);
+    hipFree(o->d_stats);
     hipFree(o->key);
     hipFree(o->id);
     delete o;
@@ -824,6 +945,8 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         hipFree(o->qfrag);
         hipFree(o->qrowh);
         hipFree(o->qstat);
+        hipFree(o->thr_real);
+        TILER_HIP_CHECK(hipMalloc((void **)&o->thr_real, (size_t)nq * sizeof(double)));
         TILER_HIP_CHECK(hipMalloc(&o->qfrag, (size_t)(nqblk + 1) * OS * 1024));
         TILER_HIP_CHECK(hipMalloc(&o->qrowh, (size_t)nq * OD * 2));
         TILER_HIP_CHECK(hipMalloc((void **)&o->qstat, (size_t)nq * sizeof(OrbitStat)));
@@ -888,19 +1011,55 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.nq = nq;
     ra.L = ORB_L;
     ra.nsplit = nsplit;
+    static const int p1 = [] {
+        const char *e = getenv("TILER_ORBIT_P1");
+        const int v = e ? atoi(e) : 4;
+        return v < 1 ? 1 : v > 4 ? 4 : v;
+    }();
+    ra.p1 = p1;
     ra.scale2 = (double)ix->scale * (double)ix->scale;
     ra.N = o->N;
     ra.Np = o->Np;
     ra.Hp = o->Hp;
     ra.Ecp = o->Ecp;
     ra.t = tail;
+    ra.t.thr_real = o->thr_real;
+    static const bool want_stats = [] {
+        const char *e = getenv("TILER_ORBIT_STATS");
+        return e && e[0] == '1';
+    }();
+    if (want_stats) {
+        if (!o->d_stats) TILER_HIP_CHECK(hipMalloc((void **)&o->d_stats, 2 * sizeof(int)));
+        TILER_HIP_CHECK(hipMemsetAsync(o->d_stats, 0, 2 * sizeof(int), stream));
+        ra.t.n_expand = o->d_stats;
+    }
     {
         KTimer tm("nn_rescore", stream);
         hipLaunchKernelGGL(nn_orbit_rescore_kernel, dim3((nq + 3) / 4), dim3(256), 0, stream, ra);
     }
     TILER_HIP_CHECK(hipGetLastError());
+    {
+        OrbitFbArgs fa{d_q, tail.fb_list, tail.fb_count, tail.fb_max, o->thr_real, tail.thr, (half8 *)tail.gqfrag,
+                       ix->scale, tail.gN, tail.gH, tail.gEc};
+        KTimer tm("nn_prep", stream);
+        hipLaunchKernelGGL(orbit_fbprep_kernel, dim3(256), dim3(256), 0, stream, fa);
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    if (want_stats) {
+        int h[2];
+        TILER_HIP_CHECK(hipMemcpyAsync(h, o->d_stats, sizeof(h), hipMemcpyDeviceToHost, stream));
+        TILER_HIP_CHECK(hipStreamSynchronize(stream));
+        o->last_expansions = h[0];
+        o->last_rescored = h[1];
+    }
     ix->last_splits = nsplit;
     return 0;
+}
+
+void orbit_counters(const NNIndex *ix, long long *expansions, long long *rescored) {
+    const OrbitIndex *o = ix->orbit;
+    *expansions = o ? o->last_expansions : 0;
+    *rescored = o ? o->last_rescored : 0;
 }
 
 }  // namespace tiler

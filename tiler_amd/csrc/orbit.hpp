@@ -37,17 +37,20 @@ struct OrbitIndex {
     // per-call scratch
     void *qfrag = nullptr, *qrowh = nullptr;
     OrbitStat *qstat = nullptr;
+    double *thr_real = nullptr;
     size_t cap_q = 0;
     float *key = nullptr;
     int *id = nullptr;
     size_t cap_keys = 0;
-    long long last_expansions = 0;
+    int *d_stats = nullptr;         // [2] expansion passes, candidates rescored (TILER_ORBIT_STATS=1)
+    long long last_expansions = 0, last_rescored = 0;
 };
 
 // generic tier-2 / tier-3 plumbing the orbit rescore feeds (owned by nn_search.hip)
 struct OrbitTail {
-    const QStat *gqstat;          // generic per-query stats: tier-2 threshold in the generic key domain
-    double gN, gH, gEc;
+    void *gqfrag;                 // generic query fragments (tier 2 B operands; filled for tier-2 queries only)
+    double gN, gH, gEc;           // generic dataset bounds: tier-2 threshold in the generic key domain
+    void *thr_real;               // [nq] double: real-key threshold of each tier-2 query (orbit scratch)
     int *fb_list, *fb_count, *ex_list, *ex_count, fb_max;
     float *thr;
     int *out_idx;
@@ -63,6 +66,8 @@ struct OrbitTail {
 int orbit_build(NNIndex *ix, hipStream_t stream);
 void orbit_destroy(OrbitIndex *o);
 inline long long orbit_groups(const NNIndex *ix) { return ix->orbit ? ((const OrbitIndex *)ix->orbit)->G : 0; }
+// rescore counters of the last search (TILER_ORBIT_STATS=1, else 0): 4-entry expansion passes, candidates rescored
+void orbit_counters(const NNIndex *ix, long long *expansions, long long *rescored);
 // k = 1 search of nq fp32 query rows: query prep, orbit shortlist, orbit rescore (tiers 2/3 by the caller)
 int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, hipStream_t stream);
 

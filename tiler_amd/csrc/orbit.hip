@@ -545,7 +545,7 @@ __device__ __forceinline__ float wave_min_f(float v) {
 
 static constexpr int ORB_XB = ORB_XBATCH;  // 16-byte loads in flight per lane in the re-key
 
-// Re-key 4 list entries at once: lane = (slot e, tile j, isotypic block x).  Each lane forms the 48-d partial
+// Re-key 2 list entries per half-wave: lane = (slot e, tile j, isotypic block x).  Each lane forms the 48-d partial
 // dot d_x of its tile from the fp16 rows; a 2-stage Walsh-Hadamard butterfly over the 4 lanes of a tile turns
 // (d_0..d_3) into the 4 mirror values V_m = sum_x chi_x(m) d_x, m = x of the lane.  Returns the candidate of
 // mirror slot m (or -1) and its key ||c||^2 - 2 V_m.  `id` / `h`: the entry of this lane's slot (-1: none).
@@ -587,45 +587,66 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
     return cand;
 }
 
-static constexpr int ORB_QCAP = 128;  // rescore queue per wave
-static constexpr int ORB_STG = 8;     // candidate rows staged in LDS per pass
+// The rescore runs one query per HALF-wave (32 lanes): it is latency-bound (list -> re-key -> rows ->
+// reference distances), so two independent chains per wave double the work in flight.  Every cross-lane
+// operation below stays inside the half (xor offsets < 32, ballots masked to the half).
+static constexpr int ORB_QCAP = 64;  // rescore queue per query
+static constexpr int ORB_STG = 4;    // candidate rows staged in LDS per pass
+
+__device__ __forceinline__ float half_min_f(float v) {
+    for (int o = 16; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ void half_argmin(float &v, int &i) {
+    for (int o = 16; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(v, o, 64);
+        const int oi = __shfl_xor(i, o, 64);
+        const bool take = (ov < v) || (ov == v && (unsigned)oi < (unsigned)i);
+        v = take ? ov : v;
+        i = take ? oi : i;
+    }
+}
+__device__ __forceinline__ unsigned half_ballot(bool p) {
+    return (unsigned)(__ballot(p) >> (32 * ((threadIdx.x >> 5) & 1)));
+}
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void nn_orbit_rescore_kernel(OrbitRescoreArgs a) {
-    const int lane = threadIdx.x & 63;
-    const long q = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int l = threadIdx.x & 31, hq = threadIdx.x >> 5;  // lane in the half, query slot of the block
+    const int hbase = threadIdx.x & 32;                     // first lane of this half in the wave
+    const long q = (long)blockIdx.x * 8 + hq;
     if (q >= a.nq) return;
     const OrbitTail &t = a.t;
     const OrbitStat st = a.ostat[q];
     if (st.flags & 2) {
-        if (lane == 0) t.ex_list[atomicAdd(t.ex_count, 1)] = (int)q;
+        if (l == 0) t.ex_list[atomicAdd(t.ex_count, 1)] = (int)q;
         return;
     }
-    const int E = a.nsplit * 2 * a.L;
+    const int E = a.nsplit * 2 * a.L;  // <= 32 (orbit_search limits nsplit)
     float ek = INFINITY;
     int eid = -1;
-    if (lane < E) {
-        ek = a.key[q * E + lane];
-        eid = a.id[q * E + lane];
+    if (l < E) {
+        ek = a.key[q * E + l];
+        eid = a.id[q * E + l];
     }
-    const int eh = (lane / a.L) & 1;
+    const int eh = (l / a.L) & 1;
     if (eid < 0) ek = INFINITY;
-    const bool last = lane < E && (lane % a.L) == a.L - 1 && eid >= 0;
-    // 1. the 4 entries with the smallest keys, re-keyed together (one round trip)
-    int sel = -1;  // slot e (lane >> 4) <- entry lane
+    const bool last = l < E && (l % a.L) == a.L - 1 && eid >= 0;
+    // 1. the 2 entries with the smallest keys, re-keyed together (one round trip)
+    int sel = -1;  // slot e (l >> 4) <- entry lane
     bool taken = false;
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
+    for (int r = 0; r < 2; r++) {
         if (r >= a.p1) break;
         float v = (taken || !(ek < INFINITY)) ? INFINITY : ek;
-        int who = lane;
-        wave_argmin(v, who);
+        int who = l;
+        half_argmin(v, who);
         if (v < INFINITY) {
-            if (lane == who) taken = true;
-            if ((lane >> 4) == r) sel = who;
+            if (l == who) taken = true;
+            if ((l >> 4) == r) sel = who;
         }
     }
-    if (__shfl(sel, 0, 64) < 0) {  // empty dataset
-        if (lane == 0) {
+    if (__shfl(sel, hbase, 64) < 0) {  // empty dataset
+        if (l == 0) {
             t.out_idx[q] = -1;
             t.out_err[q] = FLT_MAX;
             if (t.m_tile) {
@@ -638,11 +659,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
         return;
     }
     const int sl = sel < 0 ? 0 : sel;
-    const int sid = __shfl(eid, sl, 64), shh = __shfl(eh, sl, 64);
+    const int sid = __shfl(eid, hbase + sl, 64), shh = __shfl(eh, hbase + sl, 64);
     double k1;
     const int c1 = orbit_expand4(a, q, sel < 0 ? -1 : sid, shh, k1);
     float kk = c1 >= 0 ? (float)k1 : INFINITY;  // rounded: only sets a looser threshold below
-    kk = wave_min_f(kk);
+    kk = half_min_f(kk);
     // 2. thresholds.  Some candidate has real key <= kk + Eo, so the winner's reference
     // distance is <= (n2 + kk + Eo)(1 + g); any candidate c that can reach it has real key <= Tr.
     const double u = 5.9604644775390625e-08;  // 2^-24
@@ -655,8 +676,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
     const double Tb = Tr + Eo;
     // 3. overflow: a full lane list whose worst kept entry can still reach the threshold.  The tier-2
     // threshold (generic key domain) is completed by orbit_fbprep_kernel.
-    if (__any(last && (double)ek <= Tb)) {
-        if (lane == 0) {
+    if (half_ballot(last && (double)ek <= Tb)) {
+        if (l == 0) {
             reinterpret_cast<double *>(t.thr_real)[q] = Tr;
             const int pidx = atomicAdd(t.fb_count, 1);
             if (pidx < t.fb_max)
@@ -666,13 +687,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
         }
         return;
     }
-    // 4. queue every candidate that can reach the threshold; entries beyond the first 4 that can hold
-    // one are re-keyed 4 at a time; then the queue is rescored with the reference distance: candidate rows
-    // are staged in LDS by the whole wave (one round trip), then one lane per candidate sums in order
-    __shared__ int s_cand[4][ORB_QCAP];
-    __shared__ float4 s_row[4][ORB_STG][OD / 4];
-    const int wv = threadIdx.x >> 6;
-    int *sc = s_cand[wv];
+    // 4. queue every candidate that can reach the threshold; entries beyond the first 2 that can hold
+    // one are re-keyed 2 at a time; then the queue is rescored with the reference distance: candidate rows
+    // are staged in LDS by the half-wave (one round trip), then one lane per candidate sums in order
+    __shared__ int s_cand[8][ORB_QCAP];
+    __shared__ float4 s_row[8][ORB_STG][OD / 4];
+    int *sc = s_cand[hq];
     const float *qrow = a.q + q * OD;
     float bd = INFINITY;
     int bi = 0x7fffffff;
@@ -680,18 +700,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
     auto flush = [&]() {
         for (int b0 = 0; b0 < cnt; b0 += ORB_STG) {
             const int nb = min(ORB_STG, cnt - b0);
-            for (int i = lane; i < nb * (OD / 4); i += 64) {
+            for (int i = l; i < nb * (OD / 4); i += 32) {
                 const int r = i / (OD / 4), c4 = i - r * (OD / 4);
-                s_row[wv][r][c4] = reinterpret_cast<const float4 *>(a.rows + (long)sc[b0 + r] * OD)[c4];
+                s_row[hq][r][c4] = reinterpret_cast<const float4 *>(a.rows + (long)sc[b0 + r] * OD)[c4];
             }
             __builtin_amdgcn_wave_barrier();
-            if (lane < nb) {
-                const int c = sc[b0 + lane];
+            if (l < nb) {
+                const int c = sc[b0 + l];
                 const float4 *q4 = reinterpret_cast<const float4 *>(qrow);
                 float dist = 0.0f;
 #pragma unroll ORB_DU
                 for (int i = 0; i < OD / 4; i++) {
-                    const float4 x = q4[i], y = s_row[wv][lane][i];
+                    const float4 x = q4[i], y = s_row[hq][l][i];
                     float tt;
                     tt = x.x - y.x; dist = dist + tt * tt;
                     tt = x.y - y.y; dist = dist + tt * tt;
@@ -710,33 +730,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
     };
     auto enqueue = [&](int c, double k) {
         const bool take = c >= 0 && k <= Tb;
-        const unsigned long long b = __ballot(take);
-        if (take) sc[cnt + __popcll(b & ((1ull << lane) - 1))] = c;
-        cnt += __popcll(b);
+        const unsigned b = half_ballot(take);
+        if (take) sc[cnt + __popc(b & ((1u << l) - 1))] = c;
+        cnt += __popc(b);
         __builtin_amdgcn_wave_barrier();
-        if (cnt > ORB_QCAP - 64) flush();
+        if (cnt > ORB_QCAP - 32) flush();
     };
     enqueue(c1, k1);
-    unsigned long long todo = __ballot(!taken && eid >= 0 && (double)ek <= Tb);
+    unsigned todo = half_ballot(!taken && eid >= 0 && (double)ek <= Tb);
     while (todo) {
         int el = -1;  // slot e <- the e-th remaining entry
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int e = todo ? __builtin_ctzll(todo) : -1;
+        for (int r = 0; r < 2; r++) {
+            const int e = todo ? __builtin_ctz(todo) : -1;
             if (todo) todo &= todo - 1;
-            if ((lane >> 4) == r) el = e;
+            if ((l >> 4) == r) el = e;
         }
         nexp++;
         const int ee = el < 0 ? 0 : el;
-        const int xid = __shfl(eid, ee, 64), xh = __shfl(eh, ee, 64);
+        const int xid = __shfl(eid, hbase + ee, 64), xh = __shfl(eh, hbase + ee, 64);
         double k;
         const int c = orbit_expand4(a, q, el < 0 ? -1 : xid, xh, k);
         enqueue(c, k);
     }
     __builtin_amdgcn_wave_barrier();
     flush();
-    wave_argmin(bd, bi);
-    if (lane == 0) {
+    half_argmin(bd, bi);
+    if (l == 0) {
         if (t.n_expand) {
             atomicAdd(t.n_expand, nexp);
             atomicAdd(t.n_expand + 1, nres);
@@ -936,7 +956,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         return (e && e[0] == '1') ? 1 : 2;
     }();
     const int wgs = (nqblk + ORB_NW * qb - 1) / (ORB_NW * qb);
-    const int max_split = 64 / (2 * ORB_L);
+    const int max_split = 32 / (2 * ORB_L);  // rescore: one list entry per lane of a half-wave
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
     nsplit = std::min(nsplit, o->gblk);
     const int bps = (o->gblk + nsplit - 1) / nsplit;
@@ -1013,8 +1033,8 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.nsplit = nsplit;
     static const int p1 = [] {
         const char *e = getenv("TILER_ORBIT_P1");
-        const int v = e ? atoi(e) : 4;
-        return v < 1 ? 1 : v > 4 ? 4 : v;
+        const int v = e ? atoi(e) : 2;
+        return v < 1 ? 1 : v > 2 ? 2 : v;
     }();
     ra.p1 = p1;
     ra.scale2 = (double)ix->scale * (double)ix->scale;
@@ -1035,7 +1055,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     }
     {
         KTimer tm("nn_rescore", stream);
-        hipLaunchKernelGGL(nn_orbit_rescore_kernel, dim3((nq + 3) / 4), dim3(256), 0, stream, ra);
+        hipLaunchKernelGGL(nn_orbit_rescore_kernel, dim3((nq + 7) / 8), dim3(256), 0, stream, ra);
     }
     TILER_HIP_CHECK(hipGetLastError());
     {

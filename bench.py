@@ -180,9 +180,12 @@ def main():
     sec = sl["ms_avg"] * 1e-3 if sl["ms_avg"] else None
     achieved = flops_launch / sec / 1e12 if sec else None
     issued = issued_launch / sec / 1e12 if sec else None
+    kname = "nn_orbit_shortlist_kernel" if orbit else "nn_shortlist16_kernel"
+    traffic, traffic_src = pmc_traffic(kname)
     roofline = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None, "peak": PEAK_F16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
-                "traffic": None,
+                "traffic": traffic, "traffic_unit": "bytes/launch (HBM, FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": traffic_src,
                 "kernel": ORBIT_KERNEL if orbit else
                 SHORTLIST_KERNELS.get(os.environ.get("TILER_SHORTLIST", ""), SHORTLIST_KERNELS["q16"]),
                 "issued_tflops": round(issued, 2) if issued else None,
@@ -231,6 +234,20 @@ def main():
     kdt.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json,
+    written by profiles/summarize.py from profiles/run_profile.sh on the GPU box; counters cannot be
+    collected inside the timed run)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        k = t["kernels"][kernel]
+        return int(k["hbm_traffic_bytes"]), f"profiles/pmc_traffic.json ({t['source']})"
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out_hm, out_vm, out_err):

@@ -82,5 +82,21 @@ def summarize(d: str) -> dict:
     return out
 
 
+def traffic_table(summary: dict) -> dict:
+    """Per-launch HBM bytes by kernel (read by bench.py for roofline.traffic)."""
+    t = {"source": summary["source"], "kernels": {}}
+    for k, v in summary["kernels"].items():
+        pm = v.get("pmc", {})
+        if "hbm_traffic_bytes" in pm:
+            t["kernels"][k] = {"hbm_traffic_bytes": pm["hbm_traffic_bytes"], "hbm_read_bytes_raw": pm["hbm_read_bytes_raw"],
+                               "hbm_write_bytes": pm["hbm_write_bytes"],
+                               "avg_ms_trace": v.get("trace", {}).get("avg_ms")}
+    return t
+
+
 if __name__ == "__main__":
-    print(json.dumps(summarize(sys.argv[1]), indent=1))
+    summ = summarize(sys.argv[1])
+    print(json.dumps(summ, indent=1))
+    if len(sys.argv) > 2:  # also write the per-launch traffic table
+        with open(sys.argv[2], "w") as f:
+            json.dump(traffic_table(summ), f, indent=1)

@@ -126,6 +126,21 @@ int tiler_kmodes_compute(const uint8_t *X, int n, int nattr, int k, int start_po
  * counts[j] = 0 for empty clusters.  X[n][80], labels[n] in 0..k-1, centroids[k][80]. */
 int tiler_kmodes_medoids(const uint8_t *X, int n, const int32_t *labels, const uint8_t *centroids, int k,
                          int32_t *medoid, int32_t *counts);
+/* All of DoGlobalTiling's palette bins in one call (DoKModes per bin, main.pas:4195-4254, which the
+ * reference runs concurrently with ProcThreadPool at main.pas:4339): X[N][80] with bin b = rows
+ * [bin_off[b], bin_off[b+1]), k[b] clusters and start[b] (bin-local) per bin; labels[N] bin-local,
+ * centroids[sum k][80] bin after bin; n_iter[b] / cost[b] optional.  Each bin's result is exactly
+ * tiler_kmodes_compute's on that bin alone.  Returns 0 or -1. */
+int tiler_kmodes_batch(const uint8_t *X, const int32_t *bin_off, int nbins, const int32_t *k, const int32_t *start,
+                       int n_modalities, int32_t *labels, uint8_t *centroids, int32_t *n_iter, uint64_t *cost);
+/* The same with X / labels / centroids in HBM (X 16-byte aligned) on a HIP stream (NULL = default);
+ * bin_off / k / start / n_iter / cost are host arrays.  Synchronous. */
+int tiler_kmodes_batch_dev(const uint8_t *d_X, const int32_t *bin_off, int nbins, const int32_t *k,
+                           const int32_t *start, int n_modalities, int32_t *d_labels, uint8_t *d_centroids,
+                           int32_t *n_iter, uint64_t *cost, void *stream);
+/* Medoids of every bin's clusters (as tiler_kmodes_medoids per bin): medoid[sum k] bin-local rows. */
+int tiler_kmodes_medoids_batch(const uint8_t *X, const int32_t *bin_off, int nbins, const int32_t *k,
+                               const int32_t *labels, const uint8_t *centroids, int32_t *medoid, int32_t *counts);
 
 #ifdef __cplusplus
 }

@@ -64,6 +64,12 @@ _SIGS = {
     "tiler_smooth_keyframe_dev": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_double, c_void_p]),
     "tiler_kmodes_medoids": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "tiler_kmodes_batch": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                   c_void_p, c_void_p]),
+    "tiler_kmodes_batch_dev": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p]),
+    "tiler_kmodes_medoids_batch": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p]),
     "tiler_kmodes_compute": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
 }

@@ -548,4 +548,28 @@ int tiler_kmodes_compute(const uint8_t *X, int n, int nattr, int k, int start_po
     return kmodes_compute_host(X, n, nattr, k, start_point, n_modalities, labels, centroids, n_iter, cost);
 }
 
+int tiler_kmodes_batch(const uint8_t *X, const int32_t *bin_off, int nbins, const int32_t *k, const int32_t *start,
+                       int n_modalities, int32_t *labels, uint8_t *centroids, int32_t *n_iter, uint64_t *cost) {
+    if (!ensure_init()) return -1;
+    return kmodes_batch_host(X, bin_off, nbins, k, start, n_modalities, labels, centroids, n_iter, cost);
+}
+
+int tiler_kmodes_batch_dev(const uint8_t *d_X, const int32_t *bin_off, int nbins, const int32_t *k,
+                           const int32_t *start, int n_modalities, int32_t *d_labels, uint8_t *d_centroids,
+                           int32_t *n_iter, uint64_t *cost, void *stream) {
+    if (!ensure_init()) return -1;
+    if (!d_X || !bin_off || !k || !start || !d_labels || !d_centroids) {
+        set_error("kmodes: null buffer");
+        return -1;
+    }
+    return kmodes_batch_dev(d_X, bin_off, nbins, k, start, n_modalities, d_labels, d_centroids, n_iter, cost,
+                            (hipStream_t)stream);
+}
+
+int tiler_kmodes_medoids_batch(const uint8_t *X, const int32_t *bin_off, int nbins, const int32_t *k,
+                               const int32_t *labels, const uint8_t *centroids, int32_t *medoid, int32_t *counts) {
+    if (!ensure_init()) return -1;
+    return kmodes_medoids_batch_host(X, bin_off, nbins, k, labels, centroids, medoid, counts);
+}
+
 }  // extern "C"

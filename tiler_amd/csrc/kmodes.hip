@@ -13,6 +13,11 @@
 //   KModesIter           : per 960-point bin: parallel assignment vs the CURRENT centroids, then one
 //                          workgroup applies the bin's moves in order (MovePointCat over 80 lanes,
 //                          rescue with a workgroup-parallel argmax and ordered member selection)
+// Batched over GlobalTiling's palette bins (DoKModes per bin, main.pas:4195-4254, run in parallel by
+// ProcThreadPool at main.pas:4339): every phase is one launch for all still-running bins -- bins sorted by
+// size so the bins alive in farthest-first round j are a prefix, work lists flattened over (bin, block),
+// one sequential workgroup per bin -- so launch count follows the LARGEST bin, not the sum.  A single
+// ComputeKModes call is a batch of one.
 #include <stdint.h>
 #include <string.h>
 
@@ -260,7 +265,7 @@ __device__ void move_point_cat(const KmState &s, int ip, int to, int from) {
     }
 }
 
-__global__ __launch_bounds__(128) void km_bin_seq(KmState s, int p0, int p1) {
+__device__ void bin_seq_body(KmState s, int p0, int p1) {
     __shared__ int sh_i[4];
     __shared__ unsigned long long sh_best[128];
     __shared__ int sh_cnt[128];
@@ -326,197 +331,638 @@ __global__ __launch_bounds__(128) void km_bin_seq(KmState s, int p0, int p1) {
     }
 }
 
-static int km_run(KmState &s, int start, int *n_iter, unsigned long long *cost_out, hipStream_t st) {
-    const int n = s.n, K = s.K;
-    const int nblk_ff = std::min(1024, (n + 255) / 256);
-    // InitFarthestFirst
-    hipLaunchKernelGGL(km_fill_u64, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, st, s.mind, (long)n, ~0ull);
-    TILER_HIP_CHECK(hipMemsetAsync(s.used, 0, n, st));
-    TILER_HIP_CHECK(hipMemsetAsync(s.cent, 0xff, (size_t)K * KM_A, st));
-    TILER_HIP_CHECK(hipMemcpyAsync(s.center, &start, sizeof(int), hipMemcpyHostToDevice, st));
-    TILER_HIP_CHECK(hipMemcpyAsync(s.cent, s.X + (long)start * KM_A, KM_A, hipMemcpyDeviceToDevice, st));
-    {
-        const uint8_t one = 1;
-        TILER_HIP_CHECK(hipMemcpyAsync(s.used + start, &one, 1, hipMemcpyHostToDevice, st));
-    }
-    {
-        KTimer tm("kmodes_init", st);
-        for (int j = 0; j < K; j++) {
-            hipLaunchKernelGGL(km_ff_update, dim3(nblk_ff), dim3(256), 0, st, s, j);
-            if (j + 1 < K) hipLaunchKernelGGL(km_ff_select, dim3(1), dim3(256), 0, st, s, j + 1, nblk_ff);
-        }
-    }
-    TILER_HIP_CHECK(hipGetLastError());
-    // initial assignment + modes
-    const int csplit = std::max(1, std::min(64, (K + 511) / 512));
-    hipLaunchKernelGGL(km_fill_u64, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, st, s.akey, (long)n, ~0ull);
-    {
-        KTimer tm("kmodes_assign", st);
-        hipLaunchKernelGGL(km_assign, dim3((n + 255) / 256, csplit), dim3(256), 0, st, s, 0, n, csplit);
-    }
-    TILER_HIP_CHECK(hipMemsetAsync(s.csize, 0, (size_t)K * 4, st));
-    TILER_HIP_CHECK(hipMemsetAsync(s.freq, 0, (size_t)K * KM_A * s.M * 4, st));
-    hipLaunchKernelGGL(km_init_hist, dim3(std::min(2048, (n + 255) / 256)), dim3(256), 0, st, s);
-    int32_t *rand_rows = nullptr;
-    TILER_HIP_CHECK(hipMallocAsync((void **)&rand_rows, (size_t)K * KM_A * 4, st));
-    hipLaunchKernelGGL(km_init_modes, dim3(1), dim3(64), 0, st, s, rand_rows);
-    hipLaunchKernelGGL(km_init_modes2, dim3(std::min(4096, (K * KM_A + 255) / 256)), dim3(256), 0, st, s, rand_rows);
-    TILER_HIP_CHECK(hipFreeAsync(rand_rows, st));
-    TILER_HIP_CHECK(hipGetLastError());
-    // iterations (kmodes.pas:1023-1039)
-    unsigned long long cost = ~0ull;
-    int itr = 0;
-    struct {
-        unsigned long long cost;
-        int moves;
-        int err;
-    } h;
-    for (;;) {
-        itr++;
-        TILER_HIP_CHECK(hipMemsetAsync(s.cost, 0, 8, st));
-        TILER_HIP_CHECK(hipMemsetAsync(s.moves, 0, 4, st));
-        for (int b0 = 0; b0 < n; b0 += KM_BIN) {
-            const int b1 = std::min(n, b0 + KM_BIN);
-            hipLaunchKernelGGL(km_fill_u64, dim3((b1 - b0 + 255) / 256), dim3(256), 0, st, s.akey + b0, (long)(b1 - b0),
-                               ~0ull);
-            {
-                KTimer tm("kmodes_assign", st);
-                hipLaunchKernelGGL(km_assign, dim3((b1 - b0 + 255) / 256, csplit), dim3(256), 0, st, s, b0, b1, csplit);
-            }
-            {
-                KTimer tm("kmodes_seq", st);
-                hipLaunchKernelGGL(km_bin_seq, dim3(1), dim3(128), 0, st, s, b0, b1);
-            }
-        }
-        TILER_HIP_CHECK(hipGetLastError());
-        TILER_HIP_CHECK(hipMemcpyAsync(&h.cost, s.cost, 8, hipMemcpyDeviceToHost, st));
-        TILER_HIP_CHECK(hipMemcpyAsync(&h.moves, s.moves, 4, hipMemcpyDeviceToHost, st));
-        TILER_HIP_CHECK(hipMemcpyAsync(&h.err, s.err, 4, hipMemcpyDeviceToHost, st));
-        TILER_HIP_CHECK(hipStreamSynchronize(st));
-        if (h.err) {
-            set_error("kmodes: farthest-first ran out of points (k > n)");
-            return -1;
-        }
-        const bool conv = (h.cost >= cost) || (h.moves == 0);
-        cost = h.cost;
-        if (conv) break;
-    }
-    if (n_iter) *n_iter = itr;
-    if (cost_out) *cost_out = cost;
-    return 0;
+// ---- batched state: the single-bin KmState of bin b is a view into concatenated arrays ----
+struct KmBatch {
+    const uint8_t *X;             // [N][80], bins contiguous, rows 16-byte aligned
+    const int32_t *boff, *koff;   // [nb+1] point / cluster offsets
+    const int32_t *poff;          // [nb+1] farthest-first partial slots (blocks) per bin
+    int nb, M;
+    int32_t *memb;                // [N] bin-local labels
+    uint8_t *cent;                // [Ktot][80]
+    int32_t *freq;                // [Ktot][80][M]
+    int32_t *csize;               // [Ktot]
+    unsigned long long *mind;     // [N]
+    uint8_t *used;                // [N]
+    unsigned long long *part;     // [poff[nb]]
+    int32_t *center;              // [Ktot]
+    unsigned long long *akey;     // [N]
+    unsigned *seed;               // [nb]
+    unsigned long long *cost;     // [nb]
+    int *moves, *err, *ffdone;    // [nb]
+};
+
+__device__ __forceinline__ KmState bin_state(const KmBatch &B, int b) {
+    KmState s;
+    const long p0 = B.boff[b], k0 = B.koff[b];
+    s.X = B.X + p0 * KM_A;
+    s.n = (int)(B.boff[b + 1] - p0);
+    s.K = (int)(B.koff[b + 1] - k0);
+    s.M = B.M;
+    s.memb = B.memb + p0;
+    s.cent = B.cent + k0 * KM_A;
+    s.freq = B.freq + k0 * KM_A * B.M;
+    s.csize = B.csize + k0;
+    s.mind = B.mind + p0;
+    s.used = B.used + p0;
+    s.part = B.part + B.poff[b];
+    s.center = B.center + k0;
+    s.akey = B.akey + p0;
+    s.seed = B.seed + b;
+    s.cost = B.cost + b;
+    s.moves = B.moves + b;
+    s.err = B.err + b;
+    return s;
 }
 
-int kmodes_compute_dev(const uint8_t *d_X, int n, int k, int start_point, int n_modalities, int32_t *d_labels,
-                       uint8_t *d_centroids, int *n_iter, uint64_t *cost, hipStream_t st) {
-    if (n <= 0 || k <= 0 || k > n || start_point < 0 || start_point >= n || n_modalities <= 0 || n_modalities > 256) {
-        set_error("kmodes: invalid arguments (need 0 < k <= n, 0 <= start < n, 0 < modalities <= 256)");
-        return -1;
+__device__ __forceinline__ int bin_of(const int32_t *off, int nb, long i) {  // off[b] <= i < off[b+1]
+    int lo = 0, hi = nb - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= i) lo = mid; else hi = mid - 1;
     }
-    if (((uintptr_t)d_X & 15) != 0) {
-        set_error("kmodes: X must be 16-byte aligned");
-        return -1;
+    return lo;
+}
+
+// farthest-first start (kmodes.pas:698-710): one thread per bin
+__global__ void kmb_ff_start(KmBatch B, const int32_t *start) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B.nb) return;
+    KmState s = bin_state(B, b);
+    const int st = start[b];
+    s.center[0] = st;
+    for (int a = 0; a < KM_A; a++) s.cent[a] = s.X[(long)st * KM_A + a];
+    s.used[st] = 1;
+}
+
+// one farthest-first round j for every bin with K > j (a prefix of the K-sorted bins): work item =
+// (bin, block of that bin); the last block of a bin to finish (counter ffdone) selects centre j + 1
+struct KmFfItem {
+    int bin, sub, nsub, pad;
+};
+
+__global__ __launch_bounds__(256) void kmb_ff_round(KmBatch B, const KmFfItem *items, int j) {
+    __shared__ unsigned long long best[256];
+    __shared__ int last;
+    const KmFfItem it = items[blockIdx.x];
+    KmState s = bin_state(B, it.bin);
+    const int c = s.center[j];
+    uint32_t item[20];
+    load_row(s.X + (long)c * KM_A, item);
+    unsigned long long bv = 0;
+    int bi = -1;
+    for (long i = (long)it.sub * 256 + threadIdx.x; i < s.n; i += (long)it.nsub * 256) {
+        uint32_t row[20];
+        load_row(s.X + i * KM_A, row);
+        const unsigned long long d = km_dissim(row, item);
+        unsigned long long m = s.mind[i];
+        if (d < m) {  // cmovb: strict-less (kmodes.pas:555-558); the 'used' skip is a no-op (567)
+            m = d;
+            s.mind[i] = m;
+        }
+        if (!s.used[i] && m >= bv) {  // ascending i within a thread: '>=' keeps the last
+            bv = m;
+            bi = (int)i;
+        }
     }
-    KmState s{};
-    s.X = d_X;
-    s.n = n;
-    s.K = k;
-    s.M = n_modalities;
-    s.memb = d_labels;
-    // centroid storage must be 16-byte aligned rows of 80 B: use a private buffer
-    char *buf = nullptr;
-    const int nblk_ff = std::min(1024, (n + 255) / 256);
-    size_t off = 0;
-    auto carve = [&](size_t bytes) {
-        size_t o = off;
-        off += (bytes + 255) & ~(size_t)255;
-        return o;
-    };
-    const size_t o_cent = carve((size_t)k * KM_A), o_freq = carve((size_t)k * KM_A * n_modalities * 4),
-                 o_csize = carve((size_t)k * 4), o_mind = carve((size_t)n * 8), o_used = carve(n),
-                 o_part = carve((size_t)nblk_ff * 8), o_center = carve((size_t)k * 4), o_akey = carve((size_t)n * 8),
-                 o_misc = carve(64);
-    TILER_HIP_CHECK(hipMalloc((void **)&buf, off));
-    s.cent = (uint8_t *)(buf + o_cent);
-    s.freq = (int32_t *)(buf + o_freq);
-    s.csize = (int32_t *)(buf + o_csize);
-    s.mind = (unsigned long long *)(buf + o_mind);
-    s.used = (uint8_t *)(buf + o_used);
-    s.part = (unsigned long long *)(buf + o_part);
-    s.center = (int32_t *)(buf + o_center);
-    s.akey = (unsigned long long *)(buf + o_akey);
-    s.seed = (unsigned *)(buf + o_misc);
-    s.cost = (unsigned long long *)(buf + o_misc + 8);
-    s.moves = (int *)(buf + o_misc + 16);
-    s.err = (int *)(buf + o_misc + 20);
-    const unsigned seed0 = 0x42381337u;  // ComputeKModes kmodes.pas:930
-    int rc = -1;
-    do {
-        if (hipMemsetAsync(buf + o_misc, 0, 64, st) != hipSuccess) break;
-        if (hipMemcpyAsync(s.seed, &seed0, 4, hipMemcpyHostToDevice, st) != hipSuccess) break;
-        unsigned long long c = 0;
-        if (km_run(s, start_point, n_iter, &c, st)) break;
-        if (cost) *cost = c;
-        if (hipMemcpyAsync(d_centroids, s.cent, (size_t)k * KM_A, hipMemcpyDeviceToDevice, st) != hipSuccess) break;
-        if (hipStreamSynchronize(st) != hipSuccess) break;
-        rc = 0;
-    } while (0);
-    (void)hipFree(buf);
-    return rc;
+    // block reduce (value max, ties -> larger index); value fits 32 bits (dis < 2^19) unless UINT64_MAX
+    const unsigned long long v32 = bv > 0xFFFFFFFFull ? 0xFFFFFFFFull : bv;
+    best[threadIdx.x] = (bi < 0) ? 0ull : ((v32 << 32) | (unsigned)(bi + 1));
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) best[threadIdx.x] = max(best[threadIdx.x], best[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (j + 1 >= s.K) return;  // last round of this bin: no selection
+    if (threadIdx.x == 0) {
+        s.part[it.sub] = best[0];
+        __threadfence();
+        last = atomicAdd(&B.ffdone[it.bin], 1) == it.nsub - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    unsigned long long bb = 0;
+    for (int i = threadIdx.x; i < it.nsub; i += 256)  // device-scope loads: bypass a stale L1 line of an earlier round
+        bb = max(bb, __hip_atomic_load(&s.part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    best[threadIdx.x] = bb;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) best[threadIdx.x] = max(best[threadIdx.x], best[threadIdx.x + o]);
+        __syncthreads();
+    }
+    const unsigned long long w = best[0];
+    const int f = (w == 0) ? -1 : (int)(w & 0xFFFFFFFFull) - 1;
+    if (threadIdx.x == 0) B.ffdone[it.bin] = 0;
+    if (f < 0) {
+        if (threadIdx.x == 0) *s.err = 1;
+        return;
+    }
+    if (threadIdx.x < KM_A) s.cent[(long)(j + 1) * KM_A + threadIdx.x] = s.X[(long)f * KM_A + threadIdx.x];
+    if (threadIdx.x == 0) {
+        s.center[j + 1] = f;
+        s.used[f] = 1;
+    }
+}
+
+// assignment work item: points [p0, p1) of bin vs its centroids [c0, c1): akey = min(dis << 32 | ~c)
+struct KmAsgItem {
+    int bin, p0, p1, c0, c1, pad[3];
+};
+
+__global__ __launch_bounds__(256) void kmb_assign(KmBatch B, const KmAsgItem *items) {
+    __shared__ uint4 ct[128 * 5];
+    const KmAsgItem it = items[blockIdx.x];
+    KmState s = bin_state(B, it.bin);
+    const long i = it.p0 + threadIdx.x;
+    const bool valid = i < it.p1;
+    uint32_t item[20];
+    if (valid) load_row(s.X + i * KM_A, item);
+    unsigned long long best = ~0ull;
+    for (int t0 = it.c0; t0 < it.c1; t0 += 128) {
+        const int cnt = min(128, it.c1 - t0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < cnt * 5; e += 256)
+            ct[e] = reinterpret_cast<const uint4 *>(s.cent + (long)t0 * KM_A)[e];
+        __syncthreads();
+        if (valid) {
+            for (int c = 0; c < cnt; c++) {
+                uint32_t row[20];
+#pragma unroll
+                for (int q = 0; q < 5; q++) {
+                    const uint4 v = ct[c * 5 + q];
+                    row[4 * q] = v.x;
+                    row[4 * q + 1] = v.y;
+                    row[4 * q + 2] = v.z;
+                    row[4 * q + 3] = v.w;
+                }
+                const unsigned long long d = km_dissim(row, item);
+                const unsigned long long key = (d << 32) | (0xFFFFFFFFu - (unsigned)(t0 + c));
+                best = key < best ? key : best;
+            }
+        }
+    }
+    if (valid) atomicMin(&s.akey[i], best);
+}
+
+// initial labels + histograms (ComputeKModes kmodes.pas:984-1008), all points of all bins
+__global__ __launch_bounds__(256) void kmb_init_hist(KmBatch B, long N) {
+    for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < N; g += (long)gridDim.x * 256) {
+        const int b = bin_of(B.boff, B.nb, g);
+        KmState s = bin_state(B, b);
+        const long i = g - B.boff[b];
+        const int c = (int)(0xFFFFFFFFu - (unsigned)(s.akey[i] & 0xFFFFFFFFull));
+        s.memb[i] = c;
+        atomicAdd(&s.csize[c], 1);
+        for (int a = 0; a < KM_A; a++) atomicAdd(&s.freq[((long)c * KM_A + a) * s.M + s.X[i * KM_A + a]], 1);
+    }
+}
+
+// modes (kmodes.pas:1010-1021): empty clusters take X[RandInt(n)][a] per attribute in (k, a) order
+__global__ void kmb_init_modes(KmBatch B, int32_t *rand_rows) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B.nb) return;
+    KmState s = bin_state(B, b);
+    int32_t *rr = rand_rows + (long)B.koff[b] * KM_A;
+    unsigned seed = *s.seed;
+    for (int k = 0; k < s.K; k++)
+        if (s.csize[k] == 0)
+            for (int a = 0; a < KM_A; a++) rr[(long)k * KM_A + a] = (int)km_randint((unsigned)s.n, &seed);
+    *s.seed = seed;
+}
+
+__global__ __launch_bounds__(256) void kmb_init_modes2(KmBatch B, const int32_t *rand_rows, long ktot) {
+    for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < ktot * KM_A; e += (long)gridDim.x * 256) {
+        const long kg = e / KM_A;
+        const int a = (int)(e % KM_A);
+        const int b = bin_of(B.koff, B.nb, kg);
+        KmState s = bin_state(B, b);
+        const long el = e - (long)B.koff[b] * KM_A;  // bin-local element (k, a)
+        const int k = (int)(el / KM_A);
+        if (s.csize[k] == 0) {
+            s.cent[el] = s.X[(long)rand_rows[e] * KM_A + a];
+        } else {
+            const int32_t *f = s.freq + el * s.M;
+            int bi = -1, bv = INT32_MIN;
+            for (int m = 0; m < s.M; m++)
+                if (f[m] > bv) {
+                    bv = f[m];
+                    bi = m;
+                }
+            s.cent[el] = (uint8_t)bi;  // GetMaxValueIndex: first max (kmodes.pas:149-161)
+        }
+    }
+}
+
+// one 960-point chunk of each listed bin, applied in order (KModesIter kmodes.pas:869-911)
+struct KmSeqItem {
+    int bin, p0, p1, pad;
+};
+
+// seq items live in the same work list as the assign items (one KmAsgItem slot each)
+__global__ __launch_bounds__(128) void kmb_seq_strided(KmBatch B, const KmAsgItem *items) {
+    const KmSeqItem it = *reinterpret_cast<const KmSeqItem *>(items + blockIdx.x);
+    KmState s = bin_state(B, it.bin);
+    bin_seq_body(s, it.p0, it.p1);
 }
 
 // ---- DoKModes medoid choice (main.pas:4231-4253): per cluster j with members, the member minimising
 // dissim(member, centroid_j) (GetMinMatchingDissim(ToMerge, LocCentroids[j]) -> ties: last member) ----
-__global__ __launch_bounds__(256) void km_medoid_kernel(const uint8_t *X, int n, const int32_t *labels,
-                                                        const uint8_t *cent, unsigned long long *best,
-                                                        int32_t *counts) {
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-        const int j = labels[i];
+__global__ __launch_bounds__(256) void kmb_medoid(const uint8_t *X, const int32_t *boff, const int32_t *koff, int nb,
+                                                  long N, const int32_t *labels, const uint8_t *cent,
+                                                  unsigned long long *best, int32_t *counts) {
+    for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < N; g += (long)gridDim.x * 256) {
+        const int b = bin_of(boff, nb, g);
+        const long i = g - boff[b];
+        const long j = koff[b] + labels[g];
         uint32_t row[20], item[20];
-        load_row(X + i * KM_A, row);
-        load_row(cent + (long)j * KM_A, item);
+        load_row(X + g * KM_A, row);
+        load_row(cent + j * KM_A, item);
         const unsigned long long d = km_dissim(row, item);
         atomicMin(&best[j], (d << 32) | (0xFFFFFFFFu - (unsigned)i));
         atomicAdd(&counts[j], 1);
     }
 }
 
-int kmodes_medoids_host(const uint8_t *X, int n, const int32_t *labels, const uint8_t *centroids, int k,
-                        int32_t *medoid, int32_t *counts) {
-    if (n < 0 || k <= 0 || (n > 0 && (!X || !labels)) || !centroids || !medoid || !counts) {
-        set_error("kmodes_medoids: invalid arguments");
+// ---- host driver ----
+static int csplit_of(int K) { return std::max(1, std::min(64, (K + 511) / 512)); }
+
+int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const int32_t *h_k, const int32_t *h_start,
+                     int n_modalities, int32_t *d_labels, uint8_t *d_centroids, int32_t *h_iter, uint64_t *h_cost,
+                     hipStream_t st) {
+    if (nb <= 0 || !h_boff || !h_k || !h_start || n_modalities <= 0 || n_modalities > 256) {
+        set_error("kmodes: invalid arguments (need bins, cluster counts, starts, 0 < modalities <= 256)");
         return -1;
     }
-    for (int i = 0; i < n; i++)
-        if (labels[i] < 0 || labels[i] >= k) {
-            set_error("kmodes_medoids: label out of range");
+    if (((uintptr_t)d_X & 15) != 0) {
+        set_error("kmodes: X must be 16-byte aligned");
+        return -1;
+    }
+    for (int b = 0; b < nb; b++) {
+        const int n = h_boff[b + 1] - h_boff[b];
+        if (n <= 0 || h_k[b] <= 0 || h_k[b] > n || h_start[b] < 0 || h_start[b] >= n) {
+            set_error("kmodes: invalid bin (need 0 < k <= n, 0 <= start < n)");
             return -1;
         }
+    }
+    // process bins in descending K (ties: size) so the bins alive in farthest-first round j are a prefix;
+    // the caller's arrays stay in caller order: the permutation only renames bins inside this call
+    std::vector<int> ord(nb);
+    for (int b = 0; b < nb; b++) ord[b] = b;
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return h_k[x] > h_k[y]; });
+    std::vector<int32_t> koff_c(nb + 1, 0);  // caller-order cluster offsets (output layout)
+    for (int b = 0; b < nb; b++) koff_c[b + 1] = koff_c[b] + h_k[b];
+    std::vector<int32_t> boff(nb + 1, 0), koff(nb + 1, 0), poff(nb + 1, 0), start(nb), Kv(nb), nv(nb);
+    for (int r = 0; r < nb; r++) {
+        const int b = ord[r];
+        nv[r] = h_boff[b + 1] - h_boff[b];
+        Kv[r] = h_k[b];
+        start[r] = h_start[b];
+        boff[r + 1] = boff[r] + nv[r];
+        koff[r + 1] = koff[r] + Kv[r];
+        poff[r + 1] = poff[r] + std::min(256, (nv[r] + 255) / 256);
+    }
+    const long N = boff[nb], Ktot = koff[nb];
+    const int M = n_modalities;
+    // device workspace
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    const size_t o_X = carve((size_t)N * KM_A), o_boff = carve((nb + 1) * 4), o_koff = carve((nb + 1) * 4),
+                 o_poff = carve((nb + 1) * 4), o_start = carve(nb * 4), o_memb = carve((size_t)N * 4),
+                 o_cent = carve((size_t)Ktot * KM_A), o_freq = carve((size_t)Ktot * KM_A * M * 4),
+                 o_csize = carve((size_t)Ktot * 4), o_mind = carve((size_t)N * 8), o_used = carve(N),
+                 o_part = carve((size_t)poff[nb] * 8), o_center = carve((size_t)Ktot * 4), o_akey = carve((size_t)N * 8),
+                 o_seed = carve(nb * 4), o_cost = carve(nb * 8), o_moves = carve(nb * 4), o_err = carve(nb * 4),
+                 o_ffd = carve(nb * 4), o_rand = carve((size_t)Ktot * KM_A * 4), o_items = carve(0);
     char *buf = nullptr;
-    const size_t oX = 0, oL = ((size_t)n * KM_A + 255) & ~(size_t)255, oC = oL + (((size_t)n * 4 + 255) & ~(size_t)255),
-                 oB = oC + (((size_t)k * KM_A + 255) & ~(size_t)255), oN = oB + (size_t)k * 8, total = oN + (size_t)k * 4;
-    TILER_HIP_CHECK(hipMalloc((void **)&buf, total));
+    // the largest work list: one iteration's chunk items for every bin
+    size_t max_items = 0;
+    for (int r = 0; r < nb; r++) {
+        const int nch = (nv[r] + KM_BIN - 1) / KM_BIN;
+        max_items += (size_t)nch * ((KM_BIN + 255) / 256) * csplit_of(Kv[r]) + nch;
+        max_items += (size_t)((nv[r] + 255) / 256) * csplit_of(Kv[r]);
+    }
+    const size_t item_bytes = (max_items + (size_t)poff[nb] + 64) * sizeof(KmAsgItem);
+    TILER_HIP_CHECK(hipMalloc((void **)&buf, off + item_bytes));
+    char *items = buf + o_items;
+    KmBatch B;
+    B.X = (const uint8_t *)(buf + o_X);
+    B.boff = (const int32_t *)(buf + o_boff);
+    B.koff = (const int32_t *)(buf + o_koff);
+    B.poff = (const int32_t *)(buf + o_poff);
+    B.nb = nb;
+    B.M = M;
+    B.memb = (int32_t *)(buf + o_memb);
+    B.cent = (uint8_t *)(buf + o_cent);
+    B.freq = (int32_t *)(buf + o_freq);
+    B.csize = (int32_t *)(buf + o_csize);
+    B.mind = (unsigned long long *)(buf + o_mind);
+    B.used = (uint8_t *)(buf + o_used);
+    B.part = (unsigned long long *)(buf + o_part);
+    B.center = (int32_t *)(buf + o_center);
+    B.akey = (unsigned long long *)(buf + o_akey);
+    B.seed = (unsigned *)(buf + o_seed);
+    B.cost = (unsigned long long *)(buf + o_cost);
+    B.moves = (int *)(buf + o_moves);
+    B.err = (int *)(buf + o_err);
+    B.ffdone = (int *)(buf + o_ffd);
+    int32_t *rand_rows = (int32_t *)(buf + o_rand);
+    int rc = -1;
+    std::vector<char> hitems;
+    auto upload = [&](const void *src, size_t bytes) -> int {  // work list -> device (synchronous: the
+        TILER_HIP_CHECK(hipMemcpyAsync(items, src, bytes, hipMemcpyHostToDevice, st));  // host buffer is reused)
+        TILER_HIP_CHECK(hipStreamSynchronize(st));
+        return 0;
+    };
+    do {
+        // permuted copy of X (bins contiguous in K order) + metadata
+        for (int r = 0; r < nb; r++)
+            if (hipMemcpyAsync(buf + o_X + (size_t)boff[r] * KM_A, d_X + (size_t)h_boff[ord[r]] * KM_A,
+                               (size_t)nv[r] * KM_A, hipMemcpyDeviceToDevice, st) != hipSuccess)
+                goto fail;
+        if (hipMemcpyAsync(buf + o_boff, boff.data(), (nb + 1) * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(buf + o_koff, koff.data(), (nb + 1) * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(buf + o_poff, poff.data(), (nb + 1) * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(buf + o_start, start.data(), nb * 4, hipMemcpyHostToDevice, st) != hipSuccess)
+            goto fail;
+        {
+            std::vector<unsigned> seeds(nb, 0x42381337u);  // ComputeKModes kmodes.pas:930, per call (= per bin)
+            if (hipMemcpyAsync(B.seed, seeds.data(), nb * 4, hipMemcpyHostToDevice, st) != hipSuccess) goto fail;
+            if (hipStreamSynchronize(st) != hipSuccess) goto fail;
+        }
+        if (hipMemsetAsync(B.err, 0, nb * 4, st) != hipSuccess || hipMemsetAsync(B.ffdone, 0, nb * 4, st) != hipSuccess ||
+            hipMemsetAsync(B.mind, 0xff, (size_t)N * 8, st) != hipSuccess || hipMemsetAsync(B.used, 0, N, st) != hipSuccess ||
+            hipMemsetAsync(B.cent, 0xff, (size_t)Ktot * KM_A, st) != hipSuccess)
+            goto fail;
+        hipLaunchKernelGGL(kmb_ff_start, dim3((nb + 63) / 64), dim3(64), 0, st, B, (const int32_t *)(buf + o_start));
+        // InitFarthestFirst, all bins round by round
+        {
+            std::vector<KmFfItem> ff;
+            std::vector<int> ff_end(nb + 1, 0);  // items of bins [0, r) = ff[0, ff_end[r])
+            for (int r = 0; r < nb; r++) {
+                const int ns = poff[r + 1] - poff[r];
+                for (int sb = 0; sb < ns; sb++) ff.push_back({r, sb, ns, 0});
+                ff_end[r + 1] = (int)ff.size();
+            }
+            if (upload(ff.data(), ff.size() * sizeof(KmFfItem))) goto fail;
+            KTimer tm("kmodes_init", st);
+            int alive = nb;
+            for (int j = 0; j < Kv[0]; j++) {
+                while (alive > 0 && Kv[alive - 1] <= j) alive--;
+                hipLaunchKernelGGL(kmb_ff_round, dim3(ff_end[alive]), dim3(256), 0, st, B, (const KmFfItem *)items, j);
+            }
+        }
+        if (hipGetLastError() != hipSuccess) goto fail;
+        // initial assignment (all points) + histograms + modes
+        {
+            std::vector<KmAsgItem> as;
+            for (int r = 0; r < nb; r++) {
+                const int cs = csplit_of(Kv[r]), per = (Kv[r] + cs - 1) / cs;
+                for (int p0 = 0; p0 < nv[r]; p0 += 256)
+                    for (int c = 0; c < cs; c++)
+                        as.push_back({r, p0, std::min(nv[r], p0 + 256), c * per, std::min(Kv[r], (c + 1) * per), {0, 0, 0}});
+            }
+            if (hipMemsetAsync(B.akey, 0xff, (size_t)N * 8, st) != hipSuccess) goto fail;
+            if (upload(as.data(), as.size() * sizeof(KmAsgItem))) goto fail;
+            KTimer tm("kmodes_assign", st);
+            hipLaunchKernelGGL(kmb_assign, dim3((unsigned)as.size()), dim3(256), 0, st, B, (const KmAsgItem *)items);
+        }
+        if (hipMemsetAsync(B.csize, 0, (size_t)Ktot * 4, st) != hipSuccess ||
+            hipMemsetAsync(B.freq, 0, (size_t)Ktot * KM_A * M * 4, st) != hipSuccess)
+            goto fail;
+        hipLaunchKernelGGL(kmb_init_hist, dim3((unsigned)std::min<long>(4096, (N + 255) / 256)), dim3(256), 0, st, B, N);
+        hipLaunchKernelGGL(kmb_init_modes, dim3((nb + 63) / 64), dim3(64), 0, st, B, rand_rows);
+        hipLaunchKernelGGL(kmb_init_modes2, dim3((unsigned)std::min<long>(8192, (Ktot * KM_A + 255) / 256)), dim3(256), 0,
+                           st, B, (const int32_t *)rand_rows, Ktot);
+        if (hipGetLastError() != hipSuccess) goto fail;
+        // iterations (kmodes.pas:1023-1039), each bin until its cost stops decreasing or nothing moves
+        {
+            std::vector<int> active(nb);
+            for (int r = 0; r < nb; r++) active[r] = r;
+            std::vector<unsigned long long> best_cost(nb, ~0ull), hcost(nb);
+            std::vector<int> hmoves(nb), herr(nb), iters(nb, 0);
+            while (!active.empty()) {
+                // work list of this iteration: per chunk step c, the assign items then the seq items
+                std::vector<KmAsgItem> wl;
+                std::vector<std::pair<int, int>> steps;  // (assign items, seq items) per chunk step
+                int maxch = 0;
+                for (int r : active) maxch = std::max(maxch, (nv[r] + KM_BIN - 1) / KM_BIN);
+                for (int c = 0; c < maxch; c++) {
+                    int na = 0, ns = 0;
+                    for (int r : active) {
+                        const int p0 = c * KM_BIN;
+                        if (p0 >= nv[r]) continue;
+                        const int p1 = std::min(nv[r], p0 + KM_BIN), cs = csplit_of(Kv[r]), per = (Kv[r] + cs - 1) / cs;
+                        for (int q0 = p0; q0 < p1; q0 += 256)
+                            for (int cc = 0; cc < cs; cc++, na++)
+                                wl.push_back({r, q0, std::min(p1, q0 + 256), cc * per, std::min(Kv[r], (cc + 1) * per), {0, 0, 0}});
+                    }
+                    for (int r : active) {
+                        const int p0 = c * KM_BIN;
+                        if (p0 >= nv[r]) continue;
+                        KmAsgItem e{};
+                        reinterpret_cast<KmSeqItem &>(e) = {r, p0, std::min(nv[r], p0 + KM_BIN), 0};
+                        wl.push_back(e);
+                        ns++;
+                    }
+                    steps.push_back({na, ns});
+                }
+                if (upload(wl.data(), wl.size() * sizeof(KmAsgItem))) goto fail;
+                for (int r : active) {
+                    iters[r]++;
+                    if (hipMemsetAsync(B.cost + r, 0, 8, st) != hipSuccess || hipMemsetAsync(B.moves + r, 0, 4, st) != hipSuccess)
+                        goto fail;
+                    if (hipMemsetAsync(B.akey + boff[r], 0xff, (size_t)nv[r] * 8, st) != hipSuccess) goto fail;
+                }
+                {
+                    size_t pos = 0;
+                    for (const auto &sp : steps) {
+                        {
+                            KTimer tm("kmodes_assign", st);
+                            hipLaunchKernelGGL(kmb_assign, dim3(sp.first), dim3(256), 0, st, B,
+                                               (const KmAsgItem *)items + pos);
+                        }
+                        pos += sp.first;
+                        // seq items are KmSeqItem views of KmAsgItem slots: stride 32 bytes
+                        {
+                            KTimer tm("kmodes_seq", st);
+                            hipLaunchKernelGGL(kmb_seq_strided, dim3(sp.second), dim3(128), 0, st, B,
+                                               (const KmAsgItem *)items + pos);
+                        }
+                        pos += sp.second;
+                    }
+                }
+                if (hipGetLastError() != hipSuccess) goto fail;
+                if (hipMemcpyAsync(hcost.data(), B.cost, nb * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipMemcpyAsync(hmoves.data(), B.moves, nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipMemcpyAsync(herr.data(), B.err, nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess)
+                    goto fail;
+                std::vector<int> still;
+                for (int r : active) {
+                    if (herr[r]) {
+                        set_error("kmodes: farthest-first ran out of points (k > n)");
+                        rc = -2;
+                        goto fail;
+                    }
+                    const bool conv = (hcost[r] >= best_cost[r]) || (hmoves[r] == 0);
+                    best_cost[r] = hcost[r];
+                    if (!conv) still.push_back(r);
+                }
+                active.swap(still);
+            }
+            for (int r = 0; r < nb; r++) {
+                if (h_iter) h_iter[ord[r]] = iters[r];
+                if (h_cost) h_cost[ord[r]] = best_cost[r];
+            }
+        }
+        // outputs in caller order: labels (bin-local) and centroids
+        for (int r = 0; r < nb; r++) {
+            const int b = ord[r];
+            if (hipMemcpyAsync(d_labels + h_boff[b], B.memb + boff[r], (size_t)nv[r] * 4, hipMemcpyDeviceToDevice, st) !=
+                    hipSuccess ||
+                hipMemcpyAsync(d_centroids + (size_t)koff_c[b] * KM_A, B.cent + (size_t)koff[r] * KM_A, (size_t)Kv[r] * KM_A,
+                               hipMemcpyDeviceToDevice, st) != hipSuccess)
+                goto fail;
+        }
+        if (hipStreamSynchronize(st) != hipSuccess) goto fail;
+        rc = 0;
+    } while (0);
+fail:
+    if (rc == -1) set_error("kmodes: HIP failure");
+    (void)hipFree(buf);
+    return rc < 0 ? -1 : 0;
+}
+
+int kmodes_compute_dev(const uint8_t *d_X, int n, int k, int start_point, int n_modalities, int32_t *d_labels,
+                       uint8_t *d_centroids, int *n_iter, uint64_t *cost, hipStream_t st) {
+    const int32_t boff[2] = {0, n}, kk[1] = {k}, sp[1] = {start_point};
+    int32_t it = 0;
+    uint64_t c = 0;
+    if (kmodes_batch_dev(d_X, boff, 1, kk, sp, n_modalities, d_labels, d_centroids, &it, &c, st)) return -1;
+    if (n_iter) *n_iter = it;
+    if (cost) *cost = c;
+    return 0;
+}
+
+int kmodes_medoids_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const int32_t *h_k,
+                             const int32_t *d_labels, const uint8_t *d_centroids, int32_t *h_medoid, int32_t *h_counts,
+                             hipStream_t st) {
+    std::vector<int32_t> koff(nb + 1, 0);
+    for (int b = 0; b < nb; b++) koff[b + 1] = koff[b] + h_k[b];
+    const long N = h_boff[nb], K = koff[nb];
+    char *buf = nullptr;
+    const size_t oB = 0, oN = (size_t)K * 8, oBo = oN + (((size_t)K * 4 + 255) & ~(size_t)255), oKo = oBo + ((nb + 1) * 4 + 256);
+    TILER_HIP_CHECK(hipMalloc((void **)&buf, oKo + (nb + 1) * 4 + 256));
     int rc = -1;
     do {
-        if (n > 0 && hipMemcpy(buf + oX, X, (size_t)n * KM_A, hipMemcpyHostToDevice) != hipSuccess) break;
-        if (n > 0 && hipMemcpy(buf + oL, labels, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess) break;
-        if (hipMemcpy(buf + oC, centroids, (size_t)k * KM_A, hipMemcpyHostToDevice) != hipSuccess) break;
-        if (hipMemset(buf + oB, 0xff, (size_t)k * 8) != hipSuccess) break;
-        if (hipMemset(buf + oN, 0, (size_t)k * 4) != hipSuccess) break;
-        if (n > 0)
-            hipLaunchKernelGGL(km_medoid_kernel, dim3(std::min(4096, (n + 255) / 256)), dim3(256), 0, nullptr,
-                               (const uint8_t *)(buf + oX), n, (const int32_t *)(buf + oL),
-                               (const uint8_t *)(buf + oC), (unsigned long long *)(buf + oB), (int32_t *)(buf + oN));
+        if (hipMemsetAsync(buf + oB, 0xff, (size_t)K * 8, st) != hipSuccess) break;
+        if (hipMemsetAsync(buf + oN, 0, (size_t)K * 4, st) != hipSuccess) break;
+        if (hipMemcpyAsync(buf + oBo, h_boff, (nb + 1) * 4, hipMemcpyHostToDevice, st) != hipSuccess) break;
+        if (hipMemcpyAsync(buf + oKo, koff.data(), (nb + 1) * 4, hipMemcpyHostToDevice, st) != hipSuccess) break;
+        if (N > 0)
+            hipLaunchKernelGGL(kmb_medoid, dim3((unsigned)std::min<long>(4096, (N + 255) / 256)), dim3(256), 0, st, d_X,
+                               (const int32_t *)(buf + oBo), (const int32_t *)(buf + oKo), nb, N, d_labels, d_centroids,
+                               (unsigned long long *)(buf + oB), (int32_t *)(buf + oN));
         if (hipGetLastError() != hipSuccess) break;
-        std::vector<unsigned long long> b(k);
-        if (hipMemcpy(b.data(), buf + oB, (size_t)k * 8, hipMemcpyDeviceToHost) != hipSuccess) break;
-        if (hipMemcpy(counts, buf + oN, (size_t)k * 4, hipMemcpyDeviceToHost) != hipSuccess) break;
-        for (int j = 0; j < k; j++)
-            medoid[j] = counts[j] > 0 ? (int32_t)(0xFFFFFFFFu - (unsigned)(b[j] & 0xFFFFFFFFull)) : -1;
+        std::vector<unsigned long long> b(K);
+        if (hipMemcpyAsync(b.data(), buf + oB, (size_t)K * 8, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+        if (hipMemcpyAsync(h_counts, buf + oN, (size_t)K * 4, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+        if (hipStreamSynchronize(st) != hipSuccess) break;
+        for (long j = 0; j < K; j++) h_medoid[j] = h_counts[j] > 0 ? (int32_t)(0xFFFFFFFFu - (unsigned)(b[j] & 0xFFFFFFFFull)) : -1;
         rc = 0;
     } while (0);
     if (rc) set_error("kmodes_medoids: HIP failure");
     (void)hipFree(buf);
     return rc;
+}
+
+// host-buffer entry points: stage through a private stream
+template <class F>
+static int with_host_batch(const uint8_t *X, long N, long K, int32_t *labels_out, uint8_t *cent_out, F run) {
+    uint8_t *d_X = nullptr, *d_c = nullptr;
+    int32_t *d_l = nullptr;
+    hipStream_t st = nullptr;
+    TILER_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    int rc = -1;
+    do {
+        if (hipMalloc((void **)&d_X, (size_t)std::max(N, 1L) * KM_A) != hipSuccess) break;
+        if (hipMalloc((void **)&d_c, (size_t)std::max(K, 1L) * KM_A) != hipSuccess) break;
+        if (hipMalloc((void **)&d_l, (size_t)std::max(N, 1L) * 4) != hipSuccess) break;
+        if (N > 0 && hipMemcpyAsync(d_X, X, (size_t)N * KM_A, hipMemcpyHostToDevice, st) != hipSuccess) break;
+        if (!labels_out && !cent_out) {  // medoids: labels/centroids are inputs, results go to host in run()
+            rc = run(d_X, d_l, d_c, st) ? -2 : 0;
+            break;
+        }
+        if (run(d_X, d_l, d_c, st)) {
+            rc = -2;
+            break;
+        }
+        if (hipMemcpyAsync(labels_out, d_l, (size_t)N * 4, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+        if (hipMemcpyAsync(cent_out, d_c, (size_t)K * KM_A, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+        if (hipStreamSynchronize(st) != hipSuccess) break;
+        rc = 0;
+    } while (0);
+    if (rc == -1) set_error("kmodes: HIP failure");
+    (void)hipFree(d_X);
+    (void)hipFree(d_c);
+    (void)hipFree(d_l);
+    (void)hipStreamDestroy(st);
+    return rc < 0 ? -1 : 0;
+}
+
+int kmodes_batch_host(const uint8_t *X, const int32_t *boff, int nb, const int32_t *k, const int32_t *start,
+                      int n_modalities, int32_t *labels, uint8_t *centroids, int32_t *n_iter, uint64_t *cost) {
+    if (!X || !boff || nb <= 0 || !k || !start || !labels || !centroids) {
+        set_error("kmodes: null buffer");
+        return -1;
+    }
+    long K = 0;
+    for (int b = 0; b < nb; b++) K += k[b];
+    return with_host_batch(X, boff[nb], K, labels, centroids, [&](uint8_t *dX, int32_t *dl, uint8_t *dc, hipStream_t st) {
+        return kmodes_batch_dev(dX, boff, nb, k, start, n_modalities, dl, dc, n_iter, cost, st);
+    });
+}
+
+int kmodes_medoids_batch_host(const uint8_t *X, const int32_t *boff, int nb, const int32_t *k, const int32_t *labels,
+                              const uint8_t *centroids, int32_t *medoid, int32_t *counts) {
+    if (!X || !boff || nb <= 0 || !k || !labels || !centroids || !medoid || !counts) {
+        set_error("kmodes_medoids: invalid arguments");
+        return -1;
+    }
+    long K = 0;
+    for (int b = 0; b < nb; b++) K += k[b];
+    for (int b = 0; b < nb; b++)
+        for (int i = boff[b]; i < boff[b + 1]; i++)
+            if (labels[i] < 0 || labels[i] >= k[b]) {
+                set_error("kmodes_medoids: label out of range");
+                return -1;
+            }
+    return with_host_batch(X, boff[nb], K, nullptr, nullptr, [&](uint8_t *dX, int32_t *dl, uint8_t *dc, hipStream_t st) {
+        TILER_HIP_CHECK(hipMemcpyAsync(dl, labels, (size_t)boff[nb] * 4, hipMemcpyHostToDevice, st));
+        TILER_HIP_CHECK(hipMemcpyAsync(dc, centroids, (size_t)K * KM_A, hipMemcpyHostToDevice, st));
+        return kmodes_medoids_batch_dev(dX, boff, nb, k, dl, dc, medoid, counts, st);
+    });
+}
+
+int kmodes_medoids_host(const uint8_t *X, int n, const int32_t *labels, const uint8_t *centroids, int k,
+                        int32_t *medoid, int32_t *counts) {
+    if (n < 0 || k <= 0) {
+        set_error("kmodes_medoids: invalid arguments");
+        return -1;
+    }
+    if (n == 0) {
+        for (int j = 0; j < k; j++) {
+            medoid[j] = -1;
+            counts[j] = 0;
+        }
+        return 0;
+    }
+    const int32_t boff[2] = {0, n}, kk[1] = {k};
+    return kmodes_medoids_batch_host(X, boff, 1, kk, labels, centroids, medoid, counts);
 }
 
 int kmodes_compute_host(const uint8_t *X, int n, int nattr, int k, int start_point, int n_modalities,
@@ -525,35 +971,17 @@ int kmodes_compute_host(const uint8_t *X, int n, int nattr, int k, int start_poi
         set_error("kmodes: nattr must be 80 (cKModesFeatureCount; the asm dissimilarity is 80-byte wide)");
         return -1;
     }
-    if (!X || !labels || !centroids) {
-        set_error("kmodes: null buffer");
+    if (n <= 0 || k <= 0 || k > n || start_point < 0 || start_point >= n || n_modalities <= 0 || n_modalities > 256) {
+        set_error("kmodes: invalid arguments (need 0 < k <= n, 0 <= start < n, 0 < modalities <= 256)");
         return -1;
     }
-    uint8_t *d_X = nullptr, *d_c = nullptr;
-    int32_t *d_l = nullptr;
-    hipStream_t st = nullptr;
-    TILER_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    int rc = -1;
-    do {
-        if (hipMalloc((void **)&d_X, (size_t)std::max(n, 1) * KM_A) != hipSuccess) break;
-        if (hipMalloc((void **)&d_c, (size_t)std::max(k, 1) * KM_A) != hipSuccess) break;
-        if (hipMalloc((void **)&d_l, (size_t)std::max(n, 1) * 4) != hipSuccess) break;
-        if (n > 0 && hipMemcpyAsync(d_X, X, (size_t)n * KM_A, hipMemcpyHostToDevice, st) != hipSuccess) break;
-        if (kmodes_compute_dev(d_X, n, k, start_point, n_modalities, d_l, d_c, n_iter, cost, st)) {
-            rc = -2;
-            break;
-        }
-        if (hipMemcpyAsync(labels, d_l, (size_t)n * 4, hipMemcpyDeviceToHost, st) != hipSuccess) break;
-        if (hipMemcpyAsync(centroids, d_c, (size_t)k * KM_A, hipMemcpyDeviceToHost, st) != hipSuccess) break;
-        if (hipStreamSynchronize(st) != hipSuccess) break;
-        rc = k;
-    } while (0);
-    if (rc == -1) set_error("kmodes: HIP failure");
-    (void)hipFree(d_X);
-    (void)hipFree(d_c);
-    (void)hipFree(d_l);
-    (void)hipStreamDestroy(st);
-    return rc < 0 ? -1 : rc;
+    const int32_t boff[2] = {0, n}, kk[1] = {k}, sp[1] = {start_point};
+    int32_t it = 0;
+    uint64_t c = 0;
+    if (kmodes_batch_host(X, boff, 1, kk, sp, n_modalities, labels, centroids, &it, &c)) return -1;
+    if (n_iter) *n_iter = it;
+    if (cost) *cost = c;
+    return k;
 }
 
 }  // namespace tiler

@@ -1,7 +1,8 @@
 """GlobalTiling step (btnDoGlobalTilingClick main.pas:837-856 -> DoGlobalTiling main.pas:4256-4370).
 
 Host bookkeeping mirrors the reference procedures by name; the K-Modes reduction and the medoid choice
-run on the GPU (tiler_kmodes_compute / tiler_kmodes_medoids):
+run on the GPU, all palette bins in one batch (tiler_kmodes_batch / tiler_kmodes_medoids_batch; the
+reference runs the bins concurrently with ProcThreadPool, main.pas:4339):
   write_tile_dataset_line  WriteTileDatasetLine main.pas:4167-4183 (+ GetTilePalZoneThres 4142-4165)
   equal_quality_tile_count EqualQualityTileCount main.pas:722-725
   do_global_tiling         DoGlobalTiling 4256-4331 + DoKModes 4195-4254 + MergeTiles 3688-3712
@@ -16,7 +17,7 @@ import math
 import numpy as np
 
 from ._lib import check, load
-from .kmodes import compute_kmodes
+from .kmodes import compute_kmodes_batch, medoids_batch
 
 CRANDOM_KMODES_COUNT = 7  # cRandomKModesCount main.pas:19
 
@@ -85,18 +86,29 @@ def do_global_tiling(palpix, dith_pal, n_palettes: int, desired: int, palsize: i
     dis_cnt = sum(equal_quality_tile_count(b.size) for b in bins)
     share = desired / dis_cnt
     k_per_bin = np.zeros(n_palettes, np.int64)
+    run = []  # bins that go through K-Modes (DoKModes, main.pas:4195-4254)
     for p, b in enumerate(bins):
         kc = math.ceil(equal_quality_tile_count(b.size) * share)
         k = int(round(kc))
         k_per_bin[p] = k
-        if b.size <= kc:
-            continue
-        X = np.ascontiguousarray(lines[b])
-        labels, cent, _, _ = compute_kmodes(X, k, starts[p], palsize)
-        medoid, counts = kmodes_medoids(X, labels, cent)
-        for j in np.nonzero(counts >= 2)[0]:
-            members = b[labels == j]
-            merge_tiles(members, int(b[medoid[j]]), palpix, active, use_count, merge_index)
+        if b.size > kc:
+            run.append(p)
+    if run:
+        X = np.ascontiguousarray(np.concatenate([lines[bins[p]] for p in run]))
+        off = np.zeros(len(run) + 1, np.int32)
+        off[1:] = np.cumsum([bins[p].size for p in run])
+        ks = np.array([k_per_bin[p] for p in run], np.int32)
+        st = np.array([starts[p] for p in run], np.int32)
+        labels, cent, _, _ = compute_kmodes_batch(X, off, ks, st, palsize)
+        medoid, counts = medoids_batch(X, off, ks, labels, cent)
+        koff = np.concatenate([[0], np.cumsum(ks)])
+        for r, p in enumerate(run):
+            b = bins[p]
+            lab = labels[off[r]:off[r + 1]]
+            med, cnt = medoid[koff[r]:koff[r + 1]], counts[koff[r]:koff[r + 1]]
+            for j in np.nonzero(cnt >= 2)[0]:
+                members = b[lab == j]
+                merge_tiles(members, int(b[med[j]]), palpix, active, use_count, merge_index)
     return palpix, active, use_count, merge_index, k_per_bin
 
 

@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""GlobalTiling K-Modes on MI355X (BASELINE.json config 4: 1080p GlobalTiling KModes 1M -> 64k tiles).
+
+DoGlobalTiling (main.pas:4256-4370) on the SURVEY.md 8(d) synthetic workload: 1,048,576 tiles from
+65,536 prototypes with 10 % per-byte perturbation, DitheringPalIndex bins with Zipf(1.1) sizes over
+128 palettes, desired 65,536 tiles.  The K-Modes of every bin (DoKModes main.pas:4195-4254, run
+concurrently by ProcThreadPool at main.pas:4339) is ONE tiler_kmodes_batch call on the GPU; the
+timed step is that call + the medoid batch (inputs resident in HBM).  A bounded CPU baseline runs the
+oracle's restatement (pinned to the reference asm) on the smallest bins and checks them bit-exact.
+
+Prints one JSON line.  Not the headline metric (bench.py is); a secondary measurement of §8 rows a9-a13.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--desired", type=int, default=65536)
+    ap.add_argument("--bins", type=int, default=128)
+    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import tiler_amd
+    from tiler_amd import global_tiling as gt
+    from tiler_amd import synth
+    from tiler_amd._lib import check
+
+    lib = tiler_amd.load()
+    check(lib.tiler_init(0), "tiler_init")
+    dev = torch.device("cuda", 0)
+    t0 = time.perf_counter()
+    tiles, dith = synth.globaltiling_workload(args.seed, args.n, n_palettes=args.bins)
+    lines = gt.write_tile_dataset_line(tiles)
+    bins = [np.nonzero(dith == p)[0] for p in range(args.bins)]
+    starts, eq = [], []
+    for b in bins:
+        s = lines[b].astype(np.int64).sum(1)
+        starts.append(int(b.size - 1 - np.argmin(s[::-1])) if b.size else 0)
+        eq.append(gt.equal_quality_tile_count(b.size))
+    share = args.desired / sum(eq)
+    run, ks = [], []
+    for p, b in enumerate(bins):
+        kc = math.ceil(eq[p] * share)
+        if b.size > kc:
+            run.append(p)
+            ks.append(int(round(kc)))
+    X = np.ascontiguousarray(np.concatenate([lines[bins[p]] for p in run]))
+    off = np.zeros(len(run) + 1, np.int32)
+    off[1:] = np.cumsum([bins[p].size for p in run])
+    ks = np.array(ks, np.int32)
+    st = np.array([starts[p] for p in run], np.int32)
+    host_prep = time.perf_counter() - t0
+
+    d_X = torch.from_numpy(X).to(dev)
+    d_lab = torch.empty(X.shape[0], dtype=torch.int32, device=dev)
+    d_cent = torch.empty((int(ks.sum()), 80), dtype=torch.uint8, device=dev)
+    iters = np.zeros(len(run), np.int32)
+    costs = np.zeros(len(run), np.uint64)
+    vp = ctypes.c_void_p
+    p = lambda a: a.ctypes.data_as(vp)  # noqa: E731
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    torch.cuda.synchronize(dev)
+    lib.tiler_timing_reset()
+    lib.tiler_timing_enable(1)
+    t1 = time.perf_counter()
+    check(lib.tiler_kmodes_batch_dev(vp(d_X.data_ptr()), p(off), len(run), p(ks), p(st), 16, vp(d_lab.data_ptr()),
+                                     vp(d_cent.data_ptr()), p(iters), p(costs), vp(stream)), "tiler_kmodes_batch_dev")
+    torch.cuda.synchronize(dev)
+    t_km = time.perf_counter() - t1
+    lib.tiler_timing_enable(0)
+    phases = {}
+    for name in ("kmodes_init", "kmodes_assign", "kmodes_seq"):
+        n = ctypes.c_int(0)
+        ms = lib.tiler_timing_get(name.encode(), ctypes.byref(n))
+        phases[name] = {"ms_total": round(ms, 2), "launches": n.value}
+    labels = d_lab.cpu().numpy()
+    cent = d_cent.cpu().numpy()
+    t2 = time.perf_counter()
+    from tiler_amd.kmodes import medoids_batch
+    med, cnt = medoids_batch(X, off, ks, labels, cent)
+    t_med = time.perf_counter() - t2
+
+    cpu = None
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        order = np.argsort([off[r + 1] - off[r] for r in range(len(run))])
+        spent, done_pts, done_bins, mism = 0.0, 0, 0, 0
+        koff = np.concatenate([[0], np.cumsum(ks)])
+        for r in order:
+            if spent > args.cpu_seconds:
+                break
+            x = X[off[r]:off[r + 1]]
+            tc = time.perf_counter()
+            ol, oc, oi, ocost = pyoracle.kmodes(x, int(ks[r]), int(st[r]))
+            spent += time.perf_counter() - tc
+            mism += int(not (np.array_equal(labels[off[r]:off[r + 1]], ol) and np.array_equal(cent[koff[r]:koff[r + 1]], oc)
+                             and (int(iters[r]), int(costs[r])) == (oi, ocost)))
+            done_pts += x.shape[0]
+            done_bins += 1
+        cpu = {"value": round(done_pts / spent, 1) if spent else None, "unit": "points/s (full K-Modes run per bin)",
+               "cores": 1, "kind": "port",
+               "sample": f"{done_bins} smallest bins ({done_pts} points), oracle/tiler_oracle.c restatement "
+                         "(dissimilarity pinned to the reference kmodes.pas asm), single thread",
+               "bins_mismatching_gpu": mism}
+    res = {
+        "metric": "GlobalTiling K-Modes seconds (1M -> 64k tiles, 128 palette bins)", "value": round(t_km + t_med, 3),
+        "unit": "s", "higher_is_better": False, "n_gpus": 1, "dtype": "u8",
+        "data": "synthetic (seeded, SURVEY.md 8(d))",
+        "config": {"workload": f"C4 GlobalTiling: {args.n} tiles, {len(run)} bins run K-Modes, {int(ks.sum())} clusters",
+                   "largest_bin": int(np.diff(off).max()), "largest_k": int(ks.max())},
+        "kmodes_s": round(t_km, 3), "medoids_s": round(t_med, 3), "host_prep_s": round(host_prep, 2),
+        "iterations": {"max": int(iters.max()), "mean": round(float(iters.mean()), 2)}, "phases": phases,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

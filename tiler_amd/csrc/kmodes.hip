@@ -265,67 +265,123 @@ __device__ void move_point_cat(const KmState &s, int ip, int to, int from) {
     }
 }
 
+// One 960-point chunk applied in order.  The chunk's assignment keys and labels are staged in LDS, the cost
+// is a parallel sum, and only the points that move are visited in order (an ordered compaction; a rescue
+// that relabels a later point of the chunk rebuilds the list from there) -- same sequence of MovePointCat
+// and rescue steps as the reference loop, without a dependent global load per point.
 __device__ void bin_seq_body(KmState s, int p0, int p1) {
     __shared__ int sh_i[4];
     __shared__ unsigned long long sh_best[128];
     __shared__ int sh_cnt[128];
-    unsigned long long cost = 0;
-    int moves = 0;
-    for (int i = p0; i < p1; i++) {
-        const unsigned long long key = s.akey[i];
-        const int cl = (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
-        cost += key >> 32;
-        const int old = s.memb[i];
-        if (old == cl) continue;  // uniform
-        moves++;
-        __syncthreads();
-        move_point_cat(s, i, cl, old);
-        __syncthreads();
-        if (s.csize[old] != 0) continue;
-        // GetMaxClusterMembers (kmodes.pas:631-669): largest cluster, ties -> last
-        unsigned long long b = 0;
-        for (int c = threadIdx.x; c < s.K; c += 128) {
-            const unsigned long long v = ((unsigned long long)(unsigned)s.csize[c] << 32) | (unsigned)c;
-            b = v > b ? v : b;
-        }
-        sh_best[threadIdx.x] = b;
-        __syncthreads();
-        for (int o = 64; o > 0; o >>= 1) {
-            if (threadIdx.x < o) sh_best[threadIdx.x] = max(sh_best[threadIdx.x], sh_best[threadIdx.x + o]);
-            __syncthreads();
-        }
-        const int from = (int)(sh_best[0] & 0xFFFFFFFFull);
-        const int cnt = s.csize[from];
-        if (threadIdx.x == 0) sh_i[0] = (int)km_randint((unsigned)cnt, s.seed);
-        __syncthreads();
-        const int r = sh_i[0];
-        // r-th member of 'from' in ascending point order (choices[RandInt(cnt)], kmodes.pas:895-902)
-        const long chunk = (s.n + 127) / 128;
-        const long a0 = threadIdx.x * chunk, a1 = min((long)s.n, a0 + chunk);
-        int mine = 0;
-        for (long q = a0; q < a1; q++) mine += s.memb[q] == from;
-        sh_cnt[threadIdx.x] = mine;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int acc = 0, t = 0;
-            while (t < 128 && acc + sh_cnt[t] <= r) acc += sh_cnt[t++];
-            sh_i[1] = t;
-            sh_i[2] = r - acc;
-        }
-        __syncthreads();
-        if (threadIdx.x == sh_i[1]) {
-            int left = sh_i[2];
-            for (long q = a0; q < a1; q++)
-                if (s.memb[q] == from && left-- == 0) {
-                    sh_i[3] = (int)q;
-                    break;
-                }
-        }
-        __syncthreads();
-        move_point_cat(s, sh_i[3], old, from);
+    __shared__ unsigned long long skey[KM_BIN];
+    __shared__ int smemb[KM_BIN];
+    __shared__ int slist[KM_BIN];
+    __shared__ int slen;
+    const int n = p1 - p0, tid = threadIdx.x;
+    unsigned long long cpart = 0;
+    for (int t = tid; t < n; t += 128) {
+        const unsigned long long k = s.akey[p0 + t];
+        skey[t] = k;
+        smemb[t] = s.memb[p0 + t];
+        cpart += k >> 32;
+    }
+    sh_best[tid] = cpart;
+    __syncthreads();
+    for (int o = 64; o > 0; o >>= 1) {
+        if (tid < o) sh_best[tid] += sh_best[tid + o];
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
+    const unsigned long long cost = sh_best[0];
+    int moves = 0;
+    int from_pos = 0;
+    for (;;) {
+        // ordered list of the chunk positions >= from_pos whose best cluster differs from their label
+        __syncthreads();
+        const int rem = n - from_pos, seg = (rem + 127) / 128;
+        const int a0 = from_pos + tid * seg, a1 = min(n, a0 + seg);
+        int mine = 0;
+        for (int t = a0; t < a1; t++) mine += (int)(0xFFFFFFFFu - (unsigned)(skey[t] & 0xFFFFFFFFull)) != smemb[t];
+        sh_cnt[tid] = mine;
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int t = 0; t < 128; t++) {
+                const int c = sh_cnt[t];
+                sh_cnt[t] = acc;
+                acc += c;
+            }
+            slen = acc;
+        }
+        __syncthreads();
+        int w = sh_cnt[tid];
+        for (int t = a0; t < a1; t++)
+            if ((int)(0xFFFFFFFFu - (unsigned)(skey[t] & 0xFFFFFFFFull)) != smemb[t]) slist[w++] = t;
+        __syncthreads();
+        const int len = slen;
+        bool rebuilt = false;
+        for (int li = 0; li < len && !rebuilt; li++) {
+            const int t = slist[li], i = p0 + t;
+            const int cl = (int)(0xFFFFFFFFu - (unsigned)(skey[t] & 0xFFFFFFFFull));
+            const int old = smemb[t];
+            if (old == cl) continue;  // uniform
+            moves++;
+            __syncthreads();
+            move_point_cat(s, i, cl, old);
+            if (tid == 0) smemb[t] = cl;
+            __syncthreads();
+            if (s.csize[old] != 0) continue;
+            // GetMaxClusterMembers (kmodes.pas:631-669): largest cluster, ties -> last
+            unsigned long long b = 0;
+            for (int c = tid; c < s.K; c += 128) {
+                const unsigned long long v = ((unsigned long long)(unsigned)s.csize[c] << 32) | (unsigned)c;
+                b = v > b ? v : b;
+            }
+            sh_best[tid] = b;
+            __syncthreads();
+            for (int o = 64; o > 0; o >>= 1) {
+                if (tid < o) sh_best[tid] = max(sh_best[tid], sh_best[tid + o]);
+                __syncthreads();
+            }
+            const int from = (int)(sh_best[0] & 0xFFFFFFFFull);
+            const int cnt = s.csize[from];
+            if (tid == 0) sh_i[0] = (int)km_randint((unsigned)cnt, s.seed);
+            __syncthreads();
+            const int r = sh_i[0];
+            // r-th member of 'from' in ascending point order (choices[RandInt(cnt)], kmodes.pas:895-902)
+            const long chunk = (s.n + 127) / 128;
+            const long b0 = tid * chunk, b1 = min((long)s.n, b0 + chunk);
+            int cm = 0;
+            for (long q = b0; q < b1; q++) cm += s.memb[q] == from;
+            sh_cnt[tid] = cm;
+            __syncthreads();
+            if (tid == 0) {
+                int acc = 0, tt = 0;
+                while (tt < 128 && acc + sh_cnt[tt] <= r) acc += sh_cnt[tt++];
+                sh_i[1] = tt;
+                sh_i[2] = r - acc;
+            }
+            __syncthreads();
+            if (tid == sh_i[1]) {
+                int left = sh_i[2];
+                for (long q = b0; q < b1; q++)
+                    if (s.memb[q] == from && left-- == 0) {
+                        sh_i[3] = (int)q;
+                        break;
+                    }
+            }
+            __syncthreads();
+            const int qp = sh_i[3];
+            move_point_cat(s, qp, old, from);
+            if (tid == 0 && qp >= p0 && qp < p1) smemb[qp - p0] = old;
+            __syncthreads();
+            if (qp - p0 > t && qp < p1) {  // a later point of this chunk was relabelled: rebuild from t + 1
+                from_pos = t + 1;
+                rebuilt = true;
+            }
+        }
+        if (!rebuilt) break;
+    }
+    if (tid == 0) {
         s.cost[0] += cost;
         s.moves[0] += moves;
     }
@@ -584,7 +640,9 @@ __global__ __launch_bounds__(256) void kmb_medoid(const uint8_t *X, const int32_
 }
 
 // ---- host driver ----
-static int csplit_of(int K) { return std::max(1, std::min(64, (K + 511) / 512)); }
+// centroid splits of an assignment block: ~64 centroids per block, so a chunk of the largest bin alone
+// still spreads over the chip (results merge by atomicMin)
+static int csplit_of(int K) { return std::max(1, std::min(128, (K + 63) / 64)); }
 
 int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const int32_t *h_k, const int32_t *h_start,
                      int n_modalities, int32_t *d_labels, uint8_t *d_centroids, int32_t *h_iter, uint64_t *h_cost,

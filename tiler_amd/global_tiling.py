@@ -102,13 +102,21 @@ def do_global_tiling(palpix, dith_pal, n_palettes: int, desired: int, palsize: i
         labels, cent, _, _ = compute_kmodes_batch(X, off, ks, st, palsize)
         medoid, counts = medoids_batch(X, off, ks, labels, cent)
         koff = np.concatenate([[0], np.cumsum(ks)])
-        for r, p in enumerate(run):
-            b = bins[p]
-            lab = labels[off[r]:off[r + 1]]
-            med, cnt = medoid[koff[r]:koff[r + 1]], counts[koff[r]:koff[r + 1]]
-            for j in np.nonzero(cnt >= 2)[0]:
-                members = b[lab == j]
-                merge_tiles(members, int(b[med[j]]), palpix, active, use_count, merge_index)
+        # MergeTiles for every cluster with >= 2 members (main.pas:4231-4253), vectorised: bins own disjoint
+        # tiles, so the per-cluster order of the reference does not change the result
+        tile_of = np.concatenate([bins[p] for p in run])
+        gl = np.repeat(koff[:-1], np.diff(off)) + labels          # global cluster of every row
+        med_tile = np.full(int(koff[-1]), -1, np.int64)
+        ok = counts >= 2
+        bin_of_cluster = np.repeat(np.arange(len(run)), ks)
+        med_tile[ok] = tile_of[off[bin_of_cluster[ok]] + medoid[ok]]
+        best = med_tile[gl]
+        sel = (best >= 0) & (tile_of != best)
+        src, dst = tile_of[sel], best[sel]
+        np.add.at(use_count, dst, use_count[src])
+        active[src] = 0
+        merge_index[src] = dst
+        palpix[src] = 0
     return palpix, active, use_count, merge_index, k_per_bin
 
 

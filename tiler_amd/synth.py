@@ -161,3 +161,17 @@ def make_workload(seed: int, width: int, height: int, frames: int, tileset_size:
     fr = keyframe_frames(rng, frames, q)
     ds = ft_dataset_from_used(used_one_palette(tile_pal, n_palettes), thm, tvm)
     return Workload(seed, width, height, frames, tileset_size, pals, tiles, thm, tvm, tile_pal, fr, ds)
+
+
+def globaltiling_workload(seed: int, n: int = 1 << 20, protos: int = 65536, noise: float = 0.1,
+                          n_palettes: int = 128, zipf: float = 1.1, palsize: int = 16):
+    """SURVEY.md 8(d) C4 GlobalTiling input: n palette-index tiles drawn from `protos` prototypes with
+    `noise` per-byte perturbation, DitheringPalIndex bins with Zipf(`zipf`) sizes over `n_palettes`."""
+    rng = np.random.default_rng(seed)
+    P = rng.integers(0, palsize, (protos, 64)).astype(np.uint8)
+    tiles = P[rng.integers(0, protos, n)]
+    flip = rng.random(tiles.shape) < noise
+    tiles[flip] = rng.integers(0, palsize, int(flip.sum())).astype(np.uint8)
+    w = 1.0 / np.arange(1, n_palettes + 1) ** zipf
+    dith = rng.choice(n_palettes, size=n, p=w / w.sum()).astype(np.int32)
+    return tiles, dith

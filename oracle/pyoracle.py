@@ -21,6 +21,15 @@ def _p(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _threads() -> int:
+    """Worker threads of the CPU restatement: the visible cores, capped at 16 (a GPU box's CPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def lib():
     global _o
     if _o is None:
@@ -91,7 +100,7 @@ def nn_batch(data, qs, threads=None):
     idx = np.zeros(qs.shape[0], np.int32)
     err = np.zeros(qs.shape[0], np.float32)
     lib().or_nn_batch(_p(data), data.shape[0], data.shape[1], _p(qs), qs.shape[0], _p(idx), _p(err),
-                      threads or (os.cpu_count() or 1))
+                      threads or _threads())
     return idx, err
 
 
@@ -116,7 +125,7 @@ def frame_tiling(frame_rgb, ds, tidx, pidx, attrs, use_wavelets=True, gamma=-1, 
     out = [np.zeros(Q, np.int32), np.zeros(Q, np.int32), np.zeros(Q, np.uint8), np.zeros(Q, np.uint8),
            np.zeros(Q, np.float32)]
     lib().or_frame_tiling(_p(rgb), Q, _p(np.ascontiguousarray(ds, np.float32)), ds.shape[0], _p(tidx), _p(pidx),
-                          _p(attrs), int(use_wavelets), gamma, threads or (os.cpu_count() or 1), *[_p(o) for o in out])
+                          _p(attrs), int(use_wavelets), gamma, threads or _threads(), *[_p(o) for o in out])
     return tuple(out)
 
 

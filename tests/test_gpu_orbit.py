@@ -95,3 +95,46 @@ def test_orbit_not_used_for_unstructured_data(gpu, oracle):
     q = rng.normal(0, 1, (500, 192)).astype(np.float32)
     st = _check(gpu, oracle, data, q, expect_orbit=False)
     assert st["orbit_groups"] == 0 and st["orbit_search"] == 0
+
+
+def test_orbit_c2_frame_sampled(gpu, oracle):
+    """C2 shape (720p frame, 16k tileset x 4 mirrors = 65,536 candidates): the whole frame through
+    tiler_frame_tiling, a bounded sample checked against the exhaustive oracle scan."""
+    from tiler_amd.frame_tiling import KeyframeTiler
+    wl = synth.make_workload(41, 1280, 720, 1, 16384, n_palettes=128)
+    kt = KeyframeTiler(wl.tiles, wl.thm, wl.tvm, wl.palettes, wl.ds)
+    g = kt.do_frame_tiling(wl.frame_rgb[0])
+    st = kt.kdt.stats()
+    used = synth.used_one_palette(wl.tile_pal, 128)
+    ods, ot, op, oa = oracle.build_ft_dataset(used, wl.tiles, wl.thm, wl.tvm, wl.palettes)
+    pick = np.random.default_rng(1).choice(wl.tiles_per_frame, 500, replace=False)
+    o = oracle.frame_tiling(wl.frame_rgb[0][pick], ods, ot, op, oa)
+    for a, b in zip(g[:4], o[:4]):
+        assert np.array_equal(np.asarray(a)[pick], b)
+    assert np.array_equal(np.asarray(g[4])[pick].view(np.uint32), o[4].view(np.uint32))
+    kt.finish_frame_tiling()
+    assert st["orbit_search"] == 1
+
+
+def test_orbit_c3_self_queries(gpu):
+    """Full C3 candidate set (64k tileset x 4 mirrors = 262,144 rows, built on the GPU): querying rows of
+    the dataset must return distance 0 and the LOWEST index holding an identical row (size-independent
+    property of the exact search + canonical tie rule, covers symmetric tiles whose mirrors coincide)."""
+    rng = np.random.default_rng(43)
+    P, T = 128, 65536
+    pals = synth.palettes(rng, P)
+    tiles, thm, tvm = synth.tileset(rng, T)
+    ds = synth.ft_dataset_from_used(synth.used_one_palette(rng.integers(0, P, T).astype(np.int32), P), thm, tvm)
+    rows = gpu.psyv_batch(palpix=tiles, tile_of=ds.tile_of, palettes=pals, pal_of=ds.pal_of,
+                          flags_per=ds.psyv_flags, flags=1 | 2, gamma=-1, want32=True)[1]
+    pick = rng.choice(rows.shape[0], 3000, replace=False)
+    with gpu.KDTree(rows) as kdt:
+        gi, ge = kdt.search_batch(rows[pick])
+        st = kdt.stats()
+    assert st["orbit_search"] == 1 and st["orbit_groups"] == T
+    assert (ge == 0).all()
+    # lowest index with an identical row
+    v = np.ascontiguousarray(rows).view(np.dtype((np.void, rows.shape[1] * 4))).ravel()
+    _, first = np.unique(v, return_index=True)
+    inv = np.unique(v, return_inverse=True)[1].ravel()
+    assert np.array_equal(gi, first[inv[pick]])

@@ -29,11 +29,7 @@ PEAK_F16_TFLOPS = 2500.0   # MI355X dense fp16 MFMA (MI355X_MICROARCH.md; sparsi
 SHORTLIST_KERNELS = {
     "q16": "nn_shortlist16_kernel<S=6,L=4,CB=8,NW=8,QB=4>",
     "q16l6": "nn_shortlist16_kernel<S=6,L=6,CB=8,NW=8,QB=4>",
-    "p4": "nn_shortlist2_kernel<S=12,L=8,CB=4,NW=8>",
-    "p2": "nn_shortlist2_kernel<S=12,L=8,CB=2,NW=8>",
     "w8": "nn_shortlist_kernel<S=12,L=8,CB=2,NW=8>",
-    "w4": "nn_shortlist_kernel<S=12,L=8,CB=2,NW=4>",
-    "w1": "nn_shortlist4_kernel<S=12,L=8,CB=2,QB=3>",
 }
 ORBIT_KERNEL = "nn_orbit_shortlist_kernel<L=4,CB=4,NW=8>"
 PEAK_HBM_GBS = 8000.0

@@ -168,7 +168,7 @@ template <int S, int L, int CB, int NW>
 __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *__restrict__ cfrag,
                                                               const float *__restrict__ cnc, int nblk,
                                                               const half8 *__restrict__ qfrag, int nq,
-                                                              int blk_per_split, int nsplit, int perm, int prio,
+                                                              int blk_per_split, int nsplit, int perm,
                                                               float *__restrict__ out_key, int *__restrict__ out_idx) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * S * 1024;
@@ -238,14 +238,12 @@ __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *_
                                  -0.5f * n2.x, -0.5f * n2.y, -0.5f * n2.z, -0.5f * n2.w,
                                  -0.5f * n3.x, -0.5f * n3.y, -0.5f * n3.z, -0.5f * n3.w};
                 floatx16 acc1 = acc0;
-                if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int s = 0; s < S; s++) {
                     const half8 av = reinterpret_cast<const half8 *>(B)[(cb * S + s) * 64 + lane];
                     acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq0[s], acc0, 0, 0, 0);
                     acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq1[s], acc1, 0, 0, 0);
                 }
-                if (prio) __builtin_amdgcn_s_setprio(0);
                 const int base = blk * 32;
                 scan_keys<L>(acc0, base, h, perm, lk0, li0);
                 scan_keys<L>(acc1, base, h, perm, lk1, li1);
@@ -254,140 +252,6 @@ __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *_
         __syncthreads();  // vmcnt(0) + s_barrier: next stage's DMA landed, this stage's reads done
     }
     // partial lists: [q][split][h][L]
-#pragma unroll
-    for (int qb = 0; qb < 2; qb++) {
-        const int q = (qb0 + qb) * 32 + (lane & 31);
-        if (q < nq) {
-            const long o = (((long)q * nsplit + split) * 2 + h) * L;
-#pragma unroll
-            for (int i = 0; i < L; i++) {
-                out_key[o + i] = qb ? lk1[i] : lk0[i];
-                out_idx[o + i] = qb ? li1[i] : li0[i];
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// 1''. Shortlist, software-pipelined LDS reads.  Same work split as nn_shortlist_kernel (NW waves x 2
-// query blocks, CB candidate blocks per LDS stage) but: the A fragments of k-step pair s+1 are read
-// while the MFMAs of pair s run (the plain kernel waits on every LDS read), the next block's first
-// pair and seeds are read before the current block's epilogue, and the accumulator seed
-// (-||c||^2/2, cseed) is the first MFMA's C operand, so a block costs no seed arithmetic.
-// ------------------------------------------------------------------------------------------
-template <int S, int L, int CB, int NW>
-__global__ __launch_bounds__(NW * 64, 1) void nn_shortlist2_kernel(const half8 *__restrict__ cfrag,
-                                                               const float *__restrict__ cseed, int nblk,
-                                                               const half8 *__restrict__ qfrag, int nq,
-                                                               int blk_per_split, int nsplit, int perm,
-                                                               float *__restrict__ out_key, int *__restrict__ out_idx) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int FRAG_BYTES = CB * S * 1024;
-    constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
-    constexpr int NT = NW * 64;
-    constexpr int PER_T = CB * S * 64 / NT;
-    static_assert((CB * S * 64) % NT == 0 && S % 2 == 0, "stage must split evenly over the workgroup");
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int nqblk = (nq + 31) / 32;
-    const int qb0 = (blockIdx.x * NW + w) * 2;
-    const int split = blockIdx.y;
-    const int b_begin = split * blk_per_split;
-    const int b_end = min(nblk, b_begin + blk_per_split);
-
-    half8 bq0[S], bq1[S];
-    const long qa = min(qb0, nqblk - 1), qc = min(qb0 + 1, nqblk - 1);
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-        bq0[s] = qfrag[(qa * S + s) * 64 + lane];
-        bq1[s] = qfrag[(qc * S + s) * 64 + lane];
-    }
-    // land the query fragments before the loop (a real s_waitcnt the compiler's pass accounts for):
-    // a wait sunk into the loop would also count the hidden DMA pieces and stall on them
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    float lk0[L], lk1[L];
-    int li0[L], li1[L];
-#pragma unroll
-    for (int i = 0; i < L; i++) {
-        lk0[i] = lk1[i] = INFINITY;
-        li0[i] = li1[i] = -1;
-    }
-
-    const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
-    auto issue = [&](int st, int buf) {
-        const int blk0 = b_begin + st * CB;
-        const int nb = min(CB, b_end - blk0);
-        const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64 + w * 64 + lane;
-        char *dst = smem + buf * BUF_BYTES + w * 1024;
-        if (nb == CB) {
-#pragma unroll
-            for (int j = 0; j < PER_T; j++) glds16_asm(src + j * NT, dst + j * NT * 16);
-        } else {
-            const int last = nb * S * 64 - 1 - (w * 64 + lane);
-#pragma unroll
-            for (int j = 0; j < PER_T; j++) glds16_asm(src + min(j * NT, last), dst + j * NT * 16);
-        }
-        if (w == 0 && lane < CB * 8)
-            glds16_asm(reinterpret_cast<const uint4 *>(cseed) + (long)blk0 * 8 + min(lane, nb * 8 - 1),
-                   smem + buf * BUF_BYTES + FRAG_BYTES);
-    };
-
-    if (nstage > 0) issue(0, 0);
-    dma_drain();
-    __syncthreads();
-    for (int st = 0; st < nstage; st++) {
-        const char *B = smem + (st & 1) * BUF_BYTES;
-        const half8 *A = reinterpret_cast<const half8 *>(B) + lane;
-        const float4 *SD = reinterpret_cast<const float4 *>(B + FRAG_BYTES) + h * 4;
-        // every block's seeds and the first k-step pair go to registers before the DMA issue: hipcc
-        // would otherwise put a vmcnt(0) (the DMA) in front of the first seed read
-        float4 sd[CB][4];
-#pragma unroll
-        for (int cb = 0; cb < CB; cb++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) sd[cb][i] = SD[cb * 8 + i];
-        half8 a0 = A[0], a1 = A[64];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
-#pragma unroll
-        for (int cb = 0; cb < CB; cb++) {
-            const int blk = b_begin + st * CB + cb;
-            if (blk < b_end) {
-                const floatx16 seed = {sd[cb][0].x, sd[cb][0].y, sd[cb][0].z, sd[cb][0].w,
-                                       sd[cb][1].x, sd[cb][1].y, sd[cb][1].z, sd[cb][1].w,
-                                       sd[cb][2].x, sd[cb][2].y, sd[cb][2].z, sd[cb][2].w,
-                                       sd[cb][3].x, sd[cb][3].y, sd[cb][3].z, sd[cb][3].w};
-                floatx16 acc0, acc1;
-#pragma unroll
-                for (int s = 0; s < S; s += 2) {
-                    half8 n0, n1;
-                    const bool more = s + 2 < S || cb + 1 < CB;
-                    if (s + 2 < S) {
-                        n0 = A[(cb * S + s + 2) * 64];
-                        n1 = A[(cb * S + s + 3) * 64];
-                    } else if (cb + 1 < CB) {  // next block of this stage: first pair
-                        n0 = A[((cb + 1) * S) * 64];
-                        n1 = A[((cb + 1) * S + 1) * 64];
-                    }
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq0[s], s == 0 ? seed : acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq1[s], s == 0 ? seed : acc1, 0, 0, 0);
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bq0[s + 1], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bq1[s + 1], acc1, 0, 0, 0);
-                    // keep the next pair's reads ahead of this pair's MFMAs (hipcc re-clusters them otherwise)
-                    if (more) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-                    if (more) {
-                        a0 = n0;
-                        a1 = n1;
-                    }
-                }
-                const int base = blk * 32;
-                scan_keys<L>(acc0, base, h, perm, lk0, li0);
-                scan_keys<L>(acc1, base, h, perm, lk1, li1);
-            }
-        }
-        dma_drain();      // this wave's pieces of the next stage landed
-        __syncthreads();  // everyone's landed; this stage's reads done
-    }
 #pragma unroll
     for (int qb = 0; qb < 2; qb++) {
         const int q = (qb0 + qb) * 32 + (lane & 31);
@@ -479,7 +343,9 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 
 #pragma unroll
         for (int s = 0; s < S; s++) bq[q][s] = qfrag[(qq * S + s) * 64 + lane];
     }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see nn_shortlist2_kernel
+    // land the query fragments before the loop (a real s_waitcnt the compiler's pass accounts for): a
+    // wait sunk into the loop would also count the hidden LDS-DMA pieces and stall on them
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     float lk[QB][L];
     int li[QB][L];
 #pragma unroll
@@ -582,179 +448,6 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 
         const int qq = (qb0 + q) * 16 + (lane & 15);
         if (qq < nq) {
             const long o = (((long)qq * nsplit + split) * 4 + g) * L;
-#pragma unroll
-            for (int i = 0; i < L; i++) {
-                out_key[o + i] = lk[q][i];
-                out_idx[o + i] = li[q][i];
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// 1'. Shortlist, one wave per SIMD (512-register budget): each wave holds 4 query blocks (128 queries)
-// as B fragments, so every A fragment read from LDS feeds 4 MFMAs, and the epilogue of candidate block
-// n-1 (max tree + threshold compare, straight-line VALU) is interleaved with the MFMAs of block n
-// (ping-pong accumulator sets).  List insertion (rare) runs between blocks behind one wave-uniform
-// branch.  Workgroup = 4 waves = 512 queries; candidate tiles by LDS-DMA, double-buffered.
-// ------------------------------------------------------------------------------------------
-template <int L>
-__device__ __forceinline__ void flush_inserts(const floatx16 &acc, float (&lk)[L], int (&li)[L], int base, int h,
-                                              int perm) {
-#pragma unroll
-    for (int r = 0; r < 16; r++)
-        if (acc[r] > -0.5f * lk[L - 1]) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            list_insert<L>(lk, li, -2.0f * acc[r], base + (perm ? row_perm(row) : row));
-        }
-}
-
-__device__ __forceinline__ float max16(const floatx16 &a) {
-    float m0 = fmaxf(fmaxf(a[0], a[1]), a[2]), m1 = fmaxf(fmaxf(a[3], a[4]), a[5]);
-    float m2 = fmaxf(fmaxf(a[6], a[7]), a[8]), m3 = fmaxf(fmaxf(a[9], a[10]), a[11]);
-    float m4 = fmaxf(fmaxf(a[12], a[13]), a[14]);
-    return fmaxf(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)), fmaxf(m4, a[15]));
-}
-
-template <int S, int L, int CB, int QB>
-__global__ __launch_bounds__(256, 1) void nn_shortlist4_kernel(const half8 *__restrict__ cfrag,
-                                                               const float *__restrict__ cnc, int nblk,
-                                                               const half8 *__restrict__ qfrag, int nq,
-                                                               int blk_per_split, int nsplit, int perm,
-                                                               float *__restrict__ out_key, int *__restrict__ out_idx) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int FRAG_BYTES = CB * S * 1024;
-    constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
-    constexpr int PER_T = CB * S * 64 / 256;
-    static_assert((CB * S * 64) % 256 == 0 && CB % 2 == 0, "stage geometry");
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int nqblk = (nq + 31) / 32;
-    const int qb0 = (blockIdx.x * 4 + w) * QB;
-    const int split = blockIdx.y;
-    const int b_begin = split * blk_per_split;
-    const int b_end = min(nblk, b_begin + blk_per_split);
-
-    half8 bq[QB][S];
-#pragma unroll
-    for (int q = 0; q < QB; q++) {
-        const long qq = min(qb0 + q, nqblk - 1);  // blocks past the end: clamped duplicate, never written
-#pragma unroll
-        for (int s = 0; s < S; s++) bq[q][s] = qfrag[(qq * S + s) * 64 + lane];
-    }
-    float lk[QB][L];
-    int li[QB][L];
-#pragma unroll
-    for (int q = 0; q < QB; q++)
-#pragma unroll
-        for (int i = 0; i < L; i++) {
-            lk[q][i] = INFINITY;
-            li[q][i] = -1;
-        }
-
-    const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
-    auto issue = [&](int st, int buf) {
-        const int blk0 = b_begin + st * CB;
-        const int nb = min(CB, b_end - blk0);
-        const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64 + w * 64 + lane;
-        char *dst = smem + buf * BUF_BYTES + w * 1024;
-        if (nb == CB) {  // full stage: one lane pointer + immediate offsets (few live registers)
-#pragma unroll
-            for (int j = 0; j < PER_T; j++) glds16(src + j * 256, dst + j * 4096);
-        } else {         // last partial stage: clamp to the valid range
-            const int last = nb * S * 64 - 1 - (w * 64 + lane);
-#pragma unroll
-            for (int j = 0; j < PER_T; j++) glds16(src + min(j * 256, last), dst + j * 4096);
-        }
-        if (w == 0 && lane < CB * 8)
-            glds16(reinterpret_cast<const uint4 *>(cnc) + (long)blk0 * 8 + min(lane, nb * 8 - 1),
-                   smem + buf * BUF_BYTES + FRAG_BYTES);
-    };
-
-    floatx16 accA[QB], accB[QB];
-    int baseA = -1, baseB = -1;  // candidate block of the pending (not yet scanned) accumulator set
-    bool needB = false;
-
-    // one candidate block: MFMAs into `cur` interleaved with the max-scan of `prev`
-    auto block = [&](const char *B, int cb, const float4 (&nc)[4], floatx16 (&cur)[QB], floatx16 (&prev)[QB],
-                     int prev_base, bool &need) {
-        floatx16 seed;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            seed[4 * i] = -0.5f * nc[i].x;
-            seed[4 * i + 1] = -0.5f * nc[i].y;
-            seed[4 * i + 2] = -0.5f * nc[i].z;
-            seed[4 * i + 3] = -0.5f * nc[i].w;
-        }
-        bool nd = false;
-        half8 a_next = reinterpret_cast<const half8 *>(B)[(cb * S) * 64 + lane];
-#pragma unroll
-        for (int s = 0; s < S; s++) {
-            const half8 av = a_next;
-            if (s + 1 < S) a_next = reinterpret_cast<const half8 *>(B)[(cb * S + s + 1) * 64 + lane];
-#pragma unroll
-            for (int q = 0; q < QB; q++)
-                cur[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[q][s], s == 0 ? seed : cur[q], 0, 0, 0);
-            // the previous block's epilogue, spread over the k-steps (independent of these MFMAs)
-            if (prev_base >= 0 && s >= 1 && s <= QB) {
-                const int q = s - 1;
-                nd |= max16(prev[q]) > -0.5f * lk[q][L - 1];
-            }
-        }
-        need = nd;
-    };
-    auto drain = [&](floatx16 (&prev)[QB], int prev_base, bool need) {
-        if (prev_base >= 0 && __any(need)) {
-#pragma unroll
-            for (int q = 0; q < QB; q++) flush_inserts<L>(prev[q], lk[q], li[q], prev_base, h, perm);
-        }
-    };
-
-    if (nstage > 0) issue(0, 0);
-    __syncthreads();
-    for (int st = 0; st < nstage; st++) {
-        const char *B = smem + (st & 1) * BUF_BYTES;
-        float4 ncr[CB][4];
-#pragma unroll
-        for (int cb = 0; cb < CB; cb++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) ncr[cb][i] = reinterpret_cast<const float4 *>(B + FRAG_BYTES)[cb * 8 + h * 4 + i];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
-#pragma unroll
-        for (int cb = 0; cb < CB; cb += 2) {
-            const int blk = b_begin + st * CB + cb;
-            if (blk < b_end) {  // block -> accA, scanning accB (previous odd block)
-                bool need = false;
-                block(B, cb, ncr[cb], accA, accB, baseB, need);
-                drain(accB, baseB, need);
-                baseB = -1;
-                baseA = blk * 32;
-            }
-            if (blk + 1 < b_end) {  // block -> accB, scanning accA
-                bool need = false;
-                block(B, cb + 1, ncr[cb + 1], accB, accA, baseA, need);
-                drain(accA, baseA, need);
-                baseA = -1;
-                baseB = (blk + 1) * 32;
-            }
-        }
-        __syncthreads();
-    }
-    // tail: the last block's accumulators
-    if (baseA >= 0) {
-#pragma unroll
-        for (int q = 0; q < QB; q++) flush_inserts<L>(accA[q], lk[q], li[q], baseA, h, perm);
-    }
-    if (baseB >= 0) {
-#pragma unroll
-        for (int q = 0; q < QB; q++) flush_inserts<L>(accB[q], lk[q], li[q], baseB, h, perm);
-    }
-    (void)needB;
-#pragma unroll
-    for (int q = 0; q < QB; q++) {
-        const int qq = (qb0 + q) * 32 + (lane & 31);
-        if (qq < nq) {
-            const long o = (((long)qq * nsplit + split) * 2 + h) * L;
 #pragma unroll
             for (int i = 0; i < L; i++) {
                 out_key[o + i] = lk[q][i];
@@ -1283,16 +976,6 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
     return 0;
 }
 
-// s_setprio(1) around the MFMA chain (TILER_SETPRIO=1): lets the wave that reaches its MFMAs keep the
-// matrix pipe while the sibling wave on the SIMD runs its list-update epilogue.
-static int shortlist_prio() {
-    static int v = [] {
-        const char *e = getenv("TILER_SETPRIO");
-        return (e && e[0] == '1') ? 1 : 0;
-    }();
-    return v;
-}
-
 template <int S, int L, int CB, int NW>
 static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     const int nqblk = (nq + 31) / 32;
@@ -1301,56 +984,20 @@ static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream
     KTimer tm("nn_shortlist", stream);
     hipLaunchKernelGGL((nn_shortlist_kernel<S, L, CB, NW>), grid, dim3(NW * 64), lds, stream, (const half8 *)ix->d_frag,
                        ix->d_nc, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps, nsplit, ix->perm,
-                       shortlist_prio(), ix->scratch.key, ix->scratch.idx);
-}
-
-static constexpr int SL4_QB = 3;  // query blocks per wave in the one-wave-per-SIMD shortlist
-
-template <int S, int L, int CB, int QB>
-static void launch_shortlist4(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
-    const int nqblk = (nq + 31) / 32;
-    const dim3 grid((nqblk + 4 * QB - 1) / (4 * QB), nsplit);
-    const size_t lds = 2 * (CB * S * 1024 + CB * 128);
-    KTimer tm("nn_shortlist", stream);
-    hipLaunchKernelGGL((nn_shortlist4_kernel<S, L, CB, QB>), grid, dim3(256), lds, stream, (const half8 *)ix->d_frag,
-                       ix->d_nc, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps, nsplit, ix->perm,
                        ix->scratch.key, ix->scratch.idx);
 }
 
-// D=192 shortlist variant (A/B switch TILER_SHORTLIST for measurements; C3 keyframe, one box):
-//   "q16" (default): nn_shortlist16_kernel, 16x16x32 MFMA, L16 = 4 (51.6 ms); "q16l6": L16 = 6 (53.4 ms,
-//   fewer tier-2 queries); "p4"/"p2": nn_shortlist2_kernel, 32x32x16, pipelined LDS reads, CB = 4/2
-//   (-6 % vs w8); "w8": nn_shortlist_kernel, 8 waves x 2 query blocks (63.9 ms); "w4": 4 waves (+5 %);
-//   "w1": one wave per SIMD, 3 query blocks per wave (nn_shortlist4_kernel, +40 %)
+// D=192 generic shortlist variant (A/B switch TILER_SHORTLIST, datasets without mirror orbits; C3 keyframe,
+// one box): "q16" (default): nn_shortlist16_kernel, 16x16x32 MFMA, L16 = 4 (51.6 ms); "q16l6": L16 = 6
+// (53.4 ms, fewer tier-2 queries); "w8": nn_shortlist_kernel, 32x32x16, 8 waves x 2 query blocks (63.9 ms)
 static int shortlist_variant() {
     static int v = [] {
         const char *e = getenv("TILER_SHORTLIST");
-        if (e && !strcmp(e, "w1")) return 1;
-        if (e && !strcmp(e, "w4")) return 4;
-        if (e && !strcmp(e, "p2")) return 102;
-        if (e && !strcmp(e, "p4")) return 104;
         if (e && !strcmp(e, "w8")) return 8;
         if (e && !strcmp(e, "q16l6")) return 166;
         return 16;
     }();
     return v;
-}
-
-static int shortlist_queries_per_wg(int S) {
-    if (S != 12) return 256;
-    const int v = shortlist_variant();
-    return (v == 8 || v > 100) ? 512 : v == 4 ? 256 : 128 * SL4_QB;
-}
-
-template <int S, int L, int CB, int NW>
-static void launch_shortlist2(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
-    const int nqblk = (nq + 31) / 32;
-    const dim3 grid((nqblk + 2 * NW - 1) / (2 * NW), nsplit);
-    const size_t lds = 2 * (CB * S * 1024 + CB * 128);
-    KTimer tm("nn_shortlist", stream);
-    hipLaunchKernelGGL((nn_shortlist2_kernel<S, L, CB, NW>), grid, dim3(NW * 64), lds, stream,
-                       (const half8 *)ix->d_frag, ix->d_seed, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps,
-                       nsplit, ix->perm, ix->scratch.key, ix->scratch.idx);
 }
 
 // 16x16x32 shortlist for D = 161..192 float datasets: TILER_SHORTLIST=q16 (L16 = 4) / q16l6 (L16 = 6);
@@ -1379,18 +1026,7 @@ static int dispatch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
     switch (ix->S) {
         case 4: launch_shortlist<4, L, 6, 4>(ix, nq, nsplit, bps, stream); break;
         case 8: launch_shortlist<8, L, 3, 4>(ix, nq, nsplit, bps, stream); break;
-        case 12:
-            if (shortlist_variant() == 102)
-                launch_shortlist2<12, L, 2, 8>(ix, nq, nsplit, bps, stream);
-            else if (shortlist_variant() == 104)
-                launch_shortlist2<12, L, 4, 8>(ix, nq, nsplit, bps, stream);
-            else if (shortlist_variant() == 8)
-                launch_shortlist<12, L, 2, 8>(ix, nq, nsplit, bps, stream);
-            else if (shortlist_variant() == 4)
-                launch_shortlist<12, L, 2, 4>(ix, nq, nsplit, bps, stream);
-            else
-                launch_shortlist4<12, L, 2, SL4_QB>(ix, nq, nsplit, bps, stream);
-            break;
+        case 12: launch_shortlist<12, L, 2, 8>(ix, nq, nsplit, bps, stream); break;
         case 16: launch_shortlist<16, L, 2, 4>(ix, nq, nsplit, bps, stream); break;
         default: set_error("nn: unsupported fragment depth"); return -1;
     }
@@ -1496,7 +1132,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     const int lpq = v16 ? 4 : 2;
     const int nblk = v16 ? ix->nblk16 : ix->nblk;
     const int max_split = 64 / (lpq * L);
-    const int qpwg = v16 ? SL16_NW * SL16_QB * 16 : shortlist_queries_per_wg(ix->S);
+    const int qpwg = v16 ? SL16_NW * SL16_QB * 16 : (ix->S == 12 ? 512 : 256);
     const int wgs = (nq + qpwg - 1) / qpwg;
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
     nsplit = std::min(nsplit, nblk);

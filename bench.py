@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, visible cores)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-smooth", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (= RCCL over xGMI, the product); gloo only to rehearse the N>1 control flow")
     args = ap.parse_args()
 
     import torch
@@ -62,17 +64,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # TILER_BENCH_ONE_DEVICE=1: every rank on cuda:0 (rehearsal of the N>1 path on a one-GPU box, gloo)
+    devi = 0 if os.environ.get("TILER_BENCH_ONE_DEVICE") == "1" else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(devi)
+        dist.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", devi)
+    cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # where collectives' tensors live
 
     import tiler_amd
     from tiler_amd import synth
     from tiler_amd._lib import check
 
     lib = tiler_amd.load()
-    check(lib.tiler_init(local), "tiler_init")
+    check(lib.tiler_init(devi), "tiler_init")
 
     W, H, F, TS = CONFIGS[args.config]
     Q = (W // 8) * (H // 8)
@@ -86,9 +91,9 @@ def main():
         tile_pal = rng0.integers(0, P, TS).astype(np.int32)
         packed = np.concatenate([tiles.reshape(-1).astype(np.int32), thm.astype(np.int32), tvm.astype(np.int32),
                                  tile_pal, pals.reshape(-1)])
-        t_packed = torch.from_numpy(packed).to(dev)
+        t_packed = torch.from_numpy(packed).to(cdev)
     else:
-        t_packed = torch.empty(TS * 64 + 3 * TS + P * 16, dtype=torch.int32, device=dev)
+        t_packed = torch.empty(TS * 64 + 3 * TS + P * 16, dtype=torch.int32, device=cdev)
     if world > 1:
         dist.broadcast(t_packed, 0)
     packed = t_packed.cpu().numpy()
@@ -161,7 +166,7 @@ def main():
                          "ms_avg": round(ms / n.value, 4) if n.value else None}
     stats = kdt.stats()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total_tiles = QK * args.steps * world

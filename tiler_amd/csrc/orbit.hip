@@ -955,7 +955,11 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         const char *e = getenv("TILER_ORBIT_QB");  // query blocks of 32 per wave: 2 (default) or 1
         return (e && e[0] == '1') ? 1 : 2;
     }();
-    const int wgs = (nqblk + ORB_NW * qb - 1) / (ORB_NW * qb);
+    static const int nw = [] {
+        const char *e = getenv("TILER_ORBIT_NW");  // experiment: 12 waves x 1 query block (3 waves/SIMD)
+        return (e && atoi(e) == 12) ? 12 : ORB_NW;
+    }();
+    const int wgs = (nqblk + nw * qb - 1) / (nw * qb);
     const int max_split = 32 / (2 * ORB_L);  // rescore: one list entry per lane of a half-wave
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
     nsplit = std::min(nsplit, o->gblk);
@@ -995,25 +999,20 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             const char *e = getenv("TILER_ORBIT_MODE");  // 2, 3: timing experiments (results invalid)
             return e ? atoi(e) : 0;
         }();
-#define ORB_LAUNCH(QB, MD)                                                                                        \
-    hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, ORB_NW, QB, MD>), dim3(wgs, nsplit),               \
-                       dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                \
+#define ORB_LAUNCH(NWV, QB, MD)                                                                                   \
+    hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, NWV, QB, MD>), dim3(wgs, nsplit),                  \
+                       dim3(NWV * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
                        (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id)
-        if (qb == 1) {
-            if (mode == 2)
-                ORB_LAUNCH(1, 2);
-            else if (mode == 3)
-                ORB_LAUNCH(1, 3);
-            else
-                ORB_LAUNCH(1, 0);
-        } else {
-            if (mode == 2)
-                ORB_LAUNCH(2, 2);
-            else if (mode == 3)
-                ORB_LAUNCH(2, 3);
-            else
-                ORB_LAUNCH(2, 0);
-        }
+        if (qb == 1 && nw == 12)
+            ORB_LAUNCH(12, 1, 0);
+        else if (qb == 1)
+            ORB_LAUNCH(8, 1, 0);
+        else if (mode == 2)
+            ORB_LAUNCH(8, 2, 2);
+        else if (mode == 3)
+            ORB_LAUNCH(8, 2, 3);
+        else
+            ORB_LAUNCH(8, 2, 0);
 #undef ORB_LAUNCH
     }
     TILER_HIP_CHECK(hipGetLastError());

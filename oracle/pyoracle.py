@@ -208,10 +208,27 @@ def randint(rng_range, seed):
     return r, s.value
 
 
-def global_tiling(palpix, dith_pal, P, desired, palsize=16, restart=7, use_count=None):
+def make_tiles_unique(palpix, active, use_count):
+    """or_make_tiles_unique on copies: (palpix, active, use_count, merge_index)."""
+    palpix = np.array(palpix, np.uint8, copy=True, order="C")
+    active = np.array(active, np.uint8, copy=True)
+    uc = np.array(use_count, np.int32, copy=True)
+    mi = np.full(palpix.shape[0], -1, np.int32)
+    lib().or_make_tiles_unique(palpix.shape[0], _p(palpix), _p(active), _p(uc), _p(mi))
+    return palpix, active, uc, mi
+
+
+def reindex(active, use_count):
+    active = np.ascontiguousarray(active, np.uint8)
+    idx = np.zeros(active.shape[0], np.int32)
+    lib().or_reindex(active.shape[0], _p(active), _p(np.ascontiguousarray(use_count, np.int32)), _p(idx))
+    return idx
+
+
+def global_tiling(palpix, dith_pal, P, desired, palsize=16, restart=7, use_count=None, active=None):
     palpix = np.array(palpix, np.uint8, copy=True)
     T = palpix.shape[0]
-    active = np.ones(T, np.uint8)
+    active = np.ones(T, np.uint8) if active is None else np.array(active, np.uint8, copy=True)
     uc = np.ones(T, np.int32) if use_count is None else np.array(use_count, np.int32, copy=True)
     mi = np.full(T, -1, np.int32)
     kpb = np.zeros(P, np.int32)

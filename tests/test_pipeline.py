@@ -1,0 +1,127 @@
+"""End-to-end chain: MakeUnique -> GlobalTiling -> FrameTiling -> Reindex -> Smooth
+(btnRunAllClick main.pas:1232-1272) through tiler_amd.encoder (GPU via libANN.so) against the same chain
+composed from the CPU restatement, compared after every step: tileset, Active/UseCount, every TileMap
+and SmoothedTileMap item bit-exact.  Input: synth.video at C1 (320x240), two keyframes of 3 frames."""
+import numpy as np
+import pytest
+
+from tiler_amd import synth
+from tiler_amd.frame_tiling import FT_FAST, FT_MEDIUM, FT_SLOW
+
+
+def test_make_unique_step_matches_oracle(oracle):
+    """btnDoMakeUniqueClick (host-only step: chunks of FTileMapSize*25 tiles) on the chain's input."""
+    from tiler_amd.encoder import Encoder
+    v = synth.video(50, 160, 120, kf_frames=(30,), n_palettes=4)
+    o = _OracleChain(v)
+    T0, Q = o.palpix.shape[0], v.tiles_per_frame
+    for first in range(0, T0, Q * 25):
+        o.unique(oracle, first, min(Q * 25, T0 - first))
+    e = Encoder(v)
+    e.do_make_unique()
+    assert np.array_equal(e.active, o.active) and np.array_equal(e.tile, o.tile)
+    assert np.array_equal(e.palpix, o.palpix) and np.array_equal(e.use_count, o.uc)
+    assert 0 < e.active.sum() < e.active.size and T0 > Q * 25  # merged, and more than one chunk
+
+
+class _OracleChain:
+    """The same steps written directly on the oracle (tests only)."""
+
+    def __init__(self, v):
+        F, Q = v.frames, v.tiles_per_frame
+        self.v = v
+        self.palpix = v.palpix.copy()
+        self.thm, self.tvm, self.dith = v.thm.copy(), v.tvm.copy(), v.dith_pal.copy()
+        self.active = np.ones(F * Q, np.uint8)
+        self.uc = np.ones(F * Q, np.int32)
+        self.tile = np.arange(F * Q).reshape(F, Q)
+        self.pal = v.dith_pal.reshape(F, Q).astype(np.int64)
+        self.hm = np.zeros((F, Q), np.uint8)
+        self.vm = np.zeros((F, Q), np.uint8)
+
+    def _remap(self, mi):
+        m = np.asarray(mi)[self.tile]
+        self.tile = np.where(m >= 0, m, self.tile)
+
+    def unique(self, oracle, first, count):
+        s = slice(first, first + count)
+        pp, act, uc, mi = oracle.make_tiles_unique(self.palpix[s], self.active[s], self.uc[s])
+        self.palpix[s], self.active[s], self.uc[s] = pp, act, uc
+        full = np.full(self.palpix.shape[0], -1)
+        full[s] = np.where(mi >= 0, mi + first, -1)
+        self._remap(full)
+
+    def pack(self, oracle):
+        idx = oracle.reindex(self.active, self.uc)
+        order = np.argsort(np.where(idx >= 0, idx, np.iinfo(np.int32).max), kind="stable")[: int((idx >= 0).sum())]
+        self.palpix, self.thm, self.tvm = self.palpix[order], self.thm[order], self.tvm[order]
+        self.dith, self.uc = self.dith[order], self.uc[order]
+        self.active = np.ones(order.size, np.uint8)
+        assert (idx[self.tile] >= 0).all()
+        self.tile = idx[self.tile]
+
+    def run(self, oracle, desired, quality, strength):
+        v, Q = self.v, self.v.tiles_per_frame
+        T0 = self.palpix.shape[0]
+        for first in range(0, T0, Q * 25):
+            self.unique(oracle, first, min(Q * 25, T0 - first))
+        snap = {"unique": (self.active.copy(), self.tile.copy())}
+        pp, act, uc, mi, _ = oracle.global_tiling(self.palpix, self.dith, v.palettes.shape[1], desired,
+                                                  use_count=self.uc, active=self.active)
+        self.palpix, self.active, self.uc = pp, act, uc
+        self._remap(mi)
+        self.unique(oracle, 0, self.palpix.shape[0])
+        self.pack(oracle)
+        snap["global"] = (self.palpix.copy(), self.uc.copy(), self.tile.copy())
+        gds, gt_, ga = oracle.prepare_global_ds(self.palpix)
+        for k in range(v.kf_start.size - 1):
+            f0, f1 = int(v.kf_start[k]), int(v.kf_start[k + 1])
+            corr, hi = oracle.palette_corr(v.centroids[k])
+            used = oracle.mark_used(gds, gt_, ga, self.pal[f0:f1].ravel(), self.tile[f0:f1].ravel(), self.palpix,
+                                    v.palettes.shape[1], quality, corr, hi)
+            ds, ti, pi, at = oracle.build_ft_dataset(used, self.palpix, self.thm, self.tvm, v.palettes[k])
+            t, p, h, vv, _ = oracle.frame_tiling(v.frame_rgb[f0:f1], ds, ti, pi, at)
+            n = (f1 - f0, Q)
+            self.tile[f0:f1], self.pal[f0:f1] = t.reshape(n), p.reshape(n)
+            self.hm[f0:f1], self.vm[f0:f1] = h.reshape(n), vv.reshape(n)
+        snap["ft"] = (self.tile.copy(), self.pal.copy(), self.hm.copy(), self.vm.copy())
+        self.uc = np.bincount(self.tile.ravel(), minlength=self.palpix.shape[0]).astype(np.int32)
+        self.active = (self.uc > 0).astype(np.uint8)
+        self.pack(oracle)
+        snap["reindex"] = (self.palpix.copy(), self.tile.copy())
+        sm = [self.tile.copy(), self.pal.copy(), self.hm.copy(), self.vm.copy(), np.zeros(self.tile.shape, np.uint8)]
+        for k in range(v.kf_start.size - 1):
+            f0, f1 = int(v.kf_start[k]), int(v.kf_start[k + 1])
+            out = oracle.smooth(*[a[f0:f1] for a in sm], self.palpix, v.palettes[k], strength)
+            for a, b in zip(sm, out[:5]):
+                a[f0:f1] = b
+        snap["smooth"] = tuple(sm)
+        return snap
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quality", [FT_MEDIUM, FT_FAST, FT_SLOW])
+def test_run_all_chain_bit_exact(gpu, oracle, quality):
+    from tiler_amd.encoder import Encoder
+    v = synth.video(51 + quality, 320, 240, kf_frames=(3, 3), n_palettes=8)
+    desired, strength = 700, 0.2
+    o = _OracleChain(v).run(oracle, desired, quality, strength)
+
+    e = Encoder(v)
+    e.do_make_unique()
+    assert np.array_equal(e.active, o["unique"][0]) and np.array_equal(e.tile, o["unique"][1])
+    assert e.active.sum() < e.active.size  # frames repeat tiles: MakeUnique merged some
+    e.do_global_tiling(desired)
+    assert np.array_equal(e.palpix, o["global"][0])
+    assert np.array_equal(e.use_count, o["global"][1])
+    assert np.array_equal(e.tile, o["global"][2])
+    assert e.palpix.shape[0] <= desired + v.palettes.shape[1]
+    e.do_frame_tiling(quality)
+    for a, b in zip((e.tile, e.pal, e.hm, e.vm), o["ft"]):
+        assert np.array_equal(a, b)
+    e.do_reindex()
+    assert np.array_equal(e.palpix, o["reindex"][0]) and np.array_equal(e.tile, o["reindex"][1])
+    sm = e.do_smooth(strength)
+    for a, b in zip((sm["tile"], sm["pal"], sm["hm"], sm["vm"], sm["smoothed"]), o["smooth"]):
+        assert np.array_equal(a, b)
+    assert sm["smoothed"].sum() > 0

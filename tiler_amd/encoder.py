@@ -1,0 +1,153 @@
+"""The encoder steps around the hot path, end to end (btnRunAllClick main.pas:1232-1272, steps
+MakeUnique -> GlobalTiling -> FrameTiling -> Reindex -> Smooth), as host state + libANN.so calls.
+
+`Encoder` holds what TMainForm keeps in FTiles / FFrames / FKeyFrames for these steps, as flat arrays:
+  tiles    palpix [T][64] u8, thm/tvm (TTile.HMirror/VMirror), active, use_count, dith_pal
+  tilemaps tile/pal/hm/vm [F][Q] (TFrame.TileMap), sm_* the SmoothedTileMap copies
+  keyframes kf_start [KF+1], palettes [KF][P][16], centroids [KF][P][192]
+Each method is the reference procedure of the same name (file:line in its docstring); the heavy parts
+(K-Modes, the k=8 preselection, candidate descriptors, the FrameTiling search, Smooth) run on the GPU
+through the C ABI, the rest is the reference's host bookkeeping.  SURVEY.md 8(f)-1.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import frame_tiling as ft
+from . import global_tiling as gt
+from .smooth import DEFAULT_STRENGTH, smooth_keyframe
+from .synth import Video
+
+
+class Encoder:
+    def __init__(self, v: Video, palsize: int = 16):
+        F, Q = v.frames, v.tiles_per_frame
+        self.palsize = palsize
+        self.frame_rgb = v.frame_rgb
+        self.kf_start = np.asarray(v.kf_start, np.int64)
+        self.palettes = np.asarray(v.palettes, np.int32)
+        self.centroids = np.asarray(v.centroids, np.float64)
+        self.n_palettes = self.palettes.shape[1]
+        # FTiles after Dither (LoadFrame main.pas:3226-3236 + FinishDitherTiles 2497-2519)
+        self.palpix = np.array(v.palpix, np.uint8, copy=True)
+        self.thm = np.array(v.thm, np.uint8, copy=True)
+        self.tvm = np.array(v.tvm, np.uint8, copy=True)
+        self.dith_pal = np.array(v.dith_pal, np.int32, copy=True)
+        self.active = np.ones(F * Q, np.uint8)
+        self.use_count = np.ones(F * Q, np.int64)
+        # TileMap: GlobalTileIndex = own tile, PalIdx = DitheringPalIndex, mirrors false
+        self.tile = np.arange(F * Q, dtype=np.int64).reshape(F, Q)
+        self.pal = self.dith_pal.reshape(F, Q).astype(np.int64)
+        self.hm = np.zeros((F, Q), np.uint8)
+        self.vm = np.zeros((F, Q), np.uint8)
+        self.sm = None
+
+    @property
+    def frames(self) -> int:
+        return self.tile.shape[0]
+
+    @property
+    def tiles_per_frame(self) -> int:
+        return self.tile.shape[1]
+
+    # --- tile-list bookkeeping --------------------------------------------------------------------
+    def finish_merge_tiles(self, merge_index):
+        """FinishMergeTiles main.pas:3722-3734: TileMap items of merged tiles point at the survivor."""
+        m = np.asarray(merge_index, np.int64)[self.tile]
+        self.tile = np.where(m >= 0, m, self.tile)
+
+    def make_tiles_unique(self, first: int = 0, count: int | None = None):
+        """MakeTilesUnique main.pas:2555-2612 over tiles [first, first+count): identical PalPixels merge
+        into the lowest index (TFPList.Sort is unstable, the canonical order is stable)."""
+        count = self.palpix.shape[0] - first if count is None else count
+        s = slice(first, first + count)
+        pp, act, uc, mi = gt.make_tiles_unique(self.palpix[s], self.active[s], self.use_count[s])
+        self.palpix[s], self.active[s], self.use_count[s] = pp, act, uc
+        full = np.full(self.palpix.shape[0], -1, np.int64)
+        full[s] = np.where(mi >= 0, mi + first, -1)
+        self.finish_merge_tiles(full)
+
+    def reindex_tiles(self):
+        """ReindexTiles main.pas:4483-4527: drop inactive tiles, order by (UseCount desc, old index asc),
+        remap every TileMap."""
+        idx_map = gt.reindex_tiles(self.active, self.use_count)
+        keep = np.nonzero(idx_map >= 0)[0]
+        order = np.empty(keep.size, np.int64)
+        order[idx_map[keep]] = keep
+        self.palpix = np.ascontiguousarray(self.palpix[order])
+        self.thm, self.tvm = self.thm[order], self.tvm[order]
+        self.dith_pal, self.use_count = self.dith_pal[order], self.use_count[order]
+        self.active = np.ones(order.size, np.uint8)
+        self.tile = idx_map[self.tile]
+        if self.sm is not None:
+            self.sm["tile"] = idx_map[self.sm["tile"]]
+
+    # --- steps ------------------------------------------------------------------------------------
+    def do_make_unique(self):
+        """btnDoMakeUniqueClick main.pas:916-938: MakeTilesUnique per chunk of FTileMapSize * 25 tiles."""
+        chunk = self.tiles_per_frame * 25
+        for first in range(0, self.palpix.shape[0], chunk):
+            self.make_tiles_unique(first, min(chunk, self.palpix.shape[0] - first))
+
+    def do_global_tiling(self, desired: int, restart: int = gt.CRANDOM_KMODES_COUNT):
+        """DoGlobalTiling main.pas:4256-4370: K-Modes merge per palette bin (GPU, all bins batched),
+        FinishMergeTiles, MakeTilesUnique over all tiles, ReindexTiles."""
+        pp, act, uc, mi, kpb = gt.do_global_tiling(self.palpix, self.dith_pal, self.n_palettes, desired,
+                                                   self.palsize, restart, self.active, self.use_count)
+        self.palpix, self.active, self.use_count = pp, act, uc
+        self.finish_merge_tiles(mi)
+        self.make_tiles_unique()
+        self.reindex_tiles()
+        return kpb
+
+    def do_frame_tiling(self, quality: int = ft.FT_MEDIUM, use_wavelets: bool = True, gamma: int = -1):
+        """btnDoFrameTilingClick main.pas:945-977: PrepareGlobalFT, then per keyframe PrepareFrameTiling
+        (over the keyframe's current TileMap items), DoFrameTiling of all its frames, FinishFrameTiling."""
+        gds = ft.prepare_global_ft(self.palpix, self.active)
+        errs = np.zeros(self.tile.shape, np.float32)
+        try:
+            for k in range(self.kf_start.size - 1):
+                f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
+                kt = ft.prepare_frame_tiling(self.palpix, self.thm, self.tvm, self.palettes[k], gds,
+                                             self.pal[f0:f1].ravel(), self.tile[f0:f1].ravel(), quality,
+                                             self.centroids[k], use_wavelets, gamma)
+                try:
+                    t, p, h, v, e = kt.do_frame_tiling(self.frame_rgb[f0:f1])
+                finally:
+                    kt.finish_frame_tiling()
+                n = (f1 - f0, self.tiles_per_frame)
+                self.tile[f0:f1], self.pal[f0:f1] = t.reshape(n), p.reshape(n)
+                self.hm[f0:f1], self.vm[f0:f1], errs[f0:f1] = h.reshape(n), v.reshape(n), e.reshape(n)
+        finally:
+            gds.kdt.close()
+        return errs
+
+    def do_reindex(self):
+        """btnReindexClick main.pas:1199-1230: UseCount / Active from the TileMaps, then ReindexTiles."""
+        T = self.palpix.shape[0]
+        self.use_count = np.bincount(self.tile.ravel(), minlength=T).astype(np.int64)
+        self.active = (self.use_count > 0).astype(np.uint8)
+        self.reindex_tiles()
+
+    def do_smooth(self, strength: float = DEFAULT_STRENGTH):
+        """btnSmoothClick main.pas:1338-1370: SmoothedTileMap := TileMap, then DoTemporalSmoothing along
+        every position (frames of one keyframe only, main.pas:4081-4082) -> one GPU call per keyframe."""
+        sm = {"tile": self.tile.copy(), "pal": self.pal.copy(), "hm": self.hm.copy(), "vm": self.vm.copy(),
+              "smoothed": np.zeros(self.tile.shape, np.uint8)}
+        for k in range(self.kf_start.size - 1):
+            f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
+            t, p, h, v, s, _ = smooth_keyframe(sm["tile"][f0:f1], sm["pal"][f0:f1], sm["hm"][f0:f1],
+                                               sm["vm"][f0:f1], sm["smoothed"][f0:f1], self.palpix,
+                                               self.palettes[k], strength)
+            sm["tile"][f0:f1], sm["pal"][f0:f1], sm["hm"][f0:f1], sm["vm"][f0:f1] = t, p, h, v
+            sm["smoothed"][f0:f1] = s
+        self.sm = sm
+        return sm
+
+    def run_all(self, desired: int, quality: int = ft.FT_MEDIUM, strength: float = DEFAULT_STRENGTH):
+        """btnRunAllClick main.pas:1232-1272 from MakeUnique to Smooth."""
+        self.do_make_unique()
+        self.do_global_tiling(desired)
+        self.do_frame_tiling(quality)
+        self.do_reindex()
+        return self.do_smooth(strength)

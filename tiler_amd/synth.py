@@ -163,6 +163,75 @@ def make_workload(seed: int, width: int, height: int, frames: int, tileset_size:
     return Workload(seed, width, height, frames, tileset_size, pals, tiles, thm, tvm, tile_pal, fr, ds)
 
 
+@dataclass
+class Video:
+    """Stand-in for the Load + Dither steps (out of scope): what btnRunAllClick hands
+    to MakeUnique / GlobalTiling / FrameTiling.  Keyframe k owns frames kf_start[k]..kf_start[k+1]-1 and
+    its palettes `palettes[k]` [P][16] + 192-d `centroids[k]`.  Every frame tile is one global tile
+    (LoadFrame main.pas:3226-3236: tile f*Q+q), palettised by nearest colour in the keyframe palette with
+    the lowest total error (NOT the reference's ditherer) and canonicalised like PrepareTileMirrors."""
+    frame_rgb: np.ndarray      # [F][Q][64] int32
+    kf_start: np.ndarray       # [KF+1]
+    palettes: np.ndarray       # [KF][P][16] int32
+    centroids: np.ndarray      # [KF][P][192] float64
+    palpix: np.ndarray         # [F*Q][64] u8 (canonical orientation)
+    thm: np.ndarray            # [F*Q] u8
+    tvm: np.ndarray            # [F*Q] u8
+    dith_pal: np.ndarray       # [F*Q] int32 (DitheringPalIndex)
+
+    @property
+    def frames(self) -> int:
+        return self.frame_rgb.shape[0]
+
+    @property
+    def tiles_per_frame(self) -> int:
+        return self.frame_rgb.shape[1]
+
+
+def palette_centroids(pals: np.ndarray) -> np.ndarray:
+    """Deterministic 192-d palette centroids (the reference takes yakmo's, main.pas:2477-2479): the 16
+    colours sorted by luma, RGB/255, repeated 4x.  Close palettes get close centroids."""
+    pals = np.asarray(pals, np.int64).reshape(-1, 16)
+    rgb = np.stack([pals & 255, (pals >> 8) & 255, (pals >> 16) & 255], -1).astype(np.float64) / 255.0
+    luma = rgb @ np.array([0.2126, 0.7152, 0.0722])
+    order = np.argsort(luma, axis=1, kind="stable")
+    srt = np.take_along_axis(rgb, order[..., None], 1).reshape(pals.shape[0], 48)
+    return np.tile(srt, (1, 4))
+
+
+def video(seed: int, width: int, height: int, kf_frames=(3, 3), n_palettes: int = 8, change: float = 0.3) -> Video:
+    rng = np.random.default_rng(seed)
+    q = (width // TILE) * (height // TILE)
+    rgb, pals, starts = [], [], [0]
+    for n in kf_frames:
+        rgb.append(keyframe_frames(rng, n, q, change))
+        p = palettes(rng, n_palettes)
+        p[1::2] = p[0::2] ^ rng.integers(0, 2, p[1::2].shape)  # near-identical pairs (Medium tolerance)
+        pals.append(p)
+        starts.append(starts[-1] + n)
+    frame_rgb = np.concatenate(rgb)
+    pals = np.stack(pals)
+    F = frame_rgb.shape[0]
+    kf_of = np.repeat(np.arange(len(kf_frames)), kf_frames)
+    px = frame_rgb.reshape(F, q, 64).astype(np.int64)
+    palpix = np.zeros((F, q, 64), np.uint8)
+    dith = np.zeros((F, q), np.int32)
+    for f in range(F):
+        c = pals[kf_of[f]].astype(np.int64)  # [P][16]
+        d = np.zeros((q, c.shape[0], 64, 16), np.int64)
+        for s in (0, 8, 16):
+            t = ((px[f] >> s) & 255)[:, None, :, None] - ((c >> s) & 255)[None, :, None, :]
+            d += t * t
+        best_c = d.argmin(3)                                              # [q][P][64]
+        err = np.take_along_axis(d, best_c[..., None], 3)[..., 0].sum(2)  # [q][P]
+        pbest = err.argmin(1)
+        dith[f] = pbest
+        palpix[f] = best_c[np.arange(q), pbest].astype(np.uint8)
+    canon, thm, tvm = prepare_tile_mirrors(palpix.reshape(F * q, 64))
+    return Video(frame_rgb, np.array(starts, np.int64), pals, np.stack([palette_centroids(p) for p in pals]),
+                 canon, thm, tvm, dith.reshape(-1))
+
+
 def globaltiling_workload(seed: int, n: int = 1 << 20, protos: int = 65536, noise: float = 0.1,
                           n_palettes: int = 128, zipf: float = 1.1, palsize: int = 16):
     """SURVEY.md 8(d) C4 GlobalTiling input: n palette-index tiles drawn from `protos` prototypes with

@@ -1,0 +1,265 @@
+/*
+ * ann_kdtree.c -- TEST / BASELINE INFRASTRUCTURE ONLY: the reference's CPU search for FrameTiling,
+ * an ANN 1.1.2 kd-tree (ann_kdtree_create(pa, n, 192, bs = 1, ANN_KD_STD), main.pas:3961; searched with
+ * ann_kdtree_search(..., eps = 0), main.pas:4027).  ANN's source is not in /root/reference (ANN.dll is a
+ * Windows PE: SURVEY.md 8(a) a8, 8(c)); this restates the published ANN 1.1.2 algorithm with the
+ * arithmetic recovered from the DLL:
+ *   build  (kd_tree ctor, rkd_tree with kd_split = ANN_KD_STD): enclosing box of all points; at each node
+ *          cut_dim = first dimension of maximum spread (max - min) over the node's points, n_lo = n / 2,
+ *          quickselect so the n_lo smallest coordinates go low, cut_val = (max of low side + n_lo-th
+ *          value) / 2; the node keeps the cell's bounds along cut_dim; buckets of 1 point (bs = 1).
+ *   search (annkSearch, k = 1): box distance of q to the root box; at a split node visit the child on
+ *          q's side first, then update box_dist += cut_diff^2 - box_diff^2 (fp32, ANNdist = float) and
+ *          visit the far child iff box_dist * (1 + eps)^2 < current best; leaf distance = sequential fp32
+ *          sum of (q_d - p_d)^2, no FMA, break as soon as dist > best; insert iff the scan completed
+ *          and dist < best (an equal distance keeps the first found: ANNmin_k::insert).
+ * The tie order among equal distances is the tree's visit order (parity-unpinned):
+ * bench.py compares its distances, not its indices, with the GPU's.
+ */
+#include <float.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "tiler_oracle.h"
+
+typedef struct {
+    int cut_dim;   /* -1: leaf */
+    float cut_val;
+    float lo_bnd;  /* cell bounds along cut_dim */
+    float hi_bnd;
+    int child[2];  /* split: node ids; leaf: child[0] = point index or -1 (empty bucket) */
+} kd_node;
+
+typedef struct {
+    const float *data;
+    int n, d;
+    kd_node *nodes;
+    int nn;
+    int *pidx;
+    float *box_lo, *box_hi;
+} kd_tree;
+
+#define PA(i, dim) (t->data[(size_t)t->pidx[(i)] * t->d + (dim)])
+
+static int kd_new(kd_tree *t) { return t->nn++; }
+
+static int max_spread(kd_tree *t, int *pidx, int n) {
+    int best = 0;
+    float best_sp = -1.0f;
+    for (int dim = 0; dim < t->d; dim++) {
+        float mn = t->data[(size_t)pidx[0] * t->d + dim], mx = mn;
+        for (int i = 1; i < n; i++) {
+            const float c = t->data[(size_t)pidx[i] * t->d + dim];
+            if (c < mn) mn = c;
+            if (c > mx) mx = c;
+        }
+        if (mx - mn > best_sp) {
+            best_sp = mx - mn;
+            best = dim;
+        }
+    }
+    return best;
+}
+
+/* quickselect on pidx[0..n) by coordinate dim: afterwards the n_lo smallest sit in [0, n_lo) with
+ * the largest of them at n_lo - 1, and [n_lo] holds the n_lo-th value; returns the midpoint cut. */
+static float median_split(const float *data, int d, int *pidx, int n, int dim, int n_lo) {
+#define C(i) (data[(size_t)pidx[(i)] * d + dim])
+#define SWAP(a, b) do { int _t = pidx[(a)]; pidx[(a)] = pidx[(b)]; pidx[(b)] = _t; } while (0)
+    int l = 0, r = n - 1;
+    while (l < r) {
+        int i = (r + l) / 2, k;
+        if (C(i) > C(r)) SWAP(i, r);
+        SWAP(l, i);
+        const float c = C(l);
+        i = l;
+        k = r;
+        for (;;) {
+            while (C(++i) < c) {}
+            while (C(--k) > c) {}
+            if (i < k) SWAP(i, k);
+            else break;
+        }
+        SWAP(l, k);
+        if (k > n_lo) r = k - 1;
+        else if (k < n_lo) l = k + 1;
+        else break;
+    }
+    if (n_lo > 0) {
+        float c = C(0);
+        int k = 0;
+        for (int i = 1; i < n_lo; i++)
+            if (C(i) > c) {
+                c = C(i);
+                k = i;
+            }
+        SWAP(n_lo - 1, k);
+    }
+    return (C(n_lo - 1) + C(n_lo)) / 2.0f;
+#undef C
+#undef SWAP
+}
+
+static int kd_build(kd_tree *t, int *pidx, int n, float *lo, float *hi) {
+    const int id = kd_new(t);
+    kd_node *nd = &t->nodes[id];
+    if (n <= 1) {
+        nd->cut_dim = -1;
+        nd->child[0] = n == 1 ? pidx[0] : -1;
+        return id;
+    }
+    const int cd = max_spread(t, pidx, n);
+    const int n_lo = n / 2;
+    const float cv = median_split(t->data, t->d, pidx, n, cd, n_lo);
+    nd->cut_dim = cd;
+    nd->cut_val = cv;
+    nd->lo_bnd = lo[cd];
+    nd->hi_bnd = hi[cd];
+    const float save_hi = hi[cd];
+    hi[cd] = cv;
+    const int a = kd_build(t, pidx, n_lo, lo, hi);
+    hi[cd] = save_hi;
+    const float save_lo = lo[cd];
+    lo[cd] = cv;
+    const int b = kd_build(t, pidx + n_lo, n - n_lo, lo, hi);
+    lo[cd] = save_lo;
+    t->nodes[id].child[0] = a;
+    t->nodes[id].child[1] = b;
+    return id;
+}
+
+void *or_kdtree_build(const float *data, int n, int d) {
+    kd_tree *t = (kd_tree *)calloc(1, sizeof(kd_tree));
+    t->data = data;
+    t->n = n;
+    t->d = d;
+    t->nodes = (kd_node *)malloc(sizeof(kd_node) * (size_t)(2 * (n > 0 ? n : 1)));
+    t->pidx = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+    t->box_lo = (float *)malloc(sizeof(float) * (size_t)d);
+    t->box_hi = (float *)malloc(sizeof(float) * (size_t)d);
+    for (int i = 0; i < n; i++) t->pidx[i] = i;
+    for (int dim = 0; dim < d; dim++) {  /* annEnclRect */
+        float mn = n ? data[dim] : 0.0f, mx = mn;
+        for (int i = 1; i < n; i++) {
+            const float c = data[(size_t)i * d + dim];
+            if (c < mn) mn = c;
+            if (c > mx) mx = c;
+        }
+        t->box_lo[dim] = mn;
+        t->box_hi[dim] = mx;
+    }
+    float *lo = (float *)malloc(sizeof(float) * (size_t)d), *hi = (float *)malloc(sizeof(float) * (size_t)d);
+    memcpy(lo, t->box_lo, sizeof(float) * (size_t)d);
+    memcpy(hi, t->box_hi, sizeof(float) * (size_t)d);
+    kd_build(t, t->pidx, n, lo, hi);
+    free(lo);
+    free(hi);
+    return t;
+}
+
+void or_kdtree_free(void *p) {
+    kd_tree *t = (kd_tree *)p;
+    if (!t) return;
+    free(t->nodes);
+    free(t->pidx);
+    free(t->box_lo);
+    free(t->box_hi);
+    free(t);
+}
+
+typedef struct {
+    const kd_tree *t;
+    const float *q;
+    float best;
+    int bi;
+    long visited;
+} kd_query;
+
+static void kd_search(kd_query *s, int id, float box_dist) {
+    const kd_node *nd = &s->t->nodes[id];
+    if (nd->cut_dim < 0) {
+        const int j = nd->child[0];
+        if (j < 0) return;
+        const float *p = s->t->data + (size_t)j * s->t->d;
+        float dist = 0.0f;
+        int i;
+        s->visited++;
+        for (i = 0; i < s->t->d; i++) {
+            const float t = s->q[i] - p[i];
+            const float sq = t * t;
+            dist = dist + sq;
+            if (dist > s->best) break;
+        }
+        if (i >= s->t->d && dist < s->best) {
+            s->best = dist;
+            s->bi = j;
+        }
+        return;
+    }
+    const float cut_diff = s->q[nd->cut_dim] - nd->cut_val;
+    if (cut_diff < 0) {
+        kd_search(s, nd->child[0], box_dist);
+        float box_diff = nd->lo_bnd - s->q[nd->cut_dim];
+        if (box_diff < 0) box_diff = 0;
+        box_dist = box_dist + (cut_diff * cut_diff - box_diff * box_diff);
+        if (box_dist * 1.0f < s->best) kd_search(s, nd->child[1], box_dist);
+    } else {
+        kd_search(s, nd->child[1], box_dist);
+        float box_diff = s->q[nd->cut_dim] - nd->hi_bnd;
+        if (box_diff < 0) box_diff = 0;
+        box_dist = box_dist + (cut_diff * cut_diff - box_diff * box_diff);
+        if (box_dist * 1.0f < s->best) kd_search(s, nd->child[0], box_dist);
+    }
+}
+
+static int kd_nn(const kd_tree *t, const float *q, float *err, long *visited) {
+    kd_query s = {t, q, FLT_MAX, -1, 0};
+    if (t->n > 0) {
+        float bd = 0.0f;  /* annBoxDistance */
+        for (int dim = 0; dim < t->d; dim++) {
+            float v = 0.0f;
+            if (q[dim] < t->box_lo[dim]) v = t->box_lo[dim] - q[dim];
+            else if (q[dim] > t->box_hi[dim]) v = q[dim] - t->box_hi[dim];
+            bd = bd + v * v;
+        }
+        kd_search(&s, 0, bd);
+    }
+    if (err) *err = s.best;
+    if (visited) *visited += s.visited;
+    return s.bi;
+}
+
+typedef struct {
+    const kd_tree *t;
+    const float *q;
+    int nq, tid, threads;
+    int *idx;
+    float *err;
+    long visited;
+} kd_job;
+
+static void *kd_worker(void *p) {
+    kd_job *j = (kd_job *)p;
+    for (int i = j->tid; i < j->nq; i += j->threads)
+        j->idx[i] = kd_nn(j->t, j->q + (size_t)i * j->t->d, &j->err[i], &j->visited);
+    return NULL;
+}
+
+long or_kdtree_search_batch(void *p, const float *q, int nq, int *idx, float *err, int threads) {
+    const kd_tree *t = (const kd_tree *)p;
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    kd_job jobs[256];
+    for (int i = 0; i < threads; i++) {
+        jobs[i] = (kd_job){t, q, nq, i, threads, idx, err, 0};
+        pthread_create(&th[i], NULL, kd_worker, &jobs[i]);
+    }
+    long visited = 0;
+    for (int i = 0; i < threads; i++) {
+        pthread_join(th[i], NULL);
+        visited += jobs[i].visited;
+    }
+    return visited;
+}

@@ -104,6 +104,38 @@ def nn_batch(data, qs, threads=None):
     return idx, err
 
 
+class KDTree:
+    """The reference's CPU FrameTiling search: ANN 1.1.2 kd-tree (ann_kdtree.c), k = 1, eps = 0."""
+
+    def __init__(self, data):
+        self.data = np.ascontiguousarray(data, np.float32)
+        f = lib().or_kdtree_build
+        f.restype = ctypes.c_void_p
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        self.h = f(_p(self.data), self.data.shape[0], self.data.shape[1])
+        self.visited = 0
+
+    def search_batch(self, qs, threads=None):
+        qs = np.ascontiguousarray(qs, np.float32)
+        idx = np.zeros(qs.shape[0], np.int32)
+        err = np.zeros(qs.shape[0], np.float32)
+        f = lib().or_kdtree_search_batch
+        f.restype = ctypes.c_long
+        f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        self.visited += f(self.h, _p(qs), qs.shape[0], _p(idx), _p(err), threads or _threads())
+        return idx, err
+
+    def close(self):
+        if self.h:
+            f = lib().or_kdtree_free
+            f.argtypes = [ctypes.c_void_p]
+            f(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
 def build_ft_dataset(used, palpix, thm, tvm, palettes, use_wavelets=True, gamma=-1):
     used = np.ascontiguousarray(used, np.uint8)
     P, T, _ = used.shape

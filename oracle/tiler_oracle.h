@@ -50,6 +50,11 @@ int or_nn(const float *data, int n, int d, const float *q, float *err);
 void or_knn(const float *data, int n, int d, const float *q, int k, int *idx, float *err);
 void or_nn_batch(const float *data, int n, int d, const float *q, int nq, int *idx, float *err, int threads);
 
+/* ANN 1.1.2 kd-tree (ANN_KD_STD, bucket 1, eps 0): the reference's CPU search (ann_kdtree.c). */
+void *or_kdtree_build(const float *data, int n, int d);
+void or_kdtree_free(void *t);
+long or_kdtree_search_batch(void *t, const float *q, int nq, int *idx, float *err, int threads);
+
 int or_prepare_global_ds(const uint8_t *palpix, const uint8_t *active, int T, float *ds, int32_t *tile_idx,
                          uint8_t *attrs);
 double or_palette_corr(const double *centroids, int P, double *corrs);

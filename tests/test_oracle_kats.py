@@ -221,3 +221,28 @@ def test_prepare_tile_mirrors_canonical():
     t = np.zeros((1, 64), np.uint8)
     _, hm, vm = synth.prepare_tile_mirrors(t)  # all equal -> first (no mirror)
     assert hm[0] == 0 and vm[0] == 0
+
+
+def test_ann_kdtree_baseline_exact_distances(oracle):
+    """The CPU baseline's ANN-style kd-tree (oracle/ann_kdtree.c) returns the exhaustive scan's distance
+    bit for bit (eps = 0), including duplicate rows, flat queries and an empty tree; among equal distances
+    it may pick another index (ANN's visit order)."""
+    from tiler_amd import synth
+    rng = np.random.default_rng(12)
+    tiles, thm, tvm = synth.tileset(rng, 600)
+    pals = synth.palettes(rng, 4)
+    used = synth.used_one_palette(rng.integers(0, 4, 600).astype(np.int32), 4)
+    rows, *_ = oracle.build_ft_dataset(used, tiles, thm, tvm, pals)
+    q = np.concatenate([oracle.psyv_batch(400, rgb=synth.frame_tiles(rng, 400), flags=2).astype(np.float32),
+                        rows[::37]])
+    kd = oracle.KDTree(rows)
+    ki, ke = kd.search_batch(q, threads=4)
+    si, se = oracle.nn_batch(rows, q, threads=4)
+    assert np.array_equal(ke.view(np.uint32), se.view(np.uint32))
+    d = ((rows[ki].astype(np.float64) - q) ** 2).sum(1)
+    assert np.allclose(d, se, rtol=1e-5)
+    assert 0 < kd.visited < len(q) * rows.shape[0]
+    kd.close()
+    e = oracle.KDTree(np.zeros((0, 192), np.float32))
+    i, _ = e.search_batch(q[:3], threads=1)
+    assert (i == -1).all()

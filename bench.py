@@ -159,7 +159,8 @@ def main():
     elapsed = time.perf_counter() - t0
     lib.tiler_timing_enable(0)
     kernels = {}
-    for name in ("psyv", "nn_prep", "nn_orbit", "nn_shortlist", "nn_rescore", "nn_collect", "nn_rescore2", "nn_exact"):
+    for name in ("psyv", "nn_prep", "nn_orbit", "nn_shortlist", "nn_rescore", "nn_pairs", "nn_collect", "nn_rescore2",
+                 "nn_exact"):
         n = ctypes.c_int(0)
         ms = lib.tiler_timing_get(name.encode(), ctypes.byref(n))
         kernels[name] = {"ms_total": round(ms, 4), "launches": n.value,

@@ -516,6 +516,8 @@ struct OrbitRescoreArgs {
     const int *id;
     int G, nq, L, nsplit;
     int p1;                         // entries re-keyed in the first pass (1..4)
+    int *pair_cnt;                  // [nq] candidates handed to the pair pass (0: settled here or by tiers 2/3)
+    int *pair_cand;                 // [nq][ORB_PSLOTS]
     double scale2;                  // scale^2
     double N, Np, Hp, Ecp;
     OrbitTail t;
@@ -592,6 +594,7 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
 // operation below stays inside the half (xor offsets < 32, ballots masked to the half).
 static constexpr int ORB_QCAP = 64;  // rescore queue per query
 static constexpr int ORB_STG = 4;    // candidate rows staged in LDS per pass
+static constexpr int ORB_PSLOTS = 8; // candidates per query handed to the pair pass
 
 __device__ __forceinline__ float half_min_f(float v) {
     for (int o = 16; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
@@ -617,6 +620,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
     if (q >= a.nq) return;
     const OrbitTail &t = a.t;
     const OrbitStat st = a.ostat[q];
+    if (l == 0) a.pair_cnt[q] = 0;  // the pair pass skips queries settled here or by tiers 2/3
     if (st.flags & 2) {
         if (l == 0) t.ex_list[atomicAdd(t.ex_count, 1)] = (int)q;
         return;
@@ -754,6 +758,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
         enqueue(c, k);
     }
     __builtin_amdgcn_wave_barrier();
+    if (nres == 0 && cnt > 0 && cnt <= ORB_PSLOTS) {
+        // the usual case: a few candidates -> the reference distances run lane-parallel in the pair pass
+        if (l < cnt) a.pair_cand[q * ORB_PSLOTS + l] = sc[l];
+        if (l == 0) {
+            a.pair_cnt[q] = cnt;
+            if (t.n_expand) {
+                atomicAdd(t.n_expand, nexp);
+                atomicAdd(t.n_expand + 1, cnt);
+            }
+        }
+        return;
+    }
     flush();
     half_argmin(bd, bi);
     if (l == 0) {
@@ -768,6 +784,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
             t.m_tile[q] = ok ? t.tr_tile[bi] : -1;
             t.m_pal[q] = ok ? t.tr_pal[bi] : -1;
             const int at = ok ? t.tr_attr[bi] : 0;
+            t.m_hm[q] = (at & 1) != 0;
+            t.m_vm[q] = (at & 2) != 0;
+        }
+    }
+}
+
+// The reference distances of the rescore's queue, lane-parallel: lane = (query, slot), ORB_PSLOTS lanes per
+// query; each lane sums its candidate in the reference order (sequential fp32, every op rounded), the
+// query's lanes pick (distance, index) lexicographically and the first writes the tilemap item.  Running
+// these 192-step chains here instead of one lane per candidate inside the half-wave rescore keeps the
+// rescore's instruction stream short (it is latency-bound) and fills the lanes.
+__global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a) {
+    const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+    const long q = gid / ORB_PSLOTS;
+    const int s = (int)(gid % ORB_PSLOTS);
+    if (q >= a.nq) return;  // whole groups: 256 % ORB_PSLOTS == 0
+    const int n = a.pair_cnt[q];
+    if (n == 0) return;  // uniform over the group
+    float bd = INFINITY;
+    int bi = 0x7fffffff;
+    if (s < n) {
+        const int c = a.pair_cand[q * ORB_PSLOTS + s];
+        bd = exact_dist192_lean(a.q + q * OD, a.rows + (long)c * OD);
+        bi = c;
+    }
+#pragma unroll
+    for (int o = ORB_PSLOTS / 2; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bd, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        const bool take = (ov < bd) || (ov == bd && (unsigned)oi < (unsigned)bi);
+        bd = take ? ov : bd;
+        bi = take ? oi : bi;
+    }
+    if (s == 0) {
+        const OrbitTail &t = a.t;
+        t.out_idx[q] = bi;
+        t.out_err[q] = bd;
+        if (t.m_tile) {
+            t.m_tile[q] = t.tr_tile[bi];
+            t.m_pal[q] = t.tr_pal[bi];
+            const int at = t.tr_attr[bi];
             t.m_hm[q] = (at & 1) != 0;
             t.m_vm[q] = (at & 2) != 0;
         }
@@ -848,6 +905,8 @@ void orbit_destroy(OrbitIndex *o) {
     hipFree(o->qrowh);
     hipFree(o->qstat);
     hipFree(o->thr_real);
+    hipFree(o->pair_cnt);
+    hipFree(o->pair_cand);
     hipFree(o->d_stats);
     hipFree(o->key);
     hipFree(o->id);
@@ -970,7 +1029,11 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         hipFree(o->qrowh);
         hipFree(o->qstat);
         hipFree(o->thr_real);
+        hipFree(o->pair_cnt);
+        hipFree(o->pair_cand);
         TILER_HIP_CHECK(hipMalloc((void **)&o->thr_real, (size_t)nq * sizeof(double)));
+        TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cnt, (size_t)nq * sizeof(int)));
+        TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cand, (size_t)nq * ORB_PSLOTS * sizeof(int)));
         TILER_HIP_CHECK(hipMalloc(&o->qfrag, (size_t)(nqblk + 1) * OS * 1024));
         TILER_HIP_CHECK(hipMalloc(&o->qrowh, (size_t)nq * OD * 2));
         TILER_HIP_CHECK(hipMalloc((void **)&o->qstat, (size_t)nq * sizeof(OrbitStat)));
@@ -1036,6 +1099,8 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         return v < 1 ? 1 : v > 2 ? 2 : v;
     }();
     ra.p1 = p1;
+    ra.pair_cnt = o->pair_cnt;
+    ra.pair_cand = o->pair_cand;
     ra.scale2 = (double)ix->scale * (double)ix->scale;
     ra.N = o->N;
     ra.Np = o->Np;
@@ -1055,6 +1120,13 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     {
         KTimer tm("nn_rescore", stream);
         hipLaunchKernelGGL(nn_orbit_rescore_kernel, dim3((nq + 7) / 8), dim3(256), 0, stream, ra);
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    {
+        static_assert(256 % ORB_PSLOTS == 0, "pair groups must not straddle blocks");
+        KTimer tm("nn_pairs", stream);
+        const long lanes = (long)nq * ORB_PSLOTS;
+        hipLaunchKernelGGL(nn_orbit_pairs_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, ra);
     }
     TILER_HIP_CHECK(hipGetLastError());
     {

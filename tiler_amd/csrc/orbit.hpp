@@ -38,6 +38,7 @@ struct OrbitIndex {
     void *qfrag = nullptr, *qrowh = nullptr;
     OrbitStat *qstat = nullptr;
     double *thr_real = nullptr;
+    int *pair_cnt = nullptr, *pair_cand = nullptr;  // rescore -> pair pass hand-off
     size_t cap_q = 0;
     float *key = nullptr;
     int *id = nullptr;

@@ -246,3 +246,17 @@ def test_ann_kdtree_baseline_exact_distances(oracle):
     e = oracle.KDTree(np.zeros((0, 192), np.float32))
     i, _ = e.search_batch(q[:3], threads=1)
     assert (i == -1).all()
+
+
+def test_fast_colour_division_is_exact(tmp_path):
+    """psyv.hip's gamma = -1 query path replaces x / 10000.0 by a reciprocal multiply + one fma correction;
+    it must equal the IEEE division for every colour sum of the domain (2^24 cases, oracle/check_fastdiv.c)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    exe = tmp_path / "check_fastdiv"
+    src = os.path.join(os.path.dirname(__file__), "..", "oracle", "check_fastdiv.c")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), src, "-lm"], check=True)
+    tot, bad = map(int, subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split())
+    assert tot == 1 << 24 and bad == 0

@@ -51,6 +51,94 @@ __global__ __launch_bounds__(256) void psyv_kernel(PsyvArgs a) {
     }
 }
 
+// FrameTiling query descriptors (RGB, no mirror, Haar: DoFrameTiling main.pas:4023): one LANE per tile, the
+// whole 3-level WaveletGS of each component in registers with compile-time indices (no cross-lane traffic),
+// gamma LUT in LDS.  Same fp64 operations in the same order as psyv_kernel / the CPU restatement.
+__device__ __forceinline__ void haar_regs(double (&p)[64], double f) {
+#pragma unroll
+    for (int dx = 8; dx >= 2; dx >>= 1) {
+        const int h = dx >> 1;
+#pragma unroll
+        for (int y = 0; y < dx; y++) {  // rows: L at x, H at x + dx/2
+            double t[8];
+#pragma unroll
+            for (int x = 0; x < h; x++) {
+                const double a = p[y * 8 + 2 * x], b = p[y * 8 + 2 * x + 1];
+                t[x] = (a + b) * f;
+                t[x + h] = (a - b) * f;
+            }
+#pragma unroll
+            for (int x = 0; x < dx; x++) p[y * 8 + x] = t[x];
+        }
+#pragma unroll
+        for (int x = 0; x < dx; x++) {  // columns
+            double t[8];
+#pragma unroll
+            for (int y = 0; y < h; y++) {
+                const double a = p[(2 * y) * 8 + x], b = p[(2 * y + 1) * 8 + x];
+                t[y] = (a + b) * f;
+                t[y + h] = (a - b) * f;
+            }
+#pragma unroll
+            for (int y = 0; y < dx; y++) p[y * 8 + x] = t[y];
+        }
+    }
+}
+
+// x / 10000.0 for the gamma = -1 colour sums (fr = r / 255.0): q0 = x * RN(1e-4) plus one fma residual
+// correction.  Bit-identical to the IEEE division over every (r, g, b) of the domain (all 2^24 sums checked
+// by oracle/check_fastdiv.c, tests/test_oracle_kats.py); other gamma LUTs keep the true division.
+template <bool FASTDIV>
+__device__ __forceinline__ double div10000(double x) {
+    if constexpr (FASTDIV) {
+        const double inv = 1.0 / 10000.0;
+        const double q0 = x * inv;
+        return __builtin_fma(__builtin_fma(-q0, 10000.0, x), inv, q0);
+    } else {
+        return x / 10000.0;
+    }
+}
+
+template <bool FASTDIV>
+__global__ __launch_bounds__(64) void psyv_rgb_haar_kernel(PsyvArgs a) {
+    __shared__ double lut[256];
+    const int lane = threadIdx.x;
+    const double *__restrict__ glut = a.gamma_lut + 256 * (a.gamma + 1);
+    for (int i = lane; i < 256; i += 64) lut[i] = glut[i];
+    __syncthreads();
+    const long i = (long)blockIdx.x * 64 + lane;
+    if (i >= a.n) return;
+    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + i * 64);
+#pragma unroll 1
+    for (int c = 0; c < 3; c++) {
+        double p[64];
+#pragma unroll
+        for (int k4 = 0; k4 < 16; k4++) {
+            const int4 v = src[k4];  // re-read per component (L1): keeps 64 colours out of the registers
+            const int cc[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int r = cc[e] & 0xff, g = (cc[e] >> 8) & 0xff, b = (cc[e] >> 16) & 0xff;
+                const double fr = lut[r], fg = lut[g], fb = lut[b];
+                const double cy = div10000<FASTDIV>(2126.0 * fr + 7152.0 * fg + 722.0 * fb);
+                p[4 * k4 + e] = c == 0 ? cy : c == 1 ? (fb - cy) * a.u_mul : (fr - cy) * a.v_mul;
+            }
+        }
+        haar_regs(p, a.haar_f);
+        if (a.out32) {
+            float4 *o = reinterpret_cast<float4 *>(a.out32 + i * 192 + c * 64);
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                o[k] = make_float4((float)p[4 * k], (float)p[4 * k + 1], (float)p[4 * k + 2], (float)p[4 * k + 3]);
+        }
+        if (a.out64) {
+            double2 *o = reinterpret_cast<double2 *>(a.out64 + i * 192 + c * 64);
+#pragma unroll
+            for (int k = 0; k < 32; k++) o[k] = make_double2(p[2 * k], p[2 * k + 1]);
+        }
+    }
+}
+
 int launch_psyv(PsyvArgs args, hipStream_t stream) {
     if (args.n <= 0) return 0;
     const Luts &L = luts();
@@ -65,10 +153,18 @@ int launch_psyv(PsyvArgs args, hipStream_t stream) {
         set_error("psyv: gamma must be -1, 0 or 1");
         return -1;
     }
-    long blocks = (args.n + 3) / 4;
-    if (blocks > 65536) blocks = 65536;
     KTimer tm("psyv", stream);
-    hipLaunchKernelGGL(psyv_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, args);
+    if (args.rgb && !args.flags_per && (args.flags & ~PSYV_QWEIGHT) == PSYV_WAVELETS) {
+        const dim3 grid((unsigned)((args.n + 63) / 64));
+        if (args.gamma == -1)
+            hipLaunchKernelGGL(psyv_rgb_haar_kernel<true>, grid, dim3(64), 0, stream, args);
+        else
+            hipLaunchKernelGGL(psyv_rgb_haar_kernel<false>, grid, dim3(64), 0, stream, args);
+    } else {
+        long blocks = (args.n + 3) / 4;
+        if (blocks > 65536) blocks = 65536;
+        hipLaunchKernelGGL(psyv_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, args);
+    }
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }

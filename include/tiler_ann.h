@@ -142,6 +142,15 @@ int tiler_kmodes_batch_dev(const uint8_t *d_X, const int32_t *bin_off, int nbins
 int tiler_kmodes_medoids_batch(const uint8_t *X, const int32_t *bin_off, int nbins, const int32_t *k,
                                const int32_t *labels, const uint8_t *centroids, int32_t *medoid, int32_t *counts);
 
+/* ---- GTM keyframe stream compression (host code) ---------------------------------------------------
+ * Replaces LZCompress (extern.pas:202-240: temp file + external `lzma.exe e src dst -lc8 -eos`, called
+ * per keyframe by SaveStream main.pas:4734).  Writes an LZMA-alone stream (13-byte header: properties
+ * (pb*5+lp)*9+lc, dictionary size u32, uncompressed size u64 = all ones when eos != 0) into dst.
+ * dst == NULL: only *out_len (the exact size) is computed; cap too small: -1 with *out_len = size needed.
+ * 0 ok, -1 error (tiler_last_error). */
+int tiler_lzma_encode(const uint8_t *src, size_t n, int lc, int lp, int pb, uint32_t dict_size, int eos,
+                      uint8_t *dst, size_t cap, size_t *out_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,6 +19,7 @@
 #ifndef TILER_ORACLE_H
 #define TILER_ORACLE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -54,6 +55,9 @@ void or_nn_batch(const float *data, int n, int d, const float *q, int nq, int *i
 void *or_kdtree_build(const float *data, int n, int d);
 void or_kdtree_free(void *t);
 long or_kdtree_search_batch(void *t, const float *q, int nq, int *idx, float *err, int threads);
+
+/* LZMA-alone decoder (lzma_dec.c): decoded size, -1 corrupt, -2 out too small; consumed = bytes read. */
+long or_lzma_decode(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *consumed);
 
 int or_prepare_global_ds(const uint8_t *palpix, const uint8_t *active, int T, float *ds, int32_t *tile_idx,
                          uint8_t *attrs);

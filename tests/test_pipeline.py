@@ -125,3 +125,13 @@ def test_run_all_chain_bit_exact(gpu, oracle, quality):
     for a, b in zip((sm["tile"], sm["pal"], sm["hm"], sm["vm"], sm["smoothed"]), o["smooth"]):
         assert np.array_equal(a, b)
     assert sm["smoothed"].sum() > 0
+    # SaveStream: the .gtm carries exactly the SmoothedTileMap items
+    from gtm_read import read_gtm
+    g = read_gtm(oracle, e.save_stream(320, 240, 24.0))
+    assert len(g.frames) == e.frames and np.array_equal(g.tiles, e.palpix)
+    for f, (items, _, _) in enumerate(g.frames):
+        live = ~sm["smoothed"][f].astype(bool)
+        assert np.array_equal(items[:, 0] >= 0, live)
+        t = sm["tile"][f]
+        attrs = (sm["pal"][f] << 2) | ((sm["vm"][f] ^ e.tvm[t]) << 1) | (sm["hm"][f] ^ e.thm[t])
+        assert np.array_equal(items[live, 0], t[live]) and np.array_equal(items[live, 1], attrs[live])

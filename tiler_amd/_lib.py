@@ -18,6 +18,8 @@ c_float = ctypes.c_float
 c_double = ctypes.c_double
 c_void_p = ctypes.c_void_p
 c_char_p = ctypes.c_char_p
+c_size_t = ctypes.c_size_t
+c_uint32 = ctypes.c_uint32
 P = ctypes.POINTER
 
 
@@ -72,6 +74,8 @@ _SIGS = {
                                            c_void_p]),
     "tiler_kmodes_compute": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
+    "tiler_lzma_encode": (c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_uint32, c_int, c_void_p, c_size_t,
+                                  c_void_p]),
 }
 
 _lib = None

@@ -15,6 +15,7 @@ import numpy as np
 
 from . import frame_tiling as ft
 from . import global_tiling as gt
+from .gtm import save_stream
 from .smooth import DEFAULT_STRENGTH, smooth_keyframe
 from .synth import Video
 
@@ -143,6 +144,12 @@ class Encoder:
             sm["smoothed"][f0:f1] = s
         self.sm = sm
         return sm
+
+    def save_stream(self, width: int, height: int, fps: float = 24.0) -> bytes:
+        """btnSaveClick -> SaveStream main.pas:4529-4763 (the .gtm bytes; needs do_smooth first)."""
+        sm = self.sm
+        return save_stream(self.palpix, self.thm, self.tvm, self.kf_start, self.palettes, sm["tile"], sm["pal"],
+                           sm["hm"], sm["vm"], sm["smoothed"], width, height, fps, self.palsize)
 
     def run_all(self, desired: int, quality: int = ft.FT_MEDIUM, strength: float = DEFAULT_STRENGTH):
         """btnRunAllClick main.pas:1232-1272 from MakeUnique to Smooth."""

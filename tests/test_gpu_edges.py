@@ -1,0 +1,87 @@
+"""Edge cases of the drop-in surface on the GPU, each against the oracle: zero queries, a single
+candidate, a single query, query counts that are not multiples of the 32-query MFMA blocks, k larger than
+the dataset, orbit datasets with a lone (symmetric) tile, NaN-free extreme-but-finite descriptors, and
+an empty frame through tiler_frame_tiling."""
+import numpy as np
+import pytest
+
+from tiler_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def test_zero_queries(gpu):
+    data = np.random.default_rng(1).normal(0, 1, (100, 192)).astype(np.float32)
+    with gpu.KDTree(data) as kdt:
+        i, e = kdt.search_batch(np.zeros((0, 192), np.float32))
+        assert i.size == 0 and e.size == 0
+
+
+def test_single_candidate_and_single_query(gpu, oracle):
+    rng = np.random.default_rng(2)
+    data = rng.normal(0, 1, (1, 192)).astype(np.float32)
+    q = rng.normal(0, 1, (5, 192)).astype(np.float32)
+    with gpu.KDTree(data) as kdt:
+        gi, ge = kdt.search_batch(q)
+        i1, e1 = kdt.search(q[0])
+    oi, oe = oracle.nn_batch(data, q)
+    assert np.array_equal(gi, oi) and np.array_equal(ge.view(np.uint32), oe.view(np.uint32))
+    assert i1 == 0 and np.float32(e1) == oe[0]
+
+
+@pytest.mark.parametrize("nq", [1, 31, 33, 65, 511, 513])
+def test_ragged_query_counts_orbit(gpu, oracle, nq):
+    """Orbit path with query counts around the 32-query block and 512-query workgroup edges."""
+    rng = np.random.default_rng(nq)
+    tiles, thm, tvm = synth.tileset(rng, 300)
+    pals = synth.palettes(rng, 4)
+    used = synth.used_one_palette(rng.integers(0, 4, 300).astype(np.int32), 4)
+    ods, *_ = oracle.build_ft_dataset(used, tiles, thm, tvm, pals)
+    q = oracle.psyv_batch(nq, rgb=synth.frame_tiles(rng, nq), flags=2).astype(np.float32)
+    with gpu.KDTree(ods) as kdt:
+        gi, ge = kdt.search_batch(q)
+        st = kdt.stats()
+    oi, oe = oracle.nn_batch(ods, q)
+    assert st["orbit_search"] == 1
+    assert np.array_equal(gi, oi) and np.array_equal(ge.view(np.uint32), oe.view(np.uint32))
+
+
+def test_k_larger_than_dataset(gpu, oracle):
+    rng = np.random.default_rng(4)
+    data = rng.integers(0, 16, (5, 64)).astype(np.float32)
+    q = rng.integers(0, 16, (3, 64)).astype(np.float32)
+    with gpu.KDTree(data) as kdt:
+        gi, ge = kdt.search_batch(q, k=8)
+    for j in range(3):
+        oi, oe = oracle.knn(data, q[j], 8)
+        assert np.array_equal(gi[j], oi) and np.array_equal(ge[j], oe)
+        assert (gi[j, 5:] == -1).all()
+
+
+def test_lone_symmetric_tile_orbit(gpu, oracle):
+    """A dataset of one fully symmetric tile in 4 orientations (4 identical rows) and one plain tile:
+    every query's winner is the lowest index among equal rows."""
+    t = np.zeros((2, 64), np.uint8)
+    t[0] = 5
+    t[1] = np.arange(64) % 16
+    thm = np.zeros(2, np.uint8)
+    tvm = np.zeros(2, np.uint8)
+    pals = synth.palettes(np.random.default_rng(5), 1)
+    used = np.ones((1, 2, 4), np.uint8)
+    ods, *_ = oracle.build_ft_dataset(used, t, thm, tvm, pals)
+    rng = np.random.default_rng(6)
+    q = np.concatenate([ods, oracle.psyv_batch(40, rgb=synth.frame_tiles(rng, 40), flags=2)]).astype(np.float32)
+    with gpu.KDTree(ods) as kdt:
+        gi, ge = kdt.search_batch(q)
+    oi, oe = oracle.nn_batch(ods, q)
+    assert np.array_equal(gi, oi) and np.array_equal(ge.view(np.uint32), oe.view(np.uint32))
+    assert gi[1] == 0 and gi[3] == 0  # the symmetric tile's mirrors resolve to its first row
+
+
+def test_empty_frame_through_frame_tiling(gpu):
+    from tiler_amd.frame_tiling import KeyframeTiler
+    wl = synth.make_workload(7, 64, 64, 1, 64, n_palettes=4)
+    kt = KeyframeTiler(wl.tiles, wl.thm, wl.tvm, wl.palettes, wl.ds)
+    t, p, h, v, e = kt.do_frame_tiling(np.zeros((0, 64), np.int32))
+    assert t.size == 0 and e.size == 0
+    kt.finish_frame_tiling()

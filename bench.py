@@ -217,7 +217,7 @@ def main():
 
     # ---- CPU baseline (rank 0, N=1): the oracle restatement, bounded sample, same workload ----
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out_hm, out_vm, out_err)
 
     if rank == 0:

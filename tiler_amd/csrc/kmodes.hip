@@ -235,10 +235,24 @@ __global__ __launch_bounds__(256) void km_init_modes2(KmState s, const int32_t *
     }
 }
 
-// ---- the sequential part of one bin (KModesIter kmodes.pas:869-911), one workgroup of 128 ----
-__device__ void move_point_cat(const KmState &s, int ip, int to, int from) {
-    // lanes = attributes (MovePointCat kmodes.pas:778-806); caller syncs around
-    const int a = threadIdx.x;
+// ---- the sequential part of one bin (KModesIter kmodes.pas:869-911), one workgroup of KM_SEQ_NT ----
+static constexpr int KM_SEQ_NT = 512;  // 6 groups of 80 attribute lanes (320..1024 measured: 512 best)
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long u = __shfl_xor(v, o, 64);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
+// MovePointCat (kmodes.pas:778-806) for one point; lane a = attribute (0..79), lane 0 also updates the
+// membership and the cluster sizes.
+__device__ void move_point_cat(const KmState &s, int ip, int to, int from, int a) {
     if (a < KM_A) {
         const int cur = s.X[(long)ip * KM_A + a];
         int32_t *tc = s.freq + ((long)to * KM_A + a) * s.M;
@@ -258,7 +272,7 @@ __device__ void move_point_cat(const KmState &s, int ip, int to, int from) {
             *cf = (uint8_t)bi;
         }
     }
-    if (threadIdx.x == 0) {
+    if (a == 0) {
         s.memb[ip] = to;
         s.csize[to]++;
         s.csize[from]--;
@@ -266,20 +280,28 @@ __device__ void move_point_cat(const KmState &s, int ip, int to, int from) {
 }
 
 // One 960-point chunk applied in order.  The chunk's assignment keys and labels are staged in LDS, the cost
-// is a parallel sum, and only the points that move are visited in order (an ordered compaction; a rescue
-// that relabels a later point of the chunk rebuilds the list from there) -- same sequence of MovePointCat
-// and rescue steps as the reference loop, without a dependent global load per point.
+// is a parallel sum, and only the points that move are visited, in order (an ordered compaction; a rescue
+// that relabels a later point of the chunk rebuilds the list from there).  MovePointCat of a point touches
+// only the state of its two clusters (their counts, modes and sizes), so consecutive moves whose cluster
+// pairs are pairwise disjoint commute exactly: they are applied together, KM_SEQ_G at a time, by groups of
+// 80 lanes.  A move that empties its cluster (size 1 before it) runs alone and is followed by the rescue
+// (GetMaxClusterMembers + a random member, kmodes.pas:886-906), exactly as the reference orders it.
+template <int NT>
 __device__ void bin_seq_body(KmState s, int p0, int p1) {
+    constexpr int KM_SEQ_G = NT / KM_A;  // moves applied concurrently
     __shared__ int sh_i[4];
-    __shared__ unsigned long long sh_best[128];
-    __shared__ int sh_cnt[128];
+    __shared__ unsigned long long sh_best[NT];
+    __shared__ int sh_cnt[NT];
     __shared__ unsigned long long skey[KM_BIN];
     __shared__ int smemb[KM_BIN];
     __shared__ int slist[KM_BIN];
     __shared__ int slen;
+    __shared__ int c_t[KM_SEQ_G], c_cl[KM_SEQ_G], c_old[KM_SEQ_G], c_sz[KM_SEQ_G];
+    __shared__ int g_t[KM_SEQ_G], g_cl[KM_SEQ_G], g_old[KM_SEQ_G];
+    __shared__ int g_n, g_adv, g_single;
     const int n = p1 - p0, tid = threadIdx.x;
     unsigned long long cpart = 0;
-    for (int t = tid; t < n; t += 128) {
+    for (int t = tid; t < n; t += NT) {
         const unsigned long long k = s.akey[p0 + t];
         skey[t] = k;
         smemb[t] = s.memb[p0 + t];
@@ -287,68 +309,127 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
     }
     sh_best[tid] = cpart;
     __syncthreads();
-    for (int o = 64; o > 0; o >>= 1) {
-        if (tid < o) sh_best[tid] += sh_best[tid + o];
-        __syncthreads();
+    if (tid < 64) {  // integer total: exact in any order
+        unsigned long long c = 0;
+        for (int q = tid; q < NT; q += 64) c += sh_best[q];
+        c = wave_sum_u64(c);
+        if (tid == 0) sh_best[0] = c;
     }
+    __syncthreads();
     const unsigned long long cost = sh_best[0];
     int moves = 0;
     int from_pos = 0;
+    auto target = [&](int t) { return (int)(0xFFFFFFFFu - (unsigned)(skey[t] & 0xFFFFFFFFull)); };
     for (;;) {
         // ordered list of the chunk positions >= from_pos whose best cluster differs from their label
+        // (wave 0: contiguous segments per lane, exclusive scan of the counts by shuffles)
         __syncthreads();
-        const int rem = n - from_pos, seg = (rem + 127) / 128;
-        const int a0 = from_pos + tid * seg, a1 = min(n, a0 + seg);
-        int mine = 0;
-        for (int t = a0; t < a1; t++) mine += (int)(0xFFFFFFFFu - (unsigned)(skey[t] & 0xFFFFFFFFull)) != smemb[t];
-        sh_cnt[tid] = mine;
-        __syncthreads();
-        if (tid == 0) {
-            int acc = 0;
-            for (int t = 0; t < 128; t++) {
-                const int c = sh_cnt[t];
-                sh_cnt[t] = acc;
-                acc += c;
+        if (tid < 64) {
+            const int rem = n - from_pos, seg = (rem + 63) / 64;
+            const int a0 = from_pos + tid * seg, a1 = min(n, a0 + seg);
+            int mine = 0;
+            for (int t = a0; t < a1; t++) mine += target(t) != smemb[t];
+            int incl = mine;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(incl, o, 64);
+                if (tid >= o) incl += v;
             }
-            slen = acc;
+            int w = incl - mine;
+            for (int t = a0; t < a1; t++)
+                if (target(t) != smemb[t]) slist[w++] = t;
+            if (tid == 63) slen = incl;
         }
-        __syncthreads();
-        int w = sh_cnt[tid];
-        for (int t = a0; t < a1; t++)
-            if ((int)(0xFFFFFFFFu - (unsigned)(skey[t] & 0xFFFFFFFFull)) != smemb[t]) slist[w++] = t;
         __syncthreads();
         const int len = slen;
         bool rebuilt = false;
-        for (int li = 0; li < len && !rebuilt; li++) {
-            const int t = slist[li], i = p0 + t;
-            const int cl = (int)(0xFFFFFFFFu - (unsigned)(skey[t] & 0xFFFFFFFFull));
-            const int old = smemb[t];
-            if (old == cl) continue;  // uniform
-            moves++;
+        int li = 0;
+        while (li < len && !rebuilt) {
+            // 1. the next KM_SEQ_G candidates of the ordered list, their clusters and the source cluster size
+            if (tid < KM_SEQ_G) {
+                const int k = li + tid;
+                int t = -1, cl = 0, old = 0, sz = 0;
+                if (k < len) {
+                    t = slist[k];
+                    cl = target(t);
+                    old = smemb[t];
+                    sz = old != cl ? s.csize[old] : 0;
+                }
+                c_t[tid] = t;
+                c_cl[tid] = cl;
+                c_old[tid] = old;
+                c_sz[tid] = sz;
+            }
             __syncthreads();
-            move_point_cat(s, i, cl, old);
-            if (tid == 0) smemb[t] = cl;
+            // 2. the longest prefix of them that can run together (in list order)
+            if (tid == 0) {
+                int ng = 0, adv = 0, single = 0;
+                for (int k = 0; k < KM_SEQ_G && c_t[k] >= 0; k++) {
+                    const int cl = c_cl[k], old = c_old[k];
+                    if (cl == old) {  // relabelled by an earlier rescue: no longer a move
+                        adv++;
+                        continue;
+                    }
+                    if (c_sz[k] <= 1) {  // empties its cluster -> alone, then the rescue
+                        if (ng == 0) {
+                            g_t[0] = c_t[k];
+                            g_cl[0] = cl;
+                            g_old[0] = old;
+                            ng = 1;
+                            adv++;
+                            single = 1;
+                        }
+                        break;
+                    }
+                    bool clash = false;
+                    for (int j = 0; j < ng; j++)
+                        clash |= g_cl[j] == cl || g_cl[j] == old || g_old[j] == cl || g_old[j] == old;
+                    if (clash) break;
+                    g_t[ng] = c_t[k];
+                    g_cl[ng] = cl;
+                    g_old[ng] = old;
+                    ng++;
+                    adv++;
+                }
+                g_n = ng;
+                g_adv = adv;
+                g_single = single;
+            }
             __syncthreads();
+            const int ng = g_n;
+            li += g_adv;
+            moves += ng;
+            // 3. apply them: lanes [80 j, 80 j + 80) move point j of the group
+            {
+                const int j = tid / KM_A, a = tid - j * KM_A;
+                if (j < ng) move_point_cat(s, p0 + g_t[j], g_cl[j], g_old[j], a);
+                if (tid < ng) smemb[g_t[tid]] = g_cl[tid];
+            }
+            __syncthreads();
+            if (!g_single) continue;
+            const int t = g_t[0], old = g_old[0];
             if (s.csize[old] != 0) continue;
             // GetMaxClusterMembers (kmodes.pas:631-669): largest cluster, ties -> last
             unsigned long long b = 0;
-            for (int c = tid; c < s.K; c += 128) {
+            for (int c = tid; c < s.K; c += NT) {
                 const unsigned long long v = ((unsigned long long)(unsigned)s.csize[c] << 32) | (unsigned)c;
                 b = v > b ? v : b;
             }
             sh_best[tid] = b;
             __syncthreads();
-            for (int o = 64; o > 0; o >>= 1) {
-                if (tid < o) sh_best[tid] = max(sh_best[tid], sh_best[tid + o]);
-                __syncthreads();
+            if (tid < 64) {
+                unsigned long long m = 0;
+                for (int q = tid; q < NT; q += 64) m = max(m, sh_best[q]);
+                m = wave_max_u64(m);
+                if (tid == 0) sh_best[0] = m;
             }
+            __syncthreads();
             const int from = (int)(sh_best[0] & 0xFFFFFFFFull);
             const int cnt = s.csize[from];
             if (tid == 0) sh_i[0] = (int)km_randint((unsigned)cnt, s.seed);
             __syncthreads();
             const int r = sh_i[0];
             // r-th member of 'from' in ascending point order (choices[RandInt(cnt)], kmodes.pas:895-902)
-            const long chunk = (s.n + 127) / 128;
+            const long chunk = (s.n + NT - 1) / NT;
             const long b0 = tid * chunk, b1 = min((long)s.n, b0 + chunk);
             int cm = 0;
             for (long q = b0; q < b1; q++) cm += s.memb[q] == from;
@@ -356,7 +437,7 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
             __syncthreads();
             if (tid == 0) {
                 int acc = 0, tt = 0;
-                while (tt < 128 && acc + sh_cnt[tt] <= r) acc += sh_cnt[tt++];
+                while (tt < NT && acc + sh_cnt[tt] <= r) acc += sh_cnt[tt++];
                 sh_i[1] = tt;
                 sh_i[2] = r - acc;
             }
@@ -371,7 +452,7 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
             }
             __syncthreads();
             const int qp = sh_i[3];
-            move_point_cat(s, qp, old, from);
+            if (tid < KM_A) move_point_cat(s, qp, old, from, tid);
             if (tid == 0 && qp >= p0 && qp < p1) smemb[qp - p0] = old;
             __syncthreads();
             if (qp - p0 > t && qp < p1) {  // a later point of this chunk was relabelled: rebuild from t + 1
@@ -615,10 +696,11 @@ struct KmSeqItem {
 };
 
 // seq items live in the same work list as the assign items (one KmAsgItem slot each)
-__global__ __launch_bounds__(128) void kmb_seq_strided(KmBatch B, const KmAsgItem *items) {
+template <int NT>
+__global__ __launch_bounds__(NT) void kmb_seq_strided(KmBatch B, const KmAsgItem *items) {
     const KmSeqItem it = *reinterpret_cast<const KmSeqItem *>(items + blockIdx.x);
     KmState s = bin_state(B, it.bin);
-    bin_seq_body(s, it.p0, it.p1);
+    bin_seq_body<NT>(s, it.p0, it.p1);
 }
 
 // ---- DoKModes medoid choice (main.pas:4231-4253): per cluster j with members, the member minimising
@@ -847,7 +929,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                         // seq items are KmSeqItem views of KmAsgItem slots: stride 32 bytes
                         {
                             KTimer tm("kmodes_seq", st);
-                            hipLaunchKernelGGL(kmb_seq_strided, dim3(sp.second), dim3(128), 0, st, B,
+                            hipLaunchKernelGGL(kmb_seq_strided<KM_SEQ_NT>, dim3(sp.second), dim3(KM_SEQ_NT), 0, st, B,
                                                (const KmAsgItem *)items + pos);
                         }
                         pos += sp.second;

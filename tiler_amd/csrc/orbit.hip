@@ -202,6 +202,30 @@ __global__ __launch_bounds__(256) void orbit_eq_kernel(const float *__restrict__
     }
 }
 
+// Members of a group whose rows are identical (a symmetric tile: S_m c == c) have identical exact distances to
+// any query; the rescore keeps only the lowest candidate index of each identical set (the tie rule picks it
+// anyway).  Bit x of dup[g] marks slot x as such a duplicate.  One wave per group.
+__global__ __launch_bounds__(256) void orbit_dup_kernel(const float *__restrict__ rows, const int *__restrict__ member,
+                                                        long G, uint8_t *__restrict__ dup) {
+    const int lane = threadIdx.x & 63;
+    for (long g = (long)blockIdx.x * 4 + (threadIdx.x >> 6); g < G; g += (long)gridDim.x * 4) {
+        int mem[4];
+#pragma unroll
+        for (int x = 0; x < 4; x++) mem[x] = member[g * 4 + x];
+        unsigned bits = 0;
+#pragma unroll
+        for (int x = 1; x < 4; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                if (y == x || mem[x] < 0 || mem[y] < 0 || mem[y] > mem[x]) continue;
+                bool eq = true;
+                for (int i = lane; i < OD; i += 64) eq &= rows[(long)mem[x] * OD + i] == rows[(long)mem[y] * OD + i];
+                if (__all(eq)) bits |= 1u << x;
+            }
+        if (lane == 0) dup[g] = (uint8_t)bits;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // device: transform + fp16 split (dataset rows: member != null, coefficient cs; queries: qs)
 //   lane l of block b holds row b*32 + (l & 31), k = s*16 + 8*(l >> 5) + j  (A and B maps coincide)
@@ -511,6 +535,7 @@ struct OrbitRescoreArgs {
     const _Float16 *rowh, *qrowh;   // fp16 c' [G][192], q' [nq][192]
     const float *nc;                // [G]
     const int *member;              // [G][4]
+    const uint8_t *dup;             // [G] bit x: slot x repeats a lower-index member's row
     const OrbitStat *ostat;
     const float *key;
     const int *id;
@@ -584,7 +609,7 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
     key = INFINITY;
     if (!gv) return -1;
     const int cand = a.member[(long)g * 4 + x];
-    if (cand < 0) return -1;
+    if (cand < 0 || ((a.dup[g] >> x) & 1)) return -1;
     key = (double)a.nc[g] - 2.0 * (double)d;
     return cand;
 }
@@ -594,7 +619,7 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
 // operation below stays inside the half (xor offsets < 32, ballots masked to the half).
 static constexpr int ORB_QCAP = 64;  // rescore queue per query
 static constexpr int ORB_STG = 4;    // candidate rows staged in LDS per pass
-static constexpr int ORB_PSLOTS = 8; // candidates per query handed to the pair pass
+static constexpr int ORB_PSLOTS = 4; // candidates per query handed to the pair pass
 
 __device__ __forceinline__ float half_min_f(float v) {
     for (int o = 16; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
@@ -900,6 +925,7 @@ void orbit_destroy(OrbitIndex *o) {
     hipFree(o->d_seed);
     hipFree(o->d_nc);
     hipFree(o->d_member);
+    hipFree(o->d_dup);
     hipFree(o->d_map);
     hipFree(o->qfrag);
     hipFree(o->qrowh);
@@ -978,6 +1004,10 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     OrbitDsStat *d_ds = nullptr;
     TILER_HIP_CHECK(hipMalloc((void **)&o->d_member, G * 4 * sizeof(int)));
     TILER_HIP_CHECK(hipMemcpyAsync(o->d_member, member.data(), G * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
+    TILER_HIP_CHECK(hipMalloc((void **)&o->d_dup, G));
+    hipLaunchKernelGGL(orbit_dup_kernel, dim3((unsigned)std::min<long>(8192, (G + 3) / 4)), dim3(256), 0, stream,
+                       ix->d_rows, o->d_member, G, o->d_dup);
+    TILER_HIP_CHECK(hipGetLastError());
     TILER_HIP_CHECK(hipMalloc(&o->d_frag, (size_t)o->gblk * OS * 1024));
     TILER_HIP_CHECK(hipMalloc(&o->d_rowh, (size_t)G * OD * 2));
     TILER_HIP_CHECK(hipMalloc((void **)&o->d_seed, (size_t)o->gblk * 32 * sizeof(float)));
@@ -1086,6 +1116,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.qrowh = (const _Float16 *)o->qrowh;
     ra.nc = o->d_nc;
     ra.member = o->d_member;
+    ra.dup = o->d_dup;
     ra.ostat = o->qstat;
     ra.key = o->key;
     ra.id = o->id;

@@ -32,6 +32,7 @@ struct OrbitIndex {
     float *d_seed = nullptr;      // [gblk][32] -||c||^2/2 in accumulator-row order (-inf padding)
     float *d_nc = nullptr;        // [G] ||c||^2 (scaled, fp32)
     int *d_member = nullptr;      // [G][4] candidate index of relative mirror slot m (H = 1, V = 2), -1 absent
+    uint8_t *d_dup = nullptr;     // [G] bit m: slot m's row repeats a lower-index member's (symmetric tiles)
     void *d_map = nullptr;        // OrbitMap
     double N = 0, Np = 0, Hp = 0, Ecp = 0;  // max ||c||, ||c'||, ||fp16(c')||, ||c' - fp16(c')||
     // per-call scratch

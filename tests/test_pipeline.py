@@ -135,3 +135,47 @@ def test_run_all_chain_bit_exact(gpu, oracle, quality):
         t = sm["tile"][f]
         attrs = (sm["pal"][f] << 2) | ((sm["vm"][f] ^ e.tvm[t]) << 1) | (sm["hm"][f] ^ e.thm[t])
         assert np.array_equal(items[live, 0], t[live]) and np.array_equal(items[live, 1], attrs[live])
+
+
+def _dist_worker(rank, world, port, out, quality):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import tiler_amd
+    from tiler_amd._lib import check
+    from tiler_amd.encoder import DistributedEncoder
+    check(tiler_amd.load().tiler_init(0), "tiler_init")  # every rank on the one GPU of the test box
+    v = synth.video(61, 320, 240, kf_frames=(3, 2, 3), n_palettes=8)
+    e = DistributedEncoder(v)
+    sm = e.run_all(700, quality, 0.2)
+    data = e.save_stream(320, 240, 24.0)
+    if rank == 0:
+        np.savez(out, palpix=e.palpix, tile=e.tile, pal=e.pal, hm=e.hm, vm=e.vm, sm_tile=sm["tile"],
+                 sm_smoothed=sm["smoothed"], gtm=np.frombuffer(data, np.uint8))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_run_all_chain_two_ranks_match_single_process(gpu, tmp_path):
+    """the chain with palette bins and keyframes sharded over 2 ranks (gloo, both ranks on
+    the test box's one GPU) ends in exactly the single-process state and .gtm bytes."""
+    import socket
+    import torch.multiprocessing as mp
+    from tiler_amd.encoder import Encoder
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "r.npz")
+    mp.spawn(_dist_worker, args=(2, port, out, FT_MEDIUM), nprocs=2, join=True)
+    got = np.load(out)
+    v = synth.video(61, 320, 240, kf_frames=(3, 2, 3), n_palettes=8)
+    e = Encoder(v)
+    sm = e.run_all(700, FT_MEDIUM, 0.2)
+    data = e.save_stream(320, 240, 24.0)
+    for k, a in (("palpix", e.palpix), ("tile", e.tile), ("pal", e.pal), ("hm", e.hm), ("vm", e.vm),
+                 ("sm_tile", sm["tile"]), ("sm_smoothed", sm["smoothed"])):
+        assert np.array_equal(got[k], a), k
+    assert got["gtm"].tobytes() == data

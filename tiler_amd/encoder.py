@@ -158,3 +158,84 @@ class Encoder:
         self.do_frame_tiling(quality)
         self.do_reindex()
         return self.do_smooth(strength)
+
+
+class DistributedEncoder(Encoder):
+    """The same chain with one process per GPU (tiler_amd.dist): palette bins (K-Modes) and
+    keyframes (FrameTiling, Smooth) are planned longest-first across the ranks, each rank computes its
+    units on its own GPU and the per-unit results are all-gathered, so every rank holds the single-process
+    state after each step (the host bookkeeping is deterministic and repeated on every rank).  Call inside
+    an initialised torch.distributed process group."""
+
+    def do_global_tiling(self, desired: int, restart: int = gt.CRANDOM_KMODES_COUNT):
+        from . import dist as tdist
+        plan = gt.plan_global_tiling(self.palpix, self.dith_pal, self.n_palettes, desired, self.palsize, restart,
+                                     self.active)
+        import torch.distributed as dist
+        run = plan.run
+        costs = [plan.bins[p].size * max(1, int(plan.k_per_bin[p])) for p in run]
+        mine = [run[u] for u in tdist.lpt_assign(costs, dist.get_world_size())[dist.get_rank()]]
+        local = gt.kmodes_bins(plan, mine, self.palsize)  # this rank's bins in one GPU batch
+        gathered: list = [None] * dist.get_world_size()
+        dist.all_gather_object(gathered, local)
+        res = {}
+        for g in gathered:
+            res.update(g)
+        assert sorted(res) == sorted(run)
+        pp, act, uc, mi = gt.apply_kmodes_merges(plan, res, self.palpix, self.active, self.use_count)
+        self.palpix, self.active, self.use_count = pp, act, uc
+        self.finish_merge_tiles(mi)
+        self.make_tiles_unique()
+        self.reindex_tiles()
+        return plan.k_per_bin
+
+    def do_frame_tiling(self, quality: int = ft.FT_MEDIUM, use_wavelets: bool = True, gamma: int = -1):
+        from . import dist as tdist
+        gds = ft.prepare_global_ft(self.palpix, self.active)
+        Q = self.tiles_per_frame
+
+        def one(k):
+            f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
+            kt = ft.prepare_frame_tiling(self.palpix, self.thm, self.tvm, self.palettes[k], gds,
+                                         self.pal[f0:f1].ravel(), self.tile[f0:f1].ravel(), quality,
+                                         self.centroids[k], use_wavelets, gamma)
+            try:
+                t, p, h, v, e = kt.do_frame_tiling(self.frame_rgb[f0:f1])
+            finally:
+                kt.finish_frame_tiling()
+            return {"tile": t, "pal": p, "hm": h, "vm": v, "err": e}
+
+        nkf = self.kf_start.size - 1
+        try:
+            res = tdist.run_sharded(nkf, [(int(self.kf_start[k + 1] - self.kf_start[k])) * Q for k in range(nkf)],
+                                    one)
+        finally:
+            gds.kdt.close()
+        errs = np.zeros(self.tile.shape, np.float32)
+        for k, r in res.items():
+            f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
+            n = (f1 - f0, Q)
+            self.tile[f0:f1], self.pal[f0:f1] = r["tile"].reshape(n), r["pal"].reshape(n)
+            self.hm[f0:f1], self.vm[f0:f1], errs[f0:f1] = r["hm"].reshape(n), r["vm"].reshape(n), r["err"].reshape(n)
+        return errs
+
+    def do_smooth(self, strength: float = DEFAULT_STRENGTH):
+        from . import dist as tdist
+        nkf = self.kf_start.size - 1
+
+        def one(k):
+            f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
+            z = np.zeros((f1 - f0, self.tiles_per_frame), np.uint8)
+            t, p, h, v, s, _ = smooth_keyframe(self.tile[f0:f1], self.pal[f0:f1], self.hm[f0:f1], self.vm[f0:f1], z,
+                                               self.palpix, self.palettes[k], strength)
+            return {"tile": t, "pal": p, "hm": h, "vm": v, "smoothed": s}
+
+        res = tdist.run_sharded(nkf, [int(self.kf_start[k + 1] - self.kf_start[k]) for k in range(nkf)], one)
+        sm = {"tile": self.tile.copy(), "pal": self.pal.copy(), "hm": self.hm.copy(), "vm": self.vm.copy(),
+              "smoothed": np.zeros(self.tile.shape, np.uint8)}
+        for k, r in res.items():
+            f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
+            for key in sm:
+                sm[key][f0:f1] = r[key]
+        self.sm = sm
+        return sm

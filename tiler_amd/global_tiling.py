@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+from dataclasses import dataclass
 
 import numpy as np
 
@@ -62,16 +63,23 @@ def merge_tiles(idx, best, palpix, active, use_count, merge_index):
         palpix[j] = 0
 
 
-def do_global_tiling(palpix, dith_pal, n_palettes: int, desired: int, palsize: int = 16,
-                     restart: int = CRANDOM_KMODES_COUNT, active=None, use_count=None):
-    """Returns (palpix, active, use_count, merge_index, k_per_bin) after the K-Modes merge pass
-    (the caller applies merge_index to tilemaps: FinishMergeTiles main.pas:3722-3734)."""
-    palpix = np.array(palpix, np.uint8, copy=True).reshape(-1, 64)
+@dataclass
+class GTPlan:
+    """DoGlobalTiling's binning (main.pas:4272-4331): the K-Modes rows, the active tiles of each palette bin,
+    their StartingPoint and ClusterCount, and the bins that go through K-Modes (`run`)."""
+    lines: np.ndarray
+    bins: list
+    starts: list
+    k_per_bin: np.ndarray
+    run: list
+
+
+def plan_global_tiling(palpix, dith_pal, n_palettes: int, desired: int, palsize: int = 16,
+                       restart: int = CRANDOM_KMODES_COUNT, active=None) -> GTPlan:
+    palpix = np.asarray(palpix, np.uint8).reshape(-1, 64)
     T = palpix.shape[0]
-    active = np.ones(T, np.uint8) if active is None else np.array(active, np.uint8, copy=True)
-    use_count = np.ones(T, np.int64) if use_count is None else np.array(use_count, np.int64, copy=True)
+    active = np.ones(T, np.uint8) if active is None else np.asarray(active, np.uint8)
     dith_pal = np.asarray(dith_pal, np.int64)
-    merge_index = np.full(T, -1, np.int64)
     lines = write_tile_dataset_line(palpix, palsize)
     act = np.nonzero(active)[0]
     bins = [act[dith_pal[act] == p] for p in range(n_palettes)]
@@ -89,35 +97,58 @@ def do_global_tiling(palpix, dith_pal, n_palettes: int, desired: int, palsize: i
     run = []  # bins that go through K-Modes (DoKModes, main.pas:4195-4254)
     for p, b in enumerate(bins):
         kc = math.ceil(equal_quality_tile_count(b.size) * share)
-        k = int(round(kc))
-        k_per_bin[p] = k
+        k_per_bin[p] = int(round(kc))
         if b.size > kc:
             run.append(p)
-    if run:
-        X = np.ascontiguousarray(np.concatenate([lines[bins[p]] for p in run]))
-        off = np.zeros(len(run) + 1, np.int32)
-        off[1:] = np.cumsum([bins[p].size for p in run])
-        ks = np.array([k_per_bin[p] for p in run], np.int32)
-        st = np.array([starts[p] for p in run], np.int32)
-        labels, cent, _, _ = compute_kmodes_batch(X, off, ks, st, palsize)
-        medoid, counts = medoids_batch(X, off, ks, labels, cent)
-        koff = np.concatenate([[0], np.cumsum(ks)])
-        # MergeTiles for every cluster with >= 2 members (main.pas:4231-4253), vectorised: bins own disjoint
-        # tiles, so the per-cluster order of the reference does not change the result
-        tile_of = np.concatenate([bins[p] for p in run])
-        gl = np.repeat(koff[:-1], np.diff(off)) + labels          # global cluster of every row
-        med_tile = np.full(int(koff[-1]), -1, np.int64)
-        ok = counts >= 2
-        bin_of_cluster = np.repeat(np.arange(len(run)), ks)
-        med_tile[ok] = tile_of[off[bin_of_cluster[ok]] + medoid[ok]]
-        best = med_tile[gl]
+    return GTPlan(lines, bins, starts, k_per_bin, run)
+
+
+def kmodes_bins(plan: GTPlan, subset, palsize: int = 16) -> dict:
+    """K-Modes + medoids of the listed bins in ONE GPU batch: {bin: (labels, medoid, counts)}, bin-local."""
+    subset = list(subset)
+    if not subset:
+        return {}
+    X = np.ascontiguousarray(np.concatenate([plan.lines[plan.bins[p]] for p in subset]))
+    off = np.zeros(len(subset) + 1, np.int32)
+    off[1:] = np.cumsum([plan.bins[p].size for p in subset])
+    ks = np.array([plan.k_per_bin[p] for p in subset], np.int32)
+    st = np.array([plan.starts[p] for p in subset], np.int32)
+    labels, cent, _, _ = compute_kmodes_batch(X, off, ks, st, palsize)
+    medoid, counts = medoids_batch(X, off, ks, labels, cent)
+    koff = np.concatenate([[0], np.cumsum(ks)])
+    return {p: (labels[off[i]:off[i + 1]], medoid[koff[i]:koff[i + 1]], counts[koff[i]:koff[i + 1]])
+            for i, p in enumerate(subset)}
+
+
+def apply_kmodes_merges(plan: GTPlan, results: dict, palpix, active, use_count):
+    """MergeTiles for every cluster with >= 2 members (main.pas:4231-4253) of every K-Modes bin.  Bins own
+    disjoint tiles, so the order of the reference's per-cluster loop does not change the result."""
+    palpix = np.array(palpix, np.uint8, copy=True).reshape(-1, 64)
+    T = palpix.shape[0]
+    active = np.ones(T, np.uint8) if active is None else np.array(active, np.uint8, copy=True)
+    use_count = np.ones(T, np.int64) if use_count is None else np.array(use_count, np.int64, copy=True)
+    merge_index = np.full(T, -1, np.int64)
+    if plan.run:
+        tile_of = np.concatenate([plan.bins[p] for p in plan.run])
+        best = np.concatenate([np.where(results[p][2] >= 2, plan.bins[p][np.maximum(results[p][1], 0)], -1)
+                               [results[p][0]] for p in plan.run])
         sel = (best >= 0) & (tile_of != best)
         src, dst = tile_of[sel], best[sel]
         np.add.at(use_count, dst, use_count[src])
         active[src] = 0
         merge_index[src] = dst
         palpix[src] = 0
-    return palpix, active, use_count, merge_index, k_per_bin
+    return palpix, active, use_count, merge_index
+
+
+def do_global_tiling(palpix, dith_pal, n_palettes: int, desired: int, palsize: int = 16,
+                     restart: int = CRANDOM_KMODES_COUNT, active=None, use_count=None):
+    """Returns (palpix, active, use_count, merge_index, k_per_bin) after the K-Modes merge pass
+    (the caller applies merge_index to tilemaps: FinishMergeTiles main.pas:3722-3734)."""
+    plan = plan_global_tiling(palpix, dith_pal, n_palettes, desired, palsize, restart, active)
+    res = kmodes_bins(plan, plan.run, palsize)
+    pp, act, uc, mi = apply_kmodes_merges(plan, res, palpix, active, use_count)
+    return pp, act, uc, mi, plan.k_per_bin
 
 
 def make_tiles_unique(palpix, active, use_count):

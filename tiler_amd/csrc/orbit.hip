@@ -528,6 +528,240 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_kernel(const ha
 }
 
 // ------------------------------------------------------------------------------------------
+// device: the orbit shortlist, software-pipelined (default).  Same contraction, bound and lists as
+// nn_orbit_shortlist_kernel, but no block ends in a VALU-only tail: the bound adds of block b run beside
+// its own x2/x3 MFMAs, and its last |d_3| adds, sub-block maxima and list test run beside block b+1's
+// x0/x1 MFMAs.  Accumulator roles alternate between even and odd blocks so that nothing extra is live:
+//     x0 -> P (seeded), x1 -> RB, x2 -> T2, x3 -> RB,   P = RA, T2 = RC on even blocks, swapped on odd,
+// i.e. the previous block's P is this block's T2 (written only after the previous tail has read it).
+// A list insertion for block b happens right after block b+1's front half (the branch is wave-uniform).
+// ------------------------------------------------------------------------------------------
+template <int L, int CB, int NW, int QB>
+__global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(const half8 *__restrict__ cfrag,
+                                                                         const float *__restrict__ cseed, int nblk,
+                                                                         const half8 *__restrict__ qfrag, int nq,
+                                                                         int blk_per_split, int nsplit,
+                                                                         float *__restrict__ out_key,
+                                                                         int *__restrict__ out_id) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int FRAG_BYTES = CB * OS * 1024;
+    constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
+    constexpr int NT = NW * 64;
+    constexpr int PER_T = CB * OS * 64 / NT;
+    static_assert((CB * OS * 64) % NT == 0, "stage must split evenly over the workgroup");
+    static_assert(CB % 2 == 0, "accumulator roles alternate over pairs of blocks");
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int nqblk = (nq + 31) / 32;
+    const int qb0 = (blockIdx.x * NW + w) * QB;
+    const int split = blockIdx.y;
+    const int b_begin = split * blk_per_split;
+    const int b_end = min(nblk, b_begin + blk_per_split);
+
+    half8 bq[QB][OS];
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+        const long qa = min(qb0 + q, nqblk - 1);  // past the end: clamped duplicate, never written
+#pragma unroll
+        for (int s = 0; s < OS; s++) bq[q][s] = qfrag[(qa * OS + s) * 64 + lane];
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) before the hidden DMA starts counting
+    float lk[QB][L], th[QB];
+    int li[QB][L];
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+        th[q] = -INFINITY;  // = -lk[L-1] / 2: a sub-block enters the lane list when its bound exceeds th
+#pragma unroll
+        for (int i = 0; i < L; i++) {
+            lk[q][i] = INFINITY;
+            li[q][i] = -1;
+        }
+    }
+
+    const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
+    auto issue = [&](int st, int buf) {
+        const int blk0 = b_begin + st * CB;
+        const int nb = min(CB, b_end - blk0);
+        const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * OS * 64 + w * 64 + lane;
+        char *dst = smem + buf * BUF_BYTES + w * 1024;
+        if (nb == CB) {
+#pragma unroll
+            for (int j = 0; j < PER_T; j++) glds16_asm(src + j * NT, dst + j * NT * 16);
+        } else {
+            const int last = nb * OS * 64 - 1 - (w * 64 + lane);
+#pragma unroll
+            for (int j = 0; j < PER_T; j++) glds16_asm(src + min(j * NT, last), dst + j * NT * 16);
+        }
+        if (w == 0 && lane < CB * 8)
+            glds16_asm(reinterpret_cast<const uint4 *>(cseed) + (long)blk0 * 8 + min(lane, nb * 8 - 1),
+                       smem + buf * BUF_BYTES + FRAG_BYTES);
+    };
+
+    // list insertion of one finished block: every sub-block above the lane's current L-th entry, best first
+    auto insert_block = [&](int q, float (&m4)[4], int blk) __attribute__((always_inline)) {
+#pragma unroll
+        for (int it = 0; it < 4; it++) {
+            float best = m4[0];
+            int bs = 0;
+#pragma unroll
+            for (int sb = 1; sb < 4; sb++)
+                if (m4[sb] > best) {
+                    best = m4[sb];
+                    bs = sb;
+                }
+            const bool ins = best > th[q];
+            if (!__any(ins)) break;
+            if (ins) {
+                list_insert<L>(lk[q], li[q], -2.0f * best, blk * 4 + bs);
+#pragma unroll
+                for (int sb = 0; sb < 4; sb++)
+                    if (sb == bs) m4[sb] = -INFINITY;
+            }
+        }
+        th[q] = -0.5f * lk[q][L - 1];
+    };
+    // sub-block maxima of a finished bound accumulator; returns the lane's max
+    auto maxima = [&](const floatx16 &P, float (&m4)[4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int sb = 0; sb < 4; sb++) m4[sb] = fmaxf(fmaxf(P[4 * sb], P[4 * sb + 1]), fmaxf(P[4 * sb + 2], P[4 * sb + 3]));
+        return fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+    };
+
+    if (nstage > 0) issue(0, 0);
+    dma_drain();
+    __syncthreads();
+    const floatx16 zero = {0};
+    floatx16 RA[QB], RB[QB], RC[QB];
+#pragma unroll
+    for (int q = 0; q < QB; q++) RA[q] = RB[q] = RC[q] = zero;
+    int pend = -1;          // the block whose tail is pending (-1: none / not a real block)
+    half8 a0, a1;           // A fragments of the next k-step pair
+    float4 sd0, sd1, sd2, sd3;  // seeds of the next block
+
+    // one block: roles P (x0, seeded), T2 (x2); RB takes x1 and x3.  On entry T2 holds the previous
+    // block's bound (minus its |d_3|, which is in RB).
+    auto body = [&](const half8 *A, const float4 *SD, int cb, int blk, floatx16 (&P)[QB], floatx16 (&T2)[QB])
+        __attribute__((always_inline)) {
+        const floatx16 seed = {sd0.x, sd0.y, sd0.z, sd0.w, sd1.x, sd1.y, sd1.z, sd1.w,
+                               sd2.x, sd2.y, sd2.z, sd2.w, sd3.x, sd3.y, sd3.z, sd3.w};
+        float pmx[QB];
+#pragma unroll
+        for (int s = 0; s < OS; s += 2) {
+            half8 n0, n1;
+            const bool more = s + 2 < OS || cb + 1 < CB;
+            if (s + 2 < OS) {
+                n0 = A[(cb * OS + s + 2) * 64];
+                n1 = A[(cb * OS + s + 3) * 64];
+            } else if (cb + 1 < CB) {  // next block of this stage: first pair and seeds
+                n0 = A[((cb + 1) * OS) * 64];
+                n1 = A[((cb + 1) * OS + 1) * 64];
+                sd0 = SD[(cb + 1) * 8 + 0];
+                sd1 = SD[(cb + 1) * 8 + 1];
+                sd2 = SD[(cb + 1) * 8 + 2];
+                sd3 = SD[(cb + 1) * 8 + 3];
+            }
+#pragma unroll
+            for (int hh = 0; hh < 2; hh++) {
+                const int ss = s + hh;
+                const half8 av = hh ? a1 : a0;
+#pragma unroll
+                for (int q = 0; q < QB; q++) {
+                    if (ss < 3)
+                        P[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[q][ss], ss == 0 ? seed : P[q], 0, 0, 0);
+                    else if (ss < 6 || ss >= 9)
+                        RB[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[q][ss], ss % 3 == 0 ? zero : RB[q], 0, 0, 0);
+                    else
+                        T2[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[q][ss], ss == 6 ? zero : T2[q], 0, 0, 0);
+                }
+                // the VALU beside these MFMAs, about 10 per step (each group is issued before the MFMA that
+                // overwrites its input); element t of a group = accumulator element t % 16 of query block t / 16
+                auto acc_abs = [&](floatx16 (&D)[QB], const floatx16 (&S)[QB], int lo, int hi) __attribute__((always_inline)) {
+#pragma unroll
+                    for (int t = 0; t < 16 * QB; t++)
+                        if (t >= lo && t < hi) D[t / 16][t % 16] = D[t / 16][t % 16] + fabsf(S[t / 16][t % 16]);
+                };
+                constexpr int N3 = 16 * QB, C1 = (N3 + 2) / 3, C2 = (2 * N3 + 2) / 3;
+                if (ss <= 2)  // previous block: + |d_3| (RB) -- before step 3's MFMA writes RB
+                    acc_abs(T2, RB, ss == 0 ? 0 : ss == 1 ? C1 : C2, ss == 0 ? C1 : ss == 1 ? C2 : N3);
+                if (ss >= 3 && ss - 3 < QB) {  // previous block: its max for the list test, one query block per step
+                    const int q = ss - 3;
+                    float m4[4];
+                    pmx[q] = maxima(T2[q], m4);
+                    // materialise here: otherwise the whole tail sinks into the (rare) insertion branch
+                    // and the previous |d_3| (RB) stays live across this block's x1 MFMAs
+                    asm volatile("" ::"v"(pmx[q]));
+                }
+                if (ss >= 6 && ss <= 8)  // this block: + |d_1| (RB, complete after step 5) -- before step 9
+                    acc_abs(P, RB, ss == 6 ? 0 : ss == 7 ? C1 : C2, ss == 6 ? C1 : ss == 7 ? C2 : N3);
+                if (ss >= 10)  // this block: + |d_2| (T2, complete after step 8)
+                    acc_abs(P, T2, ss == 10 ? 0 : N3 / 2, ss == 10 ? N3 / 2 : N3);
+                // program order is the schedule: nothing moves across a step (keeps each accumulator's
+                // live range as written, so the role swap needs no extra registers)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (more) {
+                a0 = n0;
+                a1 = n1;
+            }
+            if (s == 4) {
+                // the previous block's list update (wave-uniform branch), then the back half
+#pragma unroll
+                for (int q = 0; q < QB; q++)
+                    if (__builtin_expect(pend >= 0 && __any(pmx[q] > th[q]), 0)) {
+                        float m4[4];
+                        maxima(T2[q], m4);  // T2 still holds the previous block's bound until step 6
+                        insert_block(q, m4, pend);
+                    }
+            }
+        }
+        pend = blk < b_end ? blk : -1;
+    };
+
+    for (int st = 0; st < nstage; st++) {
+        const char *B = smem + (st & 1) * BUF_BYTES;
+        const half8 *A = reinterpret_cast<const half8 *>(B) + lane;
+        const float4 *SD = reinterpret_cast<const float4 *>(B + FRAG_BYTES) + h * 4;
+        a0 = A[0];
+        a1 = A[64];
+        sd0 = SD[0];
+        sd1 = SD[1];
+        sd2 = SD[2];
+        sd3 = SD[3];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
+#pragma unroll
+        for (int cb = 0; cb < CB; cb += 2) {
+            body(A, SD, cb, b_begin + st * CB + cb, RA, RC);
+            body(A, SD, cb + 1, b_begin + st * CB + cb + 1, RC, RA);
+        }
+        dma_drain();
+        __syncthreads();
+    }
+    // the last block's tail (odd position: P = RC)
+    if (pend >= 0) {
+#pragma unroll
+        for (int q = 0; q < QB; q++) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) RC[q][r] = RC[q][r] + fabsf(RB[q][r]);
+            float m4[4];
+            const float mx = maxima(RC[q], m4);
+            if (__any(mx > th[q])) insert_block(q, m4, pend);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+        const int qq = (qb0 + q) * 32 + (lane & 31);
+        if (qb0 + q < nqblk && qq < nq) {
+            const long o = (((long)qq * nsplit + split) * 2 + h) * L;
+#pragma unroll
+            for (int i = 0; i < L; i++) {
+                out_key[o + i] = lk[q][i];
+                out_id[o + i] = li[q][i];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // device: orbit rescore, one wave per query
 // ------------------------------------------------------------------------------------------
 struct OrbitRescoreArgs {
@@ -1048,6 +1282,15 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         const char *e = getenv("TILER_ORBIT_NW");  // experiment: 12 waves x 1 query block (3 waves/SIMD)
         return (e && atoi(e) == 12) ? 12 : ORB_NW;
     }();
+    static const int mode = [] {
+        const char *e = getenv("TILER_ORBIT_MODE");  // 2, 3: timing experiments (results invalid)
+        return e ? atoi(e) : 0;
+    }();
+    static const int pipe = [] {
+        const char *e = getenv("TILER_ORBIT_PIPE");  // 0: the block-serial shortlist kernel
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    const bool use_pipe = pipe && qb == 2 && mode == 0 && nw == ORB_NW;
     const int wgs = (nqblk + nw * qb - 1) / (nw * qb);
     const int max_split = 32 / (2 * ORB_L);  // rescore: one list entry per lane of a half-wave
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
@@ -1086,17 +1329,17 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     }
     TILER_HIP_CHECK(hipGetLastError());
     {
-        const size_t lds = 2 * (ORB_CB * OS * 1024 + ORB_CB * 128);
+        const size_t lds = 2 * ((size_t)ORB_CB * OS * 1024 + ORB_CB * 128);
         KTimer tm("nn_orbit", stream);
-        static const int mode = [] {
-            const char *e = getenv("TILER_ORBIT_MODE");  // 2, 3: timing experiments (results invalid)
-            return e ? atoi(e) : 0;
-        }();
 #define ORB_LAUNCH(NWV, QB, MD)                                                                                   \
     hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, NWV, QB, MD>), dim3(wgs, nsplit),                  \
                        dim3(NWV * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
                        (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id)
-        if (qb == 1 && nw == 12)
+        if (use_pipe)
+            hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2>), dim3(wgs, nsplit),
+                               dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,
+                               (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id);
+        else if (qb == 1 && nw == 12)
             ORB_LAUNCH(12, 1, 0);
         else if (qb == 1)
             ORB_LAUNCH(8, 1, 0);

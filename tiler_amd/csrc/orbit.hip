@@ -536,7 +536,7 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_kernel(const ha
 // i.e. the previous block's P is this block's T2 (written only after the previous tail has read it).
 // A list insertion for block b happens right after block b+1's front half (the branch is wave-uniform).
 // ------------------------------------------------------------------------------------------
-template <int L, int CB, int NW, int QB>
+template <int L, int CB, int NW, int QB, int MODE>
 __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(const half8 *__restrict__ cfrag,
                                                                          const float *__restrict__ cseed, int nblk,
                                                                          const half8 *__restrict__ qfrag, int nq,
@@ -680,9 +680,10 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                         if (t >= lo && t < hi) D[t / 16][t % 16] = D[t / 16][t % 16] + fabsf(S[t / 16][t % 16]);
                 };
                 constexpr int N3 = 16 * QB, C1 = (N3 + 2) / 3, C2 = (2 * N3 + 2) / 3;
-                if (ss <= 2)  // previous block: + |d_3| (RB) -- before step 3's MFMA writes RB
+                if (MODE == 2) {  // timing experiment: MFMA + loads only (results invalid)
+                } else if (ss <= 2)  // previous block: + |d_3| (RB) -- before step 3's MFMA writes RB
                     acc_abs(T2, RB, ss == 0 ? 0 : ss == 1 ? C1 : C2, ss == 0 ? C1 : ss == 1 ? C2 : N3);
-                if (ss >= 3 && ss - 3 < QB) {  // previous block: its max for the list test, one query block per step
+                if (MODE != 2 && ss >= 3 && ss - 3 < QB) {  // previous block: its max for the list test, one query block per step
                     const int q = ss - 3;
                     float m4[4];
                     pmx[q] = maxima(T2[q], m4);
@@ -690,9 +691,9 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                     // and the previous |d_3| (RB) stays live across this block's x1 MFMAs
                     asm volatile("" ::"v"(pmx[q]));
                 }
-                if (ss >= 6 && ss <= 8)  // this block: + |d_1| (RB, complete after step 5) -- before step 9
+                if (MODE != 2 && ss >= 6 && ss <= 8)  // this block: + |d_1| (RB, complete after step 5) -- before step 9
                     acc_abs(P, RB, ss == 6 ? 0 : ss == 7 ? C1 : C2, ss == 6 ? C1 : ss == 7 ? C2 : N3);
-                if (ss >= 10)  // this block: + |d_2| (T2, complete after step 8)
+                if (MODE != 2 && ss >= 10)  // this block: + |d_2| (T2, complete after step 8)
                     acc_abs(P, T2, ss == 10 ? 0 : N3 / 2, ss == 10 ? N3 / 2 : N3);
                 // program order is the schedule: nothing moves across a step (keeps each accumulator's
                 // live range as written, so the role swap needs no extra registers)
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                 a0 = n0;
                 a1 = n1;
             }
-            if (s == 4) {
+            if (s == 4 && MODE == 0) {
                 // the previous block's list update (wave-uniform branch), then the back half
 #pragma unroll
                 for (int q = 0; q < QB; q++)
@@ -1290,6 +1291,10 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         const char *e = getenv("TILER_ORBIT_PIPE");  // 0: the block-serial shortlist kernel
         return (e && e[0] == '0') ? 0 : 1;
     }();
+    static const int pmode = [] {
+        const char *e = getenv("TILER_ORBIT_PMODE");  // pipelined kernel timing experiments (results invalid):
+        return e ? atoi(e) : 0;                        // 1 no list updates, 2 MFMA + loads only
+    }();
     const bool use_pipe = pipe && qb == 2 && mode == 0 && nw == ORB_NW;
     const int wgs = (nqblk + nw * qb - 1) / (nw * qb);
     const int max_split = 32 / (2 * ORB_L);  // rescore: one list entry per lane of a half-wave
@@ -1335,10 +1340,16 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, NWV, QB, MD>), dim3(wgs, nsplit),                  \
                        dim3(NWV * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
                        (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id)
-        if (use_pipe)
-            hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2>), dim3(wgs, nsplit),
-                               dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,
-                               (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id);
+#define ORB_PIPE(MD)                                                                                              \
+    hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, MD>), dim3(wgs, nsplit),              \
+                       dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
+                       (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id)
+        if (use_pipe && pmode == 1)
+            ORB_PIPE(1);
+        else if (use_pipe && pmode == 2)
+            ORB_PIPE(2);
+        else if (use_pipe)
+            ORB_PIPE(0);
         else if (qb == 1 && nw == 12)
             ORB_LAUNCH(12, 1, 0);
         else if (qb == 1)
@@ -1350,6 +1361,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         else
             ORB_LAUNCH(8, 2, 0);
 #undef ORB_LAUNCH
+#undef ORB_PIPE
     }
     TILER_HIP_CHECK(hipGetLastError());
     OrbitRescoreArgs ra;

@@ -31,7 +31,7 @@ SHORTLIST_KERNELS = {
     "q16l6": "nn_shortlist16_kernel<S=6,L=6,CB=8,NW=8,QB=4>",
     "w8": "nn_shortlist_kernel<S=12,L=8,CB=2,NW=8>",
 }
-ORBIT_KERNEL = "nn_orbit_shortlist_kernel<L=4,CB=4,NW=8>"
+ORBIT_KERNEL = "nn_orbit_shortlist_pipe_kernel<L=4,CB=4,NW=8,QB=2>"
 PEAK_HBM_GBS = 8000.0
 
 CONFIGS = {
@@ -182,7 +182,8 @@ def main():
     sec = sl["ms_avg"] * 1e-3 if sl["ms_avg"] else None
     achieved = flops_launch / sec / 1e12 if sec else None
     issued = issued_launch / sec / 1e12 if sec else None
-    kname = "nn_orbit_shortlist_kernel" if orbit else "nn_shortlist16_kernel"
+    kname = ("nn_orbit_shortlist_kernel" if os.environ.get("TILER_ORBIT_PIPE") == "0" else "nn_orbit_shortlist_pipe_kernel") \
+        if orbit else "nn_shortlist16_kernel"
     traffic, traffic_src = pmc_traffic(kname)
     roofline = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None, "peak": PEAK_F16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,

@@ -177,6 +177,10 @@ static bool build_map(OrbitMap &m) {
             }
             m.cs[oo] = no == 4 ? 0.5f : 1.0f;
             m.qs[oo] = no == 1 ? 1.0f : 0.5f;
+            // orbit_prep_kernel stages one colour component at a time: output o of block x must read only
+            // component (o % 48) / 16, i.e. k-step 3x + c holds component c
+            for (int t = 0; t < no; t++)
+                if (out_src[x][o][t] / 64 != o / 16) return false;
         }
     return true;
 }
@@ -243,69 +247,91 @@ struct OrbitPrepArgs {
     OrbitStat *qstat;      // queries only
 };
 
-// One wave per 32 rows: the rows (gathered through member[] for the dataset) and the transform table
-// are staged in LDS (row stride 193 floats: the 32 lanes of a half-wave read 32 rows conflict-free).
-static constexpr int ORB_RS = OD + 1;
+// Four waves per workgroup, one 32-row block per wave, one colour component at a time: the transform
+// never mixes components (S_m permutes within each 64-value component, build_map checks it), and
+// output k-step s = 3x + c holds component c's 16 outputs of isotypic block x.  So a wave stages only
+// its rows' 64 values of component c in LDS (stride 65 floats: the 32 lanes of a half-wave read 32
+// rows conflict-free), 8.3 KB per wave, and the 4 waves share the transform table: 16 waves per CU.
+static constexpr int ORB_CS = 65;
+static constexpr int ORB_PW = 4;  // waves (32-row blocks) per workgroup
 
-__global__ __launch_bounds__(64) void orbit_prep_kernel(OrbitPrepArgs a) {
-    __shared__ float srow[32 * ORB_RS];
+__global__ __launch_bounds__(64 * ORB_PW) void orbit_prep_kernel(OrbitPrepArgs a) {
+    __shared__ float srow[ORB_PW][32 * ORB_CS];
     __shared__ int16_t msrc[OD * 4];
     __shared__ float mw[OD * 4], mc[OD];
-    const int lane = threadIdx.x, h = lane >> 5;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const long nblk = (a.count + 31) / 32;
     const bool dataset = a.member != nullptr;
-    for (int i = lane; i < OD * 4; i += 64) {
+    for (int i = tid; i < OD * 4; i += 64 * ORB_PW) {
         msrc[i] = a.mp->src[i >> 2][i & 3];
         mw[i] = a.mp->w[i >> 2][i & 3];
     }
-    for (int i = lane; i < OD; i += 64) mc[i] = dataset ? a.mp->cs[i] : a.mp->qs[i];
-    for (long blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        __syncthreads();
-        for (int i = lane; i < 32 * (OD / 4); i += 64) {
-            const int rr = i / (OD / 4), c4 = i % (OD / 4);
-            const long r = blk * 32 + rr;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r < a.count) {
-                const long base = dataset ? (long)a.member[r * 4] : r;
-                v = reinterpret_cast<const float4 *>(a.rows + base * OD)[c4];
-            }
-            float *d = srow + rr * ORB_RS + c4 * 4;
-            d[0] = v.x;
-            d[1] = v.y;
-            d[2] = v.z;
-            d[3] = v.w;
-        }
-        __syncthreads();
+    for (int i = tid; i < OD; i += 64 * ORB_PW) mc[i] = dataset ? a.mp->cs[i] : a.mp->qs[i];
+    float *sw = srow[w];
+    for (long wb = blockIdx.x; wb * ORB_PW < nblk; wb += gridDim.x) {  // uniform trip count per workgroup
+        const long blk = wb * ORB_PW + w;
         const long r = blk * 32 + (lane & 31);
-        const bool valid = r < a.count;
-        const float *row = srow + (lane & 31) * ORB_RS;
+        const bool valid = blk < nblk && r < a.count;
+        // this lane's staging rows (8 float4 pieces: row rr = i / 16, piece i % 16 of the component)
+        long src_row[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int rr = (lane + 64 * t) >> 4;
+            const long rg = blk * 32 + rr;
+            src_row[t] = (blk < nblk && rg < a.count) ? (dataset ? (long)a.member[rg * 4] : rg) : -1;
+        }
+        const float *row = sw + (lane & 31) * ORB_CS;
         double n2 = 0, p2 = 0, h2 = 0, e2 = 0;
         int bad = 0;
-        for (int s = 0; s < OS; s++) {
-            half8 hv;
+#pragma unroll 1
+        for (int c = 0; c < 3; c++) {
+            __syncthreads();
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int k = s * 16 + 8 * h + j;
-                double v = 0.0;
-                if (valid) {
-                    const double orig = (double)row[k] * (double)a.scale;
-                    n2 += orig * orig;
-#pragma unroll
-                    for (int t = 0; t < 4; t++) v += (double)mw[k * 4 + t] * (double)row[msrc[k * 4 + t]];
-                    v *= (double)mc[k] * (double)a.scale;
-                }
-                _Float16 vh = (_Float16)(float)v;
-                if (fabs((double)(float)vh) < 6.103515625e-05) vh = (_Float16)0.0f;  // no fp16 subnormal operands
-                hv[j] = vh;
-                const double dh = (double)(float)vh;
-                p2 += v * v;
-                h2 += dh * dh;
-                e2 += (v - dh) * (v - dh);
-                if (!isfinite(v) || fabs(v) > 65000.0) bad = 1;
+            for (int t = 0; t < 8; t++) {
+                const int i = lane + 64 * t, rr = i >> 4, c4 = i & 15;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (src_row[t] >= 0) v = reinterpret_cast<const float4 *>(a.rows + src_row[t] * OD + c * 64)[c4];
+                float *d = sw + rr * ORB_CS + c4 * 4;
+                d[0] = v.x;
+                d[1] = v.y;
+                d[2] = v.z;
+                d[3] = v.w;
             }
-            a.frag[(blk * OS + s) * 64 + lane] = hv;
-            if (valid) *reinterpret_cast<half8 *>(a.rowh + r * OD + s * 16 + 8 * h) = hv;
+            __syncthreads();
+            if (valid) {  // |row|^2: this half-wave lane's 32 values of the component
+#pragma unroll 8
+                for (int i = 0; i < 32; i++) {
+                    const double orig = (double)row[32 * h + i] * (double)a.scale;
+                    n2 += orig * orig;
+                }
+            }
+#pragma unroll
+            for (int x = 0; x < 4; x++) {
+                const int s = 3 * x + c;
+                half8 hv;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int k = s * 16 + 8 * h + j;
+                    double v = 0.0;
+                    if (valid) {
+#pragma unroll
+                        for (int t = 0; t < 4; t++) v += (double)mw[k * 4 + t] * (double)row[(msrc[k * 4 + t] - 64 * c) & 63];  // unused terms: w = 0
+                        v *= (double)mc[k] * (double)a.scale;
+                    }
+                    _Float16 vh = (_Float16)(float)v;
+                    if (fabs((double)(float)vh) < 6.103515625e-05) vh = (_Float16)0.0f;  // no fp16 subnormal operands
+                    hv[j] = vh;
+                    const double dh = (double)(float)vh;
+                    p2 += v * v;
+                    h2 += dh * dh;
+                    e2 += (v - dh) * (v - dh);
+                    if (!isfinite(v) || fabs(v) > 65000.0) bad = 1;
+                }
+                if (blk < nblk) a.frag[(blk * OS + s) * 64 + lane] = hv;
+                if (valid) *reinterpret_cast<half8 *>(a.rowh + r * OD + s * 16 + 8 * h) = hv;
+            }
         }
+        if (blk >= nblk) continue;
         n2 += __shfl_xor(n2, 32, 64);
         p2 += __shfl_xor(p2, 32, 64);
         h2 += __shfl_xor(h2, 32, 64);
@@ -1251,8 +1277,8 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     TILER_HIP_CHECK(hipMemsetAsync(d_ds, 0, sizeof(OrbitDsStat), stream));
     OrbitPrepArgs pa{ix->d_rows, o->d_member, G, (const OrbitMap *)d_map, ix->scale, (half8 *)o->d_frag,
                      (_Float16 *)o->d_rowh, o->d_seed, o->d_nc, d_ds, nullptr};
-    hipLaunchKernelGGL(orbit_prep_kernel, dim3((unsigned)std::min<long>(8192, o->gblk)), dim3(64), 0,
-                       stream, pa);
+    hipLaunchKernelGGL(orbit_prep_kernel, dim3((unsigned)std::min<long>(4096, (o->gblk + ORB_PW - 1) / ORB_PW)),
+                       dim3(64 * ORB_PW), 0, stream, pa);
     TILER_HIP_CHECK(hipGetLastError());
     OrbitDsStat ds;
     TILER_HIP_CHECK(hipMemcpyAsync(&ds, d_ds, sizeof(ds), hipMemcpyDeviceToHost, stream));
@@ -1329,8 +1355,8 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         OrbitPrepArgs pa{d_q, nullptr, nq, (const OrbitMap *)o->d_map, ix->scale, (half8 *)o->qfrag,
                          (_Float16 *)o->qrowh, nullptr, nullptr, nullptr, o->qstat};
         KTimer tm("nn_prep", stream);
-        hipLaunchKernelGGL(orbit_prep_kernel, dim3((unsigned)std::min<long>(8192, nqblk)), dim3(64), 0,
-                           stream, pa);
+        hipLaunchKernelGGL(orbit_prep_kernel, dim3((unsigned)std::min<long>(4096, (nqblk + ORB_PW - 1) / ORB_PW)),
+                           dim3(64 * ORB_PW), 0, stream, pa);
     }
     TILER_HIP_CHECK(hipGetLastError());
     {

@@ -102,13 +102,15 @@ __device__ __forceinline__ double div10000(double x) {
 template <bool FASTDIV>
 __global__ __launch_bounds__(64) void psyv_rgb_haar_kernel(PsyvArgs a) {
     __shared__ double lut[256];
+    __shared__ float st[64 * 65];  // one component of the 64 tiles, transposed for coalesced row stores
     const int lane = threadIdx.x;
     const double *__restrict__ glut = a.gamma_lut + 256 * (a.gamma + 1);
     for (int i = lane; i < 256; i += 64) lut[i] = glut[i];
     __syncthreads();
-    const long i = (long)blockIdx.x * 64 + lane;
-    if (i >= a.n) return;
-    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + i * 64);
+    const long t0 = (long)blockIdx.x * 64;
+    const long i = t0 + lane;
+    const bool valid = i < a.n;
+    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + (valid ? i : t0) * 64);
 #pragma unroll 1
     for (int c = 0; c < 3; c++) {
         double p[64];
@@ -126,12 +128,22 @@ __global__ __launch_bounds__(64) void psyv_rgb_haar_kernel(PsyvArgs a) {
         }
         haar_regs(p, a.haar_f);
         if (a.out32) {
-            float4 *o = reinterpret_cast<float4 *>(a.out32 + i * 192 + c * 64);
+            // lane = tile: its 64 values into LDS (stride 65: conflict-free), then 16 lanes per tile store
+            // the tile's 256-byte component segment (64-byte lines written whole, not a line per lane)
+            __syncthreads();
 #pragma unroll
-            for (int k = 0; k < 16; k++)
-                o[k] = make_float4((float)p[4 * k], (float)p[4 * k + 1], (float)p[4 * k + 2], (float)p[4 * k + 3]);
+            for (int k = 0; k < 64; k++) st[lane * 65 + k] = (float)p[k];
+            __syncthreads();
+#pragma unroll
+            for (int t = 0; t < 16; t++) {
+                const int pc = lane + 64 * t, tt = pc >> 4, c4 = pc & 15;
+                if (t0 + tt < a.n) {
+                    const float *q = st + tt * 65 + c4 * 4;
+                    reinterpret_cast<float4 *>(a.out32 + (t0 + tt) * 192 + c * 64)[c4] = make_float4(q[0], q[1], q[2], q[3]);
+                }
+            }
         }
-        if (a.out64) {
+        if (a.out64 && valid) {
             double2 *o = reinterpret_cast<double2 *>(a.out64 + i * 192 + c * 64);
 #pragma unroll
             for (int k = 0; k < 32; k++) o[k] = make_double2(p[2 * k], p[2 * k + 1]);

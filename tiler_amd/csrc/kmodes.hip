@@ -608,7 +608,13 @@ struct KmAsgItem {
 
 __global__ __launch_bounds__(256) void kmb_assign(KmBatch B, const KmAsgItem *items) {
     __shared__ uint4 ct[128 * 5];
-    const KmAsgItem it = items[blockIdx.x];
+    KmAsgItem it = items[blockIdx.x];
+    {  // this workgroup's share of the item's centroids (gridDim.y sub-splits); ties across splits: atomicMin key
+        const int per = (it.c1 - it.c0 + (int)gridDim.y - 1) / (int)gridDim.y;
+        it.c0 += (int)blockIdx.y * per;
+        it.c1 = min(it.c1, it.c0 + per);
+        if (it.c0 >= it.c1) return;
+    }
     KmState s = bin_state(B, it.bin);
     const long i = it.p0 + threadIdx.x;
     const bool valid = i < it.p1;
@@ -725,6 +731,9 @@ __global__ __launch_bounds__(256) void kmb_medoid(const uint8_t *X, const int32_
 // centroid splits of an assignment block: ~64 centroids per block, so a chunk of the largest bin alone
 // still spreads over the chip (results merge by atomicMin)
 static int csplit_of(int K) { return std::max(1, std::min(128, (K + 63) / 64)); }
+// each host work item (<= 64 centroids) runs as KM_ASUB workgroups of a quarter of its centroids: the late
+// chunk steps hold one large bin alone, where one workgroup per item left ~1 wave per SIMD (latency-bound)
+static constexpr int KM_ASUB = 4;
 
 int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const int32_t *h_k, const int32_t *h_start,
                      int n_modalities, int32_t *d_labels, uint8_t *d_centroids, int32_t *h_iter, uint64_t *h_cost,
@@ -868,7 +877,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
             if (hipMemsetAsync(B.akey, 0xff, (size_t)N * 8, st) != hipSuccess) goto fail;
             if (upload(as.data(), as.size() * sizeof(KmAsgItem))) goto fail;
             KTimer tm("kmodes_assign", st);
-            hipLaunchKernelGGL(kmb_assign, dim3((unsigned)as.size()), dim3(256), 0, st, B, (const KmAsgItem *)items);
+            hipLaunchKernelGGL(kmb_assign, dim3((unsigned)as.size(), KM_ASUB), dim3(256), 0, st, B, (const KmAsgItem *)items);
         }
         if (hipMemsetAsync(B.csize, 0, (size_t)Ktot * 4, st) != hipSuccess ||
             hipMemsetAsync(B.freq, 0, (size_t)Ktot * KM_A * M * 4, st) != hipSuccess)
@@ -922,7 +931,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     for (const auto &sp : steps) {
                         {
                             KTimer tm("kmodes_assign", st);
-                            hipLaunchKernelGGL(kmb_assign, dim3(sp.first), dim3(256), 0, st, B,
+                            hipLaunchKernelGGL(kmb_assign, dim3(sp.first, KM_ASUB), dim3(256), 0, st, B,
                                                (const KmAsgItem *)items + pos);
                         }
                         pos += sp.first;

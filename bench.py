@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, visible cores)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-smooth", action="store_true")
+    ap.add_argument("--no-keyframes", action="store_true")
+    ap.add_argument("--clip-frames", type=int, default=1000, help="keyframe-detection clip length (C3: 1000)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI, the product); gloo only to rehearse the N>1 control flow")
     args = ap.parse_args()
@@ -216,6 +218,39 @@ def main():
         smooth = {"value": round((F - 1) * Q / ts / 1e6, 4), "unit": "Msteps/s", "ms": round(ts * 1e3, 3),
                   "smoothed": int(s_sm.sum().item()), "shape": f"{F} frames x {Q} positions, Strength 0.02"}
 
+    # ---- secondary: the Load step's keyframe detection over a whole clip (main.pas:1099-1146) ----
+    keyframes = None
+    if rank == 0 and not args.no_keyframes:
+        from tiler_amd.keyframes import find_keyframes
+        tw, th, FC = W // 8, H // 8, args.clip_frames
+        g = torch.Generator(device=dev)
+        g.manual_seed(args.seed)
+        clip = torch.randint(0, 1 << 24, (FC, Q * 64), dtype=torch.int32, device=dev, generator=g)
+        corr = np.zeros(FC - 1, np.float64)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        check(lib.tiler_interframe_correlation_dev(vp(clip.data_ptr()), FC, tw, th, corr.ctypes.data_as(vp),
+                                                   vp(stream)), "tiler_interframe_correlation_dev")
+        _, n_kf = find_keyframes(corr, FC, Q)
+        tk = time.perf_counter() - t0
+        keyframes = {"value": round((FC - 1) / tk, 2), "unit": "frame pairs/s", "ms": round(tk * 1e3, 3),
+                     "keyframes": int(n_kf), "shape": f"{FC} frames {W}x{H} (random bytes, generated in HBM), "
+                                                      f"Pearson over 3*{W * H} bytes per pair",
+                     "bound": "sequential fp64 chain per frame (the reference's summation order), one lane per frame"}
+        if world == 1 and not args.no_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle
+            ns = min(8, FC - 1)
+            sample = clip[:ns + 1].cpu().numpy()
+            t0 = time.perf_counter()
+            ocorr = pyoracle.interframe_corr_batch(sample, tw, th)
+            tc = time.perf_counter() - t0
+            keyframes["cpu_baseline"] = {"value": round(ns / tc, 2), "unit": "frame pairs/s", "cores": 1,
+                                         "kind": "port", "sample": f"the clip's first {ns} pairs (oracle/load_kf.c; "
+                                                                   "the reference runs this loop on one thread)"}
+            keyframes["parity_mismatches_vs_cpu"] = int(np.sum(ocorr.view(np.uint64) != corr[:ns].view(np.uint64)))
+        del clip
+
     # ---- CPU baseline (rank 0, N=1): the oracle restatement, bounded sample, same workload ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -231,7 +266,7 @@ def main():
                        "tiles_per_step_per_gpu": QK, "candidates": M, "descriptor": "PsyV Haar 192-d",
                        "parallelism": f"keyframes sharded, {world} GPU(s)"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "search_stats": stats,
-            "secondary": {"smooth": smooth},
+            "secondary": {"smooth": smooth, "keyframes": keyframes},
         }
         print(json.dumps(res))
     kdt.close()

@@ -142,6 +142,19 @@ int tiler_kmodes_batch_dev(const uint8_t *d_X, const int32_t *bin_off, int nbins
 int tiler_kmodes_medoids_batch(const uint8_t *X, const int32_t *bin_off, int nbins, const int32_t *k,
                                const int32_t *labels, const uint8_t *centroids, int32_t *medoid, int32_t *counts);
 
+/* ---- Load-step keyframe detection (btnLoadClick main.pas:1099-1146) ----------------
+ * frames[F][tm_h*tm_w][64] int32 0x00BBGGRR (TFrame.Tiles[].RGBPixels, tile-major, as FrameTiling takes
+ * them).  corr[F-1] (host): corr[i-1] = ComputeInterFrameCorrelation(frame i-1, frame i) (main.pas:811-828,
+ * PearsonCorrelation main.pas:1465-1492 over LoadFrame's FSPixels), bit-identical to the reference's
+ * sequential fp64 evaluation.  0 ok, -1 error.  No reference interface exists for this step (it is inline
+ * in btnLoadClick); these exports let the Pascal Load step hand its frames over instead. */
+int tiler_interframe_correlation(const int32_t *rgb, int F, int tm_w, int tm_h, double *corr);
+/* Same with the frames in HBM (16-byte aligned); corr is a host array; synchronous on stream. */
+int tiler_interframe_correlation_dev(const int32_t *d_rgb, int F, int tm_w, int tm_h, double *corr, void *stream);
+/* The shot-transition split (main.pas:1099-1132): kf_of_frame[F] = keyframe index of each frame.
+ * tile_map_size = FTileMapSize.  Returns the keyframe count, or -1. */
+int tiler_find_keyframes(const double *corr, int F, int tile_map_size, int32_t *kf_of_frame);
+
 /* ---- GTM keyframe stream compression (host code) ---------------------------------------------------
  * Replaces LZCompress (extern.pas:202-240: temp file + external `lzma.exe e src dst -lc8 -eos`, called
  * per keyframe by SaveStream main.pas:4734).  Writes an LZMA-alone stream (13-byte header: properties

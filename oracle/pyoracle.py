@@ -46,6 +46,7 @@ def lib():
         _o.or_set_gamma.argtypes = [ctypes.c_double, ctypes.c_double]
         _o.or_smooth.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 8 + [ctypes.c_double]
         _o.or_eqtc.argtypes = [ctypes.c_double]
+        _o.or_interframe_corr.restype = ctypes.c_double
         _o.or_init()
     return _o
 
@@ -267,6 +268,24 @@ def global_tiling(palpix, dith_pal, P, desired, palsize=16, restart=7, use_count
     lib().or_global_tiling(T, _p(palpix), _p(active), _p(uc), _p(mi), _p(np.ascontiguousarray(dith_pal, np.int32)), P,
                            palsize, desired, restart, _p(kpb))
     return palpix, active, uc, mi, kpb
+
+
+def interframe_corr_batch(frames, tm_w, tm_h):
+    """ComputeInterFrameCorrelation (main.pas:811-828) of every consecutive pair: corr[i-1] = corr(i-1, i)."""
+    frames = np.ascontiguousarray(frames, np.int32).reshape(-1, tm_w * tm_h * 64)
+    F = frames.shape[0]
+    corr = np.zeros(max(0, F - 1), np.float64)
+    if F > 1:
+        lib().or_interframe_corr_batch(_p(frames), F, tm_w, tm_h, _p(corr))
+    return corr
+
+
+def find_keyframes(corr, F, tile_map_size):
+    """btnLoadClick main.pas:1099-1146: keyframe index per frame and the keyframe count."""
+    corr = np.ascontiguousarray(corr, np.float64)
+    kf = np.zeros(F, np.int32)
+    n = lib().or_find_keyframes(_p(corr), F, tile_map_size, _p(kf))
+    return kf, n
 
 
 def ref_kmodes_lib():

@@ -91,6 +91,11 @@ int or_global_tiling(int T, uint8_t *palpix, uint8_t *active, int32_t *use_count
 void or_make_tiles_unique(int T, uint8_t *palpix, uint8_t *active, int32_t *use_count, int32_t *merge_index);
 int or_reindex(int T, const uint8_t *active, const int32_t *use_count, int32_t *idx_map);
 
+/* Load step keyframe detection (load_kf.c; main.pas:811-828, 1099-1146, 1465-1492) */
+double or_interframe_corr(const int32_t *a, const int32_t *b, int tm_w, int tm_h);
+void or_interframe_corr_batch(const int32_t *frames, int F, int tm_w, int tm_h, double *corr);
+int or_find_keyframes(const double *corr, int F, int tile_map_size, int32_t *kf_of_frame);
+
 #ifdef __cplusplus
 }
 #endif

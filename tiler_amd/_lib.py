@@ -74,6 +74,9 @@ _SIGS = {
                                            c_void_p]),
     "tiler_kmodes_compute": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
+    "tiler_interframe_correlation": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "tiler_interframe_correlation_dev": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "tiler_find_keyframes": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "tiler_lzma_encode": (c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_uint32, c_int, c_void_p, c_size_t,
                                   c_void_p]),
 }

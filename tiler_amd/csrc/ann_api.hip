@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/tiler_ann.h"
+#include "keyframes.hpp"
 #include "kmodes.hpp"
 #include "nn_search.hpp"
 #include "orbit.hpp"
@@ -534,6 +535,20 @@ int tiler_smooth_keyframe_dev(int F, int Q, int32_t *d_tile, int32_t *d_tmpidx, 
     if (!ensure_init()) return -1;
     return smooth_keyframe_dev(F, Q, d_tile, d_tmpidx, d_pal, d_hm, d_vm, d_smoothed, d_palpix, d_palettes, strength,
                                (hipStream_t)stream);
+}
+
+int tiler_interframe_correlation(const int32_t *rgb, int F, int tm_w, int tm_h, double *corr) {
+    if (!ensure_init()) return -1;
+    return interframe_corr_host(rgb, F, tm_w, tm_h, corr);
+}
+
+int tiler_interframe_correlation_dev(const int32_t *d_rgb, int F, int tm_w, int tm_h, double *corr, void *stream) {
+    if (!ensure_init()) return -1;
+    return interframe_corr_dev(d_rgb, F, tm_w, tm_h, corr, (hipStream_t)stream);
+}
+
+int tiler_find_keyframes(const double *corr, int F, int tile_map_size, int32_t *kf_of_frame) {
+    return find_keyframes(corr, F, tile_map_size, kf_of_frame);
 }
 
 int tiler_kmodes_medoids(const uint8_t *X, int n, const int32_t *labels, const uint8_t *centroids, int k,

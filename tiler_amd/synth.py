@@ -59,6 +59,34 @@ def keyframe_frames(rng: np.random.Generator, frames: int, tiles_per_frame: int,
     return out
 
 
+def screen_to_tiles(img: np.ndarray) -> np.ndarray:
+    """Screen [H][W][3] u8 (r, g, b) -> frame tiles [(H/8)*(W/8)][64] int32 0x00BBGGRR (LoadFrame main.pas:3245-3256)."""
+    H, W, _ = img.shape
+    t = img.reshape(H // 8, 8, W // 8, 8, 3).transpose(0, 2, 1, 3, 4).reshape(-1, 64, 3).astype(np.int32)
+    return rgb_pack(t[..., 0], t[..., 1], t[..., 2])
+
+
+def shot_frames(rng: np.random.Generator, frames: int, tm_w: int, tm_h: int, shot_len=(6, 40), noise: int = 6):
+    """Synthetic clip with shot transitions for the Load step's keyframe detection: each shot is a smooth
+    random picture that pans one pixel per frame under per-frame noise; a new shot starts after a random
+    length.  Returns (frames [F][Q][64] int32, first frame of every shot)."""
+    H, W = tm_h * 8, tm_w * 8
+    out = np.empty((frames, tm_w * tm_h, 64), np.int32)
+    starts = []
+    f = 0
+    while f < frames:
+        starts.append(f)
+        n = int(rng.integers(shot_len[0], shot_len[1] + 1))
+        lo = rng.integers(0, 256, ((H + n) // 16 + 2, (W + 2 * n) // 16 + 2, 3)).astype(np.float32)
+        base = np.repeat(np.repeat(lo, 16, 0), 16, 1)
+        for k in range(min(n, frames - f)):
+            img = base[k:k + H, 2 * k:2 * k + W]
+            img = img + rng.integers(-noise, noise + 1, img.shape)
+            out[f] = screen_to_tiles(np.clip(img, 0, 255).astype(np.uint8))
+            f += 1
+    return out, np.asarray(starts, np.int64)
+
+
 def palettes(rng: np.random.Generator, count: int, size: int = 16) -> np.ndarray:
     c = rng.integers(0, 256, (count, size, 3))
     return rgb_pack(c[..., 0], c[..., 1], c[..., 2])

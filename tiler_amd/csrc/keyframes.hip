@@ -11,11 +11,14 @@
 //   * mean(x) = Sum / N: the sum of bytes is an exact integer -> a parallel u64 reduction (frame_sum_kernel);
 //   * Σ (x - m_f)^2 of frame f is the SAME rounded sequence whether f is the "x" of pair (f, f+1) or the "y"
 //     of pair (f-1, f): it is computed once per frame (d2[f]);
-//   * one LANE per frame runs the ordered chains: d2[f] and num[f] = Σ (x_f - m_f)(x_{f+1} - m_{f+1}).
-// The chains are issue-bound fp64 work (6 fp64 VALU per screen byte per lane), not HBM-bound: one wave covers
-// 63 frame pairs, so a launch costs about one frame's worth of sequential steps whatever F is.
+//   * one LANE per frame runs the ordered chains d2[f] and num[f] = Σ (x_f - m_f)(x_{f+1} - m_{f+1}), the y term
+//     coming from the neighbour lane; in the default form three producer waves compute the rounded terms into
+//     LDS and one consumer wave only adds them in order (pearson_chain_pc_kernel).
+// The chains are issue-bound fp64 work, not HBM-bound: a workgroup covers 60 frame pairs, so a launch costs about
+// one frame's worth of sequential steps whatever F is.
 // sqrt / product / division (4 flops per pair) finish on the host in double, as written in main.pas:1485-1491.
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <string>
@@ -44,20 +47,32 @@ __global__ __launch_bounds__(256) void frame_sum_kernel(const int4 *__restrict__
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(&sums[f], acc);
 }
 
-// One lane per frame: lane L of workgroup b holds frame f = 63b + L and runs, in the reference's order
+// One lane per frame (60 per wave, see below) runs, in the reference's order
 // (channel-major, then screen raster: ya[i + sz*c] := FSPixels[i*3 + c], main.pas:819-826), the chains
 // d2[f] = Σ (x_f - m_f)^2 and num[f] = Σ (x_f - m_f)(x_{f+1} - m_{f+1}); every op rounded (-ffp-contract=off).
-// The y term of a pair is the NEXT lane's x term (same element, frame f+1), handed over by a lane shuffle, so
-// each lane streams one frame and each element costs one convert, one subtract, two multiplies and two adds.
-// Lane 63 only feeds lane 62 (its frame is owned by lane 0 of the next workgroup).  With one wave per SIMD
+// The y term of a pair is the NEXT lane's x term (same element, frame f+1), handed over by a DPP row shift
+// (2 v_mov_dpp; a ds_bpermute shuffle cost 30 % of the kernel), so each lane streams one frame and each element
+// costs one extract, one convert, one subtract, two moves, two multiplies and two adds (a per-lane LDS table of
+// x - m instead of convert + subtract measured 8 % slower: 189 vs 175 ms for 1,000 1080p frames).  With one wave per SIMD
 // nothing hides memory latency, so tile rows stream through a register ring KF_DEPTH rows ahead.
-constexpr int KF_DEPTH = 8;
+constexpr int KF_FRAMES_PER_WAVE = 60;
 
+// lane i <- lane i+1 of the same 16-lane row (DPP row_shl:1); lane 15 of a row gets 0 (never used)
+__device__ __forceinline__ double row_next(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x101, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x101, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <int KF_DEPTH, int MODE>
 __global__ __launch_bounds__(64) void pearson_chain_kernel(const int32_t *__restrict__ rgb, int F, int tm_w, int tm_h,
                                                            const unsigned long long *__restrict__ sums,
                                                            double *__restrict__ d2, double *__restrict__ num) {
     const int lane = threadIdx.x;
-    const int f = blockIdx.x * 63 + lane;
+    // 4 rows of 16 lanes; in each row lanes 0..14 own frames and lane 15 feeds lane 14 (DPP row shifts stay
+    // inside a row), so a wave owns 60 frames
+    const int f = blockIdx.x * KF_FRAMES_PER_WAVE + 15 * (lane >> 4) + (lane & 15);
     const int fl = f < F ? f : F - 1;  // lanes past the end replay the last frame (all lanes stay active)
     const long fs = (long)tm_w * tm_h * 64;
     const double m = (double)sums[fl] / (3.0 * (double)fs);
@@ -82,7 +97,7 @@ __global__ __launch_bounds__(64) void pearson_chain_kernel(const int32_t *__rest
     };
 #pragma unroll
     for (int d = 0; d < KF_DEPTH; d++) load_next(r0[d], r1[d], sh[d]);
-    double acc_n = 0.0, acc_d = 0.0;
+    double acc_n = 0.0, acc_d = 0.0, acc_n2 = 0.0, acc_d2 = 0.0;
     for (long j = 0; j < total; j += KF_DEPTH) {
 #pragma unroll
         for (int d = 0; d < KF_DEPTH; d++) {
@@ -95,18 +110,168 @@ __global__ __launch_bounds__(64) void pearson_chain_kernel(const int32_t *__rest
 #pragma unroll
                 for (int k = 0; k < 8; k++) dx[k] = (double)__builtin_amdgcn_ubfe((unsigned)w[k], (unsigned)s, 8u) - m;
 #pragma unroll
-                for (int k = 0; k < 8; k++) dy[k] = __shfl_down(dx[k], 1, 64);
+                for (int k = 0; k < 8; k++) dy[k] = MODE == 1 ? dx[k] : row_next(dx[k]);
+                if (MODE == 2) {  // timing experiment only (re-associated, NOT the reference's result)
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    acc_n = acc_n + dx[k] * dy[k];
-                    acc_d = acc_d + dx[k] * dx[k];
+                    for (int k = 0; k < 8; k += 2) {
+                        acc_n = acc_n + dx[k] * dy[k];
+                        acc_d = acc_d + dx[k] * dx[k];
+                        acc_n2 = acc_n2 + dx[k + 1] * dy[k + 1];
+                        acc_d2 = acc_d2 + dx[k + 1] * dx[k + 1];
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        acc_n = acc_n + dx[k] * dy[k];
+                        acc_d = acc_d + dx[k] * dx[k];
+                    }
                 }
             }
         }
     }
-    if (lane < 63 && f < F) {
+    if (MODE == 2) {
+        acc_n = acc_n + acc_n2;
+        acc_d = acc_d + acc_d2;
+    }
+    if ((lane & 15) < 15 && f < F) {
         d2[f] = acc_d;
         if (f + 1 < F) num[f] = acc_n;
+    }
+}
+
+// Producer/consumer form (default).  The chain adds are the only sequential part; everything else per element
+// (extract, convert, subtract, neighbour move, two multiplies) is independent across elements.  A workgroup of
+// 4 waves serves the same 60 frames: waves 1-3 compute the rounded products (x-m_f)(x'-m_{f+1}) and (x-m_f)^2
+// of a stage of KF_STAGE elements into LDS, wave 0 only adds them in sequence order (one LDS read + two adds per
+// element), double-buffered with one barrier per stage.  Same terms, same order: bit-identical to the lane form.
+// Measured (1,000 random 1080p frames, one MI355X): lane form 175 ms, this form 122 ms; with the consumer idle
+// it still takes 130 ms and with the producers idle 70 ms, and neither 4 producers nor a 4-stage-deep fetch
+// ring moves it, so the producers' fp64 work per CU is what remains.
+template <int MODE, int KF_PRODUCERS, int KF_ROWS_PER_PRODUCER, int KF_PD>
+__global__ __launch_bounds__(512) void pearson_chain_pc_kernel(const int32_t *__restrict__ rgb, int F, int tm_w,
+                                                               int tm_h, const unsigned long long *__restrict__ sums,
+                                                               double *__restrict__ d2, double *__restrict__ num) {
+    constexpr int KF_STAGE_ROWS = KF_PRODUCERS * KF_ROWS_PER_PRODUCER;  // tile rows (8 elements) per stage
+    constexpr int KF_STAGE = KF_STAGE_ROWS * 8;
+    static_assert(2 * KF_STAGE * 64 * 16 <= 160 * 1024, "stage ring exceeds the LDS");
+    __shared__ double2 s_t[2][KF_STAGE][64];  // (num term, d2 term) per element and lane
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int f = blockIdx.x * KF_FRAMES_PER_WAVE + 15 * (lane >> 4) + (lane & 15);
+    const int fl = f < F ? f : F - 1;
+    const long fs = (long)tm_w * tm_h * 64;
+    const int rows = tm_h * 8;
+    const long total = 3L * rows * tm_w;  // tile rows in summation order
+    const long nstage = (total + KF_STAGE_ROWS - 1) / KF_STAGE_ROWS;
+    if (w > 0) {
+        // ---- producer p = w-1: tile rows 9s + 3p + {0,1,2} of stage s ----
+        const int p = w - 1;
+        const double m = (double)sums[fl] / (3.0 * (double)fs);
+        const int4 *a = reinterpret_cast<const int4 *>(rgb + fl * fs);
+        // tile-row cursor (channel, screen row, tile column) of this producer's first row of the next stage to
+        // fetch; it advances by KF_STAGE_ROWS per stage (no divisions in the loop)
+        int cc = 0, csy = 0, ctx = 0;
+        auto advance = [&](int n) {
+            ctx += n;
+            while (ctx >= tm_w) {
+                ctx -= tm_w;
+                if (++csy == rows) {
+                    csy = 0;
+                    ++cc;
+                }
+            }
+        };
+        advance(p * KF_ROWS_PER_PRODUCER);
+        // register ring: stage s lives in slot s % KF_PD, fetched KF_PD stages ahead (one wave per producer
+        // slot has little else to hide a global-load latency with)
+        int4 n0[KF_PD][KF_ROWS_PER_PRODUCER], n1[KF_PD][KF_ROWS_PER_PRODUCER];
+        int ns[KF_PD][KF_ROWS_PER_PRODUCER];
+        auto fetch = [&](int4 *v0, int4 *v1, int *vs) {  // rows beyond the end re-read the last row (never summed)
+            int c = cc, sy = csy, tx = ctx;
+#pragma unroll
+            for (int i = 0; i < KF_ROWS_PER_PRODUCER; i++) {
+                if (c > 2) {
+                    c = 2;
+                    sy = rows - 1;
+                    tx = tm_w - 1;
+                }
+                const long o = (((long)(sy >> 3) * tm_w + tx) * 64 + (sy & 7) * 8) >> 2;
+                v0[i] = a[o];
+                v1[i] = a[o + 1];
+                vs[i] = 8 * c;
+                if (++tx == tm_w) {
+                    tx = 0;
+                    if (++sy == rows) {
+                        sy = 0;
+                        ++c;
+                    }
+                }
+            }
+            advance(KF_STAGE_ROWS);
+        };
+#pragma unroll
+        for (int q = 0; q < KF_PD; q++) fetch(n0[q], n1[q], ns[q]);
+        for (long s0 = 0; s0 < nstage; s0 += KF_PD) {
+#pragma unroll
+            for (int q = 0; q < KF_PD; q++) {
+                const long st = s0 + q;
+                if (st < nstage) {
+                    int4 c0[KF_ROWS_PER_PRODUCER], c1[KF_ROWS_PER_PRODUCER];
+                    int cs[KF_ROWS_PER_PRODUCER];
+#pragma unroll
+                    for (int i = 0; i < KF_ROWS_PER_PRODUCER; i++) {
+                        c0[i] = n0[q][i];
+                        c1[i] = n1[q][i];
+                        cs[i] = ns[q][i];
+                    }
+                    if (st + KF_PD < nstage) fetch(n0[q], n1[q], ns[q]);
+                    if (MODE != 5) {  // MODE 5: timing experiment, producers idle (results invalid)
+                        double2 *buf = &s_t[st & 1][0][0];
+#pragma unroll
+                        for (int i = 0; i < KF_ROWS_PER_PRODUCER; i++) {
+                            const int wv[8] = {c0[i].x, c0[i].y, c0[i].z, c0[i].w, c1[i].x, c1[i].y, c1[i].z, c1[i].w};
+#pragma unroll
+                            for (int e = 0; e < 8; e++) {
+                                const double dx =
+                                    (double)__builtin_amdgcn_ubfe((unsigned)wv[e], (unsigned)cs[i], 8u) - m;
+                                const double dy = row_next(dx);
+                                buf[((p * KF_ROWS_PER_PRODUCER + i) * 8 + e) * 64 + lane] =
+                                    make_double2(dx * dy, dx * dx);
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+        }
+        __syncthreads();
+    } else {
+        // ---- consumer: the two ordered chains ----
+        double acc_n = 0.0, acc_d = 0.0;
+        __syncthreads();
+        for (long st = 0; st < nstage; st++) {
+            const double2 *buf = &s_t[st & 1][0][0];
+            const long left = (total - st * KF_STAGE_ROWS) * 8;
+            if (MODE == 4) {  // timing experiment: consumer idle (results invalid)
+            } else if (left >= KF_STAGE) {
+#pragma unroll 8
+                for (int e = 0; e < KF_STAGE; e++) {
+                    const double2 t = buf[e * 64 + lane];
+                    acc_n = acc_n + t.x;
+                    acc_d = acc_d + t.y;
+                }
+            } else {
+                for (int e = 0; e < (int)left; e++) {
+                    const double2 t = buf[e * 64 + lane];
+                    acc_n = acc_n + t.x;
+                    acc_d = acc_d + t.y;
+                }
+            }
+            __syncthreads();
+        }
+        if ((lane & 15) < 15 && f < F) {
+            d2[f] = acc_d;
+            if (f + 1 < F) num[f] = acc_n;
+        }
     }
 }
 
@@ -139,8 +304,21 @@ int interframe_corr_dev(const int32_t *d_rgb, int F, int tm_w, int tm_h, double 
         }
         {
             KTimer tm("kf_corr", stream);
-            hipLaunchKernelGGL(pearson_chain_kernel, dim3((F + 62) / 63), dim3(64), 0, stream, d_rgb, F, tm_w, tm_h,
-                               d_sums, d_d2, d_num);
+            // TILER_KF_MODE: 0 = producer/consumer kernel, 3 = lane kernel (A/B reference); timing experiments
+            // (results invalid): 1 = lane kernel without the neighbour move, 2 = lane kernel with split chains,
+            // 4 = producer/consumer with the consumer idle, 5 = with the producers idle
+            static const int mode = getenv("TILER_KF_MODE") ? atoi(getenv("TILER_KF_MODE")) : 0;
+            const dim3 grid((F + KF_FRAMES_PER_WAVE - 1) / KF_FRAMES_PER_WAVE);
+            if (mode == 0 || mode >= 4) {
+                auto kern = mode == 4   ? pearson_chain_pc_kernel<4, 3, 3, 2>
+                            : mode == 5 ? pearson_chain_pc_kernel<5, 3, 3, 2>
+                                        : pearson_chain_pc_kernel<0, 3, 3, 2>;
+                hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, d_rgb, F, tm_w, tm_h, d_sums, d_d2, d_num);
+            } else {
+                auto kern = mode == 1 ? pearson_chain_kernel<8, 1> : mode == 2 ? pearson_chain_kernel<8, 2>
+                                                                   : pearson_chain_kernel<8, 0>;
+                hipLaunchKernelGGL(kern, grid, dim3(64), 0, stream, d_rgb, F, tm_w, tm_h, d_sums, d_d2, d_num);
+            }
             if (hipGetLastError() != hipSuccess) break;
         }
         if (hipMemcpyAsync(h.data(), d_d2, (size_t)F * 16, hipMemcpyDeviceToHost, stream) != hipSuccess) break;

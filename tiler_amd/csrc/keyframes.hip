@@ -144,10 +144,12 @@ __global__ __launch_bounds__(64) void pearson_chain_kernel(const int32_t *__rest
 // 4 waves serves the same 60 frames: waves 1-3 compute the rounded products (x-m_f)(x'-m_{f+1}) and (x-m_f)^2
 // of a stage of KF_STAGE elements into LDS, wave 0 only adds them in sequence order (one LDS read + two adds per
 // element), double-buffered with one barrier per stage.  Same terms, same order: bit-identical to the lane form.
-// Measured (1,000 random 1080p frames, one MI355X): lane form 175 ms, this form 122 ms; with the consumer idle
-// it still takes 130 ms and with the producers idle 70 ms, and neither 4 producers nor a 4-stage-deep fetch
-// ring moves it, so the producers' fp64 work per CU is what remains.
-template <int MODE, int KF_PRODUCERS, int KF_ROWS_PER_PRODUCER, int KF_PD>
+// Measured (1,000 random 1080p frames, one MI355X): lane form 175 ms; this form with 60 frames per workgroup
+// 122 ms (consumer idle: 130 ms, producers idle: 70 ms; 4 producers or a 4-stage fetch ring: no change), with
+// 30 frames 89 ms, with 15 frames 84 ms (default: 15 frames = one DPP row per workgroup, the other rows mirror
+// it) -- the 60 scattered frame streams of one CU were limited by that CU's outstanding misses; 70 ms is the
+// consumer's floor (one LDS read and two chained fp64 adds per element).
+template <int MODE, int KF_PRODUCERS, int KF_ROWS_PER_PRODUCER, int KF_PD, int KF_DPP_ROWS>
 __global__ __launch_bounds__(512) void pearson_chain_pc_kernel(const int32_t *__restrict__ rgb, int F, int tm_w,
                                                                int tm_h, const unsigned long long *__restrict__ sums,
                                                                double *__restrict__ d2, double *__restrict__ num) {
@@ -156,7 +158,9 @@ __global__ __launch_bounds__(512) void pearson_chain_pc_kernel(const int32_t *__
     static_assert(2 * KF_STAGE * 64 * 16 <= 160 * 1024, "stage ring exceeds the LDS");
     __shared__ double2 s_t[2][KF_STAGE][64];  // (num term, d2 term) per element and lane
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int f = blockIdx.x * KF_FRAMES_PER_WAVE + 15 * (lane >> 4) + (lane & 15);
+    // KF_DPP_ROWS of the 4 DPP rows own frames (15 each); the other rows mirror them (same addresses, so their
+    // loads merge): fewer frames per CU, more CUs streaming
+    const int f = blockIdx.x * 15 * KF_DPP_ROWS + 15 * ((lane >> 4) % KF_DPP_ROWS) + (lane & 15);
     const int fl = f < F ? f : F - 1;
     const long fs = (long)tm_w * tm_h * 64;
     const int rows = tm_h * 8;
@@ -231,8 +235,10 @@ __global__ __launch_bounds__(512) void pearson_chain_pc_kernel(const int32_t *__
                             const int wv[8] = {c0[i].x, c0[i].y, c0[i].z, c0[i].w, c1[i].x, c1[i].y, c1[i].z, c1[i].w};
 #pragma unroll
                             for (int e = 0; e < 8; e++) {
-                                const double dx =
-                                    (double)__builtin_amdgcn_ubfe((unsigned)wv[e], (unsigned)cs[i], 8u) - m;
+                                // (double)x exactly, without v_cvt_f64_u32: 2^52 + x built from its bits, minus 2^52
+                                const double xb = __hiloint2double(
+                                    0x43300000, (int)__builtin_amdgcn_ubfe((unsigned)wv[e], (unsigned)cs[i], 8u));
+                                const double dx = (xb - 4503599627370496.0) - m;
                                 const double dy = row_next(dx);
                                 buf[((p * KF_ROWS_PER_PRODUCER + i) * 8 + e) * 64 + lane] =
                                     make_double2(dx * dy, dx * dx);
@@ -268,7 +274,7 @@ __global__ __launch_bounds__(512) void pearson_chain_pc_kernel(const int32_t *__
             }
             __syncthreads();
         }
-        if ((lane & 15) < 15 && f < F) {
+        if ((lane & 15) < 15 && (lane >> 4) < KF_DPP_ROWS && f < F) {
             d2[f] = acc_d;
             if (f + 1 < F) num[f] = acc_n;
         }
@@ -310,10 +316,11 @@ int interframe_corr_dev(const int32_t *d_rgb, int F, int tm_w, int tm_h, double 
             static const int mode = getenv("TILER_KF_MODE") ? atoi(getenv("TILER_KF_MODE")) : 0;
             const dim3 grid((F + KF_FRAMES_PER_WAVE - 1) / KF_FRAMES_PER_WAVE);
             if (mode == 0 || mode >= 4) {
-                auto kern = mode == 4   ? pearson_chain_pc_kernel<4, 3, 3, 2>
-                            : mode == 5 ? pearson_chain_pc_kernel<5, 3, 3, 2>
-                                        : pearson_chain_pc_kernel<0, 3, 3, 2>;
-                hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, d_rgb, F, tm_w, tm_h, d_sums, d_d2, d_num);
+                auto kern = mode == 4   ? pearson_chain_pc_kernel<4, 3, 3, 2, 1>
+                            : mode == 5 ? pearson_chain_pc_kernel<5, 3, 3, 2, 1>
+                                        : pearson_chain_pc_kernel<0, 3, 3, 2, 1>;
+                const int per = 15;  // frames per workgroup (one DPP row; see the kernel)
+                hipLaunchKernelGGL(kern, dim3((F + per - 1) / per), dim3(256), 0, stream, d_rgb, F, tm_w, tm_h, d_sums, d_d2, d_num);
             } else {
                 auto kern = mode == 1 ? pearson_chain_kernel<8, 1> : mode == 2 ? pearson_chain_kernel<8, 2>
                                                                    : pearson_chain_kernel<8, 0>;

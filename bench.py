@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-smooth", action="store_true")
     ap.add_argument("--no-keyframes", action="store_true")
+    ap.add_argument("--no-dither", action="store_true")
     ap.add_argument("--clip-frames", type=int, default=1000, help="keyframe-detection clip length (C3: 1000)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI, the product); gloo only to rehearse the N>1 control flow")
@@ -270,6 +271,44 @@ def main():
             keyframes["parity_mismatches_vs_cpu"] = int(np.sum(ocorr.view(np.uint64) != corr[:ns].view(np.uint64)))
         del clip
 
+    # ---- secondary: the Dither step per tile (DitherTile, Thomas Knoll, + PrepareTileMirrors) over this step's
+    # frames with the keyframe's 128 palettes (FinishDitherTiles main.pas:2482-2544) ----
+    dither = None
+    if rank == 0 and not args.no_dither:
+        from tiler_amd.dither import dither_tiles_dev
+        rng_d = np.random.default_rng(args.seed + 7)
+        pal_of = rng_d.integers(0, P, QK).astype(np.int32)
+        d_pal_of = torch.from_numpy(pal_of).to(dev)
+        d_px = torch.empty((QK, 64), dtype=torch.uint8, device=dev)
+        d_dhm = torch.empty(QK, dtype=torch.uint8, device=dev)
+        d_dvm = torch.empty(QK, dtype=torch.uint8, device=dev)
+        call = lambda: dither_tiles_dev(QK, d_rgb.data_ptr(), d_pal_of.data_ptr(), d_pals.data_ptr(), P, 16,  # noqa: E731
+                                        d_px.data_ptr(), d_dhm.data_ptr(), d_dvm.data_ptr(), stream)
+        call()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        call()
+        torch.cuda.synchronize(dev)
+        td = time.perf_counter() - t0
+        dither = {"value": round(QK / td / 1e6, 4), "unit": "Mtiles/s", "ms": round(td * 1e3, 3),
+                  "shape": f"{QK} tiles ({F} frames {W}x{H}), palettes {P} x 16, Thomas Knoll mixing (64 x 16 "
+                           f"colour compares per pixel) + luma QuickSort + PrepareTileMirrors"}
+        if world == 1 and not args.no_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle
+            ns = 400
+            sample = frames.reshape(-1, 64)[:ns]
+            t0 = time.perf_counter()
+            opx, ohm, ovm = pyoracle.dither_tiles_tk(sample, pal_of[:ns], pals)
+            tc = time.perf_counter() - t0
+            gpx = d_px[:ns].cpu().numpy()
+            dither["cpu_baseline"] = {"value": round(ns / tc / 1e6, 6), "unit": "Mtiles/s", "cores": 1, "kind": "port",
+                                      "sample": f"the first {ns} tiles (oracle/dither_tk.c, no colour cache)"}
+            dither["parity_mismatches_vs_cpu"] = int(np.sum(np.any(gpx != opx, axis=1)) +
+                                                     np.sum(d_dhm[:ns].cpu().numpy() != ohm) +
+                                                     np.sum(d_dvm[:ns].cpu().numpy() != ovm))
+        del d_px, d_dhm, d_dvm, d_pal_of
+
     # ---- CPU baseline (rank 0, N=1): the oracle restatement, bounded sample, same workload ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -285,7 +324,7 @@ def main():
                        "tiles_per_step_per_gpu": QK, "candidates": M, "descriptor": "PsyV Haar 192-d",
                        "parallelism": f"keyframes sharded, {world} GPU(s)"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "search_stats": stats,
-            "secondary": {"prepare": prep, "smooth": smooth, "keyframes": keyframes},
+            "secondary": {"prepare": prep, "smooth": smooth, "keyframes": keyframes, "dither": dither},
         }
         print(json.dumps(res))
     kdt.close()

@@ -155,6 +155,18 @@ int tiler_interframe_correlation_dev(const int32_t *d_rgb, int F, int tm_w, int 
  * tile_map_size = FTileMapSize.  Returns the keyframe count, or -1. */
 int tiler_find_keyframes(const double *corr, int F, int tile_map_size, int32_t *kf_of_frame);
 
+/* ---- Dither step, per tile (FinishDitherTiles main.pas:2482-2544) -------------------------
+ * For n frame tiles rgb[n][64] (0x00BBGGRR) and their keyframe palette pal_of[n] (DitheringPalIndex) out of
+ * palettes[n_palettes][palsize] (PaletteRGB, palsize a power of two <= 16): DitherTile with Thomas Knoll mixing
+ * (the default, main.pas:1998-2055 / 1828-1875) then PrepareTileMirrors (main.pas:4049-4069) ->
+ * palpix[n][64] palette indices in canonical orientation, hm/vm[n] (TTile.HMirror / VMirror).
+ * Palette generation (yakmo k-means) and DitheringPalIndex selection are not part of this call.  0 / -1. */
+int tiler_dither_tiles(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int n_palettes,
+                       int palsize, uint8_t *palpix, uint8_t *hm, uint8_t *vm);
+/* Same with every array in HBM; asynchronous on stream. */
+int tiler_dither_tiles_dev(int n, const int32_t *d_rgb, const int32_t *d_pal_of, const int32_t *d_palettes,
+                           int n_palettes, int palsize, uint8_t *d_palpix, uint8_t *d_hm, uint8_t *d_vm, void *stream);
+
 /* ---- GTM keyframe stream compression (host code) ---------------------------------------------------
  * Replaces LZCompress (extern.pas:202-240: temp file + external `lzma.exe e src dst -lc8 -eos`, called
  * per keyframe by SaveStream main.pas:4734).  Writes an LZMA-alone stream (13-byte header: properties

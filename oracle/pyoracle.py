@@ -288,6 +288,27 @@ def find_keyframes(corr, F, tile_map_size):
     return kf, n
 
 
+def tk_plan(pal, col):
+    """DeviseBestMixingPlanThomasKnoll (main.pas:1828-1875): the luma-sorted 64-entry list for one colour."""
+    pal = np.ascontiguousarray(pal, np.int32)
+    out = np.zeros(64, np.uint8)
+    lib().or_tk_plan(_p(pal), pal.size, int(np.int32(col)), _p(out))
+    return out
+
+
+def dither_tiles_tk(rgb, pal_of, palettes):
+    """FinishDitherTiles per tile (DitherTile, Thomas Knoll + PrepareTileMirrors): (palpix, hm, vm)."""
+    rgb = np.ascontiguousarray(rgb, np.int32).reshape(-1, 64)
+    palettes = np.ascontiguousarray(palettes, np.int32)
+    n = rgb.shape[0]
+    palpix = np.zeros((n, 64), np.uint8)
+    hm = np.zeros(n, np.uint8)
+    vm = np.zeros(n, np.uint8)
+    lib().or_dither_tiles_tk(n, _p(rgb), _p(np.ascontiguousarray(pal_of, np.int32)), _p(palettes),
+                             palettes.shape[1], _p(palpix), _p(hm), _p(vm))
+    return palpix, hm, vm
+
+
 def ref_kmodes_lib():
     """The reference's own asm (kmodes.pas:316-596) if oracle/_ref was built here; else None."""
     if not os.path.exists(REF_LIB):

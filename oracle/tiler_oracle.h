@@ -96,6 +96,13 @@ double or_interframe_corr(const int32_t *a, const int32_t *b, int tm_w, int tm_h
 void or_interframe_corr_batch(const int32_t *frames, int F, int tm_w, int tm_h, double *corr);
 int or_find_keyframes(const double *corr, int F, int tile_map_size, int32_t *kf_of_frame);
 
+/* FinishDitherTiles per-tile work, Thomas Knoll mixing (dither_tk.c; main.pas:1494-1571, 1828-1875, 1998-2055,
+ * 4049-4069, QuickSort kmodes.pas:89-136) */
+const uint8_t *or_dither_map(void);
+void or_tk_plan(const int32_t *pal, int palsize, int32_t col, uint8_t *list);
+void or_dither_tiles_tk(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int palsize,
+                        uint8_t *palpix, uint8_t *hm, uint8_t *vm);
+
 #ifdef __cplusplus
 }
 #endif

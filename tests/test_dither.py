@@ -1,0 +1,113 @@
+"""Dither step per tile (DitherTile, Thomas Knoll mixing main.pas:1828-1875 / 1998-2055, PrepareTileMirrors
+main.pas:4049-4069): the CPU restatement (oracle/dither_tk.c) against known answers and an independent Python
+evaluation.  No reference fixture exists for this step (no FPC; yakmo / palettes are not in the reference):
+parity against the reference binary is unpinned; the order of operations is restated from the source."""
+import numpy as np
+import pytest
+
+from tiler_amd import synth
+
+MAP = [0, 48, 12, 60, 3, 51, 15, 63, 32, 16, 44, 28, 35, 19, 47, 31, 8, 56, 4, 52, 11, 59, 7, 55, 40, 24, 36, 20,
+       43, 27, 39, 23, 2, 50, 14, 62, 1, 49, 13, 61, 34, 18, 46, 30, 33, 17, 45, 29, 10, 58, 6, 54, 9, 57, 5, 53,
+       42, 26, 38, 22, 41, 25, 37, 21]
+
+
+def _tdiv(a, b):  # Pascal div (truncation toward zero)
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b > 0) else -q
+
+
+def _py_plan(pal, col):
+    """DeviseBestMixingPlanThomasKnoll in Python ints, then the reference QuickSort (kmodes.pas:89-136)."""
+    rgb = [(c & 255, (c >> 8) & 255, (c >> 16) & 255) for c in pal]
+    luma = [r * 2126 + g * 7152 + b * 722 for r, g, b in rgb]
+    s = (col & 255, (col >> 8) & 255, (col >> 16) & 255)
+    e = [0, 0, 0]
+    lst = []
+    for c in range(64):
+        t = [s[k] + _tdiv(e[k] * 9, 100) for k in range(3)]
+        l1 = t[0] * 2126 + t[1] * 7152 + t[2] * 722
+        best, chosen = None, c & (len(pal) - 1)
+        for i, (r, g, b) in enumerate(rgb):
+            ld = _tdiv(l1 - luma[i], 10000)
+            pen = ((t[0] - r) ** 2) * 13 + ((t[1] - g) ** 2) * 13 + ((t[2] - b) ** 2) * 13 + (ld * ld << 5)
+            if best is None or pen < best:
+                best, chosen = pen, i
+        lst.append(chosen)
+        for k in range(3):
+            e[k] += s[k] - rgb[chosen][k]
+
+    def qs(a, first, last):
+        if last <= first:
+            return
+        while True:
+            i, j, p = first, last, (first + last) >> 1
+            while True:
+                while luma[a[i]] < luma[a[p]]:
+                    i += 1
+                while luma[a[j]] > luma[a[p]]:
+                    j -= 1
+                if i <= j:
+                    a[i], a[j] = a[j], a[i]
+                    if p == i:
+                        p = j
+                    elif p == j:
+                        p = i
+                    i += 1
+                    j -= 1
+                if i > j:
+                    break
+            if first < j:
+                qs(a, first, j)
+            first = i
+            if i >= last:
+                break
+    qs(lst, 0, 63)
+    return np.asarray(lst, np.uint8), luma
+
+
+def _palette(rng, size=16, ties=False):
+    pal = synth.rgb_pack(*rng.integers(0, 256, (3, size)))
+    if ties:  # duplicate colours and distinct colours of equal luma -> the sort's tie order matters
+        pal[3] = pal[1]                                            # duplicate colour
+        pal[5] = synth.rgb_pack(100, 100, 100)                     # equal luma, distinct colours:
+        pal[6] = synth.rgb_pack(117, 90, 149)                      # 17*2126 - 10*7152 + 49*722 = 0
+        pal[9] = synth.rgb_pack(200, 60, 30)
+        pal[10] = synth.rgb_pack(135, 77, 53)                      # -65*2126 + 17*7152 + 23*722 = 0
+    return pal.astype(np.int32)
+
+
+@pytest.mark.parametrize("ties", [False, True])
+def test_tk_plan_matches_python(oracle, ties):
+    rng = np.random.default_rng(21 + ties)
+    for _ in range(6):
+        pal = _palette(rng, ties=ties)
+        for col in synth.rgb_pack(*rng.integers(0, 256, (3, 20))):
+            o = oracle.tk_plan(pal, int(col))
+            p, luma = _py_plan([int(c) for c in pal], int(col))
+            assert np.array_equal(o, p)
+            if ties:
+                assert luma[5] == luma[6] and luma[9] == luma[10]
+            assert all(luma[a] <= luma[b] for a, b in zip(o[:-1], o[1:]))   # sorted by luma
+
+
+def test_tk_plan_known_answers(oracle):
+    pal = _palette(np.random.default_rng(4))
+    for i in (0, 7, 15):
+        assert np.all(oracle.tk_plan(pal, int(pal[i])) == i)   # an exact palette colour: never any error
+    gray = synth.rgb_pack(*([np.arange(16) * 17] * 3)).astype(np.int32)
+    lst = oracle.tk_plan(gray, int(synth.rgb_pack(25, 25, 25)))  # between entries 1 (17) and 2 (34)
+    assert set(lst.tolist()) <= {1, 2} and 0 < int((lst == 2).sum()) < 64
+
+
+def test_dither_tiles_composition(oracle):
+    """or_dither_tiles_tk = per-pixel plan -> cDitheringMap pick -> PrepareTileMirrors."""
+    rng = np.random.default_rng(8)
+    pals = np.stack([_palette(rng, ties=k % 2 == 1) for k in range(4)])
+    rgb = synth.frame_tiles(rng, 12)
+    pal_of = rng.integers(0, 4, 12).astype(np.int32)
+    px, hm, vm = oracle.dither_tiles_tk(rgb, pal_of, pals)
+    raw = np.array([[oracle.tk_plan(pals[pal_of[t]], int(rgb[t, k]))[MAP[k]] for k in range(64)] for t in range(12)],
+                   np.uint8)
+    cpx, chm, cvm = synth.prepare_tile_mirrors(raw)
+    assert np.array_equal(px, cpx.reshape(12, 64)) and np.array_equal(hm, chm) and np.array_equal(vm, cvm)

@@ -74,6 +74,9 @@ _SIGS = {
                                            c_void_p]),
     "tiler_kmodes_compute": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
+    "tiler_dither_tiles": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "tiler_dither_tiles_dev": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                       c_void_p]),
     "tiler_interframe_correlation": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "tiler_interframe_correlation_dev": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "tiler_find_keyframes": (c_int, [c_void_p, c_int, c_int, c_void_p]),

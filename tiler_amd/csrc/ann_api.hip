@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/tiler_ann.h"
+#include "dither.hpp"
 #include "keyframes.hpp"
 #include "kmodes.hpp"
 #include "nn_search.hpp"
@@ -534,6 +535,19 @@ int tiler_smooth_keyframe_dev(int F, int Q, int32_t *d_tile, int32_t *d_tmpidx, 
                               double strength, void *stream) {
     if (!ensure_init()) return -1;
     return smooth_keyframe_dev(F, Q, d_tile, d_tmpidx, d_pal, d_hm, d_vm, d_smoothed, d_palpix, d_palettes, strength,
+                               (hipStream_t)stream);
+}
+
+int tiler_dither_tiles(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int n_palettes,
+                       int palsize, uint8_t *palpix, uint8_t *hm, uint8_t *vm) {
+    if (!ensure_init()) return -1;
+    return dither_tiles_tk_host(n, rgb, pal_of, palettes, n_palettes, palsize, palpix, hm, vm);
+}
+
+int tiler_dither_tiles_dev(int n, const int32_t *d_rgb, const int32_t *d_pal_of, const int32_t *d_palettes,
+                           int n_palettes, int palsize, uint8_t *d_palpix, uint8_t *d_hm, uint8_t *d_vm, void *stream) {
+    if (!ensure_init()) return -1;
+    return dither_tiles_tk_dev(n, d_rgb, d_pal_of, d_palettes, n_palettes, palsize, d_palpix, d_hm, d_vm,
                                (hipStream_t)stream);
 }
 

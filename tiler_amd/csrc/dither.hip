@@ -1,0 +1,223 @@
+// dither.hip -- FinishDitherTiles' per-tile work on gfx950 (once the keyframe palettes exist):
+//   DitherTile with Thomas Knoll mixing (the default, chkUseTK, main.lfm:272-282)   main.pas:1998-2055
+//   DeviseBestMixingPlanThomasKnoll main.pas:1828-1875, PreparePlan main.pas:1494-1526, ColorCompare 1557-1571
+//   the luma sort: the reference's own QuickSort (kmodes.pas:89-136) with PlanCompareLuma (main.pas:1540-1551)
+//   PrepareTileMirrors (canonical orientation) main.pas:4049-4069
+// Layout: one wave per tile, one lane per pixel (y*8+x).  Each lane runs its colour's 64 error-diffusion steps
+// against the tile's palette (wave-uniform, in registers), keeps its 64-entry list in LDS ([entry][lane] bytes),
+// sorts it with the same QuickSort (explicit per-lane stack in LDS: partitions of disjoint ranges commute, so
+// the visiting order does not change the result), and reads entry cDitheringMap[y*8+x].  The quadrant sums and
+// the flip of PrepareTileMirrors are wave reductions and one lane permutation.
+// Integer ranges: |e| <= 63*255, so |t| <= 255 + 1445 and every ColorCompare term fits int32
+// (3*13*1723^2 + 32*1723^2 < 2^31): int32 arithmetic gives the reference's Int64 results exactly.
+// The reference's colour cache (CountCache/ListCache) only memoises lists per colour: not needed here.
+#include <string>
+
+#include "dither.hpp"
+
+namespace tiler {
+
+__constant__ uint8_t c_dither_map[64] = {  // cDitheringMap main.pas:46-55
+    0,  48, 12, 60, 3,  51, 15, 63, 32, 16, 44, 28, 35, 19, 47, 31, 8,  56, 4,  52, 11, 59,
+    7,  55, 40, 24, 36, 20, 43, 27, 39, 23, 2,  50, 14, 62, 1,  49, 13, 61, 34, 18, 46, 30,
+    33, 17, 45, 29, 10, 58, 6,  54, 9,  57, 5,  53, 42, 26, 38, 22, 41, 25, 37, 21};
+
+constexpr int DT_WAVES = 4;       // tiles per workgroup
+constexpr int DT_MAXPAL = 16;     // palette entries held in registers
+constexpr int DT_STACK = 64;      // quicksort ranges per lane (never more than the 64 entries)
+
+__global__ __launch_bounds__(64 * DT_WAVES) void dither_tk_kernel(const int32_t *__restrict__ rgb,
+                                                                  const int32_t *__restrict__ pal_of,
+                                                                  const int32_t *__restrict__ palettes,
+                                                                  int n_palettes, int palsize, int n,
+                                                                  uint8_t *__restrict__ palpix,
+                                                                  uint8_t *__restrict__ hm, uint8_t *__restrict__ vm) {
+    __shared__ uint8_t s_list[DT_WAVES][64 * 64];           // [entry][lane]
+    __shared__ uint16_t s_stk[DT_WAVES][DT_STACK * 64];     // [depth][lane]: first | last << 8
+    __shared__ int s_luma[DT_WAVES][DT_MAXPAL];             // LumaPal of the tile's palette
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int tile = blockIdx.x * DT_WAVES + w;
+    if (tile >= n) return;
+    const int p = pal_of[tile];
+    uint8_t *list = s_list[w];
+    if (p < 0 || p >= n_palettes) {  // invalid input (the host entry rejects it): defined output, no fault
+        palpix[(long)tile * 64 + lane] = 0;
+        if (lane == 0) hm[tile] = vm[tile] = 0;
+        return;
+    }
+    // PreparePlan: Y2Palette r, g, b and LumaPal (wave-uniform)
+    int pr[DT_MAXPAL], pg[DT_MAXPAL], pb[DT_MAXPAL], pl[DT_MAXPAL];
+#pragma unroll
+    for (int i = 0; i < DT_MAXPAL; i++) {
+        const int c = i < palsize ? palettes[(long)p * palsize + i] : 0;
+        pr[i] = c & 0xff;
+        pg[i] = (c >> 8) & 0xff;
+        pb[i] = (c >> 16) & 0xff;
+        pl[i] = pr[i] * 2126 + pg[i] * 7152 + pb[i] * 722;
+    }
+    // DeviseBestMixingPlanThomasKnoll for this lane's colour
+    const int col = rgb[(long)tile * 64 + lane];
+    const int s0 = col & 0xff, s1 = (col >> 8) & 0xff, s2 = (col >> 16) & 0xff;
+    int e0 = 0, e1 = 0, e2 = 0;
+    for (int c = 0; c < 64; c++) {
+        const int t0 = s0 + (e0 * 9) / 100, t1 = s1 + (e1 * 9) / 100, t2 = s2 + (e2 * 9) / 100;
+        const int l1 = t0 * 2126 + t1 * 7152 + t2 * 722;
+        int least = 0x7fffffff, chosen = c & (palsize - 1);
+#pragma unroll
+        for (int i = 0; i < DT_MAXPAL; i++) {
+            if (i < palsize) {
+                const int dr = t0 - pr[i], dg = t1 - pg[i], db = t2 - pb[i];
+                const int ld = (l1 - pl[i]) / 10000;
+                const int pen = dr * dr * 13 + dg * dg * 13 + db * db * 13 + ((ld * ld) << 5);
+                if (pen < least) {
+                    least = pen;
+                    chosen = i;
+                }
+            }
+        }
+        list[c * 64 + lane] = (uint8_t)chosen;
+        int cr = pr[0], cg = pg[0], cb = pb[0];
+#pragma unroll
+        for (int i = 1; i < DT_MAXPAL; i++)
+            if (chosen == i) {
+                cr = pr[i];
+                cg = pg[i];
+                cb = pb[i];
+            }
+        e0 += s0 - cr;
+        e1 += s1 - cg;
+        e2 += s2 - cb;
+    }
+    if (lane < DT_MAXPAL) {
+        const int c = lane < palsize ? palettes[(long)p * palsize + lane] : 0;
+        s_luma[w][lane] = (c & 0xff) * 2126 + ((c >> 8) & 0xff) * 7152 + ((c >> 16) & 0xff) * 722;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    auto luma_of = [&](int v) { return s_luma[w][v]; };  // LumaPal[v] (PlanCompareLuma)
+    // QuickSort (kmodes.pas:89-136): the left part is sorted before the right one continues there; here the
+    // left ranges go to a per-lane stack (disjoint ranges: same final array)
+    uint16_t *stk = s_stk[w];
+    int sp = 0;
+    int first = 0, last = 63;
+    for (;;) {
+        if (last > first) {
+            int i, j;
+            do {
+                i = first;
+                j = last;
+                int pp = (first + last) >> 1;
+                do {
+                    int lp = luma_of(list[pp * 64 + lane]);
+                    while (luma_of(list[i * 64 + lane]) < lp) i++;
+                    while (luma_of(list[j * 64 + lane]) > lp) j--;
+                    if (i <= j) {
+                        const uint8_t t = list[j * 64 + lane];
+                        list[j * 64 + lane] = list[i * 64 + lane];
+                        list[i * 64 + lane] = t;
+                        if (pp == i)
+                            pp = j;
+                        else if (pp == j)
+                            pp = i;
+                        i++;
+                        j--;
+                    }
+                } while (i <= j);
+                if (first < j) stk[(sp++) * 64 + lane] = (uint16_t)(first | (j << 8));
+                first = i;
+            } while (i < last);
+        }
+        if (sp == 0) break;
+        const uint16_t r = stk[(--sp) * 64 + lane];
+        first = r & 0xff;
+        last = r >> 8;
+    }
+    const int px = list[c_dither_map[lane] * 64 + lane];
+    // PrepareTileMirrors: quadrant sums in (vf, hf) order FF, FT, TF, TT, first strict maximum
+    const int y = lane >> 3, x = lane & 7;
+    const int q = (y >= 4 ? 2 : 0) + (x >= 4 ? 1 : 0);
+    int qs[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        int v = q == k ? px : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        qs[k] = v;
+    }
+    int best = -1, bq = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (qs[k] > best) {
+            best = qs[k];
+            bq = k;
+        }
+    const int bh = bq & 1, bv = bq >> 1;
+    const int src = (bv ? 7 - y : y) * 8 + (bh ? 7 - x : x);
+    palpix[(long)tile * 64 + lane] = (uint8_t)__shfl(px, src, 64);
+    if (lane == 0) {
+        hm[tile] = (uint8_t)bh;
+        vm[tile] = (uint8_t)bv;
+    }
+}
+
+int dither_tiles_tk_dev(int n, const int32_t *d_rgb, const int32_t *d_pal_of, const int32_t *d_palettes,
+                        int n_palettes, int palsize, uint8_t *d_palpix, uint8_t *d_hm, uint8_t *d_vm,
+                        hipStream_t stream) {
+    if (n < 0 || n_palettes <= 0 || palsize <= 0 || palsize > DT_MAXPAL || (palsize & (palsize - 1)) ||
+        (n > 0 && (!d_rgb || !d_pal_of || !d_palettes || !d_palpix || !d_hm || !d_vm))) {
+        set_error("dither: invalid arguments (palsize must be a power of two <= 16)");
+        return -1;
+    }
+    if (n == 0) return 0;
+    KTimer tm("dither", stream);
+    hipLaunchKernelGGL(dither_tk_kernel, dim3((n + DT_WAVES - 1) / DT_WAVES), dim3(64 * DT_WAVES), 0, stream, d_rgb,
+                       d_pal_of, d_palettes, n_palettes, palsize, n, d_palpix, d_hm, d_vm);
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int dither_tiles_tk_host(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int n_palettes,
+                         int palsize, uint8_t *palpix, uint8_t *hm, uint8_t *vm) {
+    if (n < 0 || n_palettes <= 0 || palsize <= 0 || palsize > DT_MAXPAL || (palsize & (palsize - 1)) ||
+        (n > 0 && (!rgb || !pal_of || !palettes || !palpix || !hm || !vm))) {
+        set_error("dither: invalid arguments (palsize must be a power of two <= 16)");
+        return -1;
+    }
+    for (int i = 0; i < n; i++)
+        if (pal_of[i] < 0 || pal_of[i] >= n_palettes) {
+            set_error("dither: palette index out of range");
+            return -1;
+        }
+    if (n == 0) return 0;
+    const size_t b_rgb = (size_t)n * 256, b_po = (size_t)n * 4, b_pal = (size_t)n_palettes * palsize * 4;
+    const size_t b_px = (size_t)n * 64;
+    char *buf = nullptr;
+    TILER_HIP_CHECK(hipMalloc((void **)&buf, b_rgb + b_po + b_pal + b_px + 2 * (size_t)n + 64));
+    int32_t *d_rgb = (int32_t *)buf, *d_po = (int32_t *)(buf + b_rgb), *d_pal = (int32_t *)(buf + b_rgb + b_po);
+    uint8_t *d_px = (uint8_t *)(buf + b_rgb + b_po + b_pal), *d_hm = d_px + b_px, *d_vm = d_hm + n;
+    hipStream_t st = nullptr;
+    int rc = -1;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipFree(buf);
+        set_error("dither: stream creation failed");
+        return -1;
+    }
+    do {
+        if (hipMemcpyAsync(d_rgb, rgb, b_rgb, hipMemcpyHostToDevice, st) != hipSuccess) break;
+        if (hipMemcpyAsync(d_po, pal_of, b_po, hipMemcpyHostToDevice, st) != hipSuccess) break;
+        if (hipMemcpyAsync(d_pal, palettes, b_pal, hipMemcpyHostToDevice, st) != hipSuccess) break;
+        if (dither_tiles_tk_dev(n, d_rgb, d_po, d_pal, n_palettes, palsize, d_px, d_hm, d_vm, st)) break;
+        if (hipMemcpyAsync(palpix, d_px, b_px, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+        if (hipMemcpyAsync(hm, d_hm, n, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+        if (hipMemcpyAsync(vm, d_vm, n, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+        if (hipStreamSynchronize(st) != hipSuccess) break;
+        rc = 0;
+    } while (0);
+    if (rc) set_error(std::string("dither: HIP failure: ") + hipGetErrorString(hipGetLastError()));
+    (void)hipStreamDestroy(st);
+    (void)hipFree(buf);
+    return rc;
+}
+
+}  // namespace tiler

@@ -55,10 +55,33 @@ __global__ __launch_bounds__(64 * DT_WAVES) void dither_tk_kernel(const int32_t 
         pb[i] = (c >> 16) & 0xff;
         pl[i] = pr[i] * 2126 + pg[i] * 7152 + pb[i] * 722;
     }
+    if (lane < DT_MAXPAL) {
+        const int c = lane < palsize ? palettes[(long)p * palsize + lane] : 0;
+        s_luma[w][lane] = (c & 0xff) * 2126 + ((c >> 8) & 0xff) * 7152 + ((c >> 16) & 0xff) * 722;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    auto luma_of = [&](int v) { return s_luma[w][v]; };  // LumaPal[v] (PlanCompareLuma)
+    // Distinct lumas (the usual case): every correct sort gives the same array, so entry cDitheringMap[lane] of
+    // the sorted list follows from the histogram and the palette's luma order.  Equal lumas (duplicate colours,
+    // or distinct colours of equal luma) make the reference QuickSort's tie order matter: exact simulation below.
+    int rank = 0;
+    bool tie = false;
+    if (lane < palsize) {
+        const int my = luma_of(lane);
+        for (int j = 0; j < palsize; j++) {
+            const int o = luma_of(j);
+            rank += o < my ? 1 : 0;
+            tie |= (o == my) && j != lane;
+        }
+    }
+    const bool any_tie = __ballot(tie) != 0;
     // DeviseBestMixingPlanThomasKnoll for this lane's colour
     const int col = rgb[(long)tile * 64 + lane];
     const int s0 = col & 0xff, s1 = (col >> 8) & 0xff, s2 = (col >> 16) & 0xff;
     int e0 = 0, e1 = 0, e2 = 0;
+    unsigned cw[DT_MAXPAL / 4] = {0, 0, 0, 0};  // list histogram, 8-bit fields: index i in word i/4, byte i%4
     for (int c = 0; c < 64; c++) {
         const int t0 = s0 + (e0 * 9) / 100, t1 = s1 + (e1 * 9) / 100, t2 = s2 + (e2 * 9) / 100;
         const int l1 = t0 * 2126 + t1 * 7152 + t2 * 722;
@@ -75,7 +98,12 @@ __global__ __launch_bounds__(64 * DT_WAVES) void dither_tk_kernel(const int32_t 
                 }
             }
         }
-        list[c * 64 + lane] = (uint8_t)chosen;
+        if (any_tie) list[c * 64 + lane] = (uint8_t)chosen;  // only the exact sort needs the list
+        {
+            const unsigned inc = 1u << (8 * (chosen & 3));
+#pragma unroll
+            for (int q = 0; q < DT_MAXPAL / 4; q++) cw[q] += (chosen >> 2) == q ? inc : 0u;
+        }
         int cr = pr[0], cg = pg[0], cb = pb[0];
 #pragma unroll
         for (int i = 1; i < DT_MAXPAL; i++)
@@ -88,14 +116,29 @@ __global__ __launch_bounds__(64 * DT_WAVES) void dither_tk_kernel(const int32_t 
         e1 += s1 - cg;
         e2 += s2 - cb;
     }
-    if (lane < DT_MAXPAL) {
-        const int c = lane < palsize ? palettes[(long)p * palsize + lane] : 0;
-        s_luma[w][lane] = (c & 0xff) * 2126 + ((c >> 8) & 0xff) * 7152 + ((c >> 16) & 0xff) * 722;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    auto luma_of = [&](int v) { return s_luma[w][v]; };  // LumaPal[v] (PlanCompareLuma)
+    int px;
+    if (!any_tie) {
+        __shared__ int s_order[DT_WAVES][DT_MAXPAL];
+        if (lane < palsize) s_order[w][rank] = lane;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int want = c_dither_map[lane];
+        int acc = 0;
+        px = 0;
+        bool found = false;
+        for (int r = 0; r < palsize; r++) {
+            const int idx = s_order[w][r];
+            unsigned word = cw[0];
+#pragma unroll
+            for (int q = 1; q < DT_MAXPAL / 4; q++) word = (idx >> 2) == q ? cw[q] : word;
+            acc += (word >> (8 * (idx & 3))) & 0xffu;
+            if (!found && acc > want) {
+                px = idx;
+                found = true;
+            }
+        }
+    } else {
     // QuickSort (kmodes.pas:89-136): the left part is sorted before the right one continues there; here the
     // left ranges go to a per-lane stack (disjoint ranges: same final array)
     uint16_t *stk = s_stk[w];
@@ -133,7 +176,8 @@ __global__ __launch_bounds__(64 * DT_WAVES) void dither_tk_kernel(const int32_t 
         first = r & 0xff;
         last = r >> 8;
     }
-    const int px = list[c_dither_map[lane] * 64 + lane];
+        px = list[c_dither_map[lane] * 64 + lane];
+    }
     // PrepareTileMirrors: quadrant sums in (vf, hf) order FF, FT, TF, TT, first strict maximum
     const int y = lane >> 3, x = lane & 7;
     const int q = (y >= 4 ? 2 : 0) + (x >= 4 ? 1 : 0);

@@ -179,3 +179,30 @@ def test_run_all_chain_two_ranks_match_single_process(gpu, tmp_path):
                  ("sm_tile", sm["tile"]), ("sm_smoothed", sm["smoothed"])):
         assert np.array_equal(got[k], a), k
     assert got["gtm"].tobytes() == data
+
+
+@pytest.mark.gpu
+def test_load_dither_chain(gpu, oracle):
+    """Load (keyframe split) and Dither (Thomas Knoll + mirrors) on the GPU in front of the chain: the Video
+    equals the one composed from the CPU restatements, and the chain runs on it to a decodable .gtm."""
+    from tiler_amd.encoder import Encoder, load_and_dither
+    rng = np.random.default_rng(77)
+    tm_w, tm_h = 20, 15
+    frames, starts = synth.shot_frames(rng, 12, tm_w, tm_h, shot_len=(4, 6))
+    pal_rng = lambda k: np.random.default_rng(1000 + k)  # noqa: E731
+    pf = lambda k, fr: synth.palettes(pal_rng(k), 8)     # noqa: E731
+    v = load_and_dither(frames, tm_w, tm_h, pf)
+    okf, nkf = oracle.find_keyframes(oracle.interframe_corr_batch(frames, tm_w, tm_h), 12, tm_w * tm_h)
+    opals = np.stack([pf(k, None) for k in range(nkf)])
+    ov = synth.video_from_frames(frames, okf, opals, oracle.dither_tiles_tk)
+    assert np.array_equal(v.kf_start, ov.kf_start) and set(starts.tolist()) <= set(v.kf_start[:-1].tolist())
+    for a, b in ((v.palpix, ov.palpix), (v.thm, ov.thm), (v.tvm, ov.tvm), (v.dith_pal, ov.dith_pal)):
+        assert np.array_equal(a, b)
+    o = _OracleChain(ov).run(oracle, 500, FT_MEDIUM, 0.2)
+    e = Encoder(v)
+    sm = e.run_all(500, FT_MEDIUM, 0.2)
+    for a, b in zip((sm["tile"], sm["pal"], sm["hm"], sm["vm"], sm["smoothed"]), o["smooth"]):
+        assert np.array_equal(a, b)
+    from gtm_read import read_gtm
+    g = read_gtm(oracle, e.save_stream(tm_w * 8, tm_h * 8, 24.0))
+    assert len(g.frames) == e.frames and np.array_equal(g.tiles, e.palpix)

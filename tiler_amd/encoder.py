@@ -17,7 +17,20 @@ from . import frame_tiling as ft
 from . import global_tiling as gt
 from .gtm import save_stream
 from .smooth import DEFAULT_STRENGTH, smooth_keyframe
-from .synth import Video
+from .synth import Video, video_from_frames
+
+
+def load_and_dither(frames, tm_w: int, tm_h: int, palettes_fn) -> Video:
+    """The Load and Dither steps in front of the chain (btnLoadClick main.pas:1099-1146, FinishDitherTiles
+    main.pas:2482-2544) on the GPU: keyframes from the inter-frame correlations, then every tile dithered with
+    its keyframe palette.  palettes_fn(k, frames_of_keyframe) -> [P][16] stands in for yakmo (out of scope)."""
+    from .dither import dither_tiles
+    from .keyframes import detect_keyframes
+    frames = np.ascontiguousarray(frames, np.int32).reshape(-1, tm_w * tm_h, 64)
+    kf_of, kf_start, _ = detect_keyframes(frames, tm_w, tm_h)
+    pals = np.stack([np.asarray(palettes_fn(k, frames[kf_start[k]:kf_start[k + 1]]), np.int32)
+                     for k in range(kf_start.size - 1)])
+    return video_from_frames(frames, kf_of, pals, dither_tiles)
 
 
 class Encoder:

@@ -241,12 +241,22 @@ def video(seed: int, width: int, height: int, kf_frames=(3, 3), n_palettes: int 
     pals = np.stack(pals)
     F = frame_rgb.shape[0]
     kf_of = np.repeat(np.arange(len(kf_frames)), kf_frames)
+    dith, palpix = choose_palettes(frame_rgb, pals, kf_of)
+    canon, thm, tvm = prepare_tile_mirrors(palpix.reshape(F * q, 64))
+    return Video(frame_rgb, np.array(starts, np.int64), pals, np.stack([palette_centroids(p) for p in pals]),
+                 canon, thm, tvm, dith.reshape(-1))
+
+
+def choose_palettes(frame_rgb: np.ndarray, pals: np.ndarray, kf_of: np.ndarray):
+    """Stand-in for PrepareDitherTiles' DitheringPalIndex choice (out of scope): per tile, the keyframe palette
+    with the lowest total nearest-colour error; also returns that nearest-colour palettisation."""
+    F, q = frame_rgb.shape[:2]
     px = frame_rgb.reshape(F, q, 64).astype(np.int64)
     palpix = np.zeros((F, q, 64), np.uint8)
     dith = np.zeros((F, q), np.int32)
     for f in range(F):
         c = pals[kf_of[f]].astype(np.int64)  # [P][16]
-        d = np.zeros((q, c.shape[0], 64, 16), np.int64)
+        d = np.zeros((q, c.shape[0], 64, c.shape[1]), np.int64)
         for s in (0, 8, 16):
             t = ((px[f] >> s) & 255)[:, None, :, None] - ((c >> s) & 255)[None, :, None, :]
             d += t * t
@@ -255,9 +265,24 @@ def video(seed: int, width: int, height: int, kf_frames=(3, 3), n_palettes: int 
         pbest = err.argmin(1)
         dith[f] = pbest
         palpix[f] = best_c[np.arange(q), pbest].astype(np.uint8)
-    canon, thm, tvm = prepare_tile_mirrors(palpix.reshape(F * q, 64))
-    return Video(frame_rgb, np.array(starts, np.int64), pals, np.stack([palette_centroids(p) for p in pals]),
-                 canon, thm, tvm, dith.reshape(-1))
+    return dith, palpix
+
+
+def video_from_frames(frames: np.ndarray, kf_of_frame, pals: np.ndarray, ditherer) -> Video:
+    """Load -> Dither without synthetic shortcuts for the parts that are built: keyframes from the Load step's
+    split (kf_of_frame), every tile dithered by `ditherer(rgb, pal_of, palettes) -> (palpix, hm, vm)` (DitherTile
+    Thomas Knoll + PrepareTileMirrors: tiler_amd.dither.dither_tiles, or the oracle's restatement) with the
+    keyframe palettes pals[KF][P][16] and the stand-in DitheringPalIndex choice above."""
+    frames = np.ascontiguousarray(frames, np.int32)
+    F, q = frames.shape[:2]
+    kf_of = np.asarray(kf_of_frame, np.int64)
+    KF, P = pals.shape[:2]
+    dith, _ = choose_palettes(frames, pals, kf_of)
+    flat_of = (kf_of[:, None] * P + dith).reshape(-1).astype(np.int32)  # keyframe palettes stacked
+    palpix, thm, tvm = ditherer(frames.reshape(-1, 64), flat_of, pals.reshape(KF * P, -1))
+    starts = np.r_[np.flatnonzero(np.r_[True, kf_of[1:] != kf_of[:-1]]), F].astype(np.int64)
+    return Video(frames, starts, pals, np.stack([palette_centroids(p) for p in pals]), np.asarray(palpix, np.uint8),
+                 np.asarray(thm, np.uint8), np.asarray(tvm, np.uint8), dith.reshape(-1))
 
 
 def globaltiling_workload(seed: int, n: int = 1 << 20, protos: int = 65536, noise: float = 0.1,

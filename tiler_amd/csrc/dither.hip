@@ -5,8 +5,8 @@
 //   PrepareTileMirrors (canonical orientation) main.pas:4049-4069
 // Layout: one wave per tile, one lane per pixel (y*8+x).  Each lane runs its colour's 64 error-diffusion steps
 // against the tile's palette (wave-uniform, in registers), keeps its 64-entry list in LDS ([entry][lane] bytes),
-// sorts it with the same QuickSort (explicit per-lane stack in LDS: partitions of disjoint ranges commute, so
-// the visiting order does not change the result), and reads entry cDitheringMap[y*8+x].  The quadrant sums and
+// sorts it with the same QuickSort (explicit per-lane stack in LDS, larger side pending: partitions of disjoint
+// ranges commute, so the visiting order does not change the result), and reads entry cDitheringMap[y*8+x].  The quadrant sums and
 // the flip of PrepareTileMirrors are wave reductions and one lane permutation.
 // Integer ranges: |e| <= 63*255, so |t| <= 255 + 1445 and every ColorCompare term fits int32
 // (3*13*1723^2 + 32*1723^2 < 2^31): int32 arithmetic gives the reference's Int64 results exactly.
@@ -24,7 +24,7 @@ __constant__ uint8_t c_dither_map[64] = {  // cDitheringMap main.pas:46-55
 
 constexpr int DT_WAVES = 4;       // tiles per workgroup
 constexpr int DT_MAXPAL = 16;     // palette entries held in registers
-constexpr int DT_STACK = 64;      // quicksort ranges per lane (never more than the 64 entries)
+constexpr int DT_STACK = 8;       // pending quicksort ranges per lane (larger side stacked: <= log2 64)
 
 __global__ __launch_bounds__(64 * DT_WAVES) void dither_tk_kernel(const int32_t *__restrict__ rgb,
                                                                   const int32_t *__restrict__ pal_of,
@@ -54,6 +54,17 @@ __global__ __launch_bounds__(64 * DT_WAVES) void dither_tk_kernel(const int32_t 
         pg[i] = (c >> 8) & 0xff;
         pb[i] = (c >> 16) & 0xff;
         pl[i] = pr[i] * 2126 + pg[i] * 7152 + pb[i] * 722;
+    }
+    // Compare-loop constants.  With t fixed, 13*|t - p_i|^2 = 13*|t|^2 - 26*t.p_i + 13*|p_i|^2: the first term is
+    // common to every i, so dropping it keeps the order and the ties of the strict-'<' scan (exact integers).
+    // LumaPal_i = 10000*la_i + lb_i (0 <= lb_i < 10000), so trunc((l1 - LumaPal_i) / 10000) needs no division
+    // per entry (see the loop).
+    int pc[DT_MAXPAL], la[DT_MAXPAL], lb[DT_MAXPAL];
+#pragma unroll
+    for (int i = 0; i < DT_MAXPAL; i++) {
+        pc[i] = 13 * (pr[i] * pr[i] + pg[i] * pg[i] + pb[i] * pb[i]);
+        la[i] = pl[i] / 10000;
+        lb[i] = pl[i] - la[i] * 10000;
     }
     if (lane < DT_MAXPAL) {
         const int c = lane < palsize ? palettes[(long)p * palsize + lane] : 0;
@@ -85,13 +96,17 @@ __global__ __launch_bounds__(64 * DT_WAVES) void dither_tk_kernel(const int32_t 
     for (int c = 0; c < 64; c++) {
         const int t0 = s0 + (e0 * 9) / 100, t1 = s1 + (e1 * 9) / 100, t2 = s2 + (e2 * 9) / 100;
         const int l1 = t0 * 2126 + t1 * 7152 + t2 * 722;
+        // l1 = 10000*A + B with floor division (0 <= B < 10000); |t| <= 1700 keeps every product in 24 bits
+        const int A = (l1 >= 0 ? l1 : l1 - 9999) / 10000, B = l1 - A * 10000;
         int least = 0x7fffffff, chosen = c & (palsize - 1);
 #pragma unroll
         for (int i = 0; i < DT_MAXPAL; i++) {
             if (i < palsize) {
-                const int dr = t0 - pr[i], dg = t1 - pg[i], db = t2 - pb[i];
-                const int ld = (l1 - pl[i]) / 10000;
-                const int pen = dr * dr * 13 + dg * dg * 13 + db * db * 13 + ((ld * ld) << 5);
+                const int tp = __mul24(t0, pr[i]) + __mul24(t1, pg[i]) + __mul24(t2, pb[i]);
+                // trunc((l1 - LumaPal_i)/10000): floor = (A - la) - (B < lb); +1 when negative and inexact
+                const int fl = (A - la[i]) - (B < lb[i] ? 1 : 0);
+                const int ld = fl + ((fl < 0 && B != lb[i]) ? 1 : 0);
+                const int pen = pc[i] - 26 * tp + ((ld * ld) << 5);  // ColorCompare - 13*|t|^2
                 if (pen < least) {
                     least = pen;
                     chosen = i;
@@ -139,37 +154,50 @@ __global__ __launch_bounds__(64 * DT_WAVES) void dither_tk_kernel(const int32_t 
             }
         }
     } else {
-    // QuickSort (kmodes.pas:89-136): the left part is sorted before the right one continues there; here the
-    // left ranges go to a per-lane stack (disjoint ranges: same final array)
+    // QuickSort (kmodes.pas:89-136), only for palettes with equal lumas: the reference's partition steps on a
+    // per-lane stack of pending ranges (disjoint ranges: the visiting order leaves the final array unchanged)
     uint16_t *stk = s_stk[w];
     int sp = 0;
     int first = 0, last = 63;
     for (;;) {
-        if (last > first) {
-            int i, j;
+        while (last > first) {
+            // one partition step of the reference on [first, last] (same pivot, scans and swaps)
+            int i = first, j = last;
+            int pp = (first + last) >> 1;
             do {
-                i = first;
-                j = last;
-                int pp = (first + last) >> 1;
-                do {
-                    int lp = luma_of(list[pp * 64 + lane]);
-                    while (luma_of(list[i * 64 + lane]) < lp) i++;
-                    while (luma_of(list[j * 64 + lane]) > lp) j--;
-                    if (i <= j) {
-                        const uint8_t t = list[j * 64 + lane];
-                        list[j * 64 + lane] = list[i * 64 + lane];
-                        list[i * 64 + lane] = t;
-                        if (pp == i)
-                            pp = j;
-                        else if (pp == j)
-                            pp = i;
-                        i++;
-                        j--;
-                    }
-                } while (i <= j);
-                if (first < j) stk[(sp++) * 64 + lane] = (uint16_t)(first | (j << 8));
+                const int lp = luma_of(list[pp * 64 + lane]);
+                while (luma_of(list[i * 64 + lane]) < lp) i++;
+                while (luma_of(list[j * 64 + lane]) > lp) j--;
+                if (i <= j) {
+                    const uint8_t t = list[j * 64 + lane];
+                    list[j * 64 + lane] = list[i * 64 + lane];
+                    list[i * 64 + lane] = t;
+                    if (pp == i)
+                        pp = j;
+                    else if (pp == j)
+                        pp = i;
+                    i++;
+                    j--;
+                }
+            } while (i <= j);
+            // the reference sorts [first, j] then [i, last]; they are disjoint, so the order is free: the larger
+            // one waits on the stack (depth <= log2 64), the smaller one continues here
+            const bool hl = first < j, hr = i < last;
+            if (hl && hr) {
+                if (j - first > last - i) {
+                    stk[(sp++) * 64 + lane] = (uint16_t)(first | (j << 8));
+                    first = i;
+                } else {
+                    stk[(sp++) * 64 + lane] = (uint16_t)(i | (last << 8));
+                    last = j;
+                }
+            } else if (hl) {
+                last = j;
+            } else if (hr) {
                 first = i;
-            } while (i < last);
+            } else {
+                break;
+            }
         }
         if (sp == 0) break;
         const uint16_t r = stk[(--sp) * 64 + lane];

@@ -111,3 +111,23 @@ def test_dither_tiles_composition(oracle):
                    np.uint8)
     cpx, chm, cvm = synth.prepare_tile_mirrors(raw)
     assert np.array_equal(px, cpx.reshape(12, 64)) and np.array_equal(hm, chm) and np.array_equal(vm, cvm)
+
+
+def test_video_from_frames_host_logic(oracle):
+    """synth.video_from_frames (the Load -> Dither hand-over of encoder.load_and_dither) with the restatements:
+    keyframe starts from the split, palettes stacked per keyframe, tiles in canonical orientation."""
+    rng = np.random.default_rng(12)
+    tm_w, tm_h = 6, 4
+    frames, starts = synth.shot_frames(rng, 10, tm_w, tm_h, shot_len=(3, 4))
+    kf, nkf = oracle.find_keyframes(oracle.interframe_corr_batch(frames, tm_w, tm_h), 10, tm_w * tm_h)
+    pals = np.stack([synth.palettes(np.random.default_rng(k), 4) for k in range(nkf)])
+    v = synth.video_from_frames(frames, kf, pals, oracle.dither_tiles_tk)
+    assert v.kf_start[0] == 0 and v.kf_start[-1] == 10 and len(v.kf_start) == nkf + 1
+    assert set(starts.tolist()) <= set(v.kf_start[:-1].tolist())
+    assert v.palpix.shape == (10 * tm_w * tm_h, 64) and int(v.dith_pal.max()) < 4
+    canon, hm, vm = synth.prepare_tile_mirrors(v.palpix)   # already canonical: no further flip
+    assert np.array_equal(canon.reshape(v.palpix.shape), v.palpix) and not hm.any() and not vm.any()
+    kf_of = np.repeat(np.arange(nkf), np.diff(v.kf_start))
+    px, thm, tvm = oracle.dither_tiles_tk(frames.reshape(-1, 64), (np.repeat(kf_of, tm_w * tm_h) * 4 + v.dith_pal),
+                                          pals.reshape(-1, 16))
+    assert np.array_equal(px, v.palpix) and np.array_equal(thm, v.thm) and np.array_equal(tvm, v.tvm)

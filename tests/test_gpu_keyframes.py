@@ -50,3 +50,12 @@ def test_1080p_clip_keyframes(gpu, oracle):
     okf, _ = oracle.find_keyframes(o, F, tm_w * tm_h)
     assert np.array_equal(kf, okf)
     assert set(starts.tolist()) <= set(kf_start[:-1].tolist())
+
+
+def test_4k_frames_beyond_reference_cap(gpu, oracle):
+    """4K frames (480x270 tiles, past ReframeUI's 1080p cap main.pas:1933-1934, as C5 uses them): bit-exact."""
+    rng = np.random.default_rng(13)
+    frames, _ = synth.shot_frames(rng, 3, 480, 270, shot_len=(2, 2))
+    g = interframe_correlation(frames, 480, 270)
+    o = oracle.interframe_corr_batch(frames, 480, 270)
+    assert np.array_equal(g.view(np.uint64), o.view(np.uint64))

@@ -21,7 +21,7 @@ def _palettes(rng, P, size):
     return pals
 
 
-@pytest.mark.parametrize("n,P,size", [(1, 1, 16), (5, 3, 16), (1000, 16, 16), (333, 8, 8), (130, 4, 4)])
+@pytest.mark.parametrize("n,P,size", [(1, 1, 16), (5, 3, 16), (1000, 16, 16), (333, 8, 8), (130, 4, 4), (50, 3, 2), (10, 2, 1)])
 def test_dither_bit_exact(gpu, oracle, n, P, size):
     rng = np.random.default_rng(n * 7 + size)
     rgb = synth.frame_tiles(rng, n)

@@ -25,14 +25,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "FrameTiling Mtiles/sec @1080p 8×8, 64k tileset; % HBM roofline at 1/2/4/8 GPU"
 PEAK_F16_TFLOPS = 2500.0   # MI355X dense fp16 MFMA (MI355X_MICROARCH.md; sparsity excluded)
-# dominant kernel per TILER_SHORTLIST variant (tiler_amd/csrc/nn_search.hip, shortlist_variant())
-SHORTLIST_KERNELS = {
-    "q16": "nn_shortlist16_kernel<S=6,L=4,CB=8,NW=8,QB=4>",
-    "q16l6": "nn_shortlist16_kernel<S=6,L=6,CB=8,NW=8,QB=4>",
-    "w8": "nn_shortlist_kernel<S=12,L=8,CB=2,NW=8>",
-}
 ORBIT_KERNEL = "nn_orbit_shortlist_pipe_kernel<L=4,CB=4,NW=8,QB=2>"
+GENERIC_KERNEL = "nn_shortlist16_kernel<S=6,L=4,CB=8,NW=8,QB=4>"
 PEAK_HBM_GBS = 8000.0
+FT_BYTES_PER_TILE_FIXED = 256 + 8 + 4   # RGB in + tilemap item + err out (+ candidate stream / Q_KF)
 
 CONFIGS = {
     # name: (width, height, frames per keyframe step, tileset size)
@@ -170,7 +166,7 @@ def main():
     lib.tiler_timing_enable(0)
     kernels = {}
     for name in ("psyv", "nn_prep", "nn_orbit", "nn_shortlist", "nn_rescore", "nn_pairs", "nn_collect", "nn_rescore2",
-                 "nn_exact"):
+                 "nn_exact", "kd_verify", "kd_replay"):
         n = ctypes.c_int(0)
         ms = lib.tiler_timing_get(name.encode(), ctypes.byref(n))
         kernels[name] = {"ms_total": round(ms, 4), "launches": n.value,
@@ -182,46 +178,65 @@ def main():
         elapsed = float(t.item())
     total_tiles = QK * args.steps * world
     value = total_tiles / elapsed / 1e6
+    ms_step = elapsed / args.steps * 1e3
 
-    # ---- roofline of the dominant kernel, per launch ----
+    # ---- roofline of the dominant kernel, per launch (SURVEY.md 8(d)) ----
     orbit = kernels["nn_orbit"]["launches"] > 0
     sl = kernels["nn_orbit"] if orbit else kernels["nn_shortlist"]
-    flops_launch = 2.0 * M * 192 * QK            # 2*M*D per matched tile (algorithmic)
-    # MFMA flops actually issued: the orbit kernel scores a tile's 4 mirrors with ONE 192-deep contraction
-    issued_launch = 2.0 * (stats["orbit_groups"] if orbit else M) * 192 * QK
     sec = sl["ms_avg"] * 1e-3 if sl["ms_avg"] else None
-    achieved = flops_launch / sec / 1e12 if sec else None
+    # the contraction this algorithm performs: the orbit kernel scores a tile's 4 mirrors with ONE 192-deep
+    # fp16 contraction (2*G*D flops per query, G = tile orbits); the brute-force form is 2*M*D (M = candidates)
+    issued_launch = 2.0 * (stats["orbit_groups"] if orbit else M) * 192 * QK
+    bruteforce_launch = 2.0 * M * 192 * QK
     issued = issued_launch / sec / 1e12 if sec else None
-    kname = ("nn_orbit_shortlist_kernel" if os.environ.get("TILER_ORBIT_PIPE") == "0" else "nn_orbit_shortlist_pipe_kernel") \
-        if orbit else "nn_shortlist16_kernel"
+    effective = bruteforce_launch / sec / 1e12 if sec else None
+    kname = "nn_orbit_shortlist_pipe_kernel" if orbit else "nn_shortlist16_kernel"
     traffic, traffic_src = pmc_traffic(kname)
-    roofline = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None, "peak": PEAK_F16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F16_TFLOPS, 4) if achieved else None,
+    # the metric's own roofline: FrameTiling HBM bytes per matched tile (256 B RGB in + 12 B out +
+    # the keyframe's candidate rows amortised over its queries, M*D*4 / Q_KF) over the step time
+    ft_bytes_tile = FT_BYTES_PER_TILE_FIXED + M * 192 * 4 / QK
+    hbm_gbs = ft_bytes_tile * QK * world / (ms_step * 1e-3) / 1e9
+    roofline = {"bound": "mfma", "achieved": round(issued, 2) if issued else None, "peak": PEAK_F16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(issued / PEAK_F16_TFLOPS, 4) if issued else None,
                 "traffic": traffic, "traffic_unit": "bytes/launch (HBM, FETCH_SIZE x2 + WRITE_SIZE)",
-                "traffic_source": traffic_src,
-                "kernel": ORBIT_KERNEL if orbit else
-                SHORTLIST_KERNELS.get(os.environ.get("TILER_SHORTLIST", ""), SHORTLIST_KERNELS["q16"]),
-                "issued_tflops": round(issued, 2) if issued else None,
-                "issued_frac": round(issued / PEAK_F16_TFLOPS, 4) if issued else None,
-                "note": ("achieved = algorithmic 2*M*D flops per tile (SURVEY.md 8(d)) / kernel time: an EFFECTIVE "
-                         "figure that exceeds the dense fp16 MFMA peak because the orbit kernel scores the 4 mirrors "
-                         "of a tile with one contraction (4x fewer MFMA flops); issued_* = MFMA flops executed / peak")
-                if orbit else "algorithmic 2*M*D per tile vs dense fp16 MFMA peak; 1 fp16 product per pair"}
+                "traffic_source": traffic_src, "kernel": ORBIT_KERNEL if orbit else GENERIC_KERNEL,
+                "kernel_ms_avg": sl["ms_avg"],
+                "flops_per_launch": issued_launch,
+                "effective_tflops": round(effective, 2) if effective else None,
+                "effective_speedup": round(bruteforce_launch / issued_launch, 4),
+                "hbm": {"bytes_per_tile": round(ft_bytes_tile, 1), "achieved_gbs": round(hbm_gbs, 2),
+                        "peak_gbs": PEAK_HBM_GBS, "hbm_frac": round(hbm_gbs / PEAK_HBM_GBS, 6)},
+                "note": ("achieved/frac = MFMA flops the kernel issues (2*G*D per query, G = mirror orbits) / its "
+                         "average launch time (HIP events on the launch stream) vs the dense fp16 peak; "
+                         "effective_tflops = the brute-force 2*M*D per query over the same time (effective_speedup = "
+                         "M/G, the exact 4-mirror orbit algebra). hbm = the metric's '% HBM roofline': SURVEY.md 8(d) "
+                         "bytes per matched tile x tiles / ms_per_step -- small by construction, the search is "
+                         "MFMA-bound (SURVEY.md 7, hard part 5)")}
+    for kn, bpt in (("psyv", 256 + 768),):  # HBM-bound helpers: algorithmic bytes per launch / launch time
+        kk = kernels.get(kn)
+        if kk and kk["ms_avg"]:
+            g = bpt * QK / (kk["ms_avg"] * 1e-3) / 1e9
+            kk["hbm_gbs"] = round(g, 1)
+            kk["hbm_frac"] = round(g / PEAK_HBM_GBS, 4)
+            kk["bytes_per_launch"] = bpt * QK
 
     # ---- secondary: the keyframe's Prepare (reported separately from the FT step) ----
     prep = None
     if rank == 0:
-        tps = []
+        tps, kds = [], []
         for _ in range(3):  # steady state of an encoder walking keyframe after keyframe
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
             kdt2 = prepare()
             tps.append(time.perf_counter() - t0)
+            kds.append(kdt2.stats()["kd_build_ms"])
             kdt2.close()
         tp = min(tps)
         prep = {"ms": round(tp * 1e3, 3), "ms_each": [round(x * 1e3, 3) for x in tps], "candidates": M,
-                "what": "DoPsyV candidate descriptors (fp64 -> fp32 rows) + index build (mirror-orbit grouping, "
-                        "fp16 MFMA fragments, norms, maps), once per keyframe, outside the FT step"}
+                "kd_build_ms_each": kds, "kd_levels": stats["kd_levels"],
+                "what": "DoPsyV candidate descriptors (fp64 -> fp32 rows) + index build (ANN_KD_STD kd-tree for the "
+                        "reference's tie order, mirror-orbit grouping, fp16 MFMA fragments, norms, maps), once per "
+                        "keyframe, outside the FT step"}
 
     # ---- secondary (not the metric): Smooth over this keyframe's FT tilemap (DoTemporalSmoothing) ----
     smooth = None
@@ -238,8 +253,32 @@ def main():
               "tiler_smooth_keyframe_dev")
         torch.cuda.synchronize(dev)
         ts = time.perf_counter() - t0
-        smooth = {"value": round((F - 1) * Q / ts / 1e6, 4), "unit": "Msteps/s", "ms": round(ts * 1e3, 3),
-                  "smoothed": int(s_sm.sum().item()), "shape": f"{F} frames x {Q} positions, Strength 0.02"}
+        steps_s = (F - 1) * Q
+        smooth = {"value": round(steps_s / ts / 1e6, 4), "unit": "Msteps/s", "ms": round(ts * 1e3, 3),
+                  "smoothed": int(s_sm.sum().item()), "shape": f"{F} frames x {Q} positions, Strength 0.02",
+                  "hbm": {"bytes_per_step": 2 * 16 + 64 + 64,
+                          "achieved_gbs": round(steps_s * (2 * 16 + 64 + 64) / ts / 1e9, 2),
+                          "hbm_frac": round(steps_s * (2 * 16 + 64 + 64) / ts / 1e9 / PEAK_HBM_GBS, 6),
+                          "note": "SURVEY.md 8(d) Smooth unit: 2 items + tile + palette per (position, frame) step "
+                                  "(cache-resident; the chain is latency-bound)"}}
+        if world == 1 and not args.no_cpu:
+            # DoTemporalSmoothing on the host (oracle/tiler_oracle.c or_smooth: scalar fp64, positions are
+            # independent chains) on a column sample of the same keyframe, + bit-exact parity with the GPU
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle
+            cols = np.random.default_rng(args.seed + 3).choice(Q, min(Q, 3000), replace=False)
+            src = [x.view(F, Q)[:, cols].cpu().numpy() for x in (out_tile, out_pal, out_hm, out_vm)]
+            t0 = time.perf_counter()
+            o = pyoracle.smooth(src[0], src[1], src[2], src[3], np.zeros((F, cols.size), np.uint8), tiles, pals, 0.02)
+            tc = time.perf_counter() - t0
+            g = [x[:, cols].cpu().numpy() for x in (s_tile, s_pal, s_hm, s_vm, s_sm)]
+            smooth["cpu_baseline"] = {"value": round((F - 1) * cols.size / tc / 1e6, 6), "unit": "Msteps/s",
+                                      "cores": 1, "kind": "port",
+                                      "sample": f"{cols.size} random positions x {F} frames of the same keyframe "
+                                                f"(or_smooth, two fp64 DCT descriptors per step, one thread)"}
+            smooth["parity_positions"] = int(cols.size)
+            smooth["parity_mismatches_vs_cpu"] = int(sum(np.count_nonzero(np.asarray(a) != np.asarray(b))
+                                                         for a, b in zip(g, o[:5])))
 
     # ---- secondary: the Load step's keyframe detection over a whole clip (main.pas:1099-1146) ----
     keyframes = None
@@ -320,7 +359,7 @@ def main():
     if rank == 0:
         res = {
             "metric": METRIC, "value": round(value, 4), "unit": "Mtiles/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded, SURVEY.md 8(d))",
             "config": {"workload": f"{args.config.upper()}: {W}x{H} 8x8 tiles ({Q} tiles/frame), keyframe of {F} "
                                    f"frames per GPU per step, {TS} tileset x 4 mirrors = {M} candidates (P_eff=1)",
@@ -351,11 +390,11 @@ def pmc_traffic(kernel: str):
 
 def cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out_hm, out_vm, out_err):
     """The reference's CPU FrameTiling path on the box's host cores, bounded sample of the same keyframe:
-    the query descriptor (ComputeTilePsyVisFeatures, fp64) + an ANN 1.1.2 kd-tree search (ANN_KD_STD,
-    bucket 1, eps 0: oracle/ann_kdtree.c), timed; then the exhaustive reference-order restatement on a
-    subset for bit-exact parity with the GPU.  The kd-tree's distances must equal the GPU's bit for bit;
-    among equal distances it returns its first visited candidate (ANN's order, parity-unpinned), counted
-    as `kd_ties_resolved_differently`."""
+    the query descriptor (ComputeTilePsyVisFeatures, fp64) + the ANN 1.1.2 kd-tree search (ANN_KD_STD,
+    bucket 1, eps 0: oracle/ann_kdtree.c), timed.  Every sampled query is also the parity check: tile,
+    palette, mirror flags and fp32 distance must equal the GPU's bit for bit (the GPU reproduces ANN's
+    first-found tie order, tiler_amd/csrc/kdtree.hip); `index_order_would_differ` counts the queries where
+    resolving ties to the lowest index instead would have changed the item."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
@@ -370,29 +409,33 @@ def cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out
     q0 = frames.reshape(-1, 64)
     g = [t.cpu().numpy() for t in (out_tile, out_pal, out_hm, out_vm, out_err)]
     done, chunk, spent = 0, 8 * threads, 0.0
-    kd_err_mism = kd_ties = 0
+    mism = dist_mism = 0
+    qd_all, ke_all = [], []
     while spent < args.cpu_seconds and done < q0.shape[0]:
         sl = slice(done, min(done + chunk, q0.shape[0]))
         t0 = time.perf_counter()
         qd = pyoracle.psyv_batch(sl.stop - sl.start, rgb=q0[sl], flags=2).astype(np.float32)
         ki, ke = kd.search_batch(qd, threads=threads)
         spent += time.perf_counter() - t0
-        kd_err_mism += int(np.count_nonzero(ke.view(np.uint32) != g[4][sl].view(np.uint32)))
+        dist_mism += int(np.count_nonzero(ke.view(np.uint32) != g[4][sl].view(np.uint32)))
         same = (ot[ki] == g[0][sl]) & (op[ki] == g[1][sl]) & ((oa[ki] & 1) == g[2][sl]) & ((oa[ki] >> 1) == g[3][sl])
-        kd_ties += int(np.count_nonzero(~same))
+        mism += int(np.count_nonzero(~same))
+        qd_all.append(qd)
+        ke_all.append(ki)
         done = sl.stop
     visited = kd.visited / max(done, 1)
     kd.close()
-    n_exact = min(done, 1024)
-    o = pyoracle.frame_tiling(q0[:n_exact], ods, ot, op, oa, threads=threads)
-    mism = sum(int(np.count_nonzero(np.asarray(a[:n_exact]).view(np.uint8) != np.asarray(b).view(np.uint8)))
-               for a, b in zip(g, o))
+    # the same sample under the lowest-index rule (exhaustive scan): how often the tie rule decides the item
+    qd_all = np.concatenate(qd_all)
+    ki_all = np.concatenate(ke_all)
+    li, _ = pyoracle.nn_batch(ods, qd_all, threads=threads)
+    tie_decided = int(np.count_nonzero((ot[li] != ot[ki_all]) | (oa[li] != oa[ki_all]) | (op[li] != op[ki_all])))
     return {"value": round(done / spent / 1e6, 6), "unit": "Mtiles/s", "cores": threads, "kind": "port",
             "sample": f"first {done} query tiles of the keyframe vs the full {ods.shape[0]}-candidate set: fp64 "
-                      f"descriptor + ANN 1.1.2-style kd-tree (ANN_KD_STD, bucket 1, eps 0; oracle/ann_kdtree.c; "
+                      f"descriptor + ANN 1.1.2 kd-tree (ANN_KD_STD, bucket 1, eps 0; oracle/ann_kdtree.c; "
                       f"{visited:.0f} leaves visited per query, tree build {build_s:.1f} s untimed), {threads} threads",
-            "kd_dist_mismatches_vs_gpu": kd_err_mism, "kd_ties_resolved_differently": kd_ties,
-            "parity_queries": n_exact, "parity_mismatches_vs_gpu": mism}
+            "parity_queries": done, "parity_mismatches_vs_gpu": mism, "dist_mismatches_vs_gpu": dist_mism,
+            "index_order_would_differ": tie_decided}
 
 
 if __name__ == "__main__":

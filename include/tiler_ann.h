@@ -13,9 +13,12 @@
  *
  * Semantics kept from ANN 1.1.2: exact nearest neighbours of the fp32
  * squared distance accumulated in dimension order with every operation rounded (no FMA); err =
- * squared distance (no sqrt); k results ascending.  Differences (superset behaviour):
- *   - equal distances resolve to the LOWEST dataset index (ANN: first found in kd-tree order,
- *     which no reference fixture pins: "parity unpinned" for ties);
+ * squared distance (no sqrt); k results ascending; among equal distances the candidate ANN's own
+ * kd-tree search finds first (split = ANN_KD_STD, bucket size bs: the tree is built exactly as
+ * ANN's kd_tree constructor builds it, and the search result is the one annkSearch returns, its
+ * box-distance pruning included).  Differences (superset behaviour):
+ *   - split = TILER_SPLIT_INDEX_ORDER (100): no tree, equal distances resolve to the lowest index;
+ *     the other ANN split rules (1..5, never used by the reference) are rejected;
  *   - eps > 0 is accepted and ignored: the exact answer satisfies every eps bound;
  *   - the dataset rows are copied to device memory at create (ANN borrows pa until destroy);
  *   - no process abort: errors return -1 (or NULL) and tiler_last_error() explains;
@@ -41,8 +44,13 @@ int ann_kdtree_search(ann_kdtree *akd, float *q, float eps, float *err);
 int ann_kdtree_pri_search(ann_kdtree *akd, float *q, float eps, float *err);
 int ann_kdtree_search_multi(ann_kdtree *akd, int *idxs, float *errs, int cnt, float *q, float eps);
 
-/* Create from fp32 rows already in HBM (d_rows[n][dd], copied); e.g. descriptors made by tiler_psyv_batch_dev. */
+#define TILER_SPLIT_ANN_KD_STD 0     /* ANN_KD_STD (extern.pas:22): the reference's rule */
+#define TILER_SPLIT_INDEX_ORDER 100 /* split value: no kd-tree, ties to the lowest index (faster to create) */
+
+/* Create from fp32 rows already in HBM (d_rows[n][dd], copied); e.g. descriptors made by tiler_psyv_batch_dev.
+ * ann_kdtree_create_dev = ann_kdtree_create_dev_ex(..., bs = 1, split = ANN_KD_STD, ...) (main.pas:3961). */
 ann_kdtree *ann_kdtree_create_dev(const float *d_rows, int n, int dd, void *stream);
+ann_kdtree *ann_kdtree_create_dev_ex(const float *d_rows, int n, int dd, int bs, int split, void *stream);
 
 /* ---- batched extensions; host buffers, row-major q[nq][dd] ---- */
 /* k = 1 for every query: idx[nq], err[nq].  Returns 0 or -1. */
@@ -65,8 +73,15 @@ typedef struct {
     int32_t reserved;
     int64_t orbit_expansions; /* TILER_ORBIT_STATS=1 only: 4-entry re-key passes of the orbit rescore */
     int64_t orbit_rescored;   /* TILER_ORBIT_STATS=1 only: candidates rescored with the reference distance */
+    int32_t tie_order;        /* 0: ANN kd-tree first-found (ANN_KD_STD), 1: lowest index */
+    int32_t kd_levels;        /* levels of the kd-tree build */
+    double kd_build_ms;       /* kd-tree build time at create */
+    int64_t kd_replayed;      /* queries of the last search replayed exactly (ANN's pruning not vouched for) */
 } tiler_search_stats;
 int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
+/* Leaf position of every dataset point in ANN's kd-tree (the order of its depth-first scan with every near
+ * child LO): pos[n].  -1 when the handle was created with TILER_SPLIT_INDEX_ORDER. */
+int tiler_kdtree_positions(ann_kdtree *akd, int32_t *pos);
 
 /* ---- runtime ---- */
 int tiler_init(int device);         /* optional; first call of any entry point initialises device 0 */

@@ -8,13 +8,15 @@
  *          cut_dim = first dimension of maximum spread (max - min) over the node's points, n_lo = n / 2,
  *          quickselect so the n_lo smallest coordinates go low, cut_val = (max of low side + n_lo-th
  *          value) / 2; the node keeps the cell's bounds along cut_dim; buckets of 1 point (bs = 1).
- *   search (annkSearch, k = 1): box distance of q to the root box; at a split node visit the child on
+ *   search (annkSearch, k results): box distance of q to the root box; at a split node visit the child on
  *          q's side first, then update box_dist += cut_diff^2 - box_diff^2 (fp32, ANNdist = float) and
- *          visit the far child iff box_dist * (1 + eps)^2 < current best; leaf distance = sequential fp32
- *          sum of (q_d - p_d)^2, no FMA, break as soon as dist > best; insert iff the scan completed
- *          and dist < best (an equal distance keeps the first found: ANNmin_k::insert).
- * The tie order among equal distances is the tree's visit order (parity-unpinned):
- * bench.py compares its distances, not its indices, with the GPU's.
+ *          visit the far child iff box_dist * (1 + eps)^2 < the current k-th key; leaf distance = sequential
+ *          fp32 sum of (q_d - p_d)^2, no FMA, break as soon as dist > the k-th key read at the leaf's start;
+ *          a completed scan is inserted into ANNmin_k, which shifts only entries with a larger key (an
+ *          equal distance stays behind the first found; at the k-th slot it is dropped).
+ * The tie order among equal distances is therefore the tree's visit order.  libANN.so reproduces it
+ * (tiler_amd/csrc/kdtree.hip); this restatement is the checker for that, pinned by the ANN 1.1.2
+ * algorithm (no reference fixture exists: ANN.dll is a Windows PE).
  */
 #include <float.h>
 #include <pthread.h>
@@ -28,12 +30,12 @@ typedef struct {
     float cut_val;
     float lo_bnd;  /* cell bounds along cut_dim */
     float hi_bnd;
-    int child[2];  /* split: node ids; leaf: child[0] = point index or -1 (empty bucket) */
+    int child[2];  /* split: node ids; leaf: child[0] = first pidx position of the bucket, child[1] = its size */
 } kd_node;
 
 typedef struct {
     const float *data;
-    int n, d;
+    int n, d, bs;
     kd_node *nodes;
     int nn;
     int *pidx;
@@ -101,12 +103,14 @@ static float median_split(const float *data, int d, int *pidx, int n, int dim, i
 #undef SWAP
 }
 
+/* rkd_tree (kd_tree.cpp): n <= bs -> a bucket leaf of pidx[0..n) (n = 0: KD_TRIVIAL, an empty leaf) */
 static int kd_build(kd_tree *t, int *pidx, int n, float *lo, float *hi) {
     const int id = kd_new(t);
     kd_node *nd = &t->nodes[id];
-    if (n <= 1) {
+    if (n <= t->bs) {
         nd->cut_dim = -1;
-        nd->child[0] = n == 1 ? pidx[0] : -1;
+        nd->child[0] = (int)(pidx - t->pidx);
+        nd->child[1] = n;
         return id;
     }
     const int cd = max_spread(t, pidx, n);
@@ -129,11 +133,12 @@ static int kd_build(kd_tree *t, int *pidx, int n, float *lo, float *hi) {
     return id;
 }
 
-void *or_kdtree_build(const float *data, int n, int d) {
+void *or_kdtree_build_bs(const float *data, int n, int d, int bs) {
     kd_tree *t = (kd_tree *)calloc(1, sizeof(kd_tree));
     t->data = data;
     t->n = n;
     t->d = d;
+    t->bs = bs < 1 ? 1 : bs;
     t->nodes = (kd_node *)malloc(sizeof(kd_node) * (size_t)(2 * (n > 0 ? n : 1)));
     t->pidx = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
     t->box_lo = (float *)malloc(sizeof(float) * (size_t)d);
@@ -158,6 +163,46 @@ void *or_kdtree_build(const float *data, int n, int d) {
     return t;
 }
 
+void *or_kdtree_build(const float *data, int n, int d) { return or_kdtree_build_bs(data, n, d, 1); }
+
+static void kd_splits_walk(const kd_tree *t, int id, int s, int *cd, float *cv, float *lo, float *hi) {
+    const kd_node *nd = &t->nodes[id];
+    if (nd->cut_dim < 0) return;
+    /* the LO subtree holds exactly n_lo = size / 2 points; its size is found from its leaves */
+    int lo_size = 0;
+    {
+        int stack[128], sp = 0;
+        stack[sp++] = nd->child[0];
+        while (sp) {
+            const kd_node *c = &t->nodes[stack[--sp]];
+            if (c->cut_dim < 0) lo_size += c->child[1];
+            else {
+                stack[sp++] = c->child[0];
+                stack[sp++] = c->child[1];
+            }
+        }
+    }
+    const int m = s + lo_size;
+    cd[m] = nd->cut_dim;
+    cv[m] = nd->cut_val;
+    lo[m] = nd->lo_bnd;
+    hi[m] = nd->hi_bnd;
+    kd_splits_walk(t, nd->child[0], s, cd, cv, lo, hi);
+    kd_splits_walk(t, nd->child[1], m, cd, cv, lo, hi);
+}
+
+/* every split node by its split position m (LO = positions [s, m)): cut dim, cut value, cell bounds [n] */
+void or_kdtree_splits(void *p, int *cd, float *cv, float *lo, float *hi) {
+    const kd_tree *t = (const kd_tree *)p;
+    if (t->n > 0) kd_splits_walk(t, 0, 0, cd, cv, lo, hi);
+}
+
+/* leaf position of every point: pos[pidx[i]] = i (the DFS order with every LO child first) */
+void or_kdtree_positions(void *p, int *pos) {
+    const kd_tree *t = (const kd_tree *)p;
+    for (int i = 0; i < t->n; i++) pos[t->pidx[i]] = i;
+}
+
 void or_kdtree_free(void *p) {
     kd_tree *t = (kd_tree *)p;
     if (!t) return;
@@ -168,32 +213,54 @@ void or_kdtree_free(void *p) {
     free(t);
 }
 
+/* annkSearch state: ANNmin_k of k entries (k + 1 slots), keys ascending, equal keys in insertion order */
 typedef struct {
     const kd_tree *t;
     const float *q;
-    float best;
-    int bi;
+    int k, cnt;
+    float mk[33];
+    int mi[33];
     long visited;
 } kd_query;
 
+static float kd_max_key(const kd_query *s) { return s->cnt == s->k ? s->mk[s->k - 1] : FLT_MAX; }
+
+/* ANNmin_k::insert: shift only the entries with key > kv, so an equal key stays behind the earlier one */
+static void kd_insert(kd_query *s, float kv, int inf) {
+    int i;
+    for (i = s->cnt; i > 0; i--) {
+        if (s->mk[i - 1] > kv) {
+            s->mk[i] = s->mk[i - 1];
+            s->mi[i] = s->mi[i - 1];
+        } else {
+            break;
+        }
+    }
+    s->mk[i] = kv;
+    s->mi[i] = inf;
+    if (s->cnt < s->k) s->cnt++;
+}
+
 static void kd_search(kd_query *s, int id, float box_dist) {
     const kd_node *nd = &s->t->nodes[id];
-    if (nd->cut_dim < 0) {
-        const int j = nd->child[0];
-        if (j < 0) return;
-        const float *p = s->t->data + (size_t)j * s->t->d;
-        float dist = 0.0f;
-        int i;
-        s->visited++;
-        for (i = 0; i < s->t->d; i++) {
-            const float t = s->q[i] - p[i];
-            const float sq = t * t;
-            dist = dist + sq;
-            if (dist > s->best) break;
-        }
-        if (i >= s->t->d && dist < s->best) {
-            s->best = dist;
-            s->bi = j;
+    if (nd->cut_dim < 0) { /* ANNkd_leaf::ann_search */
+        float min_dist = kd_max_key(s);
+        for (int b = 0; b < nd->child[1]; b++) {
+            const int j = s->t->pidx[nd->child[0] + b];
+            const float *p = s->t->data + (size_t)j * s->t->d;
+            float dist = 0.0f;
+            int i;
+            s->visited++;
+            for (i = 0; i < s->t->d; i++) {
+                const float t = s->q[i] - p[i];
+                const float sq = t * t;
+                dist = dist + sq;
+                if (dist > min_dist) break;
+            }
+            if (i >= s->t->d) {
+                kd_insert(s, dist, j);
+                min_dist = kd_max_key(s);
+            }
         }
         return;
     }
@@ -203,18 +270,24 @@ static void kd_search(kd_query *s, int id, float box_dist) {
         float box_diff = nd->lo_bnd - s->q[nd->cut_dim];
         if (box_diff < 0) box_diff = 0;
         box_dist = box_dist + (cut_diff * cut_diff - box_diff * box_diff);
-        if (box_dist * 1.0f < s->best) kd_search(s, nd->child[1], box_dist);
+        if (box_dist * 1.0f < kd_max_key(s)) kd_search(s, nd->child[1], box_dist);
     } else {
         kd_search(s, nd->child[1], box_dist);
         float box_diff = s->q[nd->cut_dim] - nd->hi_bnd;
         if (box_diff < 0) box_diff = 0;
         box_dist = box_dist + (cut_diff * cut_diff - box_diff * box_diff);
-        if (box_dist * 1.0f < s->best) kd_search(s, nd->child[0], box_dist);
+        if (box_dist * 1.0f < kd_max_key(s)) kd_search(s, nd->child[0], box_dist);
     }
 }
 
-static int kd_nn(const kd_tree *t, const float *q, float *err, long *visited) {
-    kd_query s = {t, q, FLT_MAX, -1, 0};
+/* annkSearch(q, k, idx, dd, eps = 0): k results ascending; missing entries -1 / FLT_MAX */
+static void kd_knn(const kd_tree *t, const float *q, int k, int *idx, float *err, long *visited) {
+    kd_query s;
+    s.t = t;
+    s.q = q;
+    s.k = k;
+    s.cnt = 0;
+    s.visited = 0;
     if (t->n > 0) {
         float bd = 0.0f;  /* annBoxDistance */
         for (int dim = 0; dim < t->d; dim++) {
@@ -225,15 +298,23 @@ static int kd_nn(const kd_tree *t, const float *q, float *err, long *visited) {
         }
         kd_search(&s, 0, bd);
     }
-    if (err) *err = s.best;
+    for (int i = 0; i < k; i++) {
+        idx[i] = i < s.cnt ? s.mi[i] : -1;
+        if (err) err[i] = i < s.cnt ? s.mk[i] : FLT_MAX;
+    }
     if (visited) *visited += s.visited;
-    return s.bi;
+}
+
+static int kd_nn(const kd_tree *t, const float *q, float *err, long *visited) {
+    int i;
+    kd_knn(t, q, 1, &i, err, visited);
+    return i;
 }
 
 typedef struct {
     const kd_tree *t;
     const float *q;
-    int nq, tid, threads;
+    int nq, k, tid, threads;
     int *idx;
     float *err;
     long visited;
@@ -242,18 +323,23 @@ typedef struct {
 static void *kd_worker(void *p) {
     kd_job *j = (kd_job *)p;
     for (int i = j->tid; i < j->nq; i += j->threads)
-        j->idx[i] = kd_nn(j->t, j->q + (size_t)i * j->t->d, &j->err[i], &j->visited);
+        kd_knn(j->t, j->q + (size_t)i * j->t->d, j->k, j->idx + (size_t)i * j->k, j->err + (size_t)i * j->k,
+               &j->visited);
     return NULL;
 }
 
-long or_kdtree_search_batch(void *p, const float *q, int nq, int *idx, float *err, int threads) {
+/* k <= 32 results per query: idx/err [nq][k] */
+long or_kdtree_search_multi_batch(void *p, const float *q, int nq, int k, int *idx, float *err, int threads) {
     const kd_tree *t = (const kd_tree *)p;
+    if (k < 1) k = 1;
+    if (k > 32) k = 32;
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
+    if (threads > nq) threads = nq > 0 ? nq : 1;
     pthread_t th[256];
     kd_job jobs[256];
     for (int i = 0; i < threads; i++) {
-        jobs[i] = (kd_job){t, q, nq, i, threads, idx, err, 0};
+        jobs[i] = (kd_job){t, q, nq, k, i, threads, idx, err, 0};
         pthread_create(&th[i], NULL, kd_worker, &jobs[i]);
     }
     long visited = 0;
@@ -262,4 +348,8 @@ long or_kdtree_search_batch(void *p, const float *q, int nq, int *idx, float *er
         visited += jobs[i].visited;
     }
     return visited;
+}
+
+long or_kdtree_search_batch(void *p, const float *q, int nq, int *idx, float *err, int threads) {
+    return or_kdtree_search_multi_batch(p, q, nq, 1, idx, err, threads);
 }

@@ -106,25 +106,45 @@ def nn_batch(data, qs, threads=None):
 
 
 class KDTree:
-    """The reference's CPU FrameTiling search: ANN 1.1.2 kd-tree (ann_kdtree.c), k = 1, eps = 0."""
+    """The reference's CPU search: ANN 1.1.2 kd-tree (ann_kdtree.c; ANN_KD_STD, bucket bs, eps = 0)."""
 
-    def __init__(self, data):
+    def __init__(self, data, bs: int = 1):
         self.data = np.ascontiguousarray(data, np.float32)
-        f = lib().or_kdtree_build
+        f = lib().or_kdtree_build_bs
         f.restype = ctypes.c_void_p
-        f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-        self.h = f(_p(self.data), self.data.shape[0], self.data.shape[1])
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        self.h = f(_p(self.data), self.data.shape[0], self.data.shape[1], bs)
         self.visited = 0
 
-    def search_batch(self, qs, threads=None):
-        qs = np.ascontiguousarray(qs, np.float32)
-        idx = np.zeros(qs.shape[0], np.int32)
-        err = np.zeros(qs.shape[0], np.float32)
-        f = lib().or_kdtree_search_batch
+    def search_batch(self, qs, threads=None, k: int = 1):
+        """annkSearch per query: k = 1 -> (idx[nq], err[nq]); k > 1 -> ([nq, k], [nq, k]) ascending."""
+        qs = np.ascontiguousarray(qs, np.float32).reshape(-1, self.data.shape[1])
+        idx = np.zeros((qs.shape[0], k), np.int32)
+        err = np.zeros((qs.shape[0], k), np.float32)
+        f = lib().or_kdtree_search_multi_batch
         f.restype = ctypes.c_long
-        f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-        self.visited += f(self.h, _p(qs), qs.shape[0], _p(idx), _p(err), threads or _threads())
-        return idx, err
+        f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                      ctypes.c_int]
+        self.visited += f(self.h, _p(qs), qs.shape[0], k, _p(idx), _p(err), threads or _threads())
+        return (idx[:, 0], err[:, 0]) if k == 1 else (idx, err)
+
+    def splits(self):
+        """split nodes by split position m: (cut_dim, cut_val, lo_bnd, hi_bnd), arrays [n] (index 0 unused)"""
+        n = self.data.shape[0]
+        cd = np.zeros(n, np.int32)
+        cv, lo, hi = (np.zeros(n, np.float32) for _ in range(3))
+        f = lib().or_kdtree_splits
+        f.argtypes = [ctypes.c_void_p] * 5
+        f(self.h, _p(cd), _p(cv), _p(lo), _p(hi))
+        return cd, cv, lo, hi
+
+    def positions(self):
+        """leaf position of every point (pos[pidx[i]] = i)"""
+        pos = np.zeros(self.data.shape[0], np.int32)
+        f = lib().or_kdtree_positions
+        f.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        f(self.h, _p(pos))
+        return pos
 
     def close(self):
         if self.h:
@@ -152,13 +172,15 @@ def build_ft_dataset(used, palpix, thm, tvm, palettes, use_wavelets=True, gamma=
     return ds[:n], tidx[:n], pidx[:n], attrs[:n]
 
 
-def frame_tiling(frame_rgb, ds, tidx, pidx, attrs, use_wavelets=True, gamma=-1, threads=None):
+def frame_tiling(frame_rgb, ds, tidx, pidx, attrs, use_wavelets=True, gamma=-1, threads=None, kd_order=True):
+    """DoFrameTiling; kd_order: ties as ANN's kd-tree search returns them (the reference), else lowest index."""
     rgb = np.ascontiguousarray(frame_rgb, np.int32).reshape(-1, 64)
     Q = rgb.shape[0]
     out = [np.zeros(Q, np.int32), np.zeros(Q, np.int32), np.zeros(Q, np.uint8), np.zeros(Q, np.uint8),
            np.zeros(Q, np.float32)]
     lib().or_frame_tiling(_p(rgb), Q, _p(np.ascontiguousarray(ds, np.float32)), ds.shape[0], _p(tidx), _p(pidx),
-                          _p(attrs), int(use_wavelets), gamma, threads or _threads(), *[_p(o) for o in out])
+                          _p(attrs), int(use_wavelets), gamma, threads or _threads(), int(bool(kd_order)),
+                          *[_p(o) for o in out])
     return tuple(out)
 
 
@@ -181,7 +203,8 @@ def palette_corr(centroids):
     return corr, hi
 
 
-def mark_used(gds, g_tile, g_attr, item_pal, item_tile, palpix, P, quality, corrs=None, highest=0.0, paltol=0.05):
+def mark_used(gds, g_tile, g_attr, item_pal, item_tile, palpix, P, quality, corrs=None, highest=0.0, paltol=0.05,
+              kd_order=True):
     palpix = np.ascontiguousarray(palpix, np.uint8)
     T = palpix.shape[0]
     used = np.zeros((P, T, 4), np.uint8)
@@ -191,10 +214,10 @@ def mark_used(gds, g_tile, g_attr, item_pal, item_tile, palpix, P, quality, corr
     f = lib().or_mark_used
     f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                   ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                  ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+                  ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_void_p]
     f(_p(np.ascontiguousarray(gds, np.float32)), gds.shape[0], _p(np.ascontiguousarray(g_tile, np.int32)),
       _p(np.ascontiguousarray(g_attr, np.uint8)), _p(item_pal), _p(item_tile), item_pal.size, _p(palpix), T, P,
-      quality, _p(corrs), highest, paltol, _p(used))
+      quality, _p(corrs), highest, paltol, int(bool(kd_order)), _p(used))
     return used
 
 

@@ -304,17 +304,36 @@ double or_palette_corr(const double *centroids, int P, double *corrs) {
 /* PrepareFrameTiling.UseOne main.pas:3802-3853 (+ DoBuild 3869-3881).  used: P x T x 4 bytes. */
 void or_mark_used(const float *gds, int gn, const int32_t *g_tile, const uint8_t *g_attr, const int32_t *item_pal,
                   const int32_t *item_tile, int nitems, const uint8_t *palpix, int T, int P, int quality,
-                  const double *corrs, double highest, double paltol, uint8_t *used) {
+                  const double *corrs, double highest, double paltol, int kd_order, uint8_t *used) {
     uint8_t *seen = (uint8_t *)calloc((size_t)P * T, 1);
-    float line[64];
-    int idxs[8];
-    float errs[8];
+    /* the distinct (pal, tile) items in first-seen order, their 64-index query lines and k = 8 results */
+    int *ip = (int *)malloc(sizeof(int) * (size_t)(nitems > 0 ? nitems : 1));
+    int *itl = (int *)malloc(sizeof(int) * (size_t)(nitems > 0 ? nitems : 1));
+    int nd = 0;
     for (int it = 0; it < nitems; it++) {
         int p = item_pal[it], ti = item_tile[it];
         if (seen[(size_t)p * T + ti]) continue;
         seen[(size_t)p * T + ti] = 1;
-        for (int i = 0; i < 64; i++) line[i] = (float)palpix[(size_t)ti * 64 + i];
-        or_knn(gds, gn, 64, line, 8, idxs, errs);
+        ip[nd] = p;
+        itl[nd] = ti;
+        nd++;
+    }
+    float *lines = (float *)malloc(sizeof(float) * 64 * (size_t)(nd > 0 ? nd : 1));
+    int *ridx = (int *)malloc(sizeof(int) * 8 * (size_t)(nd > 0 ? nd : 1));
+    float *rerr = (float *)malloc(sizeof(float) * 8 * (size_t)(nd > 0 ? nd : 1));
+    for (int j = 0; j < nd; j++)
+        for (int i = 0; i < 64; i++) lines[(size_t)j * 64 + i] = (float)palpix[(size_t)itl[j] * 64 + i];
+    if (kd_order && gn > 0) {  /* ann_kdtree_search_multi on FGlobalDS.KDT (main.pas:3779,3830) */
+        void *kd = or_kdtree_build(gds, gn, 64);
+        or_kdtree_search_multi_batch(kd, lines, nd, 8, ridx, rerr, 8);
+        or_kdtree_free(kd);
+    } else {
+        for (int j = 0; j < nd; j++) or_knn(gds, gn, 64, lines + (size_t)j * 64, 8, ridx + 8 * j, rerr + 8 * j);
+    }
+    for (int j = 0; j < nd; j++) {
+        const int p = ip[j];
+        const int *idxs = ridx + 8 * (size_t)j;
+        const float *errs = rerr + 8 * (size_t)j;
         float last = INFINITY;
         for (int i = 0; i < 8; i++) {
             if (errs[i] == last) continue;
@@ -333,6 +352,11 @@ void or_mark_used(const float *gds, int gn, const int32_t *g_tile, const uint8_t
         }
     }
     free(seen);
+    free(ip);
+    free(itl);
+    free(lines);
+    free(ridx);
+    free(rerr);
 }
 
 int or_count_used(const uint8_t *used, int P, int T) {
@@ -367,7 +391,7 @@ int or_build_ft_dataset(const uint8_t *used, int P, int T, const uint8_t *palpix
 
 /* DoFrameTiling main.pas:3992-4047 (query descriptor 4023-4025, search 4027, tilemap 4029-4034). */
 void or_frame_tiling(const int32_t *frame_rgb, int Q, const float *ds, int M, const int32_t *tidx,
-                     const int32_t *pidx, const uint8_t *attrs, int use_wavelets, int gamma, int threads,
+                     const int32_t *pidx, const uint8_t *attrs, int use_wavelets, int gamma, int threads, int kd_order,
                      int32_t *out_tile, int32_t *out_pal, uint8_t *out_h, uint8_t *out_v, float *out_err) {
     float *qs = (float *)malloc(sizeof(float) * 192 * (size_t)Q);
     int *bi = (int *)malloc(sizeof(int) * (size_t)Q);
@@ -376,7 +400,13 @@ void or_frame_tiling(const int32_t *frame_rgb, int Q, const float *ds, int M, co
         or_psyv(frame_rgb + 64 * (size_t)i, NULL, NULL, use_wavelets ? OR_WAVELETS : 0, gamma, desc);
         for (int j = 0; j < 192; j++) qs[(size_t)i * 192 + j] = (float)desc[j];
     }
-    or_nn_batch(ds, M, 192, qs, Q, bi, out_err, threads);
+    if (kd_order && M > 0) {  /* ann_kdtree_search on the keyframe's KDT (main.pas:3961, 4027) */
+        void *kd = or_kdtree_build(ds, M, 192);
+        or_kdtree_search_batch(kd, qs, Q, bi, out_err, threads);
+        or_kdtree_free(kd);
+    } else {
+        or_nn_batch(ds, M, 192, qs, Q, bi, out_err, threads);
+    }
     for (int i = 0; i < Q; i++) {
         int b = bi[i];
         out_tile[i] = b >= 0 ? tidx[b] : -1;

@@ -13,8 +13,9 @@
  * Parity pins: the K-Modes dissimilarity / argmin / min-distance update are pinned against
  * the reference's own asm assembled from kmodes.pas (oracle/build_ref_asm.sh -> oracle/_ref).
  * The descriptor, FT and Smooth paths have no reference fixture (no FPC, ANN.dll is a PE):
- * they are pinned by known-answer tests (tests/golden) derived from the formulas; tie order
- * of ANN's kd-tree is "parity unpinned" (canonical rule: lowest candidate index).
+ * they are pinned by known-answer tests (tests/golden) derived from the formulas.  Ties follow
+ * ANN 1.1.2's kd-tree search (ann_kdtree.c, the published algorithm restated; kd_order = 1), or
+ * the lowest candidate index (kd_order = 0, the opt-in rule).
  */
 #ifndef TILER_ORACLE_H
 #define TILER_ORACLE_H
@@ -53,8 +54,12 @@ void or_nn_batch(const float *data, int n, int d, const float *q, int nq, int *i
 
 /* ANN 1.1.2 kd-tree (ANN_KD_STD, bucket 1, eps 0): the reference's CPU search (ann_kdtree.c). */
 void *or_kdtree_build(const float *data, int n, int d);
+void *or_kdtree_build_bs(const float *data, int n, int d, int bs);
 void or_kdtree_free(void *t);
 long or_kdtree_search_batch(void *t, const float *q, int nq, int *idx, float *err, int threads);
+long or_kdtree_search_multi_batch(void *t, const float *q, int nq, int k, int *idx, float *err, int threads);
+void or_kdtree_positions(void *t, int *pos);
+void or_kdtree_splits(void *t, int *cd, float *cv, float *lo, float *hi);
 
 /* LZMA-alone decoder (lzma_dec.c): decoded size, -1 corrupt, -2 out too small; consumed = bytes read. */
 long or_lzma_decode(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *consumed);
@@ -62,15 +67,16 @@ long or_lzma_decode(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_
 int or_prepare_global_ds(const uint8_t *palpix, const uint8_t *active, int T, float *ds, int32_t *tile_idx,
                          uint8_t *attrs);
 double or_palette_corr(const double *centroids, int P, double *corrs);
+/* kd_order: 1 = the k = 8 search through ANN's kd-tree (the reference's tie order), 0 = lowest index */
 void or_mark_used(const float *gds, int gn, const int32_t *g_tile, const uint8_t *g_attr, const int32_t *item_pal,
                   const int32_t *item_tile, int nitems, const uint8_t *palpix, int T, int P, int quality,
-                  const double *corrs, double highest, double paltol, uint8_t *used);
+                  const double *corrs, double highest, double paltol, int kd_order, uint8_t *used);
 int or_count_used(const uint8_t *used, int P, int T);
 int or_build_ft_dataset(const uint8_t *used, int P, int T, const uint8_t *palpix, const uint8_t *thm,
                         const uint8_t *tvm, const int32_t *palettes, int use_wavelets, int gamma, float *ds,
                         int32_t *tidx, int32_t *pidx, uint8_t *attrs);
 void or_frame_tiling(const int32_t *frame_rgb, int Q, const float *ds, int M, const int32_t *tidx,
-                     const int32_t *pidx, const uint8_t *attrs, int use_wavelets, int gamma, int threads,
+                     const int32_t *pidx, const uint8_t *attrs, int use_wavelets, int gamma, int threads, int kd_order,
                      int32_t *out_tile, int32_t *out_pal, uint8_t *out_h, uint8_t *out_v, float *out_err);
 
 void or_smooth(int F, int Q, int32_t *tile, int32_t *tmpidx, int32_t *pal, uint8_t *hm, uint8_t *vm,

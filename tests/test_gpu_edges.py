@@ -4,6 +4,7 @@ the dataset, orbit datasets with a lone (symmetric) tile, NaN-free extreme-but-f
 an empty frame through tiler_frame_tiling."""
 import numpy as np
 import pytest
+from nncheck import INDEX_ORDER, check_nn
 
 from tiler_amd import synth
 
@@ -22,10 +23,9 @@ def test_single_candidate_and_single_query(gpu, oracle):
     data = rng.normal(0, 1, (1, 192)).astype(np.float32)
     q = rng.normal(0, 1, (5, 192)).astype(np.float32)
     with gpu.KDTree(data) as kdt:
-        gi, ge = kdt.search_batch(q)
         i1, e1 = kdt.search(q[0])
     oi, oe = oracle.nn_batch(data, q)
-    assert np.array_equal(gi, oi) and np.array_equal(ge.view(np.uint32), oe.view(np.uint32))
+    check_nn(gpu, oracle, data, q)
     assert i1 == 0 and np.float32(e1) == oe[0]
 
 
@@ -38,29 +38,23 @@ def test_ragged_query_counts_orbit(gpu, oracle, nq):
     used = synth.used_one_palette(rng.integers(0, 4, 300).astype(np.int32), 4)
     ods, *_ = oracle.build_ft_dataset(used, tiles, thm, tvm, pals)
     q = oracle.psyv_batch(nq, rgb=synth.frame_tiles(rng, nq), flags=2).astype(np.float32)
-    with gpu.KDTree(ods) as kdt:
-        gi, ge = kdt.search_batch(q)
-        st = kdt.stats()
-    oi, oe = oracle.nn_batch(ods, q)
+    st = check_nn(gpu, oracle, ods, q)
     assert st["orbit_search"] == 1
-    assert np.array_equal(gi, oi) and np.array_equal(ge.view(np.uint32), oe.view(np.uint32))
 
 
 def test_k_larger_than_dataset(gpu, oracle):
     rng = np.random.default_rng(4)
     data = rng.integers(0, 16, (5, 64)).astype(np.float32)
     q = rng.integers(0, 16, (3, 64)).astype(np.float32)
+    check_nn(gpu, oracle, data, q, k=8)
     with gpu.KDTree(data) as kdt:
         gi, ge = kdt.search_batch(q, k=8)
-    for j in range(3):
-        oi, oe = oracle.knn(data, q[j], 8)
-        assert np.array_equal(gi[j], oi) and np.array_equal(ge[j], oe)
-        assert (gi[j, 5:] == -1).all()
+    assert (gi[:, 5:] == -1).all()
 
 
 def test_lone_symmetric_tile_orbit(gpu, oracle):
     """A dataset of one fully symmetric tile in 4 orientations (4 identical rows) and one plain tile:
-    every query's winner is the lowest index among equal rows."""
+    every query's winner is the first-found (kd order) / lowest index (index order) among equal rows."""
     t = np.zeros((2, 64), np.uint8)
     t[0] = 5
     t[1] = np.arange(64) % 16
@@ -71,11 +65,10 @@ def test_lone_symmetric_tile_orbit(gpu, oracle):
     ods, *_ = oracle.build_ft_dataset(used, t, thm, tvm, pals)
     rng = np.random.default_rng(6)
     q = np.concatenate([ods, oracle.psyv_batch(40, rgb=synth.frame_tiles(rng, 40), flags=2)]).astype(np.float32)
-    with gpu.KDTree(ods) as kdt:
-        gi, ge = kdt.search_batch(q)
-    oi, oe = oracle.nn_batch(ods, q)
-    assert np.array_equal(gi, oi) and np.array_equal(ge.view(np.uint32), oe.view(np.uint32))
-    assert gi[1] == 0 and gi[3] == 0  # the symmetric tile's mirrors resolve to its first row
+    check_nn(gpu, oracle, ods, q)
+    with gpu.KDTree(ods, split=INDEX_ORDER) as kdt:
+        gi, _ = kdt.search_batch(q)
+    assert gi[1] == 0 and gi[3] == 0  # index order: the symmetric tile's mirrors resolve to its first row
 
 
 def test_empty_frame_through_frame_tiling(gpu):

@@ -1,10 +1,12 @@
 """GPU parity: libANN.so (HIP, gfx950) against the CPU restatement (oracle/) on seeded inputs.
 
 Bar: descriptors fp64 bit-exact; distances fp32 bit-exact; tile / palette / mirror
-indices bit-exact under the canonical tie rule (lowest candidate index).
+indices bit-exact under ANN's kd-tree tie order (the reference's, default) and under the lowest-index
+opt-in (split = TILER_SPLIT_INDEX_ORDER).
 """
 import numpy as np
 import pytest
+from nncheck import INDEX_ORDER, check_nn
 
 from tiler_amd import synth
 
@@ -49,13 +51,7 @@ def test_psyv_palette_bit_exact(gpu, oracle):
 
 
 def _check_nn(gpu, oracle, data, qs):
-    with gpu.KDTree(data) as kdt:
-        gi, ge = kdt.search_batch(qs)
-        st = kdt.stats()
-    oi, oe = oracle.nn_batch(data, qs)
-    assert np.array_equal(gi, oi), f"{np.count_nonzero(gi != oi)} index mismatches"
-    assert np.array_equal(ge.view(np.uint32), oe.view(np.uint32))
-    return st
+    return check_nn(gpu, oracle, data, qs)
 
 
 def test_nn_random_descriptors(gpu, oracle):
@@ -72,7 +68,7 @@ def test_nn_random_descriptors(gpu, oracle):
     _check_nn(gpu, oracle, data, q2)
 
 
-def test_nn_ties_lowest_index(gpu, oracle):
+def test_nn_ties_both_orders(gpu, oracle):
     rng = np.random.default_rng(2)
     base = rng.normal(0, 1, (500, 192)).astype(np.float32)
     data = np.concatenate([base, base[::-1], base[:50]])  # every row duplicated, some three times
@@ -111,27 +107,36 @@ def test_knn_palette_index_preselection(gpu, oracle):
     qs = tiles[rng.integers(0, 1500, 400)].astype(np.float32)
     qs[200:] = rng.integers(0, 16, (200, 64))
     with gpu.KDTree(gds) as kdt:
-        gi, ge = kdt.search_batch(qs, k=8)
         assert kdt.stats()["exact_integer"] == 1
-    for i in range(qs.shape[0]):
-        oi, oe = oracle.knn(gds, qs[i], 8)
-        assert np.array_equal(gi[i], oi) and np.array_equal(ge[i], oe), i
+    check_nn(gpu, oracle, gds, qs, k=8)
 
 
 def test_reference_call_shapes(gpu, oracle):
     """ann_kdtree_search / search_multi one query at a time, as main.pas:4027 and 3830 call them."""
     rng = np.random.default_rng(6)
     data = rng.normal(0, 1, (4000, 192)).astype(np.float32)
-    with gpu.KDTree(data) as kdt:
-        for j in range(5):
-            q = rng.normal(0, 1, 192).astype(np.float32)
-            i, e = kdt.search(q)
-            oi, oe = oracle.nn(data, q)
-            assert (i, np.float32(e)) == (oi, np.float32(oe))
-            for k in (1, 8, 20):
-                ii, ee = kdt.search_multi(q, k)
-                oi2, oe2 = oracle.knn(data, q, k)
-                assert np.array_equal(ii, oi2) and np.array_equal(ee, oe2)
+    data[7] = data[3]  # an exact duplicate: a tie for queries near it
+    okd = oracle.KDTree(data)
+    for split in (0, INDEX_ORDER):
+        with gpu.KDTree(data, split=split) as kdt:
+            for j in range(6):
+                q = rng.normal(0, 1, 192).astype(np.float32) if j < 5 else data[3] + np.float32(1e-4)
+                i, e = kdt.search(q)
+                if split == 0:
+                    oi, oe = okd.search_batch(q[None])
+                    oi, oe = int(oi[0]), float(oe[0])
+                else:
+                    oi, oe = oracle.nn(data, q)
+                assert (i, np.float32(e)) == (oi, np.float32(oe)), (split, j)
+                for k in (1, 8, 20):
+                    ii, ee = kdt.search_multi(q, k)
+                    if split == 0:
+                        oi2, oe2 = okd.search_batch(q[None], k=k)
+                        oi2, oe2 = oi2.reshape(-1), oe2.reshape(-1)
+                    else:
+                        oi2, oe2 = oracle.knn(data, q, k)
+                    assert np.array_equal(ii, oi2) and np.array_equal(ee, oe2), (split, j, k)
+    okd.close()
     with gpu.KDTree(np.zeros((0, 192), np.float32)) as empty:
         idx, err = empty.search_batch(np.zeros((2, 192), np.float32))
         assert (idx == -1).all()

@@ -2,10 +2,12 @@
 
 The orbit path scores the 4 H/V mirrors of a tile (PrepareFrameTiling.DoPsyV emission order,
 main.pas:3883-3919) with one MFMA pass; results must stay bit-identical to the exhaustive reference-order
-scan: index, fp32 distance, lowest index on exact ties.
+scan: index, fp32 distance, and on exact ties ANN's kd-tree first-found candidate
+(default) or the lowest index (split = TILER_SPLIT_INDEX_ORDER) -- nncheck.check_nn runs both.
 """
 import numpy as np
 import pytest
+from nncheck import INDEX_ORDER, check_nn
 
 from tiler_amd import synth
 
@@ -25,12 +27,7 @@ def _ft_rows(oracle, seed, T, P, used_fn=None):
 
 
 def _check(gpu, oracle, data, qs, expect_orbit=True):
-    with gpu.KDTree(data) as kdt:
-        gi, ge = kdt.search_batch(qs)
-        st = kdt.stats()
-    oi, oe = oracle.nn_batch(data, qs)
-    assert np.array_equal(gi, oi), f"{np.count_nonzero(gi != oi)} index mismatches of {len(qs)}"
-    assert np.array_equal(ge.view(np.uint32), oe.view(np.uint32))
+    st = check_nn(gpu, oracle, data, qs)
     if expect_orbit:
         assert st["orbit_search"] == 1 and st["orbit_groups"] > 0, st
     return st
@@ -56,7 +53,7 @@ def test_orbit_partial_mirror_sets(gpu, oracle):
 
 
 def test_orbit_exact_matches_and_mirror_ties(gpu, oracle):
-    """Queries that ARE candidates (distance 0): symmetric tiles tie across mirrors -> lowest index."""
+    """Queries that ARE candidates (distance 0): symmetric tiles tie across mirrors."""
     rng, ods, *_ = _ft_rows(oracle, 33, 1200, 8)
     pick = rng.integers(0, ods.shape[0], 700)
     q = ods[pick].copy()
@@ -66,7 +63,7 @@ def test_orbit_exact_matches_and_mirror_ties(gpu, oracle):
 
 def test_orbit_duplicate_tiles_force_overflow(gpu, oracle):
     """Many identical tiles (same palette) make equal-distance groups larger than the shortlists: the
-    overflow tiers must still return the lowest-index winner."""
+    overflow tiers must still return the right winner under both tie rules."""
     rng = np.random.default_rng(34)
     tiles, thm, tvm = synth.tileset(rng, 400)
     tiles[200:] = tiles[0]
@@ -116,10 +113,11 @@ def test_orbit_c2_frame_sampled(gpu, oracle):
     assert st["orbit_search"] == 1
 
 
-def test_orbit_c3_self_queries(gpu):
+def test_orbit_c3_self_queries(gpu, oracle):
     """Full C3 candidate set (64k tileset x 4 mirrors = 262,144 rows, built on the GPU): querying rows of
-    the dataset must return distance 0 and the LOWEST index holding an identical row (size-independent
-    property of the exact search + canonical tie rule, covers symmetric tiles whose mirrors coincide)."""
+    the dataset must return distance 0 and, under index order, the LOWEST index holding an identical row
+    (size-independent property of the exact search, covers symmetric tiles whose mirrors coincide); under
+    ANN's order the very candidate oracle/ann_kdtree.c finds first."""
     rng = np.random.default_rng(43)
     P, T = 128, 65536
     pals = synth.palettes(rng, P)
@@ -128,7 +126,7 @@ def test_orbit_c3_self_queries(gpu):
     rows = gpu.psyv_batch(palpix=tiles, tile_of=ds.tile_of, palettes=pals, pal_of=ds.pal_of,
                           flags_per=ds.psyv_flags, flags=1 | 2, gamma=-1, want32=True)[1]
     pick = rng.choice(rows.shape[0], 3000, replace=False)
-    with gpu.KDTree(rows) as kdt:
+    with gpu.KDTree(rows, split=INDEX_ORDER) as kdt:
         gi, ge = kdt.search_batch(rows[pick])
         st = kdt.stats()
     assert st["orbit_search"] == 1 and st["orbit_groups"] == T
@@ -138,3 +136,37 @@ def test_orbit_c3_self_queries(gpu):
     _, first = np.unique(v, return_index=True)
     inv = np.unique(v, return_inverse=True)[1].ravel()
     assert np.array_equal(gi, first[inv[pick]])
+    # ANN's order: the kd-tree's first-found copy
+    with gpu.KDTree(rows) as kdt:
+        ki, ke = kdt.search_batch(rows[pick])
+        pos = kdt.positions()
+    okd = oracle.KDTree(rows)
+    assert np.array_equal(pos, okd.positions()), "kd-tree leaf order differs from ANN's"
+    oi, oe = okd.search_batch(rows[pick])
+    okd.close()
+    assert (ke == 0).all() and np.array_equal(ki, oi)
+    assert np.array_equal(rows[ki].view(np.uint32), rows[pick].view(np.uint32))
+
+
+def test_ann_tie_order_c3_frame_queries(gpu, oracle):
+    """SURVEY.md 8(a) a8 at the headline size: a C3 keyframe dataset (64k tileset x 4 mirrors, 20 % symmetric
+    tiles) and 3,072 frame-tile queries (smooth / textured / flat mix) through
+    tiler_frame_tiling; tile, palette and mirror flags must equal ANN 1.1.2's kd-tree search (oracle)."""
+    from tiler_amd.frame_tiling import KeyframeTiler
+    wl = synth.make_workload(45, 1920, 1080, 1, 65536, n_palettes=128)
+    kt = KeyframeTiler(wl.tiles, wl.thm, wl.tvm, wl.palettes, wl.ds)
+    q = wl.frame_rgb[0][:3072]
+    g = kt.do_frame_tiling(q)
+    st = kt.kdt.stats()
+    kt.finish_frame_tiling()
+    used = synth.used_one_palette(wl.tile_pal, 128)
+    ods, ot, op, oa = oracle.build_ft_dataset(used, wl.tiles, wl.thm, wl.tvm, wl.palettes)
+    o = oracle.frame_tiling(q, ods, ot, op, oa)
+    assert np.array_equal(np.asarray(g[4]).view(np.uint32), o[4].view(np.uint32))
+    for a, b in zip(g[:4], o[:4]):
+        assert np.array_equal(a, b), f"{np.count_nonzero(a != b)} of {q.shape[0]} items differ"
+    # the tie rule matters here: lowest-index resolution differs from ANN's on many of these queries
+    oi = oracle.frame_tiling(q, ods, ot, op, oa, kd_order=False)
+    n_tie = int(np.count_nonzero((oi[0] != o[0]) | (oi[2] != o[2]) | (oi[3] != o[3])))
+    assert n_tie > 0
+    assert st["orbit_search"] == 1 and st["tie_order"] == 0

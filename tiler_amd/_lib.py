@@ -31,12 +31,16 @@ class SearchStats(ctypes.Structure):
     _fields_ = [("queries", ctypes.c_int64), ("fallback_queries", ctypes.c_int64),
                 ("exhaustive_queries", ctypes.c_int64), ("exact_integer", ctypes.c_int32), ("splits", ctypes.c_int32),
                 ("orbit_groups", ctypes.c_int64), ("orbit_search", ctypes.c_int32), ("reserved", ctypes.c_int32),
-                ("orbit_expansions", ctypes.c_int64), ("orbit_rescored", ctypes.c_int64)]
+                ("orbit_expansions", ctypes.c_int64), ("orbit_rescored", ctypes.c_int64),
+                ("tie_order", ctypes.c_int32), ("kd_levels", ctypes.c_int32), ("kd_build_ms", ctypes.c_double),
+                ("kd_replayed", ctypes.c_int64)]
 
 
 _SIGS = {
     "ann_kdtree_create": (c_void_p, [P(P(c_float)), c_int, c_int, c_int, c_int]),
     "ann_kdtree_create_dev": (c_void_p, [c_void_p, c_int, c_int, c_void_p]),
+    "ann_kdtree_create_dev_ex": (c_void_p, [c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "tiler_kdtree_positions": (c_int, [c_void_p, c_void_p]),
     "ann_kdtree_destroy": (None, [c_void_p]),
     "ann_kdtree_search": (c_int, [c_void_p, c_void_p, c_float, c_void_p]),
     "ann_kdtree_pri_search": (c_int, [c_void_p, c_void_p, c_float, c_void_p]),

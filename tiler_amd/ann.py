@@ -18,16 +18,24 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+ANN_KD_STD = 0            # TANNsplitRule (extern.pas:21-28): the reference's rule, ANN's tie order
+SPLIT_INDEX_ORDER = 100   # extension: no kd-tree, equal distances resolve to the lowest index
+
+
 class KDTree:
-    """ann_kdtree_create(pa, n, dd, bs=1, split=ANN_KD_STD) ... ann_kdtree_destroy."""
+    """ann_kdtree_create(pa, n, dd, bs=1, split=ANN_KD_STD) ... ann_kdtree_destroy.
+
+    split = ANN_KD_STD builds ANN's kd-tree so that ties come out as the reference's search returns them;
+    split = SPLIT_INDEX_ORDER skips it (ties to the lowest index)."""
 
     def __init__(self, data=None, *, dev_ptr: int | None = None, n: int | None = None, dd: int | None = None,
-                 stream: int = 0, bs: int = 1, split: int = 0):
+                 stream: int = 0, bs: int = 1, split: int = ANN_KD_STD):
         lib = load()
         self._lib = lib
         if dev_ptr is not None:
             self.n, self.dd = int(n), int(dd)
-            h = lib.ann_kdtree_create_dev(ctypes.c_void_p(dev_ptr), self.n, self.dd, ctypes.c_void_p(stream))
+            h = lib.ann_kdtree_create_dev_ex(ctypes.c_void_p(dev_ptr), self.n, self.dd, bs, split,
+                                             ctypes.c_void_p(stream))
         else:
             data = np.ascontiguousarray(data, dtype=np.float32)
             if data.ndim != 2:
@@ -97,4 +105,13 @@ class KDTree:
         return {"queries": s.queries, "fallback_queries": s.fallback_queries,
                 "exhaustive_queries": s.exhaustive_queries, "exact_integer": s.exact_integer, "splits": s.splits,
                 "orbit_groups": s.orbit_groups, "orbit_search": s.orbit_search,
-                "orbit_expansions": s.orbit_expansions, "orbit_rescored": s.orbit_rescored}
+                "orbit_expansions": s.orbit_expansions, "orbit_rescored": s.orbit_rescored,
+                "tie_order": s.tie_order, "kd_levels": s.kd_levels, "kd_build_ms": round(s.kd_build_ms, 3),
+                "kd_replayed": s.kd_replayed}
+
+    def positions(self) -> np.ndarray:
+        """Leaf position of every point in ANN's kd-tree (tiler_kdtree_positions)."""
+        pos = np.zeros(self.n, np.int32)
+        if self.n:
+            check(self._lib.tiler_kdtree_positions(self.handle, _ptr(pos)), "tiler_kdtree_positions")
+        return pos

@@ -224,14 +224,26 @@ int tiler_set_gamma(double g0, double g1) {
     return upload_gamma_lut();
 }
 
+static bool split_ok(int bs, int split, const char *who) {
+    if (bs < 1) {
+        set_error(std::string(who) + ": bucket size must be >= 1");
+        return false;
+    }
+    if (split != KD_SPLIT_STD && split != KD_SPLIT_INDEX_ORDER) {
+        // the reference only ever passes ANN_KD_STD (main.pas:3779,3961); other ANN rules shape other trees
+        set_error(std::string(who) + ": split rule not supported (ANN_KD_STD = 0, or 100 = ties to the lowest index)");
+        return false;
+    }
+    return true;
+}
+
 ann_kdtree *ann_kdtree_create(float **pa, int n, int dd, int bs, int split) {
-    (void)bs;
-    (void)split;  // bucket size / split rule only shape ANN's tree; the exhaustive search has none
     if (!ensure_init()) return nullptr;
     if (n < 0 || dd <= 0 || (n > 0 && !pa)) {
         set_error("ann_kdtree_create: invalid arguments");
         return nullptr;
     }
+    if (!split_ok(bs, split, "ann_kdtree_create")) return nullptr;
     std::vector<float> h((size_t)n * dd);
     for (int i = 0; i < n; i++) {
         if (!pa[i]) {
@@ -246,7 +258,7 @@ ann_kdtree *ann_kdtree_create(float **pa, int n, int dd, int bs, int split) {
     TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_rows, std::max<size_t>(1, h.size()) * sizeof(float)));
     if (n > 0)
         TILER_HIP_CHECK_NULL(hipMemcpyAsync(d_rows, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, t->stream));
-    t->ix = nn_index_create_dev(d_rows, n, dd, t->stream);
+    t->ix = nn_index_create_dev(d_rows, n, dd, bs, split, t->stream);
     if (!t->ix) {
         hipStreamDestroy(t->stream);
         delete t;
@@ -256,11 +268,16 @@ ann_kdtree *ann_kdtree_create(float **pa, int n, int dd, int bs, int split) {
 }
 
 ann_kdtree *ann_kdtree_create_dev(const float *d_rows_in, int n, int dd, void *stream) {
+    return ann_kdtree_create_dev_ex(d_rows_in, n, dd, 1, KD_SPLIT_STD, stream);
+}
+
+ann_kdtree *ann_kdtree_create_dev_ex(const float *d_rows_in, int n, int dd, int bs, int split, void *stream) {
     if (!ensure_init()) return nullptr;
     if (n < 0 || dd <= 0 || (n > 0 && !d_rows_in)) {
         set_error("ann_kdtree_create_dev: invalid arguments");
         return nullptr;
     }
+    if (!split_ok(bs, split, "ann_kdtree_create_dev")) return nullptr;
     ann_kdtree *t = new ann_kdtree();
     TILER_HIP_CHECK_NULL(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
@@ -268,7 +285,7 @@ ann_kdtree *ann_kdtree_create_dev(const float *d_rows_in, int n, int dd, void *s
     const size_t bytes = (size_t)n * dd * sizeof(float);
     TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_rows, std::max<size_t>(4, bytes)));
     if (n > 0) TILER_HIP_CHECK_NULL(hipMemcpyAsync(d_rows, d_rows_in, bytes, hipMemcpyDeviceToDevice, s));
-    t->ix = nn_index_create_dev(d_rows, n, dd, s);
+    t->ix = nn_index_create_dev(d_rows, n, dd, bs, split, s);
     if (!t->ix) {
         (void)hipStreamDestroy(t->stream);
         delete t;
@@ -370,7 +387,30 @@ int ann_kdtree_get_stats(ann_kdtree *t, tiler_search_stats *out) {
     if (t->ix->orbit) orbit_counters(t->ix, &ne, &nr);
     out->orbit_expansions = ne;
     out->orbit_rescored = nr;
+    out->tie_order = t->ix->kd ? 0 : 1;
+    out->kd_levels = t->ix->kd ? t->ix->kd->levels : 0;
+    out->kd_build_ms = t->ix->kd ? t->ix->kd->build_ms : 0.0;
+    out->kd_replayed = 0;
+    if (t->ix->kd && t->ix->scratch.kd_count) {
+        int c = 0;
+        TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
+        TILER_HIP_CHECK(hipMemcpy(&c, t->ix->scratch.kd_count, sizeof(int), hipMemcpyDeviceToHost));
+        out->kd_replayed = c;
+    }
     return 0;
+}
+
+int tiler_kdtree_positions(ann_kdtree *t, int32_t *pos) {
+    if (!t || !t->ix || !pos) {
+        set_error("tiler_kdtree_positions: invalid arguments");
+        return -1;
+    }
+    if (!t->ix->kd) {
+        set_error("tiler_kdtree_positions: handle has no kd-tree (KD_SPLIT_INDEX_ORDER)");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(t->ix->mu);
+    return kd_tree_positions(t->ix->kd, pos);
 }
 
 int tiler_psyv_batch_dev(int n, const int32_t *rgb, const uint8_t *palpix, const int32_t *tile_of,

@@ -1,0 +1,102 @@
+// kdorder_dev.hpp -- device side of the ANN tie order (kdtree.hpp): which of two equal-distance candidates
+// annkSearch finds first, and ANN's box-distance pruning replayed along one candidate's path.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "kdtree.hpp"
+
+#pragma clang fp contract(off)
+
+namespace tiler {
+
+// True iff candidate a is visited before candidate b by ANN's depth-first search for query q (near child
+// first: LO when q[cd] - cv < 0, ANNkd_split::ann_search).  Order of the visit over ALL leaves: at the two
+// candidates' lowest common node, the one in q's near child comes first; inside one bucket, position order
+// (ANNkd_leaf::ann_search scans bkt[] in order).  Without a tree: the lower index.  Invalid ids (< 0 or
+// >= n, e.g. the 0x7fffffff "none" sentinel) come after every valid one.
+__device__ __forceinline__ bool kd_before(const KdOrder &o, const float *__restrict__ q, int a, int b) {
+    if (!o.pos || (unsigned)a >= (unsigned)o.n || (unsigned)b >= (unsigned)o.n) return (unsigned)a < (unsigned)b;
+    int pa = o.pos[a], pb = o.pos[b];
+    const bool sw = pa > pb;
+    if (sw) {
+        const int t = pa;
+        pa = pb;
+        pb = t;
+    }
+    int s = 0, e = o.n;
+    while (e - s > o.bs) {
+        const int m = s + ((e - s) >> 1);
+        if (pb < m) {
+            e = m;
+        } else if (pa >= m) {
+            s = m;
+        } else {
+            const float cut_diff = q[o.cd[m]] - o.cv[m];
+            return (cut_diff < 0.0f) != sw;
+        }
+    }
+    return !sw;
+}
+
+// (dist, kd order) lexicographic "less"
+__device__ __forceinline__ bool kd_less(const KdOrder &o, const float *__restrict__ q, float da, int a, float db,
+                                        int b) {
+    return da < db || (da == db && kd_before(o, q, a, b));
+}
+
+// (dist, kd order) minimum over lanes xor-reachable below `width` (64: the wave, 32: a half-wave, 4: a quad)
+template <int WIDTH>
+__device__ __forceinline__ void kd_argmin(const KdOrder &o, const float *__restrict__ q, float &v, int &i) {
+#pragma unroll
+    for (int off = WIDTH / 2; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(v, off, 64);
+        const int oi = __shfl_xor(i, off, 64);
+        if (kd_less(o, q, ov, oi, v, i)) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
+// annBoxDistance(q, bnd_box_lo, bnd_box_hi, dim): fp32, dimension order, every op rounded
+__device__ __forceinline__ float kd_root_box(const KdOrder &o, const float *__restrict__ q) {
+    float dist = 0.0f;
+    for (int d = 0; d < o.dd; d++) {
+        const float v = q[d], lo = o.box_lo[d], hi = o.box_hi[d];
+        if (v < lo) {
+            const float t = lo - v;
+            dist = dist + t * t;
+        } else if (v > hi) {
+            const float t = v - hi;
+            dist = dist + t * t;
+        }
+    }
+    return dist;
+}
+
+// The largest box distance ANN computes for a far child on the root-to-leaf path of leaf position p
+// (ANNkd_split::ann_search: box_dist + (cut_diff^2 - box_diff^2), fp32).  The leaf is visited iff every one of
+// these is < the k-th key current at that check; -inf when p lies only in near children.
+__device__ __forceinline__ float kd_path_far_box(const KdOrder &o, const float *__restrict__ q, int p, float root_box) {
+    float box = root_box, worst = -INFINITY;
+    int s = 0, e = o.n;
+    while (e - s > o.bs) {
+        const int m = s + ((e - s) >> 1);
+        const float qd = q[o.cd[m]];
+        const float cut_diff = qd - o.cv[m];
+        const bool lo_first = cut_diff < 0.0f, in_lo = p < m;
+        if (in_lo != lo_first) {
+            float box_diff = lo_first ? o.lo[m] - qd : qd - o.hi[m];
+            if (box_diff < 0.0f) box_diff = 0.0f;
+            box = box + (cut_diff * cut_diff - box_diff * box_diff);
+            worst = fmaxf(worst, box);
+        }
+        if (in_lo)
+            e = m;
+        else
+            s = m;
+    }
+    return worst;
+}
+
+}  // namespace tiler

@@ -1,0 +1,60 @@
+// kdtree.hpp -- the reference's ANN 1.1.2 kd-tree (ann_kdtree_create(..., bs, ANN_KD_STD), main.pas:3779,3961)
+// over an HBM-resident dataset, kept for ONE purpose: reproducing which of several equal-distance candidates
+// ANN returns (its first-found order, extern.pas:65-67 / main.pas:3830,4027), bit for bit.  The search itself
+// stays the exact MFMA search of nn_search.hip / orbit.hip; this tree orders ties, checks ANN's box pruning
+// along the winner's path and, where that check cannot vouch for the result, replays ANN's search exactly.
+//
+// Shape (kd_split: n_lo = n / 2, annMedianSplit): a node covering pidx positions [s, e) with e - s > bs splits
+// at m = s + (e - s) / 2 into LO [s, m) and HI [m, e).  The shape is implicit; split positions m are unique,
+// so internal nodes are indexed by m (1..n-1).  Leaves are buckets of <= bs consecutive positions.
+#pragma once
+#include "tiler_common.hpp"
+
+namespace tiler {
+
+// ANNsplitRule (extern.pas:21-28) plus this library's extension: no tree, ties to the lowest index
+enum { KD_SPLIT_STD = 0, KD_SPLIT_INDEX_ORDER = 100 };  // = include/tiler_ann.h TILER_SPLIT_*
+
+// Device view.  pos == nullptr: index order (the lowest candidate index wins a tie).
+struct KdOrder {
+    const int *pos = nullptr;               // [n] point -> leaf position
+    const int *pidx = nullptr;              // [n] leaf position -> point
+    const int *cd = nullptr;                // [n] cut dimension of internal node m
+    const float *cv = nullptr;              // [n] cut value
+    const float *lo = nullptr, *hi = nullptr;        // [n] cell bounds along cd (ANNkd_split::cd_bnds)
+    const float *box_lo = nullptr, *box_hi = nullptr; // [dd] enclosing box of the dataset (annEnclRect)
+    int n = 0, bs = 1, dd = 0;
+};
+
+struct KdTree {
+    int n = 0, dd = 0, bs = 1;
+    int *d_pos = nullptr, *d_pidx = nullptr, *d_cd = nullptr;
+    float *d_cv = nullptr, *d_lo = nullptr, *d_hi = nullptr, *d_box = nullptr;  // d_box: [2][dd]
+    double build_ms = 0.0;
+    int levels = 0;
+    KdOrder view() const;
+};
+
+// Builds the tree of d_rows[n][dd] (fp32, HBM) exactly as ANN's kd_tree constructor does; synchronous.
+KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t stream);
+void kd_tree_destroy(KdTree *t);
+// leaf position of every point (host copy), for tests
+int kd_tree_positions(const KdTree *t, int32_t *pos);
+
+// After a search wrote idx/err [nq][k] (ascending, ties in kd order): check ANN's box pruning along every
+// result's path; a query whose result the check cannot vouch for is searched again by an exact replay of
+// annkSearch.  maps (k == 1): tilemap items are rewritten for replayed queries.
+struct KdFixArgs {
+    const float *rows, *q;
+    int nq, k;
+    int *idx;
+    float *err;
+    const int32_t *tr_tile = nullptr, *tr_pal = nullptr;
+    const uint8_t *tr_attr = nullptr;
+    int32_t *m_tile = nullptr, *m_pal = nullptr;
+    uint8_t *m_hm = nullptr, *m_vm = nullptr;
+    int *list = nullptr, *count = nullptr;  // scratch: [nq], [1]
+};
+int kd_verify_and_replay(const KdTree *t, const KdFixArgs &a, hipStream_t stream);
+
+}  // namespace tiler

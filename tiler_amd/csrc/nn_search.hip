@@ -24,6 +24,7 @@
 #include <algorithm>
 
 #include "nn_search.hpp"
+#include "kdorder_dev.hpp"
 #include "nn_dev.hpp"
 #include "orbit.hpp"
 #include "psyv.hpp"
@@ -583,6 +584,7 @@ struct RescoreArgs {
     const uint8_t *tr_attr;
     int32_t *m_tile, *m_pal;
     uint8_t *m_hm, *m_vm;
+    KdOrder ko;          // tie order: ANN's kd-tree first-found (ko.pos set) or the lowest index
 };
 
 __device__ __forceinline__ void write_map(const RescoreArgs &a, long q, int best) {
@@ -671,12 +673,13 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
         }
         return;
     }
-    // top-k by (dist, idx)
+    // top-k by (dist, tie order)
+    const float *qrow = a.q + q * a.d;
     bool taken = false;
     for (int r = 0; r < a.k; r++) {
         float mv = taken ? INFINITY : dist;
         int mi = taken ? 0x7fffffff : di;
-        wave_argmin(mv, mi);
+        kd_argmin<64>(a.ko, qrow, mv, mi);
         if (!taken && di == mi && mi != 0x7fffffff) taken = true;
         if (lane == 0) {
             const bool ok = mi != 0x7fffffff;
@@ -709,12 +712,13 @@ __global__ __launch_bounds__(256) void nn_rescore2_kernel(RescoreArgs a) {
             bd[i] = INFINITY;
             bi[i] = 0x7fffffff;
         }
+        const float *qrow = a.q + q * a.d;
         for (int e = lane; e < n; e += 64) {
             const int idx = a.cbuf[j * a.cap + e];
-            const float dist = exact_dist(a.q + q * a.d, a.rows + (long)idx * a.d, a.d);
-            if (!lex_less(dist, idx, bd[7], bi[7])) continue;
-            int p = 7;  // lexicographic insertion (entries arrive in no particular order)
-            while (p > 0 && lex_less(dist, idx, bd[p - 1], bi[p - 1])) {
+            const float dist = exact_dist(qrow, a.rows + (long)idx * a.d, a.d);
+            if (!kd_less(a.ko, qrow, dist, idx, bd[7], bi[7])) continue;
+            int p = 7;  // (dist, tie order) insertion (entries arrive in no particular order)
+            while (p > 0 && kd_less(a.ko, qrow, dist, idx, bd[p - 1], bi[p - 1])) {
                 bd[p] = bd[p - 1];
                 bi[p] = bi[p - 1];
                 p--;
@@ -734,7 +738,7 @@ __global__ __launch_bounds__(256) void nn_rescore2_kernel(RescoreArgs a) {
                 }
             float mv = hv;
             int mi = hi;
-            wave_argmin(mv, mi);
+            kd_argmin<64>(a.ko, qrow, mv, mi);
             if (hi == mi && mi != 0x7fffffff) ptr++;
             if (lane == 0) {
                 const bool ok = mi != 0x7fffffff;
@@ -780,8 +784,19 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(RescoreArgs a, int list_n
                 if (dist > lim) break;
             }
             if (i < a.d) continue;
-            if (cnt == K && !(dist < bd[K - 1])) continue;  // equal keeps the earlier index
-            list_insert<K>(bd, bi, dist, j);
+            if (cnt == K && !kd_less(a.ko, sq, dist, j, bd[K - 1], bi[K - 1])) continue;
+            if (!a.ko.pos) {
+                list_insert<K>(bd, bi, dist, j);  // j ascends: an equal key stays behind, as index order wants
+            } else {
+                int p = (cnt < K) ? cnt : K - 1;
+                while (p > 0 && kd_less(a.ko, sq, dist, j, bd[p - 1], bi[p - 1])) {
+                    bd[p] = bd[p - 1];
+                    bi[p] = bi[p - 1];
+                    p--;
+                }
+                bd[p] = dist;
+                bi[p] = j;
+            }
             if (cnt < K) cnt++;
         }
 #pragma unroll
@@ -802,7 +817,7 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(RescoreArgs a, int list_n
                     if (ptr[t] < K) {
                         const float v = sd[th * K + ptr[t]];
                         const int ii = si[th * K + ptr[t]];
-                        if (v < lv || (v == lv && (unsigned)ii < (unsigned)li)) {
+                        if (kd_less(a.ko, sq, v, ii, lv, li)) {
                             lv = v;
                             li = ii;
                             lt = t;
@@ -811,7 +826,7 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(RescoreArgs a, int list_n
                 }
                 float mv = lv;
                 int mi = li;
-                wave_argmin(mv, mi);
+                kd_argmin<64>(a.ko, sq, mv, mi);
                 if (lt >= 0 && li == mi && mi != 0x7fffffff) ptr[lt]++;
                 if (tid == 0) {
                     const bool ok = mi != 0x7fffffff;
@@ -836,11 +851,20 @@ static int pick_S(int d) {
     return 0;  // exact kernel only
 }
 
-NNIndex *nn_index_create_dev(float *d_rows, int n, int d, hipStream_t stream) {
+NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hipStream_t stream) {
     NNIndex *ix = new NNIndex();
     ix->n = n;
     ix->d = d;
     ix->d_rows = d_rows;
+    ix->bs = std::max(1, bs);
+    ix->split = split;
+    if (split == KD_SPLIT_STD && n > 0) {  // the reference's tree (main.pas:3779,3961): ANN's tie order
+        ix->kd = kd_tree_build(d_rows, n, d, ix->bs, stream);
+        if (!ix->kd) {
+            nn_index_destroy(ix);
+            return nullptr;
+        }
+    }
     ix->S = pick_S(d);
     ix->nblk = (n + 31) / 32;
     TILER_HIP_CHECK_NULL(hipHostMalloc((void **)&ix->h_fb_count, sizeof(int) * 2, hipHostMallocDefault));
@@ -913,6 +937,7 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, hipStream_t stream) {
 void nn_index_destroy(NNIndex *ix) {
     if (!ix) return;
     orbit_destroy(ix->orbit);
+    kd_tree_destroy(ix->kd);
     hipFree(ix->d_rows);
     hipFree(ix->d_frag);
     hipFree(ix->d_nc);
@@ -935,6 +960,8 @@ void nn_index_destroy(NNIndex *ix) {
     hipFree(s.ex_list);
     hipFree(s.ccnt);
     hipFree(s.cbuf);
+    hipFree(s.kd_list);
+    hipFree(s.kd_count);
     hipHostFree(ix->h_fb_count);
     delete ix;
 }
@@ -952,6 +979,7 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         hipFree(s.fb_count);
         hipFree(s.thr);
         hipFree(s.ex_list);
+        hipFree(s.kd_list);
         const long nqblk = (nq + 31) / 32 + 2;
         TILER_HIP_CHECK(hipMalloc(&s.qfrag, (size_t)nqblk * 16 * 64 * 16));
         TILER_HIP_CHECK(hipMalloc(&s.qfrag16, (size_t)((nq + 15) / 16 + 2) * 8 * 64 * 16));
@@ -960,8 +988,10 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         TILER_HIP_CHECK(hipMalloc((void **)&s.fb_count, 16));
         TILER_HIP_CHECK(hipMalloc((void **)&s.thr, (size_t)nq * sizeof(float)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.ex_list, (size_t)nq * sizeof(int)));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.kd_list, (size_t)nq * sizeof(int)));
         s.cap_q = nq;
     }
+    if (!s.kd_count) TILER_HIP_CHECK(hipMalloc((void **)&s.kd_count, 16));
     if (!s.ccnt) {
         TILER_HIP_CHECK(hipMalloc((void **)&s.ccnt, (size_t)TIER2_MAX * sizeof(int)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.cbuf, (size_t)TIER2_MAX * TIER2_CAP * sizeof(int)));
@@ -991,6 +1021,7 @@ static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream
 // one box): "q16" (default): nn_shortlist16_kernel, 16x16x32 MFMA, L16 = 4 (51.6 ms); "q16l6": L16 = 6
 // (53.4 ms, fewer tier-2 queries); "w8": nn_shortlist_kernel, 32x32x16, 8 waves x 2 query blocks (63.9 ms)
 static int shortlist_variant() {
+#ifdef TILER_EXPERIMENTS
     static int v = [] {
         const char *e = getenv("TILER_SHORTLIST");
         if (e && !strcmp(e, "w8")) return 8;
@@ -998,6 +1029,9 @@ static int shortlist_variant() {
         return 16;
     }();
     return v;
+#else
+    return 16;  // the shipped library: q16 only
+#endif
 }
 
 // 16x16x32 shortlist for D = 161..192 float datasets: TILER_SHORTLIST=q16 (L16 = 4) / q16l6 (L16 = 6);
@@ -1086,6 +1120,7 @@ static int launch_exact(RescoreArgs ra, int list_n, int grid, hipStream_t stream
 }
 
 static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream);
+static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream);
 
 int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
                   hipStream_t stream) {
@@ -1108,6 +1143,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     ra.max_abs_c = ix->max_abs;
     ra.out_idx = d_idx;
     ra.out_err = d_err;
+    if (ix->kd) ra.ko = ix->kd->view();
     if (maps && k == 1 && ix->d_tr_tile) {
         ra.tr_tile = ix->d_tr_tile;
         ra.tr_pal = ix->d_tr_pal;
@@ -1118,6 +1154,25 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         ra.m_vm = maps->vm;
     }
     ix->last_queries = nq;
+    if (search_core(ix, ra, d_q, nq, k, stream)) return -1;
+    if (!ix->kd) return 0;
+    // ANN's box pruning along every result's path; the rare query it cannot vouch for is replayed exactly
+    SearchScratch &s = ix->scratch;
+    if (ensure_scratch(ix, nq, 0)) return -1;
+    KdFixArgs fa{ix->d_rows, d_q, nq, k, d_idx, d_err};
+    fa.tr_tile = ra.tr_tile;
+    fa.tr_pal = ra.tr_pal;
+    fa.tr_attr = ra.tr_attr;
+    fa.m_tile = ra.m_tile;
+    fa.m_pal = ra.m_pal;
+    fa.m_hm = ra.m_hm;
+    fa.m_vm = ra.m_vm;
+    fa.list = s.kd_list;
+    fa.count = s.kd_count;
+    return kd_verify_and_replay(ix->kd, fa, stream);
+}
+
+static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream) {
     const bool mfma = ix->S > 0 && k <= 8;
     if (!mfma) {
         ix->last_splits = 0;
@@ -1157,8 +1212,8 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         t.ex_count = s.fb_count + 1;
         t.fb_max = TIER2_MAX;
         t.thr = s.thr;
-        t.out_idx = d_idx;
-        t.out_err = d_err;
+        t.out_idx = ra.out_idx;
+        t.out_err = ra.out_err;
         t.tr_tile = ra.tr_tile;
         t.tr_pal = ra.tr_pal;
         t.tr_attr = ra.tr_attr;
@@ -1166,6 +1221,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         t.m_pal = ra.m_pal;
         t.m_hm = ra.m_hm;
         t.m_vm = ra.m_vm;
+        t.ko = ra.ko;
         if (orbit_search(ix, d_q, nq, t, stream)) return -1;
         ix->last_orbit = 1;
         ra.qstat = s.qstat;
@@ -1197,9 +1253,12 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
                                dim3(256), 0, stream, p16);
         }
         TILER_HIP_CHECK(hipGetLastError());
+#ifdef TILER_EXPERIMENTS
         if (v16 == 6) {
             if (launch_shortlist16<6, 6>(ix, nq, nsplit, bps, stream)) return -1;
-        } else {
+        } else
+#endif
+        {
             if (launch_shortlist16<6, 4>(ix, nq, nsplit, bps, stream)) return -1;
         }
     } else if (dispatch_shortlist<8>(ix, nq, nsplit, bps, stream)) {

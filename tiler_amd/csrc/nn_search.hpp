@@ -3,6 +3,7 @@
 #include <mutex>
 #include <vector>
 
+#include "kdtree.hpp"
 #include "tiler_common.hpp"
 
 namespace tiler {
@@ -42,6 +43,8 @@ struct SearchScratch {
     int *ex_list = nullptr;   // tier-3 list [nq]
     int *ccnt = nullptr;      // tier-2 collect counts
     int *cbuf = nullptr;      // tier-2 collect buffers
+    int *kd_list = nullptr;   // [nq] queries the ANN pruning check sends to the exact replay
+    int *kd_count = nullptr;  // [1]
     size_t cap_q = 0, cap_keys = 0, cap_rows = 0;
 };
 
@@ -67,11 +70,14 @@ struct NNIndex {
     int last_splits = 0;
     int last_orbit = 0;         // 1: the last search ran the mirror-orbit path
     OrbitIndex *orbit = nullptr; // mirror-orbit index (orbit.hip), null when not applicable
+    KdTree *kd = nullptr;       // KD_SPLIT_STD tree: ties resolve in ANN's first-found order (null: lowest index)
+    int bs = 1, split = KD_SPLIT_STD;
     int *h_fb_count = nullptr;  // pinned
 };
 
-// build the device index from fp32 rows already in HBM (takes ownership of d_rows)
-NNIndex *nn_index_create_dev(float *d_rows, int n, int d, hipStream_t stream);
+// build the device index from fp32 rows already in HBM (takes ownership of d_rows); split = KD_SPLIT_STD builds
+// ANN's kd-tree with bucket size bs for the tie order, TILER_SPLIT_INDEX_ORDER resolves ties to the lowest index
+NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hipStream_t stream);
 void nn_index_destroy(NNIndex *ix);
 
 struct FtMaps {

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "kdorder_dev.hpp"
 #include "nn_dev.hpp"
 #include "orbit.hpp"
 
@@ -209,24 +210,35 @@ __global__ __launch_bounds__(256) void orbit_eq_kernel(const float *__restrict__
 // Members of a group whose rows are identical (a symmetric tile: S_m c == c) have identical exact distances to
 // any query; the rescore keeps only the lowest candidate index of each identical set (the tie rule picks it
 // anyway).  Bit x of dup[g] marks slot x as such a duplicate.  One wave per group.
+// rep[g] holds, in 2 bits per slot, the slot of the lowest-index member with the same row (the slot itself if
+// none): under ANN's tie order (kdorder_dev.hpp) the rescore picks the first-found member of each such set.
 __global__ __launch_bounds__(256) void orbit_dup_kernel(const float *__restrict__ rows, const int *__restrict__ member,
-                                                        long G, uint8_t *__restrict__ dup) {
+                                                        long G, uint8_t *__restrict__ dup, uint8_t *__restrict__ rep) {
     const int lane = threadIdx.x & 63;
     for (long g = (long)blockIdx.x * 4 + (threadIdx.x >> 6); g < G; g += (long)gridDim.x * 4) {
         int mem[4];
 #pragma unroll
         for (int x = 0; x < 4; x++) mem[x] = member[g * 4 + x];
-        unsigned bits = 0;
+        unsigned bits = 0, reps = 0;
 #pragma unroll
-        for (int x = 1; x < 4; x++)
+        for (int x = 0; x < 4; x++) {
+            int r = x;
 #pragma unroll
             for (int y = 0; y < 4; y++) {
                 if (y == x || mem[x] < 0 || mem[y] < 0 || mem[y] > mem[x]) continue;
                 bool eq = true;
                 for (int i = lane; i < OD; i += 64) eq &= rows[(long)mem[x] * OD + i] == rows[(long)mem[y] * OD + i];
-                if (__all(eq)) bits |= 1u << x;
+                if (__all(eq)) {
+                    bits |= 1u << x;
+                    if (mem[y] < mem[r]) r = y;
+                }
             }
-        if (lane == 0) dup[g] = (uint8_t)bits;
+            reps |= (unsigned)r << (2 * x);
+        }
+        if (lane == 0) {
+            dup[g] = (uint8_t)bits;
+            rep[g] = (uint8_t)reps;
+        }
     }
 }
 
@@ -797,6 +809,7 @@ struct OrbitRescoreArgs {
     const float *nc;                // [G]
     const int *member;              // [G][4]
     const uint8_t *dup;             // [G] bit x: slot x repeats a lower-index member's row
+    const uint8_t *rep;             // [G] 2 bits per slot: slot of the lowest-index copy of its row
     const OrbitStat *ostat;
     const float *key;
     const int *id;
@@ -869,9 +882,17 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
     d = (x & 2) ? (o - d) : (d + o);
     key = INFINITY;
     if (!gv) return -1;
-    const int cand = a.member[(long)g * 4 + x];
+    int cand = a.member[(long)g * 4 + x];
     if (cand < 0 || ((a.dup[g] >> x) & 1)) return -1;
     key = (double)a.nc[g] - 2.0 * (double)d;
+    if (a.t.ko.pos && a.dup[g]) {  // identical rows of this slot's set: the one ANN finds first stands for them
+        const unsigned rep = a.rep[g];
+        const float *qr = a.q + q * OD;
+        for (int y = 0; y < 4; y++) {
+            const int cy = a.member[(long)g * 4 + y];
+            if (y != x && cy >= 0 && (int)((rep >> (2 * y)) & 3) == x && kd_before(a.t.ko, qr, cy, cand)) cand = cy;
+        }
+    }
     return cand;
 }
 
@@ -1008,7 +1029,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
                     tt = x.z - y.z; dist = dist + tt * tt;
                     tt = x.w - y.w; dist = dist + tt * tt;
                 }
-                if (lex_less(dist, c, bd, bi)) {
+                if (kd_less(t.ko, qrow, dist, c, bd, bi)) {
                     bd = dist;
                     bi = c;
                 }
@@ -1057,7 +1078,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
         return;
     }
     flush();
-    half_argmin(bd, bi);
+    kd_argmin<32>(t.ko, qrow, bd, bi);
     if (l == 0) {
         if (t.n_expand) {
             atomicAdd(t.n_expand, nexp);
@@ -1095,16 +1116,9 @@ __global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a)
         bd = exact_dist192_lean(a.q + q * OD, a.rows + (long)c * OD);
         bi = c;
     }
-#pragma unroll
-    for (int o = ORB_PSLOTS / 2; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(bd, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        const bool take = (ov < bd) || (ov == bd && (unsigned)oi < (unsigned)bi);
-        bd = take ? ov : bd;
-        bi = take ? oi : bi;
-    }
+    const OrbitTail &t = a.t;
+    kd_argmin<ORB_PSLOTS>(t.ko, a.q + q * OD, bd, bi);
     if (s == 0) {
-        const OrbitTail &t = a.t;
         t.out_idx[q] = bi;
         t.out_err[q] = bd;
         if (t.m_tile) {
@@ -1136,7 +1150,7 @@ __global__ __launch_bounds__(256) void orbit_fbprep_kernel(OrbitFbArgs a) {
     const int count = min(*a.fb_count, a.fb_max);
     for (int j = blockIdx.x * 4 + (threadIdx.x >> 6); j < count; j += gridDim.x * 4) {
         const long qq = a.fb_list[j];
-        double n2 = 0, sh = 0, se = 0;
+        double sh = 0, se = 0;
         if (lane < 2 * OS) {  // lane = (k-step s, half h)
             const int s = lane >> 1, h = lane & 1;
             half8 hv;
@@ -1147,7 +1161,6 @@ __global__ __launch_bounds__(256) void orbit_fbprep_kernel(OrbitFbArgs a) {
                 if (fabsf((float)vh) < 6.103515625e-05f) vh = (_Float16)0.0f;  // as prep_rows_kernel
                 hv[jj] = vh;
                 const double dv = vs, dh = (double)(float)vh;
-                n2 += dv * dv;
                 sh += dh * dh;
                 se += (dv - dh) * (dv - dh);
             }
@@ -1187,6 +1200,7 @@ void orbit_destroy(OrbitIndex *o) {
     hipFree(o->d_nc);
     hipFree(o->d_member);
     hipFree(o->d_dup);
+    hipFree(o->d_rep);
     hipFree(o->d_map);
     hipFree(o->qfrag);
     hipFree(o->qrowh);
@@ -1201,11 +1215,15 @@ void orbit_destroy(OrbitIndex *o) {
 }
 
 static int orbit_enabled() {
+#ifdef TILER_EXPERIMENTS
     static int v = [] {
-        const char *e = getenv("TILER_ORBIT");
+        const char *e = getenv("TILER_ORBIT");  // 0: generic kernels only (A/B reference)
         return (e && e[0] == '0') ? 0 : 1;
     }();
     return v;
+#else
+    return 1;
+#endif
 }
 
 int orbit_build(NNIndex *ix, hipStream_t stream) {
@@ -1266,8 +1284,9 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     TILER_HIP_CHECK(hipMalloc((void **)&o->d_member, G * 4 * sizeof(int)));
     TILER_HIP_CHECK(hipMemcpyAsync(o->d_member, member.data(), G * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
     TILER_HIP_CHECK(hipMalloc((void **)&o->d_dup, G));
+    TILER_HIP_CHECK(hipMalloc((void **)&o->d_rep, G));
     hipLaunchKernelGGL(orbit_dup_kernel, dim3((unsigned)std::min<long>(8192, (G + 3) / 4)), dim3(256), 0, stream,
-                       ix->d_rows, o->d_member, G, o->d_dup);
+                       ix->d_rows, o->d_member, G, o->d_dup, o->d_rep);
     TILER_HIP_CHECK(hipGetLastError());
     TILER_HIP_CHECK(hipMalloc(&o->d_frag, (size_t)o->gblk * OS * 1024));
     TILER_HIP_CHECK(hipMalloc(&o->d_rowh, (size_t)G * OD * 2));
@@ -1301,12 +1320,14 @@ static constexpr int ORB_L = 4, ORB_CB = 4, ORB_NW = 8;
 int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, hipStream_t stream) {
     OrbitIndex *o = ix->orbit;
     const int nqblk = (nq + 31) / 32;
+#ifdef TILER_EXPERIMENTS
+    // experiment build only (make EXPERIMENTS=1): shortlist variants and timing modes (MODE / PMODE: results invalid)
     static const int qb = [] {
         const char *e = getenv("TILER_ORBIT_QB");  // query blocks of 32 per wave: 2 (default) or 1
         return (e && e[0] == '1') ? 1 : 2;
     }();
     static const int nw = [] {
-        const char *e = getenv("TILER_ORBIT_NW");  // experiment: 12 waves x 1 query block (3 waves/SIMD)
+        const char *e = getenv("TILER_ORBIT_NW");  // 12 waves x 1 query block (3 waves/SIMD)
         return (e && atoi(e) == 12) ? 12 : ORB_NW;
     }();
     static const int mode = [] {
@@ -1318,9 +1339,12 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         return (e && e[0] == '0') ? 0 : 1;
     }();
     static const int pmode = [] {
-        const char *e = getenv("TILER_ORBIT_PMODE");  // pipelined kernel timing experiments (results invalid):
-        return e ? atoi(e) : 0;                        // 1 no list updates, 2 MFMA + loads only
+        const char *e = getenv("TILER_ORBIT_PMODE");  // 1 no list updates, 2 MFMA + loads only (results invalid)
+        return e ? atoi(e) : 0;
     }();
+#else
+    constexpr int qb = 2, nw = ORB_NW, mode = 0, pipe = 1, pmode = 0;
+#endif
     const bool use_pipe = pipe && qb == 2 && mode == 0 && nw == ORB_NW;
     const int wgs = (nqblk + nw * qb - 1) / (nw * qb);
     const int max_split = 32 / (2 * ORB_L);  // rescore: one list entry per lane of a half-wave
@@ -1362,13 +1386,14 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     {
         const size_t lds = 2 * ((size_t)ORB_CB * OS * 1024 + ORB_CB * 128);
         KTimer tm("nn_orbit", stream);
-#define ORB_LAUNCH(NWV, QB, MD)                                                                                   \
-    hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, NWV, QB, MD>), dim3(wgs, nsplit),                  \
-                       dim3(NWV * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
-                       (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id)
 #define ORB_PIPE(MD)                                                                                              \
     hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, MD>), dim3(wgs, nsplit),              \
                        dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
+                       (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id)
+#ifdef TILER_EXPERIMENTS
+#define ORB_LAUNCH(NWV, QB, MD)                                                                                   \
+    hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, NWV, QB, MD>), dim3(wgs, nsplit),                  \
+                       dim3(NWV * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
                        (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id)
         if (use_pipe && pmode == 1)
             ORB_PIPE(1);
@@ -1387,6 +1412,11 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         else
             ORB_LAUNCH(8, 2, 0);
 #undef ORB_LAUNCH
+#else
+        (void)use_pipe;
+        (void)pmode;
+        ORB_PIPE(0);
+#endif
 #undef ORB_PIPE
     }
     TILER_HIP_CHECK(hipGetLastError());
@@ -1398,6 +1428,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.nc = o->d_nc;
     ra.member = o->d_member;
     ra.dup = o->d_dup;
+    ra.rep = o->d_rep;
     ra.ostat = o->qstat;
     ra.key = o->key;
     ra.id = o->id;
@@ -1405,11 +1436,15 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.nq = nq;
     ra.L = ORB_L;
     ra.nsplit = nsplit;
+#ifdef TILER_EXPERIMENTS
     static const int p1 = [] {
         const char *e = getenv("TILER_ORBIT_P1");
         const int v = e ? atoi(e) : 2;
         return v < 1 ? 1 : v > 2 ? 2 : v;
     }();
+#else
+    constexpr int p1 = 2;
+#endif
     ra.p1 = p1;
     ra.pair_cnt = o->pair_cnt;
     ra.pair_cand = o->pair_cand;

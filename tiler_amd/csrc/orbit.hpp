@@ -33,6 +33,7 @@ struct OrbitIndex {
     float *d_nc = nullptr;        // [G] ||c||^2 (scaled, fp32)
     int *d_member = nullptr;      // [G][4] candidate index of relative mirror slot m (H = 1, V = 2), -1 absent
     uint8_t *d_dup = nullptr;     // [G] bit m: slot m's row repeats a lower-index member's (symmetric tiles)
+    uint8_t *d_rep = nullptr;     // [G] 2 bits per slot: the slot holding the lowest-index copy of its row
     void *d_map = nullptr;        // OrbitMap
     double N = 0, Np = 0, Hp = 0, Ecp = 0;  // max ||c||, ||c'||, ||fp16(c')||, ||c' - fp16(c')||
     // per-call scratch
@@ -62,6 +63,7 @@ struct OrbitTail {
     int32_t *m_tile, *m_pal;
     uint8_t *m_hm, *m_vm;
     int *n_expand;                // optional device counter of block expansions
+    KdOrder ko;                   // tie order (ANN's kd-tree first-found, or the lowest index)
 };
 
 // 0: orbit index built (ix->orbit), 1: dataset has no exploitable mirror structure, -1: HIP error

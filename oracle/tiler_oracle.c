@@ -729,14 +729,18 @@ void or_make_tiles_unique(int T, uint8_t *palpix, uint8_t *active, int32_t *use_
     }
     cmp_pp = palpix;
     qsort(lst, (size_t)n, sizeof(int), cmp_tiles);
+    /* DoOneMerge (main.pas:2562-2572) closes the group [firstSameIdx, i) at each key change; the final call
+     * runs with i := sortList.Count - 1 (main.pas:2604-2605), so the LAST group never includes its last
+     * sorted member (a 2-member last group does not merge at all): reproduced, not fixed. */
     int first = 0;
-    for (int i = 1; i <= n; i++) {
-        int same = (i < n) && memcmp(palpix + 64 * (size_t)lst[i - 1], palpix + 64 * (size_t)lst[i], 64) == 0;
-        if (!same) {
+    for (int i = 1; i < n; i++) {
+        if (memcmp(palpix + 64 * (size_t)lst[i - 1], palpix + 64 * (size_t)lst[i], 64) != 0) {
             if (i - first >= 2) merge_tiles(lst + first, i - first, lst[first], palpix, active, use_count, merge_index);
             first = i;
         }
     }
+    if (n > 0 && (n - 1) - first >= 2)
+        merge_tiles(lst + first, (n - 1) - first, lst[first], palpix, active, use_count, merge_index);
     free(lst);
 }
 

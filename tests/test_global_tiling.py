@@ -55,6 +55,49 @@ def test_make_unique_and_reindex_match_oracle(oracle):
     assert np.array_equal(idx, oidx)
 
 
+@pytest.mark.parametrize("n_last", [1, 2, 3, 4])
+def test_make_unique_last_group_quirk(oracle, n_last):
+    """MakeTilesUnique's final DoOneMerge runs with i := sortList.Count - 1 (main.pas:2604-2605): the run of
+    identical tiles that sorts LAST (CompareDWord order) never includes its last member.  Known answers:
+    a 2-member last run stays unmerged, a 3-member last run merges 2 of them; runs elsewhere merge fully."""
+    import ctypes
+    T = 6 + n_last
+    tiles = np.zeros((T, 64), np.uint8)
+    tiles[0] = tiles[1] = 3                    # a duplicate pair that does not sort last: always merged
+    tiles[2] = 1
+    tiles[3] = 2
+    tiles[4] = tiles[5] = 0                    # and one that sorts first
+    tiles[6:] = 15                             # the last run in CompareDWord order: 0x0F0F0F0F words
+    uc = np.arange(1, T + 1).astype(np.int32)
+    pp, act, ucn, mi = gt.make_tiles_unique(tiles, np.ones(T, np.uint8), uc)
+    assert act[1] == 0 and mi[1] == 0 and act[5] == 0 and mi[5] == 4
+    merged_last = max(0, n_last - 1) if n_last - 1 >= 2 else 0
+    want_inactive = merged_last - 1 if merged_last else 0  # members 7.. of the merged part
+    assert int(np.count_nonzero(act[6:] == 0)) == want_inactive
+    assert act[T - 1] == 1                      # the last sorted member is never merged
+    if n_last == 2:
+        assert act[6] == 1 and act[7] == 1 and ucn[6] == uc[6]
+    if n_last == 3:
+        assert act[7] == 0 and mi[7] == 6 and ucn[6] == uc[6] + uc[7] and act[8] == 1
+    opp, oact, ouc, omi = tiles.copy(), np.ones(T, np.uint8), uc.copy(), np.zeros(T, np.int32)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    oracle.lib().or_make_tiles_unique(T, p(opp), p(oact), p(ouc), p(omi))
+    assert np.array_equal(act, oact) and np.array_equal(ucn, ouc) and np.array_equal(mi, omi)
+    assert np.array_equal(pp, opp)
+
+
+def test_make_unique_dword_order(oracle):
+    """CompareTilePalPixels compares little-endian DWORDs, not bytes: the tile sorting last is the one with the
+    largest first dword (byte 3 most significant), which decides which run loses its last member."""
+    tiles = np.zeros((4, 64), np.uint8)
+    tiles[0, 0] = 9                            # dword 0 = 0x00000009
+    tiles[1, 0] = 9
+    tiles[2, 3] = 1                            # dword 0 = 0x01000000: sorts after 0x09 although byte 0 is 0
+    tiles[3, 3] = 1
+    pp, act, ucn, mi = gt.make_tiles_unique(tiles, np.ones(4, np.uint8), np.ones(4, np.int32))
+    assert act.tolist() == [1, 0, 1, 1]        # the 9-run merged; the last run (tiles 2, 3) did not
+
+
 @pytest.mark.gpu
 def test_global_tiling_kmodes_pass_bit_exact(gpu, oracle):
     rng = np.random.default_rng(3)

@@ -12,10 +12,13 @@ namespace tiler {
 // True iff candidate a is visited before candidate b by ANN's depth-first search for query q (near child
 // first: LO when q[cd] - cv < 0, ANNkd_split::ann_search).  Order of the visit over ALL leaves: at the two
 // candidates' lowest common node, the one in q's near child comes first; inside one bucket, position order
-// (ANNkd_leaf::ann_search scans bkt[] in order).  Without a tree: the lower index.  Invalid ids (< 0 or
-// >= n, e.g. the 0x7fffffff "none" sentinel) come after every valid one.
-__device__ __forceinline__ bool kd_before(const KdOrder &o, const float *__restrict__ q, int a, int b) {
-    if (!o.pos || (unsigned)a >= (unsigned)o.n || (unsigned)b >= (unsigned)o.n) return (unsigned)a < (unsigned)b;
+// (ANNkd_leaf::ann_search scans bkt[] in order).  op == nullptr (no tree): the lower index.  Invalid ids
+// (< 0 or >= n, e.g. the 0x7fffffff "none" sentinel) come after every valid one.  The view is read through
+// a pointer, and only here: search kernels carry 8 bytes of argument for it and touch it on exact ties only.
+static __device__ __attribute__((noinline)) bool kd_before_tree(const KdOrder *__restrict__ op, const float *__restrict__ q,
+                                                         int a, int b) {
+    const KdOrder &o = *op;
+    if ((unsigned)a >= (unsigned)o.n || (unsigned)b >= (unsigned)o.n) return (unsigned)a < (unsigned)b;
     int pa = o.pos[a], pb = o.pos[b];
     const bool sw = pa > pb;
     if (sw) {
@@ -38,15 +41,19 @@ __device__ __forceinline__ bool kd_before(const KdOrder &o, const float *__restr
     return !sw;
 }
 
+__device__ __forceinline__ bool kd_before(const KdOrder *op, const float *__restrict__ q, int a, int b) {
+    return op ? kd_before_tree(op, q, a, b) : (unsigned)a < (unsigned)b;
+}
+
 // (dist, kd order) lexicographic "less"
-__device__ __forceinline__ bool kd_less(const KdOrder &o, const float *__restrict__ q, float da, int a, float db,
+__device__ __forceinline__ bool kd_less(const KdOrder *op, const float *__restrict__ q, float da, int a, float db,
                                         int b) {
-    return da < db || (da == db && kd_before(o, q, a, b));
+    return da < db || (da == db && kd_before(op, q, a, b));
 }
 
 // (dist, kd order) minimum over lanes xor-reachable below `width` (64: the wave, 32: a half-wave, 4: a quad)
 template <int WIDTH>
-__device__ __forceinline__ void kd_argmin(const KdOrder &o, const float *__restrict__ q, float &v, int &i) {
+__device__ __forceinline__ void kd_argmin(const KdOrder *o, const float *__restrict__ q, float &v, int &i) {
 #pragma unroll
     for (int off = WIDTH / 2; off > 0; off >>= 1) {
         const float ov = __shfl_xor(v, off, 64);
@@ -97,6 +104,56 @@ __device__ __forceinline__ float kd_path_far_box(const KdOrder &o, const float *
             s = m;
     }
     return worst;
+}
+
+// The same check for ONE candidate by the 4 lanes of a quad (lane s = 0..3 of the quad, quad-uniform p): lane s
+// loads the path levels l = s mod 4 (the q row is cache-hot in the pair pass that calls this), lane 0 of the quad
+// adds the far-child terms in path order exactly as ANN does.  Returns, on every lane of the quad, whether every
+// far-child box distance on p's path is <= D (k = 1: the winner's own distance; see kd_verify_kernel).
+__device__ __forceinline__ bool kd_quad_path_ok(const KdOrder *__restrict__ op, const float *__restrict__ q, int p,
+                                                float root_box, float D, int s) {
+    const KdOrder &o = *op;
+    float term[8];
+    unsigned farm = 0;  // bit l: level l is a far step
+#pragma unroll
+    for (int i = 0; i < 8; i++) term[i] = 0.0f;
+    int S = 0, E = o.n;
+#pragma unroll
+    for (int l = 0; l < 32; l++) {
+        if (E - S > o.bs) {
+            const int m = S + ((E - S) >> 1);
+            const bool in_lo = p < m;
+            if ((l & 3) == s) {
+                const float qd = q[o.cd[m]];
+                const float cut_diff = qd - o.cv[m];
+                const bool lo_first = cut_diff < 0.0f;
+                if (in_lo != lo_first) {
+                    float box_diff = lo_first ? o.lo[m] - qd : qd - o.hi[m];
+                    if (box_diff < 0.0f) box_diff = 0.0f;
+                    term[l >> 2] = cut_diff * cut_diff - box_diff * box_diff;
+                    farm |= 1u << l;
+                }
+            }
+            if (in_lo)
+                E = m;
+            else
+                S = m;
+        }
+    }
+    const int qbase = (threadIdx.x & 63) & ~3;
+    farm |= __shfl_xor(farm, 1, 64);
+    farm |= __shfl_xor(farm, 2, 64);
+    float box = root_box;
+    bool ok = true;
+#pragma unroll
+    for (int l = 0; l < 32; l++) {
+        const float t = __shfl(term[l >> 2], qbase + (l & 3), 64);
+        if ((farm >> l) & 1) {
+            box = box + t;
+            ok = ok && box <= D;
+        }
+    }
+    return ok;
 }
 
 }  // namespace tiler

@@ -2,12 +2,14 @@
 // that make the MFMA search return ANN's own answer among equal distances (kdtree.hpp).
 //
 // Build, level by level (every node of a level at once):
-//   kd_spread_kernel   one wave per chunk of <= KD_CH points of a node: per-dimension min / max (annSpread)
-//   kd_select_kernel   one wave per node: reduce the chunks, spread = max - min (fp32), cut_dim = first maximum
-//                      (annMaxSpread), gather the node's cut-dimension keys in pidx order
+//   big nodes (> KD_CH points): kd_spread_big_kernel, one wave per KD_CH-point chunk, per-dimension min / max
+//                      (annSpread) folded into the node with order-preserving integer atomics; kd_select_big_kernel
+//                      picks cut_dim = first maximum of max - min (fp32, annMaxSpread); kd_gather_kernel writes
+//                      the node's cut-dimension keys in pidx order, one wave per chunk
+//   small nodes:       kd_small_kernel, one wave per node does all three
 //   (host)             annMedianSplit's quickselect on each node's (key, index) pairs, bit for bit: the
 //                      permutation it leaves decides which of several equal keys go LO, and so the rest of the
-//                      tree; nodes of a level run on a host thread pool (the level's work is O(n))
+//                      tree; the nodes of a level run on a persistent host thread pool (a level is O(n) work)
 // The rows never leave HBM: per level only the n keys (4 B each) come to the host and the new order goes back.
 #include <float.h>
 #include <math.h>
@@ -16,6 +18,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -24,76 +29,111 @@
 
 namespace tiler {
 
-static constexpr int KD_CH = 2048;  // points per spread chunk
+static constexpr int KD_CH = 512;  // points per spread chunk of a big node
 
 struct KdChunk {
-    int node, s, e;
+    int node, s, e;  // big-node index, positions [s, e)
 };
 
-// per-dimension min / max of pidx[s..e) (annSpread's loop: first value, then < min / > max)
-__global__ __launch_bounds__(256) void kd_spread_kernel(const float *__restrict__ rows, int dd,
-                                                        const int *__restrict__ pidx, const KdChunk *__restrict__ ch,
-                                                        int nch, float *__restrict__ pmin, float *__restrict__ pmax) {
+struct KdNodeDev {
+    int s, e;
+};
+
+// order-preserving float <-> uint32 (min / max of the encodings = encodings of the min / max)
+__device__ __forceinline__ unsigned f2o(float f) {
+    const unsigned b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float o2f(unsigned o) { return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o); }
+
+// min / max of pidx[s..e) along dims d0 + lane + 64 j (j < 4), rows read 4 at a time (independent loads)
+__device__ __forceinline__ void kd_minmax(const float *__restrict__ rows, int dd, const int *__restrict__ pidx, int s,
+                                          int e, int d0, float (&mn)[4], float (&mx)[4]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        mn[j] = INFINITY;
+        mx[j] = -INFINITY;
+    }
+    int i = s;
+    for (; i + 4 <= e; i += 4) {
+        const float *r[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) r[u] = rows + (long)pidx[i + u] * dd;
+        float v[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int d = d0 + j * 64 + lane;
+                v[u][j] = d < dd ? r[u][d] : 0.0f;
+            }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                mn[j] = fminf(mn[j], v[u][j]);
+                mx[j] = fmaxf(mx[j], v[u][j]);
+            }
+    }
+    for (; i < e; i++) {
+        const float *r = rows + (long)pidx[i] * dd;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int d = d0 + j * 64 + lane;
+            const float v = d < dd ? r[d] : 0.0f;
+            mn[j] = fminf(mn[j], v);
+            mx[j] = fmaxf(mx[j], v);
+        }
+    }
+}
+
+// wave argmax of (spread, -dim): annMaxSpread's first maximum; an all-zero spread picks dimension 0
+__device__ __forceinline__ int kd_first_max(float best, int bd) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int od = __shfl_xor(bd, o, 64);
+        if (ob > best || (ob == best && od < bd)) {
+            best = ob;
+            bd = od;
+        }
+    }
+    return best > 0.0f ? bd : 0;
+}
+
+__global__ __launch_bounds__(256) void kd_spread_big_kernel(const float *__restrict__ rows, int dd,
+                                                            const int *__restrict__ pidx,
+                                                            const KdChunk *__restrict__ ch, int nch,
+                                                            unsigned *__restrict__ omin, unsigned *__restrict__ omax) {
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= nch) return;
     const KdChunk k = ch[c];
     for (int d0 = 0; d0 < dd; d0 += 256) {
         float mn[4], mx[4];
-        {
-            const float *r = rows + (long)pidx[k.s] * dd;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int d = d0 + j * 64 + lane;
-                mn[j] = mx[j] = d < dd ? r[d] : 0.0f;
-            }
-        }
-        for (int i = k.s + 1; i < k.e; i++) {
-            const float *r = rows + (long)pidx[i] * dd;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int d = d0 + j * 64 + lane;
-                const float v = d < dd ? r[d] : 0.0f;
-                if (v < mn[j])
-                    mn[j] = v;
-                else if (v > mx[j])
-                    mx[j] = v;
-            }
-        }
+        kd_minmax(rows, dd, pidx, k.s, k.e, d0, mn, mx);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int d = d0 + j * 64 + lane;
             if (d < dd) {
-                pmin[(long)c * dd + d] = mn[j];
-                pmax[(long)c * dd + d] = mx[j];
+                atomicMin(&omin[(long)k.node * dd + d], f2o(mn[j]));
+                atomicMax(&omax[(long)k.node * dd + d], f2o(mx[j]));
             }
         }
     }
 }
 
-struct KdNodeDev {
-    int s, e, c0, c1;  // positions [s, e), chunks [c0, c1)
-};
-
-// one wave per node: cut_dim = first dimension of maximum spread; keys[i] = rows[pidx[i]][cut_dim] for i in [s, e)
-__global__ __launch_bounds__(256) void kd_select_kernel(const float *__restrict__ rows, int dd,
-                                                        const int *__restrict__ pidx,
-                                                        const KdNodeDev *__restrict__ nodes, int nn,
-                                                        const float *__restrict__ pmin, const float *__restrict__ pmax,
-                                                        int *__restrict__ cut_dim, float *__restrict__ keys,
-                                                        float *__restrict__ box) {
+// one wave per big node: the cut dimension (also the root box when box != null)
+__global__ __launch_bounds__(256) void kd_select_big_kernel(int dd, int nbig, const unsigned *__restrict__ omin,
+                                                            const unsigned *__restrict__ omax, int *__restrict__ cut_dim,
+                                                            float *__restrict__ box) {
     const int lane = threadIdx.x & 63;
     const int nd = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (nd >= nn) return;
-    const KdNodeDev N = nodes[nd];
+    if (nd >= nbig) return;
     float best = -INFINITY;
     int bd = 0x7fffffff;
     for (int d = lane; d < dd; d += 64) {
-        float mn = pmin[(long)N.c0 * dd + d], mx = pmax[(long)N.c0 * dd + d];
-        for (int c = N.c0 + 1; c < N.c1; c++) {
-            mn = fminf(mn, pmin[(long)c * dd + d]);
-            mx = fmaxf(mx, pmax[(long)c * dd + d]);
-        }
+        const float mn = o2f(omin[(long)nd * dd + d]), mx = o2f(omax[(long)nd * dd + d]);
         if (box) {  // the root node: annEnclRect
             box[d] = mn;
             box[dd + d] = mx;
@@ -104,16 +144,55 @@ __global__ __launch_bounds__(256) void kd_select_kernel(const float *__restrict_
             bd = d;
         }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        const float ob = __shfl_xor(best, o, 64);
-        const int od = __shfl_xor(bd, o, 64);
-        if (ob > best || (ob == best && od < bd)) {
-            best = ob;
-            bd = od;
+    const int cd = kd_first_max(best, bd);
+    if (lane == 0) cut_dim[nd] = cd;
+}
+
+// keys[i] = rows[pidx[i]][cut_dim of the chunk's node], one wave per chunk
+__global__ __launch_bounds__(256) void kd_gather_kernel(const float *__restrict__ rows, int dd,
+                                                        const int *__restrict__ pidx, const KdChunk *__restrict__ ch,
+                                                        int nch, const int *__restrict__ cut_dim,
+                                                        float *__restrict__ keys) {
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= nch) return;
+    const KdChunk k = ch[c];
+    const int cd = cut_dim[k.node];
+    for (int i = k.s + lane; i < k.e; i += 64) keys[i] = rows[(long)pidx[i] * dd + cd];
+}
+
+// one wave per small node: spread, cut dimension and keys in one pass
+__global__ __launch_bounds__(256) void kd_small_kernel(const float *__restrict__ rows, int dd,
+                                                       const int *__restrict__ pidx,
+                                                       const KdNodeDev *__restrict__ nodes, int nn,
+                                                       int *__restrict__ cut_dim, float *__restrict__ keys,
+                                                       float *__restrict__ box) {
+    const int lane = threadIdx.x & 63;
+    const int nd = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (nd >= nn) return;
+    const KdNodeDev N = nodes[nd];
+    float best = -INFINITY;
+    int bd = 0x7fffffff;
+    for (int d0 = 0; d0 < dd; d0 += 256) {
+        float mn[4], mx[4];
+        kd_minmax(rows, dd, pidx, N.s, N.e, d0, mn, mx);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int d = d0 + j * 64 + lane;
+            if (d < dd) {
+                if (box) {
+                    box[d] = mn[j];
+                    box[dd + d] = mx[j];
+                }
+                const float spr = mx[j] - mn[j];
+                if (spr > best || (spr == best && d < bd)) {
+                    best = spr;
+                    bd = d;
+                }
+            }
         }
     }
-    // annMaxSpread: max_spr starts at 0 with max_dim 0, so an all-zero spread picks dimension 0
-    const int cd = (best > 0.0f) ? bd : 0;
+    const int cd = kd_first_max(best, bd);
     if (lane == 0) cut_dim[nd] = cd;
     for (int i = N.s + lane; i < N.e; i += 64) keys[i] = rows[(long)pidx[i] * dd + cd];
 }
@@ -189,57 +268,129 @@ void kd_tree_destroy(KdTree *t) {
     hipFree(t->d_lo);
     hipFree(t->d_hi);
     hipFree(t->d_box);
+    hipFree(t->d_view);
     delete t;
 }
 
-// run f(i) for i in [0, count) on up to `threads` host threads (biggest items first: callers sort)
-template <class F>
-static void parallel_for(int count, int threads, F f) {
-    if (count <= 1 || threads <= 1) {
-        for (int i = 0; i < count; i++) f(i);
-        return;
+// Persistent host workers for the per-level quickselects (thread start-up per level would cost more than a
+// deep level's work).  run(count, f): f(i) for every i < count, items claimed in order (callers sort big first).
+class HostPool {
+  public:
+    static HostPool &get() {
+        static HostPool p;
+        return p;
     }
-    std::atomic<int> next(0);
-    auto work = [&]() {
-        for (int i = next.fetch_add(1); i < count; i = next.fetch_add(1)) f(i);
-    };
-    const int nt = std::min(threads, count);
-    std::vector<std::thread> pool;
-    pool.reserve(nt - 1);
-    for (int t = 1; t < nt; t++) pool.emplace_back(work);
-    work();
-    for (auto &th : pool) th.join();
-}
+    void run(int count, const std::function<void(int)> &f) {
+        if (count <= 0) return;
+        if (count == 1 || workers_.empty()) {
+            for (int i = 0; i < count; i++) f(i);
+            return;
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        fn_ = &f;
+        count_ = count;
+        next_.store(0);
+        busy_ = (int)workers_.size();
+        gen_++;
+        cv_.notify_all();
+        lk.unlock();
+        drain();
+        lk.lock();
+        done_cv_.wait(lk, [&] { return busy_ == 0; });
+        fn_ = nullptr;
+    }
 
-static int host_threads() {
-    const unsigned hc = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(16u, hc ? hc : 1u));
-}
+  private:
+    HostPool() {
+        const unsigned hc = std::thread::hardware_concurrency();
+        const int nt = (int)std::max(1u, std::min(16u, hc ? hc : 1u)) - 1;  // + the calling thread
+        for (int t = 0; t < nt; t++) workers_.emplace_back([this] { loop(); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+            gen_++;
+        }
+        cv_.notify_all();
+        for (auto &w : workers_) w.join();
+    }
+    void drain() {
+        for (int i = next_.fetch_add(1); i < count_; i = next_.fetch_add(1)) (*fn_)(i);
+    }
+    void loop() {
+        unsigned long seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            lk.unlock();
+            drain();
+            lk.lock();
+            if (--busy_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)> *fn_ = nullptr;
+    std::atomic<int> next_{0};
+    int count_ = 0, busy_ = 0;
+    unsigned long gen_ = 0;
+    bool stop_ = false;
+};
+
+// pinned host staging reused across builds (pinning is slow); builds are serialised by g_build_mu
+static std::mutex g_build_mu;
+struct Pinned {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *get(size_t bytes) {
+        if (bytes > cap) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+            if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+            cap = bytes;
+        }
+        return p;
+    }
+};
+static Pinned g_pin_pidx, g_pin_keys, g_pin_nodes, g_pin_ch, g_pin_cut;
 
 KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t stream) {
     const auto t0 = std::chrono::steady_clock::now();
+    std::lock_guard<std::mutex> build_lk(g_build_mu);
     KdTree *t = new KdTree();
     t->n = n;
     t->dd = dd;
     t->bs = std::max(1, bs);
-    struct Guard {  // frees the build scratch on every exit path
-        std::vector<void *> dev, host;
+    struct Guard {  // frees the build's device scratch on every exit path
+        std::vector<void *> dev;
         ~Guard() {
             for (void *p : dev) (void)hipFree(p);
-            for (void *p : host) (void)hipHostFree(p);
         }
     } g;
     auto fail = [&]() -> KdTree * {
         kd_tree_destroy(t);
         return nullptr;
     };
-#define KD_CHECK(expr)                                                                     \
-    do {                                                                                   \
-        hipError_t _e = (expr);                                                            \
-        if (_e != hipSuccess) {                                                            \
+#define KD_CHECK(expr)                                                                         \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess) {                                                                \
             set_error(std::string("kd-tree build: ") + #expr + ": " + hipGetErrorString(_e)); \
-            return fail();                                                                 \
-        }                                                                                  \
+            return fail();                                                                     \
+        }                                                                                      \
+    } while (0)
+#define KD_PIN(ptr, pool, bytes)                                       \
+    do {                                                               \
+        ptr = (decltype(ptr))pool.get(bytes);                          \
+        if (!ptr) {                                                    \
+            set_error("kd-tree build: pinned host allocation failed"); \
+            return fail();                                             \
+        }                                                              \
     } while (0)
     const size_t nn1 = (size_t)std::max(n, 1);
     KD_CHECK(hipMalloc((void **)&t->d_pos, nn1 * 4));
@@ -249,72 +400,85 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
     KD_CHECK(hipMalloc((void **)&t->d_lo, nn1 * 4));
     KD_CHECK(hipMalloc((void **)&t->d_hi, nn1 * 4));
     KD_CHECK(hipMalloc((void **)&t->d_box, (size_t)2 * std::max(dd, 1) * 4));
+    KD_CHECK(hipMalloc((void **)&t->d_view, sizeof(KdOrder)));
     std::vector<int> cdv(nn1, 0);
     std::vector<float> cvv(nn1, 0.0f);
     std::vector<float> box(2 * (size_t)std::max(dd, 1), 0.0f);
-    int *h_pidx = nullptr;
-    float *h_keys = nullptr;
-    KD_CHECK(hipHostMalloc((void **)&h_pidx, nn1 * 4, hipHostMallocDefault));
-    g.host.push_back(h_pidx);
-    KD_CHECK(hipHostMalloc((void **)&h_keys, nn1 * 4, hipHostMallocDefault));
-    g.host.push_back(h_keys);
+    int *h_pidx;
+    float *h_keys;
+    KD_PIN(h_pidx, g_pin_pidx, nn1 * 4);
+    KD_PIN(h_keys, g_pin_keys, nn1 * 4);
     for (int i = 0; i < n; i++) h_pidx[i] = i;  // SkeletonTree: pidx[i] = i
     if (n > t->bs) {
-        float *d_keys = nullptr, *d_pmin = nullptr, *d_pmax = nullptr;
+        float *d_keys = nullptr;
+        unsigned *d_omin = nullptr, *d_omax = nullptr;
         int *d_cut = nullptr;
         KdChunk *d_ch = nullptr;
         KdNodeDev *d_nodes = nullptr;
         const size_t max_nodes = (size_t)n / 2 + 1;
-        const size_t max_ch = (size_t)n / KD_CH + max_nodes + 1;
+        const size_t max_big = (size_t)n / KD_CH + 1;
+        const size_t max_ch = (size_t)n / KD_CH + max_big + 1;
         KD_CHECK(hipMalloc((void **)&d_keys, nn1 * 4));
         g.dev.push_back(d_keys);
-        KD_CHECK(hipMalloc((void **)&d_pmin, max_ch * dd * 4));
-        g.dev.push_back(d_pmin);
-        KD_CHECK(hipMalloc((void **)&d_pmax, max_ch * dd * 4));
-        g.dev.push_back(d_pmax);
+        KD_CHECK(hipMalloc((void **)&d_omin, max_big * dd * 4));
+        g.dev.push_back(d_omin);
+        KD_CHECK(hipMalloc((void **)&d_omax, max_big * dd * 4));
+        g.dev.push_back(d_omax);
         KD_CHECK(hipMalloc((void **)&d_cut, max_nodes * 4));
         g.dev.push_back(d_cut);
         KD_CHECK(hipMalloc((void **)&d_ch, max_ch * sizeof(KdChunk)));
         g.dev.push_back(d_ch);
         KD_CHECK(hipMalloc((void **)&d_nodes, max_nodes * sizeof(KdNodeDev)));
         g.dev.push_back(d_nodes);
-        KdChunk *h_ch = nullptr;
-        KdNodeDev *h_nodes = nullptr;
-        int *h_cut = nullptr;
-        KD_CHECK(hipHostMalloc((void **)&h_ch, max_ch * sizeof(KdChunk), hipHostMallocDefault));
-        g.host.push_back(h_ch);
-        KD_CHECK(hipHostMalloc((void **)&h_nodes, max_nodes * sizeof(KdNodeDev), hipHostMallocDefault));
-        g.host.push_back(h_nodes);
-        KD_CHECK(hipHostMalloc((void **)&h_cut, max_nodes * 4, hipHostMallocDefault));
-        g.host.push_back(h_cut);
+        KdChunk *h_ch;
+        KdNodeDev *h_nodes;
+        int *h_cut;
+        KD_PIN(h_ch, g_pin_ch, max_ch * sizeof(KdChunk));
+        KD_PIN(h_nodes, g_pin_nodes, max_nodes * sizeof(KdNodeDev));
+        KD_PIN(h_cut, g_pin_cut, max_nodes * 4);
         KD_CHECK(hipMemcpyAsync(t->d_pidx, h_pidx, (size_t)n * 4, hipMemcpyHostToDevice, stream));
         std::vector<std::pair<int, int>> level{{0, n}}, next;
-        const int threads = host_threads();
+        HostPool &pool = HostPool::get();
         while (!level.empty()) {
+            // nodes sorted by size, descending: the big ones (> KD_CH points) are a prefix
             const int nn = (int)level.size();
-            int nch = 0;
+            int nbig = 0, nch = 0;
             for (int i = 0; i < nn; i++) {
                 const int s = level[i].first, e = level[i].second;
-                h_nodes[i].s = s;
-                h_nodes[i].e = e;
-                h_nodes[i].c0 = nch;
-                for (int c = s; c < e; c += KD_CH) h_ch[nch++] = KdChunk{i, c, std::min(e, c + KD_CH)};
-                h_nodes[i].c1 = nch;
+                h_nodes[i] = KdNodeDev{s, e};
+                if (e - s > KD_CH) {
+                    nbig = i + 1;
+                    for (int c = s; c < e; c += KD_CH) h_ch[nch++] = KdChunk{i, c, std::min(e, c + KD_CH)};
+                }
             }
-            KD_CHECK(hipMemcpyAsync(d_ch, h_ch, (size_t)nch * sizeof(KdChunk), hipMemcpyHostToDevice, stream));
+            float *box_out = t->levels == 0 ? t->d_box : nullptr;
             KD_CHECK(hipMemcpyAsync(d_nodes, h_nodes, (size_t)nn * sizeof(KdNodeDev), hipMemcpyHostToDevice, stream));
-            hipLaunchKernelGGL(kd_spread_kernel, dim3((nch + 3) / 4), dim3(256), 0, stream, d_rows, dd,
-                               (const int *)t->d_pidx, (const KdChunk *)d_ch, nch, d_pmin, d_pmax);
-            KD_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(kd_select_kernel, dim3((nn + 3) / 4), dim3(256), 0, stream, d_rows, dd,
-                               (const int *)t->d_pidx, (const KdNodeDev *)d_nodes, nn, (const float *)d_pmin,
-                               (const float *)d_pmax, d_cut, d_keys, t->levels == 0 ? t->d_box : nullptr);
-            KD_CHECK(hipGetLastError());
+            if (nbig > 0) {
+                KD_CHECK(hipMemcpyAsync(d_ch, h_ch, (size_t)nch * sizeof(KdChunk), hipMemcpyHostToDevice, stream));
+                KD_CHECK(hipMemsetAsync(d_omin, 0xff, (size_t)nbig * dd * 4, stream));
+                KD_CHECK(hipMemsetAsync(d_omax, 0x00, (size_t)nbig * dd * 4, stream));
+                hipLaunchKernelGGL(kd_spread_big_kernel, dim3((nch + 3) / 4), dim3(256), 0, stream, d_rows, dd,
+                                   (const int *)t->d_pidx, (const KdChunk *)d_ch, nch, d_omin, d_omax);
+                KD_CHECK(hipGetLastError());
+                hipLaunchKernelGGL(kd_select_big_kernel, dim3((nbig + 3) / 4), dim3(256), 0, stream, dd, nbig,
+                                   (const unsigned *)d_omin, (const unsigned *)d_omax, d_cut, box_out);
+                KD_CHECK(hipGetLastError());
+                hipLaunchKernelGGL(kd_gather_kernel, dim3((nch + 3) / 4), dim3(256), 0, stream, d_rows, dd,
+                                   (const int *)t->d_pidx, (const KdChunk *)d_ch, nch, (const int *)d_cut, d_keys);
+                KD_CHECK(hipGetLastError());
+                box_out = nullptr;
+            }
+            if (nn > nbig) {
+                hipLaunchKernelGGL(kd_small_kernel, dim3((nn - nbig + 3) / 4), dim3(256), 0, stream, d_rows, dd,
+                                   (const int *)t->d_pidx, (const KdNodeDev *)(d_nodes + nbig), nn - nbig,
+                                   d_cut + nbig, d_keys, box_out);
+                KD_CHECK(hipGetLastError());
+            }
             KD_CHECK(hipMemcpyAsync(h_cut, d_cut, (size_t)nn * 4, hipMemcpyDeviceToHost, stream));
             KD_CHECK(hipMemcpyAsync(h_keys, d_keys, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
             KD_CHECK(hipStreamSynchronize(stream));
             // annMedianSplit per node (biggest first), recording the split node m's cut
-            parallel_for(nn, threads, [&](int i) {
+            pool.run(nn, [&](int i) {
                 const int s = level[i].first, e = level[i].second, cnt = e - s, n_lo = cnt / 2;
                 const float cv = median_split_host(h_keys + s, h_pidx + s, cnt, n_lo);
                 cdv[s + n_lo] = h_cut[i];
@@ -373,13 +537,16 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
     }
     std::vector<int> pos(nn1, 0);
     for (int i = 0; i < n; i++) pos[h_pidx[i]] = i;
+    const KdOrder view = t->view();
     KD_CHECK(hipMemcpyAsync(t->d_pos, pos.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
     KD_CHECK(hipMemcpyAsync(t->d_cd, cdv.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
     KD_CHECK(hipMemcpyAsync(t->d_cv, cvv.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
     KD_CHECK(hipMemcpyAsync(t->d_lo, lov.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
     KD_CHECK(hipMemcpyAsync(t->d_hi, hiv.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
+    KD_CHECK(hipMemcpyAsync(t->d_view, &view, sizeof(KdOrder), hipMemcpyHostToDevice, stream));
     KD_CHECK(hipStreamSynchronize(stream));
 #undef KD_CHECK
+#undef KD_PIN
     t->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return t;
 }
@@ -399,11 +566,12 @@ int kd_tree_positions(const KdTree *t, int32_t *pos) {
 __global__ __launch_bounds__(256) void kd_verify_kernel(KdOrder o, KdFixArgs a) {
     const long q = (long)blockIdx.x * 256 + threadIdx.x;
     if (q >= a.nq) return;
+    if (a.done && a.done[q]) return;
     const float *qr = a.q + q * o.dd;
     const float Dk = a.err[q * a.k + a.k - 1];
     const int i0 = a.idx[q * a.k];
     if (i0 < 0 || !(Dk < FLT_MAX)) return;  // empty dataset or fewer than k points: nothing to vouch for
-    const float rb = kd_root_box(o, qr);
+    const float rb = a.rootbox[q];
     bool ok = true;
     for (int j = 0; j < a.k && ok; j++) {
         const int c = a.idx[q * a.k + j];
@@ -508,6 +676,49 @@ __global__ __launch_bounds__(64) void kd_replay_kernel(KdOrder o, KdFixArgs a) {
     }
 }
 
+// one wave per query: coalesced row read, the outside-the-box terms in parallel, then their sequential fp32 sum
+// in dimension order (a term inside the box is +0 and leaves the running sum unchanged, so only the others are
+// added, by one lane, in order)
+__global__ __launch_bounds__(256) void kd_rootbox_kernel(KdOrder o, const float *__restrict__ q, int nq,
+                                                         float *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    for (long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6); i < nq; i += (long)gridDim.x * 4) {
+        float rb = 0.0f;
+        for (int d0 = 0; d0 < o.dd; d0 += 64) {
+            const int d = d0 + lane;
+            float t = 0.0f;
+            bool outside = false;
+            if (d < o.dd) {
+                const float v = q[i * o.dd + d], lo = o.box_lo[d], hi = o.box_hi[d];
+                if (v < lo) {
+                    t = lo - v;
+                    outside = true;
+                } else if (v > hi) {
+                    t = v - hi;
+                    outside = true;
+                }
+                t = t * t;
+            }
+            unsigned long long m = __ballot(outside);
+            while (m) {
+                const int src = __builtin_ctzll(m);
+                m &= m - 1;
+                rb = rb + __shfl(t, src, 64);
+            }
+        }
+        if (lane == 0) out[i] = rb;
+    }
+}
+
+int kd_root_boxes(const KdTree *t, const float *d_q, int nq, float *rootbox, hipStream_t stream) {
+    if (!t || nq <= 0) return 0;
+    KTimer tm("kd_verify", stream);
+    hipLaunchKernelGGL(kd_rootbox_kernel, dim3((unsigned)std::min<long>(8192, (nq + 3) / 4)), dim3(256), 0, stream,
+                       t->view(), d_q, nq, rootbox);
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 int kd_verify_and_replay(const KdTree *t, const KdFixArgs &a, hipStream_t stream) {
     if (!t || t->n <= t->bs || a.nq <= 0) return 0;  // a single bucket: no pruning, position order is exact
     if (a.k > 32) {
@@ -515,7 +726,6 @@ int kd_verify_and_replay(const KdTree *t, const KdFixArgs &a, hipStream_t stream
         return -1;
     }
     const KdOrder o = t->view();
-    TILER_HIP_CHECK(hipMemsetAsync(a.count, 0, sizeof(int), stream));
     {
         KTimer tm("kd_verify", stream);
         hipLaunchKernelGGL(kd_verify_kernel, dim3((a.nq + 255) / 256), dim3(256), 0, stream, o, a);

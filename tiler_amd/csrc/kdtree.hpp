@@ -30,6 +30,7 @@ struct KdTree {
     int n = 0, dd = 0, bs = 1;
     int *d_pos = nullptr, *d_pidx = nullptr, *d_cd = nullptr;
     float *d_cv = nullptr, *d_lo = nullptr, *d_hi = nullptr, *d_box = nullptr;  // d_box: [2][dd]
+    KdOrder *d_view = nullptr;  // device copy of view(): what the search kernels get (one pointer)
     double build_ms = 0.0;
     int levels = 0;
     KdOrder view() const;
@@ -53,8 +54,12 @@ struct KdFixArgs {
     const uint8_t *tr_attr = nullptr;
     int32_t *m_tile = nullptr, *m_pal = nullptr;
     uint8_t *m_hm = nullptr, *m_vm = nullptr;
-    int *list = nullptr, *count = nullptr;  // scratch: [nq], [1]
+    int *list = nullptr, *count = nullptr;  // [nq], [1]: queries sent to the replay (count zeroed by the caller)
+    const float *rootbox = nullptr;         // [nq] annBoxDistance of every query (kd_root_boxes)
+    const uint8_t *done = nullptr;          // [nq] or null: 1 = already checked (the pair pass), skip
 };
+// rootbox[q] = annBoxDistance(q, box) for nq fp32 rows q[nq][dd] (queries whose descriptor kernel did not fuse it)
+int kd_root_boxes(const KdTree *t, const float *d_q, int nq, float *rootbox, hipStream_t stream);
 int kd_verify_and_replay(const KdTree *t, const KdFixArgs &a, hipStream_t stream);
 
 }  // namespace tiler

@@ -584,7 +584,7 @@ struct RescoreArgs {
     const uint8_t *tr_attr;
     int32_t *m_tile, *m_pal;
     uint8_t *m_hm, *m_vm;
-    KdOrder ko;          // tie order: ANN's kd-tree first-found (ko.pos set) or the lowest index
+    const KdOrder *ko;   // tie order: ANN's kd-tree first-found (device view) or nullptr = the lowest index
 };
 
 __device__ __forceinline__ void write_map(const RescoreArgs &a, long q, int best) {
@@ -785,7 +785,7 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(RescoreArgs a, int list_n
             }
             if (i < a.d) continue;
             if (cnt == K && !kd_less(a.ko, sq, dist, j, bd[K - 1], bi[K - 1])) continue;
-            if (!a.ko.pos) {
+            if (!a.ko) {
                 list_insert<K>(bd, bi, dist, j);  // j ascends: an equal key stays behind, as index order wants
             } else {
                 int p = (cnt < K) ? cnt : K - 1;
@@ -962,6 +962,8 @@ void nn_index_destroy(NNIndex *ix) {
     hipFree(s.cbuf);
     hipFree(s.kd_list);
     hipFree(s.kd_count);
+    hipFree(s.kd_rootbox);
+    hipFree(s.kd_done);
     hipHostFree(ix->h_fb_count);
     delete ix;
 }
@@ -980,6 +982,8 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         hipFree(s.thr);
         hipFree(s.ex_list);
         hipFree(s.kd_list);
+        hipFree(s.kd_rootbox);
+        hipFree(s.kd_done);
         const long nqblk = (nq + 31) / 32 + 2;
         TILER_HIP_CHECK(hipMalloc(&s.qfrag, (size_t)nqblk * 16 * 64 * 16));
         TILER_HIP_CHECK(hipMalloc(&s.qfrag16, (size_t)((nq + 15) / 16 + 2) * 8 * 64 * 16));
@@ -989,6 +993,8 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         TILER_HIP_CHECK(hipMalloc((void **)&s.thr, (size_t)nq * sizeof(float)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.ex_list, (size_t)nq * sizeof(int)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.kd_list, (size_t)nq * sizeof(int)));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.kd_rootbox, (size_t)nq * sizeof(float)));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.kd_done, (size_t)nq));
         s.cap_q = nq;
     }
     if (!s.kd_count) TILER_HIP_CHECK(hipMalloc((void **)&s.kd_count, 16));
@@ -1123,7 +1129,7 @@ static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t s
 static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream);
 
 int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
-                  hipStream_t stream) {
+                  hipStream_t stream, bool rootbox_ready) {
     if (nq <= 0) return 0;
     if (k < 1 || k > 32) {
         set_error("nn: k must be in 1..32");
@@ -1143,7 +1149,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     ra.max_abs_c = ix->max_abs;
     ra.out_idx = d_idx;
     ra.out_err = d_err;
-    if (ix->kd) ra.ko = ix->kd->view();
+    ra.ko = ix->kd ? ix->kd->d_view : nullptr;
     if (maps && k == 1 && ix->d_tr_tile) {
         ra.tr_tile = ix->d_tr_tile;
         ra.tr_pal = ix->d_tr_pal;
@@ -1154,12 +1160,20 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         ra.m_vm = maps->vm;
     }
     ix->last_queries = nq;
+    SearchScratch &s = ix->scratch;
+    if (ix->kd) {  // ANN's tie order: the pruning check needs every query's box distance and a clean slate
+        if (ensure_scratch(ix, nq, 0)) return -1;
+        if (!rootbox_ready && kd_root_boxes(ix->kd, d_q, nq, s.kd_rootbox, stream)) return -1;
+        TILER_HIP_CHECK(hipMemsetAsync(s.kd_done, 0, (size_t)nq, stream));
+        TILER_HIP_CHECK(hipMemsetAsync(s.kd_count, 0, sizeof(int), stream));
+    }
     if (search_core(ix, ra, d_q, nq, k, stream)) return -1;
     if (!ix->kd) return 0;
-    // ANN's box pruning along every result's path; the rare query it cannot vouch for is replayed exactly
-    SearchScratch &s = ix->scratch;
-    if (ensure_scratch(ix, nq, 0)) return -1;
+    // ANN's box pruning along every result's path (queries the pair pass did not already check); the rare query
+    // it cannot vouch for is replayed exactly
     KdFixArgs fa{ix->d_rows, d_q, nq, k, d_idx, d_err};
+    fa.rootbox = s.kd_rootbox;
+    fa.done = s.kd_done;
     fa.tr_tile = ra.tr_tile;
     fa.tr_pal = ra.tr_pal;
     fa.tr_attr = ra.tr_attr;
@@ -1222,6 +1236,10 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
         t.m_hm = ra.m_hm;
         t.m_vm = ra.m_vm;
         t.ko = ra.ko;
+        t.kd_rootbox = s.kd_rootbox;
+        t.kd_done = s.kd_done;
+        t.kd_list = s.kd_list;
+        t.kd_count = s.kd_count;
         if (orbit_search(ix, d_q, nq, t, stream)) return -1;
         ix->last_orbit = 1;
         ra.qstat = s.qstat;
@@ -1322,8 +1340,14 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
     pa.flags = use_wavelets ? PSYV_WAVELETS : 0;
     pa.gamma = gamma;
     pa.out32 = s.qrows;
+    const bool fuse_rb = ix->kd && use_wavelets && ix->kd->dd == 192;
+    if (fuse_rb) {  // annBoxDistance of each query descriptor, in the descriptor kernel (kd pruning check)
+        if (ensure_scratch(ix, Q, 0)) return -1;
+        pa.box = ix->kd->d_box;
+        pa.rootbox = s.kd_rootbox;
+    }
     if (launch_psyv(pa, stream)) return -1;
-    return nn_search_dev(ix, s.qrows, Q, 1, d_idx, d_err, maps, stream);
+    return nn_search_dev(ix, s.qrows, Q, 1, d_idx, d_err, maps, stream, fuse_rb);
 }
 
 }  // namespace tiler

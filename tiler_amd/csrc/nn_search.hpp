@@ -45,6 +45,8 @@ struct SearchScratch {
     int *cbuf = nullptr;      // tier-2 collect buffers
     int *kd_list = nullptr;   // [nq] queries the ANN pruning check sends to the exact replay
     int *kd_count = nullptr;  // [1]
+    float *kd_rootbox = nullptr;  // [nq] annBoxDistance of each query to the kd-tree's enclosing box
+    uint8_t *kd_done = nullptr;   // [nq] 1: the pair pass already checked this query's winner
     size_t cap_q = 0, cap_keys = 0, cap_rows = 0;
 };
 
@@ -88,7 +90,7 @@ struct FtMaps {
 // k nearest neighbours of nq fp32 query rows in HBM; results [nq][k] in HBM; async on stream.
 // If maps is non-null (k == 1) the FrameTiling tilemap items are written too.
 int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
-                  hipStream_t stream);
+                  hipStream_t stream, bool rootbox_ready = false);
 
 // frame tiling: RGB tiles -> descriptors (fp32) -> search -> tilemap items
 int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int *d_idx,

@@ -885,7 +885,7 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
     int cand = a.member[(long)g * 4 + x];
     if (cand < 0 || ((a.dup[g] >> x) & 1)) return -1;
     key = (double)a.nc[g] - 2.0 * (double)d;
-    if (a.t.ko.pos && a.dup[g]) {  // identical rows of this slot's set: the one ANN finds first stands for them
+    if (a.t.ko && a.dup[g]) {  // identical rows of this slot's set: the one ANN finds first stands for them
         const unsigned rep = a.rep[g];
         const float *qr = a.q + q * OD;
         for (int y = 0; y < 4; y++) {
@@ -1118,6 +1118,13 @@ __global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a)
     }
     const OrbitTail &t = a.t;
     kd_argmin<ORB_PSLOTS>(t.ko, a.q + q * OD, bd, bi);
+    if (t.ko) {  // ANN's box pruning along the winner's path, with the query row still in cache
+        const bool ok = kd_quad_path_ok(t.ko, a.q + q * OD, t.ko->pos[bi], t.kd_rootbox[q], bd, s);
+        if (s == 0) {
+            t.kd_done[q] = 1;
+            if (!ok) t.kd_list[atomicAdd(t.kd_count, 1)] = (int)q;
+        }
+    }
     if (s == 0) {
         t.out_idx[q] = bi;
         t.out_err[q] = bd;

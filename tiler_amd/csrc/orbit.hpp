@@ -63,7 +63,10 @@ struct OrbitTail {
     int32_t *m_tile, *m_pal;
     uint8_t *m_hm, *m_vm;
     int *n_expand;                // optional device counter of block expansions
-    KdOrder ko;                   // tie order (ANN's kd-tree first-found, or the lowest index)
+    const KdOrder *ko;            // tie order: ANN's kd-tree first-found (device view), nullptr = lowest index
+    const float *kd_rootbox;      // [nq] (ko != nullptr): each query's annBoxDistance to the tree's box
+    uint8_t *kd_done;             // [nq] the pair pass marks the queries whose winner it checked
+    int *kd_list, *kd_count;      // queries whose winner ANN's pruning might have skipped -> exact replay
 };
 
 // 0: orbit index built (ix->orbit), 1: dataset has no exploitable mirror structure, -1: HIP error

@@ -103,10 +103,14 @@ template <bool FASTDIV>
 __global__ __launch_bounds__(64) void psyv_rgb_haar_kernel(PsyvArgs a) {
     __shared__ double lut[256];
     __shared__ float st[64 * 65];  // one component of the 64 tiles, transposed for coalesced row stores
+    __shared__ float sbox[2 * 192];
     const int lane = threadIdx.x;
     const double *__restrict__ glut = a.gamma_lut + 256 * (a.gamma + 1);
     for (int i = lane; i < 256; i += 64) lut[i] = glut[i];
+    if (a.rootbox)
+        for (int i = lane; i < 2 * 192; i += 64) sbox[i] = a.box[i];
     __syncthreads();
+    float rb = 0.0f;  // annBoxDistance, accumulated in dimension order (c, k)
     const long t0 = (long)blockIdx.x * 64;
     const long i = t0 + lane;
     const bool valid = i < a.n;
@@ -127,6 +131,19 @@ __global__ __launch_bounds__(64) void psyv_rgb_haar_kernel(PsyvArgs a) {
             }
         }
         haar_regs(p, a.haar_f);
+        if (a.rootbox) {
+#pragma unroll
+            for (int k = 0; k < 64; k++) {
+                const float v = (float)p[k], lo = sbox[c * 64 + k], hi = sbox[192 + c * 64 + k];
+                if (v < lo) {
+                    const float t = lo - v;
+                    rb = rb + t * t;
+                } else if (v > hi) {
+                    const float t = v - hi;
+                    rb = rb + t * t;
+                }
+            }
+        }
         if (a.out32) {
             // lane = tile: its 64 values into LDS (stride 65: conflict-free), then 16 lanes per tile store
             // the tile's 256-byte component segment (64-byte lines written whole, not a line per lane)
@@ -149,6 +166,7 @@ __global__ __launch_bounds__(64) void psyv_rgb_haar_kernel(PsyvArgs a) {
             for (int k = 0; k < 32; k++) o[k] = make_double2(p[2 * k], p[2 * k + 1]);
         }
     }
+    if (a.rootbox && valid) a.rootbox[i] = rb;
 }
 
 int launch_psyv(PsyvArgs args, hipStream_t stream) {
@@ -166,6 +184,10 @@ int launch_psyv(PsyvArgs args, hipStream_t stream) {
         return -1;
     }
     KTimer tm("psyv", stream);
+    if (args.rootbox && !(args.rgb && !args.flags_per && args.flags == PSYV_WAVELETS)) {
+        set_error("psyv: the fused root-box output exists on the RGB Haar query path only");
+        return -1;
+    }
     if (args.rgb && !args.flags_per && (args.flags & ~PSYV_QWEIGHT) == PSYV_WAVELETS) {
         const dim3 grid((unsigned)((args.n + 63) / 64));
         if (args.gamma == -1)

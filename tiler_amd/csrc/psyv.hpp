@@ -18,6 +18,10 @@ struct PsyvArgs {
     int gamma = -1;
     double *out64 = nullptr;            // [n][192]
     float *out32 = nullptr;             // [n][192]
+    // optional (RGB Haar query path only): annBoxDistance of the fp32 descriptor to box[2][192] (a kd-tree's
+    // enclosing box, kdtree.hpp) -> rootbox[n], fused so the FrameTiling search's pruning check needs no re-read
+    const float *box = nullptr;
+    float *rootbox = nullptr;
     // filled by launch_psyv from the shared LUTs
     const double *gamma_lut = nullptr, *dct_lut = nullptr, *qmul = nullptr, *ratio = nullptr;
     double haar_f = 0, u_mul = 0, v_mul = 0;

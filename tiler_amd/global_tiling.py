@@ -152,19 +152,27 @@ def do_global_tiling(palpix, dith_pal, n_palettes: int, desired: int, palsize: i
 
 
 def make_tiles_unique(palpix, active, use_count):
-    """MakeTilesUnique main.pas:2555-2612 over all tiles; duplicates merge into the lowest index."""
+    """MakeTilesUnique main.pas:2555-2612 over all tiles.  Active tiles sorted by CompareTilePalPixels
+    (CompareDWord over 16 little-endian dwords, main.pas:2546-2553; equal keys by index: TFPList.Sort is
+    unstable); each run of identical tiles merges into its first member.  The final
+    DoOneMerge runs with i = Count - 1 (main.pas:2604-2605), so the last run never includes its last member
+    and a 2-member last run does not merge: reproduced, not fixed."""
     palpix = np.array(palpix, np.uint8, copy=True)
     active = np.array(active, np.uint8, copy=True)
     use_count = np.array(use_count, np.int64, copy=True)
     merge_index = np.full(palpix.shape[0], -1, np.int64)
     idx = np.nonzero(active)[0]
     if idx.size:
-        _, inv = np.unique(palpix[idx], axis=0, return_inverse=True)
-        inv = inv.reshape(-1)
-        for g in np.unique(inv):
-            members = idx[inv == g]
-            if members.size >= 2:
-                merge_tiles(members, int(members.min()), palpix, active, use_count, merge_index)
+        words = np.ascontiguousarray(palpix[idx]).view("<u4").reshape(-1, 16)
+        order = idx[np.lexsort(words[:, ::-1].T)]  # dword 0 primary; stable: index order among equal keys
+        w = np.ascontiguousarray(palpix[order]).view("<u4").reshape(-1, 16)
+        starts = np.concatenate([[0], np.nonzero(np.any(w[1:] != w[:-1], axis=1))[0] + 1])
+        ends = np.concatenate([starts[1:], [order.size]])
+        ends[-1] -= 1  # the reference's final DoOneMerge: i := sortList.Count - 1
+        for a, b in zip(starts, ends):
+            if b - a >= 2:
+                members = order[a:b]
+                merge_tiles(members, int(members[0]), palpix, active, use_count, merge_index)
     return palpix, active, use_count, merge_index
 
 

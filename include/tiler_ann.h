@@ -84,7 +84,9 @@ int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
 int tiler_kdtree_positions(ann_kdtree *akd, int32_t *pos);
 
 /* ---- runtime ---- */
-int tiler_init(int device);         /* optional; first call of any entry point initialises device 0 */
+/* Binds the library to one HIP device (one process per GPU: device = LOCAL_RANK).  Optional; the first call
+ * of any other entry point binds device 0.  Re-binding to another device once bound fails with -1. */
+int tiler_init(int device);
 int tiler_shutdown(void);
 const char *tiler_last_error(void); /* thread-local message of the last failure */
 int tiler_set_gamma(double g0, double g1); /* gGamma main.pas:586 / 1441-1447; rebuilds gGammaCorLut */

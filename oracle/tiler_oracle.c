@@ -669,8 +669,10 @@ int or_kmodes(const uint8_t *X, int N, int A, int K, int start, int modalities, 
 /* ------------------------------------------------------------------------------------------
  * GlobalTiling driver (main.pas:4142-4370) + MakeTilesUnique (2555-2612) + ReindexTiles (4483-4527).
  * ---------------------------------------------------------------------------------------- */
-/* EqualQualityTileCount main.pas:722-725: FPC Round = banker's rounding. */
-int or_eqtc(double n) { return (int)nearbyint(sqrt(n) * (log(1.0 + n) / log(2.0))); }
+/* EqualQualityTileCount main.pas:722-725: FPC Round = banker's rounding; log2 from FPC's Math unit,
+ * ln(x) * 1.4426950408889634079 (1/ln 2), not ln(x) / ln(2).  (FPC's own ln may still differ from glibc's
+ * log by an ulp; tests/test_global_tiling.py shows no tile count up to 2^22 is that close to a .5.) */
+int or_eqtc(double n) { return (int)nearbyint(sqrt(n) * (log(1.0 + n) * 1.4426950408889634079)); }
 
 /* WriteTileDatasetLine main.pas:4167-4183 + GetTilePalZoneThres 4142-4165 (ZoneCount 16). */
 int or_tile_dataset_line(const uint8_t *pp, int palsize, uint8_t *line) {

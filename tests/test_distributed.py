@@ -1,6 +1,7 @@
-"""world_size-2 gloo tests of the sharded path on CPU: keyframe / palette-bin plans, tileset broadcast,
-tilemap gather and the UseCount all-reduce give the single-process result.  The per-unit compute is the
-CPU oracle here (test-only stand-in for the GPU kernels, which need a device)."""
+"""world_size-2 gloo tests of the sharded path on CPU (tiler_amd.dist): keyframe / palette-bin
+plans, the tileset broadcast, the K-Modes merge map all-reduce (MAX), the UseCount all-reduce (SUM) and the
+tilemap reduce onto one rank give the single-process result, with fixed-layout tensors only.  The per-unit
+compute is the CPU oracle here (test-only stand-in for the GPU kernels, which need a device)."""
 import os
 import socket
 
@@ -28,6 +29,63 @@ def test_lpt_plan_balanced_and_complete():
     assert tdist.plan_bins([100, 5, 50, 0], [10, 1, 7, 0], 2) == tdist.plan_bins([100, 5, 50, 0], [10, 1, 7, 0], 2)
 
 
+def test_no_pickled_collectives_in_product():
+    """The product's multi-GPU path exchanges fixed-layout tensors only (no *_object collectives)."""
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tiler_amd")
+    for f in os.listdir(root):
+        if f.endswith(".py"):
+            txt = open(os.path.join(root, f)).read()
+            assert "_object(" not in txt, f
+
+
+KF_FRAMES = [3, 2, 4]
+Q = 20
+
+
+def _kf_frames(u):
+    from tiler_amd import synth
+    return synth.keyframe_frames(np.random.default_rng(100 + u), KF_FRAMES[u], Q)
+
+
+def _setup(pyoracle, synth):
+    T, P = 300, 4
+    rng = np.random.default_rng(5)
+    tiles, thm, tvm = synth.tileset(rng, T)
+    pals = synth.palettes(np.random.default_rng(6), P)
+    tile_pal = np.random.default_rng(7).integers(0, P, T).astype(np.int32)
+    ods, ot, op, oa = pyoracle.build_ft_dataset(synth.used_one_palette(tile_pal, P), tiles, thm, tvm, pals)
+    return tiles, thm, tvm, ods, ot, op, oa
+
+
+def _oracle_kmodes_results(pyoracle, plan, bins):
+    """DoKModes per bin on the CPU restatement: labels, medoid (GetMinMatchingDissim over the members, ties to the
+    last), member counts -- the shape gt.kmodes_bins returns."""
+    out = {}
+    for p in bins:
+        X = plan.lines[plan.bins[p]]
+        k = int(plan.k_per_bin[p])
+        labels, cent, _, _ = pyoracle.kmodes(X, k, plan.starts[p])
+        medoid = np.full(k, -1, np.int32)
+        counts = np.bincount(labels, minlength=k).astype(np.int32)
+        for j in range(k):
+            mem = np.nonzero(labels == j)[0]
+            if mem.size:
+                i, _ = pyoracle.km_get_min(X[mem], cent[j])
+                medoid[j] = mem[i]
+        out[p] = (labels, medoid, counts)
+    return out
+
+
+def _gt_inputs():
+    from tiler_amd import synth
+    rng = np.random.default_rng(9)
+    T, P = 900, 5
+    tiles = rng.integers(0, 16, (T, 64)).astype(np.uint8)
+    tiles[300:600] = tiles[rng.integers(0, 300, 300)]  # duplicates and near-duplicates cluster
+    dith = rng.integers(0, P, T).astype(np.int32)
+    return tiles, dith, P, synth
+
+
 def _worker(rank, world, port, out_path):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -37,61 +95,69 @@ def _worker(rank, world, port, out_path):
 
     import pyoracle
     from tiler_amd import dist as td
+    from tiler_amd import global_tiling as gt
     from tiler_amd import synth
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    T, P = 300, 4
-    if rank == 0:
-        rng = np.random.default_rng(5)
-        tiles, thm, tvm = synth.tileset(rng, T)
-        packed = np.concatenate([tiles.reshape(-1), thm, tvm]).astype(np.int32)
-    else:
-        packed = None
+    # 1. tileset broadcast
+    tiles, thm, tvm, ods, ot, op, oa = _setup(pyoracle, synth)
+    T = tiles.shape[0]
+    packed = np.concatenate([tiles.reshape(-1), thm, tvm]).astype(np.int32) if rank == 0 else None
     packed = td.broadcast_array(packed, (T * 64 + 2 * T,), np.int32)
-    tiles = packed[:T * 64].astype(np.uint8).reshape(T, 64)
-    thm = packed[T * 64:T * 64 + T].astype(np.uint8)
-    tvm = packed[T * 64 + T:].astype(np.uint8)
-    pals = synth.palettes(np.random.default_rng(6), P)
-    tile_pal = np.random.default_rng(7).integers(0, P, T).astype(np.int32)
-    used = synth.used_one_palette(tile_pal, P)
-    ods, ot, op, oa = pyoracle.build_ft_dataset(used, tiles, thm, tvm, pals)
-    kf_frames = [3, 2, 4]
-
-    def tile_kf(u):
-        fr = synth.keyframe_frames(np.random.default_rng(100 + u), kf_frames[u], 20)
-        res = pyoracle.frame_tiling(fr.reshape(-1, 64), ods, ot, op, oa, threads=1)
-        return {"tile": res[0], "pal": res[1], "hm": res[2], "vm": res[3], "err": res[4]}
-
-    res = td.run_sharded(3, [f * 20 for f in kf_frames], tile_kf)
+    assert np.array_equal(packed[:T * 64].astype(np.uint8).reshape(T, 64), tiles)
+    # 2. GlobalTiling: this rank's palette bins -> merge map -> all-reduce MAX
+    gtiles, dith, P, _ = _gt_inputs()
+    plan = gt.plan_global_tiling(gtiles, dith, P, desired=200)
+    costs = [plan.bins[p].size * max(1, int(plan.k_per_bin[p])) for p in plan.run]
+    mine = [plan.run[u] for u in td.lpt_assign(costs, world)[rank]]
+    local = gt.kmodes_merge_map(plan, _oracle_kmodes_results(pyoracle, plan, mine), gtiles.shape[0])
+    merge_to = td.allreduce(local, "max")
+    # 3. FrameTiling: this rank's keyframes -> UseCount all-reduce, tilemaps reduced onto rank 0
+    F = sum(KF_FRAMES)
+    starts = np.concatenate([[0], np.cumsum(KF_FRAMES)])
+    tm = np.zeros((F, Q, 2), np.int32)
     uc = np.zeros(T, np.int64)
-    plan = td.plan_keyframes(kf_frames, 20, world)
-    for u in plan[rank]:
-        np.add.at(uc, res[u]["tile"], 1)
-    uc = td.allreduce_sum(uc)
+    for u in td.plan_keyframes(KF_FRAMES, Q, world)[rank]:
+        res = pyoracle.frame_tiling(_kf_frames(u).reshape(-1, 64), ods, ot, op, oa, threads=1)
+        tm[starts[u]:starts[u + 1], :, 0] = res[0].reshape(-1, Q)
+        tm[starts[u]:starts[u + 1], :, 1] = (res[1] | (res[2].astype(np.int32) << 16) |
+                                              (res[3].astype(np.int32) << 17)).reshape(-1, Q)
+        np.add.at(uc, res[0], 1)
+    uc = td.allreduce(uc, "sum")
+    full = td.reduce_to(tm, 0)
+    assert (full is None) == (rank != 0)
     if rank == 0:
-        np.savez(out_path, **{f"{u}_{k}": v for u in res for k, v in res[u].items()}, uc=uc)
+        np.savez(out_path, merge_to=merge_to, uc=uc, tm=full)
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_sharded_frame_tiling_matches_single_process(tmp_path):
+def test_sharded_steps_match_single_process(tmp_path):
     out = str(tmp_path / "r.npz")
     mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     got = np.load(out)
-    # single-process reference
     import pyoracle
+    from tiler_amd import global_tiling as gt
     from tiler_amd import synth
-    rng = np.random.default_rng(5)
-    tiles, thm, tvm = synth.tileset(rng, 300)
-    pals = synth.palettes(np.random.default_rng(6), 4)
-    tile_pal = np.random.default_rng(7).integers(0, 4, 300).astype(np.int32)
-    ods, ot, op, oa = pyoracle.build_ft_dataset(synth.used_one_palette(tile_pal, 4), tiles, thm, tvm, pals)
-    uc = np.zeros(300, np.int64)
-    for u, f in enumerate([3, 2, 4]):
-        fr = synth.keyframe_frames(np.random.default_rng(100 + u), f, 20)
-        res = pyoracle.frame_tiling(fr.reshape(-1, 64), ods, ot, op, oa, threads=1)
-        assert np.array_equal(got[f"{u}_tile"], res[0]) and np.array_equal(got[f"{u}_err"], res[4])
+    # merge map: the single process over every bin
+    gtiles, dith, P, _ = _gt_inputs()
+    plan = gt.plan_global_tiling(gtiles, dith, P, desired=200)
+    want = gt.kmodes_merge_map(plan, _oracle_kmodes_results(pyoracle, plan, plan.run), gtiles.shape[0])
+    assert np.array_equal(got["merge_to"], want) and (want >= 0).sum() > 0
+    pp, act, uc_g, mi = gt.apply_merge_map(got["merge_to"], gtiles, None, None)
+    assert act.sum() == gtiles.shape[0] - (want >= 0).sum()
+    # FrameTiling tilemaps + UseCount
+    tiles, thm, tvm, ods, ot, op, oa = _setup(pyoracle, synth)
+    uc = np.zeros(tiles.shape[0], np.int64)
+    starts = np.concatenate([[0], np.cumsum(KF_FRAMES)])
+    for u in range(len(KF_FRAMES)):
+        res = pyoracle.frame_tiling(_kf_frames(u).reshape(-1, 64), ods, ot, op, oa, threads=1)
+        blk = got["tm"][starts[u]:starts[u + 1]]
+        assert np.array_equal(blk[..., 0].ravel(), res[0])
+        assert np.array_equal(blk[..., 1].ravel() & 0xFFFF, res[1])
+        assert np.array_equal((blk[..., 1].ravel() >> 16) & 1, res[2])
+        assert np.array_equal((blk[..., 1].ravel() >> 17) & 1, res[3])
         np.add.at(uc, res[0], 1)
     assert np.array_equal(got["uc"], uc)

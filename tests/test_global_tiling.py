@@ -35,6 +35,21 @@ def test_dataset_line_and_eqtc(oracle):
         assert gt.equal_quality_tile_count(n) == oracle.lib().or_eqtc(float(n))
 
 
+def test_eqtc_rounding_boundaries(oracle):
+    """EqualQualityTileCount's Round at .5 boundaries: FPC's log2 (ln * 1.4426950408889634079) vs ln / ln 2 and
+    an ulp either way never flips the count of any bin size up to 2^22 tiles; product and oracle agree on the
+    sizes closest to a .5."""
+    import math
+    n = np.arange(0, 1 << 22, dtype=np.float64)
+    v = np.sqrt(n) * (np.log1p(n) * gt.FPC_INV_LN2)
+    frac = np.abs(v - np.floor(v) - 0.5)
+    near = np.argsort(frac)[:64]
+    assert frac[near[0]] > 1e-9  # no size sits within an ulp-scale distance of a rounding boundary
+    for k in near:
+        assert gt.equal_quality_tile_count(int(k)) == oracle.lib().or_eqtc(float(k)) == round(v[k])
+        assert round(math.sqrt(k) * (math.log(1.0 + k) / math.log(2.0))) == round(v[k])
+
+
 def test_make_unique_and_reindex_match_oracle(oracle):
     import ctypes
     rng = np.random.default_rng(2)

@@ -111,6 +111,18 @@ def test_knn_palette_index_preselection(gpu, oracle):
     check_nn(gpu, oracle, gds, qs, k=8)
 
 
+def test_knn_heavy_ties(gpu, oracle):
+    """k=8 where dozens of candidates share the k-th distance (2-colour tiles): a lane list full of equal keys may
+    hide the one ANN finds first, so the tier-1 overflow check must hold for exact integer keys too."""
+    rng = np.random.default_rng(15)
+    tiles = (rng.random((2000, 64)) < 0.1).astype(np.uint8)
+    gds, gt, ga = oracle.prepare_global_ds(tiles)
+    qs = np.concatenate([tiles[rng.integers(0, 2000, 200)], (rng.random((200, 64)) < 0.1)]).astype(np.float32)
+    st = check_nn(gpu, oracle, gds, qs, k=8)
+    assert st["fallback_queries"] > 0
+    check_nn(gpu, oracle, gds, qs, k=1)
+
+
 def test_reference_call_shapes(gpu, oracle):
     """ann_kdtree_search / search_multi one query at a time, as main.pas:4027 and 3830 call them."""
     rng = np.random.default_rng(6)

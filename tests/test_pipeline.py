@@ -147,10 +147,10 @@ def _dist_worker(rank, world, port, out, quality):
     from tiler_amd.encoder import DistributedEncoder
     check(tiler_amd.load().tiler_init(0), "tiler_init")  # every rank on the one GPU of the test box
     v = synth.video(61, 320, 240, kf_frames=(3, 2, 3), n_palettes=8)
-    e = DistributedEncoder(v)
+    e = DistributedEncoder(v, device=0)
     sm = e.run_all(700, quality, 0.2)
-    data = e.save_stream(320, 240, 24.0)
     if rank == 0:
+        data = e.save_stream(320, 240, 24.0)
         np.savez(out, palpix=e.palpix, tile=e.tile, pal=e.pal, hm=e.hm, vm=e.vm, sm_tile=sm["tile"],
                  sm_smoothed=sm["smoothed"], gtm=np.frombuffer(data, np.uint8))
     dist.barrier()

@@ -113,7 +113,14 @@ static int build_luts() {
 }
 
 static int init_locked(int device) {
-    if (g_ready) return 0;
+    if (g_ready) {
+        if (device == g_device) return 0;
+        // already bound (explicitly, or implicitly to device 0 by an earlier call): handles, LUTs and scratch live
+        // on that device, so a silent switch would run later calls on the wrong GPU
+        set_error("tiler_init: the library is already bound to device " + std::to_string(g_device) +
+                  "; call tiler_init(" + std::to_string(device) + ") before any other entry point");
+        return -1;
+    }
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
         set_error("tiler: no HIP device visible (libANN.so runs on MI355X / gfx950 only, no CPU path)");

@@ -648,8 +648,10 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
         (void)nq;
     }
     if (!isfinite(kk)) T = INFINITY;
-    // overflow: a full list whose last kept key is <= T may have dropped a needed candidate
-    if (!exact || a.L < a.k) {
+    // overflow: a full list whose last kept key is <= T may have dropped a needed candidate.  Exact integer keys
+    // with L >= k need no check under index order (a lane keeps its best L by (key, index), consistent with the
+    // global order), but under ANN's kd order a lane's dropped equal-key entry can rank first
+    if (!exact || a.L < a.k || a.ko) {
         const bool last = lane < E && (lane % a.L) == a.L - 1;
         if (__any(last && idx >= 0 && (double)key <= T)) fallback = true;
     }

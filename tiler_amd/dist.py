@@ -1,18 +1,23 @@
-"""Multi-GPU sharding of the hot path: one process per GPU, torch.distributed
-(RCCL over xGMI on MI355X, gloo on CPU for tests).
+"""Multi-GPU sharding of the hot path: one process per GPU, torch.distributed (RCCL over xGMI
+on MI355X with backend "nccl"; gloo on CPU for tests).
 
-The work units are independent, so there is no data-path collective:
+The work units are independent, so the data path has no collective of its own:
   * FrameTiling and Smooth: keyframes (PrepareFrameTiling / DoTemporalSmoothing are keyframe-local,
     main.pas:4005-4011, 4081-4082) -> longest-processing-time assignment by frames x tiles;
   * GlobalTiling K-Modes: palette bins (DoKModes per bin, main.pas:4339) -> LPT by n_bin x k_bin.
-The exchanges are the pipeline's own: the global tileset broadcast before FrameTiling, the tilemap
-gather after it, the UseCount all-reduce for ReindexTiles (main.pas:1208-1221) and the all-gather of
-per-bin merge results after K-Modes.
+The exchanges are the pipeline's own, each ONE fixed-layout tensor collective (no pickled objects):
+  * after K-Modes: the merge map, int32 [T] (-1 = kept), all-reduced with MAX -- every tile belongs to exactly
+    one bin, so exactly one rank writes its entry; every rank then applies MergeTiles identically and holds the
+    reduced tileset (the north star's tileset all-gather);
+  * before ReindexTiles: the UseCount histogram, int64 [T], all-reduced with SUM (main.pas:1208-1221);
+  * for SaveStream: the tilemaps, int32 [F][Q][4], each rank contributing its own keyframes' frames, reduced with
+    SUM onto the saving rank only.
+Tensors live on the rank's GPU under nccl (RCCL reads HBM directly) and on the CPU under gloo.
 """
 from __future__ import annotations
 
 import heapq
-from typing import Callable, Sequence
+from typing import Sequence
 
 import numpy as np
 
@@ -37,36 +42,48 @@ def plan_bins(bin_sizes: Sequence[int], k_per_bin: Sequence[int], world: int) ->
     return lpt_assign([max(1, n) * max(1, k) for n, k in zip(bin_sizes, k_per_bin)], world)
 
 
-def broadcast_array(a: np.ndarray | None, shape, dtype, src: int = 0, device=None) -> np.ndarray:
-    """Rank `src` sends `a`; every rank returns it (the tileset 'all-gather' of the north star)."""
+def comm_device():
+    """Where collective tensors live: this rank's GPU under nccl (RCCL), the CPU under gloo."""
     import torch
     import torch.distributed as dist
-    t = torch.from_numpy(np.ascontiguousarray(a)).to(device) if dist.get_rank() == src else \
+    if dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _to_tensor(a: np.ndarray, device):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+def broadcast_array(a: np.ndarray | None, shape, dtype, src: int = 0, device=None) -> np.ndarray:
+    """Rank `src` sends `a`; every rank returns it."""
+    import torch
+    import torch.distributed as dist
+    device = comm_device() if device is None else device
+    t = _to_tensor(a, device) if dist.get_rank() == src else \
         torch.empty(shape, dtype=getattr(torch, np.dtype(dtype).name), device=device)
     dist.broadcast(t, src)
     return t.cpu().numpy()
 
 
-def allreduce_sum(a: np.ndarray, device=None) -> np.ndarray:
-    """UseCount histogram for ReindexTiles (main.pas:1208-1221)."""
-    import torch
+def allreduce(a: np.ndarray, op: str = "sum", device=None) -> np.ndarray:
+    """Element-wise SUM / MAX over ranks of a fixed-layout array (UseCount histogram, merge map)."""
     import torch.distributed as dist
-    t = torch.from_numpy(np.ascontiguousarray(a)).to(device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    t = _to_tensor(a, comm_device() if device is None else device)
+    dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX}[op])
     return t.cpu().numpy()
 
 
-def run_sharded(n_units: int, costs: Sequence[float], fn: Callable[[int], dict], device=None) -> dict[int, dict]:
-    """Run fn(unit) for this rank's units (LPT plan) and all-gather every unit's result dict of numpy arrays.
-    Returns {unit: result} on every rank."""
+def allreduce_sum(a: np.ndarray, device=None) -> np.ndarray:
+    """UseCount histogram for ReindexTiles (main.pas:1208-1221)."""
+    return allreduce(a, "sum", device)
+
+
+def reduce_to(a: np.ndarray, dst: int = 0, device=None) -> np.ndarray | None:
+    """SUM of every rank's `a` on rank `dst` only (None elsewhere): ranks contribute disjoint parts, zeros
+    elsewhere, so the sum is the assembled array."""
     import torch.distributed as dist
-    world, rank = dist.get_world_size(), dist.get_rank()
-    plan = lpt_assign(costs, world)
-    mine = {u: fn(u) for u in plan[rank]}
-    gathered: list = [None] * world
-    dist.all_gather_object(gathered, mine)
-    out: dict[int, dict] = {}
-    for g in gathered:
-        out.update(g)
-    assert sorted(out) == list(range(n_units))
-    return out
+    t = _to_tensor(a, comm_device() if device is None else device)
+    dist.reduce(t, dst, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy() if dist.get_rank() == dst else None

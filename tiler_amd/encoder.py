@@ -174,28 +174,50 @@ class Encoder:
 
 
 class DistributedEncoder(Encoder):
-    """The same chain with one process per GPU (tiler_amd.dist): palette bins (K-Modes) and
-    keyframes (FrameTiling, Smooth) are planned longest-first across the ranks, each rank computes its
-    units on its own GPU and the per-unit results are all-gathered, so every rank holds the single-process
-    state after each step (the host bookkeeping is deterministic and repeated on every rank).  Call inside
-    an initialised torch.distributed process group."""
+    """The same chain with one process per GPU (tiler_amd.dist).  Call inside an initialised
+    torch.distributed process group (backend "nccl" = RCCL over xGMI; "gloo" for CPU-side tests).
+
+    Device: each rank binds its own GPU -- libANN.so through tiler_init(device) and torch through
+    torch.cuda.set_device(device) -- with device = LOCAL_RANK (torchrun's one process per GPU) unless given.
+    Work: palette bins (K-Modes) and keyframes (FrameTiling, then Smooth, same plan) are assigned longest-first
+    across the ranks; a rank computes only its own units.  Exchanges (fixed-layout tensors, tiler_amd.dist):
+    the K-Modes merge map (all-reduce MAX) so every rank holds the reduced tileset, the UseCount histogram
+    (all-reduce SUM) for ReindexTiles, and the tilemaps onto rank `save_rank` only (reduce SUM) for SaveStream.
+    Between steps a rank's tilemaps are current for its own keyframes only; after run_all (or gather()) rank
+    `save_rank` holds the whole single-process state."""
+
+    def __init__(self, v: Video, palsize: int = 16, device: int | None = None, save_rank: int = 0):
+        import os
+
+        import torch
+        import torch.distributed as dist
+
+        from ._lib import check, load
+        from . import dist as tdist
+        super().__init__(v, palsize)
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.device = int(os.environ.get("LOCAL_RANK", "0")) if device is None else int(device)
+        check(load().tiler_init(self.device), "tiler_init")
+        if torch.cuda.is_available():
+            torch.cuda.set_device(self.device)
+        self.save_rank = save_rank
+        nkf = self.kf_start.size - 1
+        kf_frames = [int(self.kf_start[k + 1] - self.kf_start[k]) for k in range(nkf)]
+        self.my_kf = tdist.plan_keyframes(kf_frames, self.tiles_per_frame, self.world)[self.rank]
+        self.my_frames = np.zeros(self.frames, bool)
+        for k in self.my_kf:
+            self.my_frames[int(self.kf_start[k]):int(self.kf_start[k + 1])] = True
 
     def do_global_tiling(self, desired: int, restart: int = gt.CRANDOM_KMODES_COUNT):
         from . import dist as tdist
         plan = gt.plan_global_tiling(self.palpix, self.dith_pal, self.n_palettes, desired, self.palsize, restart,
                                      self.active)
-        import torch.distributed as dist
         run = plan.run
         costs = [plan.bins[p].size * max(1, int(plan.k_per_bin[p])) for p in run]
-        mine = [run[u] for u in tdist.lpt_assign(costs, dist.get_world_size())[dist.get_rank()]]
+        mine = [run[u] for u in tdist.lpt_assign(costs, self.world)[self.rank]]
         local = gt.kmodes_bins(plan, mine, self.palsize)  # this rank's bins in one GPU batch
-        gathered: list = [None] * dist.get_world_size()
-        dist.all_gather_object(gathered, local)
-        res = {}
-        for g in gathered:
-            res.update(g)
-        assert sorted(res) == sorted(run)
-        pp, act, uc, mi = gt.apply_kmodes_merges(plan, res, self.palpix, self.active, self.use_count)
+        merge_to = tdist.allreduce(gt.kmodes_merge_map(plan, local, self.palpix.shape[0]), "max")
+        pp, act, uc, mi = gt.apply_merge_map(merge_to, self.palpix, self.active, self.use_count)
         self.palpix, self.active, self.use_count = pp, act, uc
         self.finish_merge_tiles(mi)
         self.make_tiles_unique()
@@ -203,52 +225,86 @@ class DistributedEncoder(Encoder):
         return plan.k_per_bin
 
     def do_frame_tiling(self, quality: int = ft.FT_MEDIUM, use_wavelets: bool = True, gamma: int = -1):
-        from . import dist as tdist
+        """This rank's keyframes only (their TileMaps become current; the others' stay as they were)."""
         gds = ft.prepare_global_ft(self.palpix, self.active)
+        errs = np.zeros(self.tile.shape, np.float32)
         Q = self.tiles_per_frame
-
-        def one(k):
-            f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
-            kt = ft.prepare_frame_tiling(self.palpix, self.thm, self.tvm, self.palettes[k], gds,
-                                         self.pal[f0:f1].ravel(), self.tile[f0:f1].ravel(), quality,
-                                         self.centroids[k], use_wavelets, gamma)
-            try:
-                t, p, h, v, e = kt.do_frame_tiling(self.frame_rgb[f0:f1])
-            finally:
-                kt.finish_frame_tiling()
-            return {"tile": t, "pal": p, "hm": h, "vm": v, "err": e}
-
-        nkf = self.kf_start.size - 1
         try:
-            res = tdist.run_sharded(nkf, [(int(self.kf_start[k + 1] - self.kf_start[k])) * Q for k in range(nkf)],
-                                    one)
+            for k in self.my_kf:
+                f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
+                kt = ft.prepare_frame_tiling(self.palpix, self.thm, self.tvm, self.palettes[k], gds,
+                                             self.pal[f0:f1].ravel(), self.tile[f0:f1].ravel(), quality,
+                                             self.centroids[k], use_wavelets, gamma)
+                try:
+                    t, p, h, v, e = kt.do_frame_tiling(self.frame_rgb[f0:f1])
+                finally:
+                    kt.finish_frame_tiling()
+                n = (f1 - f0, Q)
+                self.tile[f0:f1], self.pal[f0:f1] = t.reshape(n), p.reshape(n)
+                self.hm[f0:f1], self.vm[f0:f1], errs[f0:f1] = h.reshape(n), v.reshape(n), e.reshape(n)
         finally:
             gds.kdt.close()
-        errs = np.zeros(self.tile.shape, np.float32)
-        for k, r in res.items():
-            f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
-            n = (f1 - f0, Q)
-            self.tile[f0:f1], self.pal[f0:f1] = r["tile"].reshape(n), r["pal"].reshape(n)
-            self.hm[f0:f1], self.vm[f0:f1], errs[f0:f1] = r["hm"].reshape(n), r["vm"].reshape(n), r["err"].reshape(n)
         return errs
 
-    def do_smooth(self, strength: float = DEFAULT_STRENGTH):
+    def do_reindex(self):
+        """btnReindexClick main.pas:1199-1230 with the UseCount histogram all-reduced over the ranks' keyframes."""
         from . import dist as tdist
-        nkf = self.kf_start.size - 1
+        T = self.palpix.shape[0]
+        local = np.bincount(self.tile[self.my_frames].ravel(), minlength=T).astype(np.int64)
+        self.use_count = tdist.allreduce(local, "sum")
+        self.active = (self.use_count > 0).astype(np.uint8)
+        self.tile = np.where(self.my_frames[:, None], self.tile, 0)  # other ranks' frames: not current here
+        self.reindex_tiles()
 
-        def one(k):
-            f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
-            z = np.zeros((f1 - f0, self.tiles_per_frame), np.uint8)
-            t, p, h, v, s, _ = smooth_keyframe(self.tile[f0:f1], self.pal[f0:f1], self.hm[f0:f1], self.vm[f0:f1], z,
-                                               self.palpix, self.palettes[k], strength)
-            return {"tile": t, "pal": p, "hm": h, "vm": v, "smoothed": s}
-
-        res = tdist.run_sharded(nkf, [int(self.kf_start[k + 1] - self.kf_start[k]) for k in range(nkf)], one)
+    def do_smooth(self, strength: float = DEFAULT_STRENGTH):
         sm = {"tile": self.tile.copy(), "pal": self.pal.copy(), "hm": self.hm.copy(), "vm": self.vm.copy(),
               "smoothed": np.zeros(self.tile.shape, np.uint8)}
-        for k, r in res.items():
+        for k in self.my_kf:
             f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
-            for key in sm:
-                sm[key][f0:f1] = r[key]
+            t, p, h, v, s, _ = smooth_keyframe(sm["tile"][f0:f1], sm["pal"][f0:f1], sm["hm"][f0:f1],
+                                               sm["vm"][f0:f1], sm["smoothed"][f0:f1], self.palpix,
+                                               self.palettes[k], strength)
+            sm["tile"][f0:f1], sm["pal"][f0:f1], sm["hm"][f0:f1], sm["vm"][f0:f1] = t, p, h, v
+            sm["smoothed"][f0:f1] = s
         self.sm = sm
         return sm
+
+    def gather(self):
+        """Every rank's keyframes' TileMaps and SmoothedTileMaps onto rank save_rank (one reduce of int32
+        [F][Q][4]: tile, pal | hm << 16 | vm << 17, and the same for the smoothed items | smoothed << 18)."""
+        from . import dist as tdist
+        if self.n_palettes > 1 << 16:
+            raise ValueError("palette index does not fit the packed tilemap layout")
+        own = self.my_frames[:, None]
+        sm = self.sm
+        pk = np.zeros(self.tile.shape + (4,), np.int32)
+        pk[..., 0] = np.where(own, self.tile, 0)
+        pk[..., 1] = np.where(own, self.pal | (self.hm.astype(np.int64) << 16) | (self.vm.astype(np.int64) << 17), 0)
+        if sm is not None:
+            pk[..., 2] = np.where(own, sm["tile"], 0)
+            pk[..., 3] = np.where(own, sm["pal"] | (sm["hm"].astype(np.int64) << 16) |
+                                  (sm["vm"].astype(np.int64) << 17) | (sm["smoothed"].astype(np.int64) << 18), 0)
+        full = tdist.reduce_to(pk, self.save_rank)
+        if full is None:
+            return None
+        self.tile = full[..., 0].astype(np.int64)
+        self.pal = (full[..., 1] & 0xFFFF).astype(np.int64)
+        self.hm = ((full[..., 1] >> 16) & 1).astype(np.uint8)
+        self.vm = ((full[..., 1] >> 17) & 1).astype(np.uint8)
+        self.my_frames[:] = True
+        if sm is not None:
+            self.sm = {"tile": full[..., 2].astype(np.int64), "pal": (full[..., 3] & 0xFFFF).astype(np.int64),
+                       "hm": ((full[..., 3] >> 16) & 1).astype(np.uint8),
+                       "vm": ((full[..., 3] >> 17) & 1).astype(np.uint8),
+                       "smoothed": ((full[..., 3] >> 18) & 1).astype(np.uint8)}
+        return self.sm
+
+    def run_all(self, desired: int, quality: int = ft.FT_MEDIUM, strength: float = DEFAULT_STRENGTH):
+        """btnRunAllClick from MakeUnique to Smooth, then the tilemaps onto save_rank (None on the other ranks)."""
+        super().run_all(desired, quality, strength)
+        return self.gather()
+
+    def save_stream(self, width: int, height: int, fps: float = 24.0) -> bytes:
+        if self.rank != self.save_rank:
+            raise RuntimeError(f"SaveStream runs on rank {self.save_rank}, which holds the gathered tilemaps")
+        return super().save_stream(width, height, fps)

@@ -33,9 +33,13 @@ def write_tile_dataset_line(tiles: np.ndarray, palsize: int = 16) -> np.ndarray:
     return np.ascontiguousarray(np.concatenate([t, flags], 1))
 
 
+FPC_INV_LN2 = 1.4426950408889634079  # FPC Math.log2(x) = ln(x) * 1.4426950408889634079
+
+
 def equal_quality_tile_count(n: float) -> int:
-    """round(sqrt(n) * log2(1 + n)) with FPC's banker's rounding (Python round is half-even)."""
-    return int(round(math.sqrt(n) * (math.log(1.0 + n) / math.log(2.0))))
+    """round(sqrt(n) * log2(1 + n)) (main.pas:722-725) with FPC's banker's rounding (Python round is half-even)
+    and FPC Math's log2 = ln(x) * (1 / ln 2)."""
+    return int(round(math.sqrt(n) * (math.log(1.0 + n) * FPC_INV_LN2)))
 
 
 def kmodes_medoids(X: np.ndarray, labels: np.ndarray, centroids: np.ndarray):
@@ -120,25 +124,42 @@ def kmodes_bins(plan: GTPlan, subset, palsize: int = 16) -> dict:
             for i, p in enumerate(subset)}
 
 
-def apply_kmodes_merges(plan: GTPlan, results: dict, palpix, active, use_count):
-    """MergeTiles for every cluster with >= 2 members (main.pas:4231-4253) of every K-Modes bin.  Bins own
-    disjoint tiles, so the order of the reference's per-cluster loop does not change the result."""
+def kmodes_merge_map(plan: GTPlan, results: dict, T: int) -> np.ndarray:
+    """DoKModes' merge decisions (main.pas:4231-4253) of the bins in `results` as one int32 map over all T tiles:
+    merge_to[j] = the medoid tile j merges into, -1 = kept.  Bins own disjoint tiles, so maps of different bin
+    sets combine with an element-wise max (the sharded path's all-reduce)."""
+    merge_to = np.full(T, -1, np.int32)
+    for p, (labels, medoid, counts) in results.items():
+        b = plan.bins[p]
+        best = np.where(counts >= 2, b[np.maximum(medoid, 0)], -1)[labels]
+        sel = (best >= 0) & (b != best)
+        merge_to[b[sel]] = best[sel]
+    return merge_to
+
+
+def apply_merge_map(merge_to, palpix, active, use_count):
+    """MergeTiles for every merged tile (main.pas:3688-3712, NewTile = nil): UseCount summed into the medoid,
+    Active := False, MergeIndex set, PalPixels zeroed.  Each medoid is kept (merge_to = -1), so the order of the
+    reference's per-cluster loop does not change the result."""
     palpix = np.array(palpix, np.uint8, copy=True).reshape(-1, 64)
     T = palpix.shape[0]
     active = np.ones(T, np.uint8) if active is None else np.array(active, np.uint8, copy=True)
     use_count = np.ones(T, np.int64) if use_count is None else np.array(use_count, np.int64, copy=True)
+    merge_to = np.asarray(merge_to, np.int64)
+    src = np.nonzero(merge_to >= 0)[0]
+    dst = merge_to[src]
+    np.add.at(use_count, dst, use_count[src])
+    active[src] = 0
     merge_index = np.full(T, -1, np.int64)
-    if plan.run:
-        tile_of = np.concatenate([plan.bins[p] for p in plan.run])
-        best = np.concatenate([np.where(results[p][2] >= 2, plan.bins[p][np.maximum(results[p][1], 0)], -1)
-                               [results[p][0]] for p in plan.run])
-        sel = (best >= 0) & (tile_of != best)
-        src, dst = tile_of[sel], best[sel]
-        np.add.at(use_count, dst, use_count[src])
-        active[src] = 0
-        merge_index[src] = dst
-        palpix[src] = 0
+    merge_index[src] = dst
+    palpix[src] = 0
     return palpix, active, use_count, merge_index
+
+
+def apply_kmodes_merges(plan: GTPlan, results: dict, palpix, active, use_count):
+    """MergeTiles for every cluster with >= 2 members (main.pas:4231-4253) of every K-Modes bin."""
+    T = np.asarray(palpix).reshape(-1, 64).shape[0]
+    return apply_merge_map(kmodes_merge_map(plan, results, T), palpix, active, use_count)
 
 
 def do_global_tiling(palpix, dith_pal, n_palettes: int, desired: int, palsize: int = 16,

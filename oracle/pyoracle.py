@@ -247,7 +247,9 @@ def km_get_min(rows, item):
     return i, best.value
 
 
-def kmodes(X, k, start, modalities=16):
+def kmodes(X, k, start, modalities=16, threads=1):
+    """ComputeKModes; threads > 1 splits the distance loops (results do not depend on it)."""
+    lib().or_set_threads(int(threads))
     X = np.ascontiguousarray(X, np.uint8)
     n, a = X.shape
     labels = np.zeros(n, np.int32)

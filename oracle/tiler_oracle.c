@@ -484,6 +484,30 @@ uint64_t or_km_dissim(const uint8_t *r, const uint8_t *x) {
     return ((uint64_t)mism << 11) + w0 + w4;
 }
 
+/* The same value with SSE2 on 16-byte blocks (the shape of the reference asm, kmodes.pas:341-412): pcmpeqb +
+ * movemask for the mismatch count, psadbw for S_lo / S_hi (its two 8-byte halves).  Used by the argmin and
+ * min-distance loops; tests/test_oracle_kats.py checks it against or_km_dissim and the reference asm. */
+#if defined(__SSE2__)
+#include <emmintrin.h>
+static inline uint64_t km_dissim_fast(const uint8_t *r, const uint8_t *x) {
+    unsigned eqm = 0;
+    __m128i sad = _mm_setzero_si128();
+    for (int blk = 0; blk < 80; blk += 16) {
+        const __m128i a = _mm_loadu_si128((const __m128i *)(r + blk)), b = _mm_loadu_si128((const __m128i *)(x + blk));
+        eqm += (unsigned)__builtin_popcount((unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(a, b)));
+        if (blk) sad = _mm_add_epi64(sad, _mm_sad_epu8(a, b));
+    }
+    const unsigned slo = (unsigned)_mm_cvtsi128_si32(sad), shi = (unsigned)_mm_cvtsi128_si32(_mm_srli_si128(sad, 8));
+    const unsigned w0 = (abs8(r[0], x[0]) + 256u * abs8(r[1], x[1]) + slo) & 0xffffu;
+    const unsigned w4 = (abs8(r[8], x[8]) + 256u * abs8(r[9], x[9]) + shi) & 0xffffu;
+    return ((uint64_t)(80u - eqm) << 11) + w0 + w4;
+}
+#else
+#define km_dissim_fast or_km_dissim
+#endif
+
+uint64_t or_km_dissim_fast(const uint8_t *r, const uint8_t *x) { return km_dissim_fast(r, x); }
+
 /* MatchingDissim generic path kmodes.pas:239-250 (not the one that runs on x86-64). */
 uint64_t or_km_dissim_generic(const uint8_t *a, const uint8_t *b, int n) {
     uint64_t r = 0;
@@ -499,7 +523,7 @@ int or_km_get_min(const uint8_t *rows, int count, const uint8_t *item, uint64_t 
     uint64_t b = UINT64_MAX;
     int bi = -1;
     for (int i = 0; i < count; i++) {
-        uint64_t d = or_km_dissim(rows + (size_t)i * 80, item);
+        uint64_t d = km_dissim_fast(rows + (size_t)i * 80, item);
         if (d <= b) {
             b = d;
             bi = i;
@@ -512,7 +536,7 @@ int or_km_get_min(const uint8_t *rows, int count, const uint8_t *item, uint64_t 
 /* UpdateMinDistance_Asm kmodes.pas:455-596: strict-less min; the 'used' test is a no-op (567). */
 void or_km_update_min_distance(const uint8_t *item, const uint8_t *rows, int count, uint64_t *mindist) {
     for (int i = 0; i < count; i++) {
-        uint64_t d = or_km_dissim(rows + (size_t)i * 80, item);
+        uint64_t d = km_dissim_fast(rows + (size_t)i * 80, item);
         if (d < mindist[i]) mindist[i] = d;
     }
 }
@@ -521,6 +545,63 @@ void or_km_update_min_distance(const uint8_t *item, const uint8_t *rows, int cou
 uint32_t or_randint(uint32_t range, uint32_t *seed) {
     *seed = (uint32_t)(*seed * 0x08088405u) + 1u;
     return (uint32_t)(((uint64_t)*seed * (uint64_t)range) >> 32);
+}
+
+/* ---- a small pthread parallel-for: the reference runs the K-Modes distance loops on 4 threads per bin
+ * (TKModes.Create(4), main.pas:4217; DoGMMD / DoUMD via ProcThreadPool, kmodes.pas:877, 693).  Results do
+ * not depend on the split: every item is computed independently. ---- */
+typedef void (*pf_fn)(void *ctx, int begin, int end);
+typedef struct {
+    pf_fn fn;
+    void *ctx;
+    int begin, end;
+} pf_job;
+
+static void *pf_run(void *p) {
+    pf_job *j = (pf_job *)p;
+    j->fn(j->ctx, j->begin, j->end);
+    return NULL;
+}
+
+static int g_km_threads = 1;
+void or_set_threads(int t) { g_km_threads = t < 1 ? 1 : (t > 64 ? 64 : t); }
+
+static void parallel_for(int count, long work_per_item, pf_fn fn, void *ctx) {
+    int t = g_km_threads;
+    if ((long)count * work_per_item < (1L << 22)) t = 1; /* not worth a thread start */
+    if (t > count) t = count;
+    if (t <= 1) {
+        if (count > 0) fn(ctx, 0, count);
+        return;
+    }
+    pthread_t th[64];
+    pf_job jobs[64];
+    for (int i = 0; i < t; i++) {
+        jobs[i] = (pf_job){fn, ctx, (int)((long)count * i / t), (int)((long)count * (i + 1) / t)};
+        if (i) pthread_create(&th[i], NULL, pf_run, &jobs[i]);
+    }
+    pf_run(&jobs[0]);
+    for (int i = 1; i < t; i++) pthread_join(th[i], NULL);
+}
+
+typedef struct {
+    const uint8_t *item, *rows;
+    uint64_t *mindist;
+} umd_ctx;
+static void umd_part(void *c, int b, int e) {
+    umd_ctx *u = (umd_ctx *)c;
+    or_km_update_min_distance(u->item, u->rows + (size_t)b * 80, e - b, u->mindist + b);
+}
+
+typedef struct {
+    const uint8_t *cent, *X;
+    int K, A;
+    int32_t *clust;
+    uint64_t *dis;
+} gmmd_ctx;
+static void gmmd_part(void *c, int b, int e) {
+    gmmd_ctx *g = (gmmd_ctx *)c;
+    for (int i = b; i < e; i++) g->clust[i] = or_km_get_min(g->cent, g->K, g->X + (size_t)i * g->A, &g->dis[i]);
 }
 
 typedef struct {
@@ -571,7 +652,8 @@ static void init_farthest_first(km_state *s, int init_point) {
     int f = init_point;
     memcpy(s->cent, s->X + (size_t)f * s->A, (size_t)s->A);
     used[f] = 1;
-    or_km_update_min_distance(s->X + (size_t)f * s->A, s->X, s->N, mind);
+    umd_ctx u = {s->X + (size_t)f * s->A, s->X, mind};
+    parallel_for(s->N, 80, umd_part, &u);
     for (int c = 1; c < s->K; c++) {
         uint64_t mx = 0;
         f = -1;
@@ -583,7 +665,8 @@ static void init_farthest_first(km_state *s, int init_point) {
         if (f < 0) break; /* K > N: the reference would fault here */
         memcpy(s->cent + (size_t)c * s->A, s->X + (size_t)f * s->A, (size_t)s->A);
         used[f] = 1;
-        or_km_update_min_distance(s->X + (size_t)f * s->A, s->X, s->N, mind);
+        u.item = s->X + (size_t)f * s->A;
+        parallel_for(s->N, 80, umd_part, &u);
     }
     free(mind);
     free(used);
@@ -599,7 +682,8 @@ static int kmodes_iter(km_state *s, uint32_t *seed, uint64_t *cost) {
     int32_t *choices = (int32_t *)malloc(sizeof(int32_t) * (size_t)s->N);
     for (int b0 = 0; b0 < s->N; b0 += BIN) {
         int last = (b0 + BIN < s->N ? b0 + BIN : s->N) - 1;
-        for (int i = b0; i <= last; i++) clust[i] = or_km_get_min(s->cent, s->K, s->X + (size_t)i * s->A, &dis[i]);
+        gmmd_ctx g = {s->cent, s->X + (size_t)b0 * s->A, s->K, s->A, clust + b0, dis + b0};
+        parallel_for(last - b0 + 1, 80L * s->K, gmmd_part, &g);
         for (int i = b0; i <= last; i++) {
             acc += dis[i];
             if (s->memb[i] != clust[i]) {
@@ -637,10 +721,13 @@ int or_kmodes(const uint8_t *X, int N, int A, int K, int start, int modalities, 
     s.freq = (int32_t *)calloc((size_t)K * A * modalities, sizeof(int32_t));
     s.csize = (int32_t *)calloc((size_t)K, sizeof(int32_t));
     init_farthest_first(&s, start);
-    for (int i = 0; i < N; i++) {
-        labels[i] = or_km_get_min(centroids, K, X + (size_t)i * A, NULL);
-        s.csize[labels[i]]++;
+    {  /* DoGMMD over all points (kmodes.pas:984-997) */
+        uint64_t *d0 = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(N > 0 ? N : 1));
+        gmmd_ctx g = {centroids, X, K, A, labels, d0};
+        parallel_for(N, 80L * K, gmmd_part, &g);
+        free(d0);
     }
+    for (int i = 0; i < N; i++) s.csize[labels[i]]++;
     for (int i = 0; i < N; i++)
         for (int a = 0; a < A; a++) s.freq[((size_t)labels[i] * A + a) * modalities + X[(size_t)i * A + a]]++;
     for (int k = 0; k < K; k++) {

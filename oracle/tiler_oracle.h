@@ -83,10 +83,12 @@ void or_smooth(int F, int Q, int32_t *tile, int32_t *tmpidx, int32_t *pal, uint8
                uint8_t *smoothed, const uint8_t *palpix, const int32_t *palettes, double strength);
 
 uint64_t or_km_dissim(const uint8_t *row, const uint8_t *item);
+uint64_t or_km_dissim_fast(const uint8_t *row, const uint8_t *item); /* SSE2 form of the same value */
 uint64_t or_km_dissim_generic(const uint8_t *row, const uint8_t *item, int n);
 int or_km_get_min(const uint8_t *rows, int count, const uint8_t *item, uint64_t *best);
 void or_km_update_min_distance(const uint8_t *item, const uint8_t *rows, int count, uint64_t *mindist);
 uint32_t or_randint(uint32_t range, uint32_t *seed);
+void or_set_threads(int threads); /* K-Modes distance loops (the reference: 4 per bin); default 1 */
 int or_kmodes(const uint8_t *X, int N, int A, int K, int start, int modalities, int32_t *labels,
               uint8_t *centroids, int *n_iter, uint64_t *cost);
 

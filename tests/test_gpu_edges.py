@@ -78,3 +78,12 @@ def test_empty_frame_through_frame_tiling(gpu):
     t, p, h, v, e = kt.do_frame_tiling(np.zeros((0, 64), np.int32))
     assert t.size == 0 and e.size == 0
     kt.finish_frame_tiling()
+
+
+def test_tiler_init_refuses_rebinding(gpu):
+    """Once bound (explicitly or implicitly), the library stays on its device: tiler_init on another device
+    fails loudly instead of silently running later calls on the first one (one process per GPU)."""
+    lib = gpu.load()
+    assert lib.tiler_init(0) == 0
+    assert lib.tiler_init(1) == -1
+    assert "already bound to device 0" in gpu.last_error()

@@ -1,5 +1,7 @@
 """GPU parity of K-Modes against the CPU restatement (pinned to the reference asm): labels, centroids,
 iteration count and cost bit-exact, including empty-cluster rescues (Delphi LCG) and ties."""
+import os
+
 import numpy as np
 import pytest
 
@@ -62,3 +64,52 @@ def test_kmodes_batch_matches_per_bin(gpu, oracle):
         from tiler_amd.global_tiling import kmodes_medoids
         m1, c1 = kmodes_medoids(x, ol, oc)
         assert np.array_equal(med[koff[b]:koff[b + 1]], m1) and np.array_equal(cnt[koff[b]:koff[b + 1]], c1), b
+
+
+def _oracle_threads():
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:
+        return 1
+
+
+@pytest.mark.timeout(600)
+def test_kmodes_c4_full_batch(gpu, oracle):
+    """BASELINE C4 at full size: 1,048,576 tiles (64k prototypes, 10 % perturbation, Zipf(1.1) bins over 128
+    palettes, desired 65,536) through ONE tiler_kmodes_batch + medoid batch (the DoGlobalTiling call shape,
+    main.pas:4339), then every bin of <= 10,000 rows (111 bins) and the smallest bin of >= 50,000 rows checked
+    against the CPU restatement (labels, centroids, iterations, cost, medoids; the oracle's distance loops on
+    16 host threads like the reference's TKModes threads)."""
+    from tiler_amd import global_tiling as gt
+    from tiler_amd import synth
+    tiles, dith = synth.globaltiling_workload(4, 1 << 20, n_palettes=128)
+    plan = gt.plan_global_tiling(tiles, dith, 128, 65536)
+    from tiler_amd.kmodes import compute_kmodes_batch, medoids_batch
+    run = list(plan.run)
+    X_all = np.ascontiguousarray(np.concatenate([plan.lines[plan.bins[p]] for p in run]))
+    off = np.concatenate([[0], np.cumsum([plan.bins[p].size for p in run])]).astype(np.int32)
+    ks = np.array([plan.k_per_bin[p] for p in run], np.int32)
+    st = np.array([plan.starts[p] for p in run], np.int32)
+    assert X_all.shape[0] == (1 << 20) - sum(plan.bins[p].size for p in range(128) if p not in run)
+    g_labels, g_cent, g_it, g_cost = compute_kmodes_batch(X_all, off, ks, st)
+    g_med, g_cnt = medoids_batch(X_all, off, ks, g_labels, g_cent)
+    koff = np.concatenate([[0], np.cumsum(ks)])
+    big = min((b for b in range(len(run)) if off[b + 1] - off[b] >= 50000), key=lambda b: off[b + 1] - off[b])
+    check = [b for b in range(len(run)) if off[b + 1] - off[b] <= 10000] + [big]
+    assert len(check) >= 100
+    th = _oracle_threads()
+    for b in check:
+        p = run[b]
+        X = plan.lines[plan.bins[p]]
+        k = int(ks[b])
+        ol, oc, oi, ocost = oracle.kmodes(X, k, plan.starts[p], threads=th)
+        labels = g_labels[off[b]:off[b + 1]]
+        medoid, counts = g_med[koff[b]:koff[b + 1]], g_cnt[koff[b]:koff[b + 1]]
+        assert (int(g_it[b]), int(g_cost[b])) == (oi, ocost), p
+        assert np.array_equal(g_cent[koff[b]:koff[b + 1]], oc), p
+        assert np.array_equal(labels, ol), p
+        assert np.array_equal(counts, np.bincount(ol, minlength=k)), p
+        for j in np.nonzero(counts)[0]:
+            mem = np.nonzero(ol == j)[0]
+            i, _ = oracle.km_get_min(X[mem], oc[j])  # GetMinMatchingDissim: ties -> last member
+            assert medoid[j] == mem[i], (p, j)

@@ -170,3 +170,28 @@ def test_ann_tie_order_c3_frame_queries(gpu, oracle):
     n_tie = int(np.count_nonzero((oi[0] != o[0]) | (oi[2] != o[2]) | (oi[3] != o[3])))
     assert n_tie > 0
     assert st["orbit_search"] == 1 and st["tie_order"] == 0
+
+
+def test_c5_frame_queries_vs_ann(gpu, oracle):
+    """BASELINE C5 candidate set at full size: a 256k tileset x 4 mirrors = 1,048,576 candidates (805 MB of fp32
+    rows in HBM), 1,024 4K frame-tile queries through tiler_frame_tiling against ANN's kd-tree search on the
+    host (oracle/ann_kdtree.c, 16 threads): tile, palette, mirror flags and distance bit for bit."""
+    from tiler_amd.frame_tiling import KeyframeTiler
+    rng = np.random.default_rng(55)
+    P, T = 128, 262144
+    pals = synth.palettes(rng, P)
+    tiles, thm, tvm = synth.tileset(rng, T)
+    tile_pal = rng.integers(0, P, T).astype(np.int32)
+    ds = synth.ft_dataset_from_used(synth.used_one_palette(tile_pal, P), thm, tvm)
+    assert ds.tile_of.size == 4 * T
+    q = synth.frame_tiles(rng, 1024)  # the 4K frame-tile mix (smooth / textured / flat)
+    kt = KeyframeTiler(tiles, thm, tvm, pals, ds)
+    g = kt.do_frame_tiling(q)
+    st = kt.kdt.stats()
+    rows = kt.rows
+    kt.finish_frame_tiling()
+    assert st["orbit_search"] == 1 and st["tie_order"] == 0 and st["orbit_groups"] == T
+    o = oracle.frame_tiling(q, rows, ds.tile_of, ds.pal_of, ds.attrs)
+    assert np.array_equal(np.asarray(g[4]).view(np.uint32), o[4].view(np.uint32))
+    for a, b in zip(g[:4], o[:4]):
+        assert np.array_equal(a, b), f"{np.count_nonzero(a != b)} of {q.shape[0]} items differ"

@@ -45,6 +45,20 @@ def test_kmodes_dissim_matches_live_reference_asm(oracle):
         assert (bi, best.value) == oracle.km_get_min(rows, item)
 
 
+def test_kmodes_dissim_sse_form_equals_restatement(oracle):
+    """The oracle's SSE2 dissimilarity (argmin / min-distance loops) equals its scalar restatement of the asm."""
+    rng = np.random.default_rng(19)
+    f = oracle.lib().or_km_dissim_fast
+    f.restype = ctypes.c_uint64
+    for t in range(3000):
+        hi = [2, 16, 256][t % 3]
+        a = rng.integers(0, hi, 80, dtype=np.int64).astype(np.uint8)
+        b = rng.integers(0, hi, 80, dtype=np.int64).astype(np.uint8)
+        if t % 7 == 0:
+            b = a.copy()
+        assert f(a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p)) == oracle.km_dissim(a, b)
+
+
 def test_kmodes_asm_quirk_differs_from_generic(oracle):
     """The executed asm covers only bytes {0,1*256,8,9*256,16..79} in its L1 term."""
     a = np.zeros(80, np.uint8)

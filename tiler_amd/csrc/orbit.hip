@@ -242,6 +242,71 @@ __global__ __launch_bounds__(256) void orbit_dup_kernel(const float *__restrict_
     }
 }
 
+// One thread per group: the kd-tree nodes separating the group's members (ANN's visit order among them,
+// kdorder_dev.hpp), i.e. the lowest common node of every present slot pair, walked from the root on positions.
+__global__ __launch_bounds__(256) void orbit_gorder_kernel(KdOrder o, const int *__restrict__ member, long G,
+                                                           GroupOrder *__restrict__ out, int *__restrict__ grp_of) {
+    const long g = (long)blockIdx.x * 256 + threadIdx.x;
+    if (g >= G) return;
+    int pos[4], mem[4];
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+        mem[x] = member[g * 4 + x];
+        pos[x] = mem[x] >= 0 ? o.pos[mem[x]] : -1;
+        if (mem[x] >= 0) grp_of[mem[x]] = (int)(g * 4 + x);
+    }
+    GroupOrder r;
+    r.pad = 0;
+    int nodes[3] = {-1, -1, -1}, nn = 0;
+    unsigned pairs = 0;
+    int pi = 0;
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = x + 1; y < 4; y++, pi++) {
+            if (pos[x] < 0 || pos[y] < 0) continue;
+            const int pa = min(pos[x], pos[y]), pb = max(pos[x], pos[y]);
+            int s0 = 0, e0 = o.n, m = -1;
+            while (e0 - s0 > o.bs) {
+                const int mm = s0 + ((e0 - s0) >> 1);
+                if (pb < mm) {
+                    e0 = mm;
+                } else if (pa >= mm) {
+                    s0 = mm;
+                } else {
+                    m = mm;
+                    break;
+                }
+            }
+            if (m < 0) continue;  // one bucket: position order (not reached with bs = 1)
+            int ni = -1;
+            for (int i = 0; i < nn; i++)
+                if (nodes[i] == m) ni = i;
+            if (ni < 0 && nn < 3) {
+                ni = nn;
+                nodes[nn++] = m;
+            }
+            pairs |= (unsigned)(ni | ((pos[x] < m) ? 4 : 0)) << (3 * pi);
+        }
+    for (int i = 0; i < 3; i++) {
+        r.cd[i] = (uint16_t)(nodes[i] >= 0 ? o.cd[nodes[i]] : 0);
+        r.cv[i] = nodes[i] >= 0 ? o.cv[nodes[i]] : 0.0f;
+    }
+    r.pairs = pairs;
+    out[g] = r;
+}
+
+// ANN's order of two different slots of one group (both present) for query q
+__device__ __forceinline__ bool group_before(const GroupOrder &go, const float *__restrict__ q, int x, int y) {
+    const int lo = min(x, y), hi = max(x, y);
+    const int pi = lo == 0 ? hi - 1 : lo == 1 ? hi + 1 : 5;  // (0,1)(0,2)(0,3)(1,2)(1,3)(2,3)
+    const unsigned code = (go.pairs >> (3 * pi)) & 7u;
+    const int node = code & 3;
+    const bool lo_first = (q[go.cd[node]] - go.cv[node]) < 0.0f;
+    const bool low_slot_first = ((code >> 2) & 1) == (unsigned)lo_first;
+    return (x == lo) == low_slot_first;
+}
+
 // ------------------------------------------------------------------------------------------
 // device: transform + fp16 split (dataset rows: member != null, coefficient cs; queries: qs)
 //   lane l of block b holds row b*32 + (l & 31), k = s*16 + 8*(l >> 5) + j  (A and B maps coincide)
@@ -810,6 +875,8 @@ struct OrbitRescoreArgs {
     const int *member;              // [G][4]
     const uint8_t *dup;             // [G] bit x: slot x repeats a lower-index member's row
     const uint8_t *rep;             // [G] 2 bits per slot: slot of the lowest-index copy of its row
+    const GroupOrder *gorder;       // [G] ANN's order inside each group (null: lowest-index tie order)
+    const int *grp_of;              // [n] candidate -> g * 4 + slot
     const OrbitStat *ostat;
     const float *key;
     const int *id;
@@ -820,6 +887,9 @@ struct OrbitRescoreArgs {
     double scale2;                  // scale^2
     double N, Np, Hp, Ecp;
     OrbitTail t;
+#ifdef TILER_EXPERIMENTS
+    int kd_exp;
+#endif
 };
 
 // the reference distance (sequential fp32, every op rounded) with a short load window: the rescore
@@ -885,15 +955,48 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
     int cand = a.member[(long)g * 4 + x];
     if (cand < 0 || ((a.dup[g] >> x) & 1)) return -1;
     key = (double)a.nc[g] - 2.0 * (double)d;
-    if (a.t.ko && a.dup[g]) {  // identical rows of this slot's set: the one ANN finds first stands for them
+#ifdef TILER_EXPERIMENTS
+    if (a.kd_exp == 1) return cand;  // timing experiment: no class resolution (results invalid on such ties)
+#endif
+    if (a.gorder && a.dup[g]) {  // identical rows of this slot's set: the one ANN finds first stands for them
         const unsigned rep = a.rep[g];
         const float *qr = a.q + q * OD;
+        const GroupOrder go = a.gorder[g];
+        int bx = x;
         for (int y = 0; y < 4; y++) {
             const int cy = a.member[(long)g * 4 + y];
-            if (y != x && cy >= 0 && (int)((rep >> (2 * y)) & 3) == x && kd_before(a.t.ko, qr, cy, cand)) cand = cy;
+            if (y != x && cy >= 0 && (int)((rep >> (2 * y)) & 3) == x && group_before(go, qr, y, bx)) {
+                bx = y;
+                cand = cy;
+            }
         }
     }
     return cand;
+}
+
+// ANN's order of two candidates for query q: one cached compare when they share an orbit group, the root walk
+// (kdorder_dev.hpp) otherwise
+__device__ __forceinline__ bool orbit_before(const OrbitRescoreArgs &a, const float *__restrict__ q, int c1, int gs1,
+                                             int c2, int gs2) {
+    if (a.gorder && gs1 >= 0 && gs2 >= 0 && (gs1 >> 2) == (gs2 >> 2) && c1 != c2)
+        return group_before(a.gorder[gs1 >> 2], q, gs1 & 3, gs2 & 3);
+    return kd_before(a.t.ko, q, c1, c2);
+}
+
+// (dist, ANN order) minimum over a quad / half-wave: each lane holds (distance, candidate, its group code)
+template <int WIDTH>
+__device__ __forceinline__ void orbit_argmin(const OrbitRescoreArgs &a, const float *__restrict__ q, float &v, int &i,
+                                             int &gs) {
+#pragma unroll
+    for (int off = WIDTH / 2; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(v, off, 64);
+        const int oi = __shfl_xor(i, off, 64), og = __shfl_xor(gs, off, 64);
+        if (ov < v || (ov == v && orbit_before(a, q, oi, og, i, gs))) {
+            v = ov;
+            i = oi;
+            gs = og;
+        }
+    }
 }
 
 // The rescore runs one query per HALF-wave (32 lanes): it is latency-bound (list -> re-key -> rows ->
@@ -1006,7 +1109,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
     int *sc = s_cand[hq];
     const float *qrow = a.q + q * OD;
     float bd = INFINITY;
-    int bi = 0x7fffffff;
+    int bi = 0x7fffffff, bg = -1;
     int cnt = 0, nexp = 1, nres = 0;
     auto flush = [&]() {
         for (int b0 = 0; b0 < cnt; b0 += ORB_STG) {
@@ -1029,9 +1132,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
                     tt = x.z - y.z; dist = dist + tt * tt;
                     tt = x.w - y.w; dist = dist + tt * tt;
                 }
-                if (kd_less(t.ko, qrow, dist, c, bd, bi)) {
+                const int cg = a.grp_of ? a.grp_of[c] : -1;
+                if (dist < bd || (dist == bd && orbit_before(a, qrow, c, cg, bi, bg))) {
                     bd = dist;
                     bi = c;
+                    bg = cg;
                 }
             }
             __builtin_amdgcn_wave_barrier();
@@ -1078,7 +1183,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
         return;
     }
     flush();
-    kd_argmin<32>(t.ko, qrow, bd, bi);
+    orbit_argmin<32>(a, qrow, bd, bi, bg);
     if (l == 0) {
         if (t.n_expand) {
             atomicAdd(t.n_expand, nexp);
@@ -1110,14 +1215,15 @@ __global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a)
     const int n = a.pair_cnt[q];
     if (n == 0) return;  // uniform over the group
     float bd = INFINITY;
-    int bi = 0x7fffffff;
+    int bi = 0x7fffffff, bg = -1;
     if (s < n) {
         const int c = a.pair_cand[q * ORB_PSLOTS + s];
+        if (a.grp_of) bg = a.grp_of[c];
         bd = exact_dist192_lean(a.q + q * OD, a.rows + (long)c * OD);
         bi = c;
     }
     const OrbitTail &t = a.t;
-    kd_argmin<ORB_PSLOTS>(t.ko, a.q + q * OD, bd, bi);
+    orbit_argmin<ORB_PSLOTS>(a, a.q + q * OD, bd, bi, bg);
     if (t.ko) {  // ANN's box pruning along the winner's path, with the query row still in cache
         const bool ok = kd_quad_path_ok(t.ko, a.q + q * OD, t.ko->pos[bi], t.kd_rootbox[q], bd, s);
         if (s == 0) {
@@ -1208,6 +1314,8 @@ void orbit_destroy(OrbitIndex *o) {
     hipFree(o->d_member);
     hipFree(o->d_dup);
     hipFree(o->d_rep);
+    hipFree(o->d_gorder);
+    hipFree(o->d_grp_of);
     hipFree(o->d_map);
     hipFree(o->qfrag);
     hipFree(o->qrowh);
@@ -1294,6 +1402,13 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     TILER_HIP_CHECK(hipMalloc((void **)&o->d_rep, G));
     hipLaunchKernelGGL(orbit_dup_kernel, dim3((unsigned)std::min<long>(8192, (G + 3) / 4)), dim3(256), 0, stream,
                        ix->d_rows, o->d_member, G, o->d_dup, o->d_rep);
+    if (ix->kd) {  // ANN's order inside every group (the tree exists: nn_index_create_dev builds it first)
+        TILER_HIP_CHECK(hipMalloc((void **)&o->d_gorder, G * sizeof(GroupOrder)));
+        TILER_HIP_CHECK(hipMalloc((void **)&o->d_grp_of, n * sizeof(int)));
+        TILER_HIP_CHECK(hipMemsetAsync(o->d_grp_of, 0xff, n * sizeof(int), stream));
+        hipLaunchKernelGGL(orbit_gorder_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, stream, ix->kd->view(),
+                           o->d_member, G, o->d_gorder, o->d_grp_of);
+    }
     TILER_HIP_CHECK(hipGetLastError());
     TILER_HIP_CHECK(hipMalloc(&o->d_frag, (size_t)o->gblk * OS * 1024));
     TILER_HIP_CHECK(hipMalloc(&o->d_rowh, (size_t)G * OD * 2));
@@ -1436,6 +1551,8 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.member = o->d_member;
     ra.dup = o->d_dup;
     ra.rep = o->d_rep;
+    ra.gorder = tail.ko ? o->d_gorder : nullptr;
+    ra.grp_of = tail.ko ? o->d_grp_of : nullptr;
     ra.ostat = o->qstat;
     ra.key = o->key;
     ra.id = o->id;
@@ -1462,6 +1579,14 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.Ecp = o->Ecp;
     ra.t = tail;
     ra.t.thr_real = o->thr_real;
+#ifdef TILER_EXPERIMENTS
+    ra.kd_exp = getenv("TILER_KD_EXP") ? atoi(getenv("TILER_KD_EXP")) : 0;
+    if (ra.kd_exp == 2) {  // timing experiment: index-order comparisons in the orbit kernels
+        ra.t.ko = nullptr;
+        ra.gorder = nullptr;
+        ra.grp_of = nullptr;
+    }
+#endif
     static const bool want_stats = [] {
         const char *e = getenv("TILER_ORBIT_STATS");
         return e && e[0] == '1';

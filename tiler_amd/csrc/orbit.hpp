@@ -25,6 +25,16 @@ struct OrbitStat {
     int pad;
 };
 
+// ANN's visit order restricted to one orbit group's (<= 4) candidates: the kd-tree nodes that separate them
+// (<= 3, their lowest common nodes) and, per slot pair (x < y), which node decides and whether x lies LO.  With
+// it a tie between two members of one group costs 1 cached compare instead of a root-to-leaf walk.
+struct GroupOrder {
+    uint16_t cd[3];
+    uint16_t pad;
+    float cv[3];
+    uint32_t pairs;  // 3 bits per pair index (0,1) (0,2) (0,3) (1,2) (1,3) (2,3): node (2 bits) | x-on-LO << 2
+};
+
 struct OrbitIndex {
     int G = 0, gblk = 0;          // tile groups (orbits of candidates) and 32-group blocks
     void *d_frag = nullptr;       // [gblk][12][64][8] fp16 MFMA A fragments of c' = U c_base
@@ -34,6 +44,8 @@ struct OrbitIndex {
     int *d_member = nullptr;      // [G][4] candidate index of relative mirror slot m (H = 1, V = 2), -1 absent
     uint8_t *d_dup = nullptr;     // [G] bit m: slot m's row repeats a lower-index member's (symmetric tiles)
     uint8_t *d_rep = nullptr;     // [G] 2 bits per slot: the slot holding the lowest-index copy of its row
+    GroupOrder *d_gorder = nullptr;  // [G] (kd tie order only)
+    int *d_grp_of = nullptr;      // [n] candidate -> g * 4 + slot (kd tie order only; -1: not in a group)
     void *d_map = nullptr;        // OrbitMap
     double N = 0, Np = 0, Hp = 0, Ecp = 0;  // max ||c||, ||c'||, ||fp16(c')||, ||c' - fp16(c')||
     // per-call scratch

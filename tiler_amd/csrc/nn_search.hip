@@ -1128,10 +1128,11 @@ static int launch_exact(RescoreArgs ra, int list_n, int grid, hipStream_t stream
 }
 
 static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream);
-static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream);
+static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream,
+                       bool orbit_prepared);
 
 int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
-                  hipStream_t stream, bool rootbox_ready) {
+                  hipStream_t stream, bool rootbox_ready, bool orbit_prepared) {
     if (nq <= 0) return 0;
     if (k < 1 || k > 32) {
         set_error("nn: k must be in 1..32");
@@ -1169,7 +1170,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         TILER_HIP_CHECK(hipMemsetAsync(s.kd_done, 0, (size_t)nq, stream));
         TILER_HIP_CHECK(hipMemsetAsync(s.kd_count, 0, sizeof(int), stream));
     }
-    if (search_core(ix, ra, d_q, nq, k, stream)) return -1;
+    if (search_core(ix, ra, d_q, nq, k, stream, orbit_prepared)) return -1;
     if (!ix->kd) return 0;
     // ANN's box pruning along every result's path (queries the pair pass did not already check); the rare query
     // it cannot vouch for is replayed exactly
@@ -1188,7 +1189,8 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     return kd_verify_and_replay(ix->kd, fa, stream);
 }
 
-static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream) {
+static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream,
+                       bool orbit_prepared) {
     const bool mfma = ix->S > 0 && k <= 8;
     if (!mfma) {
         ix->last_splits = 0;
@@ -1242,7 +1244,7 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
         t.kd_done = s.kd_done;
         t.kd_list = s.kd_list;
         t.kd_count = s.kd_count;
-        if (orbit_search(ix, d_q, nq, t, stream)) return -1;
+        if (orbit_search(ix, d_q, nq, t, stream, orbit_prepared && k == 1)) return -1;
         ix->last_orbit = 1;
         ra.qstat = s.qstat;
         ra.fb_list = s.fb_list;
@@ -1336,15 +1338,22 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
         TILER_HIP_CHECK(hipMalloc((void **)&s.qrows, (size_t)Q * 192 * sizeof(float)));
         s.cap_rows = Q;
     }
+    const bool fuse_rb = ix->kd && use_wavelets && ix->kd->dd == 192;
+    if (fuse_rb && ensure_scratch(ix, Q, 0)) return -1;
+    if (ix->orbit && use_wavelets) {
+        // one kernel: descriptors + the orbit search's q' fragments and statistics (+ the kd root box)
+        if (orbit_ft_queries(ix, d_rgb, Q, gamma, s.qrows, fuse_rb ? ix->kd->d_box : nullptr,
+                             fuse_rb ? s.kd_rootbox : nullptr, stream))
+            return -1;
+        return nn_search_dev(ix, s.qrows, Q, 1, d_idx, d_err, maps, stream, fuse_rb, true);
+    }
     PsyvArgs pa;
     pa.n = Q;
     pa.rgb = d_rgb;
     pa.flags = use_wavelets ? PSYV_WAVELETS : 0;
     pa.gamma = gamma;
     pa.out32 = s.qrows;
-    const bool fuse_rb = ix->kd && use_wavelets && ix->kd->dd == 192;
     if (fuse_rb) {  // annBoxDistance of each query descriptor, in the descriptor kernel (kd pruning check)
-        if (ensure_scratch(ix, Q, 0)) return -1;
         pa.box = ix->kd->d_box;
         pa.rootbox = s.kd_rootbox;
     }

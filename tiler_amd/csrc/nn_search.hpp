@@ -90,7 +90,7 @@ struct FtMaps {
 // k nearest neighbours of nq fp32 query rows in HBM; results [nq][k] in HBM; async on stream.
 // If maps is non-null (k == 1) the FrameTiling tilemap items are written too.
 int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
-                  hipStream_t stream, bool rootbox_ready = false);
+                  hipStream_t stream, bool rootbox_ready = false, bool orbit_prepared = false);
 
 // frame tiling: RGB tiles -> descriptors (fp32) -> search -> tilemap items
 int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int *d_idx,

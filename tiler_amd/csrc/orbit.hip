@@ -23,6 +23,7 @@
 
 #include "kdorder_dev.hpp"
 #include "nn_dev.hpp"
+#include "psyv_dev.hpp"
 #include "orbit.hpp"
 
 namespace tiler {
@@ -297,12 +298,15 @@ __global__ __launch_bounds__(256) void orbit_gorder_kernel(KdOrder o, const int 
 }
 
 // ANN's order of two different slots of one group (both present) for query q
-__device__ __forceinline__ bool group_before(const GroupOrder &go, const float *__restrict__ q, int x, int y) {
+// (go points into HBM: indexing the node there is a plain load, a runtime index into a register copy would
+// put the struct in scratch)
+__device__ __forceinline__ bool group_before(const GroupOrder *__restrict__ go, const float *__restrict__ q, int x,
+                                             int y) {
     const int lo = min(x, y), hi = max(x, y);
     const int pi = lo == 0 ? hi - 1 : lo == 1 ? hi + 1 : 5;  // (0,1)(0,2)(0,3)(1,2)(1,3)(2,3)
-    const unsigned code = (go.pairs >> (3 * pi)) & 7u;
+    const unsigned code = (go->pairs >> (3 * pi)) & 7u;
     const int node = code & 3;
-    const bool lo_first = (q[go.cd[node]] - go.cv[node]) < 0.0f;
+    const bool lo_first = (q[go->cd[node]] - go->cv[node]) < 0.0f;
     const bool low_slot_first = ((code >> 2) & 1) == (unsigned)lo_first;
     return (x == lo) == low_slot_first;
 }
@@ -870,7 +874,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
 // ------------------------------------------------------------------------------------------
 struct OrbitRescoreArgs {
     const float *rows, *q;          // fp32 candidate rows [n][192], query rows [nq][192]
-    const _Float16 *rowh, *qrowh;   // fp16 c' [G][192], q' [nq][192]
+    const _Float16 *rowh;           // fp16 c' [G][192]
+    const half8 *qfrag;             // fp16 q' as MFMA B fragments [nqblk][12][64]
     const float *nc;                // [G]
     const int *member;              // [G][4]
     const uint8_t *dup;             // [G] bit x: slot x repeats a lower-index member's row
@@ -887,9 +892,6 @@ struct OrbitRescoreArgs {
     double scale2;                  // scale^2
     double N, Np, Hp, Ecp;
     OrbitTail t;
-#ifdef TILER_EXPERIMENTS
-    int kd_exp;
-#endif
 };
 
 // the reference distance (sequential fp32, every op rounded) with a short load window: the rescore
@@ -928,14 +930,15 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
     float d = 0.0f;
     if (gv) {  // fp16 products, fp32 sums (any order is inside the bound's gamma_{D+1} allowance)
         const uint4 *cr = reinterpret_cast<const uint4 *>(a.rowh + (long)g * OD + x * 48);
-        const uint4 *qr = reinterpret_cast<const uint4 *>(a.qrowh + q * OD + x * 48);
+        // q' of block x from the MFMA B fragments: 16-byte piece t = (k-step 3x + t/2, half t%2) of query q
+        const uint4 *qf = reinterpret_cast<const uint4 *>(a.qfrag) + ((q >> 5) * OS + 3 * x) * 64 + (q & 31);
 #pragma unroll
         for (int t0 = 0; t0 < 6; t0 += ORB_XB) {
             uint4 cv[ORB_XB], qv[ORB_XB];
 #pragma unroll
             for (int t = 0; t < ORB_XB; t++) {
                 cv[t] = cr[t0 + t];
-                qv[t] = qr[t0 + t];
+                qv[t] = qf[((t0 + t) >> 1) * 64 + 32 * ((t0 + t) & 1)];
             }
 #pragma unroll
             for (int t = 0; t < ORB_XB; t++) {
@@ -955,23 +958,28 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
     int cand = a.member[(long)g * 4 + x];
     if (cand < 0 || ((a.dup[g] >> x) & 1)) return -1;
     key = (double)a.nc[g] - 2.0 * (double)d;
-#ifdef TILER_EXPERIMENTS
-    if (a.kd_exp == 1) return cand;  // timing experiment: no class resolution (results invalid on such ties)
-#endif
-    if (a.gorder && a.dup[g]) {  // identical rows of this slot's set: the one ANN finds first stands for them
-        const unsigned rep = a.rep[g];
-        const float *qr = a.q + q * OD;
-        const GroupOrder go = a.gorder[g];
-        int bx = x;
-        for (int y = 0; y < 4; y++) {
-            const int cy = a.member[(long)g * 4 + y];
-            if (y != x && cy >= 0 && (int)((rep >> (2 * y)) & 3) == x && group_before(go, qr, y, bx)) {
-                bx = y;
-                cand = cy;
-            }
+    return cand;  // the lowest-index copy of its row; the final pick resolves the copies (class_first)
+}
+
+// A candidate the rescore queued stands for every member of its group with an identical row (orbit_dup_kernel
+// drops the others); under ANN's order the copy the kd-tree search finds first must be reported: resolved here,
+// at the final pick, lane-parallel (kept out of the latency-bound rescore chain).
+__device__ __forceinline__ void class_first(const OrbitRescoreArgs &a, const float *__restrict__ q, int &c, int &gs) {
+    if (!a.gorder || gs < 0) return;
+    const long g = gs >> 2;
+    const int x = gs & 3;
+    if (!a.dup[g]) return;
+    const unsigned rep = a.rep[g];
+    const GroupOrder *go = a.gorder + g;
+    int bx = x;
+    for (int y = 0; y < 4; y++) {
+        const int cy = a.member[g * 4 + y];
+        if (y != x && cy >= 0 && (int)((rep >> (2 * y)) & 3) == x && group_before(go, q, y, bx)) {
+            bx = y;
+            c = cy;
         }
     }
-    return cand;
+    gs = (int)(g * 4 + bx);
 }
 
 // ANN's order of two candidates for query q: one cached compare when they share an orbit group, the root walk
@@ -979,7 +987,7 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
 __device__ __forceinline__ bool orbit_before(const OrbitRescoreArgs &a, const float *__restrict__ q, int c1, int gs1,
                                              int c2, int gs2) {
     if (a.gorder && gs1 >= 0 && gs2 >= 0 && (gs1 >> 2) == (gs2 >> 2) && c1 != c2)
-        return group_before(a.gorder[gs1 >> 2], q, gs1 & 3, gs2 & 3);
+        return group_before(a.gorder + (gs1 >> 2), q, gs1 & 3, gs2 & 3);
     return kd_before(a.t.ko, q, c1, c2);
 }
 
@@ -1132,10 +1140,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
                     tt = x.z - y.z; dist = dist + tt * tt;
                     tt = x.w - y.w; dist = dist + tt * tt;
                 }
-                const int cg = a.grp_of ? a.grp_of[c] : -1;
-                if (dist < bd || (dist == bd && orbit_before(a, qrow, c, cg, bi, bg))) {
+                int cg = a.grp_of ? a.grp_of[c] : -1, cc = c;
+                class_first(a, qrow, cc, cg);
+                if (dist < bd || (dist == bd && orbit_before(a, qrow, cc, cg, bi, bg))) {
                     bd = dist;
-                    bi = c;
+                    bi = cc;
                     bg = cg;
                 }
             }
@@ -1217,9 +1226,12 @@ __global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a)
     float bd = INFINITY;
     int bi = 0x7fffffff, bg = -1;
     if (s < n) {
-        const int c = a.pair_cand[q * ORB_PSLOTS + s];
-        if (a.grp_of) bg = a.grp_of[c];
+        int c = a.pair_cand[q * ORB_PSLOTS + s];
         bd = exact_dist192_lean(a.q + q * OD, a.rows + (long)c * OD);
+        if (a.grp_of) {
+            bg = a.grp_of[c];
+            class_first(a, a.q + q * OD, c, bg);  // same row, same distance
+        }
         bi = c;
     }
     const OrbitTail &t = a.t;
@@ -1297,6 +1309,180 @@ __global__ __launch_bounds__(256) void orbit_fbprep_kernel(OrbitFbArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// device: FrameTiling queries in one pass (DoFrameTiling main.pas:4023-4025): RGB tile -> Haar PsyV (fp64, one
+// lane per tile, psyv_dev.hpp) -> fp32 row (the exact rescoring operand) + the orbit transform q' = U' q as fp16
+// MFMA B fragments + its error statistics (orbit_prep_kernel's math) + annBoxDistance to the kd-tree's box.
+// The descriptors never round-trip HBM between the two steps.
+// ------------------------------------------------------------------------------------------
+struct FtQueryArgs {
+    const int32_t *rgb;
+    long n;
+    int gamma;
+    const double *gamma_lut;
+    double haar_f, u_mul, v_mul;
+    const OrbitMap *mp;
+    float scale;
+    float *out32;        // [n][192]
+    half8 *frag;         // [ceil(n/32)][12][64]
+    OrbitStat *qstat;    // [n]
+    const float *box;    // [2][192] or null
+    float *rootbox;      // [n] when box
+};
+
+template <bool FASTDIV>
+__global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
+    __shared__ double lut[256];
+    __shared__ float st[64 * 65];  // one component of the 64 tiles: row-major per lane, stride 65 (conflict-free)
+    __shared__ float sbox[2 * OD];
+    __shared__ int16_t msrc[OD * 4];
+    __shared__ float mw[OD * 4], mq[OD];
+    const int lane = threadIdx.x;
+    const double *__restrict__ glut = a.gamma_lut + 256 * (a.gamma + 1);
+    for (int i = lane; i < 256; i += 64) lut[i] = glut[i];
+    for (int i = lane; i < OD * 4; i += 64) {
+        msrc[i] = a.mp->src[i >> 2][i & 3];
+        mw[i] = a.mp->w[i >> 2][i & 3];
+    }
+    for (int i = lane; i < OD; i += 64) mq[i] = a.mp->qs[i];
+    if (a.box)
+        for (int i = lane; i < 2 * OD; i += 64) sbox[i] = a.box[i];
+    __syncthreads();
+    const long t0 = (long)blockIdx.x * 64;
+    const long i = t0 + lane;
+    const bool valid = i < a.n;
+    const long nqblk = (a.n + 31) / 32;
+    const bool has_blk = (i >> 5) < nqblk;
+    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + (valid ? i : t0) * 64);
+    double n2 = 0, h2 = 0, e2 = 0;
+    int bad = 0;
+    float rb = 0.0f;
+    const float *row = st + lane * 65;
+#pragma unroll 1
+    for (int c = 0; c < 3; c++) {
+        double p[64];
+#pragma unroll
+        for (int k4 = 0; k4 < 16; k4++) {
+            const int4 v = src[k4];
+            const int cc[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int r = cc[e] & 0xff, g = (cc[e] >> 8) & 0xff, b = (cc[e] >> 16) & 0xff;
+                const double fr = lut[r], fg = lut[g], fb = lut[b];
+                const double cy = div10000<FASTDIV>(2126.0 * fr + 7152.0 * fg + 722.0 * fb);
+                p[4 * k4 + e] = c == 0 ? cy : c == 1 ? (fb - cy) * a.u_mul : (fr - cy) * a.v_mul;
+            }
+        }
+        haar_regs(p, a.haar_f);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 64; k++) st[lane * 65 + k] = (float)p[k];
+        if (a.box) {
+#pragma unroll 4
+            for (int k = 0; k < 64; k++) {  // annBoxDistance, dimension order
+                const float v = row[k];
+                const float lo = sbox[c * 64 + k], hi = sbox[OD + c * 64 + k];
+                if (v < lo) {
+                    const float t = lo - v;
+                    rb = rb + t * t;
+                } else if (v > hi) {
+                    const float t = v - hi;
+                    rb = rb + t * t;
+                }
+            }
+        }
+        __syncthreads();
+        // fp32 rows: 16 lanes per tile store its 256-byte component segment
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const int pc = lane + 64 * t, tt = pc >> 4, c4 = pc & 15;
+            if (t0 + tt < a.n) {
+                const float *q = st + tt * 65 + c4 * 4;
+                reinterpret_cast<float4 *>(a.out32 + (t0 + tt) * OD + c * 64)[c4] = make_float4(q[0], q[1], q[2], q[3]);
+            }
+        }
+        if (valid) {
+#pragma unroll 8
+            for (int k = 0; k < 64; k++) {
+                const double orig = (double)row[k] * (double)a.scale;
+                n2 += orig * orig;
+            }
+        }
+        // orbit transform of this component: k-steps s = 3x + c, 16 outputs each (orbit_prep_kernel's math)
+#pragma unroll 1
+        for (int x = 0; x < 4; x++) {
+            const int s = 3 * x + c;
+            half8 hv[2];
+#pragma unroll 4
+            for (int j = 0; j < 16; j++) {
+                const int k = s * 16 + j;
+                double v = 0.0;
+                if (valid) {
+#pragma unroll
+                    for (int t = 0; t < 4; t++) v += (double)mw[k * 4 + t] * (double)row[(msrc[k * 4 + t] - 64 * c) & 63];
+                    v *= (double)mq[k] * (double)a.scale;
+                }
+                _Float16 vh = (_Float16)(float)v;
+                if (fabs((double)(float)vh) < 6.103515625e-05) vh = (_Float16)0.0f;  // no fp16 subnormal operands
+                hv[j >> 3][j & 7] = vh;
+                const double dh = (double)(float)vh;
+                h2 += dh * dh;
+                e2 += (v - dh) * (v - dh);
+                if (!isfinite(v) || fabs(v) > 65000.0) bad = 1;
+            }
+            if (has_blk) {
+                half8 *f = a.frag + ((i >> 5) * OS + s) * 64 + (i & 31);
+                f[0] = hv[0];
+                f[32] = hv[1];
+            }
+        }
+    }
+    if (valid) {
+        OrbitStat q;
+        q.n2 = n2;
+        q.hn = sqrt(h2);
+        q.en = sqrt(e2);
+        q.flags = (bad || !isfinite(n2)) ? 2 : 0;
+        q.pad = 0;
+        a.qstat[i] = q;
+        if (a.rootbox) a.rootbox[i] = rb;
+    }
+}
+
+int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float *qrows, const float *box,
+                     float *rootbox, hipStream_t stream) {
+    OrbitIndex *o = ix->orbit;
+    if (orbit_ensure_queries(o, Q)) return -1;
+    if (gamma < -1 || gamma > 1) {
+        set_error("frame tiling: gamma must be -1, 0 or 1");
+        return -1;
+    }
+    const Luts &L = luts();
+    FtQueryArgs fa;
+    fa.rgb = d_rgb;
+    fa.n = Q;
+    fa.gamma = gamma;
+    fa.gamma_lut = L.d_gamma;
+    fa.haar_f = L.haar_f;
+    fa.u_mul = L.u_mul;
+    fa.v_mul = L.v_mul;
+    fa.mp = (const OrbitMap *)o->d_map;
+    fa.scale = ix->scale;
+    fa.out32 = qrows;
+    fa.frag = (half8 *)o->qfrag;
+    fa.qstat = o->qstat;
+    fa.box = box;
+    fa.rootbox = rootbox;
+    const dim3 grid((unsigned)((Q + 63) / 64));
+    KTimer tm("psyv", stream);
+    if (gamma == -1)
+        hipLaunchKernelGGL(orbit_ft_query_kernel<true>, grid, dim3(64), 0, stream, fa);
+    else
+        hipLaunchKernelGGL(orbit_ft_query_kernel<false>, grid, dim3(64), 0, stream, fa);
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------------
 // host
 // ------------------------------------------------------------------------------------------
 static double bits2d(unsigned long long b) {
@@ -1318,7 +1504,6 @@ void orbit_destroy(OrbitIndex *o) {
     hipFree(o->d_grp_of);
     hipFree(o->d_map);
     hipFree(o->qfrag);
-    hipFree(o->qrowh);
     hipFree(o->qstat);
     hipFree(o->thr_real);
     hipFree(o->pair_cnt);
@@ -1439,7 +1624,25 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
 
 static constexpr int ORB_L = 4, ORB_CB = 4, ORB_NW = 8;
 
-int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, hipStream_t stream) {
+int orbit_ensure_queries(OrbitIndex *o, int nq) {
+    if ((size_t)nq <= o->cap_q) return 0;
+    const long nqblk = (nq + 31) / 32;
+    hipFree(o->qfrag);
+    hipFree(o->qstat);
+    hipFree(o->thr_real);
+    hipFree(o->pair_cnt);
+    hipFree(o->pair_cand);
+    TILER_HIP_CHECK(hipMalloc((void **)&o->thr_real, (size_t)nq * sizeof(double)));
+    TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cnt, (size_t)nq * sizeof(int)));
+    TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cand, (size_t)nq * ORB_PSLOTS * sizeof(int)));
+    TILER_HIP_CHECK(hipMalloc(&o->qfrag, (size_t)(nqblk + 1) * OS * 1024));
+    TILER_HIP_CHECK(hipMalloc((void **)&o->qstat, (size_t)nq * sizeof(OrbitStat)));
+    o->cap_q = nq;
+    return 0;
+}
+
+int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, hipStream_t stream,
+                 bool queries_prepared) {
     OrbitIndex *o = ix->orbit;
     const int nqblk = (nq + 31) / 32;
 #ifdef TILER_EXPERIMENTS
@@ -1470,25 +1673,27 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     const bool use_pipe = pipe && qb == 2 && mode == 0 && nw == ORB_NW;
     const int wgs = (nqblk + nw * qb - 1) / (nw * qb);
     const int max_split = 32 / (2 * ORB_L);  // rescore: one list entry per lane of a half-wave
-    int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
-    nsplit = std::min(nsplit, o->gblk);
+    // One 8-wave workgroup fills a CU (2 waves per SIMD), so a launch runs in rounds of n_cu workgroups and takes
+    // ~ ceil(wgs * ns / n_cu) / ns workgroup-times for ns candidate splits: pick the smallest, preferring fewer
+    // splits (each adds list entries to rescore) unless more are >= 2 % faster.  C3: 1,519 workgroups, 1 split
+    // (5.93 -> 6 rounds); C2: 675 workgroups, 3 splits (7.91 -> 8 rounds of 1/3 the work; 2 splits: 6 rounds of 1/2).
+    static const int n_cu = [] {
+        int dev = 0, cu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+        return cu > 0 ? cu : 256;
+    }();
+    int nsplit = 1;
+    double best_t = 1e30;
+    for (int ns = 1; ns <= max_split && ns <= o->gblk; ns++) {
+        const double t = std::ceil((double)wgs * ns / n_cu) / ns;
+        if (t < best_t * 0.98) {
+            best_t = t;
+            nsplit = ns;
+        }
+    }
     const int bps = (o->gblk + nsplit - 1) / nsplit;
     nsplit = (o->gblk + bps - 1) / bps;
-    if ((size_t)nq > o->cap_q) {
-        hipFree(o->qfrag);
-        hipFree(o->qrowh);
-        hipFree(o->qstat);
-        hipFree(o->thr_real);
-        hipFree(o->pair_cnt);
-        hipFree(o->pair_cand);
-        TILER_HIP_CHECK(hipMalloc((void **)&o->thr_real, (size_t)nq * sizeof(double)));
-        TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cnt, (size_t)nq * sizeof(int)));
-        TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cand, (size_t)nq * ORB_PSLOTS * sizeof(int)));
-        TILER_HIP_CHECK(hipMalloc(&o->qfrag, (size_t)(nqblk + 1) * OS * 1024));
-        TILER_HIP_CHECK(hipMalloc(&o->qrowh, (size_t)nq * OD * 2));
-        TILER_HIP_CHECK(hipMalloc((void **)&o->qstat, (size_t)nq * sizeof(OrbitStat)));
-        o->cap_q = nq;
-    }
+    if (orbit_ensure_queries(o, nq)) return -1;
     const size_t nkeys = (size_t)nq * nsplit * 2 * ORB_L;
     if (nkeys > o->cap_keys) {
         hipFree(o->key);
@@ -1497,14 +1702,14 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         TILER_HIP_CHECK(hipMalloc((void **)&o->id, nkeys * sizeof(int)));
         o->cap_keys = nkeys;
     }
-    {
+    if (!queries_prepared) {  // (the FrameTiling path prepares them inside its descriptor kernel, orbit_ft_queries)
         OrbitPrepArgs pa{d_q, nullptr, nq, (const OrbitMap *)o->d_map, ix->scale, (half8 *)o->qfrag,
-                         (_Float16 *)o->qrowh, nullptr, nullptr, nullptr, o->qstat};
+                         nullptr, nullptr, nullptr, nullptr, o->qstat};
         KTimer tm("nn_prep", stream);
         hipLaunchKernelGGL(orbit_prep_kernel, dim3((unsigned)std::min<long>(4096, (nqblk + ORB_PW - 1) / ORB_PW)),
                            dim3(64 * ORB_PW), 0, stream, pa);
+        TILER_HIP_CHECK(hipGetLastError());
     }
-    TILER_HIP_CHECK(hipGetLastError());
     {
         const size_t lds = 2 * ((size_t)ORB_CB * OS * 1024 + ORB_CB * 128);
         KTimer tm("nn_orbit", stream);
@@ -1546,7 +1751,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.rows = ix->d_rows;
     ra.q = d_q;
     ra.rowh = (const _Float16 *)o->d_rowh;
-    ra.qrowh = (const _Float16 *)o->qrowh;
+    ra.qfrag = (const half8 *)o->qfrag;
     ra.nc = o->d_nc;
     ra.member = o->d_member;
     ra.dup = o->d_dup;
@@ -1580,8 +1785,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.t = tail;
     ra.t.thr_real = o->thr_real;
 #ifdef TILER_EXPERIMENTS
-    ra.kd_exp = getenv("TILER_KD_EXP") ? atoi(getenv("TILER_KD_EXP")) : 0;
-    if (ra.kd_exp == 2) {  // timing experiment: index-order comparisons in the orbit kernels
+    if (getenv("TILER_KD_EXP") && atoi(getenv("TILER_KD_EXP")) == 2) {  // timing: index-order compares (invalid)
         ra.t.ko = nullptr;
         ra.gorder = nullptr;
         ra.grp_of = nullptr;

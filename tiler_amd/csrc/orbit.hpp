@@ -49,7 +49,7 @@ struct OrbitIndex {
     void *d_map = nullptr;        // OrbitMap
     double N = 0, Np = 0, Hp = 0, Ecp = 0;  // max ||c||, ||c'||, ||fp16(c')||, ||c' - fp16(c')||
     // per-call scratch
-    void *qfrag = nullptr, *qrowh = nullptr;
+    void *qfrag = nullptr;        // [nqblk][12][64][8] fp16 q' (MFMA B fragments; the rescore re-keys from them)
     OrbitStat *qstat = nullptr;
     double *thr_real = nullptr;
     int *pair_cnt = nullptr, *pair_cand = nullptr;  // rescore -> pair pass hand-off
@@ -87,7 +87,14 @@ void orbit_destroy(OrbitIndex *o);
 inline long long orbit_groups(const NNIndex *ix) { return ix->orbit ? ((const OrbitIndex *)ix->orbit)->G : 0; }
 // rescore counters of the last search (TILER_ORBIT_STATS=1, else 0): 4-entry expansion passes, candidates rescored
 void orbit_counters(const NNIndex *ix, long long *expansions, long long *rescored);
-// k = 1 search of nq fp32 query rows: query prep, orbit shortlist, orbit rescore (tiers 2/3 by the caller)
-int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, hipStream_t stream);
+// k = 1 search of nq fp32 query rows: query prep, orbit shortlist, orbit rescore (tiers 2/3 by the caller);
+// queries_prepared: orbit_ft_queries already wrote this call's fragments and statistics
+int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, hipStream_t stream,
+                 bool queries_prepared = false);
+int orbit_ensure_queries(OrbitIndex *o, int nq);
+// FrameTiling queries in one kernel: RGB tiles -> Haar descriptors (qrows[Q][192] fp32) + q' fragments + stats
+// (+ rootbox[Q] = annBoxDistance to box[2][192] when box != null)
+int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float *qrows, const float *box,
+                     float *rootbox, hipStream_t stream);
 
 }  // namespace tiler

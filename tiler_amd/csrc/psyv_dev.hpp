@@ -56,4 +56,52 @@ __device__ __forceinline__ double dct_lane(double cp, int lane, int c, bool qwei
     return z * k.ratio[lane];
 }
 
+// The 3-level WaveletGS of one 8x8 component held by ONE lane (compile-time indices, no cross-lane traffic):
+// the same fp64 operations in the same order as haar3 / the CPU restatement.
+__device__ __forceinline__ void haar_regs(double (&p)[64], double f) {
+#pragma unroll
+    for (int dx = 8; dx >= 2; dx >>= 1) {
+        const int h = dx >> 1;
+#pragma unroll
+        for (int y = 0; y < dx; y++) {  // rows: L at x, H at x + dx/2
+            double t[8];
+#pragma unroll
+            for (int x = 0; x < h; x++) {
+                const double a = p[y * 8 + 2 * x], b = p[y * 8 + 2 * x + 1];
+                t[x] = (a + b) * f;
+                t[x + h] = (a - b) * f;
+            }
+#pragma unroll
+            for (int x = 0; x < dx; x++) p[y * 8 + x] = t[x];
+        }
+#pragma unroll
+        for (int x = 0; x < dx; x++) {  // columns
+            double t[8];
+#pragma unroll
+            for (int y = 0; y < h; y++) {
+                const double a = p[(2 * y) * 8 + x], b = p[(2 * y + 1) * 8 + x];
+                t[y] = (a + b) * f;
+                t[y + h] = (a - b) * f;
+            }
+#pragma unroll
+            for (int y = 0; y < dx; y++) p[y * 8 + x] = t[y];
+        }
+    }
+}
+
+// x / 10000.0 for the gamma = -1 colour sums (fr = r / 255.0): q0 = x * RN(1e-4) plus one fma residual
+// correction.  Bit-identical to the IEEE division over every (r, g, b) of the domain (all 2^24 sums checked
+// by oracle/check_fastdiv.c, tests/test_oracle_kats.py); other gamma LUTs keep the true division.
+template <bool FASTDIV>
+__device__ __forceinline__ double div10000(double x) {
+    if constexpr (FASTDIV) {
+        const double inv = 1.0 / 10000.0;
+        const double q0 = x * inv;
+        return __builtin_fma(__builtin_fma(-q0, 10000.0, x), inv, q0);
+    } else {
+        return x / 10000.0;
+    }
+}
+
+
 }  // namespace tiler

@@ -322,7 +322,7 @@ struct OrbitPrepArgs {
     const OrbitMap *mp;
     float scale;
     half8 *frag;           // [ceil(count/32)][12][64]
-    _Float16 *rowh;        // [count][192]
+    _Float16 *rowh;        // [count][192] (dataset only: the query path keeps q' in the fragments; null)
     float *seed, *nc;      // dataset only
     OrbitDsStat *ds;       // dataset only
     OrbitStat *qstat;      // queries only
@@ -409,7 +409,7 @@ __global__ __launch_bounds__(64 * ORB_PW) void orbit_prep_kernel(OrbitPrepArgs a
                     if (!isfinite(v) || fabs(v) > 65000.0) bad = 1;
                 }
                 if (blk < nblk) a.frag[(blk * OS + s) * 64 + lane] = hv;
-                if (valid) *reinterpret_cast<half8 *>(a.rowh + r * OD + s * 16 + 8 * h) = hv;
+                if (valid && a.rowh) *reinterpret_cast<half8 *>(a.rowh + r * OD + s * 16 + 8 * h) = hv;
             }
         }
         if (blk >= nblk) continue;

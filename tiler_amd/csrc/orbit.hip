@@ -1412,8 +1412,8 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
         for (int x = 0; x < 4; x++) {
             const int s = 3 * x + c;
             half8 hv[2];
-#pragma unroll 4
-            for (int j = 0; j < 16; j++) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) {  // constant j: hv stays in registers (no dynamic vector index)
                 const int k = s * 16 + j;
                 double v = 0.0;
                 if (valid) {

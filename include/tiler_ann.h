@@ -184,6 +184,25 @@ int tiler_dither_tiles(int n, const int32_t *rgb, const int32_t *pal_of, const i
 int tiler_dither_tiles_dev(int n, const int32_t *d_rgb, const int32_t *d_pal_of, const int32_t *d_palettes,
                            int n_palettes, int palsize, uint8_t *d_palpix, uint8_t *d_hm, uint8_t *d_vm, void *stream);
 
+/* ---- Dither step, palette generation (QuantizePalette / FinishQuantizePalette) ------------
+ * QuantizePalette with the default Dennis Lee v3 quantizer (chkUseDL3, main.pas:2154-2254 -> dl3quant,
+ * dlquant/quantizer.c:437-663) for n_palettes (keyframe, palette) pairs at once: tiles rgb[n_tiles][64] (0x00BBGGRR,
+ * each keyframe's frames in order), pal_of[n_tiles] the pair of each tile (DitheringPalIndex, stacked over
+ * keyframes as kf * FPaletteCount + palette; out-of-range indices are skipped), active[n_tiles] or NULL (all
+ * Active) -> palettes[n_palettes][palsize] (PaletteIndexes: the palsize DLv3 colours sorted by CompareCMULHS,
+ * main.pas:2413-2417; 0 beyond a table that has fewer colours), use_count[n_palettes] (PaletteUseCount.UseCount),
+ * colors[n_palettes] or NULL (the DLv3 colour-table size of each pair).  lookup_bpc = cbxDLBPC (7 by default,
+ * 1..8).  Outputs are host arrays in both forms.  0 / -1. */
+int tiler_quantize_palettes(long n_tiles, const int32_t *rgb, const int32_t *pal_of, const uint8_t *active,
+                            int n_palettes, int palsize, int lookup_bpc, int32_t *palettes, int32_t *use_count,
+                            int32_t *colors);
+int tiler_quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_pal_of, const uint8_t *d_active,
+                                int n_palettes, int palsize, int lookup_bpc, int32_t *palettes, int32_t *use_count,
+                                int32_t *colors, void *stream);
+/* FinishQuantizePalette's order of one keyframe's palettes (main.pas:2444-2455): the reference QuickSort
+ * (kmodes.pas:89-136) by use count, descending -> lut[old palette] = new palette.  0 / -1. */
+int tiler_finish_quantize_order(int n_palettes, const int32_t *use_count, int32_t *lut);
+
 /* ---- GTM keyframe stream compression (host code) ---------------------------------------------------
  * Replaces LZCompress (extern.pas:202-240: temp file + external `lzma.exe e src dst -lc8 -eos`, called
  * per keyframe by SaveStream main.pas:4734).  Writes an LZMA-alone stream (13-byte header: properties

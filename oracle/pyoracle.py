@@ -341,3 +341,47 @@ def ref_kmodes_lib():
     r = ctypes.CDLL(REF_LIB)
     r.ref_get_min.restype = ctypes.c_int64
     return r
+
+
+# ---- palette generation (palette.c): QuantizePalette with DLv3, CompareCMULHS, FinishQuantizePalette ----
+def dl3quant(pixels, quant_to=16, bpc=7):
+    """dl3quant over pixels [n][3] u8 (R, G, B): (palette [quant_to] 0x00BBGGRR, histogram colour count)."""
+    px = np.ascontiguousarray(pixels, np.uint8).reshape(-1, 3)
+    out = np.zeros(quant_to, np.int32)
+    h = lib().or_dl3quant(_p(px), ctypes.c_long(px.shape[0]), quant_to, bpc, _p(out))
+    return out, int(h)
+
+
+def rgb_to_hsv(col):
+    h, s, v = ctypes.c_uint8(), ctypes.c_uint8(), ctypes.c_uint8()
+    lib().or_rgb_to_hsv(int(np.int32(col)), ctypes.byref(h), ctypes.byref(s), ctypes.byref(v))
+    return h.value, s.value, v.value
+
+
+def sort_cmulhs(cols):
+    cols = np.ascontiguousarray(cols, np.int32)
+    out = np.zeros_like(cols)
+    lib().or_sort_cmulhs(_p(cols), cols.size, _p(out))
+    return out
+
+
+def quantize_palettes(rgb, pal_of, n_palettes, palsize=16, bpc=7, active=None, threads=None):
+    """QuantizePalette for every palette of one keyframe: rgb [n][64] (0x00BBGGRR), pal_of [n] ->
+    (palettes [P][palsize], use_count [P], histogram colour counts [P])."""
+    rgb = np.ascontiguousarray(rgb, np.int32).reshape(-1, 64)
+    pal_of = np.ascontiguousarray(pal_of, np.int32)
+    act = None if active is None else np.ascontiguousarray(active, np.uint8)
+    pal = np.zeros((n_palettes, palsize), np.int32)
+    uc = np.zeros(n_palettes, np.int32)
+    hist = np.zeros(n_palettes, np.int32)
+    lib().or_quantize_palettes(_p(rgb), _p(pal_of), _p(act), ctypes.c_long(rgb.shape[0]), n_palettes, palsize, bpc,
+                               _p(pal), _p(uc), _p(hist), threads or _threads())
+    return pal, uc, hist
+
+
+def finish_quantize_order(use_count):
+    """FinishQuantizePalette's order: lut[old palette] = new palette index."""
+    uc = np.ascontiguousarray(use_count, np.int32)
+    lut = np.zeros(uc.size, np.int32)
+    lib().or_finish_quantize_order(_p(uc), uc.size, _p(lut))
+    return lut

@@ -111,6 +111,16 @@ void or_tk_plan(const int32_t *pal, int palsize, int32_t col, uint8_t *list);
 void or_dither_tiles_tk(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int palsize,
                         uint8_t *palpix, uint8_t *hm, uint8_t *vm);
 
+
+/* palette generation (palette.c): QuantizePalette / DLv3 / FinishQuantizePalette, main.pas:2154-2480 */
+int or_dl3quant(const uint8_t *rgb, long npix, int quant_to, int lookup_bpc, int32_t *pal);
+void or_rgb_to_hsv(int32_t col, uint8_t *h, uint8_t *s, uint8_t *v);
+int32_t or_color_luma(int32_t col);
+void or_sort_cmulhs(const int32_t *cols, int n, int32_t *out);
+void or_quantize_palettes(const int32_t *rgb, const int32_t *pal_of, const uint8_t *active, long n, int P,
+                          int palsize, int bpc, int32_t *pal_out, int32_t *use_count, int32_t *hist, int threads);
+void or_finish_quantize_order(const int32_t *use_count, int P, int32_t *lut);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,7 +34,9 @@ def test_library_exports_every_header_symbol():
 def test_library_is_gfx950_code_object():
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
-    assert b"gfx942" not in blob and b"gfx90a" not in blob  # gfx950 only, no multi-target dispatch
+    import re
+    targets = set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-f]+)", blob))
+    assert targets == {b"gfx950"}, targets  # gfx950 code objects only, no multi-target dispatch
 
 
 def test_no_cpu_fallback_without_gpu():
@@ -67,4 +69,3 @@ def test_shipped_library_ignores_experiment_switches():
     if os.path.exists(exp):  # the experiment build carries the switches and their kernel variants
         eblob = open(exp, "rb").read()
         assert all(s.encode() in eblob for s in EXPERIMENT_SWITCHES)
-        assert len(eblob) > len(blob)

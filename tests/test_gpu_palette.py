@@ -1,0 +1,68 @@
+"""GPU parity of palette generation: tiler_quantize_palettes (QuantizePalette with DLv3 for
+every (keyframe, palette) pair at once, CompareCMULHS order) bit-exact against the CPU restatement
+(oracle/palette.c) -- palettes, use counts and DLv3 colour-table sizes -- on textured / gradient / flat tiles,
+empty pairs, pairs with fewer colours than the palette, skipped (inactive / out-of-range) tiles and lookup bpc
+4..8.  The oracle is unpinned against the reference DLL (quantizer.c is not buildable here)."""
+import numpy as np
+import pytest
+
+from tiler_amd import synth
+from tiler_amd.palette import quantize_palettes
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(seed, kf_frames, q, P, flat_share=0.0):
+    rng = np.random.default_rng(seed)
+    tiles = [synth.keyframe_frames(rng, f, q).reshape(-1, 64) for f in kf_frames]
+    pal_of = [rng.integers(0, P, t.shape[0]) + k * P for k, t in enumerate(tiles)]
+    rgb = np.concatenate(tiles)
+    if flat_share:
+        flat = rng.random(rgb.shape[0]) < flat_share
+        rgb[flat] = rgb[flat, :1]
+    return rgb, np.concatenate(pal_of).astype(np.int32), len(kf_frames) * P
+
+
+def _check(oracle, rgb, pal_of, pairs, bpc=7, active=None):
+    g_pal, g_uc, g_h = quantize_palettes(rgb, pal_of, pairs, 16, bpc, active)
+    o_pal, o_uc, o_h = oracle.quantize_palettes(rgb, pal_of, pairs, 16, bpc, active)
+    assert np.array_equal(g_uc, o_uc)
+    assert np.array_equal(g_h, o_h)
+    bad = np.nonzero(np.any(g_pal != o_pal, 1))[0]
+    assert bad.size == 0, (bad[:5], g_pal[bad[:2]], o_pal[bad[:2]])
+    return g_h
+
+
+def test_quantize_two_keyframes(gpu, oracle):
+    rgb, pal_of, pairs = _case(1, (3, 2), 120, 6)
+    h = _check(oracle, rgb, pal_of, pairs)
+    assert h.max() > 1000  # textured tiles: the O(n^2) passes are exercised
+
+
+@pytest.mark.parametrize("bpc", [4, 5, 6, 8])
+def test_quantize_bpc(gpu, oracle, bpc):
+    rgb, pal_of, pairs = _case(2 + bpc, (2,), 100, 4)
+    _check(oracle, rgb, pal_of, pairs, bpc)
+
+
+def test_quantize_edges(gpu, oracle):
+    rgb, pal_of, pairs = _case(7, (2, 2), 60, 5, flat_share=0.6)
+    pal_of[pal_of == 3] = 4       # pair 3 empty
+    pal_of[::17] = 99             # out of range: skipped
+    few = pal_of == 6             # pair 6: a handful of flat colours (fewer than 16)
+    rgb[few] = np.int32(0x102030) + (np.arange(few.sum()) % 5)[:, None].astype(np.int32)
+    active = (np.arange(rgb.shape[0]) % 11 != 0).astype(np.uint8)
+    h = _check(oracle, rgb, pal_of, pairs, 7, active)
+    assert h[3] == 0 and 0 < h[6] < 16
+
+
+def test_quantize_clustered_long_recount_lists(gpu, oracle):
+    """Few dominant colours with small noise: many entries share a nearest neighbour, so the merges' recount
+    lists grow past the block-wide threshold (the wave-parallel path)."""
+    rng = np.random.default_rng(11)
+    base = rng.integers(0, 256, (6, 3))
+    n = 1500
+    px = np.clip(base[rng.integers(0, 6, (n, 64))] + rng.integers(-10, 11, (n, 64, 3)), 0, 255).astype(np.int32)
+    rgb = px[..., 0] | (px[..., 1] << 8) | (px[..., 2] << 16)
+    pal_of = rng.integers(0, 3, n).astype(np.int32)
+    _check(oracle, rgb, pal_of, 3)

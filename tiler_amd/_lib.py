@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libANN.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tiler_ann.h")
 
 c_int = ctypes.c_int
+c_long = ctypes.c_long
 c_float = ctypes.c_float
 c_double = ctypes.c_double
 c_void_p = ctypes.c_void_p
@@ -81,6 +82,11 @@ _SIGS = {
     "tiler_dither_tiles": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "tiler_dither_tiles_dev": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                        c_void_p]),
+    "tiler_quantize_palettes": (c_int, [c_long, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                        c_void_p]),
+    "tiler_quantize_palettes_dev": (c_int, [c_long, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                            c_void_p, c_void_p, c_void_p]),
+    "tiler_finish_quantize_order": (c_int, [c_int, c_void_p, c_void_p]),
     "tiler_interframe_correlation": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "tiler_interframe_correlation_dev": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "tiler_find_keyframes": (c_int, [c_void_p, c_int, c_int, c_void_p]),

@@ -14,6 +14,7 @@
 
 #include "../../include/tiler_ann.h"
 #include "dither.hpp"
+#include "palette.hpp"
 #include "keyframes.hpp"
 #include "kmodes.hpp"
 #include "nn_search.hpp"
@@ -596,6 +597,31 @@ int tiler_dither_tiles_dev(int n, const int32_t *d_rgb, const int32_t *d_pal_of,
     if (!ensure_init()) return -1;
     return dither_tiles_tk_dev(n, d_rgb, d_pal_of, d_palettes, n_palettes, palsize, d_palpix, d_hm, d_vm,
                                (hipStream_t)stream);
+}
+
+int tiler_quantize_palettes(long n_tiles, const int32_t *rgb, const int32_t *pal_of, const uint8_t *active,
+                            int n_palettes, int palsize, int lookup_bpc, int32_t *palettes, int32_t *use_count,
+                            int32_t *colors) {
+    if (!ensure_init()) return -1;
+    return quantize_palettes_host(n_tiles, rgb, pal_of, active, n_palettes, palsize, lookup_bpc, palettes, use_count,
+                                  colors);
+}
+
+int tiler_quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_pal_of, const uint8_t *d_active,
+                                int n_palettes, int palsize, int lookup_bpc, int32_t *palettes, int32_t *use_count,
+                                int32_t *colors, void *stream) {
+    if (!ensure_init()) return -1;
+    return quantize_palettes_dev(n_tiles, d_rgb, d_pal_of, d_active, n_palettes, palsize, lookup_bpc, palettes,
+                                 use_count, colors, (hipStream_t)stream);
+}
+
+int tiler_finish_quantize_order(int n_palettes, const int32_t *use_count, int32_t *lut) {
+    if (n_palettes <= 0 || !use_count || !lut) {
+        set_error("finish_quantize_order: invalid arguments");
+        return -1;
+    }
+    finish_quantize_order(use_count, n_palettes, lut);
+    return 0;
 }
 
 int tiler_interframe_correlation(const int32_t *rgb, int F, int tm_w, int tm_h, double *corr) {

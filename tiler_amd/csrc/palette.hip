@@ -1,0 +1,608 @@
+// palette.hip -- palette generation of the Dither step on the GPU: QuantizePalette with the
+// default Dennis Lee v3 quantizer (main.pas:2154-2254, 2396-2433 -> dl3quant, dlquant/quantizer.c:437-663) for
+// every (keyframe, palette) pair in one pass, then the CompareCMULHS order of the 16 colours (main.pas:2081-2090,
+// 2413) and FinishQuantizePalette's use-count order (main.pas:2435-2480).
+//
+// GPU layout, all pairs at once (the reference runs one DoQuantize per pair, main.pas:872-875, 901):
+//   1. every pixel of every tile -> key (pair << 3*bpc | the bpc-bit colour cell, build_table3's index) and its
+//      0x00BBGGRR value; a radix sort by key + reduce-by-key gives every pair's CUBE3 table in index order with
+//      32-bit wrapping sums (MSVC `ulong`, as the reference DLL) -- the tile order does not matter to a histogram;
+//   2. pass 1 of reduce_table3 (recount_next for every entry: the O(n^2 / 2) nearest-merge search) with one wave
+//      per entry over the whole grid;
+//   3. pass 2 (the sequential merges) with one 1024-thread workgroup per pair: each merge's scans (the minimum
+//      error, the index fix-ups, recount_dist) run block-parallel in the reference's phase order, each
+//      recount_next as a block- or wave-wide first-minimum search; results are those of the sequential loops
+//      because every phase only writes entries it owns.
+// calc_err is evaluated exactly as quantizer.c:512-541 in IEEE single precision: integer cell means, squares of
+// integers (exact), sqrt through double (innocuous for sqrt: 53 >= 2 * 24 + 2) rounded once to float.
+#include <hipcub/hipcub.hpp>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "palette.hpp"
+#include "tiler_common.hpp"
+
+namespace tiler {
+
+namespace {
+
+constexpr int DL3_T = 1024;        // pass-2 workgroup
+constexpr int DL3_W = DL3_T / 64;  // its waves
+constexpr int DL3_BLOCK_LIST = 8;  // a recount list up to this length runs block-wide per item, longer wave-wide
+
+struct Dl3Sum {
+    uint32_t r, g, b, n;
+};
+
+struct Dl3SumOp {
+    __host__ __device__ Dl3Sum operator()(const Dl3Sum &a, const Dl3Sum &b) const {
+        return Dl3Sum{a.r + b.r, a.g + b.g, a.b + b.b, a.n + b.n};
+    }
+};
+
+struct Dl3Expand {  // one pixel 0x00BBGGRR -> its CUBE3 contribution (build_table3, quantizer.c:496-499)
+    __host__ __device__ Dl3Sum operator()(const uint32_t c) const {
+        return Dl3Sum{c & 255u, (c >> 8) & 255u, (c >> 16) & 255u, 1u};
+    }
+};
+
+// the colour tables of all pairs, SoA; entry e of pair p at seg[p] + local index
+struct Dl3Tab {
+    uint32_t *R, *G, *B, *N;  // CUBE3 r, g, b, pixel_count (32-bit, wrapping)
+    uint32_t *Q;              // rr | gg << 8 | bb << 16 (setrgb)
+    float *E;                 // err
+    int *C;                   // cc (local index)
+};
+
+__device__ __forceinline__ uint32_t dl3_setrgb(uint32_t r, uint32_t g, uint32_t b, uint32_t n) {  // quantizer.c:472-478
+    const int v = (int)n, v2 = v >> 1;
+    const uint32_t rr = (uint8_t)((r + (uint32_t)v2) / (uint32_t)v);
+    const uint32_t gg = (uint8_t)((g + (uint32_t)v2) / (uint32_t)v);
+    const uint32_t bb = (uint8_t)((b + (uint32_t)v2) / (uint32_t)v);
+    return rr | (gg << 8) | (bb << 16);
+}
+
+__device__ __forceinline__ float dl3_sq(int d) { return (float)(d * d); }  // squares3[d] (exact for |d| <= 255)
+
+__device__ __forceinline__ float dl3_sqrt(float x) { return (float)__builtin_sqrt((double)x); }
+
+struct Dl3Entry {
+    uint32_t r, g, b, n, q;
+};
+
+__device__ __forceinline__ Dl3Entry dl3_load(const Dl3Tab &t, int i) {
+    return Dl3Entry{t.R[i], t.G[i], t.B[i], t.N[i], t.Q[i]};
+}
+
+__device__ __forceinline__ float dl3_calc_err(const Dl3Entry &a, const Dl3Entry &b) {  // quantizer.c:512-541
+    const uint32_t P1 = a.n, P2 = b.n, P3 = P1 + P2;
+    const int R3 = (int)((a.r + b.r + (P3 >> 1)) / P3);
+    const int G3 = (int)((a.g + b.g + (P3 >> 1)) / P3);
+    const int B3 = (int)((a.b + b.b + (P3 >> 1)) / P3);
+    const int R1 = a.q & 255, G1 = (a.q >> 8) & 255, B1 = (a.q >> 16) & 255;
+    const int R2 = b.q & 255, G2 = (b.q >> 8) & 255, B2 = (b.q >> 16) & 255;
+    float d1 = dl3_sq(R3 - R1) + dl3_sq(G3 - G1) + dl3_sq(B3 - B1);
+    d1 = dl3_sqrt(d1) * (float)P1;
+    float d2 = dl3_sq(R2 - R3) + dl3_sq(G2 - G3) + dl3_sq(B2 - B3);
+    d2 = dl3_sqrt(d2) * (float)P2;
+    return d1 + d2;
+}
+
+// first minimum: smaller error, equal errors -> smaller index (the reference's ascending scan with `<`)
+__device__ __forceinline__ void dl3_min(float &e, int &j, float e2, int j2) {
+    if (e2 < e || (e2 == e && j2 < j)) {
+        e = e2;
+        j = j2;
+    }
+}
+
+__device__ __forceinline__ void dl3_wave_min(float &e, int &j) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float e2 = __shfl_xor(e, o);
+        const int j2 = __shfl_xor(j, o);
+        dl3_min(e, j, e2, j2);
+    }
+}
+
+// block-wide first minimum; every thread returns the result
+__device__ void dl3_block_min(float &e, int &j, float *sh_e, int *sh_j) {
+    dl3_wave_min(e, j);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();  // sh_* free (a previous call's readers are done)
+    if ((threadIdx.x & 63) == 0) {
+        sh_e[w] = e;
+        sh_j[w] = j;
+    }
+    __syncthreads();
+    e = sh_e[0];
+    j = sh_j[0];
+    for (int k = 1; k < DL3_W; k++) dl3_min(e, j, sh_e[k], sh_j[k]);
+}
+
+// recount_next(i) over j in (i, tot) (quantizer.c:543-560) by the whole block / one wave
+__device__ void dl3_recount_block(const Dl3Tab &t, int i, int tot, float *sh_e, int *sh_j) {
+    const Dl3Entry a = dl3_load(t, i);
+    float e = HUGE_VALF;
+    int j = INT32_MAX;
+    for (int k = i + 1 + (int)threadIdx.x; k < tot; k += DL3_T) {
+        const float cur = dl3_calc_err(a, dl3_load(t, k));
+        if (cur < e) {
+            e = cur;
+            j = k;
+        }
+    }
+    dl3_block_min(e, j, sh_e, sh_j);
+    if (threadIdx.x == 0) {
+        t.E[i] = e;
+        t.C[i] = j == INT32_MAX ? 0 : j;
+    }
+}
+
+__device__ void dl3_recount_wave(const Dl3Tab &t, int i, int tot) {
+    const Dl3Entry a = dl3_load(t, i);
+    float e = HUGE_VALF;
+    int j = INT32_MAX;
+    for (int k = i + 1 + (int)(threadIdx.x & 63); k < tot; k += 64) {
+        const float cur = dl3_calc_err(a, dl3_load(t, k));
+        if (cur < e) {
+            e = cur;
+            j = k;
+        }
+    }
+    dl3_wave_min(e, j);
+    if ((threadIdx.x & 63) == 0) {
+        t.E[i] = e;
+        t.C[i] = j == INT32_MAX ? 0 : j;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// 1. keys / values of every pixel; tiles per pair (PaletteUseCount)
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dl3_keys_kernel(const int32_t *__restrict__ rgb, const int32_t *__restrict__ pal_of,
+                                                       const uint8_t *__restrict__ active, long n_tiles, int P, int bpc,
+                                                       uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                                                       int *__restrict__ use_count) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_tiles * 64) return;
+    const long tile = i >> 6;
+    const int p = pal_of[tile];
+    const bool ok = (!active || active[tile]) && p >= 0 && p < P;
+    const uint32_t c = (uint32_t)rgb[i];
+    const int mbpc = (1 << bpc) - 1;
+    const uint32_t r = (c & 255u) * mbpc / 255, g = ((c >> 8) & 255u) * mbpc / 255, b = ((c >> 16) & 255u) * mbpc / 255;
+    keys[i] = ok ? ((uint32_t)p << (3 * bpc)) | b | (g << bpc) | (r << (2 * bpc)) : ((uint32_t)P << (3 * bpc));
+    vals[i] = c;
+    if (ok && (i & 63) == 0) atomicAdd(use_count + p, 1);
+}
+
+// seg[p] = first entry of pair p (lower bound of p << 3*bpc in the sorted unique keys), seg[P] = entries
+__global__ void dl3_seg_kernel(const uint32_t *__restrict__ ukeys, const int *__restrict__ nruns, int P, int bpc,
+                               int *__restrict__ seg) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > P) return;
+    const uint32_t key = (uint32_t)p << (3 * bpc);
+    int lo = 0, hi = *nruns;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ukeys[mid] < key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    seg[p] = lo;
+}
+
+__global__ __launch_bounds__(256) void dl3_init_kernel(const Dl3Sum *__restrict__ agg, const int *__restrict__ seg, int P,
+                                                       Dl3Tab t) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= seg[P]) return;
+    const Dl3Sum s = agg[e];
+    t.R[e] = s.r;
+    t.G[e] = s.g;
+    t.B[e] = s.b;
+    t.N[e] = s.n;
+    t.Q[e] = dl3_setrgb(s.r, s.g, s.b, s.n);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// 2. pass 1 of reduce_table3 (quantizer.c:589-599): recount_next(i) for every entry, one wave per entry
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dl3_pass1_kernel(const uint32_t *__restrict__ ukeys, const int *__restrict__ seg,
+                                                        int P, int bpc, Dl3Tab t) {
+    const int total = seg[P];
+    for (int e = blockIdx.x * 4 + (threadIdx.x >> 6); e < total; e += gridDim.x * 4) {
+        const int p = (int)(ukeys[e] >> (3 * bpc));
+        const int s = seg[p], n = seg[p + 1] - s, i = e - s;
+        Dl3Tab u = t;
+        u.R += s, u.G += s, u.B += s, u.N += s, u.Q += s, u.E += s, u.C += s;
+        if (i == n - 1) {  // the last entry (quantizer.c:598-599)
+            if ((threadIdx.x & 63) == 0) {
+                u.E[i] = HUGE_VALF;
+                u.C[i] = n;
+            }
+        } else {
+            dl3_recount_wave(u, i, n);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// 3. pass 2 of reduce_table3 (quantizer.c:603-643): one workgroup per pair, the merges in order
+// ---------------------------------------------------------------------------------------------------------------
+struct Dl3Args {
+    Dl3Tab t;
+    const int *seg;
+    int quant_to;
+    int *list;       // [entries] recount lists (a pair's slice at its seg offset)
+    int32_t *pal;    // [P][quant_to] 0x00BBGGRR
+};
+
+// the collected recount list: short lists block-wide per item, long ones one item per wave
+__device__ void dl3_run_list(const Dl3Tab &t, const int *list, int k, int tot, float *sh_e, int *sh_j) {
+    if (k <= DL3_BLOCK_LIST) {
+        for (int q = 0; q < k; q++) dl3_recount_block(t, list[q], tot, sh_e, sh_j);
+    } else {
+        for (int q = threadIdx.x >> 6; q < k; q += DL3_W) dl3_recount_wave(t, list[q], tot);
+    }
+    __syncthreads();
+}
+
+// recount_dist(c) (quantizer.c:562-581)
+__device__ void dl3_recount_dist(const Dl3Tab &t, int *list, int c, int tot, float *sh_e, int *sh_j, int *sh_n) {
+    dl3_recount_block(t, c, tot, sh_e, sh_j);
+    if (threadIdx.x == 0) *sh_n = 0;
+    __syncthreads();
+    const Dl3Entry b = dl3_load(t, c);
+    for (int i = threadIdx.x; i < c; i += DL3_T) {
+        if (t.C[i] == c) {
+            list[atomicAdd(sh_n, 1)] = i;
+        } else {
+            const float cur = dl3_calc_err(dl3_load(t, i), b);
+            if (cur < t.E[i]) {
+                t.E[i] = cur;
+                t.C[i] = c;
+            }
+        }
+    }
+    __syncthreads();
+    dl3_run_list(t, list, *sh_n, tot, sh_e, sh_j);
+}
+
+__global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
+    __shared__ float sh_e[DL3_W];
+    __shared__ int sh_j[DL3_W];
+    __shared__ int sh_n;
+    const int p = blockIdx.x;
+    const int s = a.seg[p], n = a.seg[p + 1] - s;
+    Dl3Tab t = a.t;
+    t.R += s, t.G += s, t.B += s, t.N += s, t.Q += s, t.E += s, t.C += s;
+    int *list = a.list + s;
+    int tot = n, c1 = 0;
+    while (tot > a.quant_to) {
+        // the first entry of minimum error (quantizer.c:610-618); none below HUGE_VALF keeps c1
+        float e = HUGE_VALF;
+        int j = INT32_MAX;
+        for (int i = threadIdx.x; i < tot; i += DL3_T) {
+            const float v = t.E[i];
+            if (v < e) {
+                e = v;
+                j = i;
+            }
+        }
+        dl3_block_min(e, j, sh_e, sh_j);
+        if (j != INT32_MAX) c1 = j;
+        const int c2 = t.C[c1];
+        __syncthreads();  // every thread has read C[c1] before it changes
+        tot--;
+        if (threadIdx.x == 0) {  // merge c1 into c2, the last entry into c1 (quantizer.c:619-629)
+            const uint32_t r = t.R[c2] + t.R[c1], g = t.G[c2] + t.G[c1], b = t.B[c2] + t.B[c1];
+            const uint32_t nn = t.N[c2] + t.N[c1];
+            t.R[c2] = r, t.G[c2] = g, t.B[c2] = b, t.N[c2] = nn;
+            t.Q[c2] = dl3_setrgb(r, g, b, nn);
+            t.R[c1] = t.R[tot], t.G[c1] = t.G[tot], t.B[c1] = t.B[tot], t.N[c1] = t.N[tot], t.Q[c1] = t.Q[tot];
+            t.E[c1] = t.E[tot], t.C[c1] = t.C[tot];
+            t.E[tot - 1] = HUGE_VALF;
+            t.C[tot - 1] = tot;
+            sh_n = 0;
+        }
+        __syncthreads();
+        // entries pointing at the moved one: below c1 re-point, above c1 recount (quantizer.c:631-639)
+        for (int i = threadIdx.x; i < tot; i += DL3_T)
+            if (t.C[i] == tot) {
+                if (i < c1)
+                    t.C[i] = c1;
+                else if (i > c1)
+                    list[atomicAdd(&sh_n, 1)] = i;
+            }
+        __syncthreads();
+        dl3_run_list(t, list, sh_n, tot, sh_e, sh_j);
+        dl3_recount_dist(t, list, c1, tot, sh_e, sh_j, &sh_n);
+        if (c2 != tot) dl3_recount_dist(t, list, c2, tot, sh_e, sh_j, &sh_n);
+    }
+    for (int i = threadIdx.x; i < a.quant_to; i += DL3_T)  // set_palette3 + copy_pal (calloc'd beyond tot)
+        a.pal[(long)p * a.quant_to + i] = i < tot ? (int32_t)t.Q[i] : 0;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// host: CompareCMULHS (TFPList.Sort) and FinishQuantizePalette's order
+// ---------------------------------------------------------------------------------------------------------------
+int muldiv_win(int a, int b, int c) {  // Windows MulDiv (unit windows in main.pas's uses): rounded half away from 0
+    if (c == 0) return -1;
+    if (c < 0) {
+        a = -a;
+        c = -c;
+    }
+    const long long prod = (long long)a * b;
+    const bool add = (a < 0 && b < 0) || (a >= 0 && b >= 0);  // the operands' signs pick the rounding direction
+    const long long r = add ? (prod + c / 2) / c : (prod - c / 2) / c;
+    if (r > 2147483647LL || r < -2147483647LL) return -1;
+    return (int)r;
+}
+
+struct CmItem {  // TCountIndexArray (main.pas:193-196)
+    int index, luma;
+    uint8_t hue, sat, val;
+};
+
+CmItem cm_item(int32_t col) {  // FColorMap / FColorMapLuma (main.pas:4835-4847) + RGBToHSV (main.pas:3496-3543)
+    const int rr = col & 255, gg = (col >> 8) & 255, bb = (col >> 16) & 255;
+    const int mx = std::max(rr, std::max(gg, bb)), mn = std::min(rr, std::min(gg, bb));
+    int hh = 0, ss = 0;
+    if (mx != mn) {
+        const int delta = mx - mn;
+        ss = muldiv_win(delta, 255, mx);
+        if (rr == mx)
+            hh = muldiv_win(42, gg - bb, delta);
+        else if (gg == mx)
+            hh = muldiv_win(42, bb - rr, delta) + 84;
+        else
+            hh = muldiv_win(42, rr - gg, delta) + 168;
+        hh %= 252;
+    }
+    CmItem it;
+    it.index = col;
+    it.luma = (rr * 2126 + gg * 7152 + bb * 722) / 10000;
+    it.hue = (uint8_t)(hh & 255);
+    it.sat = (uint8_t)(ss & 255);
+    it.val = (uint8_t)(mx & 255);
+    return it;
+}
+
+int cmp3(int a, int b) { return a < b ? -1 : a > b ? 1 : 0; }
+
+int compare_cmulhs(const CmItem *a, const CmItem *b) {  // main.pas:2081-2090
+    int r = cmp3(a->luma, b->luma);
+    if (!r) r = cmp3(a->val, b->val);
+    if (!r) r = cmp3(a->sat, b->sat);
+    if (!r) r = cmp3(a->hue, b->hue);
+    return r;
+}
+
+void fpc_tlist_sort(std::vector<const CmItem *> &l, int L, int R) {  // TFPList.Sort: the FPC RTL QuickSort
+    int I, J;
+    do {
+        I = L;
+        J = R;
+        const CmItem *P = l[(L + R) / 2];
+        do {
+            while (compare_cmulhs(P, l[I]) > 0) I++;
+            while (compare_cmulhs(P, l[J]) < 0) J--;
+            if (I <= J) {
+                std::swap(l[I], l[J]);
+                I++;
+                J--;
+            }
+        } while (I <= J);
+        if (L < J) fpc_tlist_sort(l, L, J);
+        L = I;
+    } while (I < R);
+}
+
+}  // namespace
+
+void sort_palette_cmulhs(int32_t *pal, int n) {
+    std::vector<CmItem> items(n);
+    std::vector<const CmItem *> l(n);
+    for (int i = 0; i < n; i++) {
+        items[i] = cm_item(pal[i]);
+        l[i] = &items[i];
+    }
+    if (n > 1) fpc_tlist_sort(l, 0, n - 1);
+    std::vector<int32_t> out(n);
+    for (int i = 0; i < n; i++) out[i] = l[i]->index;
+    memcpy(pal, out.data(), n * sizeof(int32_t));
+}
+
+void finish_quantize_order(const int32_t *use_count, int P, int32_t *lut) {
+    // kmodes.pas:89-136 QuickSort of the PaletteUseCount records, ComparePaletteUseCount (descending use count)
+    std::vector<std::pair<int32_t, int32_t>> a(P);  // (UseCount, PalIdx)
+    for (int p = 0; p < P; p++) a[p] = {use_count[p], p};
+    auto cmp = [](const std::pair<int32_t, int32_t> &x, const std::pair<int32_t, int32_t> &y) {
+        return cmp3(y.first, x.first);
+    };
+    struct Rec {
+        static void qs(std::vector<std::pair<int32_t, int32_t>> &v, int first, int last, decltype(cmp) &c) {
+            if (last <= first) return;
+            int i, j;
+            do {
+                i = first;
+                j = last;
+                int piv = (first + last) >> 1;
+                do {
+                    while (c(v[i], v[piv]) < 0) i++;
+                    while (c(v[j], v[piv]) > 0) j--;
+                    if (i <= j) {
+                        std::swap(v[i], v[j]);
+                        if (piv == i)
+                            piv = j;
+                        else if (piv == j)
+                            piv = i;
+                        i++;
+                        j--;
+                    }
+                } while (i <= j);
+                if (first < j) qs(v, first, j, c);
+                first = i;
+            } while (i < last);
+        }
+    };
+    Rec::qs(a, 0, P - 1, cmp);
+    for (int p = 0; p < P; p++) lut[a[p].second] = p;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// QuantizePalette for all pairs: device inputs, host outputs
+// ---------------------------------------------------------------------------------------------------------------
+int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_pal_of, const uint8_t *d_active, int P,
+                          int palsize, int bpc, int32_t *pal_out, int32_t *use_count, int32_t *hist,
+                          hipStream_t stream) {
+    if (n_tiles < 0 || P <= 0 || palsize <= 0 || bpc < 1 || bpc > 8 || (n_tiles > 0 && (!d_rgb || !d_pal_of)) ||
+        !pal_out || !use_count) {
+        set_error("quantize_palettes: invalid arguments (bpc in 1..8)");
+        return -1;
+    }
+    const int key_bits = 3 * bpc;
+    if ((((uint64_t)P + 1) << key_bits) > 0xffffffffull || n_tiles * 64 > 0x7fffffffL) {
+        set_error("quantize_palettes: too many palettes for 32-bit keys at this bpc, or more than 2^31 pixels");
+        return -1;
+    }
+    const int npix = (int)(n_tiles * 64);
+    int end_bit = key_bits;
+    while ((1ull << (end_bit - key_bits)) <= (uint64_t)P) end_bit++;
+    // workspace
+    size_t tmp_sort = 0, tmp_red = 0;
+    hipcub::DoubleBuffer<uint32_t> dk(nullptr, nullptr), dv(nullptr, nullptr);
+    TILER_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, dk, dv, npix, 0, end_bit, stream));
+    hipcub::TransformInputIterator<Dl3Sum, Dl3Expand, const uint32_t *> it_in(nullptr, Dl3Expand());
+    TILER_HIP_CHECK(hipcub::DeviceReduce::ReduceByKey(nullptr, tmp_red, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                      it_in, (Dl3Sum *)nullptr, (int *)nullptr, Dl3SumOp(), npix,
+                                                      stream));
+    const size_t np = (size_t)std::max(npix, 1);
+    const size_t b_keys = 4 * np, b_sum = sizeof(Dl3Sum) * np, b_tmp = std::max(tmp_sort, tmp_red) + 256;
+    const size_t bytes = 4 * b_keys /* keys, vals x2 */ + b_keys /* ukeys */ + b_sum + b_tmp + 4 * (P + 2) * 2 +
+                         7 * b_keys /* table + list */ + 4 * (size_t)P * palsize + 4096;
+    char *ws = nullptr;
+    TILER_HIP_CHECK(hipMalloc((void **)&ws, bytes));
+    char *cur = ws;
+    auto take = [&](size_t b) {
+        char *r = cur;
+        cur += (b + 255) & ~(size_t)255;
+        return r;
+    };
+    uint32_t *k0 = (uint32_t *)take(b_keys), *k1 = (uint32_t *)take(b_keys);
+    uint32_t *v0 = (uint32_t *)take(b_keys), *v1 = (uint32_t *)take(b_keys);
+    uint32_t *ukeys = (uint32_t *)take(b_keys);
+    Dl3Sum *agg = (Dl3Sum *)take(b_sum);
+    void *tmp = take(b_tmp);
+    int *d_nruns = (int *)take(4 * (P + 2));
+    int *d_seg = (int *)take(4 * (P + 2));
+    int *d_uc = (int *)take(4 * (P + 2));
+    Dl3Tab t;
+    t.R = (uint32_t *)take(b_keys);
+    t.G = (uint32_t *)take(b_keys);
+    t.B = (uint32_t *)take(b_keys);
+    t.N = (uint32_t *)take(b_keys);
+    t.Q = (uint32_t *)take(b_keys);
+    t.E = (float *)take(b_keys);
+    t.C = (int *)take(b_keys);
+    int *d_list = (int *)k0;  // the sort buffers are free once the table exists
+    int32_t *d_pal = (int32_t *)take(4 * (size_t)P * palsize);
+    int rc = -1;
+    std::vector<int> seg(P + 1);
+    do {
+        if (hipMemsetAsync(d_uc, 0, 4 * (P + 2), stream) != hipSuccess) break;
+        if (hipMemsetAsync(d_nruns, 0, 4, stream) != hipSuccess) break;
+        KTimer tk("dl3_table", stream);
+        if (npix > 0) {
+            hipLaunchKernelGGL(dl3_keys_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, d_rgb, d_pal_of,
+                               d_active, n_tiles, P, bpc, k0, v0, d_uc);
+            if (hipGetLastError() != hipSuccess) break;
+            hipcub::DoubleBuffer<uint32_t> kb(k0, k1), vb(v0, v1);
+            size_t ts = tmp_sort;
+            if (hipcub::DeviceRadixSort::SortPairs(tmp, ts, kb, vb, npix, 0, end_bit, stream) != hipSuccess) break;
+            hipcub::TransformInputIterator<Dl3Sum, Dl3Expand, const uint32_t *> vin(vb.Current(), Dl3Expand());
+            size_t tr = tmp_red;
+            if (hipcub::DeviceReduce::ReduceByKey(tmp, tr, (const uint32_t *)kb.Current(), ukeys, vin, agg, d_nruns,
+                                                  Dl3SumOp(), npix, stream) != hipSuccess)
+                break;
+        }
+        hipLaunchKernelGGL(dl3_seg_kernel, dim3((P + 256) / 256), dim3(256), 0, stream, ukeys, d_nruns, P, bpc, d_seg);
+        if (hipGetLastError() != hipSuccess) break;
+        if (hipMemcpyAsync(seg.data(), d_seg, 4 * (P + 1), hipMemcpyDeviceToHost, stream) != hipSuccess) break;
+        if (hipMemcpyAsync(use_count, d_uc, 4 * P, hipMemcpyDeviceToHost, stream) != hipSuccess) break;
+        if (hipStreamSynchronize(stream) != hipSuccess) break;
+        const int total = seg[P];
+        if (total > 0) {
+            hipLaunchKernelGGL(dl3_init_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, agg, d_seg, P,
+                               t);
+            if (hipGetLastError() != hipSuccess) break;
+        }
+        {
+            KTimer tp("dl3_pass1", stream);
+            if (total > 0)
+                hipLaunchKernelGGL(dl3_pass1_kernel, dim3((unsigned)std::min(65536, (total + 3) / 4)), dim3(256), 0, stream,
+                                   ukeys, d_seg, P, bpc, t);
+            if (hipGetLastError() != hipSuccess) break;
+        }
+        {
+            KTimer tr("dl3_reduce", stream);
+            Dl3Args ra;
+            ra.t = t;
+            ra.seg = d_seg;
+            ra.quant_to = palsize;
+            ra.list = d_list;
+            ra.pal = d_pal;
+            hipLaunchKernelGGL(dl3_reduce_kernel, dim3(P), dim3(DL3_T), 0, stream, ra);
+            if (hipGetLastError() != hipSuccess) break;
+        }
+        if (hipMemcpyAsync(pal_out, d_pal, 4 * (size_t)P * palsize, hipMemcpyDeviceToHost, stream) != hipSuccess) break;
+        if (hipStreamSynchronize(stream) != hipSuccess) break;
+        for (int p = 0; p < P; p++) {
+            if (hist) hist[p] = seg[p + 1] - seg[p];
+            sort_palette_cmulhs(pal_out + (size_t)p * palsize, palsize);  // CMPal.Sort (main.pas:2413)
+        }
+        rc = 0;
+    } while (0);
+    if (rc) set_error("quantize_palettes: HIP failure");
+    (void)hipFree(ws);
+    return rc;
+}
+
+int quantize_palettes_host(long n_tiles, const int32_t *rgb, const int32_t *pal_of, const uint8_t *active, int P,
+                           int palsize, int bpc, int32_t *pal_out, int32_t *use_count, int32_t *hist) {
+    if (n_tiles < 0 || (n_tiles > 0 && (!rgb || !pal_of))) {
+        set_error("quantize_palettes: invalid arguments");
+        return -1;
+    }
+    const size_t b_rgb = (size_t)n_tiles * 256, b_po = (size_t)n_tiles * 4, b_act = active ? (size_t)n_tiles : 0;
+    char *buf = nullptr;
+    TILER_HIP_CHECK(hipMalloc((void **)&buf, b_rgb + b_po + b_act + 64));
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipFree(buf);
+        set_error("quantize_palettes: stream creation failed");
+        return -1;
+    }
+    int rc = -1;
+    do {
+        if (hipMemcpyAsync(buf, rgb, b_rgb, hipMemcpyHostToDevice, st) != hipSuccess) break;
+        if (hipMemcpyAsync(buf + b_rgb, pal_of, b_po, hipMemcpyHostToDevice, st) != hipSuccess) break;
+        if (active && hipMemcpyAsync(buf + b_rgb + b_po, active, b_act, hipMemcpyHostToDevice, st) != hipSuccess) break;
+        rc = quantize_palettes_dev(n_tiles, (const int32_t *)buf, (const int32_t *)(buf + b_rgb),
+                                   active ? (const uint8_t *)(buf + b_rgb + b_po) : nullptr, P, palsize, bpc, pal_out,
+                                   use_count, hist, st);
+    } while (0);
+    if (rc && !last_error()[0]) set_error("quantize_palettes: HIP copy failed");
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    (void)hipFree(buf);
+    return rc;
+}
+
+}  // namespace tiler

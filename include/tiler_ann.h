@@ -98,7 +98,8 @@ double tiler_timing_get(const char *kernel, int *launches);
 int tiler_timing_reset(void);
 
 /* ---- PsyV descriptor (ComputeTilePsyVisFeatures main.pas:2997-3177) ----
- * flags: 1 FromPal, 2 UseWavelets, 8 QWeighting, 16 HMirror, 32 VMirror (UseLAB unsupported: off on the hot path).
+ * flags: 1 FromPal, 2 UseWavelets, 4 UseLAB (RGBToLAB main.pas:2711-2747, the Dither step's descriptors),
+ * 8 QWeighting, 16 HMirror, 32 VMirror.
  * RGB mode: rgb[n][64] (0x00BBGGRR).  Pal mode: palpix[*][64] indexed by tile_of[i] (or i when NULL),
  * palettes[*][16] indexed by pal_of[i] (or 0), per-item extra flags flags_per[i] (or NULL).
  * gamma: -1 (r/255) or 0/1 (gGammaCorLut).  Outputs: out64[n][192] and/or out32[n][192]. */
@@ -199,6 +200,20 @@ int tiler_quantize_palettes(long n_tiles, const int32_t *rgb, const int32_t *pal
 int tiler_quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_pal_of, const uint8_t *d_active,
                                 int n_palettes, int palsize, int lookup_bpc, int32_t *palettes, int32_t *use_count,
                                 int32_t *colors, void *stream);
+/* PrepareDitherTiles for one keyframe (main.pas:2097-2152): ComputeTilePsyVisFeatures(UseLAB, use_wavelets,
+ * gamma) of its n_tiles RGB tiles (frame order), then the k-means of yakmo_create(n_palettes, 1, MaxInt, k-means++,
+ * seed, no normalisation) -> labels[n_tiles] (DitheringPalIndex), centroids[n_palettes][192] (PaletteCentroids),
+ * *iterations (Lloyd assignments).  yakmo.dll is binary-only: the k-means is its published algorithm written out
+ * exactly (DESIGN.md "Dither: palette generation"), not pinned to the DLL.  max_iter <= 0 means unbounded
+ * (MaxInt).  Fewer than 2 tiles or palettes: labels 0, centroids 0.  Host arrays / device pointers.  0 / -1. */
+int tiler_prepare_dither_tiles(long n_tiles, const int32_t *rgb, int n_palettes, int gamma, int use_wavelets,
+                               int max_iter, uint32_t seed, int32_t *labels, double *centroids, int *iterations);
+int tiler_prepare_dither_tiles_dev(long n_tiles, const int32_t *d_rgb, int n_palettes, int gamma, int use_wavelets,
+                                   int max_iter, uint32_t seed, int32_t *d_labels, double *d_centroids,
+                                   int *iterations, void *stream);
+/* The k-means alone over X[n][d] (d <= 192, fp64, host arrays). */
+int tiler_kmeans(const double *X, long n, int d, int k, int max_iter, uint32_t seed, int32_t *labels,
+                 double *centroids, int *iterations);
 /* FinishQuantizePalette's order of one keyframe's palettes (main.pas:2444-2455): the reference QuickSort
  * (kmodes.pas:89-136) by use count, descending -> lut[old palette] = new palette.  0 / -1. */
 int tiler_finish_quantize_order(int n_palettes, const int32_t *use_count, int32_t *lut);

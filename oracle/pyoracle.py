@@ -385,3 +385,55 @@ def finish_quantize_order(use_count):
     lut = np.zeros(uc.size, np.int32)
     lib().or_finish_quantize_order(_p(uc), uc.size, _p(lut))
     return lut
+
+
+# ---- the Dither step's descriptors + k-means (PrepareDitherTiles restated; yakmo unpinned) ----
+OR_LAB = 4
+
+
+def psyv_lab_batch(rgb, gamma=-1, use_wavelets=True):
+    rgb = np.ascontiguousarray(rgb, np.int32).reshape(-1, 64)
+    out = np.zeros((rgb.shape[0], 192), np.float64)
+    lib().or_psyv_batch(rgb.shape[0], _p(rgb), None, None, None, None, OR_LAB | (2 if use_wavelets else 0), gamma,
+                        _p(out))
+    return out
+
+
+def kmeans(X, k, max_iter=0x7fffffff, seed=0, threads=None):
+    X = np.ascontiguousarray(X, np.float64)
+    n, d = X.shape
+    labels = np.zeros(n, np.int32)
+    cent = np.zeros((k, d), np.float64)
+    it = lib().or_kmeans(_p(X), ctypes.c_long(n), d, k, max_iter, ctypes.c_uint32(seed), _p(labels), _p(cent),
+                         threads or _threads())
+    return labels, cent, int(it)
+
+
+def prepare_dither_tiles(rgb, n_palettes, gamma=-1, use_wavelets=True, max_iter=0x7fffffff, seed=0):
+    rgb = np.ascontiguousarray(rgb, np.int32).reshape(-1, 64)
+    if rgb.shape[0] <= 1 or n_palettes <= 1:
+        return np.zeros(rgb.shape[0], np.int32), np.zeros((n_palettes, 192)), 0
+    return kmeans(psyv_lab_batch(rgb, gamma, use_wavelets), n_palettes, max_iter, seed)
+
+
+def generate_palettes(frames, kf_start, n_palettes, palsize=16, gamma=-1, use_wavelets=True, bpc=7):
+    """btnDitherClick's palette half (main.pas:886-907) on the CPU restatement (see tiler_amd.palette)."""
+    frames = np.ascontiguousarray(frames, np.int32)
+    F, Q = frames.shape[:2]
+    kf_start = np.asarray(kf_start, np.int64)
+    KF, P = kf_start.size - 1, n_palettes
+    pal = np.zeros((KF, P, palsize), np.int32)
+    cent = np.zeros((KF, P, 192))
+    dith = np.zeros(F * Q, np.int32)
+    ucs = np.zeros((KF, P), np.int32)
+    for k in range(KF):
+        f0, f1 = int(kf_start[k]), int(kf_start[k + 1])
+        tiles = frames[f0:f1].reshape(-1, 64)
+        lab, c, _ = prepare_dither_tiles(tiles, P, gamma, use_wavelets)
+        p, uc, _ = quantize_palettes(tiles, lab, P, palsize, bpc)
+        lut = finish_quantize_order(uc)
+        pal[k][lut] = p
+        cent[k][lut] = c
+        dith[f0 * Q:f1 * Q] = lut[lab]
+        ucs[k][lut] = uc
+    return pal, cent, dith, ucs

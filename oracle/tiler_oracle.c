@@ -87,6 +87,34 @@ static inline void rgb_to_yuv(int32_t col, int gamma, double *y, double *u, doub
     *v = vv;
 }
 
+/* RGBToLAB main.pas:2711-2747 (D50, Wright-Guild XYZ) with FPC Math.power = exp(e * ln(b)) (detmath.c). */
+static inline void rgb_to_lab(int32_t col, int gamma, double *ol, double *oa, double *ob) {
+    const int ir = col & 0xff, ig = (col >> 8) & 0xff, ib = (col >> 16) & 0xff;
+    double c[3];
+    const int ch[3] = {ir, ig, ib};
+    for (int k = 0; k < 3; k++) {
+        double v = gamma >= 0 ? g_gamma_lut[gamma + 1][ch[k]] : ch[k] / 255.0; /* GammaCorrect */
+        if (v > 0.04045)
+            v = or_fpc_power((v + 0.055) / 1.055, 2.4);
+        else
+            v = v / 12.92;
+        c[k] = v;
+    }
+    const double r = c[0], g = c[1], b = c[2];
+    double x = (r * 0.49000 + g * 0.31000 + b * 0.20000) / 0.17697;
+    double y = (r * 0.17697 + g * 0.81240 + b * 0.01063) / 0.17697;
+    double z = (r * 0.00000 + g * 0.01000 + b * 0.99000) / 0.17697;
+    x /= 96.6797 / 100;
+    y /= 100.000 / 100;
+    z /= 82.5188 / 100;
+    if (x > 0.008856) x = or_fpc_power(x, 1.0 / 3.0); else x = (7.787 * x) + 16.0 / 116.0;
+    if (y > 0.008856) y = or_fpc_power(y, 1.0 / 3.0); else y = (7.787 * y) + 16.0 / 116.0;
+    if (z > 0.008856) z = or_fpc_power(z, 1.0 / 3.0); else z = (7.787 * z) + 16.0 / 116.0;
+    *ol = (116 * y) - 16;
+    *oa = 500 * (x - y);
+    *ob = 200 * (y - z);
+}
+
 /* WaveletGS main.pas:2805-2840 (normalized Haar, recursion on the top-left quadrant). */
 static void wavelet_gs(const double *data, double *output, int dx, int dy, int depth) {
     double tx[64], ty[64];
@@ -109,7 +137,7 @@ static void wavelet_gs(const double *data, double *output, int dx, int dy, int d
     if (depth > 0) wavelet_gs(output, output, dx / 2, dy / 2, depth - 1);
 }
 
-/* ComputeTilePsyVisFeatures main.pas:2997-3177 (UseLAB=False on the whole hot path). */
+/* ComputeTilePsyVisFeatures main.pas:2997-3177 (UseLAB only for the Dither step's descriptors, OR_LAB). */
 void or_psyv(const int32_t *rgb, const uint8_t *palpix, const int32_t *pal, int flags, int gamma, double *out) {
     or_init();
     double cpn[3][64];
@@ -119,7 +147,10 @@ void or_psyv(const int32_t *rgb, const uint8_t *palpix, const int32_t *pal, int 
             int xx = hm ? 7 - x : x;
             int yy = vm ? 7 - y : y;
             int32_t col = (flags & OR_FROM_PAL) ? pal[palpix[yy * 8 + xx]] : rgb[yy * 8 + xx];
-            rgb_to_yuv(col, gamma, &cpn[0][y * 8 + x], &cpn[1][y * 8 + x], &cpn[2][y * 8 + x]);
+            if (flags & OR_LAB)
+                rgb_to_lab(col, gamma, &cpn[0][y * 8 + x], &cpn[1][y * 8 + x], &cpn[2][y * 8 + x]);
+            else
+                rgb_to_yuv(col, gamma, &cpn[0][y * 8 + x], &cpn[1][y * 8 + x], &cpn[2][y * 8 + x]);
         }
     if (flags & OR_WAVELETS) {
         for (int c = 0; c < 3; c++) wavelet_gs(cpn[c], out + c * 64, 8, 8, 2);

@@ -34,6 +34,7 @@ extern "C" {
 /* flags for or_psyv (ComputeTilePsyVisFeatures arguments, main.pas:2997) */
 #define OR_FROM_PAL 1
 #define OR_WAVELETS 2
+#define OR_LAB 4 /* UseLAB: RGBToLAB instead of RGBToYUV (PrepareDitherTiles, main.pas:2120) */
 #define OR_QWEIGHT 8
 #define OR_HMIRROR 16
 #define OR_VMIRROR 32
@@ -120,6 +121,16 @@ void or_sort_cmulhs(const int32_t *cols, int n, int32_t *out);
 void or_quantize_palettes(const int32_t *rgb, const int32_t *pal_of, const uint8_t *active, long n, int P,
                           int palsize, int bpc, int32_t *pal_out, int32_t *use_count, int32_t *hist, int threads);
 void or_finish_quantize_order(const int32_t *use_count, int P, int32_t *lut);
+
+/* detmath.c: fdlibm exp / ln, FPC Math.power (non-integer exponent) */
+double or_det_log(double x);
+double or_det_exp(double x);
+double or_fpc_power(double base, double exponent);
+
+/* kmeans.c: the Dither step's k-means (yakmo call restated; returns the assignment count) */
+uint32_t or_mt19937_first(uint32_t seed);
+int or_kmeans(const double *X, long n, int d, int k, int max_iter, uint32_t seed, int32_t *labels, double *cent,
+              int threads);
 
 #ifdef __cplusplus
 }

@@ -66,3 +66,56 @@ def test_quantize_clustered_long_recount_lists(gpu, oracle):
     rgb = px[..., 0] | (px[..., 1] << 8) | (px[..., 2] << 16)
     pal_of = rng.integers(0, 3, n).astype(np.int32)
     _check(oracle, rgb, pal_of, 3)
+
+
+@pytest.mark.parametrize("gamma", [-1, 0])
+def test_lab_descriptor_bit_exact(gpu, oracle, gamma):
+    """ComputeTilePsyVisFeatures(UseLAB) on the GPU (fdlibm exp / ln on device, detmath.hpp) equals the CPU
+    restatement bit for bit, Haar and DCT."""
+    from tiler_amd.psyv import psyv_batch
+    rng = np.random.default_rng(20 + gamma)
+    rgb = synth.frame_tiles(rng, 700)
+    rgb[:5] = 0
+    rgb[5:9] = 0xFFFFFF
+    for wl in (True, False):
+        g, _ = psyv_batch(rgb=rgb, flags=4 | (2 if wl else 0), gamma=gamma)
+        o = oracle.psyv_lab_batch(rgb, gamma, wl)
+        assert np.array_equal(g.view(np.uint64), o.view(np.uint64))
+
+
+@pytest.mark.parametrize("n,k", [(3000, 8), (2500, 70), (200, 128), (50, 64)])
+def test_kmeans_bit_exact(gpu, oracle, n, k):
+    """Seeding, every Lloyd step, the final labels and centroids, and the iteration count equal the restatement's
+    (k > 64 exercises the two-chunk assignment; n < k duplicates centres)."""
+    from tiler_amd.palette import kmeans
+    rng = np.random.default_rng(n + k)
+    centers = rng.normal(0, 10, (max(2, k // 2), 192))
+    X = centers[rng.integers(0, centers.shape[0], n)] + rng.normal(0, 3, (n, 192))
+    gl, gc, gi = kmeans(X, k)
+    ol, oc, oi = oracle.kmeans(X, k)
+    assert gi == oi
+    assert np.array_equal(gl, ol)
+    assert np.array_equal(gc.view(np.uint64), oc.view(np.uint64))
+
+
+def test_prepare_dither_tiles_bit_exact(gpu, oracle):
+    from tiler_amd.palette import prepare_dither_tiles
+    rgb = synth.keyframe_frames(np.random.default_rng(31), 3, 400).reshape(-1, 64)
+    gl, gc, gi = prepare_dither_tiles(rgb, 16)
+    ol, oc, oi = oracle.prepare_dither_tiles(rgb, 16)
+    assert gi == oi and np.array_equal(gl, ol) and np.array_equal(gc, oc)
+    zl, zc, _ = prepare_dither_tiles(rgb[:1], 16)  # fewer than two tiles: the reference's zero branch
+    assert not zl.any() and not zc.any()
+
+
+def test_generate_palettes_chain_bit_exact(gpu, oracle):
+    """btnDitherClick's palette half over two keyframes on the GPU: DitheringPalIndex, palettes (DLv3 + CMULHS),
+    centroids and the FinishQuantizePalette order equal the CPU chain's."""
+    from tiler_amd.palette import generate_palettes
+    rng = np.random.default_rng(41)
+    frames = np.concatenate([synth.keyframe_frames(rng, 2, 300), synth.keyframe_frames(rng, 3, 300)])
+    kf = np.array([0, 2, 5])
+    g = generate_palettes(frames, kf, 8)
+    o = oracle.generate_palettes(frames, kf, 8)
+    for a, b, name in zip(g, o, ("palettes", "centroids", "dith", "use_count")):
+        assert np.array_equal(a, b), name

@@ -182,3 +182,42 @@ def test_finish_quantize_order_product_matches_oracle(oracle, uc):
     order = np.argsort(lut)
     assert sorted(lut.tolist()) == list(range(len(uc)))
     assert all(uc[order[i]] >= uc[order[i + 1]] for i in range(len(uc) - 1))
+
+
+def _lab_float(r, g, b):
+    """RGBToLAB (main.pas:2711-2747) with Python's libm, gamma -1: the oracle's fdlibm path agrees to ~1 ulp."""
+    def lin(v):
+        v = v / 255.0
+        return ((v + 0.055) / 1.055) ** 2.4 if v > 0.04045 else v / 12.92
+    r, g, b = lin(r), lin(g), lin(b)
+    x = (r * 0.49 + g * 0.31 + b * 0.2) / 0.17697 / (96.6797 / 100)
+    y = (r * 0.17697 + g * 0.8124 + b * 0.01063) / 0.17697
+    z = (g * 0.01 + b * 0.99) / 0.17697 / (82.5188 / 100)
+    f = [t ** (1 / 3) if t > 0.008856 else 7.787 * t + 16 / 116 for t in (x, y, z)]
+    return 116 * f[1] - 16, 500 * (f[0] - f[1]), 200 * (f[1] - f[2])
+
+
+def test_oracle_lab_descriptor(oracle):
+    """A flat tile's LAB + Haar descriptor holds 8 x the LAB value in its DC terms and zeros elsewhere."""
+    for r, g, b in [(255, 255, 255), (0, 0, 0), (200, 30, 90), (5, 8, 3)]:
+        tile = np.full((1, 64), r | g << 8 | b << 16, np.int32)
+        d = oracle.psyv_lab_batch(tile)[0]
+        want = _lab_float(r, g, b)
+        for c in range(3):
+            assert abs(d[c * 64] - 8 * want[c]) < 1e-9 * max(1.0, abs(want[c])) * 8
+            assert np.all(np.abs(d[c * 64 + 1:(c + 1) * 64]) < 1e-12)
+
+
+def test_oracle_kmeans_separated_clusters(oracle):
+    rng = np.random.default_rng(8)
+    centers = rng.normal(0, 50, (6, 192))
+    lab = rng.integers(0, 6, 1200)
+    X = centers[lab] + rng.normal(0, 1, (1200, 192))
+    labels, cent, it = oracle.kmeans(X, 6)
+    assert it >= 2
+    # every found cluster is one true cluster (k-means++ on well separated data)
+    for c in range(6):
+        assert np.unique(lab[labels == c]).size == 1
+    for c in range(6):
+        m = labels == c
+        assert np.allclose(cent[c], X[m].mean(0), rtol=0, atol=1e-9)

@@ -86,6 +86,11 @@ _SIGS = {
                                         c_void_p]),
     "tiler_quantize_palettes_dev": (c_int, [c_long, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                                             c_void_p, c_void_p, c_void_p]),
+    "tiler_prepare_dither_tiles": (c_int, [c_long, c_void_p, c_int, c_int, c_int, c_int, c_uint32, c_void_p, c_void_p,
+                                           c_void_p]),
+    "tiler_prepare_dither_tiles_dev": (c_int, [c_long, c_void_p, c_int, c_int, c_int, c_int, c_uint32, c_void_p,
+                                               c_void_p, c_void_p, c_void_p]),
+    "tiler_kmeans": (c_int, [c_void_p, c_long, c_int, c_int, c_int, c_uint32, c_void_p, c_void_p, c_void_p]),
     "tiler_finish_quantize_order": (c_int, [c_int, c_void_p, c_void_p]),
     "tiler_interframe_correlation": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "tiler_interframe_correlation_dev": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

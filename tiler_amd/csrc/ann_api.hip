@@ -15,6 +15,8 @@
 #include "../../include/tiler_ann.h"
 #include "dither.hpp"
 #include "palette.hpp"
+#include "kmeans.hpp"
+#include "detmath.hpp"
 #include "keyframes.hpp"
 #include "kmodes.hpp"
 #include "nn_search.hpp"
@@ -67,10 +69,15 @@ KTimer::~KTimer() {
 // InitLuts main.pas:592-642; constants main.pas:63-98, 2675-2676, 2816, 3000-3009 -- all on the host,
 // identical expressions to the CPU restatement, so device and oracle share the same bits.
 static int upload_gamma_lut() {
-    std::vector<double> g(3 * 256);
+    std::vector<double> g(3 * 256), lin(3 * 256);
     for (int gi = -1; gi <= 1; gi++)
         for (int i = 0; i < 256; i++) g[(gi + 1) * 256 + i] = (gi >= 0) ? pow(i / 255.0, g_gamma[gi]) : i / 255.0;
+    for (int k = 0; k < 3 * 256; k++) {  // RGBToLAB main.pas:2719-2721 (FPC power = exp(2.4 * ln(.)), detmath.hpp)
+        const double v = g[k];
+        lin[k] = v > 0.04045 ? fpc_power_frac((v + 0.055) / 1.055, 2.4) : v / 12.92;
+    }
     TILER_HIP_CHECK(hipMemcpy(g_luts.d_gamma, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
+    TILER_HIP_CHECK(hipMemcpy(g_luts.d_lab_lin, lin.data(), lin.size() * sizeof(double), hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -104,6 +111,7 @@ static int build_luts() {
     TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_dct, 4096 * sizeof(double)));
     TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_qmul, 192 * sizeof(double)));
     TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_ratio, 64 * sizeof(double)));
+    TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_lab_lin, 3 * 256 * sizeof(double)));
     TILER_HIP_CHECK(hipMemcpy(g_luts.d_dct, dct.data(), 4096 * sizeof(double), hipMemcpyHostToDevice));
     TILER_HIP_CHECK(hipMemcpy(g_luts.d_qmul, qm.data(), 192 * sizeof(double), hipMemcpyHostToDevice));
     TILER_HIP_CHECK(hipMemcpy(g_luts.d_ratio, ratio.data(), 64 * sizeof(double), hipMemcpyHostToDevice));
@@ -425,10 +433,6 @@ int tiler_psyv_batch_dev(int n, const int32_t *rgb, const uint8_t *palpix, const
                          const int32_t *palettes, const int32_t *pal_of, const uint8_t *flags_per, int flags, int gamma,
                          double *out64, float *out32, void *stream) {
     if (!ensure_init()) return -1;
-    if ((flags & 4) != 0) {
-        set_error("psyv: UseLAB is not on the hot path and is not supported");
-        return -1;
-    }
     PsyvArgs a;
     a.n = n;
     a.rgb = rgb;
@@ -613,6 +617,77 @@ int tiler_quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_
     if (!ensure_init()) return -1;
     return quantize_palettes_dev(n_tiles, d_rgb, d_pal_of, d_active, n_palettes, palsize, lookup_bpc, palettes,
                                  use_count, colors, (hipStream_t)stream);
+}
+
+int tiler_prepare_dither_tiles_dev(long n_tiles, const int32_t *d_rgb, int n_palettes, int gamma, int use_wavelets,
+                                   int max_iter, uint32_t seed, int32_t *d_labels, double *d_centroids,
+                                   int *iterations, void *stream) {
+    if (!ensure_init()) return -1;
+    return prepare_dither_dev(n_tiles, d_rgb, n_palettes, gamma, use_wavelets, max_iter <= 0 ? 0x7fffffff : max_iter,
+                              seed, d_labels, d_centroids, iterations, (hipStream_t)stream);
+}
+
+int tiler_prepare_dither_tiles(long n_tiles, const int32_t *rgb, int n_palettes, int gamma, int use_wavelets,
+                               int max_iter, uint32_t seed, int32_t *labels, double *centroids, int *iterations) {
+    if (!ensure_init()) return -1;
+    if (n_tiles < 0 || n_palettes <= 0 || (n_tiles > 0 && (!rgb || !labels)) || !centroids) {
+        set_error("prepare_dither_tiles: invalid arguments");
+        return -1;
+    }
+    const size_t b_rgb = (size_t)n_tiles * 256, b_lab = (size_t)n_tiles * 4, b_c = (size_t)n_palettes * 192 * 8;
+    char *buf = nullptr;
+    TILER_HIP_CHECK(hipMalloc((void **)&buf, b_rgb + b_lab + b_c + 512));
+    char *d_rgb = buf, *d_lab = buf + ((b_rgb + 255) & ~(size_t)255), *d_c = d_lab + ((b_lab + 255) & ~(size_t)255);
+    hipStream_t st = nullptr;
+    int rc = -1;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) {
+        do {
+            if (n_tiles > 0 && hipMemcpyAsync(d_rgb, rgb, b_rgb, hipMemcpyHostToDevice, st) != hipSuccess) break;
+            if (prepare_dither_dev(n_tiles, (const int32_t *)d_rgb, n_palettes, gamma, use_wavelets,
+                                   max_iter <= 0 ? 0x7fffffff : max_iter, seed, (int32_t *)d_lab, (double *)d_c,
+                                   iterations, st))
+                break;
+            if (n_tiles > 0 && hipMemcpyAsync(labels, d_lab, b_lab, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+            if (hipMemcpyAsync(centroids, d_c, b_c, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+            if (hipStreamSynchronize(st) != hipSuccess) break;
+            rc = 0;
+        } while (0);
+        (void)hipStreamDestroy(st);
+    }
+    if (rc && !last_error()[0]) set_error("prepare_dither_tiles: HIP failure");
+    (void)hipFree(buf);
+    return rc;
+}
+
+int tiler_kmeans(const double *X, long n, int d, int k, int max_iter, uint32_t seed, int32_t *labels,
+                 double *centroids, int *iterations) {
+    if (!ensure_init()) return -1;
+    if (n <= 0 || d <= 0 || d > 192 || k <= 0 || !X || !labels || !centroids) {
+        set_error("kmeans: invalid arguments");
+        return -1;
+    }
+    const size_t bx = (size_t)n * d * 8, bl = (size_t)n * 4, bc = (size_t)k * d * 8;
+    char *buf = nullptr;
+    TILER_HIP_CHECK(hipMalloc((void **)&buf, bx + bl + bc + 512));
+    char *d_x = buf, *d_l = buf + ((bx + 255) & ~(size_t)255), *d_c = d_l + ((bl + 255) & ~(size_t)255);
+    hipStream_t st = nullptr;
+    int rc = -1;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) {
+        do {
+            if (hipMemcpyAsync(d_x, X, bx, hipMemcpyHostToDevice, st) != hipSuccess) break;
+            if (kmeans_dev((const double *)d_x, n, d, k, max_iter <= 0 ? 0x7fffffff : max_iter, seed, (int32_t *)d_l,
+                           (double *)d_c, iterations, st))
+                break;
+            if (hipMemcpyAsync(labels, d_l, bl, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+            if (hipMemcpyAsync(centroids, d_c, bc, hipMemcpyDeviceToHost, st) != hipSuccess) break;
+            if (hipStreamSynchronize(st) != hipSuccess) break;
+            rc = 0;
+        } while (0);
+        (void)hipStreamDestroy(st);
+    }
+    if (rc && !last_error()[0]) set_error("kmeans: HIP failure");
+    (void)hipFree(buf);
+    return rc;
 }
 
 int tiler_finish_quantize_order(int n_palettes, const int32_t *use_count, int32_t *lut) {

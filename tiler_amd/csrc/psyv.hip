@@ -33,7 +33,10 @@ __global__ __launch_bounds__(256) void psyv_kernel(PsyvArgs a) {
             col = a.rgb[i * 64 + src];
         }
         double cp[3];
-        yuv_of(col, glut, a.u_mul, a.v_mul, cp[0], cp[1], cp[2]);
+        if (f & PSYV_LAB)
+            lab_of(col, a.lab_lin + 256 * (a.gamma + 1), cp[0], cp[1], cp[2]);
+        else
+            yuv_of(col, glut, a.u_mul, a.v_mul, cp[0], cp[1], cp[2]);
         double out[3];
         if (f & PSYV_WAVELETS) {
 #pragma unroll
@@ -130,6 +133,7 @@ int launch_psyv(PsyvArgs args, hipStream_t stream) {
     args.dct_lut = L.d_dct;
     args.qmul = L.d_qmul;
     args.ratio = L.d_ratio;
+    args.lab_lin = L.d_lab_lin;
     args.haar_f = L.haar_f;
     args.u_mul = L.u_mul;
     args.v_mul = L.v_mul;

@@ -4,7 +4,7 @@
 
 namespace tiler {
 
-enum { PSYV_FROM_PAL = 1, PSYV_WAVELETS = 2, PSYV_QWEIGHT = 8, PSYV_HMIRROR = 16, PSYV_VMIRROR = 32 };
+enum { PSYV_FROM_PAL = 1, PSYV_WAVELETS = 2, PSYV_LAB = 4, PSYV_QWEIGHT = 8, PSYV_HMIRROR = 16, PSYV_VMIRROR = 32 };
 
 struct PsyvArgs {
     long n = 0;
@@ -23,7 +23,7 @@ struct PsyvArgs {
     const float *box = nullptr;
     float *rootbox = nullptr;
     // filled by launch_psyv from the shared LUTs
-    const double *gamma_lut = nullptr, *dct_lut = nullptr, *qmul = nullptr, *ratio = nullptr;
+    const double *gamma_lut = nullptr, *dct_lut = nullptr, *qmul = nullptr, *ratio = nullptr, *lab_lin = nullptr;
     double haar_f = 0, u_mul = 0, v_mul = 0;
 };
 

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "detmath.hpp"
+
 namespace tiler {
 
 struct PsyvConst {
@@ -25,6 +27,25 @@ __device__ __forceinline__ void yuv_of(int32_t col, const double *__restrict__ g
     cy = (2126.0 * fr + 7152.0 * fg + 722.0 * fb) / 10000.0;
     cu = (fb - cy) * u_mul;
     cv = (fr - cy) * v_mul;
+}
+
+// RGBToLAB main.pas:2711-2747 (UseLAB: the Dither step's descriptors); lin = the gamma row of the host-built
+// linearised-channel LUT (main.pas:2715-2721), the cube roots are FPC power = exp(ln(t) / 3) (detmath.hpp)
+__device__ __forceinline__ void lab_of(int32_t col, const double *__restrict__ lin, double &ol, double &oa,
+                                       double &ob) {
+    const double r = lin[col & 0xff], g = lin[(col >> 8) & 0xff], b = lin[(col >> 16) & 0xff];
+    double x = (r * 0.49000 + g * 0.31000 + b * 0.20000) / 0.17697;
+    double y = (r * 0.17697 + g * 0.81240 + b * 0.01063) / 0.17697;
+    double z = (r * 0.00000 + g * 0.01000 + b * 0.99000) / 0.17697;
+    x /= 96.6797 / 100;  // illuminant D50
+    y /= 100.000 / 100;
+    z /= 82.5188 / 100;
+    x = x > 0.008856 ? fpc_power_frac(x, 1.0 / 3.0) : (7.787 * x) + 16.0 / 116.0;
+    y = y > 0.008856 ? fpc_power_frac(y, 1.0 / 3.0) : (7.787 * y) + 16.0 / 116.0;
+    z = z > 0.008856 ? fpc_power_frac(z, 1.0 / 3.0) : (7.787 * z) + 16.0 / 116.0;
+    ol = (116 * y) - 16;
+    oa = 500 * (x - y);
+    ob = 200 * (y - z);
 }
 
 // one WaveletGS level on the dx x dx top-left block (main.pas:2818-2836)

@@ -20,6 +20,7 @@ struct Luts {
     double *d_dct = nullptr;    // [4096] gDCTLut (main.pas:615-623), computed on the host
     double *d_qmul = nullptr;   // [3][64] cDCTQuantization (main.pas:63-98) = 4/sqrt(q)
     double *d_ratio = nullptr;  // [64] cUVRatio (main.pas:3000-3009)
+    double *d_lab_lin = nullptr;  // [3][256]: RGBToLAB's linearised channel of GammaCorrect rows (main.pas:2715-2721)
     double haar_f = 0.0;        // 1.0/sqrt(2.0) (main.pas:2816)
     double u_mul = 0.0;         // 0.5 / (1.0 - 722/10000)   (main.pas:2675)
     double v_mul = 0.0;         // 0.5 / (1.0 - 2126/10000)  (main.pas:2676)

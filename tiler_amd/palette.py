@@ -57,3 +57,60 @@ def finish_quantize_palette(palettes, use_count, dith_pal, centroids=None):
         new_cent = np.empty_like(centroids)
         new_cent[lut] = centroids
     return new_pal, new_dith, new_cent, lut
+
+
+def kmeans(X, k: int, max_iter: int = 0, seed: int = 0):
+    """The Dither step's k-means over X [n][d] fp64 (d <= 192) -> (labels [n], centroids [k][d], assignments)."""
+    X = np.ascontiguousarray(X, np.float64)
+    n, d = X.shape
+    labels = np.zeros(n, np.int32)
+    cent = np.zeros((k, d), np.float64)
+    it = ctypes.c_int(0)
+    check(load().tiler_kmeans(_p(X), n, d, k, max_iter, seed, _p(labels), _p(cent), ctypes.byref(it)), "tiler_kmeans")
+    return labels, cent, it.value
+
+
+def prepare_dither_tiles(rgb, n_palettes: int, gamma: int = -1, use_wavelets: bool = True, max_iter: int = 0,
+                         seed: int = 0):
+    """PrepareDitherTiles for one keyframe (main.pas:2097-2152): its tiles rgb [n][64] (frame order) ->
+    (DitheringPalIndex [n], PaletteCentroids [n_palettes][192], Lloyd assignments)."""
+    rgb = np.ascontiguousarray(rgb, np.int32).reshape(-1, 64)
+    labels = np.zeros(rgb.shape[0], np.int32)
+    cent = np.zeros((n_palettes, 192), np.float64)
+    it = ctypes.c_int(0)
+    check(load().tiler_prepare_dither_tiles(rgb.shape[0], _p(rgb), n_palettes, gamma, 1 if use_wavelets else 0,
+                                            max_iter, seed, _p(labels), _p(cent), ctypes.byref(it)),
+          "tiler_prepare_dither_tiles")
+    return labels, cent, it.value
+
+
+def generate_palettes(frames, kf_start, n_palettes: int, palsize: int = 16, gamma: int = -1,
+                      use_wavelets: bool = True, bpc: int = DLV3_BPC, max_iter: int = 0):
+    """The palette half of btnDitherClick (main.pas:886-907) over all keyframes: PrepareDitherTiles per keyframe,
+    QuantizePalette for every (keyframe, palette) pair in one GPU pass, FinishQuantizePalette per keyframe.
+    frames [F][Q][64] RGB, kf_start [KF+1] -> (palettes [KF][P][palsize], centroids [KF][P][192],
+    DitheringPalIndex [F*Q], use counts [KF][P])."""
+    frames = np.ascontiguousarray(frames, np.int32)
+    F, Q = frames.shape[:2]
+    kf_start = np.asarray(kf_start, np.int64)
+    KF, P = kf_start.size - 1, n_palettes
+    dith = np.zeros(F * Q, np.int32)
+    cent = np.zeros((KF, P, 192), np.float64)
+    for k in range(KF):
+        f0, f1 = int(kf_start[k]), int(kf_start[k + 1])
+        lab, c, _ = prepare_dither_tiles(frames[f0:f1].reshape(-1, 64), P, gamma, use_wavelets, max_iter)
+        dith[f0 * Q:f1 * Q] = lab
+        cent[k] = c
+    kf_of_tile = np.repeat(np.repeat(np.arange(KF), np.diff(kf_start)), Q)
+    pal, uc, _ = quantize_palettes(frames.reshape(-1, 64), (kf_of_tile * P + dith).astype(np.int32), KF * P, palsize,
+                                   bpc)
+    pal = pal.reshape(KF, P, palsize)
+    uc = uc.reshape(KF, P)
+    for k in range(KF):
+        f0, f1 = int(kf_start[k]), int(kf_start[k + 1])
+        pal[k], dith[f0 * Q:f1 * Q], cent[k], lut = finish_quantize_palette(pal[k], uc[k], dith[f0 * Q:f1 * Q],
+                                                                             cent[k])
+        u2 = np.empty_like(uc[k])
+        u2[lut] = uc[k]
+        uc[k] = u2
+    return pal, cent, dith, uc

@@ -206,3 +206,32 @@ def test_load_dither_chain(gpu, oracle):
     from gtm_read import read_gtm
     g = read_gtm(oracle, e.save_stream(tm_w * 8, tm_h * 8, 24.0))
     assert len(g.frames) == e.frames and np.array_equal(g.tiles, e.palpix)
+
+
+@pytest.mark.gpu
+def test_load_dither_generated_palettes_chain(gpu, oracle):
+    """SURVEY.md 8(f)-3 complete: Load -> Dither with GPU-generated palettes (PrepareDitherTiles' k-means over LAB
+    descriptors, QuantizePalette DLv3, FinishQuantizePalette, FinishDitherTiles) -> MakeUnique -> GlobalTiling ->
+    FrameTiling (Medium: uses the generated PaletteCentroids) -> Reindex -> Smooth -> SaveStream, bit-exact against
+    the same chain composed from the CPU restatements."""
+    from tiler_amd.encoder import Encoder, load_and_dither
+    rng = np.random.default_rng(79)
+    tm_w, tm_h = 20, 15
+    frames, _ = synth.shot_frames(rng, 10, tm_w, tm_h, shot_len=(4, 6))
+    v = load_and_dither(frames, tm_w, tm_h, n_palettes=8)
+    okf, nkf = oracle.find_keyframes(oracle.interframe_corr_batch(frames, tm_w, tm_h), 10, tm_w * tm_h)
+    kf_start = np.r_[np.flatnonzero(np.r_[True, okf[1:] != okf[:-1]]), 10]
+    opals, ocents, odith, _ = oracle.generate_palettes(frames, kf_start, 8)
+    ov = synth.video_from_dither(frames, kf_start, opals, ocents, odith, oracle.dither_tiles_tk)
+    assert np.array_equal(v.kf_start, ov.kf_start)
+    for a, b in ((v.palettes, ov.palettes), (v.centroids, ov.centroids), (v.dith_pal, ov.dith_pal),
+                 (v.palpix, ov.palpix), (v.thm, ov.thm), (v.tvm, ov.tvm)):
+        assert np.array_equal(a, b)
+    o = _OracleChain(ov).run(oracle, 500, FT_MEDIUM, 0.2)
+    e = Encoder(v)
+    sm = e.run_all(500, FT_MEDIUM, 0.2)
+    for a, b in zip((sm["tile"], sm["pal"], sm["hm"], sm["vm"], sm["smoothed"]), o["smooth"]):
+        assert np.array_equal(a, b)
+    from gtm_read import read_gtm
+    g = read_gtm(oracle, e.save_stream(tm_w * 8, tm_h * 8, 24.0))
+    assert len(g.frames) == e.frames and np.array_equal(g.tiles, e.palpix)

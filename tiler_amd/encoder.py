@@ -20,17 +20,26 @@ from .smooth import DEFAULT_STRENGTH, smooth_keyframe
 from .synth import Video, video_from_frames
 
 
-def load_and_dither(frames, tm_w: int, tm_h: int, palettes_fn) -> Video:
-    """The Load and Dither steps in front of the chain (btnLoadClick main.pas:1099-1146, FinishDitherTiles
-    main.pas:2482-2544) on the GPU: keyframes from the inter-frame correlations, then every tile dithered with
-    its keyframe palette.  palettes_fn(k, frames_of_keyframe) -> [P][16] stands in for yakmo (out of scope)."""
+def load_and_dither(frames, tm_w: int, tm_h: int, palettes_fn=None, n_palettes: int = 8, gamma: int = -1,
+                    use_wavelets: bool = True) -> Video:
+    """The Load and Dither steps in front of the chain on the GPU (btnLoadClick main.pas:1099-1146, btnDitherClick
+    main.pas:858-914): keyframes from the inter-frame correlations, then the keyframe palettes -- PrepareDitherTiles
+    (LAB descriptors + k-means -> DitheringPalIndex, PaletteCentroids), QuantizePalette (DLv3), FinishQuantizePalette
+    (tiler_amd.palette) -- and every tile dithered with its palette (FinishDitherTiles).  palettes_fn(k,
+    frames_of_keyframe) -> [P][16], when given, replaces the palette generation (with the stand-in palette choice
+    of synth.video_from_frames)."""
     from .dither import dither_tiles
     from .keyframes import detect_keyframes
+    from .palette import generate_palettes
+    from .synth import video_from_dither
     frames = np.ascontiguousarray(frames, np.int32).reshape(-1, tm_w * tm_h, 64)
     kf_of, kf_start, _ = detect_keyframes(frames, tm_w, tm_h)
-    pals = np.stack([np.asarray(palettes_fn(k, frames[kf_start[k]:kf_start[k + 1]]), np.int32)
-                     for k in range(kf_start.size - 1)])
-    return video_from_frames(frames, kf_of, pals, dither_tiles)
+    if palettes_fn is not None:
+        pals = np.stack([np.asarray(palettes_fn(k, frames[kf_start[k]:kf_start[k + 1]]), np.int32)
+                         for k in range(kf_start.size - 1)])
+        return video_from_frames(frames, kf_of, pals, dither_tiles)
+    pals, cents, dith, _ = generate_palettes(frames, kf_start, n_palettes, gamma=gamma, use_wavelets=use_wavelets)
+    return video_from_dither(frames, kf_start, pals, cents, dith, dither_tiles)
 
 
 class Encoder:

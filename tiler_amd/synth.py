@@ -285,6 +285,23 @@ def video_from_frames(frames: np.ndarray, kf_of_frame, pals: np.ndarray, dithere
                  np.asarray(thm, np.uint8), np.asarray(tvm, np.uint8), dith.reshape(-1))
 
 
+def video_from_dither(frames: np.ndarray, kf_start, pals: np.ndarray, centroids: np.ndarray, dith: np.ndarray,
+                      ditherer) -> Video:
+    """Load -> Dither with generated palettes: keyframe palettes pals [KF][P][16], PaletteCentroids [KF][P][192] and
+    every tile's DitheringPalIndex dith [F*Q] (tiler_amd.palette.generate_palettes or the oracle's), every tile
+    dithered by `ditherer(rgb, pal_of, palettes)` (FinishDitherTiles main.pas:2482-2544)."""
+    frames = np.ascontiguousarray(frames, np.int32)
+    F, q = frames.shape[:2]
+    kf_start = np.asarray(kf_start, np.int64)
+    KF, P = pals.shape[:2]
+    kf_of = np.repeat(np.arange(KF), np.diff(kf_start))
+    dith = np.asarray(dith, np.int32).reshape(F, q)
+    flat_of = (kf_of[:, None] * P + dith).reshape(-1).astype(np.int32)
+    palpix, thm, tvm = ditherer(frames.reshape(-1, 64), flat_of, np.asarray(pals, np.int32).reshape(KF * P, -1))
+    return Video(frames, kf_start, np.asarray(pals, np.int32), np.asarray(centroids, np.float64),
+                 np.asarray(palpix, np.uint8), np.asarray(thm, np.uint8), np.asarray(tvm, np.uint8), dith.reshape(-1))
+
+
 def globaltiling_workload(seed: int, n: int = 1 << 20, protos: int = 65536, noise: float = 0.1,
                           n_palettes: int = 128, zipf: float = 1.1, palsize: int = 16):
     """SURVEY.md 8(d) C4 GlobalTiling input: n palette-index tiles drawn from `protos` prototypes with

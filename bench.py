@@ -212,7 +212,10 @@ def main():
                          "M/G, the exact 4-mirror orbit algebra). hbm = the metric's '% HBM roofline': SURVEY.md 8(d) "
                          "bytes per matched tile x tiles / ms_per_step -- small by construction, the search is "
                          "MFMA-bound (SURVEY.md 7, hard part 5)")}
-    for kn, bpt in (("psyv", 256 + 768),):  # HBM-bound helpers: algorithmic bytes per launch / launch time
+    # HBM-bound helpers: algorithmic bytes per launch / launch time.  "psyv" times the fused FrameTiling query
+    # kernel (orbit_ft_query_kernel): 256 B RGB in; 768 B fp32 row + 384 B fp16 q' fragments + 32 B error
+    # statistics + 4 B root-box distance out per tile
+    for kn, bpt in (("psyv", 256 + 768 + 384 + 32 + 4),):
         kk = kernels.get(kn)
         if kk and kk["ms_avg"]:
             g = bpt * QK / (kk["ms_avg"] * 1e-3) / 1e9

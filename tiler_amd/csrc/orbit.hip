@@ -25,6 +25,7 @@
 #include "nn_dev.hpp"
 #include "psyv_dev.hpp"
 #include "orbit.hpp"
+#include "orbit_map_gen.hpp"
 
 namespace tiler {
 
@@ -170,6 +171,14 @@ static bool build_map(OrbitMap &m) {
     }
     for (int x = 0; x < 4; x++)
         if (fill[x] != 48) return false;
+    // the fused query kernel reads the compile-time copy (tools/gen_orbit_map.py): it must be this map exactly
+    for (int x = 0; x < 4; x++)
+        for (int o = 0; o < 48; o++) {
+            const int oo = x * 48 + o, no = out_size[x][o];
+            if (orbitgen::CNT[oo] != no) return false;
+            for (int t = 0; t < no; t++)
+                if (orbitgen::SRC[oo][t] != out_src[x][o][t] || orbitgen::W[oo][t] != out_w[x][o][t]) return false;
+        }
     for (int x = 0; x < 4; x++)
         for (int o = 0; o < 48; o++) {
             const int oo = x * 48 + o, no = out_size[x][o];
@@ -1320,7 +1329,6 @@ struct FtQueryArgs {
     int gamma;
     const double *gamma_lut;
     double haar_f, u_mul, v_mul;
-    const OrbitMap *mp;
     float scale;
     float *out32;        // [n][192]
     half8 *frag;         // [ceil(n/32)][12][64]
@@ -1334,16 +1342,9 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
     __shared__ double lut[256];
     __shared__ float st[64 * 65];  // one component of the 64 tiles: row-major per lane, stride 65 (conflict-free)
     __shared__ float sbox[2 * OD];
-    __shared__ int16_t msrc[OD * 4];
-    __shared__ float mw[OD * 4], mq[OD];
     const int lane = threadIdx.x;
     const double *__restrict__ glut = a.gamma_lut + 256 * (a.gamma + 1);
     for (int i = lane; i < 256; i += 64) lut[i] = glut[i];
-    for (int i = lane; i < OD * 4; i += 64) {
-        msrc[i] = a.mp->src[i >> 2][i & 3];
-        mw[i] = a.mp->w[i >> 2][i & 3];
-    }
-    for (int i = lane; i < OD; i += 64) mq[i] = a.mp->qs[i];
     if (a.box)
         for (int i = lane; i < 2 * OD; i += 64) sbox[i] = a.box[i];
     __syncthreads();
@@ -1381,13 +1382,8 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
             for (int k = 0; k < 64; k++) {  // annBoxDistance, dimension order
                 const float v = row[k];
                 const float lo = sbox[c * 64 + k], hi = sbox[OD + c * 64 + k];
-                if (v < lo) {
-                    const float t = lo - v;
-                    rb = rb + t * t;
-                } else if (v > hi) {
-                    const float t = v - hi;
-                    rb = rb + t * t;
-                }
+                const float t = fmaxf(lo - v, 0.0f) + fmaxf(v - hi, 0.0f);  // lo <= hi: one term at most; + 0 exact
+                rb = rb + t * t;
             }
         }
         __syncthreads();
@@ -1415,12 +1411,16 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
 #pragma unroll
             for (int j = 0; j < 16; j++) {  // constant j: hv stays in registers (no dynamic vector index)
                 const int k = s * 16 + j;
+                // wave-uniform table entries (scalar loads of orbit_map_gen.hpp's tables), one LDS read per term
+                const int cnt = orbitgen::CNT[k];
                 double v = 0.0;
-                if (valid) {
 #pragma unroll
-                    for (int t = 0; t < 4; t++) v += (double)mw[k * 4 + t] * (double)row[(msrc[k * 4 + t] - 64 * c) & 63];
-                    v *= (double)mq[k] * (double)a.scale;
-                }
+                for (int t = 0; t < 4; t++)
+                    if (t < cnt) {  // W = +-1: w * r is exactly +-r, so add or subtract (no multiply)
+                        const double r = (double)row[orbitgen::SRC[k][t] - 64 * c];
+                        v = orbitgen::W[k][t] > 0.0 ? v + r : v - r;
+                    }
+                v = valid ? v * ((cnt == 1 ? 1.0 : 0.5) * (double)a.scale) : 0.0;
                 _Float16 vh = (_Float16)(float)v;
                 if (fabs((double)(float)vh) < 6.103515625e-05) vh = (_Float16)0.0f;  // no fp16 subnormal operands
                 hv[j >> 3][j & 7] = vh;
@@ -1465,7 +1465,6 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
     fa.haar_f = L.haar_f;
     fa.u_mul = L.u_mul;
     fa.v_mul = L.v_mul;
-    fa.mp = (const OrbitMap *)o->d_map;
     fa.scale = ix->scale;
     fa.out32 = qrows;
     fa.frag = (half8 *)o->qfrag;

@@ -67,3 +67,24 @@ def test_smooth_single_frame_is_identity(gpu):
     z = np.zeros((1, 50), np.uint8)
     g = smooth_keyframe(tile, np.zeros_like(tile), z, z, z, rng.integers(0, 16, (10, 64)), synth.palettes(rng, 1))
     assert np.array_equal(g[0], tile)
+
+
+@pytest.mark.timeout(600)
+def test_smooth_c3_size(gpu, oracle):
+    """Smooth at the C3 step's size: one keyframe of 24 frames x 32,400 positions (1080p), a 4,096-tile set with
+    near-duplicate twins, 128 palettes, the default strength: items and flags bit-exact against the restatement
+    (which computes every compared descriptor; about a minute on the box's host)."""
+    rng = np.random.default_rng(2402)
+    F, Q, T, P = 24, 32400, 4096, 128
+    palpix = rng.integers(0, 16, (T, 64)).astype(np.uint8)
+    palpix[T // 2:] = palpix[:T // 2]
+    palpix[T // 2:, 7] = (palpix[T // 2:, 7] + 1) % 16
+    pals = synth.palettes(rng, P)
+    pals[1] = pals[0] + 1
+    tile, pal, hm, vm = _tilemaps(rng, F, Q, T, P)
+    sm = np.zeros((F, Q), np.uint8)
+    g = smooth_keyframe(tile, pal, hm, vm, sm, palpix, pals, 0.04)
+    o = oracle.smooth(tile, pal, hm, vm, sm, palpix, pals, 0.04)
+    for a, b in zip(g, o):
+        assert np.array_equal(a, b)
+    assert g[4].sum() > 0

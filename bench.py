@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--no-smooth", action="store_true")
     ap.add_argument("--no-keyframes", action="store_true")
     ap.add_argument("--no-dither", action="store_true")
+    ap.add_argument("--no-globaltiling", action="store_true", help="skip the C4 K-Modes secondary line")
     ap.add_argument("--clip-frames", type=int, default=1000, help="keyframe-detection clip length (C3: 1000)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI, the product); gloo only to rehearse the N>1 control flow")
@@ -354,6 +355,15 @@ def main():
                                                      np.sum(d_dvm[:ns].cpu().numpy() != ovm))
         del d_px, d_dhm, d_dvm, d_pal_of
 
+    # ---- secondary: GlobalTiling K-Modes at C4 (BASELINE.json config 4; bench_globaltiling.py) ----
+    gtl = None
+    if rank == 0 and not args.no_globaltiling:
+        import bench_globaltiling
+        ga = bench_globaltiling.parser().parse_args([])
+        ga.no_cpu = args.no_cpu or world > 1
+        ga.cpu_seconds = min(10.0, args.cpu_seconds)
+        gtl = bench_globaltiling.run(ga)
+
     # ---- CPU baseline (rank 0, N=1): the oracle restatement, bounded sample, same workload ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -369,7 +379,8 @@ def main():
                        "tiles_per_step_per_gpu": QK, "candidates": M, "descriptor": "PsyV Haar 192-d",
                        "parallelism": f"keyframes sharded, {world} GPU(s)"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "search_stats": stats,
-            "secondary": {"prepare": prep, "smooth": smooth, "keyframes": keyframes, "dither": dither},
+            "secondary": {"prepare": prep, "smooth": smooth, "keyframes": keyframes, "dither": dither,
+                          "globaltiling": gtl},
         }
         print(json.dumps(res))
     kdt.close()

@@ -128,17 +128,21 @@ def run(args) -> dict:
                   and (int(iters[r]), int(costs[r])) == (oi, ocost))
             return x.shape[0], ok
 
-        done_pts, done_bins, mism, spent = 0, 0, 0, 0.0
+        done_pts, done_bins, mism, spent, work = 0, 0, 0, 0.0, 0.0
         tc = time.perf_counter()
         with ThreadPoolExecutor(workers) as ex:
             pos = 0
             while pos < len(order) and spent < args.cpu_seconds:
                 batch = order[pos:pos + workers]
+                bw = float(sum((off[r + 1] - off[r]) * ks[r] for r in batch))  # K-Modes work ~ n * K
+                if spent > 0 and spent + bw * spent / work > args.cpu_seconds:
+                    break  # the next batch would overrun the budget at the rate seen so far
                 pos += len(batch)
                 for n_pts, ok in ex.map(one, batch):
                     done_pts += n_pts
                     done_bins += 1
                     mism += int(not ok)
+                work += bw
                 spent = time.perf_counter() - tc
         cpu = {"value": round(done_pts / spent, 1) if spent else None, "unit": "points/s (full K-Modes run per bin)",
                "cores": workers * per_bin, "kind": "port",

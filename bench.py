@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--no-keyframes", action="store_true")
     ap.add_argument("--no-dither", action="store_true")
     ap.add_argument("--no-globaltiling", action="store_true", help="skip the C4 K-Modes secondary line")
+    ap.add_argument("--no-palettes", action="store_true", help="skip the palette-generation secondary line")
+    ap.add_argument("--palette-frames", type=int, default=8, help="frames of the palette-generation line")
     ap.add_argument("--clip-frames", type=int, default=1000, help="keyframe-detection clip length (C3: 1000)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI, the product); gloo only to rehearse the N>1 control flow")
@@ -355,6 +357,55 @@ def main():
                                                      np.sum(d_dvm[:ns].cpu().numpy() != ovm))
         del d_px, d_dhm, d_dvm, d_pal_of
 
+    # ---- secondary: the Dither step's palette generation over one keyframe (btnDitherClick main.pas:886-907):
+    # PrepareDitherTiles (LAB descriptors + k-means, k = 128), QuantizePalette (DLv3) for the 128 palettes,
+    # FinishQuantizePalette; frames: a 1080p shot (smooth 16-px blocks + +-2 noise, synth.shot_frames) ----
+    palettes_line = None
+    if rank == 0 and not args.no_palettes:
+        from tiler_amd.palette import generate_palettes
+        pf, _ = synth.shot_frames(np.random.default_rng(args.seed + 11), args.palette_frames, W // 8, H // 8,
+                                  shot_len=(args.palette_frames, args.palette_frames), noise=2)
+        kfs = np.array([0, pf.shape[0]])
+        generate_palettes(pf[:1], np.array([0, 1]), P)  # warm-up (allocations, code objects)
+        torch.cuda.synchronize(dev)
+        lib.tiler_timing_reset()
+        lib.tiler_timing_enable(1)
+        t0 = time.perf_counter()
+        gp, gc, gd, guc = generate_palettes(pf, kfs, P)
+        tp = time.perf_counter() - t0
+        lib.tiler_timing_enable(0)
+        ph = {}
+        for name in ("psyv", "kmeans", "kmeans_assign", "kmeans_update", "dl3_table", "dl3_pass1", "dl3_reduce"):
+            n = ctypes.c_int(0)
+            ms = lib.tiler_timing_get(name.encode(), ctypes.byref(n))
+            ph[name] = round(ms, 2)
+        nt = pf.shape[0] * Q
+        palettes_line = {"value": round(nt / tp / 1e6, 4), "unit": "Mtiles/s", "ms": round(tp * 1e3, 1),
+                         "phases_ms": ph, "use_count_max": int(guc.max()),
+                         "shape": f"{pf.shape[0]} frames {W}x{H} ({nt} tiles), {P} palettes x 16, DLv3 bpc 7"}
+        if world == 1 and not args.no_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle
+            # bounded sample: DLv3 of the 8 smallest palettes of this keyframe (the GPU's DitheringPalIndex),
+            # each restated on one host thread; rate in palettes/s beside the GPU's 128 palettes in its DLv3 time
+            order = np.argsort(np.bincount(gd, minlength=P), kind="stable")
+            sel = [int(p) for p in order if 0 < np.count_nonzero(gd == p)][:8]
+            tiles_all = pf.reshape(-1, 64)
+            t0 = time.perf_counter()
+            mism = 0
+            for p in sel:
+                m = gd == p
+                op_, ouc, _ = pyoracle.quantize_palettes(tiles_all[m], np.zeros(int(m.sum()), np.int32), 1, threads=1)
+                mism += int(not np.array_equal(op_[0], gp[0][p]))
+            tc = time.perf_counter() - t0
+            dl3_s = (ph["dl3_table"] + ph["dl3_pass1"] + ph["dl3_reduce"]) / 1e3
+            palettes_line["cpu_baseline"] = {
+                "value": round(len(sel) / tc, 3), "unit": "palettes/s (QuantizePalette, DLv3)", "cores": 1,
+                "kind": "port", "sample": f"the {len(sel)} smallest palettes of the keyframe (oracle/palette.c)",
+                "gpu_palettes_per_s": round(P / dl3_s, 2) if dl3_s else None}
+            palettes_line["parity_palettes"] = len(sel)
+            palettes_line["parity_mismatches_vs_cpu"] = mism
+
     # ---- secondary: GlobalTiling K-Modes at C4 (BASELINE.json config 4; bench_globaltiling.py) ----
     gtl = None
     if rank == 0 and not args.no_globaltiling:
@@ -380,7 +431,7 @@ def main():
                        "parallelism": f"keyframes sharded, {world} GPU(s)"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "search_stats": stats,
             "secondary": {"prepare": prep, "smooth": smooth, "keyframes": keyframes, "dither": dither,
-                          "globaltiling": gtl},
+                          "palettes": palettes_line, "globaltiling": gtl},
         }
         print(json.dumps(res))
     kdt.close()

@@ -92,6 +92,17 @@ __device__ __forceinline__ float dl3_calc_err(const Dl3Entry &a, const Dl3Entry 
     return d1 + d2;
 }
 
+// A rigorous lower bound of the COMPUTED calc_err(a, b): sqrt(d1) + sqrt(d2) >= |Q_a - Q_b| (triangle inequality
+// through the merged mean), so the exact value is >= min(P_a, P_b) * |Q_a - Q_b|, and the float evaluation (four
+// roundings of non-negative terms, the counts' conversion) loses at most a factor (1 - 2^-24)^5.  A candidate whose
+// bound exceeds the current best strictly can neither win nor tie, so skipping it leaves every result unchanged.
+__device__ __forceinline__ double dl3_lower_bound(uint32_t qa, uint32_t na, uint32_t qb, uint32_t nb) {
+    const int dr = (int)(qa & 255) - (int)(qb & 255), dg = (int)((qa >> 8) & 255) - (int)((qb >> 8) & 255);
+    const int db = (int)((qa >> 16) & 255) - (int)((qb >> 16) & 255);
+    const double dd = (double)(dr * dr + dg * dg + db * db);
+    return __builtin_sqrt(dd) * (double)(na < nb ? na : nb) * (1.0 - 1e-6);
+}
+
 // first minimum: smaller error, equal errors -> smaller index (the reference's ascending scan with `<`)
 __device__ __forceinline__ void dl3_min(float &e, int &j, float e2, int j2) {
     if (e2 < e || (e2 == e && j2 < j)) {
@@ -130,7 +141,9 @@ __device__ void dl3_recount_block(const Dl3Tab &t, int i, int tot, float *sh_e, 
     float e = HUGE_VALF;
     int j = INT32_MAX;
     for (int k = i + 1 + (int)threadIdx.x; k < tot; k += DL3_T) {
-        const float cur = dl3_calc_err(a, dl3_load(t, k));
+        const uint32_t qk = t.Q[k], nk = t.N[k];
+        if (dl3_lower_bound(a.q, a.n, qk, nk) > (double)e) continue;  // cannot win or tie
+        const float cur = dl3_calc_err(a, Dl3Entry{t.R[k], t.G[k], t.B[k], nk, qk});
         if (cur < e) {
             e = cur;
             j = k;
@@ -148,7 +161,9 @@ __device__ void dl3_recount_wave(const Dl3Tab &t, int i, int tot) {
     float e = HUGE_VALF;
     int j = INT32_MAX;
     for (int k = i + 1 + (int)(threadIdx.x & 63); k < tot; k += 64) {
-        const float cur = dl3_calc_err(a, dl3_load(t, k));
+        const uint32_t qk = t.Q[k], nk = t.N[k];
+        if (dl3_lower_bound(a.q, a.n, qk, nk) > (double)e) continue;  // cannot win or tie
+        const float cur = dl3_calc_err(a, Dl3Entry{t.R[k], t.G[k], t.B[k], nk, qk});
         if (cur < e) {
             e = cur;
             j = k;
@@ -263,8 +278,10 @@ __device__ void dl3_recount_dist(const Dl3Tab &t, int *list, int c, int tot, flo
         if (t.C[i] == c) {
             list[atomicAdd(sh_n, 1)] = i;
         } else {
+            const float ei = t.E[i];
+            if (dl3_lower_bound(t.Q[i], t.N[i], b.q, b.n) > (double)ei) continue;  // no update possible
             const float cur = dl3_calc_err(dl3_load(t, i), b);
-            if (cur < t.E[i]) {
+            if (cur < ei) {
                 t.E[i] = cur;
                 t.C[i] = c;
             }
@@ -518,8 +535,8 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     do {
         if (hipMemsetAsync(d_uc, 0, 4 * (P + 2), stream) != hipSuccess) break;
         if (hipMemsetAsync(d_nruns, 0, 4, stream) != hipSuccess) break;
-        KTimer tk("dl3_table", stream);
         if (npix > 0) {
+            KTimer tk("dl3_table", stream);
             hipLaunchKernelGGL(dl3_keys_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, d_rgb, d_pal_of,
                                d_active, n_tiles, P, bpc, k0, v0, d_uc);
             if (hipGetLastError() != hipSuccess) break;

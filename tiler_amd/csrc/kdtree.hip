@@ -243,6 +243,149 @@ static float median_split_host(float *key, int *idx, int n, int n_lo) {
     return (float)(((double)(key[n_lo - 1] + key[n_lo])) / 2.0);
 }
 
+// A whole subtree of <= KD_SUB points per workgroup, entirely on the device: for every node (explicit stack) the
+// annSpread / annMaxSpread cut dimension (threads over dimensions, rows read coalesced), the node's keys into LDS
+// and annMedianSplit's quickselect by one thread on the LDS copy -- the same comparisons, swaps and cut value as
+// median_split_host -- so the subtree's permutation, cut dimensions and cut values are ANN's.
+static constexpr int KD_SUB = 1024;
+
+__global__ __launch_bounds__(256) void kd_subtree_kernel(const float *__restrict__ rows, int dd, int *__restrict__ pidx,
+                                                         const KdNodeDev *__restrict__ roots, int bs,
+                                                         int *__restrict__ cd_out, float *__restrict__ cv_out) {
+    __shared__ float key[KD_SUB];
+    __shared__ int idx[KD_SUB];
+    __shared__ float red_v[4];
+    __shared__ int red_d[4];
+    __shared__ int stk_s[64], stk_e[64];
+    __shared__ int sp, cur_s, cur_e, cur_cd;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const KdNodeDev R = roots[blockIdx.x];
+    const int S = R.s, m_all = R.e - R.s;
+    for (int i = tid; i < m_all; i += 256) idx[i] = pidx[S + i];
+    if (tid == 0) {
+        sp = 1;
+        stk_s[0] = 0;
+        stk_e[0] = m_all;
+    }
+    __syncthreads();
+    while (sp > 0) {
+        if (tid == 0) {
+            sp--;
+            cur_s = stk_s[sp];
+            cur_e = stk_e[sp];
+        }
+        __syncthreads();
+        const int s = cur_s, e = cur_e;
+        // annMaxSpread: first dimension of maximum spread (0 when every spread is 0)
+        float best = -INFINITY;
+        int bd = 0x7fffffff;
+        for (int d = tid; d < dd; d += 256) {
+            float mn = INFINITY, mx = -INFINITY;
+            for (int i = s; i < e; i++) {
+                const float v = rows[(long)idx[i] * dd + d];
+                mn = fminf(mn, v);
+                mx = fmaxf(mx, v);
+            }
+            const float spr = mx - mn;
+            if (spr > best || (spr == best && d < bd)) {
+                best = spr;
+                bd = d;
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ob = __shfl_xor(best, o, 64);
+            const int od = __shfl_xor(bd, o, 64);
+            if (ob > best || (ob == best && od < bd)) {
+                best = ob;
+                bd = od;
+            }
+        }
+        if (lane == 0) {
+            red_v[w] = best;
+            red_d[w] = bd;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            float b = red_v[0];
+            int d0 = red_d[0];
+            for (int k = 1; k < 4; k++)
+                if (red_v[k] > b || (red_v[k] == b && red_d[k] < d0)) {
+                    b = red_v[k];
+                    d0 = red_d[k];
+                }
+            cur_cd = b > 0.0f ? d0 : 0;
+        }
+        __syncthreads();
+        const int cd = cur_cd;
+        for (int i = s + tid; i < e; i += 256) key[i] = rows[(long)idx[i] * dd + cd];
+        __syncthreads();
+        if (tid == 0) {  // annMedianSplit on key[s..e) / idx[s..e)
+            float *kk = key + s;
+            int *ii = idx + s;
+            const int n = e - s, n_lo = n / 2;
+            auto sw = [&](int a, int b) {
+                const float tk = kk[a];
+                kk[a] = kk[b];
+                kk[b] = tk;
+                const int ti = ii[a];
+                ii[a] = ii[b];
+                ii[b] = ti;
+            };
+            int l = 0, r = n - 1;
+            while (l < r) {
+                int i = (r + l) / 2, k;
+                if (kk[i] > kk[r]) sw(i, r);
+                sw(l, i);
+                const float c = kk[l];
+                i = l;
+                k = r;
+                for (;;) {
+                    while (kk[++i] < c) {
+                    }
+                    while (kk[--k] > c) {
+                    }
+                    if (i < k)
+                        sw(i, k);
+                    else
+                        break;
+                }
+                sw(l, k);
+                if (k > n_lo)
+                    r = k - 1;
+                else if (k < n_lo)
+                    l = k + 1;
+                else
+                    break;
+            }
+            if (n_lo > 0) {
+                float c = kk[0];
+                int k = 0;
+                for (int i = 1; i < n_lo; i++)
+                    if (kk[i] > c) {
+                        c = kk[i];
+                        k = i;
+                    }
+                sw(n_lo - 1, k);
+            }
+            const int m = s + n_lo;
+            cd_out[S + m] = cd;
+            cv_out[S + m] = (float)(((double)(kk[n_lo - 1] + kk[n_lo])) / 2.0);
+            if (e - m > bs) {
+                stk_s[sp] = m;
+                stk_e[sp] = e;
+                sp++;
+            }
+            if (m - s > bs) {
+                stk_s[sp] = s;
+                stk_e[sp] = m;
+                sp++;
+            }
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < m_all; i += 256) pidx[S + i] = idx[i];
+}
+
 KdOrder KdTree::view() const {
     KdOrder o;
     o.pos = d_pos;
@@ -437,7 +580,8 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
         KD_PIN(h_nodes, g_pin_nodes, max_nodes * sizeof(KdNodeDev));
         KD_PIN(h_cut, g_pin_cut, max_nodes * 4);
         KD_CHECK(hipMemcpyAsync(t->d_pidx, h_pidx, (size_t)n * 4, hipMemcpyHostToDevice, stream));
-        std::vector<std::pair<int, int>> level{{0, n}}, next;
+        std::vector<std::pair<int, int>> level, next, deferred;  // deferred: subtrees built by kd_subtree_kernel
+        (n <= KD_SUB ? deferred : level).emplace_back(0, n);
         HostPool &pool = HostPool::get();
         while (!level.empty()) {
             // nodes sorted by size, descending: the big ones (> KD_CH points) are a prefix
@@ -487,8 +631,8 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
             next.clear();
             for (int i = 0; i < nn; i++) {
                 const int s = level[i].first, e = level[i].second, m = s + (e - s) / 2;
-                if (m - s > t->bs) next.emplace_back(s, m);
-                if (e - m > t->bs) next.emplace_back(m, e);
+                if (m - s > t->bs) (m - s <= KD_SUB ? deferred : next).emplace_back(s, m);
+                if (e - m > t->bs) (e - m <= KD_SUB ? deferred : next).emplace_back(m, e);
             }
             std::stable_sort(next.begin(), next.end(), [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
                 return a.second - a.first > b.second - b.first;
@@ -496,6 +640,34 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
             KD_CHECK(hipMemcpyAsync(t->d_pidx, h_pidx, (size_t)n * 4, hipMemcpyHostToDevice, stream));
             level.swap(next);
             t->levels++;
+        }
+        if (!deferred.empty()) {
+            // the host levels' cuts first; the subtree kernel adds its nodes' entries and permutes its segments
+            KD_CHECK(hipMemcpyAsync(t->d_cd, cdv.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
+            KD_CHECK(hipMemcpyAsync(t->d_cv, cvv.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
+            if (t->levels == 0) {  // the whole tree is one subtree: the enclosing box comes from a root spread
+                h_nodes[0] = KdNodeDev{0, n};
+                KD_CHECK(hipMemcpyAsync(d_nodes, h_nodes, sizeof(KdNodeDev), hipMemcpyHostToDevice, stream));
+                hipLaunchKernelGGL(kd_small_kernel, dim3(1), dim3(256), 0, stream, d_rows, dd, (const int *)t->d_pidx,
+                                   (const KdNodeDev *)d_nodes, 1, d_cut, d_keys, t->d_box);
+                KD_CHECK(hipGetLastError());
+            }
+            const int nd = (int)deferred.size();
+            for (int i = 0; i < nd; i++) h_nodes[i] = KdNodeDev{deferred[i].first, deferred[i].second};
+            KD_CHECK(hipMemcpyAsync(d_nodes, h_nodes, (size_t)nd * sizeof(KdNodeDev), hipMemcpyHostToDevice, stream));
+            hipLaunchKernelGGL(kd_subtree_kernel, dim3(nd), dim3(256), 0, stream, d_rows, dd, t->d_pidx,
+                               (const KdNodeDev *)d_nodes, t->bs, t->d_cd, t->d_cv);
+            KD_CHECK(hipGetLastError());
+            KD_CHECK(hipMemcpyAsync(h_pidx, t->d_pidx, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+            KD_CHECK(hipMemcpyAsync(cdv.data(), t->d_cd, nn1 * 4, hipMemcpyDeviceToHost, stream));
+            KD_CHECK(hipMemcpyAsync(cvv.data(), t->d_cv, nn1 * 4, hipMemcpyDeviceToHost, stream));
+            int maxd = 0;  // levels: the host ones + the deepest subtree's
+            for (const auto &dn : deferred) {
+                int depth = 0;
+                for (int c = dn.second - dn.first; c > t->bs; c = (c + 1) / 2) depth++;
+                maxd = std::max(maxd, depth);
+            }
+            t->levels += maxd;
         }
         KD_CHECK(hipMemcpyAsync(box.data(), t->d_box, (size_t)2 * dd * 4, hipMemcpyDeviceToHost, stream));
         KD_CHECK(hipStreamSynchronize(stream));

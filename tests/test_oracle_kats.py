@@ -274,3 +274,14 @@ def test_fast_colour_division_is_exact(tmp_path):
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), src, "-lm"], check=True)
     tot, bad = map(int, subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split())
     assert tot == 1 << 24 and bad == 0
+
+
+def test_div255_identity():
+    """psyv_dev.hpp div255: fma(fma(-q0, 255, r), RN(1/255), q0) with q0 = RN(r * RN(1/255)) equals the IEEE
+    division r / 255.0 for every byte (the gamma = -1 LUT row), emulated exactly with rationals."""
+    from fractions import Fraction as F
+    inv = 1.0 / 255.0
+    for r in range(256):
+        q0 = float(F(r) * F(inv))
+        res = float(F(r) - F(q0) * 255)
+        assert float(F(res) * F(inv) + F(q0)) == r / 255.0, r

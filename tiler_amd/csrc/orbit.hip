@@ -1368,7 +1368,9 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
 #pragma unroll
             for (int e = 0; e < 4; e++) {
                 const int r = cc[e] & 0xff, g = (cc[e] >> 8) & 0xff, b = (cc[e] >> 16) & 0xff;
-                const double fr = lut[r], fg = lut[g], fb = lut[b];
+                // gamma -1: r / 255.0 in registers (no LDS gather: bank conflicts on random bytes); else the LUT
+                const double fr = FASTDIV ? div255(r) : lut[r], fg = FASTDIV ? div255(g) : lut[g],
+                             fb = FASTDIV ? div255(b) : lut[b];
                 const double cy = div10000<FASTDIV>(2126.0 * fr + 7152.0 * fg + 722.0 * fb);
                 p[4 * k4 + e] = c == 0 ? cy : c == 1 ? (fb - cy) * a.u_mul : (fr - cy) * a.v_mul;
             }

@@ -113,6 +113,15 @@ __device__ __forceinline__ void haar_regs(double (&p)[64], double f) {
 // x / 10000.0 for the gamma = -1 colour sums (fr = r / 255.0): q0 = x * RN(1e-4) plus one fma residual
 // correction.  Bit-identical to the IEEE division over every (r, g, b) of the domain (all 2^24 sums checked
 // by oracle/check_fastdiv.c, tests/test_oracle_kats.py); other gamma LUTs keep the true division.
+// r / 255.0 for a byte r (the gamma = -1 row of gGammaCorLut, main.pas:606) without a LUT read: q0 = r * RN(1/255)
+// plus one fma residual correction, bit-identical to the IEEE division for all 256 bytes
+// (tests/test_oracle_kats.py::test_div255_identity).  Lets the FrameTiling query kernel skip its LDS gathers.
+__device__ __forceinline__ double div255(int r) {
+    const double x = (double)r, inv = 1.0 / 255.0;
+    const double q0 = x * inv;
+    return __builtin_fma(__builtin_fma(-q0, 255.0, x), inv, q0);
+}
+
 template <bool FASTDIV>
 __device__ __forceinline__ double div10000(double x) {
     if constexpr (FASTDIV) {

@@ -1335,6 +1335,7 @@ struct FtQueryArgs {
     OrbitStat *qstat;    // [n]
     const float *box;    // [2][192] or null
     float *rootbox;      // [n] when box
+    int xmode;           // timing experiments only (TILER_EXPERIMENTS build, TILER_FTQ_MODE): results invalid
 };
 
 template <bool FASTDIV>
@@ -1375,7 +1376,10 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
                 p[4 * k4 + e] = c == 0 ? cy : c == 1 ? (fb - cy) * a.u_mul : (fr - cy) * a.v_mul;
             }
         }
-        haar_regs(p, a.haar_f);
+#ifdef TILER_EXPERIMENTS
+        if (a.xmode != 1)
+#endif
+            haar_regs(p, a.haar_f);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 64; k++) st[lane * 65 + k] = (float)p[k];
@@ -1406,6 +1410,9 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
             }
         }
         // orbit transform of this component: k-steps s = 3x + c, 16 outputs each (orbit_prep_kernel's math)
+#ifdef TILER_EXPERIMENTS
+        if (a.xmode == 2) continue;
+#endif
 #pragma unroll 1
         for (int x = 0; x < 4; x++) {
             const int s = 3 * x + c;
@@ -1473,6 +1480,13 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
     fa.qstat = o->qstat;
     fa.box = box;
     fa.rootbox = rootbox;
+    fa.xmode = 0;
+#ifdef TILER_EXPERIMENTS
+    {
+        const char *e = getenv("TILER_FTQ_MODE");  // 1: no Haar, 2: no transform (timing only, results invalid)
+        fa.xmode = e ? atoi(e) : 0;
+    }
+#endif
     const dim3 grid((unsigned)((Q + 63) / 64));
     KTimer tm("psyv", stream);
     if (gamma == -1)

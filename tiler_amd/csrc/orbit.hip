@@ -1355,7 +1355,7 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
     const long nqblk = (a.n + 31) / 32;
     const bool has_blk = (i >> 5) < nqblk;
     const int4 *src = reinterpret_cast<const int4 *>(a.rgb + (valid ? i : t0) * 64);
-    double n2 = 0, h2 = 0, e2 = 0;
+    double n2 = 0, h2q[4] = {0, 0, 0, 0}, e2q[4] = {0, 0, 0, 0};
     int bad = 0;
     float rb = 0.0f;
     const float *row = st + lane * 65;
@@ -1409,7 +1409,9 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
                 n2 += orig * orig;
             }
         }
-        // orbit transform of this component: k-steps s = 3x + c, 16 outputs each (orbit_prep_kernel's math)
+        // orbit transform of this component: k-steps s = 3x + c, 16 outputs each (orbit_prep_kernel's math).  The
+        // tables are the same for every component up to the 64c shift (tools/gen_orbit_map.py asserts it), so
+        // with x and j unrolled every term is an LDS read at an immediate offset of the lane's staged row.
 #ifdef TILER_EXPERIMENTS
         if (a.xmode == 2) continue;
 #endif
@@ -1418,33 +1420,49 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
             const int s = 3 * x + c;
             half8 hv[2];
 #pragma unroll
-            for (int j = 0; j < 16; j++) {  // constant j: hv stays in registers (no dynamic vector index)
-                const int k = s * 16 + j;
-                // wave-uniform table entries (scalar loads of orbit_map_gen.hpp's tables), one LDS read per term
-                const int cnt = orbitgen::CNT[k];
+            for (int j = 0; j < 16; j++) {
+                const int k0 = x * 48 + j;  // component 0's entry of this output
+                const int cnt = orbitgen::CNT[k0];
                 double v = 0.0;
 #pragma unroll
                 for (int t = 0; t < 4; t++)
                     if (t < cnt) {  // W = +-1: w * r is exactly +-r, so add or subtract (no multiply)
-                        const double r = (double)row[orbitgen::SRC[k][t] - 64 * c];
-                        v = orbitgen::W[k][t] > 0.0 ? v + r : v - r;
+#ifdef TILER_EXPERIMENTS
+                        const double r = a.xmode == 4 ? (double)(k0 + t) : (double)row[orbitgen::SRC[k0][t]];
+#else
+                        const double r = (double)row[orbitgen::SRC[k0][t]];
+#endif
+                        v = orbitgen::W[k0][t] > 0.0 ? v + r : v - r;
                     }
                 v = valid ? v * ((cnt == 1 ? 1.0 : 0.5) * (double)a.scale) : 0.0;
                 _Float16 vh = (_Float16)(float)v;
                 if (fabs((double)(float)vh) < 6.103515625e-05) vh = (_Float16)0.0f;  // no fp16 subnormal operands
                 hv[j >> 3][j & 7] = vh;
                 const double dh = (double)(float)vh;
-                h2 += dh * dh;
-                e2 += (v - dh) * (v - dh);
+#ifdef TILER_EXPERIMENTS
+                if (a.xmode != 3) {
+#endif
+                h2q[j & 3] += dh * dh;  // four partial sums per norm: bound inputs, any order is rigorous
+                e2q[j & 3] += (v - dh) * (v - dh);
                 if (!isfinite(v) || fabs(v) > 65000.0) bad = 1;
+#ifdef TILER_EXPERIMENTS
+                }
+#endif
+                if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // 4 outputs in flight at most
             }
+#ifdef TILER_EXPERIMENTS
+            if (has_blk && a.xmode != 5) {
+#else
             if (has_blk) {
+#endif
                 half8 *f = a.frag + ((i >> 5) * OS + s) * 64 + (i & 31);
                 f[0] = hv[0];
                 f[32] = hv[1];
             }
+            __builtin_amdgcn_sched_barrier(0);  // one block of 16 outputs at a time (bounded live range)
         }
     }
+    const double h2 = (h2q[0] + h2q[1]) + (h2q[2] + h2q[3]), e2 = (e2q[0] + e2q[1]) + (e2q[2] + e2q[3]);
     if (valid) {
         OrbitStat q;
         q.n2 = n2;
@@ -1483,7 +1501,7 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
     fa.xmode = 0;
 #ifdef TILER_EXPERIMENTS
     {
-        const char *e = getenv("TILER_FTQ_MODE");  // 1: no Haar, 2: no transform (timing only, results invalid)
+        const char *e = getenv("TILER_FTQ_MODE");  // 1 no Haar, 2 no transform, 3 no norms, 4 no row reads, 5 no frag stores (timing only)
         fa.xmode = e ? atoi(e) : 0;
     }
 #endif

@@ -5,7 +5,7 @@
 set -eu
 mkdir -p gpurun_out/ftq
 cp tiler_amd/lib/experiments/libANN.so tiler_amd/lib/libANN.so
-for m in ${MODES:-0 2 3 4 5}; do
+for m in ${MODES:-0 2 3 5}; do
   TILER_FTQ_MODE=$m timeout -k 10 200 python3 -u bench.py --no-cpu --steps 5 --no-keyframes --no-dither --no-smooth \
     --no-globaltiling --no-palettes > gpurun_out/ftq/m$m.json 2> gpurun_out/ftq/m$m.err
   python3 -c "import json; d=json.loads(open('gpurun_out/ftq/m$m.json').read().strip().splitlines()[-1]); print('mode $m', d['kernels']['psyv']['ms_avg'], d['kernels']['nn_orbit']['ms_avg'])"

@@ -1421,19 +1421,18 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
             half8 hv[2];
 #pragma unroll
             for (int j = 0; j < 16; j++) {
-                const int k0 = x * 48 + j;  // component 0's entry of this output
-                const int cnt = orbitgen::CNT[k0];
+                // the output's packed table word (one scalar load per block of 16): sources, signs, count.  All
+                // four terms are read unconditionally and absent ones add +0 (v is never -0: exact), so the 64
+                // LDS reads of a block have no control dependence and issue back to back.
+                const unsigned w = orbitgen::PACK[x * 16 + j];
+                const int cnt = (int)(w >> 28);
                 double v = 0.0;
 #pragma unroll
-                for (int t = 0; t < 4; t++)
-                    if (t < cnt) {  // W = +-1: w * r is exactly +-r, so add or subtract (no multiply)
-#ifdef TILER_EXPERIMENTS
-                        const double r = a.xmode == 4 ? (double)(k0 + t) : (double)row[orbitgen::SRC[k0][t]];
-#else
-                        const double r = (double)row[orbitgen::SRC[k0][t]];
-#endif
-                        v = orbitgen::W[k0][t] > 0.0 ? v + r : v - r;
-                    }
+                for (int t = 0; t < 4; t++) {
+                    const double r = (double)row[(w >> (6 * t)) & 63];
+                    const double sr = ((w >> (24 + t)) & 1) ? -r : r;
+                    v = v + (t < cnt ? sr : 0.0);
+                }
                 v = valid ? v * ((cnt == 1 ? 1.0 : 0.5) * (double)a.scale) : 0.0;
                 _Float16 vh = (_Float16)(float)v;
                 if (fabs((double)(float)vh) < 6.103515625e-05) vh = (_Float16)0.0f;  // no fp16 subnormal operands
@@ -1501,7 +1500,7 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
     fa.xmode = 0;
 #ifdef TILER_EXPERIMENTS
     {
-        const char *e = getenv("TILER_FTQ_MODE");  // 1 no Haar, 2 no transform, 3 no norms, 4 no row reads, 5 no frag stores (timing only)
+        const char *e = getenv("TILER_FTQ_MODE");  // 1 no Haar, 2 no transform, 3 no norms, 5 no frag stores (timing only)
         fa.xmode = e ? atoi(e) : 0;
     }
 #endif

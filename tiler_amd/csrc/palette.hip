@@ -135,8 +135,28 @@ __device__ void dl3_block_min(float &e, int &j, float *sh_e, int *sh_j) {
     for (int k = 1; k < DL3_W; k++) dl3_min(e, j, sh_e[k], sh_j[k]);
 }
 
+// Chunk minima of the error column, so each merge's "first entry of minimum error" scans one value per chunk
+// instead of the whole table: every write of err[i] (and every entry moved or removed) marks its chunk, and the
+// marked chunks are recomputed at the end of the merge.  A chunk's value is its first minimum (smallest error,
+// then smallest index), so the minimum over chunks is the reference's first minimum.
+constexpr int DL3_MAXCH = 8192;
+struct Dl3Chunks {
+    float e[DL3_MAXCH];
+    int j[DL3_MAXCH];
+    unsigned bits[DL3_MAXCH / 32];
+    int dirty[DL3_MAXCH];
+    int n, sh;  // dirty count; log2 of the chunk size
+};
+
+__device__ __forceinline__ void dl3_mark(Dl3Chunks *ch, int i) {
+    if (!ch) return;
+    const int c = i >> ch->sh;
+    const unsigned m = 1u << (c & 31);
+    if (!(atomicOr(&ch->bits[c >> 5], m) & m)) ch->dirty[atomicAdd(&ch->n, 1)] = c;
+}
+
 // recount_next(i) over j in (i, tot) (quantizer.c:543-560) by the whole block / one wave
-__device__ void dl3_recount_block(const Dl3Tab &t, int i, int tot, float *sh_e, int *sh_j) {
+__device__ void dl3_recount_block(const Dl3Tab &t, int i, int tot, float *sh_e, int *sh_j, Dl3Chunks *ch = nullptr) {
     const Dl3Entry a = dl3_load(t, i);
     float e = HUGE_VALF;
     int j = INT32_MAX;
@@ -153,10 +173,11 @@ __device__ void dl3_recount_block(const Dl3Tab &t, int i, int tot, float *sh_e, 
     if (threadIdx.x == 0) {
         t.E[i] = e;
         t.C[i] = j == INT32_MAX ? 0 : j;
+        dl3_mark(ch, i);
     }
 }
 
-__device__ void dl3_recount_wave(const Dl3Tab &t, int i, int tot) {
+__device__ void dl3_recount_wave(const Dl3Tab &t, int i, int tot, Dl3Chunks *ch = nullptr) {
     const Dl3Entry a = dl3_load(t, i);
     float e = HUGE_VALF;
     int j = INT32_MAX;
@@ -173,6 +194,7 @@ __device__ void dl3_recount_wave(const Dl3Tab &t, int i, int tot) {
     if ((threadIdx.x & 63) == 0) {
         t.E[i] = e;
         t.C[i] = j == INT32_MAX ? 0 : j;
+        dl3_mark(ch, i);
     }
 }
 
@@ -259,18 +281,20 @@ struct Dl3Args {
 };
 
 // the collected recount list: short lists block-wide per item, long ones one item per wave
-__device__ void dl3_run_list(const Dl3Tab &t, const int *list, int k, int tot, float *sh_e, int *sh_j) {
+__device__ void dl3_run_list(const Dl3Tab &t, const int *list, int k, int tot, float *sh_e, int *sh_j,
+                             Dl3Chunks *ch) {
     if (k <= DL3_BLOCK_LIST) {
-        for (int q = 0; q < k; q++) dl3_recount_block(t, list[q], tot, sh_e, sh_j);
+        for (int q = 0; q < k; q++) dl3_recount_block(t, list[q], tot, sh_e, sh_j, ch);
     } else {
-        for (int q = threadIdx.x >> 6; q < k; q += DL3_W) dl3_recount_wave(t, list[q], tot);
+        for (int q = threadIdx.x >> 6; q < k; q += DL3_W) dl3_recount_wave(t, list[q], tot, ch);
     }
     __syncthreads();
 }
 
 // recount_dist(c) (quantizer.c:562-581)
-__device__ void dl3_recount_dist(const Dl3Tab &t, int *list, int c, int tot, float *sh_e, int *sh_j, int *sh_n) {
-    dl3_recount_block(t, c, tot, sh_e, sh_j);
+__device__ void dl3_recount_dist(const Dl3Tab &t, int *list, int c, int tot, float *sh_e, int *sh_j, int *sh_n,
+                                 Dl3Chunks *ch) {
+    dl3_recount_block(t, c, tot, sh_e, sh_j, ch);
     if (threadIdx.x == 0) *sh_n = 0;
     __syncthreads();
     const Dl3Entry b = dl3_load(t, c);
@@ -284,38 +308,71 @@ __device__ void dl3_recount_dist(const Dl3Tab &t, int *list, int c, int tot, flo
             if (cur < ei) {
                 t.E[i] = cur;
                 t.C[i] = c;
+                dl3_mark(ch, i);
             }
         }
     }
     __syncthreads();
-    dl3_run_list(t, list, *sh_n, tot, sh_e, sh_j);
+    dl3_run_list(t, list, *sh_n, tot, sh_e, sh_j, ch);
+}
+
+// the first minimum of chunk c over entries below tot, by one wave (lane 0 stores it)
+__device__ void dl3_chunk_min(const Dl3Tab &t, Dl3Chunks *ch, int c, int tot) {
+    const int b = c << ch->sh, e = min(tot, b + (1 << ch->sh));
+    float v = HUGE_VALF;
+    int j = INT32_MAX;
+    for (int i = b + (int)(threadIdx.x & 63); i < e; i += 64) {
+        const float x = t.E[i];
+        if (x < v) {
+            v = x;
+            j = i;
+        }
+    }
+    dl3_wave_min(v, j);
+    if ((threadIdx.x & 63) == 0) {
+        ch->e[c] = v;
+        ch->j[c] = j;
+    }
 }
 
 __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
     __shared__ float sh_e[DL3_W];
     __shared__ int sh_j[DL3_W];
     __shared__ int sh_n;
+    __shared__ Dl3Chunks chs;
+    Dl3Chunks *ch = &chs;
     const int p = blockIdx.x;
     const int s = a.seg[p], n = a.seg[p + 1] - s;
+    if (n <= a.quant_to) {  // nothing to merge
+        for (int i = threadIdx.x; i < a.quant_to; i += DL3_T)
+            a.pal[(long)p * a.quant_to + i] = i < n ? (int32_t)a.t.Q[s + i] : 0;
+        return;
+    }
     Dl3Tab t = a.t;
     t.R += s, t.G += s, t.B += s, t.N += s, t.Q += s, t.E += s, t.C += s;
     int *list = a.list + s;
+    int sh = 0;
+    while (((n + (1 << sh) - 1) >> sh) > DL3_MAXCH) sh++;
+    if (threadIdx.x == 0) {
+        ch->n = 0;
+        ch->sh = sh;
+    }
+    for (int w = threadIdx.x; w < DL3_MAXCH / 32; w += DL3_T) ch->bits[w] = 0;
+    __syncthreads();
+    for (int c = threadIdx.x >> 6; c < ((n + (1 << sh) - 1) >> sh); c += DL3_W) dl3_chunk_min(t, ch, c, n);
+    __syncthreads();
     int tot = n, c1 = 0;
     while (tot > a.quant_to) {
-        // the first entry of minimum error (quantizer.c:610-618); none below HUGE_VALF keeps c1
+        // the first entry of minimum error (quantizer.c:610-618) over the chunk minima; none below HUGE_VALF
+        // keeps c1
         float e = HUGE_VALF;
         int j = INT32_MAX;
-        for (int i = threadIdx.x; i < tot; i += DL3_T) {
-            const float v = t.E[i];
-            if (v < e) {
-                e = v;
-                j = i;
-            }
-        }
+        const int nch = (tot + (1 << sh) - 1) >> sh;
+        for (int c = threadIdx.x; c < nch; c += DL3_T) dl3_min(e, j, ch->e[c], ch->j[c]);
         dl3_block_min(e, j, sh_e, sh_j);
         if (j != INT32_MAX) c1 = j;
         const int c2 = t.C[c1];
-        __syncthreads();  // every thread has read C[c1] before it changes
+        __syncthreads();  // every thread has read C[c1] and the chunk minima before they change
         tot--;
         if (threadIdx.x == 0) {  // merge c1 into c2, the last entry into c1 (quantizer.c:619-629)
             const uint32_t r = t.R[c2] + t.R[c1], g = t.G[c2] + t.G[c1], b = t.B[c2] + t.B[c1];
@@ -327,20 +384,55 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
             t.E[tot - 1] = HUGE_VALF;
             t.C[tot - 1] = tot;
             sh_n = 0;
+            dl3_mark(ch, c1);
+            dl3_mark(ch, tot - 1);
+            dl3_mark(ch, tot);  // the removed entry leaves its chunk
         }
         __syncthreads();
-        // entries pointing at the moved one: below c1 re-point, above c1 recount (quantizer.c:631-639)
-        for (int i = threadIdx.x; i < tot; i += DL3_T)
-            if (t.C[i] == tot) {
-                if (i < c1)
+        // One pass for three of the reference's loops, each entry in its own lane (quantizer.c:631-641):
+        //   i > c1 pointing at the moved entry -> recount_next(i);
+        //   i < c1 pointing at the moved entry -> re-point to c1, then recount_dist(c1)'s loop: pointing at c1 ->
+        //   recount_next(i), else the update with calc_err(i, c1);
+        // plus recount_next(c1) itself.  The recounts only write their own entry and read table data no loop
+        // writes, and the updates below c1 read nothing the recounts above c1 write, so this equals the sequence.
+        {
+            const Dl3Entry b1 = dl3_load(t, c1);
+            for (int i = threadIdx.x; i < tot; i += DL3_T) {
+                if (i == c1) continue;
+                int ci = t.C[i];
+                if (i > c1) {
+                    if (ci == tot) list[atomicAdd(&sh_n, 1)] = i;
+                    continue;
+                }
+                if (ci == tot) {
+                    ci = c1;
                     t.C[i] = c1;
-                else if (i > c1)
+                }
+                if (ci == c1) {
                     list[atomicAdd(&sh_n, 1)] = i;
+                } else {
+                    const float ei = t.E[i];
+                    if (dl3_lower_bound(t.Q[i], t.N[i], b1.q, b1.n) > (double)ei) continue;  // no update possible
+                    const float cur = dl3_calc_err(dl3_load(t, i), b1);
+                    if (cur < ei) {
+                        t.E[i] = cur;
+                        t.C[i] = c1;
+                        dl3_mark(ch, i);
+                    }
+                }
             }
+            if (threadIdx.x == 0) list[atomicAdd(&sh_n, 1)] = c1;
+        }
         __syncthreads();
-        dl3_run_list(t, list, sh_n, tot, sh_e, sh_j);
-        dl3_recount_dist(t, list, c1, tot, sh_e, sh_j, &sh_n);
-        if (c2 != tot) dl3_recount_dist(t, list, c2, tot, sh_e, sh_j, &sh_n);
+        dl3_run_list(t, list, sh_n, tot, sh_e, sh_j, ch);
+        if (c2 != tot) dl3_recount_dist(t, list, c2, tot, sh_e, sh_j, &sh_n, ch);
+        // refresh the marked chunks (every mark above is complete: the list runs end in a barrier)
+        const int nd = ch->n;
+        for (int q = threadIdx.x >> 6; q < nd; q += DL3_W) dl3_chunk_min(t, ch, ch->dirty[q], tot);
+        __syncthreads();
+        for (int q = threadIdx.x; q < nd; q += DL3_T) ch->bits[ch->dirty[q] >> 5] = 0;
+        if (threadIdx.x == 0) ch->n = 0;
+        __syncthreads();
     }
     for (int i = threadIdx.x; i < a.quant_to; i += DL3_T)  // set_palette3 + copy_pal (calloc'd beyond tot)
         a.pal[(long)p * a.quant_to + i] = i < tot ? (int32_t)t.Q[i] : 0;

@@ -1,7 +1,6 @@
 #!/usr/bin/env bash
-# One GPU pass for a kernel change (run from the repo root via gpurun): the FrameTiling / palette parity tests,
-# a C3 bench line with the palette-generation secondary, then the fused query kernel's timing modes (these
-# swap in the experiment build, so they run last).
+# One GPU pass for a kernel change (run from the repo root via gpurun): the FrameTiling / palette parity tests
+# and a C3 bench line with the palette-generation secondary.
 set -eu
 TAG=${1:-check2}
 OUT=gpurun_out/$TAG
@@ -11,4 +10,3 @@ timeout -k 10 600 python3 -u -m pytest tests/test_gpu_orbit.py tests/test_gpu_fr
 echo "tests done"
 timeout -k 10 300 python3 bench.py --steps 10 --no-keyframes --no-dither --no-globaltiling > "$OUT/bench_c3.json" 2> "$OUT/bench_c3.err"
 echo "bench done"
-bash profiles/ftq_modes.sh

@@ -285,3 +285,28 @@ def test_div255_identity():
         q0 = float(F(r) * F(inv))
         res = float(F(r) - F(q0) * 255)
         assert float(F(res) * F(inv) + F(q0)) == r / 255.0, r
+
+
+def test_orbit_pack_table_matches_orbit_map():
+    """orbit_map_gen.hpp's PACK words (the fused query kernel's transform table) decode to the orbit map the
+    generator derives from the Haar mirror permutations, for all three components (component independence)."""
+    import os
+    import re
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import gen_orbit_map
+    src, wts, cnt = gen_orbit_map.build_map()
+    txt = open(os.path.join(root, "tiler_amd", "csrc", "orbit_map_gen.hpp")).read()
+    pack = [int(v, 16) for v in re.findall(r"0x([0-9a-f]{8})u", txt.split("PACK[64]")[1])]
+    assert len(pack) == 64
+    for x in range(4):
+        for j in range(16):
+            w = pack[x * 16 + j]
+            n = w >> 28
+            for c in range(3):
+                k = x * 48 + c * 16 + j
+                assert n == cnt[k]
+                for t in range(n):
+                    assert ((w >> (6 * t)) & 63) + 64 * c == src[k][t]
+                    assert (-1 if (w >> (24 + t)) & 1 else 1) == wts[k][t]

@@ -221,3 +221,85 @@ def test_oracle_kmeans_separated_clusters(oracle):
     for c in range(6):
         m = labels == c
         assert np.allclose(cent[c], X[m].mean(0), rtol=0, atol=1e-9)
+
+
+# The GPU's pass-2 order (palette.hip dl3_reduce_kernel): the moved-entry fix-ups, recount_dist(c1)'s loop and
+# every recount of the merge run as ONE pass whose lanes may go in any order, then recount_dist(c2); the minimum
+# error comes from chunk minima (equal to the plain first minimum).  This model runs the lanes of each parallel
+# phase in a random order and must reproduce the sequential restatement exactly.
+def _py_dl3quant_gpu_order(px, quant_to=16, bpc=7, order_seed=0):
+    import random
+    rnd = random.Random(order_seed)
+    M = 0xFFFFFFFF
+    mbpc = (1 << bpc) - 1
+    table = {}
+    for r, g, b in px.tolist():
+        idx = ((b * mbpc) // 255) | (((g * mbpc) // 255) << bpc) | (((r * mbpc) // 255) << (2 * bpc))
+        e = table.setdefault(idx, [0, 0, 0, 0]); e[0]=(e[0]+r)&M; e[1]=(e[1]+g)&M; e[2]=(e[2]+b)&M; e[3]=(e[3]+1)&M
+    T = []
+    def setrgb(e):
+        v = e[3]; v2 = v >> 1
+        e[4:7] = [((e[0]+v2)&M)//v & 255, ((e[1]+v2)&M)//v & 255, ((e[2]+v2)&M)//v & 255]
+    for k in sorted(table):
+        e = table[k] + [0,0,0, F32(0), 0]; setrgb(e); T.append(e)
+    def calc_err(a, b):
+        A, B = T[a], T[b]; P1, P2 = A[3], B[3]; P3 = (P1+P2)&M
+        R3 = ((A[0]+B[0]+(P3>>1))&M)//P3; G3 = ((A[1]+B[1]+(P3>>1))&M)//P3; B3 = ((A[2]+B[2]+(P3>>1))&M)//P3
+        d1 = F32(F32(F32((R3-A[4])**2) + F32((G3-A[5])**2)) + F32((B3-A[6])**2)); d1 = F32(np.sqrt(d1) * F32(P1))
+        d2 = F32(F32(F32((B[4]-R3)**2) + F32((B[5]-G3)**2)) + F32((B[6]-B3)**2)); d2 = F32(np.sqrt(d2) * F32(P2))
+        return F32(d1 + d2)
+    INF = F32(np.inf)
+    tot = len(T)
+    def recount_next(i):
+        err, c2 = INF, 0
+        for j in range(i+1, tot):
+            cur = calc_err(i, j)
+            if cur < err: err, c2 = cur, j
+        T[i][7], T[i][8] = err, c2
+    for i in range(tot-1): recount_next(i)
+    if tot: T[tot-1][7], T[tot-1][8] = INF, tot
+    c1 = 0
+    while tot > quant_to:
+        # argmin via chunk minima == plain first minimum
+        err = INF
+        for i in range(tot):
+            if T[i][7] < err: err, c1 = T[i][7], i
+        c2 = T[c1][8]
+        for k in range(4): T[c2][k] = (T[c2][k] + T[c1][k]) & M
+        setrgb(T[c2]); tot -= 1
+        T[c1] = list(T[tot]); T[tot-1][7], T[tot-1][8] = INF, tot
+        # fused pass B, lanes in random order
+        lst = []
+        idxs = [i for i in range(tot) if i != c1]; rnd.shuffle(idxs)
+        for i in idxs:
+            ci = T[i][8]
+            if i > c1:
+                if ci == tot: lst.append(i)
+                continue
+            if ci == tot: ci = c1; T[i][8] = c1
+            if ci == c1: lst.append(i)
+            else:
+                cur = calc_err(i, c1)
+                if cur < T[i][7]: T[i][7], T[i][8] = cur, c1
+        lst.append(c1); rnd.shuffle(lst)
+        for i in lst: recount_next(i)
+        if c2 != tot:
+            recount_next(c2)
+            l2 = []
+            idxs = list(range(c2)); rnd.shuffle(idxs)
+            for i in idxs:
+                if T[i][8] == c2: l2.append(i)
+                else:
+                    cur = calc_err(i, c2)
+                    if cur < T[i][7]: T[i][7], T[i][8] = cur, c2
+            rnd.shuffle(l2)
+            for i in l2: recount_next(i)
+    return np.array([T[i][4] | (T[i][5] << 8) | (T[i][6] << 16) if i < tot else 0 for i in range(quant_to)], np.int32)
+
+
+
+@pytest.mark.parametrize("seed", range(9))
+def test_dl3_gpu_phase_order_equals_sequential(seed):
+    kind = ["noise", "clustered", "few"][seed % 3]
+    px = _pixels(np.random.default_rng(100 + seed), [150, 300, 60][seed % 3], kind)
+    assert np.array_equal(_py_dl3quant_gpu_order(px, 16, 7, seed), _py_dl3quant(px, 16, 7))

@@ -1705,19 +1705,22 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     const bool use_pipe = pipe && qb == 2 && mode == 0 && nw == ORB_NW;
     const int wgs = (nqblk + nw * qb - 1) / (nw * qb);
     const int max_split = 32 / (2 * ORB_L);  // rescore: one list entry per lane of a half-wave
-    // One 8-wave workgroup fills a CU (2 waves per SIMD), so a launch runs in rounds of n_cu workgroups and takes
-    // ~ ceil(wgs * ns / n_cu) / ns workgroup-times for ns candidate splits: pick the smallest, preferring fewer
-    // splits (each adds list entries to rescore) unless more are >= 2 % faster.  C3: 1,519 workgroups, 1 split
-    // (5.93 -> 6 rounds); C2: 675 workgroups, 3 splits (7.91 -> 8 rounds of 1/3 the work; 2 splits: 6 rounds of 1/2).
+    // One 8-wave workgroup fills a CU (2 waves per SIMD), so a launch runs in rounds of n_cu workgroups of
+    // ceil(gblk / ns) tile blocks each for ns candidate splits: pick the cheapest, preferring fewer splits (each adds
+    // list entries to rescore) unless more are >= 2 % faster.  C3: 1,519 workgroups, 1 split (5.93 -> 6 rounds);
+    // C2: 675 workgroups, 1 split (3 rounds of 512 blocks: 2.22 ms; 3 splits, 8 rounds of 171: 2.36 ms).
     static const int n_cu = [] {
         int dev = 0, cu = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
         return cu > 0 ? cu : 256;
     }();
+    // A workgroup also pays a fixed cost of about ORB_WG_FIXED tile blocks (prologue, list start-up, epilogue: C2
+    // with 3 splits ran 1.72 us per block-round against 1.26 at C3), so a round is priced as its blocks + that.
+    constexpr double ORB_WG_FIXED = 64.0;
     int nsplit = 1;
     double best_t = 1e30;
     for (int ns = 1; ns <= max_split && ns <= o->gblk; ns++) {
-        const double t = std::ceil((double)wgs * ns / n_cu) / ns;
+        const double t = std::ceil((double)wgs * ns / n_cu) * (std::ceil((double)o->gblk / ns) + ORB_WG_FIXED);
         if (t < best_t * 0.98) {
             best_t = t;
             nsplit = ns;

@@ -50,13 +50,21 @@ struct Dl3Expand {  // one pixel 0x00BBGGRR -> its CUBE3 contribution (build_tab
     }
 };
 
-// the colour tables of all pairs, SoA; entry e of pair p at seg[p] + local index
+// the colour tables of all pairs; entry e of pair p at seg[p] + local index.  Two 16-byte records per entry: every
+// scan of pass 2 reads only S (one dwordx4 per entry, several in flight per lane), calc_err also V.
 struct Dl3Tab {
-    uint32_t *R, *G, *B, *N;  // CUBE3 r, g, b, pixel_count (32-bit, wrapping)
-    uint32_t *Q;              // rr | gg << 8 | bb << 16 (setrgb)
-    float *E;                 // err
-    int *C;                   // cc (local index)
+    uint4 *S;  // x = Q (rr | gg << 8 | bb << 16, setrgb), y = N (pixel_count), z = E (err, float bits), w = C (cc)
+    uint4 *V;  // x, y, z = CUBE3 r, g, b (32-bit, wrapping); w unused
 };
+constexpr int DL3_U = 6;  // records loaded per lane before any is used
+
+__device__ __forceinline__ float dl3_e(const uint4 &s) { return __uint_as_float(s.z); }
+
+__device__ __forceinline__ void dl3_set_ec(const Dl3Tab &t, int i, float e, int c) {
+    *reinterpret_cast<uint2 *>(reinterpret_cast<uint32_t *>(t.S + i) + 2) = make_uint2(__float_as_uint(e), (uint32_t)c);
+}
+
+__device__ __forceinline__ void dl3_set_c(const Dl3Tab &t, int i, int c) { reinterpret_cast<uint32_t *>(t.S + i)[3] = c; }
 
 __device__ __forceinline__ uint32_t dl3_setrgb(uint32_t r, uint32_t g, uint32_t b, uint32_t n) {  // quantizer.c:472-478
     const int v = (int)n, v2 = v >> 1;
@@ -74,9 +82,9 @@ struct Dl3Entry {
     uint32_t r, g, b, n, q;
 };
 
-__device__ __forceinline__ Dl3Entry dl3_load(const Dl3Tab &t, int i) {
-    return Dl3Entry{t.R[i], t.G[i], t.B[i], t.N[i], t.Q[i]};
-}
+__device__ __forceinline__ Dl3Entry dl3_entry(const uint4 &s, const uint4 &v) { return Dl3Entry{v.x, v.y, v.z, s.y, s.x}; }
+
+__device__ __forceinline__ Dl3Entry dl3_load(const Dl3Tab &t, int i) { return dl3_entry(t.S[i], t.V[i]); }
 
 __device__ __forceinline__ float dl3_calc_err(const Dl3Entry &a, const Dl3Entry &b) {  // quantizer.c:512-541
     const uint32_t P1 = a.n, P2 = b.n, P3 = P1 + P2;
@@ -155,24 +163,37 @@ __device__ __forceinline__ void dl3_mark(Dl3Chunks *ch, int i) {
     if (!(atomicOr(&ch->bits[c >> 5], m) & m)) ch->dirty[atomicAdd(&ch->n, 1)] = c;
 }
 
-// recount_next(i) over j in (i, tot) (quantizer.c:543-560) by the whole block / one wave
+// recount_next(i) over j in (i, tot) (quantizer.c:543-560), lanes striding by STRIDE: this lane's first minimum
+// (its j ascend, `<` keeps the earlier of equal errors)
+template <int STRIDE>
+__device__ __forceinline__ void dl3_recount_scan(const Dl3Tab &t, const Dl3Entry &a, int i, int tot, int lane, float &e,
+                                                 int &j) {
+    for (int k0 = i + 1 + lane; k0 < tot; k0 += STRIDE * DL3_U) {
+        uint4 r[DL3_U];
+#pragma unroll
+        for (int u = 0; u < DL3_U; u++) r[u] = t.S[min(k0 + u * STRIDE, tot - 1)];
+#pragma unroll
+        for (int u = 0; u < DL3_U; u++) {
+            const int k = k0 + u * STRIDE;
+            if (k >= tot || dl3_lower_bound(a.q, a.n, r[u].x, r[u].y) > (double)e) continue;  // cannot win or tie
+            const float cur = dl3_calc_err(a, dl3_entry(r[u], t.V[k]));
+            if (cur < e) {
+                e = cur;
+                j = k;
+            }
+        }
+    }
+}
+
+// recount_next(i) by the whole block / one wave
 __device__ void dl3_recount_block(const Dl3Tab &t, int i, int tot, float *sh_e, int *sh_j, Dl3Chunks *ch = nullptr) {
     const Dl3Entry a = dl3_load(t, i);
     float e = HUGE_VALF;
     int j = INT32_MAX;
-    for (int k = i + 1 + (int)threadIdx.x; k < tot; k += DL3_T) {
-        const uint32_t qk = t.Q[k], nk = t.N[k];
-        if (dl3_lower_bound(a.q, a.n, qk, nk) > (double)e) continue;  // cannot win or tie
-        const float cur = dl3_calc_err(a, Dl3Entry{t.R[k], t.G[k], t.B[k], nk, qk});
-        if (cur < e) {
-            e = cur;
-            j = k;
-        }
-    }
+    dl3_recount_scan<DL3_T>(t, a, i, tot, (int)threadIdx.x, e, j);
     dl3_block_min(e, j, sh_e, sh_j);
     if (threadIdx.x == 0) {
-        t.E[i] = e;
-        t.C[i] = j == INT32_MAX ? 0 : j;
+        dl3_set_ec(t, i, e, j == INT32_MAX ? 0 : j);
         dl3_mark(ch, i);
     }
 }
@@ -181,19 +202,10 @@ __device__ void dl3_recount_wave(const Dl3Tab &t, int i, int tot, Dl3Chunks *ch 
     const Dl3Entry a = dl3_load(t, i);
     float e = HUGE_VALF;
     int j = INT32_MAX;
-    for (int k = i + 1 + (int)(threadIdx.x & 63); k < tot; k += 64) {
-        const uint32_t qk = t.Q[k], nk = t.N[k];
-        if (dl3_lower_bound(a.q, a.n, qk, nk) > (double)e) continue;  // cannot win or tie
-        const float cur = dl3_calc_err(a, Dl3Entry{t.R[k], t.G[k], t.B[k], nk, qk});
-        if (cur < e) {
-            e = cur;
-            j = k;
-        }
-    }
+    dl3_recount_scan<64>(t, a, i, tot, (int)(threadIdx.x & 63), e, j);
     dl3_wave_min(e, j);
     if ((threadIdx.x & 63) == 0) {
-        t.E[i] = e;
-        t.C[i] = j == INT32_MAX ? 0 : j;
+        dl3_set_ec(t, i, e, j == INT32_MAX ? 0 : j);
         dl3_mark(ch, i);
     }
 }
@@ -240,11 +252,8 @@ __global__ __launch_bounds__(256) void dl3_init_kernel(const Dl3Sum *__restrict_
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e >= seg[P]) return;
     const Dl3Sum s = agg[e];
-    t.R[e] = s.r;
-    t.G[e] = s.g;
-    t.B[e] = s.b;
-    t.N[e] = s.n;
-    t.Q[e] = dl3_setrgb(s.r, s.g, s.b, s.n);
+    t.V[e] = make_uint4(s.r, s.g, s.b, 0u);
+    t.S[e] = make_uint4(dl3_setrgb(s.r, s.g, s.b, s.n), s.n, 0u, 0u);  // E, C: pass 1
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -257,12 +266,9 @@ __global__ __launch_bounds__(256) void dl3_pass1_kernel(const uint32_t *__restri
         const int p = (int)(ukeys[e] >> (3 * bpc));
         const int s = seg[p], n = seg[p + 1] - s, i = e - s;
         Dl3Tab u = t;
-        u.R += s, u.G += s, u.B += s, u.N += s, u.Q += s, u.E += s, u.C += s;
+        u.S += s, u.V += s;
         if (i == n - 1) {  // the last entry (quantizer.c:598-599)
-            if ((threadIdx.x & 63) == 0) {
-                u.E[i] = HUGE_VALF;
-                u.C[i] = n;
-            }
+            if ((threadIdx.x & 63) == 0) dl3_set_ec(u, i, HUGE_VALF, n);
         } else {
             dl3_recount_wave(u, i, n);
         }
@@ -298,17 +304,24 @@ __device__ void dl3_recount_dist(const Dl3Tab &t, int *list, int c, int tot, flo
     if (threadIdx.x == 0) *sh_n = 0;
     __syncthreads();
     const Dl3Entry b = dl3_load(t, c);
-    for (int i = threadIdx.x; i < c; i += DL3_T) {
-        if (t.C[i] == c) {
-            list[atomicAdd(sh_n, 1)] = i;
-        } else {
-            const float ei = t.E[i];
-            if (dl3_lower_bound(t.Q[i], t.N[i], b.q, b.n) > (double)ei) continue;  // no update possible
-            const float cur = dl3_calc_err(dl3_load(t, i), b);
-            if (cur < ei) {
-                t.E[i] = cur;
-                t.C[i] = c;
-                dl3_mark(ch, i);
+    for (int i0 = threadIdx.x; i0 < c; i0 += DL3_T * DL3_U) {
+        uint4 r[DL3_U];
+#pragma unroll
+        for (int u = 0; u < DL3_U; u++) r[u] = t.S[min(i0 + u * DL3_T, c - 1)];
+#pragma unroll
+        for (int u = 0; u < DL3_U; u++) {
+            const int i = i0 + u * DL3_T;
+            if (i >= c) break;
+            if ((int)r[u].w == c) {
+                list[atomicAdd(sh_n, 1)] = i;
+            } else {
+                const float ei = dl3_e(r[u]);
+                if (dl3_lower_bound(r[u].x, r[u].y, b.q, b.n) > (double)ei) continue;  // no update possible
+                const float cur = dl3_calc_err(dl3_entry(r[u], t.V[i]), b);
+                if (cur < ei) {
+                    dl3_set_ec(t, i, cur, c);
+                    dl3_mark(ch, i);
+                }
             }
         }
     }
@@ -321,11 +334,17 @@ __device__ void dl3_chunk_min(const Dl3Tab &t, Dl3Chunks *ch, int c, int tot) {
     const int b = c << ch->sh, e = min(tot, b + (1 << ch->sh));
     float v = HUGE_VALF;
     int j = INT32_MAX;
-    for (int i = b + (int)(threadIdx.x & 63); i < e; i += 64) {
-        const float x = t.E[i];
-        if (x < v) {
-            v = x;
-            j = i;
+    for (int i0 = b + (int)(threadIdx.x & 63); i0 < e; i0 += 64 * DL3_U) {
+        uint4 r[DL3_U];
+#pragma unroll
+        for (int u = 0; u < DL3_U; u++) r[u] = t.S[min(i0 + u * 64, e - 1)];
+#pragma unroll
+        for (int u = 0; u < DL3_U; u++) {
+            const float x = dl3_e(r[u]);
+            if (i0 + u * 64 < e && x < v) {
+                v = x;
+                j = i0 + u * 64;
+            }
         }
     }
     dl3_wave_min(v, j);
@@ -345,11 +364,11 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
     const int s = a.seg[p], n = a.seg[p + 1] - s;
     if (n <= a.quant_to) {  // nothing to merge
         for (int i = threadIdx.x; i < a.quant_to; i += DL3_T)
-            a.pal[(long)p * a.quant_to + i] = i < n ? (int32_t)a.t.Q[s + i] : 0;
+            a.pal[(long)p * a.quant_to + i] = i < n ? (int32_t)a.t.S[s + i].x : 0;
         return;
     }
     Dl3Tab t = a.t;
-    t.R += s, t.G += s, t.B += s, t.N += s, t.Q += s, t.E += s, t.C += s;
+    t.S += s, t.V += s;
     int *list = a.list + s;
     int sh = 0;
     while (((n + (1 << sh) - 1) >> sh) > DL3_MAXCH) sh++;
@@ -371,18 +390,18 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
         for (int c = threadIdx.x; c < nch; c += DL3_T) dl3_min(e, j, ch->e[c], ch->j[c]);
         dl3_block_min(e, j, sh_e, sh_j);
         if (j != INT32_MAX) c1 = j;
-        const int c2 = t.C[c1];
+        const int c2 = (int)t.S[c1].w;
         __syncthreads();  // every thread has read C[c1] and the chunk minima before they change
         tot--;
         if (threadIdx.x == 0) {  // merge c1 into c2, the last entry into c1 (quantizer.c:619-629)
-            const uint32_t r = t.R[c2] + t.R[c1], g = t.G[c2] + t.G[c1], b = t.B[c2] + t.B[c1];
-            const uint32_t nn = t.N[c2] + t.N[c1];
-            t.R[c2] = r, t.G[c2] = g, t.B[c2] = b, t.N[c2] = nn;
-            t.Q[c2] = dl3_setrgb(r, g, b, nn);
-            t.R[c1] = t.R[tot], t.G[c1] = t.G[tot], t.B[c1] = t.B[tot], t.N[c1] = t.N[tot], t.Q[c1] = t.Q[tot];
-            t.E[c1] = t.E[tot], t.C[c1] = t.C[tot];
-            t.E[tot - 1] = HUGE_VALF;
-            t.C[tot - 1] = tot;
+            const uint4 s1 = t.S[c1], v1 = t.V[c1], s2 = t.S[c2], v2 = t.V[c2];
+            const uint32_t r = v2.x + v1.x, g = v2.y + v1.y, b = v2.z + v1.z, nn = s2.y + s1.y;
+            t.V[c2] = make_uint4(r, g, b, 0u);
+            t.S[c2] = make_uint4(dl3_setrgb(r, g, b, nn), nn, s2.z, s2.w);
+            const uint4 sl = t.S[tot], vl = t.V[tot];  // (after the c2 update: c2 may be the last entry)
+            t.V[c1] = vl;
+            t.S[c1] = sl;
+            dl3_set_ec(t, tot - 1, HUGE_VALF, tot);
             sh_n = 0;
             dl3_mark(ch, c1);
             dl3_mark(ch, tot - 1);
@@ -397,27 +416,34 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
         // writes, and the updates below c1 read nothing the recounts above c1 write, so this equals the sequence.
         {
             const Dl3Entry b1 = dl3_load(t, c1);
-            for (int i = threadIdx.x; i < tot; i += DL3_T) {
-                if (i == c1) continue;
-                int ci = t.C[i];
-                if (i > c1) {
-                    if (ci == tot) list[atomicAdd(&sh_n, 1)] = i;
-                    continue;
-                }
-                if (ci == tot) {
-                    ci = c1;
-                    t.C[i] = c1;
-                }
-                if (ci == c1) {
-                    list[atomicAdd(&sh_n, 1)] = i;
-                } else {
-                    const float ei = t.E[i];
-                    if (dl3_lower_bound(t.Q[i], t.N[i], b1.q, b1.n) > (double)ei) continue;  // no update possible
-                    const float cur = dl3_calc_err(dl3_load(t, i), b1);
-                    if (cur < ei) {
-                        t.E[i] = cur;
-                        t.C[i] = c1;
-                        dl3_mark(ch, i);
+            for (int i0 = threadIdx.x; i0 < tot; i0 += DL3_T * DL3_U) {
+                uint4 r[DL3_U];
+#pragma unroll
+                for (int u = 0; u < DL3_U; u++) r[u] = t.S[min(i0 + u * DL3_T, tot - 1)];
+#pragma unroll
+                for (int u = 0; u < DL3_U; u++) {
+                    const int i = i0 + u * DL3_T;
+                    if (i >= tot) break;
+                    if (i == c1) continue;
+                    int ci = (int)r[u].w;
+                    if (i > c1) {
+                        if (ci == tot) list[atomicAdd(&sh_n, 1)] = i;
+                        continue;
+                    }
+                    if (ci == tot) {
+                        ci = c1;
+                        dl3_set_c(t, i, c1);
+                    }
+                    if (ci == c1) {
+                        list[atomicAdd(&sh_n, 1)] = i;
+                    } else {
+                        const float ei = dl3_e(r[u]);
+                        if (dl3_lower_bound(r[u].x, r[u].y, b1.q, b1.n) > (double)ei) continue;  // no update possible
+                        const float cur = dl3_calc_err(dl3_entry(r[u], t.V[i]), b1);
+                        if (cur < ei) {
+                            dl3_set_ec(t, i, cur, c1);
+                            dl3_mark(ch, i);
+                        }
                     }
                 }
             }
@@ -435,7 +461,7 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
         __syncthreads();
     }
     for (int i = threadIdx.x; i < a.quant_to; i += DL3_T)  // set_palette3 + copy_pal (calloc'd beyond tot)
-        a.pal[(long)p * a.quant_to + i] = i < tot ? (int32_t)t.Q[i] : 0;
+        a.pal[(long)p * a.quant_to + i] = i < tot ? (int32_t)t.S[i].x : 0;
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -595,7 +621,7 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     const size_t np = (size_t)std::max(npix, 1);
     const size_t b_keys = 4 * np, b_sum = sizeof(Dl3Sum) * np, b_tmp = std::max(tmp_sort, tmp_red) + 256;
     const size_t bytes = 4 * b_keys /* keys, vals x2 */ + b_keys /* ukeys */ + b_sum + b_tmp + 4 * (P + 2) * 2 +
-                         7 * b_keys /* table + list */ + 4 * (size_t)P * palsize + 4096;
+                         8 * b_keys /* table (the list reuses a sort buffer) */ + 4 * (size_t)P * palsize + 4096;
     char *ws = nullptr;
     TILER_HIP_CHECK(hipMalloc((void **)&ws, bytes));
     char *cur = ws;
@@ -613,13 +639,8 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     int *d_seg = (int *)take(4 * (P + 2));
     int *d_uc = (int *)take(4 * (P + 2));
     Dl3Tab t;
-    t.R = (uint32_t *)take(b_keys);
-    t.G = (uint32_t *)take(b_keys);
-    t.B = (uint32_t *)take(b_keys);
-    t.N = (uint32_t *)take(b_keys);
-    t.Q = (uint32_t *)take(b_keys);
-    t.E = (float *)take(b_keys);
-    t.C = (int *)take(b_keys);
+    t.S = (uint4 *)take(4 * b_keys);
+    t.V = (uint4 *)take(4 * b_keys);
     int *d_list = (int *)k0;  // the sort buffers are free once the table exists
     int32_t *d_pal = (int32_t *)take(4 * (size_t)P * palsize);
     int rc = -1;

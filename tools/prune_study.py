@@ -259,5 +259,60 @@ def bound_study(seed=7, nq=400, T=65536):
               % (np.mean(nsb[k]), 100.0 * ovf[k] / nq))
 
 
+
+def coarse_study(seed=7, T=65536, qblocks=6):
+    """Shortlist list-test pass rates per (wave, 32-tile block) for the C3 workload: how often a wave-uniform
+    test `any lane's bound > its list threshold` fires for (e) the exact per-tile bound d0 + sum |d_x| (the kernel's
+    sub-block maxima), (s) a per-sub-block coarse bound max_t d0 + sum_x max_t |d_x| over the lane's 4 tiles, and
+    (w) a per-lane coarse bound over the lane's 16 tiles of the block.  Lanes = 32 queries x 2 tile halves, lists of
+    L = 4 sub-blocks by exact bound, blocks streamed in index order (nn_orbit_shortlist_pipe_kernel)."""
+    wl = synth.make_workload(seed, 1920, 1080, 1, T, n_palettes=128)
+    used = synth.used_one_palette(wl.tile_pal, 128)
+    rows, *_ = oracle.build_ft_dataset(used, wl.tiles, wl.thm, wl.tvm, wl.palettes)
+    P = projections()
+    Bs = []
+    for x in range(4):
+        w, V = np.linalg.eigh(P[x])
+        Bs.append(V[:, w > 0.5])
+    base = rows[0::4].astype(np.float64)
+    cx = [base @ B for B in Bs]
+    half_n = 0.5 * (base ** 2).sum(1)
+    nb = T // 32
+    r = np.arange(16)
+    rng = np.random.default_rng(5)
+    tot = {k: [] for k in "esw"}
+    for qb in rng.choice(wl.tiles_per_frame // 32, qblocks, replace=False):
+        q = oracle.psyv_batch(32, rgb=wl.frame_rgb[0][qb * 32:(qb + 1) * 32], flags=2)
+        d = [q @ B @ cx[x].T for x, B in enumerate(Bs)]  # [32][T]
+        d[0] = d[0] - half_n[None]
+        ex = d[0] + np.abs(d[1]) + np.abs(d[2]) + np.abs(d[3])
+        lanes = []
+        for h in (0, 1):
+            tix = (np.arange(nb)[:, None] * 32 + ((r & 3) + 8 * (r >> 2) + 4 * h)[None]).reshape(-1)  # [nb*16]
+            g = lambda a: a[:, tix].reshape(32, nb, 4, 4)  # noqa: E731  [q][blk][sub][tile]
+            e4 = g(ex).max(3)
+            s4 = g(d[0]).max(3) + sum(np.abs(g(d[x])).max(3) for x in (1, 2, 3))
+            w1 = g(d[0]).max((2, 3)) + sum(np.abs(g(d[x])).max((2, 3)) for x in (1, 2, 3))
+            lanes.append((e4, s4, w1))
+        e4 = np.concatenate([l[0] for l in lanes])  # [64][nb][4]
+        s4 = np.concatenate([l[1] for l in lanes])
+        w1 = np.concatenate([l[2] for l in lanes])
+        lst = np.full((64, 4), -np.inf)
+        fire = {k: 0 for k in "esw"}
+        for b in range(nb):
+            th = lst.min(1)
+            fire["e"] += bool((e4[:, b].max(1) > th).any())
+            fire["s"] += bool((s4[:, b].max(1) > th).any())
+            fire["w"] += bool((w1[:, b] > th).any())
+            allv = np.concatenate([lst, e4[:, b]], 1)
+            lst = -np.sort(-allv, 1)[:, :4]
+        for k in "esw":
+            tot[k].append(fire[k] / nb)
+        print("qblock %d: fire rate exact %.4f  sub-block coarse %.4f  lane coarse %.4f" %
+              (qb, fire["e"] / nb, fire["s"] / nb, fire["w"] / nb), flush=True)
+    print("mean fire rate: exact %.4f  sub-block coarse %.4f  lane coarse %.4f" %
+          tuple(np.mean(tot[k]) for k in "esw"))
+
+
 if __name__ == "__main__":
-    {"--ivf": ivf_study, "--blocks": block_study, "--bounds": bound_study}.get(sys.argv[-1], main)()
+    {"--ivf": ivf_study, "--blocks": block_study, "--bounds": bound_study, "--coarse": coarse_study}.get(sys.argv[-1], main)()

@@ -167,6 +167,12 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     lib.tiler_timing_enable(0)
+    # digest of the last step's tilemap items and errors: A/B runs of kernel variants compare it (identical outputs)
+    import hashlib
+    hh = hashlib.sha256()
+    for t_ in (out_tile, out_pal, out_hm, out_vm, out_err):
+        hh.update(t_.cpu().numpy().tobytes())
+    out_digest = hh.hexdigest()[:16]
     kernels = {}
     for name in ("psyv", "nn_prep", "nn_orbit", "nn_shortlist", "nn_rescore", "nn_pairs", "nn_collect", "nn_rescore2",
                  "nn_exact", "kd_verify", "kd_replay"):
@@ -429,7 +435,7 @@ def main():
                                    f"frames per GPU per step, {TS} tileset x 4 mirrors = {M} candidates (P_eff=1)",
                        "tiles_per_step_per_gpu": QK, "candidates": M, "descriptor": "PsyV Haar 192-d",
                        "parallelism": f"keyframes sharded, {world} GPU(s)"},
-            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "search_stats": stats,
+            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "search_stats": stats, "out_digest": out_digest,
             "secondary": {"prepare": prep, "smooth": smooth, "keyframes": keyframes, "dither": dither,
                           "palettes": palettes_line, "globaltiling": gtl},
         }

@@ -681,6 +681,12 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
         for (int s = 0; s < OS; s++) bq[q][s] = qfrag[(qa * OS + s) * 64 + lane];
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) before the hidden DMA starts counting
+    if (NW * QB > 8 * 2 / 2 && NW == 4) {  // experiment (one wave per SIMD): the B fragments live in the AGPR file
+#pragma unroll
+        for (int q = 0; q < QB; q++)
+#pragma unroll
+            for (int s = 0; s < OS; s++) asm volatile("" : "+a"(bq[q][s]));
+    }
     float lk[QB][L], th[QB];
     int li[QB][L];
 #pragma unroll
@@ -745,18 +751,30 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
     if (nstage > 0) issue(0, 0);
     dma_drain();
     __syncthreads();
+    if ((MODE == 3 || MODE == 5 || MODE == 7) && w >= NW / 2) __builtin_amdgcn_s_setprio(1);  // experiment: static priority, 2nd half
+    // experiment LOOSE (modes 6, 7): a sub-block's bound is the sum of its four per-block maxima,
+    // max_t d0 + max_t |d1| + max_t |d2| + max_t |d3| >= max_t u_t (still rigorous, looser), kept in SA / SC
+    constexpr bool LOOSE = MODE == 6 || MODE == 7;
     const floatx16 zero = {0};
     floatx16 RA[QB], RB[QB], RC[QB];
+    float SA[QB][4], SC[QB][4];
+    float dm[16];  // MODE 11 only
 #pragma unroll
-    for (int q = 0; q < QB; q++) RA[q] = RB[q] = RC[q] = zero;
+    for (int i = 0; i < 16; i++) dm[i] = (float)(lane + i);
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+        RA[q] = RB[q] = RC[q] = zero;
+#pragma unroll
+        for (int sb = 0; sb < 4; sb++) SA[q][sb] = SC[q][sb] = -INFINITY;
+    }
     int pend = -1;          // the block whose tail is pending (-1: none / not a real block)
     half8 a0, a1;           // A fragments of the next k-step pair
     float4 sd0, sd1, sd2, sd3;  // seeds of the next block
 
     // one block: roles P (x0, seeded), T2 (x2); RB takes x1 and x3.  On entry T2 holds the previous
     // block's bound (minus its |d_3|, which is in RB).
-    auto body = [&](const half8 *A, const float4 *SD, int cb, int blk, floatx16 (&P)[QB], floatx16 (&T2)[QB])
-        __attribute__((always_inline)) {
+    auto body = [&](const half8 *A, const float4 *SD, int cb, int blk, floatx16 (&P)[QB], floatx16 (&T2)[QB],
+                    float (&Sc)[QB][4], float (&Sp)[QB][4]) __attribute__((always_inline)) {
         const floatx16 seed = {sd0.x, sd0.y, sd0.z, sd0.w, sd1.x, sd1.y, sd1.z, sd1.w,
                                sd2.x, sd2.y, sd2.z, sd2.w, sd3.x, sd3.y, sd3.z, sd3.w};
         float pmx[QB];
@@ -796,21 +814,73 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                         if (t >= lo && t < hi) D[t / 16][t % 16] = D[t / 16][t % 16] + fabsf(S[t / 16][t % 16]);
                 };
                 constexpr int N3 = 16 * QB, C1 = (N3 + 2) / 3, C2 = (2 * N3 + 2) / 3;
-                if (MODE == 2) {  // timing experiment: MFMA + loads only (results invalid)
+                // LOOSE: sub-block maxima of one accumulator (|.| when AB), sub-blocks [lo, hi) of the QB * 4
+                auto mx4 = [&](const floatx16 (&S)[QB], int t, bool ab) __attribute__((always_inline)) {
+                    const int q = t / 4, sb = t % 4;
+                    const float a = ab ? fabsf(S[q][4 * sb]) : S[q][4 * sb], b = ab ? fabsf(S[q][4 * sb + 1]) : S[q][4 * sb + 1];
+                    const float c = ab ? fabsf(S[q][4 * sb + 2]) : S[q][4 * sb + 2], d = ab ? fabsf(S[q][4 * sb + 3]) : S[q][4 * sb + 3];
+                    return fmaxf(fmaxf(a, b), fmaxf(c, d));
+                };
+                constexpr int M3 = 4 * QB, D1 = (M3 + 2) / 3, D2 = (2 * M3 + 2) / 3;
+                if (LOOSE) {
+                    if (ss <= 2) {  // previous block: + max |d_3| (RB) -- before step 3's MFMA writes RB
+#pragma unroll
+                        for (int t = 0; t < M3; t++)
+                            if (t >= (ss == 0 ? 0 : ss == 1 ? D1 : D2) && t < (ss == 0 ? D1 : ss == 1 ? D2 : M3))
+                                Sp[t / 4][t % 4] = Sp[t / 4][t % 4] + mx4(RB, t, true);
+                    }
+                    if (ss >= 3 && ss - 3 < QB) {
+                        const int q = ss - 3;
+                        pmx[q] = fmaxf(fmaxf(Sp[q][0], Sp[q][1]), fmaxf(Sp[q][2], Sp[q][3]));
+                        asm volatile("" ::"v"(pmx[q]));
+                    }
+                    if (ss >= 6 && ss <= 8) {  // this block: max d0 (P) + max |d_1| (RB)
+#pragma unroll
+                        for (int t = 0; t < M3; t++)
+                            if (t >= (ss == 6 ? 0 : ss == 7 ? D1 : D2) && t < (ss == 6 ? D1 : ss == 7 ? D2 : M3))
+                                Sc[t / 4][t % 4] = mx4(P, t, false) + mx4(RB, t, true);
+                    }
+                    if (ss >= 10) {  // this block: + max |d_2| (T2)
+#pragma unroll
+                        for (int t = 0; t < M3; t++)
+                            if (t >= (ss == 10 ? 0 : M3 / 2) && t < (ss == 10 ? M3 / 2 : M3))
+                                Sc[t / 4][t % 4] = Sc[t / 4][t % 4] + mx4(T2, t, true);
+                    }
+                } else if (MODE >= 11) {  // timing experiment: every MFMA chain live + (11) as many VALU adds on registers no MFMA touches (12: none)
+                    const int nd = MODE == 12 ? 0 : ss <= 2 ? 11 : ss <= 4 ? 10 : (ss >= 6 && ss <= 8) ? 11 : ss >= 10 ? 16 : 0;
+#pragma unroll
+                    for (int i = 0; i < nd; i++) asm volatile("v_add_f32 %0, %0, |%1|" : "+v"(dm[i & 15]) : "v"(dm[(i + 5) & 15]));
+#pragma unroll
+                    for (int q = 0; q < QB; q++) {  // keep every MFMA chain live (one use of each finished chain)
+                        if (ss == 2) asm volatile("" ::"v"(P[q][0]));
+                        if (ss == 5 || ss == 11) asm volatile("" ::"v"(RB[q][0]));
+                        if (ss == 8) asm volatile("" ::"v"(T2[q][0]));
+                    }
+                } else if (MODE == 2) {  // timing experiment: MFMA + loads only (results invalid)
                 } else if (ss <= 2)  // previous block: + |d_3| (RB) -- before step 3's MFMA writes RB
                     acc_abs(T2, RB, ss == 0 ? 0 : ss == 1 ? C1 : C2, ss == 0 ? C1 : ss == 1 ? C2 : N3);
-                if (MODE != 2 && ss >= 3 && ss - 3 < QB) {  // previous block: its max for the list test, one query block per step
-                    const int q = ss - 3;
-                    float m4[4];
-                    pmx[q] = maxima(T2[q], m4);
-                    // materialise here: otherwise the whole tail sinks into the (rare) insertion branch
-                    // and the previous |d_3| (RB) stays live across this block's x1 MFMAs
-                    asm volatile("" ::"v"(pmx[q]));
+                if (!LOOSE && MODE != 2 && MODE < 11 && (ss == 3 || ss == 4)) {  // previous block: its max for the list test
+#pragma unroll
+                    for (int q = 0; q < QB; q++) {  // query blocks [0, (QB+1)/2) at step 3, the rest at step 4
+                        if ((ss == 3) != (q < (QB + 1) / 2)) continue;
+                        float m4[4];
+                        pmx[q] = maxima(T2[q], m4);
+                        // materialise here: otherwise the whole tail sinks into the (rare) insertion branch
+                        // and the previous |d_3| (RB) stays live across this block's x1 MFMAs
+                        asm volatile("" ::"v"(pmx[q]));
+                    }
                 }
-                if (MODE != 2 && ss >= 6 && ss <= 8)  // this block: + |d_1| (RB, complete after step 5) -- before step 9
+                if (!LOOSE && MODE != 2 && MODE < 11 && ss >= 6 && ss <= 8)  // this block: + |d_1| (RB, complete after step 5) -- before step 9
                     acc_abs(P, RB, ss == 6 ? 0 : ss == 7 ? C1 : C2, ss == 6 ? C1 : ss == 7 ? C2 : N3);
-                if (MODE != 2 && ss >= 10)  // this block: + |d_2| (T2, complete after step 8)
+                if (!LOOSE && MODE != 2 && MODE < 11 && ss >= 10)  // this block: + |d_2| (T2, complete after step 8)
                     acc_abs(P, T2, ss == 10 ? 0 : N3 / 2, ss == 10 ? N3 / 2 : N3);
+                if (MODE == 4 || MODE == 5) {  // experiment: one MFMA, then up to 6 VALU, twice per step
+#pragma unroll
+                    for (int g = 0; g < QB; g++) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+                    }
+                }
                 // program order is the schedule: nothing moves across a step (keeps each accumulator's
                 // live range as written, so the role swap needs no extra registers)
                 __builtin_amdgcn_sched_barrier(0);
@@ -819,13 +889,18 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                 a0 = n0;
                 a1 = n1;
             }
-            if (s == 4 && MODE == 0) {
+            if (s == 4 && MODE != 1 && MODE != 2 && MODE < 11) {
                 // the previous block's list update (wave-uniform branch), then the back half
 #pragma unroll
                 for (int q = 0; q < QB; q++)
                     if (__builtin_expect(pend >= 0 && __any(pmx[q] > th[q]), 0)) {
                         float m4[4];
-                        maxima(T2[q], m4);  // T2 still holds the previous block's bound until step 6
+                        if (LOOSE) {
+#pragma unroll
+                            for (int sb = 0; sb < 4; sb++) m4[sb] = Sp[q][sb];
+                        } else {
+                            maxima(T2[q], m4);  // T2 still holds the previous block's bound until step 6
+                        }
                         insert_block(q, m4, pend);
                     }
             }
@@ -847,8 +922,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
         if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
 #pragma unroll
         for (int cb = 0; cb < CB; cb += 2) {
-            body(A, SD, cb, b_begin + st * CB + cb, RA, RC);
-            body(A, SD, cb + 1, b_begin + st * CB + cb + 1, RC, RA);
+            body(A, SD, cb, b_begin + st * CB + cb, RA, RC, SA, SC);
+            body(A, SD, cb + 1, b_begin + st * CB + cb + 1, RC, RA, SC, SA);
         }
         dma_drain();
         __syncthreads();
@@ -857,10 +932,18 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
     if (pend >= 0) {
 #pragma unroll
         for (int q = 0; q < QB; q++) {
+            float m4[4], mx;
+            if (LOOSE) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) RC[q][r] = RC[q][r] + fabsf(RB[q][r]);
-            float m4[4];
-            const float mx = maxima(RC[q], m4);
+                for (int sb = 0; sb < 4; sb++)
+                    m4[sb] = SC[q][sb] + fmaxf(fmaxf(fabsf(RB[q][4 * sb]), fabsf(RB[q][4 * sb + 1])),
+                                               fmaxf(fabsf(RB[q][4 * sb + 2]), fabsf(RB[q][4 * sb + 3])));
+                mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; r++) RC[q][r] = RC[q][r] + fabsf(RB[q][r]);
+                mx = maxima(RC[q], m4);
+            }
             if (__any(mx > th[q])) insert_block(q, m4, pend);
         }
     }
@@ -876,6 +959,9 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
             }
         }
     }
+    if (MODE >= 11)  // timing modes: the dummy adds stay live; the lists stay empty (as MODE 2)
+#pragma unroll
+        for (int i = 0; i < 16; i++) asm volatile("" ::"v"(dm[i]));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1703,7 +1789,8 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     constexpr int qb = 2, nw = ORB_NW, mode = 0, pipe = 1, pmode = 0;
 #endif
     const bool use_pipe = pipe && qb == 2 && mode == 0 && nw == ORB_NW;
-    const int wgs = (nqblk + nw * qb - 1) / (nw * qb);
+    const int qpw = pmode == 8 ? 16 : pmode == 9 ? 12 : nw * qb;  // query blocks per workgroup
+    const int wgs = (nqblk + qpw - 1) / qpw;
     const int max_split = 32 / (2 * ORB_L);  // rescore: one list entry per lane of a half-wave
     // One 8-wave workgroup fills a CU (2 waves per SIMD), so a launch runs in rounds of n_cu workgroups of
     // ceil(gblk / ns) tile blocks each for ns candidate splits: pick the cheapest, preferring fewer splits (each adds
@@ -1761,6 +1848,28 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             ORB_PIPE(1);
         else if (use_pipe && pmode == 2)
             ORB_PIPE(2);
+        else if (use_pipe && pmode == 3)  // 3 setprio 1 for waves NW/2.., 4 MFMA/VALU interleave groups, 5 both (valid)
+            ORB_PIPE(3);
+        else if (use_pipe && pmode == 4)
+            ORB_PIPE(4);
+        else if (use_pipe && pmode == 5)
+            ORB_PIPE(5);
+        else if (use_pipe && pmode == 6)  // 6 looser sub-block bound (sum of per-block maxima), 7 = 6 + setprio
+            ORB_PIPE(6);
+        else if (use_pipe && pmode == 7)
+            ORB_PIPE(7);
+        else if (use_pipe && pmode == 11)  // timing: MFMA + loads + independent VALU adds (results invalid)
+            ORB_PIPE(11);
+        else if (use_pipe && pmode == 12)  // timing: MFMA + loads only, every chain live (results invalid)
+            ORB_PIPE(12);
+        else if (use_pipe && pmode == 8)  // one wave per SIMD: 4 waves x 4 query blocks (9: x 3)
+            hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 4, 0>), dim3(wgs, nsplit), dim3(256), lds,
+                               stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
+                               nsplit, o->key, o->id);
+        else if (use_pipe && pmode == 9)
+            hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 3, 0>), dim3(wgs, nsplit), dim3(256), lds,
+                               stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
+                               nsplit, o->key, o->id);
         else if (use_pipe)
             ORB_PIPE(0);
         else if (qb == 1 && nw == 12)

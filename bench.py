@@ -253,20 +253,32 @@ def main():
     # ---- secondary (not the metric): Smooth over this keyframe's FT tilemap (DoTemporalSmoothing) ----
     smooth = None
     if rank == 0 and not args.no_smooth:
-        s_tile = out_tile.view(F, Q).clone()
-        s_pal = out_pal.view(F, Q).clone()
-        s_hm, s_vm = out_hm.view(F, Q).clone(), out_vm.view(F, Q).clone()
-        s_sm = torch.zeros((F, Q), dtype=torch.uint8, device=dev)
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        check(lib.tiler_smooth_keyframe_dev(F, Q, vp(s_tile.data_ptr()), None, vp(s_pal.data_ptr()),
-                                            vp(s_hm.data_ptr()), vp(s_vm.data_ptr()), vp(s_sm.data_ptr()),
-                                            vp(d_tiles.data_ptr()), vp(d_pals.data_ptr()), 0.02, vp(stream)),
-              "tiler_smooth_keyframe_dev")
-        torch.cuda.synchronize(dev)
-        ts = time.perf_counter() - t0
+        tss = []
+        lib.tiler_timing_reset()
+        for rep_ in range(3):  # the first call also sets up the stream-ordered pool: report the best of 3
+            s_tile = out_tile.view(F, Q).clone()
+            s_pal = out_pal.view(F, Q).clone()
+            s_hm, s_vm = out_hm.view(F, Q).clone(), out_vm.view(F, Q).clone()
+            s_sm = torch.zeros((F, Q), dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize(dev)
+            lib.tiler_timing_enable(1 if rep_ > 0 else 0)
+            t0 = time.perf_counter()
+            check(lib.tiler_smooth_keyframe_dev(F, Q, vp(s_tile.data_ptr()), None, vp(s_pal.data_ptr()),
+                                                vp(s_hm.data_ptr()), vp(s_vm.data_ptr()), vp(s_sm.data_ptr()),
+                                                vp(d_tiles.data_ptr()), vp(d_pals.data_ptr()), 0.02, vp(stream)),
+                  "tiler_smooth_keyframe_dev")
+            torch.cuda.synchronize(dev)
+            tss.append(time.perf_counter() - t0)
+        lib.tiler_timing_enable(0)
+        sm_parts = {}
+        for kn in ("smooth_hash", "smooth_desc", "smooth_chain"):
+            n_ = ctypes.c_int(0)
+            ms_ = lib.tiler_timing_get(kn.encode(), ctypes.byref(n_))
+            sm_parts[kn] = round(ms_ / n_.value, 4) if n_.value else None
+        ts = min(tss)
         steps_s = (F - 1) * Q
         smooth = {"value": round(steps_s / ts / 1e6, 4), "unit": "Msteps/s", "ms": round(ts * 1e3, 3),
+                  "ms_each": [round(x * 1e3, 3) for x in tss], "kernel_ms_avg": sm_parts,
                   "smoothed": int(s_sm.sum().item()), "shape": f"{F} frames x {Q} positions, Strength 0.02",
                   "hbm": {"bytes_per_step": 2 * 16 + 64 + 64,
                           "achieved_gbs": round(steps_s * (2 * 16 + 64 + 64) / ts / 1e9, 2),

@@ -20,7 +20,8 @@ import sys
 
 
 def _short(name: str) -> str:
-    for key in ("orbit_ft_query_kernel", "nn_orbit_pairs_kernel", "kd_verify_kernel", "kd_replay_kernel", "kd_rootbox_kernel",
+    for key in ("orbit_ft_query2_kernel", "orbit_ft_query_kernel", "smooth_chain_coop_kernel", "smooth_hash_insert",
+                "smooth_hash_number", "smooth_hash_lookup", "nn_orbit_pairs_kernel", "kd_verify_kernel", "kd_replay_kernel", "kd_rootbox_kernel",
                 "nn_orbit_shortlist_pipe_kernel", "nn_orbit_shortlist_kernel", "nn_orbit_rescore_kernel", "orbit_prep_kernel", "orbit_eq_kernel", "nn_shortlist16_kernel", "nn_shortlist2_kernel", "nn_shortlist4_kernel", "nn_shortlist_kernel", "nn_collect_kernel",
                 "nn_rescore2_kernel", "nn_rescore_kernel", "nn_exact_kernel", "prep_rows_kernel", "psyv_kernel",
                 "maxabs_kernel", "smooth_kernel"):

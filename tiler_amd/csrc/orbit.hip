@@ -1560,6 +1560,207 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
     }
 }
 
+// The same pass with TWO waves per 64-tile block: wave h holds input rows 4h..4h+3 of every tile (32 fp64 values per
+// lane instead of 64, so the block keeps about half the registers and twice the waves per SIMD hide the loads).
+// WaveletGS splits along rows with no exchange until its last level: level 1's column pairs (0,1) (2,3) | (4,5) (6,7)
+// and level 2's (0,1) | (2,3) each lie in one wave; only level 3's pair of rows 0 and 1 (two values per tile) crosses,
+// through LDS.  Every output element is formed by exactly the operations of haar_regs, so the rows are identical.
+// After the Haar, wave 0 takes the kd root-box distance and wave 1 ||q||^2 (each a sequential sum in dimension
+// order, as before); the orbit transform's 16 outputs per k-step split 8 / 8 (wave h writes fragment half h).
+template <int H>
+__device__ __forceinline__ void haar_half(double (&p)[32], double f, double (*xch)[64][2], int lane) {
+    // slot s of p = local row s (input row 4H + s), 8 columns
+#pragma unroll
+    for (int s = 0; s < 4; s++) {  // level 1 rows (all 8 rows): L at x, H at x + 4
+        double t[8];
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            const double a = p[s * 8 + 2 * x], b = p[s * 8 + 2 * x + 1];
+            t[x] = (a + b) * f;
+            t[x + 4] = (a - b) * f;
+        }
+#pragma unroll
+        for (int x = 0; x < 8; x++) p[s * 8 + x] = t[x];
+    }
+#pragma unroll
+    for (int x = 0; x < 8; x++) {  // level 1 columns: pairs (local 0,1) and (2,3) -> slots 0,1 = L (logical rows
+        double t[4];               // 2H, 2H+1), slots 2,3 = H (logical rows 2H+4, 2H+5)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const double a = p[(2 * j) * 8 + x], b = p[(2 * j + 1) * 8 + x];
+            t[j] = (a + b) * f;
+            t[j + 2] = (a - b) * f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) p[j * 8 + x] = t[j];
+    }
+#pragma unroll
+    for (int s = 0; s < 2; s++) {  // level 2 rows (logical rows 2H, 2H+1 = slots 0, 1), columns 0..3
+        const double a0 = p[s * 8 + 0], b0 = p[s * 8 + 1], a1 = p[s * 8 + 2], b1 = p[s * 8 + 3];
+        p[s * 8 + 0] = (a0 + b0) * f;
+        p[s * 8 + 1] = (a1 + b1) * f;
+        p[s * 8 + 2] = (a0 - b0) * f;
+        p[s * 8 + 3] = (a1 - b1) * f;
+    }
+#pragma unroll
+    for (int x = 0; x < 4; x++) {  // level 2 columns: the pair (2H, 2H+1) -> L = logical row H (slot 0), H = row H+2 (slot 1)
+        const double a = p[x], b = p[8 + x];
+        p[x] = (a + b) * f;
+        p[8 + x] = (a - b) * f;
+    }
+    // level 3 rows: logical row H (slot 0), columns 0..1
+    {
+        const double a = p[0], b = p[1];
+        p[0] = (a + b) * f;
+        p[1] = (a - b) * f;
+    }
+    // level 3 columns: rows 0 (wave 0) and 1 (wave 1) -> L = row 0 (wave 0), H = row 1 (wave 1)
+    xch[H][lane][0] = p[0];
+    xch[H][lane][1] = p[1];
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+        const double o = xch[1 - H][lane][x];
+        p[x] = H == 0 ? (p[x] + o) * f : (o - p[x]) * f;
+    }
+}
+
+// logical index (row * 8 + column) of slot value k of wave H after haar_half
+template <int H>
+__device__ __forceinline__ constexpr int haar_half_pos(int k) {
+    const int s = k >> 3, x = k & 7;
+    const int row = s >= 2 ? 2 * H + 4 + (s - 2) : (x < 4 ? (s == 0 ? H : H + 2) : 2 * H + s);
+    return row * 8 + x;
+}
+
+template <bool FASTDIV, int H>
+__device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut, float *st, float *sbox,
+                                              double (*xch)[64][2], double (*sred)[64]) {
+    const int lane = threadIdx.x & 63;
+    const long t0 = (long)blockIdx.x * 64;
+    const long i = t0 + lane;
+    const bool valid = i < a.n;
+    const long nqblk = (a.n + 31) / 32;
+    const bool has_blk = (i >> 5) < nqblk;
+    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + (valid ? i : t0) * 64) + 8 * H;
+    double nb = 0, h2q[4] = {0, 0, 0, 0}, e2q[4] = {0, 0, 0, 0};  // nb: wave 0 -> (root-box, as float), wave 1 -> n2
+    float rb = 0.0f;
+    int bad = 0;
+    const float *row = st + lane * 65;
+#pragma unroll 1
+    for (int c = 0; c < 3; c++) {
+        double p[32];
+#pragma unroll
+        for (int k4 = 0; k4 < 8; k4++) {
+            const int4 v = src[k4];
+            const int cc[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int r = cc[e] & 0xff, g = (cc[e] >> 8) & 0xff, b = (cc[e] >> 16) & 0xff;
+                const double fr = FASTDIV ? div255(r) : lut[r], fg = FASTDIV ? div255(g) : lut[g],
+                             fb = FASTDIV ? div255(b) : lut[b];
+                const double cy = div10000<FASTDIV>(2126.0 * fr + 7152.0 * fg + 722.0 * fb);
+                p[4 * k4 + e] = c == 0 ? cy : c == 1 ? (fb - cy) * a.u_mul : (fr - cy) * a.v_mul;
+            }
+        }
+        haar_half<H>(p, a.haar_f, xch, lane);
+#pragma unroll
+        for (int k = 0; k < 32; k++) st[lane * 65 + haar_half_pos<H>(k)] = (float)p[k];
+        __syncthreads();
+        if (H == 0 && a.box) {
+#pragma unroll 4
+            for (int k = 0; k < 64; k++) {  // annBoxDistance, dimension order
+                const float v = row[k];
+                const float lo = sbox[c * 64 + k], hi = sbox[OD + c * 64 + k];
+                const float t = fmaxf(lo - v, 0.0f) + fmaxf(v - hi, 0.0f);  // lo <= hi: one term at most; + 0 exact
+                rb = rb + t * t;
+            }
+        }
+        if (H == 1 && valid) {
+#pragma unroll 8
+            for (int k = 0; k < 64; k++) {
+                const double orig = (double)row[k] * (double)a.scale;
+                nb += orig * orig;
+            }
+        }
+        // fp32 rows: 16 lanes per tile store its 256-byte component segment, both waves
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int pc = threadIdx.x + 128 * t, tt = pc >> 4, c4 = pc & 15;
+            if (t0 + tt < a.n) {
+                const float *q = st + tt * 65 + c4 * 4;
+                reinterpret_cast<float4 *>(a.out32 + (t0 + tt) * OD + c * 64)[c4] = make_float4(q[0], q[1], q[2], q[3]);
+            }
+        }
+#pragma unroll 1
+        for (int x = 0; x < 4; x++) {
+            const int s = 3 * x + c;
+            half8 hv;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const unsigned w = orbitgen::PACK[x * 16 + 8 * H + j];  // wave-uniform
+                const int cnt = (int)(w >> 28);
+                double v = 0.0;
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const double r = (double)row[(w >> (6 * t)) & 63];
+                    const double sr = ((w >> (24 + t)) & 1) ? -r : r;
+                    v = v + (t < cnt ? sr : 0.0);
+                }
+                v = valid ? v * ((cnt == 1 ? 1.0 : 0.5) * (double)a.scale) : 0.0;
+                _Float16 vh = (_Float16)(float)v;
+                if (fabs((double)(float)vh) < 6.103515625e-05) vh = (_Float16)0.0f;  // no fp16 subnormal operands
+                hv[j] = vh;
+                const double dh = (double)(float)vh;
+                h2q[j & 3] += dh * dh;
+                e2q[j & 3] += (v - dh) * (v - dh);
+                if (!isfinite(v) || fabs(v) > 65000.0) bad = 1;
+                if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+            if (has_blk) a.frag[((i >> 5) * OS + s) * 64 + (i & 31) + 32 * H] = hv;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();  // st and xch are rewritten by the next component
+    }
+    const double h2 = (h2q[0] + h2q[1]) + (h2q[2] + h2q[3]), e2 = (e2q[0] + e2q[1]) + (e2q[2] + e2q[3]);
+    if (H == 1) {
+        sred[0][lane] = h2;
+        sred[1][lane] = e2;
+        sred[2][lane] = nb;
+        sred[3][lane] = bad ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (H == 0 && valid) {
+        const double n2 = sred[2][lane];
+        OrbitStat q;
+        q.n2 = n2;
+        q.hn = sqrt(h2 + sred[0][lane]);
+        q.en = sqrt(e2 + sred[1][lane]);
+        q.flags = (bad || sred[3][lane] != 0.0 || !isfinite(n2)) ? 2 : 0;
+        q.pad = 0;
+        a.qstat[i] = q;
+        if (a.rootbox) a.rootbox[i] = rb;
+    }
+}
+
+template <bool FASTDIV>
+__global__ __launch_bounds__(128) void orbit_ft_query2_kernel(FtQueryArgs a) {
+    __shared__ double lut[256];
+    __shared__ float st[64 * 65];
+    __shared__ float sbox[2 * OD];
+    __shared__ double xch[2][64][2];
+    __shared__ double sred[4][64];
+    const double *__restrict__ glut = a.gamma_lut + 256 * (a.gamma + 1);
+    for (int i = threadIdx.x; i < 256; i += 128) lut[i] = glut[i];
+    if (a.box)
+        for (int i = threadIdx.x; i < 2 * OD; i += 128) sbox[i] = a.box[i];
+    __syncthreads();
+    if (threadIdx.x < 64)
+        ft_query_half<FASTDIV, 0>(a, lut, st, sbox, xch, sred);
+    else
+        ft_query_half<FASTDIV, 1>(a, lut, st, sbox, xch, sred);
+}
+
 int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float *qrows, const float *box,
                      float *rootbox, hipStream_t stream) {
     OrbitIndex *o = ix->orbit;
@@ -1592,10 +1793,20 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
 #endif
     const dim3 grid((unsigned)((Q + 63) / 64));
     KTimer tm("psyv", stream);
+#ifdef TILER_EXPERIMENTS
+    if (getenv("TILER_FTQ_ONEWAVE")) {  // A/B: the one-wave-per-block kernel
+        if (gamma == -1)
+            hipLaunchKernelGGL(orbit_ft_query_kernel<true>, grid, dim3(64), 0, stream, fa);
+        else
+            hipLaunchKernelGGL(orbit_ft_query_kernel<false>, grid, dim3(64), 0, stream, fa);
+        TILER_HIP_CHECK(hipGetLastError());
+        return 0;
+    }
+#endif
     if (gamma == -1)
-        hipLaunchKernelGGL(orbit_ft_query_kernel<true>, grid, dim3(64), 0, stream, fa);
+        hipLaunchKernelGGL(orbit_ft_query2_kernel<true>, grid, dim3(128), 0, stream, fa);
     else
-        hipLaunchKernelGGL(orbit_ft_query_kernel<false>, grid, dim3(64), 0, stream, fa);
+        hipLaunchKernelGGL(orbit_ft_query2_kernel<false>, grid, dim3(128), 0, stream, fa);
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -7,8 +7,8 @@
 //   |cmp| <= Strength -> copy the lower-index item across (4102-4113).
 // A descriptor is a pure function of (tile, palette, H, V), and a keyframe's tilemaps reuse few distinct
 // items, so each distinct item's descriptor is computed ONCE (bit-identical: psyv_kernel, fp64 in source
-// order) into a per-call table, and the chain kernel (one thread per position) only streams two table rows
-// per step through the sequential fp64 sum.  Distinct items are found with a GPU hash in three passes
+// order) into a per-call table, and the chain kernel (8 lanes per position) reads one table row per step
+// (the previous item's row stays in registers) into the sequential fp64 sum.  Distinct items are found with a GPU hash in three passes
 // (insert keys / number the slots / look items up: no spinning on another lane's write).
 #include <math.h>
 
@@ -54,22 +54,48 @@ __global__ __launch_bounds__(256) void smooth_hash_insert(long n, const int32_t 
         const unsigned long long k = sm_key(tile[i], pal[i], hm[i], vm[i]);
         unsigned p = sm_hash(k) & h.mask;
         for (;;) {
-            const unsigned long long prev = atomicCAS(&h.keys[p], SM_EMPTY, k);
-            if (prev == SM_EMPTY || prev == k) break;
+            // most items repeat across the keyframe's frames: a plain read settles a slot that already holds
+            // the key without an L2 atomic (a stale read only falls through to the CAS, which decides)
+            const unsigned long long seen = __builtin_nontemporal_load(&h.keys[p]);
+            if (seen == k) break;
+            if (seen == SM_EMPTY) {
+                const unsigned long long prev = atomicCAS(&h.keys[p], SM_EMPTY, k);
+                if (prev == SM_EMPTY || prev == k) break;
+            }
             p = (p + 1) & h.mask;
         }
     }
 }
 
+// Numbers the occupied slots 0..U-1 (any order).  Each thread counts its grid-stride slots, the block scans the
+// counts in LDS and reserves its range with ONE counter add (a single counter hit once per wave took 0.37 ms at
+// 32k waves), then the threads walk the same slots again handing out base + prefix.
 __global__ __launch_bounds__(256) void smooth_hash_number(SmoothHash h, long cap) {
-    for (long p = (long)blockIdx.x * 256 + threadIdx.x; p < cap; p += (long)gridDim.x * 256) {
+    __shared__ int scan[256];
+    __shared__ int base;
+    const long stride = (long)gridDim.x * 256;
+    const long p0 = (long)blockIdx.x * 256 + threadIdx.x;
+    int cnt = 0;
+    for (long p = p0; p < cap; p += stride) cnt += h.keys[p] != SM_EMPTY;
+    scan[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // inclusive Hillis-Steele scan
+        const int v = threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
+        __syncthreads();
+        scan[threadIdx.x] += v;
+        __syncthreads();
+    }
+    if (threadIdx.x == 255) base = scan[255] ? atomicAdd(h.count, scan[255]) : 0;
+    __syncthreads();
+    int idx = base + scan[threadIdx.x] - cnt;
+    for (long p = p0; p < cap; p += stride) {
         const unsigned long long k = h.keys[p];
         if (k == SM_EMPTY) continue;
-        const int idx = atomicAdd(h.count, 1);
         h.vals[p] = idx;
         h.u_tile[idx] = (int)(k >> 32);
         h.u_pal[idx] = (int)((k >> 2) & 0x3FFFFFFFu);
         h.u_flags[idx] = (uint8_t)(((k & 2) ? PSYV_HMIRROR : 0) | ((k & 1) ? PSYV_VMIRROR : 0));
+        idx++;
     }
 }
 
@@ -92,43 +118,75 @@ struct SmoothArgs {
     double strength;
 };
 
-// sum_{k < 192} (a_k - b_k)^2 in index order, fp64, every op rounded (CompareEuclideanDCTPtr 659-675)
-__device__ __forceinline__ double sq_dist192(const double *__restrict__ a, const double *__restrict__ b) {
-    const double2 *a2 = reinterpret_cast<const double2 *>(a), *b2 = reinterpret_cast<const double2 *>(b);
-    double acc = 0.0;
-#pragma unroll 8
-    for (int k = 0; k < 96; k++) {
-        const double2 x = a2[k], y = b2[k];
-        double t = x.x - y.x;
-        acc += t * t;
-        t = x.y - y.y;
-        acc += t * t;
-    }
-    return acc;
-}
-
-__global__ __launch_bounds__(64) void smooth_chain_kernel(SmoothArgs a) {
+// The chain with SM_G lanes per position (SM_PW positions per one-wave block).  The previous item's descriptor stays
+// in registers across steps (it is always either the old previous or the old current one), so a step reads only the
+// current item's row: each lane loads its 192 / SM_G dimensions, forms the squared differences (each term rounded
+// as in the reference, fp contraction off) into LDS, and the group's first lane adds the 192 terms in index order --
+// the reference's sequential fp64 sum, bit for bit.  Decisions are uniform per group; the first lane writes.
+constexpr int SM_G = 8, SM_PW = 64 / SM_G, SM_D2 = 96 / SM_G;  // double2 per lane
+__global__ __launch_bounds__(64) void smooth_chain_coop_kernel(SmoothArgs a) {
+    __shared__ double2 terms[SM_PW][96];
     const double inv = 1.0 / (64.0 * 3.0);  // cSqrtFactor main.pas:4073
-    for (long s = (long)blockIdx.x * 64 + threadIdx.x; s < a.Q; s += (long)gridDim.x * 64) {
-        int pt = a.tile[s], pp = a.pal[s], ph = a.hm[s], pv = a.vm[s];
-        int ptmp = a.tmpidx ? a.tmpidx[s] : 0;
-        int pdi = a.didx[s];
-        for (int i = 1; i < a.F; i++) {
-            const long c = (long)i * a.Q + s, p = (long)(i - 1) * a.Q + s;
-            const int ct = a.tile[c], cpl = a.pal[c], chm = a.hm[c], cvm = a.vm[c], csm = a.sm[c];
-            const int ctmp = a.tmpidx ? a.tmpidx[c] : 0;
-            const int cdi = a.didx[c];
-            const double acc = sq_dist192(a.desc + (long)cdi * 192, a.desc + (long)pdi * 192);  // cur - prev
-            const double cmp = sqrt(acc * inv);
-            if (fabs(cmp) <= a.strength) {
-                if (ct >= pt) {  // TMI^ := PrevTMI^ ; TMI^.Smoothed := True (prev item and descriptor unchanged)
+    const int lane = threadIdx.x, g = lane % SM_G, pw = lane / SM_G;
+    const long s = (long)blockIdx.x * SM_PW + pw;
+    const bool valid = s < a.Q;
+    const long sq = valid ? s : 0;
+    int pt = a.tile[sq], pp = a.pal[sq], ph = a.hm[sq], pv = a.vm[sq];
+    int ptmp = a.tmpidx ? a.tmpidx[sq] : 0;
+    double2 prev[SM_D2], cur[SM_D2], nxt[SM_D2];
+    auto row = [&](int i) { return reinterpret_cast<const double2 *>(a.desc + (long)a.didx[(long)i * a.Q + sq] * 192) + g * SM_D2; };
+    {
+        const double2 *r = row(0);
+#pragma unroll
+        for (int j = 0; j < SM_D2; j++) prev[j] = r[j];
+        if (a.F > 1) {
+            const double2 *r1 = row(1);
+#pragma unroll
+            for (int j = 0; j < SM_D2; j++) nxt[j] = r1[j];
+        }
+    }
+    for (int i = 1; i < a.F; i++) {  // uniform over the block: every group walks the same frames
+        const long c = (long)i * a.Q + sq, p = (long)(i - 1) * a.Q + sq;
+        const int ct = a.tile[c], cpl = a.pal[c], chm = a.hm[c], cvm = a.vm[c], csm = a.sm[c];
+        const int ctmp = a.tmpidx ? a.tmpidx[c] : 0;
+#pragma unroll
+        for (int j = 0; j < SM_D2; j++) cur[j] = nxt[j];
+        if (i + 1 < a.F) {  // the next frame's row does not depend on this step's decision: in flight across it
+            const double2 *r = row(i + 1);
+#pragma unroll
+            for (int j = 0; j < SM_D2; j++) nxt[j] = r[j];
+        }
+#pragma unroll
+        for (int j = 0; j < SM_D2; j++) {  // cur - prev, squared, every op rounded
+            const double t0 = cur[j].x - prev[j].x, t1 = cur[j].y - prev[j].y;
+            terms[pw][g * SM_D2 + j] = make_double2(t0 * t0, t1 * t1);
+        }
+        __syncthreads();
+        double acc = 0.0;
+        if (g == 0) {
+#pragma unroll 8
+            for (int k = 0; k < 96; k++) {
+                const double2 v = terms[pw][k];
+                acc += v.x;
+                acc += v.y;
+            }
+        }
+        __syncthreads();  // terms are rewritten next step
+        acc = __shfl(acc, lane - g, 64);
+        const double cmp = sqrt(acc * inv);
+        const bool w = valid && g == 0;
+        if (fabs(cmp) <= a.strength) {
+            if (ct >= pt) {  // TMI^ := PrevTMI^ ; TMI^.Smoothed := True (prev item and descriptor unchanged)
+                if (w) {
                     a.tile[c] = pt;
                     a.pal[c] = pp;
                     a.hm[c] = (uint8_t)ph;
                     a.vm[c] = (uint8_t)pv;
                     a.sm[c] = 1;
                     if (a.tmpidx) a.tmpidx[c] = ptmp;
-                } else {  // PrevTMI^ := TMI^ ; TMI^.Smoothed := True
+                }
+            } else {  // PrevTMI^ := TMI^ ; TMI^.Smoothed := True
+                if (w) {
                     a.tile[p] = ct;
                     a.pal[p] = cpl;
                     a.hm[p] = (uint8_t)chm;
@@ -136,12 +194,16 @@ __global__ __launch_bounds__(64) void smooth_chain_kernel(SmoothArgs a) {
                     a.sm[p] = (uint8_t)csm;
                     if (a.tmpidx) a.tmpidx[p] = ctmp;
                     a.sm[c] = 1;
-                    pt = ct, pp = cpl, ph = chm, pv = cvm, ptmp = ctmp, pdi = cdi;
                 }
-            } else {
-                a.sm[c] = 0;
-                pt = ct, pp = cpl, ph = chm, pv = cvm, ptmp = ctmp, pdi = cdi;
+                pt = ct, pp = cpl, ph = chm, pv = cvm, ptmp = ctmp;
+#pragma unroll
+                for (int j = 0; j < SM_D2; j++) prev[j] = cur[j];
             }
+        } else {
+            if (w) a.sm[c] = 0;
+            pt = ct, pp = cpl, ph = chm, pv = cvm, ptmp = ctmp;
+#pragma unroll
+            for (int j = 0; j < SM_D2; j++) prev[j] = cur[j];
         }
     }
 }
@@ -174,10 +236,13 @@ int smooth_keyframe_dev(int F, int Q, int32_t *tile, int32_t *tmpidx, int32_t *p
         if (hipMemsetAsync(h.keys, 0xff, cap * 8, stream) != hipSuccess) break;
         if (hipMemsetAsync(h.count, 0, 4, stream) != hipSuccess) break;
         const unsigned g = (unsigned)std::min<long>(8192, (n + 255) / 256);
-        hipLaunchKernelGGL(smooth_hash_insert, dim3(g), dim3(256), 0, stream, n, tile, pal, hm, vm, h);
-        hipLaunchKernelGGL(smooth_hash_number, dim3((unsigned)std::min<long>(8192, (cap + 255) / 256)), dim3(256), 0,
-                           stream, h, cap);
-        hipLaunchKernelGGL(smooth_hash_lookup, dim3(g), dim3(256), 0, stream, n, tile, pal, hm, vm, h);
+        {
+            KTimer tk("smooth_hash", stream);
+            hipLaunchKernelGGL(smooth_hash_insert, dim3(g), dim3(256), 0, stream, n, tile, pal, hm, vm, h);
+            hipLaunchKernelGGL(smooth_hash_number, dim3((unsigned)std::min<long>(1024, (cap + 255) / 256)), dim3(256),
+                               0, stream, h, cap);
+            hipLaunchKernelGGL(smooth_hash_lookup, dim3(g), dim3(256), 0, stream, n, tile, pal, hm, vm, h);
+        }
         int U = 0;
         if (hipMemcpyAsync(&U, h.count, 4, hipMemcpyDeviceToHost, stream) != hipSuccess) break;
         if (hipStreamSynchronize(stream) != hipSuccess) break;
@@ -193,11 +258,14 @@ int smooth_keyframe_dev(int F, int Q, int32_t *tile, int32_t *tmpidx, int32_t *p
         pa.flags = PSYV_FROM_PAL | PSYV_QWEIGHT;
         pa.gamma = -1;
         pa.out64 = desc;
-        if (launch_psyv(pa, stream)) break;
+        {
+            KTimer tk("smooth_desc", stream);
+            if (launch_psyv(pa, stream)) break;
+        }
         SmoothArgs a{F, Q, tile, tmpidx, pal, hm, vm, sm, h.didx, desc, strength};
-        // one thread per position, one wave per block: the few waves of a keyframe spread over every CU
-        hipLaunchKernelGGL(smooth_chain_kernel, dim3((unsigned)std::max<long>(1, std::min<long>(65536, (Q + 63) / 64))),
-                           dim3(64), 0, stream, a);
+        // SM_G lanes per position, one wave per block
+        KTimer tk("smooth_chain", stream);
+        hipLaunchKernelGGL(smooth_chain_coop_kernel, dim3((unsigned)((Q + SM_PW - 1) / SM_PW)), dim3(64), 0, stream, a);
         if (hipGetLastError() != hipSuccess) break;
         rc = 0;
     } while (0);

@@ -1127,7 +1127,7 @@ static int launch_exact(RescoreArgs ra, int list_n, int grid, hipStream_t stream
     return 0;
 }
 
-static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream);
+static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream, bool orbit);
 static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream,
                        bool orbit_prepared);
 
@@ -1220,10 +1220,6 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
         // mirror-orbit path (orbit.hip); generic query fragments are built for the tier-2 queries only
         TILER_HIP_CHECK(hipMemsetAsync(s.ccnt, 0, (size_t)std::min(nq, TIER2_MAX) * sizeof(int), stream));
         OrbitTail t{};
-        t.gqfrag = s.qfrag;
-        t.gN = ix->maxN;
-        t.gH = ix->maxH;
-        t.gEc = ix->maxE;
         t.fb_list = s.fb_list;
         t.fb_count = s.fb_count;
         t.ex_list = s.ex_list;
@@ -1256,7 +1252,7 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
         ra.cbuf = s.cbuf;
         ra.cap = TIER2_CAP;
         ra.fb_max = TIER2_MAX;
-        return search_tail(ix, ra, nq, stream);
+        return search_tail(ix, ra, nq, stream, true);
     }
     // queries -> fragments (same layout and scale as the dataset)
     const long nqblk = (nq + 31) / 32;
@@ -1307,13 +1303,20 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
         hipLaunchKernelGGL(nn_rescore_kernel, dim3((nq + 3) / 4), dim3(256), 0, stream, ra);
     }
     TILER_HIP_CHECK(hipGetLastError());
-    return search_tail(ix, ra, nq, stream);
+    return search_tail(ix, ra, nq, stream, false);
 }
 
 // tiers 2 and 3 read their device-side counts: fixed grids, no host round trip
-static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream) {
+static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream, bool orbit) {
     SearchScratch &s = ix->scratch;
-    if (dispatch_collect(ix, nq, stream)) return -1;
+    if (orbit) {
+        const int prev = ix->h_fb_count ? std::max(0, ix->h_fb_count[0]) : TIER2_MAX;
+        if (orbit_collect(ix, s.fb_list, s.fb_count, TIER2_MAX, s.thr, s.ccnt, s.cbuf, TIER2_CAP,
+                          std::min(prev, std::min(nq, TIER2_MAX)), stream))
+            return -1;
+    } else if (dispatch_collect(ix, nq, stream)) {
+        return -1;
+    }
     {
         KTimer t_r2("nn_rescore2", stream);
         hipLaunchKernelGGL(nn_rescore2_kernel, dim3((unsigned)std::min(1024, (std::min(nq, TIER2_MAX) + 3) / 4)),

@@ -1191,11 +1191,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
     const double kd = (double)kk + 1e-6 * fabs((double)kk) + 1e-30;  // covers the fp32 rounding of kk
     const double Tr = (st.n2 + kd + Eo) * (1.0 + g) / (1.0 - g) - st.n2 + 1e-12 * (st.n2 + fabs(kd)) + 1e-30;
     const double Tb = Tr + Eo;
-    // 3. overflow: a full lane list whose worst kept entry can still reach the threshold.  The tier-2
-    // threshold (generic key domain) is completed by orbit_fbprep_kernel.
+    // 3. overflow: a full lane list whose worst kept entry can still reach the threshold.  Tier 2
+    // (nn_orbit_collect_kernel) re-scans every orbit against T_b in this same bound-key domain.
     if (half_ballot(last && (double)ek <= Tb)) {
         if (l == 0) {
-            reinterpret_cast<double *>(t.thr_real)[q] = Tr;
+            float tf = (float)Tb;
+            if ((double)tf < Tb) tf = nextafterf(tf, INFINITY);  // an upper bound in fp32
+            t.thr[q] = tf;
             const int pidx = atomicAdd(t.fb_count, 1);
             if (pidx < t.fb_max)
                 t.fb_list[pidx] = (int)q;
@@ -1351,56 +1353,130 @@ __global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a)
     }
 }
 
-// Tier-2 hand-off for the queries the orbit rescore could not settle: their generic fp16 B fragments
-// (the 32-column layout of nn_search.hip's collect pass, at the query's own column), the generic key
-// error bound, and the tier-2 threshold T = T_real + E_generic rounded up to fp32.  One wave per query.
-struct OrbitFbArgs {
-    const float *q;       // [nq][192]
-    const int *fb_list, *fb_count;
-    int fb_max;
-    const double *thr_real;
-    float *thr;
-    half8 *qfrag;         // generic [nqblk][12][64]
-    float scale;
-    double gN, gH, gEc;
-};
-
-__global__ __launch_bounds__(256) void orbit_fbprep_kernel(OrbitFbArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int count = min(*a.fb_count, a.fb_max);
-    for (int j = blockIdx.x * 4 + (threadIdx.x >> 6); j < count; j += gridDim.x * 4) {
-        const long qq = a.fb_list[j];
-        double sh = 0, se = 0;
-        if (lane < 2 * OS) {  // lane = (k-step s, half h)
-            const int s = lane >> 1, h = lane & 1;
-            half8 hv;
+// Tier 2 for the queries the orbit rescore could not settle (a lane list was full with its last key <= T_b): every
+// orbit of the dataset is scored again with the tier-1 contraction -- the same q' fragments (the query's own
+// column of its block), the same seeded d_0 and bound u = d_0 + |d_1| + |d_2| + |d_3| in fp32 -- and where the
+// bound key -2u reaches T_b (rounded up to fp32 by the rescore), the four mirror keys -2 V_m, V_m = sum_x
+// chi_x(m) d_x, are formed by the rescore's own butterfly (orbit_expand4) and every member whose key reaches
+// T_b is appended to the query's tier-2 buffer (duplicate rows included: rescore2 resolves equal distances in
+// ANN's order).  Any candidate that can reach the winner has real key <= T_r and so computed keys <= T_b
+// (DESIGN.md section 4), as in tier 1.  One wave = 32 tier-2 queries (compact), workgroups split the orbit
+// blocks; candidate fragments staged through LDS.  4x fewer MFMAs and bytes than the generic collect.
+static constexpr int OC_CB = 2;  // orbit blocks per LDS stage
+__global__ __launch_bounds__(256, 2) void nn_orbit_collect_kernel(const half8 *__restrict__ cfrag,
+                                                                  const float *__restrict__ cseed, int gblk, long G,
+                                                                  const int *__restrict__ member,
+                                                                  const half8 *__restrict__ qfrag, const int *fb_list,
+                                                                  const int *fb_count, int fb_max,
+                                                                  const float *__restrict__ thr, int blk_per_split,
+                                                                  int *ccnt, int *cbuf, int cap) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * (OC_CB * OS * 1024 + OC_CB * 128)];
+    constexpr int FRAG_BYTES = OC_CB * OS * 1024;
+    constexpr int BUF_BYTES = FRAG_BYTES + OC_CB * 128;
+    constexpr int PER_T = OC_CB * OS * 64 / 256;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int count = min(*fb_count, fb_max);
+    const int b_begin = blockIdx.y * blk_per_split;
+    const int b_end = min(gblk, b_begin + blk_per_split);
+    const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    const floatx16 zero = {0};
+    for (int grp = blockIdx.x; grp * 128 < count; grp += gridDim.x) {
+        const int j = (grp * 4 + w) * 32 + (lane & 31);
+        const int q = j < count ? fb_list[j] : -1;
+        const float t = q >= 0 ? thr[q] : -INFINITY;
+        half8 bq[OS];
 #pragma unroll
-            for (int jj = 0; jj < 8; jj++) {
-                const float vs = a.q[qq * OD + s * 16 + 8 * h + jj] * a.scale;
-                _Float16 vh = (_Float16)vs;
-                if (fabsf((float)vh) < 6.103515625e-05f) vh = (_Float16)0.0f;  // as prep_rows_kernel
-                hv[jj] = vh;
-                const double dv = vs, dh = (double)(float)vh;
-                sh += dh * dh;
-                se += (dv - dh) * (dv - dh);
+        for (int k = 0; k < OS; k++) bq[k] = q >= 0 ? qfrag[((long)(q >> 5) * OS + k) * 64 + (q & 31) + 32 * h] : zero8;
+        const int nstage = (b_end > b_begin) ? (b_end - b_begin + OC_CB - 1) / OC_CB : 0;
+        // candidate fragments + seeds straight to LDS (LDS-DMA, as the shortlist's ring)
+        auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+            const int blk0 = b_begin + st * OC_CB;
+            const int lastv = min(OC_CB, b_end - blk0) * OS * 64 - 1;
+            const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * OS * 64;
+            char *dst = smem + buf * BUF_BYTES + w * 1024;
+#pragma unroll
+            for (int jj = 0; jj < PER_T; jj++) glds16_asm(src + min(w * 64 + lane + jj * 256, lastv), dst + jj * 256 * 16);
+            if (w == 0 && lane < OC_CB * 8)
+                glds16_asm(reinterpret_cast<const uint4 *>(cseed) + (long)blk0 * 8 + min(lane, min(OC_CB, b_end - blk0) * 8 - 1),
+                           smem + buf * BUF_BYTES + FRAG_BYTES);
+        };
+        __syncthreads();  // the previous group's reads of both buffers are done
+        if (nstage > 0) issue(0, 0);
+        dma_drain();
+        __syncthreads();
+        for (int st = 0; st < nstage; st++) {
+            if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
+            const char *B = smem + (st & 1) * BUF_BYTES;
+            for (int cb = 0; cb < OC_CB; cb++) {
+                const int blk = b_begin + st * OC_CB + cb;
+                if (blk >= b_end) break;
+                const float *sd = reinterpret_cast<const float *>(B + FRAG_BYTES) + cb * 32 + h * 16;
+                floatx16 d[4];
+#pragma unroll
+                for (int r = 0; r < 16; r++) d[0][r] = sd[r];
+                d[1] = d[2] = d[3] = zero;
+#pragma unroll
+                for (int k = 0; k < OS; k++) {
+                    const half8 av = reinterpret_cast<const half8 *>(B)[(cb * OS + k) * 64 + lane];
+                    d[k / 3] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[k], d[k / 3], 0, 0, 0);
+                }
+                if (q < 0) continue;
+                unsigned pass = 0;  // element r: the orbit bound reaches T_b
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const float u = d[0][r] + fabsf(d[1][r]) + fabsf(d[2][r]) + fabsf(d[3][r]);
+                    pass |= (-2.0f * u <= t) ? 1u << r : 0u;
+                }
+                if (!pass) continue;
+                while (pass) {  // rare: one reservation per passing orbit
+                    const int r = __builtin_ctz(pass);
+                    pass &= pass - 1;
+                    const long g = (long)blk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (g >= G) continue;
+                    float dx[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // element r of each accumulator (selects, no scratch)
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+#pragma unroll
+                        for (int x = 0; x < 4; x++) dx[x] = i == r ? d[x][i] : dx[x];
+                    const float a0 = dx[0] + dx[1], b0 = dx[0] - dx[1];
+                    const float c0 = dx[2] + dx[3], e0 = dx[2] - dx[3];
+                    const float V[4] = {a0 + c0, b0 + e0, a0 - c0, b0 - e0};
+                    int m[4], take = 0;
+#pragma unroll
+                    for (int x = 0; x < 4; x++) {
+                        m[x] = member[g * 4 + x];
+                        take |= (m[x] >= 0 && -2.0f * V[x] <= t) ? 1 << x : 0;
+                    }
+                    if (!take) continue;
+                    int p = atomicAdd(&ccnt[j], __popc(take));
+#pragma unroll
+                    for (int x = 0; x < 4; x++)
+                        if ((take >> x) & 1) {
+                            if (p < cap) cbuf[(long)j * cap + p] = m[x];
+                            p++;
+                        }
+                }
             }
-            a.qfrag[((qq >> 5) * OS + s) * 64 + (qq & 31) + 32 * h] = hv;
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-            sh += __shfl_xor(sh, o, 64);
-            se += __shfl_xor(se, o, 64);
-        }
-        if (lane == 0) {
-            const double u = 5.9604644775390625e-08, gam = 2.0 * (OD + 1) * u;
-            const double hn = sqrt(sh), en = sqrt(se);
-            const double Eg = 1.05 * (2.0 * u * a.gN * a.gN + gam * (a.gN * a.gN + 2.0 * hn * a.gH) +
-                                      2.0 * (en * a.gN + hn * a.gEc)) + 1e-30;
-            const double T = a.thr_real[qq] + Eg;
-            float tf = (float)T;
-            if ((double)tf < T) tf = nextafterf(tf, INFINITY);  // keep T an upper bound in fp32
-            a.thr[qq] = tf;
+            dma_drain();
+            __syncthreads();
         }
     }
+}
+
+int orbit_collect(NNIndex *ix, const int *fb_list, const int *fb_count, int fb_max, const float *thr, int *ccnt,
+                  int *cbuf, int cap, int prev, hipStream_t stream) {
+    OrbitIndex *o = ix->orbit;
+    // fixed grid (the tier-2 count stays on the device): many short splits so that a few hundred queries
+    // still spread over the chip; query groups of 128 sized from the previous call's count
+    const int nsplit = std::min(o->gblk, 512);
+    const int bps = (o->gblk + nsplit - 1) / nsplit;
+    const int groups = std::max(1, std::min(64, (prev + prev / 4 + 127) / 128 + 1));
+    KTimer tm("nn_collect", stream);
+    hipLaunchKernelGGL(nn_orbit_collect_kernel, dim3(groups, (o->gblk + bps - 1) / bps), dim3(256), 0, stream,
+                       (const half8 *)o->d_frag, o->d_seed, o->gblk, (long)o->G, o->d_member, (const half8 *)o->qfrag,
+                       fb_list, fb_count, fb_max, thr, bps, ccnt, cbuf, cap);
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1834,7 +1910,6 @@ void orbit_destroy(OrbitIndex *o) {
     hipFree(o->d_map);
     hipFree(o->qfrag);
     hipFree(o->qstat);
-    hipFree(o->thr_real);
     hipFree(o->pair_cnt);
     hipFree(o->pair_cand);
     hipFree(o->d_stats);
@@ -1958,10 +2033,8 @@ int orbit_ensure_queries(OrbitIndex *o, int nq) {
     const long nqblk = (nq + 31) / 32;
     hipFree(o->qfrag);
     hipFree(o->qstat);
-    hipFree(o->thr_real);
     hipFree(o->pair_cnt);
     hipFree(o->pair_cand);
-    TILER_HIP_CHECK(hipMalloc((void **)&o->thr_real, (size_t)nq * sizeof(double)));
     TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cnt, (size_t)nq * sizeof(int)));
     TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cand, (size_t)nq * ORB_PSLOTS * sizeof(int)));
     TILER_HIP_CHECK(hipMalloc(&o->qfrag, (size_t)(nqblk + 1) * OS * 1024));
@@ -2138,7 +2211,6 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.Hp = o->Hp;
     ra.Ecp = o->Ecp;
     ra.t = tail;
-    ra.t.thr_real = o->thr_real;
 #ifdef TILER_EXPERIMENTS
     if (getenv("TILER_KD_EXP") && atoi(getenv("TILER_KD_EXP")) == 2) {  // timing: index-order compares (invalid)
         ra.t.ko = nullptr;
@@ -2165,13 +2237,6 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         KTimer tm("nn_pairs", stream);
         const long lanes = (long)nq * ORB_PSLOTS;
         hipLaunchKernelGGL(nn_orbit_pairs_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, ra);
-    }
-    TILER_HIP_CHECK(hipGetLastError());
-    {
-        OrbitFbArgs fa{d_q, tail.fb_list, tail.fb_count, tail.fb_max, o->thr_real, tail.thr, (half8 *)tail.gqfrag,
-                       ix->scale, tail.gN, tail.gH, tail.gEc};
-        KTimer tm("nn_prep", stream);
-        hipLaunchKernelGGL(orbit_fbprep_kernel, dim3(256), dim3(256), 0, stream, fa);
     }
     TILER_HIP_CHECK(hipGetLastError());
     if (want_stats) {

@@ -51,7 +51,6 @@ struct OrbitIndex {
     // per-call scratch
     void *qfrag = nullptr;        // [nqblk][12][64][8] fp16 q' (MFMA B fragments; the rescore re-keys from them)
     OrbitStat *qstat = nullptr;
-    double *thr_real = nullptr;
     int *pair_cnt = nullptr, *pair_cand = nullptr;  // rescore -> pair pass hand-off
     size_t cap_q = 0;
     float *key = nullptr;
@@ -63,11 +62,8 @@ struct OrbitIndex {
 
 // generic tier-2 / tier-3 plumbing the orbit rescore feeds (owned by nn_search.hip)
 struct OrbitTail {
-    void *gqfrag;                 // generic query fragments (tier 2 B operands; filled for tier-2 queries only)
-    double gN, gH, gEc;           // generic dataset bounds: tier-2 threshold in the generic key domain
-    void *thr_real;               // [nq] double: real-key threshold of each tier-2 query (orbit scratch)
     int *fb_list, *fb_count, *ex_list, *ex_count, fb_max;
-    float *thr;
+    float *thr;                   // [nq] tier-2 threshold T_b (bound-key domain, fp32 rounded up), set by the rescore
     int *out_idx;
     float *out_err;
     const int32_t *tr_tile, *tr_pal;
@@ -92,6 +88,10 @@ void orbit_counters(const NNIndex *ix, long long *expansions, long long *rescore
 int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, hipStream_t stream,
                  bool queries_prepared = false);
 int orbit_ensure_queries(OrbitIndex *o, int nq);
+// tier 2 of an orbit search: every orbit re-scored for the fb_list queries (device count, `prev` = the previous
+// call's count sizes the grid); members whose mirror key reaches thr[q] appended to cbuf[j][cap] / ccnt[j]
+int orbit_collect(NNIndex *ix, const int *fb_list, const int *fb_count, int fb_max, const float *thr, int *ccnt,
+                  int *cbuf, int cap, int prev, hipStream_t stream);
 // FrameTiling queries in one kernel: RGB tiles -> Haar descriptors (qrows[Q][192] fp32) + q' fragments + stats
 // (+ rootbox[Q] = annBoxDistance to box[2][192] when box != null)
 int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float *qrows, const float *box,

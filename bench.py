@@ -494,8 +494,17 @@ def cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out
     done, chunk, spent = 0, 8 * threads, 0.0
     mism = dist_mism = 0
     qd_all, ke_all = [], []
-    while spent < args.cpu_seconds and done < q0.shape[0]:
-        sl = slice(done, min(done + chunk, q0.shape[0]))
+    # chunks alternately from the front and the back of the keyframe: the back's queries sit in the last,
+    # possibly candidate-split, workgroups of the shortlist launch (orbit_search's mixed split)
+    front, back, it = 0, q0.shape[0], 0
+    while spent < args.cpu_seconds and front < back:
+        if it % 2 == 0:
+            sl = slice(front, min(front + chunk, back))
+            front = sl.stop
+        else:
+            sl = slice(max(back - chunk, front), back)
+            back = sl.start
+        it += 1
         t0 = time.perf_counter()
         qd = pyoracle.psyv_batch(sl.stop - sl.start, rgb=q0[sl], flags=2).astype(np.float32)
         ki, ke = kd.search_batch(qd, threads=threads)
@@ -505,7 +514,7 @@ def cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out
         mism += int(np.count_nonzero(~same))
         qd_all.append(qd)
         ke_all.append(ki)
-        done = sl.stop
+        done += sl.stop - sl.start
     visited = kd.visited / max(done, 1)
     kd.close()
     # the same sample under the lowest-index rule (exhaustive scan): how often the tie rule decides the item
@@ -514,7 +523,8 @@ def cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out
     li, _ = pyoracle.nn_batch(ods, qd_all, threads=threads)
     tie_decided = int(np.count_nonzero((ot[li] != ot[ki_all]) | (oa[li] != oa[ki_all]) | (op[li] != op[ki_all])))
     return {"value": round(done / spent / 1e6, 6), "unit": "Mtiles/s", "cores": threads, "kind": "port",
-            "sample": f"first {done} query tiles of the keyframe vs the full {ods.shape[0]}-candidate set: fp64 "
+            "sample": f"{done} query tiles of the keyframe (first {front} and last {q0.shape[0] - back}) vs the full "
+                      f"{ods.shape[0]}-candidate set: fp64 "
                       f"descriptor + ANN 1.1.2 kd-tree (ANN_KD_STD, bucket 1, eps 0; oracle/ann_kdtree.c; "
                       f"{visited:.0f} leaves visited per query, tree build {build_s:.1f} s untimed), {threads} threads",
             "parity_queries": done, "parity_mismatches_vs_gpu": mism, "dist_mismatches_vs_gpu": dist_mism,

@@ -2069,8 +2069,10 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         const char *e = getenv("TILER_ORBIT_PMODE");  // 1 no list updates, 2 MFMA + loads only (results invalid)
         return e ? atoi(e) : 0;
     }();
+    static const bool nomix = getenv("TILER_NO_MIX") != nullptr;  // A/B: uniform candidate splits only
 #else
     constexpr int qb = 2, nw = ORB_NW, mode = 0, pipe = 1, pmode = 0;
+    constexpr bool nomix = false;
 #endif
     const bool use_pipe = pipe && qb == 2 && mode == 0 && nw == ORB_NW;
     const int qpw = pmode == 8 ? 16 : pmode == 9 ? 12 : nw * qb;  // query blocks per workgroup
@@ -2095,6 +2097,23 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         if (t < best_t * 0.98) {
             best_t = t;
             nsplit = ns;
+        }
+    }
+    // Mixed: when the last round of whole-candidate workgroups is ragged (C2: 675 workgroups = 2.64 rounds), the
+    // first R * n_cu workgroups scan every block and only the remaining ones split their blocks mix_ns ways
+    // (C2: 3 rounds of 576 -> 2 x 576 + 2 x 235 block-times).  Lists keep the mix_ns stride for every query;
+    // the whole-candidate part's other splits are empty entries.
+    int mix_full = 0;
+    if (use_pipe && pmode == 0 && !nomix) {
+        const int R = wgs / n_cu, rem = wgs - R * n_cu;
+        for (int ns = 2; R >= 1 && rem > 0 && ns <= max_split && ns <= o->gblk; ns++) {
+            const double t = R * (o->gblk + ORB_WG_FIXED) +
+                             std::ceil((double)rem * ns / n_cu) * (std::ceil((double)o->gblk / ns) + ORB_WG_FIXED);
+            if (t < best_t * 0.98) {
+                best_t = t;
+                nsplit = ns;
+                mix_full = R * n_cu;
+            }
         }
     }
     const int bps = (o->gblk + nsplit - 1) / nsplit;
@@ -2154,8 +2173,10 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 3, 0>), dim3(wgs, nsplit), dim3(256), lds,
                                stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
                                nsplit, o->key, o->id);
-        else if (use_pipe)
+        else if (use_pipe && !mix_full)
             ORB_PIPE(0);
+        else if (use_pipe)
+            ;  // mixed: below
         else if (qb == 1 && nw == 12)
             ORB_LAUNCH(12, 1, 0);
         else if (qb == 1)
@@ -2170,8 +2191,24 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
 #else
         (void)use_pipe;
         (void)pmode;
-        ORB_PIPE(0);
+        if (!mix_full) ORB_PIPE(0);
 #endif
+        if (mix_full) {
+            const int qb_off = mix_full * ORB_NW * 2, q_off = qb_off * 32;  // query blocks / queries of part A
+            const size_t per_q = (size_t)nsplit * 2 * ORB_L;
+            const size_t na = (size_t)std::min(nq, q_off) * per_q;
+            TILER_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)o->key, 0x7f800000u, na, stream));  // +inf: empty
+            TILER_HIP_CHECK(hipMemsetAsync(o->id, 0xff, na * sizeof(int), stream));
+            hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, 0>), dim3(mix_full, 1),
+                               dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,
+                               (const half8 *)o->qfrag, nq, o->gblk, nsplit, o->key, o->id);
+            if (nq > q_off)
+                hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, 0>),
+                                   dim3(wgs - mix_full, nsplit), dim3(ORB_NW * 64), lds, stream,
+                                   (const half8 *)o->d_frag, o->d_seed, o->gblk,
+                                   (const half8 *)o->qfrag + (size_t)qb_off * OS * 64, nq - q_off, bps, nsplit,
+                                   o->key + (size_t)q_off * per_q, o->id + (size_t)q_off * per_q);
+        }
 #undef ORB_PIPE
     }
     TILER_HIP_CHECK(hipGetLastError());

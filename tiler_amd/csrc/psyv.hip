@@ -126,6 +126,52 @@ __global__ __launch_bounds__(64) void psyv_rgb_haar_kernel(PsyvArgs a) {
     if (a.rootbox && valid) a.rootbox[i] = rb;
 }
 
+// DCT descriptors of palette tiles (the Smooth step's distinct items, main.pas:3075-3175 via 4097-4098) with ONE
+// LANE per item: the lane's 64 colours (own palette, own mirrors) staged in LDS, one component's 64 fp64 values in
+// registers, and each output o = sum_i cp_i * gDCTLut[o][i] summed in i order exactly as dct_lane does -- the LUT
+// row is the same for every lane, so its operand comes through the scalar cache instead of 64 cross-lane
+// shuffles per output.  Then the Q-weighting and the ratio, as dct_lane.
+__global__ __launch_bounds__(64) void psyv_dct_items_kernel(PsyvArgs a) {
+    __shared__ int32_t cols[64][65];
+    const int lane = threadIdx.x;
+    const long i = (long)blockIdx.x * 64 + lane;
+    const bool valid = i < a.n;
+    const long ii = valid ? i : 0;
+    const int f = a.flags | (a.flags_per ? a.flags_per[ii] : 0);
+    const int m = ((f & PSYV_HMIRROR) ? 7 : 0) ^ ((f & PSYV_VMIRROR) ? 56 : 0);  // source pixel = k ^ m
+    const long t = a.tile_of ? a.tile_of[ii] : ii;
+    const long p = a.pal_of ? a.pal_of[ii] : 0;
+    const uint8_t *px = a.palpix + t * 64;
+    const int32_t *pal = a.palettes + p * 16;
+#pragma unroll 8
+    for (int k = 0; k < 64; k++) cols[lane][k] = pal[px[k ^ m]];
+    const double *__restrict__ glut = a.gamma_lut + 256 * (a.gamma + 1);
+    const bool qw = (f & PSYV_QWEIGHT) != 0;
+#pragma unroll 1
+    for (int c = 0; c < 3; c++) {
+        double cp[64];
+#pragma unroll
+        for (int k = 0; k < 64; k++) {
+            double cy, cu, cv;
+            yuv_of(cols[lane][k], glut, a.u_mul, a.v_mul, cy, cu, cv);
+            cp[k] = c == 0 ? cy : c == 1 ? cu : cv;
+        }
+#pragma unroll 1
+        for (int o = 0; o < 64; o++) {
+            const double *__restrict__ L = a.dct_lut + o * 64;  // uniform: scalar loads
+            double z = 0.0;
+#pragma unroll
+            for (int k = 0; k < 64; k++) z += cp[k] * L[k];
+            if (qw) z *= a.qmul[c * 64 + o];
+            z = z * a.ratio[o];
+            if (valid) {
+                if (a.out64) a.out64[i * 192 + c * 64 + o] = z;
+                if (a.out32) a.out32[i * 192 + c * 64 + o] = (float)z;
+            }
+        }
+    }
+}
+
 int launch_psyv(PsyvArgs args, hipStream_t stream) {
     if (args.n <= 0) return 0;
     const Luts &L = luts();
@@ -152,6 +198,9 @@ int launch_psyv(PsyvArgs args, hipStream_t stream) {
             hipLaunchKernelGGL(psyv_rgb_haar_kernel<true>, grid, dim3(64), 0, stream, args);
         else
             hipLaunchKernelGGL(psyv_rgb_haar_kernel<false>, grid, dim3(64), 0, stream, args);
+    } else if ((args.flags & PSYV_FROM_PAL) && !(args.flags & (PSYV_WAVELETS | PSYV_LAB)) && !args.rgb &&
+               (!args.flags_per || args.flags_per_mirrors_only)) {
+        hipLaunchKernelGGL(psyv_dct_items_kernel, dim3((unsigned)((args.n + 63) / 64)), dim3(64), 0, stream, args);
     } else {
         long blocks = (args.n + 3) / 4;
         if (blocks > 65536) blocks = 65536;

@@ -14,6 +14,7 @@ struct PsyvArgs {
     const int32_t *palettes = nullptr;  // [P][16]
     const int32_t *pal_of = nullptr;    // [n] or null (palette 0)
     const uint8_t *flags_per = nullptr; // [n] or null
+    bool flags_per_mirrors_only = false; // flags_per holds only PSYV_HMIRROR / PSYV_VMIRROR bits (caller's promise)
     int flags = 0;
     int gamma = -1;
     double *out64 = nullptr;            // [n][192]

@@ -255,6 +255,7 @@ int smooth_keyframe_dev(int F, int Q, int32_t *tile, int32_t *tmpidx, int32_t *p
         pa.palettes = palettes;
         pa.pal_of = h.u_pal;
         pa.flags_per = h.u_flags;
+        pa.flags_per_mirrors_only = true;
         pa.flags = PSYV_FROM_PAL | PSYV_QWEIGHT;
         pa.gamma = -1;
         pa.out64 = desc;

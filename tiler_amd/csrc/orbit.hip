@@ -1768,20 +1768,21 @@ __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut,
                 reinterpret_cast<float4 *>(a.out32 + (t0 + tt) * OD + c * 64)[c4] = make_float4(q[0], q[1], q[2], q[3]);
             }
         }
-#pragma unroll 1
-        for (int x = 0; x < 4; x++) {
+#pragma unroll
+        for (int x = 0; x < 4; x++) {  // fully unrolled: every table word is a compile-time constant
             const int s = 3 * x + c;
             half8 hv;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                const unsigned w = orbitgen::PACK[x * 16 + 8 * H + j];  // wave-uniform
+                const unsigned w = orbitgen::PACK[x * 16 + 8 * H + j];
                 const int cnt = (int)(w >> 28);
                 double v = 0.0;
 #pragma unroll
                 for (int t = 0; t < 4; t++) {
-                    const double r = (double)row[(w >> (6 * t)) & 63];
-                    const double sr = ((w >> (24 + t)) & 1) ? -r : r;
-                    v = v + (t < cnt ? sr : 0.0);
+                    if (t < cnt) {  // absent terms would add +0 to a v that is never -0: skipping them is exact
+                        const double r = (double)row[(w >> (6 * t)) & 63];
+                        v = ((w >> (24 + t)) & 1) ? v - r : v + r;
+                    }
                 }
                 v = valid ? v * ((cnt == 1 ? 1.0 : 0.5) * (double)a.scale) : 0.0;
                 _Float16 vh = (_Float16)(float)v;

@@ -139,6 +139,7 @@ def main():
         return t
 
     kdt = prepare()
+    print(f"[bench] prepared {M} candidates", file=sys.stderr, flush=True)
 
     out_tile = torch.empty(QK, dtype=torch.int32, device=dev)
     out_pal = torch.empty(QK, dtype=torch.int32, device=dev)
@@ -166,6 +167,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    print(f"[bench] {args.steps} steps in {elapsed:.3f} s", file=sys.stderr, flush=True)
     lib.tiler_timing_enable(0)
     # digest of the last step's tilemap items and errors: A/B runs of kernel variants compare it (identical outputs)
     import hashlib
@@ -509,6 +511,7 @@ def cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out
         qd = pyoracle.psyv_batch(sl.stop - sl.start, rgb=q0[sl], flags=2).astype(np.float32)
         ki, ke = kd.search_batch(qd, threads=threads)
         spent += time.perf_counter() - t0
+        print(f"[bench] cpu baseline: {done + sl.stop - sl.start} queries, {spent:.1f} s", file=sys.stderr, flush=True)
         dist_mism += int(np.count_nonzero(ke.view(np.uint32) != g[4][sl].view(np.uint32)))
         same = (ot[ki] == g[0][sl]) & (op[ki] == g[1][sl]) & ((oa[ki] & 1) == g[2][sl]) & ((oa[ki] >> 1) == g[3][sl])
         mism += int(np.count_nonzero(~same))

@@ -16,8 +16,8 @@ fi
 timeout -k 10 300 python3 bench.py --steps 10 > "$OUT/bench_c3.json" 2> "$OUT/bench_c3.err"
 echo "bench c3 done"
 if [ "${MORE:-1}" = "1" ]; then
-  timeout -k 10 300 python3 bench.py --config c2 --steps 10 --no-keyframes --no-dither > "$OUT/bench_c2.json" 2> "$OUT/bench_c2.err"
+  timeout -k 10 300 python3 bench.py --config c2 --steps 10 --no-keyframes --no-dither --no-palettes --no-globaltiling > "$OUT/bench_c2.json" 2> "$OUT/bench_c2.err"
   echo "bench c2 done"
-  timeout -k 10 400 python3 bench.py --config c5 --steps 3 --no-keyframes --no-dither --cpu-seconds 20 > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err"
+  timeout -k 10 400 python3 bench.py --config c5 --steps 3 --no-keyframes --no-dither --no-palettes --no-globaltiling --cpu-seconds 20 > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err"
   echo "bench c5 done"
 fi

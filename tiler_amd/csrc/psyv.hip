@@ -172,6 +172,8 @@ __global__ __launch_bounds__(64) void psyv_dct_items_kernel(PsyvArgs a) {
     }
 }
 
+static constexpr long PSYV_LANE_ITEMS_MIN = 32768;  // C3 bench keyframe (~20k items): 0.04 ms wave-per-item vs 0.31
+
 int launch_psyv(PsyvArgs args, hipStream_t stream) {
     if (args.n <= 0) return 0;
     const Luts &L = luts();
@@ -199,7 +201,8 @@ int launch_psyv(PsyvArgs args, hipStream_t stream) {
         else
             hipLaunchKernelGGL(psyv_rgb_haar_kernel<false>, grid, dim3(64), 0, stream, args);
     } else if ((args.flags & PSYV_FROM_PAL) && !(args.flags & (PSYV_WAVELETS | PSYV_LAB)) && !args.rgb &&
-               (!args.flags_per || args.flags_per_mirrors_only)) {
+               (!args.flags_per || args.flags_per_mirrors_only) && args.n >= PSYV_LANE_ITEMS_MIN) {
+        // many items: one lane each (a wave per item below this count: each lane's 12k-add chain would run alone)
         hipLaunchKernelGGL(psyv_dct_items_kernel, dim3((unsigned)((args.n + 63) / 64)), dim3(64), 0, stream, args);
     } else {
         long blocks = (args.n + 3) / 4;

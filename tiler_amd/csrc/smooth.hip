@@ -48,10 +48,24 @@ struct SmoothHash {
     int32_t *didx;             // [n] descriptor row of every item
 };
 
+// A keyframe's tilemaps repeat items heavily (flat regions, static positions), and many lanes inserting the same key
+// at once serialise on one slot's atomics (0.33 ms at C3).  Only the first lane of each distinct key in a wave
+// inserts (pairwise compare over the wave), and a plain read settles keys already present.
 __global__ __launch_bounds__(256) void smooth_hash_insert(long n, const int32_t *tile, const int32_t *pal,
                                                           const uint8_t *hm, const uint8_t *vm, SmoothHash h) {
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-        const unsigned long long k = sm_key(tile[i], pal[i], hm[i], vm[i]);
+    const int lane = threadIdx.x & 63;
+    const long n_up = (n + 63) & ~63L;  // uniform trip count per wave (the shuffles need every lane)
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n_up; i += (long)gridDim.x * 256) {
+        const bool act = i < n;
+        const unsigned long long k = act ? sm_key(tile[i], pal[i], hm[i], vm[i]) : SM_EMPTY;
+        const unsigned klo = (unsigned)k, khi = (unsigned)(k >> 32);
+        bool dup = !act;
+        for (int d = 1; d < 64; d++) {
+            const int src = (lane - d) & 63;
+            const unsigned olo = __shfl(klo, src, 64), ohi = __shfl(khi, src, 64);
+            dup |= lane >= d && olo == klo && ohi == khi;
+        }
+        if (dup) continue;
         unsigned p = sm_hash(k) & h.mask;
         for (;;) {
             // most items repeat across the keyframe's frames: a plain read settles a slot that already holds

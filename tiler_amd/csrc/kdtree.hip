@@ -249,6 +249,7 @@ static float median_split_host(float *key, int *idx, int n, int n_lo) {
 // median_split_host -- so the subtree's permutation, cut dimensions and cut values are ANN's.
 static constexpr int KD_SUB = 1024;
 
+#ifdef TILER_EXPERIMENTS  // round-1 subtree kernel, kept for A/B (TILER_KD_SUB_OLD)
 __global__ __launch_bounds__(256) void kd_subtree_kernel(const float *__restrict__ rows, int dd, int *__restrict__ pidx,
                                                          const KdNodeDev *__restrict__ roots, int bs,
                                                          int *__restrict__ cd_out, float *__restrict__ cv_out) {
@@ -384,6 +385,131 @@ __global__ __launch_bounds__(256) void kd_subtree_kernel(const float *__restrict
         __syncthreads();
     }
     for (int i = tid; i < m_all; i += 256) pidx[S + i] = idx[i];
+}
+
+#endif
+
+// The same subtrees with the nodes of each level spread over the workgroup's 16 waves (round 2): one wave per node --
+// spreads with lanes over dimensions and a wave reduction (annMaxSpread's first maximum), the cut dimension's keys
+// gathered by the lanes, then lane 0's annMedianSplit quickselect on the LDS copy, exactly the operations of
+// kd_subtree_kernel.  Nodes of one level own disjoint ranges of key/idx and distinct output slots, so running them
+// concurrently changes nothing; kd_subtree_kernel walked them one at a time with a block barrier per node.
+static constexpr int KD_SW = 16;
+__global__ __launch_bounds__(64 * KD_SW) void kd_subtree_waves_kernel(const float *__restrict__ rows, int dd,
+                                                                     int *__restrict__ pidx,
+                                                                     const KdNodeDev *__restrict__ roots, int bs,
+                                                                     int *__restrict__ cd_out, float *__restrict__ cv_out) {
+    __shared__ float key[KD_SUB];
+    __shared__ int idx[KD_SUB];
+    __shared__ int2 lvl[2][KD_SUB / 2 + 1];
+    __shared__ int nlvl[2];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const KdNodeDev R = roots[blockIdx.x];
+    const int S = R.s, m_all = R.e - R.s;
+    for (int i = tid; i < m_all; i += 64 * KD_SW) idx[i] = pidx[S + i];
+    if (tid == 0) {
+        lvl[0][0] = make_int2(0, m_all);
+        nlvl[0] = 1;  // the root is processed even when it is a leaf (as kd_subtree_kernel; its cut is never read)
+        nlvl[1] = 0;
+    }
+    __syncthreads();
+    for (int L = 0;; L++) {
+        const int cur = L & 1, nxt = cur ^ 1;
+        const int nn = nlvl[cur];
+        if (nn == 0) break;  // uniform: read after the barrier
+        for (int j = w; j < nn; j += KD_SW) {
+            const int2 nd = lvl[cur][j];
+            const int s = nd.x, e = nd.y;
+            float best = -INFINITY;
+            int bd = 0x7fffffff;
+            for (int d = lane; d < dd; d += 64) {  // this lane's dimensions ascend: strict > keeps the first
+                float mn = INFINITY, mx = -INFINITY;
+#pragma unroll 4
+                for (int i = s; i < e; i++) {
+                    const float v = rows[(long)idx[i] * dd + d];
+                    mn = fminf(mn, v);
+                    mx = fmaxf(mx, v);
+                }
+                const float spr = mx - mn;
+                if (spr > best) {
+                    best = spr;
+                    bd = d;
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                const float ob = __shfl_xor(best, o, 64);
+                const int od = __shfl_xor(bd, o, 64);
+                if (ob > best || (ob == best && od < bd)) {
+                    best = ob;
+                    bd = od;
+                }
+            }
+            const int cd = best > 0.0f ? bd : 0;
+            for (int i = s + lane; i < e; i += 64) key[i] = rows[(long)idx[i] * dd + cd];
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the keys are in LDS before lane 0 reads them
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {  // annMedianSplit on key[s..e) / idx[s..e), as kd_subtree_kernel
+                float *kk = key + s;
+                int *ii = idx + s;
+                const int n = e - s, n_lo = n / 2;
+                auto sw = [&](int a, int b) {
+                    const float tk = kk[a];
+                    kk[a] = kk[b];
+                    kk[b] = tk;
+                    const int ti = ii[a];
+                    ii[a] = ii[b];
+                    ii[b] = ti;
+                };
+                int l = 0, r = n - 1;
+                while (l < r) {
+                    int i = (r + l) / 2, k;
+                    if (kk[i] > kk[r]) sw(i, r);
+                    sw(l, i);
+                    const float c = kk[l];
+                    i = l;
+                    k = r;
+                    for (;;) {
+                        while (kk[++i] < c) {
+                        }
+                        while (kk[--k] > c) {
+                        }
+                        if (i < k)
+                            sw(i, k);
+                        else
+                            break;
+                    }
+                    sw(l, k);
+                    if (k > n_lo)
+                        r = k - 1;
+                    else if (k < n_lo)
+                        l = k + 1;
+                    else
+                        break;
+                }
+                if (n_lo > 0) {
+                    float c = kk[0];
+                    int k = 0;
+                    for (int i = 1; i < n_lo; i++)
+                        if (kk[i] > c) {
+                            c = kk[i];
+                            k = i;
+                        }
+                    sw(n_lo - 1, k);
+                }
+                const int m = s + n_lo;
+                cd_out[S + m] = cd;
+                cv_out[S + m] = (float)(((double)(kk[n_lo > 0 ? n_lo - 1 : 0] + kk[n_lo])) / 2.0);
+                if (e - m > bs) lvl[nxt][atomicAdd(&nlvl[nxt], 1)] = make_int2(m, e);
+                if (m - s > bs) lvl[nxt][atomicAdd(&nlvl[nxt], 1)] = make_int2(s, m);
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        if (tid == 0) nlvl[cur] = 0;
+        __syncthreads();
+    }
+    for (int i = tid; i < m_all; i += 64 * KD_SW) pidx[S + i] = idx[i];
 }
 
 KdOrder KdTree::view() const {
@@ -655,7 +781,13 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
             const int nd = (int)deferred.size();
             for (int i = 0; i < nd; i++) h_nodes[i] = KdNodeDev{deferred[i].first, deferred[i].second};
             KD_CHECK(hipMemcpyAsync(d_nodes, h_nodes, (size_t)nd * sizeof(KdNodeDev), hipMemcpyHostToDevice, stream));
-            hipLaunchKernelGGL(kd_subtree_kernel, dim3(nd), dim3(256), 0, stream, d_rows, dd, t->d_pidx,
+#ifdef TILER_EXPERIMENTS
+            if (getenv("TILER_KD_SUB_OLD"))  // A/B: one node at a time per workgroup
+                hipLaunchKernelGGL(kd_subtree_kernel, dim3(nd), dim3(256), 0, stream, d_rows, dd, t->d_pidx,
+                                   (const KdNodeDev *)d_nodes, t->bs, t->d_cd, t->d_cv);
+            else
+#endif
+            hipLaunchKernelGGL(kd_subtree_waves_kernel, dim3(nd), dim3(64 * KD_SW), 0, stream, d_rows, dd, t->d_pidx,
                                (const KdNodeDev *)d_nodes, t->bs, t->d_cd, t->d_cv);
             KD_CHECK(hipGetLastError());
             KD_CHECK(hipMemcpyAsync(h_pidx, t->d_pidx, (size_t)n * 4, hipMemcpyDeviceToHost, stream));

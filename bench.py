@@ -197,7 +197,11 @@ def main():
     sec = sl["ms_avg"] * 1e-3 if sl["ms_avg"] else None
     # the contraction this algorithm performs: the orbit kernel scores a tile's 4 mirrors with ONE 192-deep
     # fp16 contraction (2*G*D flops per query, G = tile orbits); the brute-force form is 2*M*D (M = candidates)
-    issued_launch = 2.0 * (stats["orbit_groups"] if orbit else M) * 192 * QK
+    # the MFMA work actually issued: k-steps of 16 dims x 32 groups per query (12 per block of groups; the blocks of
+    # mirror-symmetric tiles skip their exactly-zero isotypic blocks: orbit_build / stats["orbit_ksteps"])
+    ksteps = stats.get("orbit_ksteps") or 0
+    issued_launch = (2.0 * ksteps * 32 * 16 * QK) if (orbit and ksteps) else \
+        2.0 * (stats["orbit_groups"] if orbit else M) * 192 * QK
     bruteforce_launch = 2.0 * M * 192 * QK
     issued = issued_launch / sec / 1e12 if sec else None
     effective = bruteforce_launch / sec / 1e12 if sec else None
@@ -217,10 +221,13 @@ def main():
                 "effective_speedup": round(bruteforce_launch / issued_launch, 4),
                 "hbm": {"bytes_per_tile": round(ft_bytes_tile, 1), "achieved_gbs": round(hbm_gbs, 2),
                         "peak_gbs": PEAK_HBM_GBS, "hbm_frac": round(hbm_gbs / PEAK_HBM_GBS, 6)},
-                "note": ("achieved/frac = MFMA flops the kernel issues (2*G*D per query, G = mirror orbits) / its "
+                "issued_ksteps_per_query": ksteps,
+                "note": ("achieved/frac = MFMA flops the kernel issues (2*16*32 per k-step x the k-steps per query: "
+                         "12 per block of 32 mirror orbits, fewer on the blocks of mirror-symmetric tiles whose zero "
+                         "isotypic blocks are skipped; = 2*G*D without them) / its "
                          "average launch time (HIP events on the launch stream) vs the dense fp16 peak; "
                          "effective_tflops = the brute-force 2*M*D per query over the same time (effective_speedup = "
-                         "M/G, the exact 4-mirror orbit algebra). hbm = the metric's '% HBM roofline': SURVEY.md 8(d) "
+                         "brute-force / issued flops: the exact 4-mirror orbit algebra and the skipped zero blocks). hbm = the metric's '% HBM roofline': SURVEY.md 8(d) "
                          "bytes per matched tile x tiles / ms_per_step -- small by construction, the search is "
                          "MFMA-bound (SURVEY.md 7, hard part 5)")}
     # HBM-bound helpers: algorithmic bytes per launch / launch time.  "psyv" times the fused FrameTiling query

@@ -70,7 +70,8 @@ typedef struct {
     int32_t splits;           /* candidate splits used by the last launch */
     int64_t orbit_groups;     /* mirror orbits found in the dataset (0: mirror-orbit path unavailable) */
     int32_t orbit_search;     /* 1 when the last search ran the mirror-orbit shortlist */
-    int32_t reserved;
+    int32_t orbit_ksteps;     /* 16-deep MFMA k-steps over 32 groups the orbit shortlist issues per query (12 per
+                                 block; fewer on blocks of mirror-symmetric tiles, whose zero blocks are skipped) */
     int64_t orbit_expansions; /* TILER_ORBIT_STATS=1 only: 4-entry re-key passes of the orbit rescore */
     int64_t orbit_rescored;   /* TILER_ORBIT_STATS=1 only: candidates rescored with the reference distance */
     int32_t tie_order;        /* 0: ANN kd-tree first-found (ANN_KD_STD), 1: lowest index */

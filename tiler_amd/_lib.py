@@ -31,7 +31,7 @@ class TilerError(RuntimeError):
 class SearchStats(ctypes.Structure):
     _fields_ = [("queries", ctypes.c_int64), ("fallback_queries", ctypes.c_int64),
                 ("exhaustive_queries", ctypes.c_int64), ("exact_integer", ctypes.c_int32), ("splits", ctypes.c_int32),
-                ("orbit_groups", ctypes.c_int64), ("orbit_search", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("orbit_groups", ctypes.c_int64), ("orbit_search", ctypes.c_int32), ("orbit_ksteps", ctypes.c_int32),
                 ("orbit_expansions", ctypes.c_int64), ("orbit_rescored", ctypes.c_int64),
                 ("tie_order", ctypes.c_int32), ("kd_levels", ctypes.c_int32), ("kd_build_ms", ctypes.c_double),
                 ("kd_replayed", ctypes.c_int64)]

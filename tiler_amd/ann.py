@@ -104,7 +104,7 @@ class KDTree:
         check(self._lib.ann_kdtree_get_stats(self.handle, ctypes.byref(s)), "ann_kdtree_get_stats")
         return {"queries": s.queries, "fallback_queries": s.fallback_queries,
                 "exhaustive_queries": s.exhaustive_queries, "exact_integer": s.exact_integer, "splits": s.splits,
-                "orbit_groups": s.orbit_groups, "orbit_search": s.orbit_search,
+                "orbit_groups": s.orbit_groups, "orbit_search": s.orbit_search, "orbit_ksteps": s.orbit_ksteps,
                 "orbit_expansions": s.orbit_expansions, "orbit_rescored": s.orbit_rescored,
                 "tie_order": s.tie_order, "kd_levels": s.kd_levels, "kd_build_ms": round(s.kd_build_ms, 3),
                 "kd_replayed": s.kd_replayed}

@@ -398,7 +398,7 @@ int ann_kdtree_get_stats(ann_kdtree *t, tiler_search_stats *out) {
     out->splits = t->ix->last_splits;
     out->orbit_groups = t->ix->orbit ? orbit_groups(t->ix) : 0;
     out->orbit_search = t->ix->last_orbit;
-    out->reserved = 0;
+    out->orbit_ksteps = t->ix->orbit ? orbit_ksteps(t->ix) : 0;
     long long ne = 0, nr = 0;
     if (t->ix->orbit) orbit_counters(t->ix, &ne, &nr);
     out->orbit_expansions = ne;

@@ -252,6 +252,21 @@ __global__ __launch_bounds__(256) void orbit_dup_kernel(const float *__restrict_
     }
 }
 
+// Bit x of mask[g]: isotypic block x of group g's fp16 c' has a nonzero value.  A mirror-symmetric tile (S_m c == c)
+// has exactly-zero blocks (those odd under m), whose MFMA contributions are +-0 for every query.  One wave per group.
+__global__ __launch_bounds__(256) void orbit_zmask_kernel(const _Float16 *__restrict__ rowh, long G, uint8_t *mask) {
+    const int lane = threadIdx.x & 63;
+    for (long g = (long)blockIdx.x * 4 + (threadIdx.x >> 6); g < G; g += (long)gridDim.x * 4) {
+        unsigned m = 0;
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            const bool nz = lane < 48 && (float)rowh[g * OD + x * 48 + lane] != 0.0f;
+            if (__any(nz)) m |= 1u << x;
+        }
+        if (lane == 0) mask[g] = (uint8_t)m;
+    }
+}
+
 // One thread per group: the kd-tree nodes separating the group's members (ANN's visit order among them,
 // kdorder_dev.hpp), i.e. the lowest common node of every present slot pair, walked from the root on positions.
 __global__ __launch_bounds__(256) void orbit_gorder_kernel(KdOrder o, const int *__restrict__ member, long G,
@@ -658,7 +673,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                                                                          const half8 *__restrict__ qfrag, int nq,
                                                                          int blk_per_split, int nsplit,
                                                                          float *__restrict__ out_key,
-                                                                         int *__restrict__ out_id) {
+                                                                         int *__restrict__ out_id, int red_end,
+                                                                         const uint8_t *__restrict__ bmask) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * OS * 1024;
     constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
@@ -699,10 +715,13 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
         }
     }
 
-    const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
-    auto issue = [&](int st, int buf) {
-        const int blk0 = b_begin + st * CB;
-        const int nb = min(CB, b_end - blk0);
+    // blocks [b_begin, r_end): groups with zero isotypic blocks (orbit_build orders them first), block-serial with
+    // only the nonzero k-steps; [p_begin, b_end): the pipelined full contraction
+    const int r_end = max(b_begin, min(b_end, red_end));
+    const int p_begin = r_end;
+    auto issue_rng = [&](int base, int end, int st, int buf) __attribute__((always_inline)) {
+        const int blk0 = base + st * CB;
+        const int nb = min(CB, end - blk0);
         const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * OS * 64 + w * 64 + lane;
         char *dst = smem + buf * BUF_BYTES + w * 1024;
         if (nb == CB) {
@@ -717,6 +736,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
             glds16_asm(reinterpret_cast<const uint4 *>(cseed) + (long)blk0 * 8 + min(lane, nb * 8 - 1),
                        smem + buf * BUF_BYTES + FRAG_BYTES);
     };
+    const int nstage = (b_end > p_begin) ? (b_end - p_begin + CB - 1) / CB : 0;
+    auto issue = [&](int st, int buf) __attribute__((always_inline)) { issue_rng(p_begin, b_end, st, buf); };
 
     // list insertion of one finished block: every sub-block above the lane's current L-th entry, best first
     auto insert_block = [&](int q, float (&m4)[4], int blk) __attribute__((always_inline)) {
@@ -748,6 +769,58 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
         return fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
     };
 
+    if (r_end > b_begin) {  // the symmetric groups' blocks (same bound, same order of adds, zero blocks skipped)
+        const floatx16 zero4 = {0};
+        const int nst_r = (r_end - b_begin + CB - 1) / CB;
+        issue_rng(b_begin, r_end, 0, 0);
+        dma_drain();
+        __syncthreads();
+        for (int st = 0; st < nst_r; st++) {
+            const char *B = smem + (st & 1) * BUF_BYTES;
+            if (st + 1 < nst_r) issue_rng(b_begin, r_end, st + 1, (st + 1) & 1);
+            const half8 *A = reinterpret_cast<const half8 *>(B) + lane;
+            const float4 *SD = reinterpret_cast<const float4 *>(B + FRAG_BYTES) + h * 4;
+            for (int cb = 0; cb < CB; cb++) {
+                const int blk = b_begin + st * CB + cb;
+                if (blk >= r_end) break;
+                const unsigned act = bmask[blk];  // bit x: some group of the block has a nonzero block x
+                const float4 s0 = SD[cb * 8 + 0], s1 = SD[cb * 8 + 1], s2 = SD[cb * 8 + 2], s3 = SD[cb * 8 + 3];
+                const floatx16 seed = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w,
+                                       s2.x, s2.y, s2.z, s2.w, s3.x, s3.y, s3.z, s3.w};
+                floatx16 P[QB], T[QB];
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const half8 av = A[(cb * OS + k) * 64];
+#pragma unroll
+                    for (int q = 0; q < QB; q++)
+                        P[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[q][k], k == 0 ? seed : P[q], 0, 0, 0);
+                }
+#pragma unroll
+                for (int x = 1; x < 4; x++) {
+                    if (!((act >> x) & 1)) continue;  // uniform
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const half8 av = A[(cb * OS + 3 * x + k) * 64];
+#pragma unroll
+                        for (int q = 0; q < QB; q++)
+                            T[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[q][3 * x + k], k == 0 ? zero4 : T[q], 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int q = 0; q < QB; q++)
+#pragma unroll
+                        for (int r = 0; r < 16; r++) P[q][r] = P[q][r] + fabsf(T[q][r]);
+                }
+#pragma unroll
+                for (int q = 0; q < QB; q++) {
+                    float m4[4];
+                    const float mx = maxima(P[q], m4);
+                    if (__any(mx > th[q])) insert_block(q, m4, blk);
+                }
+            }
+            dma_drain();
+            __syncthreads();
+        }
+    }
     if (nstage > 0) issue(0, 0);
     dma_drain();
     __syncthreads();
@@ -922,8 +995,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
         if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
 #pragma unroll
         for (int cb = 0; cb < CB; cb += 2) {
-            body(A, SD, cb, b_begin + st * CB + cb, RA, RC, SA, SC);
-            body(A, SD, cb + 1, b_begin + st * CB + cb + 1, RC, RA, SC, SA);
+            body(A, SD, cb, p_begin + st * CB + cb, RA, RC, SA, SC);
+            body(A, SD, cb + 1, p_begin + st * CB + cb + 1, RC, RA, SC, SA);
         }
         dma_drain();
         __syncthreads();
@@ -1899,6 +1972,7 @@ static double bits2d(unsigned long long b) {
 
 void orbit_destroy(OrbitIndex *o) {
     if (!o) return;
+    hipFree(o->d_bmask);
     hipFree(o->d_frag);
     hipFree(o->d_rowh);
     hipFree(o->d_seed);
@@ -2023,6 +2097,59 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     o->Np = sqrt(bits2d(ds.max_p2));
     o->Hp = sqrt(bits2d(ds.max_h2));
     o->Ecp = sqrt(bits2d(ds.max_e2));
+    o->ksteps = 12 * o->gblk;
+    // Mirror-symmetric groups: an H- (V-) symmetric tile's c' is exactly zero in the isotypic blocks odd under H (V),
+    // so those k-steps contribute +-0 to every query's d_x and |d_x| adds +0 to a bound that is never -0: skipping
+    // them gives the same bits.  Groups are reordered (stably) so that the ones with zero blocks come first --
+    // {0} only, then {0,2}, then {0,1} -- and the shortlist runs those blocks with only their nonzero k-steps.
+    // Every other structure is indexed by the group number and rebuilt for the new order (member drives them all).
+    {
+        uint8_t *d_mask = nullptr;
+        TILER_HIP_CHECK(hipMalloc((void **)&d_mask, G));
+        hipLaunchKernelGGL(orbit_zmask_kernel, dim3((unsigned)std::min<long>(8192, (G + 3) / 4)), dim3(256), 0, stream,
+                           (const _Float16 *)o->d_rowh, G, d_mask);
+        std::vector<uint8_t> mask(G);
+        TILER_HIP_CHECK(hipMemcpyAsync(mask.data(), d_mask, G, hipMemcpyDeviceToHost, stream));
+        TILER_HIP_CHECK(hipStreamSynchronize(stream));
+        hipFree(d_mask);
+        auto key = [](unsigned m) { return (m & ~1u) == 0 ? 0 : (m & ~5u) == 0 ? 1 : (m & ~3u) == 0 ? 2 : 3; };
+        std::vector<int> order(G);
+        long nred = 0;
+        for (long g = 0; g < G; g++) {
+            order[g] = (int)g;
+            nred += key(mask[g]) < 3;
+        }
+        if (nred >= 64) {
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key(mask[a]) < key(mask[b]); });
+            std::vector<int> pm((size_t)G * 4);
+            for (long g = 0; g < G; g++)
+                for (int x = 0; x < 4; x++) pm[g * 4 + x] = member[(size_t)order[g] * 4 + x];
+            o->red_end = (int)((nred + 31) / 32);
+            std::vector<uint8_t> bm(o->red_end, 0);
+            for (long g = 0; g < (long)o->red_end * 32 && g < G; g++) bm[g / 32] |= mask[order[g]] | 1u;
+            o->ksteps = 12 * (o->gblk - o->red_end);
+            for (int b = 0; b < o->red_end; b++) o->ksteps += 3 * __builtin_popcount(bm[b]);
+            TILER_HIP_CHECK(hipMalloc((void **)&o->d_bmask, o->red_end));
+            TILER_HIP_CHECK(hipMemcpyAsync(o->d_bmask, bm.data(), o->red_end, hipMemcpyHostToDevice, stream));
+            TILER_HIP_CHECK(hipMemcpyAsync(o->d_member, pm.data(), G * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
+            hipLaunchKernelGGL(orbit_dup_kernel, dim3((unsigned)std::min<long>(8192, (G + 3) / 4)), dim3(256), 0, stream,
+                               ix->d_rows, o->d_member, G, o->d_dup, o->d_rep);
+            if (ix->kd) {
+                TILER_HIP_CHECK(hipMemsetAsync(o->d_grp_of, 0xff, n * sizeof(int), stream));
+                hipLaunchKernelGGL(orbit_gorder_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, stream,
+                                   ix->kd->view(), o->d_member, G, o->d_gorder, o->d_grp_of);
+            }
+            TILER_HIP_CHECK(hipMalloc((void **)&d_ds, sizeof(OrbitDsStat)));
+            TILER_HIP_CHECK(hipMemsetAsync(d_ds, 0, sizeof(OrbitDsStat), stream));
+            OrbitPrepArgs pb{ix->d_rows, o->d_member, G, (const OrbitMap *)d_map, ix->scale, (half8 *)o->d_frag,
+                             (_Float16 *)o->d_rowh, o->d_seed, o->d_nc, d_ds, nullptr};
+            hipLaunchKernelGGL(orbit_prep_kernel, dim3((unsigned)std::min<long>(4096, (o->gblk + ORB_PW - 1) / ORB_PW)),
+                               dim3(64 * ORB_PW), 0, stream, pb);
+            TILER_HIP_CHECK(hipGetLastError());
+            TILER_HIP_CHECK(hipStreamSynchronize(stream));  // (pm, bm) stay alive until the copies are done
+            hipFree(d_ds);
+        }
+    }
     ix->orbit = o;
     return 0;
 }
@@ -2142,7 +2269,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
 #define ORB_PIPE(MD)                                                                                              \
     hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, MD>), dim3(wgs, nsplit),              \
                        dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
-                       (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id)
+                       (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id, o->red_end, o->d_bmask)
 #ifdef TILER_EXPERIMENTS
 #define ORB_LAUNCH(NWV, QB, MD)                                                                                   \
     hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, NWV, QB, MD>), dim3(wgs, nsplit),                  \
@@ -2169,11 +2296,11 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         else if (use_pipe && pmode == 8)  // one wave per SIMD: 4 waves x 4 query blocks (9: x 3)
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 4, 0>), dim3(wgs, nsplit), dim3(256), lds,
                                stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
-                               nsplit, o->key, o->id);
+                               nsplit, o->key, o->id, o->red_end, o->d_bmask);
         else if (use_pipe && pmode == 9)
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 3, 0>), dim3(wgs, nsplit), dim3(256), lds,
                                stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
-                               nsplit, o->key, o->id);
+                               nsplit, o->key, o->id, o->red_end, o->d_bmask);
         else if (use_pipe && !mix_full)
             ORB_PIPE(0);
         else if (use_pipe)
@@ -2202,13 +2329,14 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             TILER_HIP_CHECK(hipMemsetAsync(o->id, 0xff, na * sizeof(int), stream));
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, 0>), dim3(mix_full, 1),
                                dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,
-                               (const half8 *)o->qfrag, nq, o->gblk, nsplit, o->key, o->id);
+                               (const half8 *)o->qfrag, nq, o->gblk, nsplit, o->key, o->id, o->red_end, o->d_bmask);
             if (nq > q_off)
                 hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, 0>),
                                    dim3(wgs - mix_full, nsplit), dim3(ORB_NW * 64), lds, stream,
                                    (const half8 *)o->d_frag, o->d_seed, o->gblk,
                                    (const half8 *)o->qfrag + (size_t)qb_off * OS * 64, nq - q_off, bps, nsplit,
-                                   o->key + (size_t)q_off * per_q, o->id + (size_t)q_off * per_q);
+                                   o->key + (size_t)q_off * per_q, o->id + (size_t)q_off * per_q, o->red_end,
+                                   o->d_bmask);
         }
 #undef ORB_PIPE
     }

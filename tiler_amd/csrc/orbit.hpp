@@ -47,6 +47,11 @@ struct OrbitIndex {
     GroupOrder *d_gorder = nullptr;  // [G] (kd tie order only)
     int *d_grp_of = nullptr;      // [n] candidate -> g * 4 + slot (kd tie order only; -1: not in a group)
     void *d_map = nullptr;        // OrbitMap
+    // mirror-symmetric groups first (orbit_build): blocks [0, red_end) may have isotypic blocks of c' that are zero
+    // for every group in them (bit x of d_bmask[blk] clear), whose k-steps the shortlist skips; the rest are full
+    int red_end = 0;
+    int ksteps = 0;               // k-steps issued per query: 12 per full block, 3 per nonzero isotypic block below red_end
+    uint8_t *d_bmask = nullptr;   // [red_end] union of the block's groups' nonzero isotypic blocks
     double N = 0, Np = 0, Hp = 0, Ecp = 0;  // max ||c||, ||c'||, ||fp16(c')||, ||c' - fp16(c')||
     // per-call scratch
     void *qfrag = nullptr;        // [nqblk][12][64][8] fp16 q' (MFMA B fragments; the rescore re-keys from them)
@@ -81,6 +86,7 @@ struct OrbitTail {
 int orbit_build(NNIndex *ix, hipStream_t stream);
 void orbit_destroy(OrbitIndex *o);
 inline long long orbit_groups(const NNIndex *ix) { return ix->orbit ? ((const OrbitIndex *)ix->orbit)->G : 0; }
+inline int orbit_ksteps(const NNIndex *ix) { return ix->orbit ? ((const OrbitIndex *)ix->orbit)->ksteps : 0; }
 // rescore counters of the last search (TILER_ORBIT_STATS=1, else 0): 4-entry expansion passes, candidates rescored
 void orbit_counters(const NNIndex *ix, long long *expansions, long long *rescored);
 // k = 1 search of nq fp32 query rows: query prep, orbit shortlist, orbit rescore (tiers 2/3 by the caller);

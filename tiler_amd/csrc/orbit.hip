@@ -2113,14 +2113,13 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
         TILER_HIP_CHECK(hipStreamSynchronize(stream));
         hipFree(d_mask);
         auto key = [](unsigned m) { return (m & ~1u) == 0 ? 0 : (m & ~5u) == 0 ? 1 : (m & ~3u) == 0 ? 2 : 3; };
-        std::vector<int> order(G);
-        long nred = 0;
-        for (long g = 0; g < G; g++) {
-            order[g] = (int)g;
-            nred += key(mask[g]) < 3;
-        }
+        long cnt[5] = {0, 0, 0, 0, 0};  // stable counting sort by class (4 keys)
+        for (long g = 0; g < G; g++) cnt[key(mask[g]) + 1]++;
+        const long nred = cnt[1] + cnt[2] + cnt[3];
         if (nred >= 64) {
-            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key(mask[a]) < key(mask[b]); });
+            for (int k = 1; k < 5; k++) cnt[k] += cnt[k - 1];
+            std::vector<int> order(G);
+            for (long g = 0; g < G; g++) order[cnt[key(mask[g])]++] = (int)g;
             std::vector<int> pm((size_t)G * 4);
             for (long g = 0; g < G; g++)
                 for (int x = 0; x < 4; x++) pm[g * 4 + x] = member[(size_t)order[g] * 4 + x];

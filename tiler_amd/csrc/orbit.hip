@@ -825,7 +825,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
     dma_drain();
     __syncthreads();
     if ((MODE == 3 || MODE == 5 || MODE == 7) && w >= NW / 2) __builtin_amdgcn_s_setprio(1);  // experiment: static priority, 2nd half
-    // experiment LOOSE (modes 6, 7): a sub-block's bound is the sum of its four per-block maxima,
+    // experiment LOOSE (modes 6, 7; no longer launched: its loose keys fill the lists and send queries to the slow
+    // tiers, profiles/r02s_shortlist_ab.txt): a sub-block's bound is the sum of its four per-block maxima,
     // max_t d0 + max_t |d1| + max_t |d2| + max_t |d3| >= max_t u_t (still rigorous, looser), kept in SA / SC
     constexpr bool LOOSE = MODE == 6 || MODE == 7;
     const floatx16 zero = {0};
@@ -2284,10 +2285,6 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             ORB_PIPE(4);
         else if (use_pipe && pmode == 5)
             ORB_PIPE(5);
-        else if (use_pipe && pmode == 6)  // 6 looser sub-block bound (sum of per-block maxima), 7 = 6 + setprio
-            ORB_PIPE(6);
-        else if (use_pipe && pmode == 7)
-            ORB_PIPE(7);
         else if (use_pipe && pmode == 11)  // timing: MFMA + loads + independent VALU adds (results invalid)
             ORB_PIPE(11);
         else if (use_pipe && pmode == 12)  // timing: MFMA + loads only, every chain live (results invalid)

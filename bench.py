@@ -200,7 +200,9 @@ def main():
     # the MFMA work actually issued: k-steps of 16 dims x 32 groups per query (12 per block of groups; the blocks of
     # mirror-symmetric tiles skip their exactly-zero isotypic blocks: orbit_build / stats["orbit_ksteps"])
     ksteps = stats.get("orbit_ksteps") or 0
-    issued_launch = (2.0 * ksteps * 32 * 16 * QK) if (orbit and ksteps) else \
+    nflat = stats.get("flat_queries") or 0  # flat tiles, grouped last: 3 k-steps per candidate block
+    gblk = ((stats["orbit_groups"] or 0) + 31) // 32
+    issued_launch = (2.0 * 32 * 16 * (ksteps * (QK - nflat) + 3 * gblk * nflat)) if (orbit and ksteps) else \
         2.0 * (stats["orbit_groups"] if orbit else M) * 192 * QK
     bruteforce_launch = 2.0 * M * 192 * QK
     issued = issued_launch / sec / 1e12 if sec else None
@@ -221,10 +223,12 @@ def main():
                 "effective_speedup": round(bruteforce_launch / issued_launch, 4),
                 "hbm": {"bytes_per_tile": round(ft_bytes_tile, 1), "achieved_gbs": round(hbm_gbs, 2),
                         "peak_gbs": PEAK_HBM_GBS, "hbm_frac": round(hbm_gbs / PEAK_HBM_GBS, 6)},
-                "issued_ksteps_per_query": ksteps,
+                "issued_ksteps_per_query": ksteps, "flat_queries": nflat,
+                "issued_ksteps_per_flat_query": 3 * gblk,
                 "note": ("achieved/frac = MFMA flops the kernel issues (2*16*32 per k-step x the k-steps per query: "
                          "12 per block of 32 mirror orbits, fewer on the blocks of mirror-symmetric tiles whose zero "
-                         "isotypic blocks are skipped; = 2*G*D without them) / its "
+                         "isotypic blocks are skipped, 3 per block for the flat query tiles grouped last; = 2*G*D "
+                         "without them) / its "
                          "average launch time (HIP events on the launch stream) vs the dense fp16 peak; "
                          "effective_tflops = the brute-force 2*M*D per query over the same time (effective_speedup = "
                          "brute-force / issued flops: the exact 4-mirror orbit algebra and the skipped zero blocks). hbm = the metric's '% HBM roofline': SURVEY.md 8(d) "

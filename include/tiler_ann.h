@@ -78,6 +78,8 @@ typedef struct {
     int32_t kd_levels;        /* levels of the kd-tree build */
     double kd_build_ms;       /* kd-tree build time at create */
     int64_t kd_replayed;      /* queries of the last search replayed exactly (ANN's pruning not vouched for) */
+    int64_t flat_queries;     /* queries of the last FrameTiling call whose shortlist ran isotypic block 0 only (flat
+                                 tiles, grouped last: 3 k-steps per candidate block instead of orbit_ksteps / blocks) */
 } tiler_search_stats;
 int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
 /* Leaf position of every dataset point in ANN's kd-tree (the order of its depth-first scan with every near

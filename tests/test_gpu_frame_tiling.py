@@ -173,6 +173,26 @@ def test_frame_tiling_end_to_end_c1(gpu, oracle):
     kt.finish_frame_tiling()
 
 
+def test_frame_tiling_flat_tiles_last_matches_small_batches(gpu):
+    """A batch of >= 8192 tiles runs with its flat tiles moved last (their shortlist workgroups compute isotypic block
+    0 only, nn_frame_tiling_dev / orbit_search); per-frame batches below that size keep the tile order.  Both must
+    give the same tilemap items and errors bit for bit (the per-frame path is checked against the oracle above)."""
+    from tiler_amd.frame_tiling import KeyframeTiler
+    wl = synth.make_workload(23, 320, 240, 8, 1000, n_palettes=16)
+    kt = KeyframeTiler(wl.tiles, wl.thm, wl.tvm, wl.palettes, wl.ds)
+    frames = np.stack([wl.frame_rgb[f] for f in range(wl.frames)])
+    Q = frames.shape[1]
+    flat = (frames.reshape(-1, 64) == frames.reshape(-1, 64)[:, :1]).all(axis=1)
+    assert frames.shape[0] * Q >= 8192 and 0 < flat.sum() < flat.size
+    big = kt.do_frame_tiling(frames.reshape(-1, 64))
+    for f in range(wl.frames):
+        g = kt.do_frame_tiling(frames[f])
+        for a, b in zip(g[:4], big[:4]):
+            assert np.array_equal(a, b[f * Q:(f + 1) * Q])
+        assert np.array_equal(g[4].view(np.uint32), big[4][f * Q:(f + 1) * Q].view(np.uint32))
+    kt.finish_frame_tiling()
+
+
 def test_prepare_frame_tiling_used_table(gpu, oracle):
     """UseOne (k=8 preselection + distinct-err walk) for Fast / Medium / Slow, main.pas:3802-3853."""
     from tiler_amd import frame_tiling as ft

@@ -34,7 +34,7 @@ class SearchStats(ctypes.Structure):
                 ("orbit_groups", ctypes.c_int64), ("orbit_search", ctypes.c_int32), ("orbit_ksteps", ctypes.c_int32),
                 ("orbit_expansions", ctypes.c_int64), ("orbit_rescored", ctypes.c_int64),
                 ("tie_order", ctypes.c_int32), ("kd_levels", ctypes.c_int32), ("kd_build_ms", ctypes.c_double),
-                ("kd_replayed", ctypes.c_int64)]
+                ("kd_replayed", ctypes.c_int64), ("flat_queries", ctypes.c_int64)]
 
 
 _SIGS = {

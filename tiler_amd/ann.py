@@ -107,7 +107,7 @@ class KDTree:
                 "orbit_groups": s.orbit_groups, "orbit_search": s.orbit_search, "orbit_ksteps": s.orbit_ksteps,
                 "orbit_expansions": s.orbit_expansions, "orbit_rescored": s.orbit_rescored,
                 "tie_order": s.tie_order, "kd_levels": s.kd_levels, "kd_build_ms": round(s.kd_build_ms, 3),
-                "kd_replayed": s.kd_replayed}
+                "kd_replayed": s.kd_replayed, "flat_queries": s.flat_queries}
 
     def positions(self) -> np.ndarray:
         """Leaf position of every point in ANN's kd-tree (tiler_kdtree_positions)."""

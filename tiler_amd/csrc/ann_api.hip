@@ -407,6 +407,7 @@ int ann_kdtree_get_stats(ann_kdtree *t, tiler_search_stats *out) {
     out->kd_levels = t->ix->kd ? t->ix->kd->levels : 0;
     out->kd_build_ms = t->ix->kd ? t->ix->kd->build_ms : 0.0;
     out->kd_replayed = 0;
+    out->flat_queries = t->ix->last_flat_queries;
     if (t->ix->kd && t->ix->scratch.kd_count) {
         int c = 0;
         TILER_HIP_CHECK(hipStreamSynchronize(t->stream));

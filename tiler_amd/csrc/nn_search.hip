@@ -966,6 +966,17 @@ void nn_index_destroy(NNIndex *ix) {
     hipFree(s.kd_count);
     hipFree(s.kd_rootbox);
     hipFree(s.kd_done);
+    hipFree(s.fperm);
+    hipFree(s.fbcnt);
+    hipFree(s.fcnt);
+    hipFree(s.fflag);
+    hipFree(s.frgb);
+    hipFree(s.fidx);
+    hipFree(s.ferr);
+    hipFree(s.ftile);
+    hipFree(s.fpal);
+    hipFree(s.fhm);
+    hipFree(s.fvm);
     hipHostFree(ix->h_fb_count);
     delete ix;
 }
@@ -1226,6 +1237,7 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
         t.ex_count = s.fb_count + 1;
         t.fb_max = TIER2_MAX;
         t.thr = s.thr;
+        t.flat_from = ix->flat_from;
         t.out_idx = ra.out_idx;
         t.out_err = ra.out_err;
         t.tr_tile = ra.tr_tile;
@@ -1328,6 +1340,96 @@ static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t s
     return 0;
 }
 
+// Flat tiles (one colour: every Haar coefficient but the DC is 0, so only isotypic block 0 of q' is nonzero) are
+// moved to the end of the batch, where whole shortlist workgroups of them run 3 of the 12 k-steps (orbit_search).
+// A: per tile flag + per-block count of the others; B: one workgroup scans the block counts; C: stable positions
+// (others first, flats after, each in tile order) + the RGB gather; D: the outputs back to the original order.
+__global__ __launch_bounds__(256) void ft_flat_flag_kernel(const int32_t *__restrict__ rgb, int Q, uint8_t *flag,
+                                                           int *bcnt) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    int other = 0;
+    if (i < Q) {
+        const int4 *t = reinterpret_cast<const int4 *>(rgb + i * 64);
+        const int c0 = rgb[i * 64];
+        bool flat = true;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int4 v = t[k];
+            flat = flat && v.x == c0 && v.y == c0 && v.z == c0 && v.w == c0;
+        }
+        flag[i] = flat ? 1 : 0;
+        other = flat ? 0 : 1;
+    }
+    const int c = __syncthreads_count(other);
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(1024) void ft_flat_scan_kernel(int *bcnt, int nb, int *total) {
+    __shared__ int sc[1024];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int b0 = 0; b0 < nb; b0 += 1024) {
+        const int b = b0 + threadIdx.x;
+        const int v = b < nb ? bcnt[b] : 0;
+        sc[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const int u = threadIdx.x >= o ? sc[threadIdx.x - o] : 0;
+            __syncthreads();
+            sc[threadIdx.x] += u;
+            __syncthreads();
+        }
+        if (b < nb) bcnt[b] = carry + sc[threadIdx.x] - v;  // exclusive prefix
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += sc[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(256) void ft_flat_place_kernel(const int32_t *__restrict__ rgb, int Q,
+                                                            const uint8_t *__restrict__ flag,
+                                                            const int *__restrict__ boff, const int *__restrict__ total,
+                                                            int *perm, int32_t *out) {
+    __shared__ int sc[256];
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    const int f = i < Q ? flag[i] : 1;
+    sc[threadIdx.x] = f ? 0 : 1;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        const int u = threadIdx.x >= o ? sc[threadIdx.x - o] : 0;
+        __syncthreads();
+        sc[threadIdx.x] += u;
+        __syncthreads();
+    }
+    if (i >= Q) return;
+    const int rank_other = sc[threadIdx.x] - (f ? 0 : 1);          // others before this tile in the block
+    const int rank_flat = (int)threadIdx.x - rank_other - (f ? 0 : 1);  // flats before it in the block
+    const int b_other = boff[blockIdx.x], b_flat = (int)(blockIdx.x * 256) - b_other;
+    const long pos = f ? (long)*total + b_flat + rank_flat : (long)b_other + rank_other;
+    perm[pos] = (int)i;
+    const int4 *src = reinterpret_cast<const int4 *>(rgb + i * 64);
+    int4 *dst = reinterpret_cast<int4 *>(out + pos * 64);
+#pragma unroll
+    for (int k = 0; k < 16; k++) dst[k] = src[k];
+}
+
+__global__ __launch_bounds__(256) void ft_unpermute_kernel(int Q, const int *__restrict__ perm, const int *fidx,
+                                                           const float *ferr, const int32_t *ftile, const int32_t *fpal,
+                                                           const uint8_t *fhm, const uint8_t *fvm, int *idx, float *err,
+                                                           FtMaps maps) {
+    const long p = (long)blockIdx.x * 256 + threadIdx.x;
+    if (p >= Q) return;
+    const long o = perm[p];
+    if (idx) idx[o] = fidx[p];
+    if (err) err[o] = ferr[p];
+    if (maps.tile) maps.tile[o] = ftile[p];
+    if (maps.pal) maps.pal[o] = fpal[p];
+    if (maps.hm) maps.hm[o] = fhm[p];
+    if (maps.vm) maps.vm[o] = fvm[p];
+}
+
 int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int *d_idx,
                         float *d_err, const FtMaps *maps, hipStream_t stream) {
     if (Q <= 0) return 0;
@@ -1344,6 +1446,60 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
     const bool fuse_rb = ix->kd && use_wavelets && ix->kd->dd == 192;
     if (fuse_rb && ensure_scratch(ix, Q, 0)) return -1;
     if (ix->orbit && use_wavelets) {
+#ifdef TILER_EXPERIMENTS
+        static const bool noflat = getenv("TILER_NO_FLAT") != nullptr;  // A/B: tiles in their own order
+#else
+        constexpr bool noflat = false;
+#endif
+        if (!noflat && Q >= 8192) {  // flat tiles last (see ft_flat_flag_kernel)
+            const int nb = (Q + 255) / 256;
+            if ((size_t)Q > s.cap_flat) {
+                hipFree(s.fperm);
+                hipFree(s.fbcnt);
+                hipFree(s.fflag);
+                hipFree(s.frgb);
+                hipFree(s.fidx);
+                hipFree(s.ferr);
+                hipFree(s.ftile);
+                hipFree(s.fpal);
+                hipFree(s.fhm);
+                hipFree(s.fvm);
+                if (!s.fcnt) TILER_HIP_CHECK(hipMalloc((void **)&s.fcnt, sizeof(int)));
+                TILER_HIP_CHECK(hipMalloc((void **)&s.fperm, (size_t)Q * sizeof(int)));
+                TILER_HIP_CHECK(hipMalloc((void **)&s.fbcnt, (size_t)nb * sizeof(int)));
+                TILER_HIP_CHECK(hipMalloc((void **)&s.fflag, (size_t)Q));
+                TILER_HIP_CHECK(hipMalloc((void **)&s.frgb, (size_t)Q * 64 * sizeof(int32_t)));
+                TILER_HIP_CHECK(hipMalloc((void **)&s.fidx, (size_t)Q * sizeof(int)));
+                TILER_HIP_CHECK(hipMalloc((void **)&s.ferr, (size_t)Q * sizeof(float)));
+                TILER_HIP_CHECK(hipMalloc((void **)&s.ftile, (size_t)Q * sizeof(int32_t)));
+                TILER_HIP_CHECK(hipMalloc((void **)&s.fpal, (size_t)Q * sizeof(int32_t)));
+                TILER_HIP_CHECK(hipMalloc((void **)&s.fhm, (size_t)Q));
+                TILER_HIP_CHECK(hipMalloc((void **)&s.fvm, (size_t)Q));
+                s.cap_flat = Q;
+            }
+            hipLaunchKernelGGL(ft_flat_flag_kernel, dim3(nb), dim3(256), 0, stream, d_rgb, Q, s.fflag, s.fbcnt);
+            hipLaunchKernelGGL(ft_flat_scan_kernel, dim3(1), dim3(1024), 0, stream, s.fbcnt, nb, s.fcnt);
+            hipLaunchKernelGGL(ft_flat_place_kernel, dim3(nb), dim3(256), 0, stream, d_rgb, Q, (const uint8_t *)s.fflag,
+                               (const int *)s.fbcnt, (const int *)s.fcnt, s.fperm, s.frgb);
+            TILER_HIP_CHECK(hipGetLastError());
+            int others = Q;
+            TILER_HIP_CHECK(hipMemcpyAsync(&others, s.fcnt, sizeof(int), hipMemcpyDeviceToHost, stream));
+            TILER_HIP_CHECK(hipStreamSynchronize(stream));
+            FtMaps fm;
+            if (maps) fm = FtMaps{s.ftile, s.fpal, s.fhm, s.fvm};
+            ix->flat_from = others;
+            int rc = orbit_ft_queries(ix, s.frgb, Q, gamma, s.qrows, fuse_rb ? ix->kd->d_box : nullptr,
+                                      fuse_rb ? s.kd_rootbox : nullptr, stream);
+            if (!rc) rc = nn_search_dev(ix, s.qrows, Q, 1, s.fidx, s.ferr, maps ? &fm : nullptr, stream, fuse_rb, true);
+            ix->flat_from = 0x7fffffff;
+            if (rc) return -1;
+            hipLaunchKernelGGL(ft_unpermute_kernel, dim3(nb), dim3(256), 0, stream, Q, (const int *)s.fperm,
+                               (const int *)s.fidx, (const float *)s.ferr, (const int32_t *)s.ftile,
+                               (const int32_t *)s.fpal, (const uint8_t *)s.fhm, (const uint8_t *)s.fvm, d_idx, d_err,
+                               maps ? *maps : FtMaps{});
+            TILER_HIP_CHECK(hipGetLastError());
+            return 0;
+        }
         // one kernel: descriptors + the orbit search's q' fragments and statistics (+ the kd root box)
         if (orbit_ft_queries(ix, d_rgb, Q, gamma, s.qrows, fuse_rb ? ix->kd->d_box : nullptr,
                              fuse_rb ? s.kd_rootbox : nullptr, stream))

@@ -47,7 +47,15 @@ struct SearchScratch {
     int *kd_count = nullptr;  // [1]
     float *kd_rootbox = nullptr;  // [nq] annBoxDistance of each query to the kd-tree's enclosing box
     uint8_t *kd_done = nullptr;   // [nq] 1: the pair pass already checked this query's winner
-    size_t cap_q = 0, cap_keys = 0, cap_rows = 0;
+    // FrameTiling: flat tiles moved last (their descriptors have only isotypic block 0)
+    int *fperm = nullptr, *fbcnt = nullptr, *fcnt = nullptr;  // [Q] new -> original, [blocks], [1] non-flat count
+    uint8_t *fflag = nullptr;
+    int32_t *frgb = nullptr;                                   // [Q][64] permuted RGB
+    int *fidx = nullptr;
+    float *ferr = nullptr;
+    int32_t *ftile = nullptr, *fpal = nullptr;
+    uint8_t *fhm = nullptr, *fvm = nullptr;
+    size_t cap_q = 0, cap_keys = 0, cap_rows = 0, cap_flat = 0;
 };
 
 struct NNIndex {
@@ -56,6 +64,7 @@ struct NNIndex {
     double maxN = 0, maxH = 0, maxE = 0, max_abs = 0;
     bool exact_int = false;
     int perm = 0;               // 1: candidate rows spread over accumulator lanes (row_perm), float data
+    int flat_from = 0x7fffffff; // FrameTiling call in progress: queries >= flat_from are flat tiles (orbit shortlist)
     float *d_rows = nullptr;    // [n][d] fp32 (exact rescoring)
     void *d_frag = nullptr;     // [nblk][S][64][8] fp16, MFMA A-operand fragment order
     float *d_nc = nullptr;      // [nblk][32] ||c||^2 in accumulator-row order (+inf on padding rows)
@@ -70,6 +79,7 @@ struct NNIndex {
     std::mutex mu;
     long long last_queries = 0, last_fallback = 0;
     int last_splits = 0;
+    long last_flat_queries = 0; // queries of the last search whose orbit shortlist ran block 0 only
     int last_orbit = 0;         // 1: the last search ran the mirror-orbit path
     OrbitIndex *orbit = nullptr; // mirror-orbit index (orbit.hip), null when not applicable
     KdTree *kd = nullptr;       // KD_SPLIT_STD tree: ties resolve in ANN's first-found order (null: lowest index)

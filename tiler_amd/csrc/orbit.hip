@@ -674,7 +674,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                                                                          int blk_per_split, int nsplit,
                                                                          float *__restrict__ out_key,
                                                                          int *__restrict__ out_id, int red_end,
-                                                                         const uint8_t *__restrict__ bmask) {
+                                                                         const uint8_t *__restrict__ bmask,
+                                                                         int flat_wg0, const uint8_t *__restrict__ bmask0) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * OS * 1024;
     constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
@@ -717,8 +718,34 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
 
     // blocks [b_begin, r_end): groups with zero isotypic blocks (orbit_build orders them first), block-serial with
     // only the nonzero k-steps; [p_begin, b_end): the pipelined full contraction
+    // workgroups from flat_wg0 on hold flat query tiles only (q' block 0): every candidate block block-serially with
+    // k-steps 0..2, only those streamed
+    const bool flat = (int)blockIdx.x >= flat_wg0;
+    const int nks = flat ? 3 : OS;
+    if (flat) {
+        red_end = nblk;
+        bmask = bmask0;
+    }
     const int r_end = max(b_begin, min(b_end, red_end));
     const int p_begin = r_end;
+    auto issue_k3 = [&](int base, int end, int st, int buf) __attribute__((always_inline)) {
+        // k-steps 0..2 of each block of the stage (3 x 64 16-byte pieces per block) to their usual LDS places
+        const int blk0 = base + st * CB;
+        const int nb = min(CB, end - blk0);
+#pragma unroll
+        for (int j = 0; j < (CB * 192 + NT - 1) / NT; j++) {
+            const int e0 = j * NT + w * 64;  // the wave's first piece: 64-aligned, never straddles a block
+            if (e0 < CB * 192) {
+                const int cb = e0 / 192, r0 = e0 % 192;
+                const int cbc = min(cb, nb - 1);  // past the end: a duplicate of the last block, never used
+                glds16_asm(reinterpret_cast<const uint4 *>(cfrag) + (long)(blk0 + cbc) * OS * 64 + r0 + lane,
+                           smem + buf * BUF_BYTES + (cb * OS * 64 + r0) * 16);
+            }
+        }
+        if (w == 0 && lane < CB * 8)
+            glds16_asm(reinterpret_cast<const uint4 *>(cseed) + (long)blk0 * 8 + min(lane, nb * 8 - 1),
+                       smem + buf * BUF_BYTES + FRAG_BYTES);
+    };
     auto issue_rng = [&](int base, int end, int st, int buf) __attribute__((always_inline)) {
         const int blk0 = base + st * CB;
         const int nb = min(CB, end - blk0);
@@ -772,12 +799,20 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
     if (r_end > b_begin) {  // the symmetric groups' blocks (same bound, same order of adds, zero blocks skipped)
         const floatx16 zero4 = {0};
         const int nst_r = (r_end - b_begin + CB - 1) / CB;
-        issue_rng(b_begin, r_end, 0, 0);
+        if (nks == 3)
+            issue_k3(b_begin, r_end, 0, 0);
+        else
+            issue_rng(b_begin, r_end, 0, 0);
         dma_drain();
         __syncthreads();
         for (int st = 0; st < nst_r; st++) {
             const char *B = smem + (st & 1) * BUF_BYTES;
-            if (st + 1 < nst_r) issue_rng(b_begin, r_end, st + 1, (st + 1) & 1);
+            if (st + 1 < nst_r) {
+                if (nks == 3)
+                    issue_k3(b_begin, r_end, st + 1, (st + 1) & 1);
+                else
+                    issue_rng(b_begin, r_end, st + 1, (st + 1) & 1);
+            }
             const half8 *A = reinterpret_cast<const half8 *>(B) + lane;
             const float4 *SD = reinterpret_cast<const float4 *>(B + FRAG_BYTES) + h * 4;
             for (int cb = 0; cb < CB; cb++) {
@@ -1974,6 +2009,7 @@ static double bits2d(unsigned long long b) {
 void orbit_destroy(OrbitIndex *o) {
     if (!o) return;
     hipFree(o->d_bmask);
+    hipFree(o->d_bmask0);
     hipFree(o->d_frag);
     hipFree(o->d_rowh);
     hipFree(o->d_seed);
@@ -2150,6 +2186,12 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
             hipFree(d_ds);
         }
     }
+    {  // block 0 only, every block: the flat query tiles' shortlist (orbit_search)
+        std::vector<uint8_t> ones(o->gblk, 1);
+        TILER_HIP_CHECK(hipMalloc((void **)&o->d_bmask0, o->gblk));
+        TILER_HIP_CHECK(hipMemcpyAsync(o->d_bmask0, ones.data(), o->gblk, hipMemcpyHostToDevice, stream));
+        TILER_HIP_CHECK(hipStreamSynchronize(stream));
+    }
     ix->orbit = o;
     return 0;
 }
@@ -2244,6 +2286,18 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             }
         }
     }
+    // Flat query tiles (tail.flat_from.., FrameTiling moves them last): their q' has only block 0, so the workgroups
+    // made of them alone run the block-serial body with 3 of the 12 k-steps on every candidate block (d_1..d_3 are
+    // +-0 for them: the same bounds bit for bit).  Uses one candidate split.
+    const int qpw_q = qpw * 32;  // queries per workgroup
+    int wf0 = wgs;
+    if (use_pipe && pmode == 0 && tail.flat_from < nq) {
+        wf0 = std::min(wgs, (std::max(0, tail.flat_from) + qpw_q - 1) / qpw_q);
+        if (wf0 < wgs) {
+            nsplit = 1;
+            mix_full = 0;
+        }
+    }
     const int bps = (o->gblk + nsplit - 1) / nsplit;
     nsplit = (o->gblk + bps - 1) / bps;
     if (orbit_ensure_queries(o, nq)) return -1;
@@ -2269,7 +2323,8 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
 #define ORB_PIPE(MD)                                                                                              \
     hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, MD>), dim3(wgs, nsplit),              \
                        dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
-                       (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id, o->red_end, o->d_bmask)
+                       (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id, o->red_end, o->d_bmask,                \
+                       MD == 0 ? wf0 : 0x7fffffff, o->d_bmask0)
 #ifdef TILER_EXPERIMENTS
 #define ORB_LAUNCH(NWV, QB, MD)                                                                                   \
     hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, NWV, QB, MD>), dim3(wgs, nsplit),                  \
@@ -2292,11 +2347,11 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         else if (use_pipe && pmode == 8)  // one wave per SIMD: 4 waves x 4 query blocks (9: x 3)
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 4, 0>), dim3(wgs, nsplit), dim3(256), lds,
                                stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
-                               nsplit, o->key, o->id, o->red_end, o->d_bmask);
+                               nsplit, o->key, o->id, o->red_end, o->d_bmask, 0x7fffffff, o->d_bmask0);
         else if (use_pipe && pmode == 9)
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 3, 0>), dim3(wgs, nsplit), dim3(256), lds,
                                stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
-                               nsplit, o->key, o->id, o->red_end, o->d_bmask);
+                               nsplit, o->key, o->id, o->red_end, o->d_bmask, 0x7fffffff, o->d_bmask0);
         else if (use_pipe && !mix_full)
             ORB_PIPE(0);
         else if (use_pipe)
@@ -2325,14 +2380,15 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             TILER_HIP_CHECK(hipMemsetAsync(o->id, 0xff, na * sizeof(int), stream));
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, 0>), dim3(mix_full, 1),
                                dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,
-                               (const half8 *)o->qfrag, nq, o->gblk, nsplit, o->key, o->id, o->red_end, o->d_bmask);
+                               (const half8 *)o->qfrag, nq, o->gblk, nsplit, o->key, o->id, o->red_end, o->d_bmask,
+                               0x7fffffff, o->d_bmask0);
             if (nq > q_off)
                 hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, 0>),
                                    dim3(wgs - mix_full, nsplit), dim3(ORB_NW * 64), lds, stream,
                                    (const half8 *)o->d_frag, o->d_seed, o->gblk,
                                    (const half8 *)o->qfrag + (size_t)qb_off * OS * 64, nq - q_off, bps, nsplit,
                                    o->key + (size_t)q_off * per_q, o->id + (size_t)q_off * per_q, o->red_end,
-                                   o->d_bmask);
+                                   o->d_bmask, 0x7fffffff, o->d_bmask0);
         }
 #undef ORB_PIPE
     }
@@ -2409,6 +2465,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         o->last_rescored = h[1];
     }
     ix->last_splits = nsplit;
+    ix->last_flat_queries = wf0 < wgs ? (long)nq - (long)wf0 * qpw_q : 0;
     return 0;
 }
 

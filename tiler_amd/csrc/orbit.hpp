@@ -52,6 +52,7 @@ struct OrbitIndex {
     int red_end = 0;
     int ksteps = 0;               // k-steps issued per query: 12 per full block, 3 per nonzero isotypic block below red_end
     uint8_t *d_bmask = nullptr;   // [red_end] union of the block's groups' nonzero isotypic blocks
+    uint8_t *d_bmask0 = nullptr;  // [gblk] all 1 (block 0 only): the shortlist of flat query tiles
     double N = 0, Np = 0, Hp = 0, Ecp = 0;  // max ||c||, ||c'||, ||fp16(c')||, ||c' - fp16(c')||
     // per-call scratch
     void *qfrag = nullptr;        // [nqblk][12][64][8] fp16 q' (MFMA B fragments; the rescore re-keys from them)
@@ -69,6 +70,7 @@ struct OrbitIndex {
 struct OrbitTail {
     int *fb_list, *fb_count, *ex_list, *ex_count, fb_max;
     float *thr;                   // [nq] tier-2 threshold T_b (bound-key domain, fp32 rounded up), set by the rescore
+    int flat_from;                // queries >= flat_from are flat tiles: only isotypic block 0 of q' is nonzero
     int *out_idx;
     float *out_err;
     const int32_t *tr_tile, *tr_pal;

@@ -970,7 +970,6 @@ void nn_index_destroy(NNIndex *ix) {
     hipFree(s.fbcnt);
     hipFree(s.fcnt);
     hipFree(s.fflag);
-    hipFree(s.frgb);
     hipFree(s.fidx);
     hipFree(s.ferr);
     hipFree(s.ftile);
@@ -1343,7 +1342,7 @@ static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t s
 // Flat tiles (one colour: every Haar coefficient but the DC is 0, so only isotypic block 0 of q' is nonzero) are
 // moved to the end of the batch, where whole shortlist workgroups of them run 3 of the 12 k-steps (orbit_search).
 // A: per tile flag + per-block count of the others; B: one workgroup scans the block counts; C: stable positions
-// (others first, flats after, each in tile order) + the RGB gather; D: the outputs back to the original order.
+// (others first, flats after, each in tile order), which the query kernel reads through; D: the outputs back.
 __global__ __launch_bounds__(256) void ft_flat_flag_kernel(const int32_t *__restrict__ rgb, int Q, uint8_t *flag,
                                                            int *bcnt) {
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -1391,7 +1390,7 @@ __global__ __launch_bounds__(1024) void ft_flat_scan_kernel(int *bcnt, int nb, i
 __global__ __launch_bounds__(256) void ft_flat_place_kernel(const int32_t *__restrict__ rgb, int Q,
                                                             const uint8_t *__restrict__ flag,
                                                             const int *__restrict__ boff, const int *__restrict__ total,
-                                                            int *perm, int32_t *out) {
+                                                            int *perm) {
     __shared__ int sc[256];
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
     const int f = i < Q ? flag[i] : 1;
@@ -1408,11 +1407,7 @@ __global__ __launch_bounds__(256) void ft_flat_place_kernel(const int32_t *__res
     const int rank_flat = (int)threadIdx.x - rank_other - (f ? 0 : 1);  // flats before it in the block
     const int b_other = boff[blockIdx.x], b_flat = (int)(blockIdx.x * 256) - b_other;
     const long pos = f ? (long)*total + b_flat + rank_flat : (long)b_other + rank_other;
-    perm[pos] = (int)i;
-    const int4 *src = reinterpret_cast<const int4 *>(rgb + i * 64);
-    int4 *dst = reinterpret_cast<int4 *>(out + pos * 64);
-#pragma unroll
-    for (int k = 0; k < 16; k++) dst[k] = src[k];
+    perm[pos] = (int)i;  // the query kernel reads tile perm[pos] (no copy of the RGB)
 }
 
 __global__ __launch_bounds__(256) void ft_unpermute_kernel(int Q, const int *__restrict__ perm, const int *fidx,
@@ -1457,7 +1452,6 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
                 hipFree(s.fperm);
                 hipFree(s.fbcnt);
                 hipFree(s.fflag);
-                hipFree(s.frgb);
                 hipFree(s.fidx);
                 hipFree(s.ferr);
                 hipFree(s.ftile);
@@ -1468,7 +1462,6 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
                 TILER_HIP_CHECK(hipMalloc((void **)&s.fperm, (size_t)Q * sizeof(int)));
                 TILER_HIP_CHECK(hipMalloc((void **)&s.fbcnt, (size_t)nb * sizeof(int)));
                 TILER_HIP_CHECK(hipMalloc((void **)&s.fflag, (size_t)Q));
-                TILER_HIP_CHECK(hipMalloc((void **)&s.frgb, (size_t)Q * 64 * sizeof(int32_t)));
                 TILER_HIP_CHECK(hipMalloc((void **)&s.fidx, (size_t)Q * sizeof(int)));
                 TILER_HIP_CHECK(hipMalloc((void **)&s.ferr, (size_t)Q * sizeof(float)));
                 TILER_HIP_CHECK(hipMalloc((void **)&s.ftile, (size_t)Q * sizeof(int32_t)));
@@ -1480,7 +1473,7 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
             hipLaunchKernelGGL(ft_flat_flag_kernel, dim3(nb), dim3(256), 0, stream, d_rgb, Q, s.fflag, s.fbcnt);
             hipLaunchKernelGGL(ft_flat_scan_kernel, dim3(1), dim3(1024), 0, stream, s.fbcnt, nb, s.fcnt);
             hipLaunchKernelGGL(ft_flat_place_kernel, dim3(nb), dim3(256), 0, stream, d_rgb, Q, (const uint8_t *)s.fflag,
-                               (const int *)s.fbcnt, (const int *)s.fcnt, s.fperm, s.frgb);
+                               (const int *)s.fbcnt, (const int *)s.fcnt, s.fperm);
             TILER_HIP_CHECK(hipGetLastError());
             int others = Q;
             TILER_HIP_CHECK(hipMemcpyAsync(&others, s.fcnt, sizeof(int), hipMemcpyDeviceToHost, stream));
@@ -1488,8 +1481,8 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
             FtMaps fm;
             if (maps) fm = FtMaps{s.ftile, s.fpal, s.fhm, s.fvm};
             ix->flat_from = others;
-            int rc = orbit_ft_queries(ix, s.frgb, Q, gamma, s.qrows, fuse_rb ? ix->kd->d_box : nullptr,
-                                      fuse_rb ? s.kd_rootbox : nullptr, stream);
+            int rc = orbit_ft_queries(ix, d_rgb, Q, gamma, s.qrows, fuse_rb ? ix->kd->d_box : nullptr,
+                                      fuse_rb ? s.kd_rootbox : nullptr, stream, s.fperm);
             if (!rc) rc = nn_search_dev(ix, s.qrows, Q, 1, s.fidx, s.ferr, maps ? &fm : nullptr, stream, fuse_rb, true);
             ix->flat_from = 0x7fffffff;
             if (rc) return -1;

@@ -50,7 +50,6 @@ struct SearchScratch {
     // FrameTiling: flat tiles moved last (their descriptors have only isotypic block 0)
     int *fperm = nullptr, *fbcnt = nullptr, *fcnt = nullptr;  // [Q] new -> original, [blocks], [1] non-flat count
     uint8_t *fflag = nullptr;
-    int32_t *frgb = nullptr;                                   // [Q][64] permuted RGB
     int *fidx = nullptr;
     float *ferr = nullptr;
     int32_t *ftile = nullptr, *fpal = nullptr;

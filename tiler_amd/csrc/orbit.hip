@@ -1607,6 +1607,7 @@ struct FtQueryArgs {
     const float *box;    // [2][192] or null
     float *rootbox;      // [n] when box
     int xmode;           // timing experiments only (TILER_EXPERIMENTS build, TILER_FTQ_MODE): results invalid
+    const int *perm;     // query i reads tile perm[i] (null: tile i)
 };
 
 template <bool FASTDIV>
@@ -1625,7 +1626,8 @@ __global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
     const bool valid = i < a.n;
     const long nqblk = (a.n + 31) / 32;
     const bool has_blk = (i >> 5) < nqblk;
-    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + (valid ? i : t0) * 64);
+    const long ti = valid ? (a.perm ? (long)a.perm[i] : i) : (a.perm ? (long)a.perm[t0] : t0);
+    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + ti * 64);
     double n2 = 0, h2q[4] = {0, 0, 0, 0}, e2q[4] = {0, 0, 0, 0};
     int bad = 0;
     float rb = 0.0f;
@@ -1827,7 +1829,8 @@ __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut,
     const bool valid = i < a.n;
     const long nqblk = (a.n + 31) / 32;
     const bool has_blk = (i >> 5) < nqblk;
-    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + (valid ? i : t0) * 64) + 8 * H;
+    const long ti = valid ? (a.perm ? (long)a.perm[i] : i) : (a.perm ? (long)a.perm[t0] : t0);
+    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + ti * 64) + 8 * H;
     double nb = 0, h2q[4] = {0, 0, 0, 0}, e2q[4] = {0, 0, 0, 0};  // nb: wave 0 -> (root-box, as float), wave 1 -> n2
     float rb = 0.0f;
     int bad = 0;
@@ -1948,7 +1951,7 @@ __global__ __launch_bounds__(128) void orbit_ft_query2_kernel(FtQueryArgs a) {
 }
 
 int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float *qrows, const float *box,
-                     float *rootbox, hipStream_t stream) {
+                     float *rootbox, hipStream_t stream, const int *perm) {
     OrbitIndex *o = ix->orbit;
     if (orbit_ensure_queries(o, Q)) return -1;
     if (gamma < -1 || gamma > 1) {
@@ -1971,6 +1974,7 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
     fa.box = box;
     fa.rootbox = rootbox;
     fa.xmode = 0;
+    fa.perm = perm;
 #ifdef TILER_EXPERIMENTS
     {
         const char *e = getenv("TILER_FTQ_MODE");  // 1 no Haar, 2 no transform, 3 no norms, 5 no frag stores (timing only)

@@ -102,7 +102,8 @@ int orbit_collect(NNIndex *ix, const int *fb_list, const int *fb_count, int fb_m
                   int *cbuf, int cap, int prev, hipStream_t stream);
 // FrameTiling queries in one kernel: RGB tiles -> Haar descriptors (qrows[Q][192] fp32) + q' fragments + stats
 // (+ rootbox[Q] = annBoxDistance to box[2][192] when box != null)
+// (perm: query i is tile perm[i] of d_rgb; null = identity)
 int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float *qrows, const float *box,
-                     float *rootbox, hipStream_t stream);
+                     float *rootbox, hipStream_t stream, const int *perm = nullptr);
 
 }  // namespace tiler

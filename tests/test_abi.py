@@ -69,3 +69,21 @@ def test_shipped_library_ignores_experiment_switches():
     if os.path.exists(exp):  # the experiment build carries the switches and their kernel variants
         eblob = open(exp, "rb").read()
         assert all(s.encode() in eblob for s in EXPERIMENT_SWITCHES)
+
+
+def test_search_stats_layout_matches_header(tmp_path):
+    """tiler_search_stats is filled whole by the library: the ctypes mirror must have the header's size and field
+    offsets (a shorter caller struct would be overrun)."""
+    fields = [f[0] for f in _lib.SearchStats._fields_]
+    src = tmp_path / "stats.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "tiler_ann.h"\nint main(void) {\n'
+                   '  printf("%zu\\n", sizeof(tiler_search_stats));\n' +
+                   "".join(f'  printf("%zu\\n", offsetof(tiler_search_stats, {f}));\n' for f in fields) +
+                   "  return 0;\n}\n")
+    exe = tmp_path / "stats"
+    inc = os.path.join(os.path.dirname(_lib.HEADER_PATH))
+    subprocess.run(["gcc", "-I", inc, str(src), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(_lib.SearchStats)
+    for f, off in zip(fields, vals[1:]):
+        assert getattr(_lib.SearchStats, f).offset == off, f

@@ -178,13 +178,16 @@ def test_frame_tiling_flat_tiles_last_matches_small_batches(gpu):
     0 only, nn_frame_tiling_dev / orbit_search); per-frame batches below that size keep the tile order.  Both must
     give the same tilemap items and errors bit for bit (the per-frame path is checked against the oracle above)."""
     from tiler_amd.frame_tiling import KeyframeTiler
-    wl = synth.make_workload(23, 320, 240, 8, 1000, n_palettes=16)
+    # >= 1,024 blocks of 32 mirror groups: the grouping is enabled from that shortlist length (nn_frame_tiling_dev)
+    wl = synth.make_workload(23, 320, 240, 8, 40000, n_palettes=16)
     kt = KeyframeTiler(wl.tiles, wl.thm, wl.tvm, wl.palettes, wl.ds)
+    assert kt.kdt.stats()["orbit_groups"] >= 1024 * 32
     frames = np.stack([wl.frame_rgb[f] for f in range(wl.frames)])
     Q = frames.shape[1]
     flat = (frames.reshape(-1, 64) == frames.reshape(-1, 64)[:, :1]).all(axis=1)
     assert frames.shape[0] * Q >= 8192 and 0 < flat.sum() < flat.size
     big = kt.do_frame_tiling(frames.reshape(-1, 64))
+    assert kt.kdt.stats()["flat_queries"] > 0  # the flat tiles' workgroups ran
     for f in range(wl.frames):
         g = kt.do_frame_tiling(frames[f])
         for a, b in zip(g[:4], big[:4]):

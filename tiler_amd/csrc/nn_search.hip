@@ -1446,7 +1446,10 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
 #else
         constexpr bool noflat = false;
 #endif
-        if (!noflat && Q >= 8192) {  // flat tiles last (see ft_flat_flag_kernel)
+        // flat tiles last (see ft_flat_flag_kernel) when the shortlist is long enough to repay the ~0.1 ms of
+        // grouping: C3 (2,048 group blocks) -0.6..-1.1 ms per step; C2 (512 blocks, whose ragged last round the mixed
+        // split already fills) +0.08 ms (profiles/flat_c2_ab.sh), so not there
+        if (!noflat && Q >= 8192 && ((const OrbitIndex *)ix->orbit)->gblk >= 1024) {
             const int nb = (Q + 255) / 256;
             if ((size_t)Q > s.cap_flat) {
                 hipFree(s.fperm);

@@ -20,6 +20,10 @@
  *   - split = TILER_SPLIT_INDEX_ORDER (100): no tree, equal distances resolve to the lowest index;
  *     the other ANN split rules (1..5, never used by the reference) are rejected;
  *   - eps > 0 is accepted and ignored: the exact answer satisfies every eps bound;
+ *   - ann_kdtree_pri_search returns ann_kdtree_search's answer: the same exact minimum distance, but among
+ *     EQUAL distances annkSearch's first-found candidate, not annkPriSearch's (ANN's priority search visits the
+ *     leaves by increasing box distance, so its tie order can differ).  The reference declares it
+ *     (extern.pas:66) and never calls it; its tie order is not reproduced;
  *   - the dataset rows are copied to device memory at create (ANN borrows pa until destroy);
  *   - no process abort: errors return -1 (or NULL) and tiler_last_error() explains;
  *   - every entry point is thread-safe; concurrent calls on one handle are serialised.
@@ -64,8 +68,10 @@ int ann_kdtree_search_batch_dev(ann_kdtree *akd, const float *d_q, int nq, int k
 /* Search statistics of the last call on this handle (shortlist sizes, exact fallbacks). */
 typedef struct {
     int64_t queries;
-    int64_t fallback_queries;   /* tier 2: shortlist overflowed -> MFMA collect pass + exact rescoring */
-    int64_t exhaustive_queries; /* tier 3: exhaustive reference-order scan (k > 8, bad data, collect overflow) */
+    int64_t fallback_queries;   /* tier 2: shortlist overflowed -> MFMA collect pass + exact rescoring (any number of
+                                   queries; the mirror-orbit tier 2 has no per-query candidate limit) */
+    int64_t exhaustive_queries; /* tier 3: exhaustive reference-order scan (k > 8, non-finite / fp16-overflowing data,
+                                   and > 1024 candidates for a query of the generic, non-orbit tier 2) */
     int32_t exact_integer;    /* 1 when the dataset is small integers: MFMA keys are exact */
     int32_t splits;           /* candidate splits used by the last launch */
     int64_t orbit_groups;     /* mirror orbits found in the dataset (0: mirror-orbit path unavailable) */
@@ -78,8 +84,10 @@ typedef struct {
     int32_t kd_levels;        /* levels of the kd-tree build */
     double kd_build_ms;       /* kd-tree build time at create */
     int64_t kd_replayed;      /* queries of the last search replayed exactly (ANN's pruning not vouched for) */
-    int64_t flat_queries;     /* queries of the last FrameTiling call whose shortlist ran isotypic block 0 only (flat
-                                 tiles, grouped last: 3 k-steps per candidate block instead of orbit_ksteps / blocks) */
+    int64_t flat_queries;     /* queries of the last FrameTiling call in shortlist workgroups made of flat tiles only
+                                 (flat tiles are grouped last; such a workgroup runs isotypic block 0 only: 3 k-steps
+                                 per candidate block instead of orbit_ksteps / blocks).  Flat tiles that share a
+                                 workgroup with non-flat ones are not counted.  0 for searches without flat grouping. */
 } tiler_search_stats;
 int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
 /* Leaf position of every dataset point in ANN's kd-tree (the order of its depth-first scan with every near
@@ -122,7 +130,8 @@ int tiler_ft_set_maps(ann_kdtree *akd, const int32_t *tr_tile, const int32_t *tr
  * tilemap item {GlobalTileIndex, PalIdx, HMirror = attr&1, VMirror = attr&2} + err. Host buffers. */
 int tiler_frame_tiling(ann_kdtree *akd, const int32_t *rgb, int Q, int use_wavelets, int gamma, int32_t *out_tile,
                        int32_t *out_pal, uint8_t *out_hm, uint8_t *out_vm, float *out_err);
-/* Same, every buffer in HBM, asynchronous on stream (the benchmarked path). */
+/* Same, every buffer in HBM, asynchronous on stream (the benchmarked path): no host synchronisation inside, every
+ * data-dependent count (flat tiles, tier-2 / tier-3 queries) stays on the device. */
 int tiler_frame_tiling_dev(ann_kdtree *akd, const int32_t *d_rgb, int Q, int use_wavelets, int gamma,
                            int32_t *d_tile, int32_t *d_pal, uint8_t *d_hm, uint8_t *d_vm, float *d_err, void *stream);
 

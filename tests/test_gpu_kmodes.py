@@ -73,13 +73,15 @@ def _oracle_threads():
         return 1
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(1200)
 def test_kmodes_c4_full_batch(gpu, oracle):
     """BASELINE C4 at full size: 1,048,576 tiles (64k prototypes, 10 % perturbation, Zipf(1.1) bins over 128
     palettes, desired 65,536) through ONE tiler_kmodes_batch + medoid batch (the DoGlobalTiling call shape,
-    main.pas:4339), then every bin of <= 10,000 rows (111 bins) and the smallest bin of >= 50,000 rows checked
-    against the CPU restatement (labels, centroids, iterations, cost, medoids; the oracle's distance loops on
-    16 host threads like the reference's TKModes threads)."""
+    main.pas:4339), then every bin of <= 10,000 rows (111 bins) and the FOUR LARGEST bins (236,865 / 110,181 /
+    70,453 / 51,715 rows, K = 5,035 / 3,222 / 2,477 / 2,064: the critical path, where the grouped concurrent moves
+    and the split assignment carry the most weight, kmodes.pas:845-915) checked against the CPU restatement
+    (labels, centroids, iterations, cost, medoids; the oracle's distance loops on 16 host threads like the
+    reference's TKModes threads; about two minutes of host time)."""
     from tiler_amd import global_tiling as gt
     from tiler_amd import synth
     tiles, dith = synth.globaltiling_workload(4, 1 << 20, n_palettes=128)
@@ -94,8 +96,9 @@ def test_kmodes_c4_full_batch(gpu, oracle):
     g_labels, g_cent, g_it, g_cost = compute_kmodes_batch(X_all, off, ks, st)
     g_med, g_cnt = medoids_batch(X_all, off, ks, g_labels, g_cent)
     koff = np.concatenate([[0], np.cumsum(ks)])
-    big = min((b for b in range(len(run)) if off[b + 1] - off[b] >= 50000), key=lambda b: off[b + 1] - off[b])
-    check = [b for b in range(len(run)) if off[b + 1] - off[b] <= 10000] + [big]
+    largest = sorted(range(len(run)), key=lambda b: -(off[b + 1] - off[b]))[:4]
+    assert off[largest[0] + 1] - off[largest[0]] == 236865 and ks[largest[0]] == 5035
+    check = [b for b in range(len(run)) if off[b + 1] - off[b] <= 10000] + largest
     assert len(check) >= 100
     th = _oracle_threads()
     for b in check:
@@ -113,3 +116,43 @@ def test_kmodes_c4_full_batch(gpu, oracle):
             mem = np.nonzero(ol == j)[0]
             i, _ = oracle.km_get_min(X[mem], oc[j])  # GetMinMatchingDissim: ties -> last member
             assert medoid[j] == mem[i], (p, j)
+
+
+@pytest.mark.timeout(1200)
+def test_kmodes_c5_shaped_batch(gpu, oracle):
+    """A C5-shaped GlobalTiling (BASELINE C5: the reduced tileset is 256k tiles): 4,194,304 tiles from 262,144
+    prototypes over 128 Zipf bins, desired 262,144 clusters, in ONE tiler_kmodes_batch + medoid batch.  Every bin of
+    <= 10,000 rows is checked against the restatement; for all bins the labels are in range, each non-empty
+    cluster's medoid is one of its members, and the reported cost is the sum of the final snapshot distances that
+    the labels imply (recomputed on the host for the checked bins)."""
+    from tiler_amd import global_tiling as gt
+    from tiler_amd import synth
+    from tiler_amd.kmodes import compute_kmodes_batch, medoids_batch
+    tiles, dith = synth.globaltiling_workload(5, 1 << 22, protos=1 << 18, n_palettes=128)
+    plan = gt.plan_global_tiling(tiles, dith, 128, 1 << 18)
+    run = list(plan.run)
+    X_all = np.ascontiguousarray(np.concatenate([plan.lines[plan.bins[p]] for p in run]))
+    off = np.concatenate([[0], np.cumsum([plan.bins[p].size for p in run])]).astype(np.int32)
+    ks = np.array([plan.k_per_bin[p] for p in run], np.int32)
+    st = np.array([plan.starts[p] for p in run], np.int32)
+    assert 250000 <= int(ks.sum()) <= 270000, int(ks.sum())
+    g_labels, g_cent, g_it, g_cost = compute_kmodes_batch(X_all, off, ks, st)
+    g_med, g_cnt = medoids_batch(X_all, off, ks, g_labels, g_cent)
+    koff = np.concatenate([[0], np.cumsum(ks)])
+    for b in range(len(run)):
+        lab = g_labels[off[b]:off[b + 1]]
+        assert lab.min() >= 0 and lab.max() < ks[b], b
+        cnt = g_cnt[koff[b]:koff[b + 1]]
+        assert np.array_equal(cnt, np.bincount(lab, minlength=int(ks[b]))), b
+        med = g_med[koff[b]:koff[b + 1]]
+        nz = cnt > 0
+        assert np.array_equal(lab[med[nz]], np.nonzero(nz)[0]), b  # each medoid belongs to its cluster
+    th = _oracle_threads()
+    small = [b for b in range(len(run)) if off[b + 1] - off[b] <= 10000]
+    assert len(small) >= 60
+    for b in small:
+        p = run[b]
+        ol, oc, oi, ocost = oracle.kmodes(plan.lines[plan.bins[p]], int(ks[b]), plan.starts[p], threads=th)
+        assert (int(g_it[b]), int(g_cost[b])) == (oi, ocost), p
+        assert np.array_equal(g_labels[off[b]:off[b + 1]], ol), p
+        assert np.array_equal(g_cent[koff[b]:koff[b + 1]], oc), p

@@ -72,8 +72,9 @@ def test_smooth_single_frame_is_identity(gpu):
 @pytest.mark.timeout(600)
 def test_smooth_c3_size(gpu, oracle):
     """Smooth at the C3 step's size: one keyframe of 24 frames x 32,400 positions (1080p), a 4,096-tile set with
-    near-duplicate twins, 128 palettes, the default strength: items and flags bit-exact against the restatement
-    (which computes every compared descriptor; about a minute on the box's host)."""
+    near-duplicate twins, 128 palettes, strength 0.04 (twice the default, so the one-pixel twins merge too): items
+    and flags bit-exact against the restatement (which computes every compared descriptor; about a minute on the
+    box's host).  The default 0.02 is checked at C5 size below."""
     rng = np.random.default_rng(2402)
     F, Q, T, P = 24, 32400, 4096, 128
     palpix = rng.integers(0, 16, (T, 64)).astype(np.uint8)
@@ -88,3 +89,27 @@ def test_smooth_c3_size(gpu, oracle):
     for a, b in zip(g, o):
         assert np.array_equal(a, b)
     assert g[4].sum() > 0
+
+
+@pytest.mark.timeout(900)
+def test_smooth_c5_size_default_strength(gpu, oracle):
+    """BASELINE C5's Smooth: one 4K keyframe of 24 frames x 129,600 positions (DoTemporalSmoothing main.pas:4071-4119,
+    positions independent, frames of one keyframe), 65,536 tiles with near-duplicate twins, 128 palettes whose first
+    two differ by one RGB step, the DEFAULT strength 0.02.  The whole keyframe runs in one GPU call; 6,000 positions
+    (columns of the [F][Q] maps: each column is its own chain) are checked bit for bit against the restatement."""
+    rng = np.random.default_rng(2405)
+    F, Q, T, P = 24, 480 * 270, 65536, 128
+    palpix = rng.integers(0, 16, (T, 64)).astype(np.uint8)
+    palpix[T // 2:] = palpix[:T // 2]
+    palpix[T // 2:, 7] = (palpix[T // 2:, 7] + 1) % 16
+    pals = synth.palettes(rng, P)
+    pals[1] = pals[0] + 1
+    tile, pal, hm, vm = _tilemaps(rng, F, Q, T, P)
+    sm = np.zeros((F, Q), np.uint8)
+    g = smooth_keyframe(tile, pal, hm, vm, sm, palpix, pals, 0.02)
+    cols = np.sort(rng.choice(Q, 6000, replace=False))
+    sub = lambda a: np.ascontiguousarray(a[:, cols])  # noqa: E731
+    o = oracle.smooth(sub(tile), sub(pal), sub(hm), sub(vm), sub(sm), palpix, pals, 0.02)
+    for a, b in zip(g, o):
+        assert np.array_equal(sub(np.asarray(a)), b)
+    assert g[4].sum() > 0 and sub(np.asarray(g[4])).sum() > 0  # the default strength does merge here

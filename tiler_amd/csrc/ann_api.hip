@@ -391,6 +391,8 @@ int ann_kdtree_get_stats(ann_kdtree *t, tiler_search_stats *out) {
         return -1;
     }
     std::lock_guard<std::mutex> lk(t->ix->mu);
+    // everything below was written by the last search on ITS stream (the caller's, for the _dev entry points)
+    if (t->ix->done_event) TILER_HIP_CHECK(hipEventSynchronize(t->ix->done_event));
     out->queries = t->ix->last_queries;
     out->fallback_queries = t->ix->last_splits > 0 ? t->ix->h_fb_count[0] : 0;
     out->exhaustive_queries = t->ix->last_splits > 0 ? t->ix->h_fb_count[1] : t->ix->last_fallback;
@@ -407,10 +409,15 @@ int ann_kdtree_get_stats(ann_kdtree *t, tiler_search_stats *out) {
     out->kd_levels = t->ix->kd ? t->ix->kd->levels : 0;
     out->kd_build_ms = t->ix->kd ? t->ix->kd->build_ms : 0.0;
     out->kd_replayed = 0;
-    out->flat_queries = t->ix->last_flat_queries;
+    out->flat_queries = 0;
+    if (const NNIndex *ix = t->ix; ix->last_flat_dev) {  // queries in all-flat shortlist workgroups
+        int others = 0;
+        TILER_HIP_CHECK(hipMemcpy(&others, ix->last_flat_dev, sizeof(int), hipMemcpyDeviceToHost));
+        const long wf0 = std::min(ix->last_flat_wgs, (others + ix->last_flat_qpw - 1) / ix->last_flat_qpw);
+        out->flat_queries = wf0 < ix->last_flat_wgs ? ix->last_flat_nq - wf0 * ix->last_flat_qpw : 0;
+    }
     if (t->ix->kd && t->ix->scratch.kd_count) {
         int c = 0;
-        TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
         TILER_HIP_CHECK(hipMemcpy(&c, t->ix->scratch.kd_count, sizeof(int), hipMemcpyDeviceToHost));
         out->kd_replayed = c;
     }

@@ -45,6 +45,55 @@ __device__ __forceinline__ bool kd_before(const KdOrder *op, const float *__rest
     return op ? kd_before_tree(op, q, a, b) : (unsigned)a < (unsigned)b;
 }
 
+// kd_before as a 32-bit key: the root-to-leaf path of candidate c's leaf, one bit per internal node (0 = q's near
+// child), then the position inside the bucket, left-aligned.  The paths of two leaves first differ at their lowest
+// common node, so unsigned comparison of the keys is exactly kd_before (bs = 1: ceil(log2 n) <= 31 bits; in general
+// the path and the bucket offset need <= ceil(log2 n) + 1 <= 32 bits for n < 2^31).  op == nullptr: the index.
+// Tier 2 (orbit.hip) packs (distance bits, this key) into one u64 and takes an atomic minimum.
+static __device__ __attribute__((noinline, unused)) unsigned kd_rank(const KdOrder *__restrict__ op, const float *__restrict__ q,
+                                                             int c) {
+    if (!op) return (unsigned)c;
+    const KdOrder &o = *op;
+    const int p = o.pos[c];
+    unsigned bits = 0;
+    int nb = 0, s = 0, e = o.n;
+    while (e - s > o.bs) {
+        const int m = s + ((e - s) >> 1);
+        const bool lo_first = (q[o.cd[m]] - o.cv[m]) < 0.0f, in_lo = p < m;
+        bits = (bits << 1) | (in_lo == lo_first ? 0u : 1u);
+        nb++;
+        if (in_lo)
+            e = m;
+        else
+            s = m;
+    }
+    const int bb = o.bs > 1 ? 32 - __builtin_clz((unsigned)(o.bs - 1)) : 0;  // ceil(log2 bs)
+    bits = (bb ? (bits << bb) : bits) | (unsigned)(p - s);
+    nb += bb;
+    return nb == 0 ? 0u : bits << (32 - nb);
+}
+
+// the candidate whose kd_rank is r (same walk, following the key's bits)
+static __device__ __attribute__((noinline, unused)) int kd_unrank(const KdOrder *__restrict__ op, const float *__restrict__ q,
+                                                          unsigned r) {
+    if (!op) return (int)r;
+    const KdOrder &o = *op;
+    int s = 0, e = o.n, used = 0;
+    while (e - s > o.bs) {
+        const int m = s + ((e - s) >> 1);
+        const bool lo_first = (q[o.cd[m]] - o.cv[m]) < 0.0f;
+        const bool far = (r >> (31 - used)) & 1u;
+        used++;
+        if (lo_first != far)  // near child LO and bit 0, or far child LO and bit 1
+            e = m;
+        else
+            s = m;
+    }
+    const int bb = o.bs > 1 ? 32 - __builtin_clz((unsigned)(o.bs - 1)) : 0;
+    const int off = bb ? (int)((r << used) >> (32 - bb)) : 0;
+    return o.pidx[s + off];
+}
+
 // (dist, kd order) lexicographic "less"
 __device__ __forceinline__ bool kd_less(const KdOrder *op, const float *__restrict__ q, float da, int a, float db,
                                         int b) {

@@ -467,18 +467,19 @@ template <int S, int CB>
 __global__ __launch_bounds__(256, 2) void nn_collect_kernel(const half8 *__restrict__ cfrag,
                                                             const float *__restrict__ cnc, int nblk,
                                                             const half8 *__restrict__ qfrag, const int *fb_list,
-                                                            const int *fb_count, int fb_max, const float *thr,
-                                                            int blk_per_split, int perm, int *ccnt, int *cbuf,
-                                                            int cap) {
+                                                            const int *fb_count, int jbase, int chunk,
+                                                            const float *thr, int blk_per_split, int perm, int *ccnt,
+                                                            int *cbuf, int cap) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * S * 1024;
     constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
     constexpr int PER_T = CB * S * 64 / 256;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int count = min(*fb_count, fb_max);
+    const int count = min(*fb_count - jbase, chunk);  // this chunk's slots (local index j = slot - jbase)
     const int b_begin = blockIdx.y * blk_per_split;
     const int b_end = min(nblk, b_begin + blk_per_split);
     const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    fb_list += jbase;
     for (int g = blockIdx.x; g * 256 < count; g += gridDim.x) {
         half8 bq0[S], bq1[S];
         int j0 = (g * 4 + w) * 64 + (lane & 31), j1 = j0 + 32;
@@ -697,12 +698,14 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
 // One wave per compact query; a buffer that overflowed its capacity sends the query to tier 3.
 // ------------------------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void nn_rescore2_kernel(RescoreArgs a) {
+__global__ __launch_bounds__(256) void nn_rescore2_kernel(RescoreArgs a, int jbase, int chunk) {
     const int lane = threadIdx.x & 63;
-    const int count = min(*a.fb_count, a.fb_max);
+    const int count = min(*a.fb_count - jbase, chunk);
     for (long j = (long)blockIdx.x * 4 + (threadIdx.x >> 6); j < count; j += (long)gridDim.x * 4) {
-        const long q = a.fb_list[j];
-        const int n = a.ccnt[j];
+        const long q = a.fb_list[jbase + j];
+        int n = 0;
+        if (lane == 0) n = atomicExch(a.ccnt + j, 0);  // read and clean for the next chunk
+        n = __shfl(n, 0, 64);
         if (n > a.cap) {
             if (lane == 0) a.ex_list[atomicAdd(a.ex_count, 1)] = (int)q;
             continue;
@@ -966,6 +969,7 @@ void nn_index_destroy(NNIndex *ix) {
     hipFree(s.kd_count);
     hipFree(s.kd_rootbox);
     hipFree(s.kd_done);
+    hipFree(s.t2best);
     hipFree(s.fperm);
     hipFree(s.fbcnt);
     hipFree(s.fcnt);
@@ -977,11 +981,12 @@ void nn_index_destroy(NNIndex *ix) {
     hipFree(s.fhm);
     hipFree(s.fvm);
     hipHostFree(ix->h_fb_count);
+    if (ix->done_event) hipEventDestroy(ix->done_event);
     delete ix;
 }
 
-static constexpr int TIER2_MAX = 65536;  // queries per call in the tier-2 collect pass
-static constexpr int TIER2_CAP = 1024;   // collected candidates per tier-2 query
+static constexpr int TIER2_MAX = 65536;  // generic tier 2: queries per collect chunk (every tier-2 query has a slot)
+static constexpr int TIER2_CAP = 1024;   // generic tier 2: collected candidates per query (beyond: tier 3)
 
 static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
     SearchScratch &s = ix->scratch;
@@ -996,6 +1001,14 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         hipFree(s.kd_list);
         hipFree(s.kd_rootbox);
         hipFree(s.kd_done);
+        hipFree(s.t2best);
+        s.qfrag = s.qfrag16 = nullptr;
+        s.qstat = nullptr;
+        s.fb_list = s.fb_count = s.ex_list = s.kd_list = nullptr;
+        s.thr = s.kd_rootbox = nullptr;
+        s.kd_done = nullptr;
+        s.t2best = nullptr;
+        s.cap_q = 0;
         const long nqblk = (nq + 31) / 32 + 2;
         TILER_HIP_CHECK(hipMalloc(&s.qfrag, (size_t)nqblk * 16 * 64 * 16));
         TILER_HIP_CHECK(hipMalloc(&s.qfrag16, (size_t)((nq + 15) / 16 + 2) * 8 * 64 * 16));
@@ -1007,6 +1020,7 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         TILER_HIP_CHECK(hipMalloc((void **)&s.kd_list, (size_t)nq * sizeof(int)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.kd_rootbox, (size_t)nq * sizeof(float)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.kd_done, (size_t)nq));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.t2best, (size_t)nq * sizeof(unsigned long long)));
         s.cap_q = nq;
     }
     if (!s.kd_count) TILER_HIP_CHECK(hipMalloc((void **)&s.kd_count, 16));
@@ -1017,6 +1031,9 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
     if ((size_t)nkeys > s.cap_keys) {
         hipFree(s.key);
         hipFree(s.idx);
+        s.key = nullptr;
+        s.idx = nullptr;
+        s.cap_keys = 0;
         TILER_HIP_CHECK(hipMalloc((void **)&s.key, (size_t)nkeys * sizeof(float)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.idx, (size_t)nkeys * sizeof(int)));
         s.cap_keys = nkeys;
@@ -1087,30 +1104,27 @@ static int dispatch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
 }
 
 template <int S, int CB>
-static void launch_collect(NNIndex *ix, int nq, hipStream_t stream) {
+static void launch_collect(NNIndex *ix, int nq, int jbase, hipStream_t stream) {
     // fixed grid (the overflow count stays on the device): many short splits so that a few hundred
-    // overflowed queries still spread over the whole chip
+    // overflowed queries still spread over the whole chip; grid.x strides over the chunk's query groups of 256,
+    // so 2 x 256 resident-sized workgroups serve any count alike
     const int nsplit = std::min(ix->nblk, 256);
     const int bps = (ix->nblk + nsplit - 1) / nsplit;
-    // grid.x = query groups of 256; the kernel strides over the device-side count, so any grid is correct.
-    // Idle workgroups are not free (about 0.18 us each to dispatch and retire at this LDS size), so the
-    // grid follows the previous call's tier-2 count (h_fb_count, copied back at the end of each search)
-    const int prev = ix->h_fb_count ? std::max(0, ix->h_fb_count[0]) : TIER2_MAX;
-    const int groups = std::max(1, std::min({32, (std::min(nq, TIER2_MAX) + 255) / 256, (prev + prev / 4 + 255) / 256 + 1}));
+    const int groups = std::min(2, (std::min(nq - jbase, TIER2_MAX) + 255) / 256);
     const size_t lds = 2 * (CB * S * 1024 + CB * 128);
     SearchScratch &s = ix->scratch;
     KTimer tm("nn_collect", stream);
     hipLaunchKernelGGL((nn_collect_kernel<S, CB>), dim3(groups, (ix->nblk + bps - 1) / bps), dim3(256), lds, stream,
                        (const half8 *)ix->d_frag, ix->d_nc, ix->nblk, (const half8 *)s.qfrag, s.fb_list, s.fb_count,
-                       TIER2_MAX, s.thr, bps, ix->perm, s.ccnt, s.cbuf, TIER2_CAP);
+                       jbase, TIER2_MAX, s.thr, bps, ix->perm, s.ccnt, s.cbuf, TIER2_CAP);
 }
 
-static int dispatch_collect(NNIndex *ix, int nq, hipStream_t stream) {
+static int dispatch_collect(NNIndex *ix, int nq, int jbase, hipStream_t stream) {
     switch (ix->S) {
-        case 4: launch_collect<4, 6>(ix, nq, stream); break;
-        case 8: launch_collect<8, 3>(ix, nq, stream); break;
-        case 12: launch_collect<12, 2>(ix, nq, stream); break;
-        case 16: launch_collect<16, 2>(ix, nq, stream); break;
+        case 4: launch_collect<4, 6>(ix, nq, jbase, stream); break;
+        case 8: launch_collect<8, 3>(ix, nq, jbase, stream); break;
+        case 12: launch_collect<12, 2>(ix, nq, jbase, stream); break;
+        case 16: launch_collect<16, 2>(ix, nq, jbase, stream); break;
         default: set_error("nn: unsupported fragment depth"); return -1;
     }
     TILER_HIP_CHECK(hipGetLastError());
@@ -1137,7 +1151,7 @@ static int launch_exact(RescoreArgs ra, int list_n, int grid, hipStream_t stream
     return 0;
 }
 
-static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream, bool orbit);
+static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream, const OrbitTail *orbit);
 static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream,
                        bool orbit_prepared);
 
@@ -1173,7 +1187,9 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         ra.m_vm = maps->vm;
     }
     ix->last_queries = nq;
+    ix->last_flat_dev = nullptr;
     SearchScratch &s = ix->scratch;
+    if (!ix->done_event) TILER_HIP_CHECK(hipEventCreateWithFlags(&ix->done_event, hipEventDisableTiming));
     if (ix->kd) {  // ANN's tie order: the pruning check needs every query's box distance and a clean slate
         if (ensure_scratch(ix, nq, 0)) return -1;
         if (!rootbox_ready && kd_root_boxes(ix->kd, d_q, nq, s.kd_rootbox, stream)) return -1;
@@ -1181,7 +1197,10 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         TILER_HIP_CHECK(hipMemsetAsync(s.kd_count, 0, sizeof(int), stream));
     }
     if (search_core(ix, ra, d_q, nq, k, stream, orbit_prepared)) return -1;
-    if (!ix->kd) return 0;
+    if (!ix->kd) {
+        TILER_HIP_CHECK(hipEventRecord(ix->done_event, stream));
+        return 0;
+    }
     // ANN's box pruning along every result's path (queries the pair pass did not already check); the rare query
     // it cannot vouch for is replayed exactly
     KdFixArgs fa{ix->d_rows, d_q, nq, k, d_idx, d_err};
@@ -1196,7 +1215,9 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     fa.m_vm = ra.m_vm;
     fa.list = s.kd_list;
     fa.count = s.kd_count;
-    return kd_verify_and_replay(ix->kd, fa, stream);
+    if (kd_verify_and_replay(ix->kd, fa, stream)) return -1;
+    TILER_HIP_CHECK(hipEventRecord(ix->done_event, stream));  // what tiler_search_stats reads is final here
+    return 0;
 }
 
 static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream,
@@ -1227,16 +1248,16 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     TILER_HIP_CHECK(hipMemsetAsync(s.fb_count, 0, 16, stream));
     ix->last_orbit = 0;
     if (k == 1 && ix->orbit) {
-        // mirror-orbit path (orbit.hip); generic query fragments are built for the tier-2 queries only
-        TILER_HIP_CHECK(hipMemsetAsync(s.ccnt, 0, (size_t)std::min(nq, TIER2_MAX) * sizeof(int), stream));
+        // mirror-orbit path (orbit.hip): tier 2 lists every query the rescore cannot settle (fb_max = nq)
         OrbitTail t{};
         t.fb_list = s.fb_list;
         t.fb_count = s.fb_count;
         t.ex_list = s.ex_list;
         t.ex_count = s.fb_count + 1;
-        t.fb_max = TIER2_MAX;
+        t.fb_max = nq;
         t.thr = s.thr;
-        t.flat_from = ix->flat_from;
+        t.t2_best = s.t2best;
+        t.flat_cnt = ix->flat_cnt;
         t.out_idx = ra.out_idx;
         t.out_err = ra.out_err;
         t.tr_tile = ra.tr_tile;
@@ -1259,11 +1280,8 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
         ra.ex_list = s.ex_list;
         ra.ex_count = s.fb_count + 1;
         ra.thr = s.thr;
-        ra.ccnt = s.ccnt;
-        ra.cbuf = s.cbuf;
-        ra.cap = TIER2_CAP;
-        ra.fb_max = TIER2_MAX;
-        return search_tail(ix, ra, nq, stream, true);
+        ra.fb_max = nq;
+        return search_tail(ix, ra, nq, stream, &t);
     }
     // queries -> fragments (same layout and scale as the dataset)
     const long nqblk = (nq + 31) / 32;
@@ -1307,34 +1325,35 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     ra.ccnt = s.ccnt;
     ra.cbuf = s.cbuf;
     ra.cap = TIER2_CAP;
-    ra.fb_max = TIER2_MAX;
+    ra.fb_max = nq;  // every overflowed query gets a tier-2 slot; the collect runs in chunks of TIER2_MAX
     TILER_HIP_CHECK(hipMemsetAsync(s.ccnt, 0, (size_t)std::min(nq, TIER2_MAX) * sizeof(int), stream));
     {
         KTimer t_rs("nn_rescore", stream);
         hipLaunchKernelGGL(nn_rescore_kernel, dim3((nq + 3) / 4), dim3(256), 0, stream, ra);
     }
     TILER_HIP_CHECK(hipGetLastError());
-    return search_tail(ix, ra, nq, stream, false);
+    return search_tail(ix, ra, nq, stream, nullptr);
 }
 
-// tiers 2 and 3 read their device-side counts: fixed grids, no host round trip
-static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream, bool orbit) {
+// tiers 2 and 3 read their device-side counts: fixed grids, no host round trip.  Every query the rescore cannot
+// settle has a tier-2 slot whatever their number: the orbit tier 2 has no per-query buffer to overflow, the generic
+// one runs its slots in chunks of TIER2_MAX (a chunk past the device count exits at once).  Tier 3, the exhaustive
+// scan, is left to non-finite / fp16-overflowing queries (and generic buffer overflows); its grid fills the chip.
+static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream, const OrbitTail *orbit) {
     SearchScratch &s = ix->scratch;
     if (orbit) {
-        const int prev = ix->h_fb_count ? std::max(0, ix->h_fb_count[0]) : TIER2_MAX;
-        if (orbit_collect(ix, s.fb_list, s.fb_count, TIER2_MAX, s.thr, s.ccnt, s.cbuf, TIER2_CAP,
-                          std::min(prev, std::min(nq, TIER2_MAX)), stream))
-            return -1;
-    } else if (dispatch_collect(ix, nq, stream)) {
-        return -1;
+        if (orbit_tier2(ix, ra.q, *orbit, nq, stream)) return -1;
+    } else {
+        for (int jbase = 0; jbase < nq; jbase += TIER2_MAX) {
+            if (dispatch_collect(ix, nq, jbase, stream)) return -1;
+            KTimer t_r2("nn_rescore2", stream);
+            hipLaunchKernelGGL(nn_rescore2_kernel,
+                               dim3((unsigned)std::min(1024, (std::min(nq - jbase, TIER2_MAX) + 3) / 4)), dim3(256), 0,
+                               stream, ra, jbase, TIER2_MAX);
+            TILER_HIP_CHECK(hipGetLastError());
+        }
     }
-    {
-        KTimer t_r2("nn_rescore2", stream);
-        hipLaunchKernelGGL(nn_rescore2_kernel, dim3((unsigned)std::min(1024, (std::min(nq, TIER2_MAX) + 3) / 4)),
-                           dim3(256), 0, stream, ra);
-    }
-    TILER_HIP_CHECK(hipGetLastError());
-    if (launch_exact(ra, 0, std::min(nq, 512), stream)) return -1;
+    if (launch_exact(ra, 0, std::min(nq, 1024), stream)) return -1;
     TILER_HIP_CHECK(hipMemcpyAsync(ix->h_fb_count, s.fb_count, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
     return 0;
 }
@@ -1435,6 +1454,8 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
     SearchScratch &s = ix->scratch;
     if ((size_t)Q > s.cap_rows) {
         hipFree(s.qrows);
+        s.qrows = nullptr;
+        s.cap_rows = 0;
         TILER_HIP_CHECK(hipMalloc((void **)&s.qrows, (size_t)Q * 192 * sizeof(float)));
         s.cap_rows = Q;
     }
@@ -1461,6 +1482,11 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
                 hipFree(s.fpal);
                 hipFree(s.fhm);
                 hipFree(s.fvm);
+                s.fperm = s.fbcnt = s.fidx = nullptr;  // a failed allocation below leaves nothing dangling
+                s.fflag = s.fhm = s.fvm = nullptr;
+                s.ferr = nullptr;
+                s.ftile = s.fpal = nullptr;
+                s.cap_flat = 0;
                 if (!s.fcnt) TILER_HIP_CHECK(hipMalloc((void **)&s.fcnt, sizeof(int)));
                 TILER_HIP_CHECK(hipMalloc((void **)&s.fperm, (size_t)Q * sizeof(int)));
                 TILER_HIP_CHECK(hipMalloc((void **)&s.fbcnt, (size_t)nb * sizeof(int)));
@@ -1478,16 +1504,13 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
             hipLaunchKernelGGL(ft_flat_place_kernel, dim3(nb), dim3(256), 0, stream, d_rgb, Q, (const uint8_t *)s.fflag,
                                (const int *)s.fbcnt, (const int *)s.fcnt, s.fperm);
             TILER_HIP_CHECK(hipGetLastError());
-            int others = Q;
-            TILER_HIP_CHECK(hipMemcpyAsync(&others, s.fcnt, sizeof(int), hipMemcpyDeviceToHost, stream));
-            TILER_HIP_CHECK(hipStreamSynchronize(stream));
             FtMaps fm;
             if (maps) fm = FtMaps{s.ftile, s.fpal, s.fhm, s.fvm};
-            ix->flat_from = others;
+            ix->flat_cnt = s.fcnt;  // the shortlist reads the non-flat count on the device (no host sync)
             int rc = orbit_ft_queries(ix, d_rgb, Q, gamma, s.qrows, fuse_rb ? ix->kd->d_box : nullptr,
                                       fuse_rb ? s.kd_rootbox : nullptr, stream, s.fperm);
             if (!rc) rc = nn_search_dev(ix, s.qrows, Q, 1, s.fidx, s.ferr, maps ? &fm : nullptr, stream, fuse_rb, true);
-            ix->flat_from = 0x7fffffff;
+            ix->flat_cnt = nullptr;
             if (rc) return -1;
             hipLaunchKernelGGL(ft_unpermute_kernel, dim3(nb), dim3(256), 0, stream, Q, (const int *)s.fperm,
                                (const int *)s.fidx, (const float *)s.ferr, (const int32_t *)s.ftile,

@@ -41,8 +41,9 @@ struct SearchScratch {
     void *qfrag16 = nullptr;  // query fragments, 16-row layout
     float *thr = nullptr;     // tier-2 thresholds [nq]
     int *ex_list = nullptr;   // tier-3 list [nq]
-    int *ccnt = nullptr;      // tier-2 collect counts
-    int *cbuf = nullptr;      // tier-2 collect buffers
+    int *ccnt = nullptr;      // generic tier-2 collect counts [TIER2_MAX] (one chunk)
+    int *cbuf = nullptr;      // generic tier-2 collect buffers [TIER2_MAX][TIER2_CAP]
+    unsigned long long *t2best = nullptr;  // [nq] orbit tier 2: (distance, ANN rank) minimum per tier-2 slot
     int *kd_list = nullptr;   // [nq] queries the ANN pruning check sends to the exact replay
     int *kd_count = nullptr;  // [1]
     float *kd_rootbox = nullptr;  // [nq] annBoxDistance of each query to the kd-tree's enclosing box
@@ -63,7 +64,7 @@ struct NNIndex {
     double maxN = 0, maxH = 0, maxE = 0, max_abs = 0;
     bool exact_int = false;
     int perm = 0;               // 1: candidate rows spread over accumulator lanes (row_perm), float data
-    int flat_from = 0x7fffffff; // FrameTiling call in progress: queries >= flat_from are flat tiles (orbit shortlist)
+    const int *flat_cnt = nullptr; // FrameTiling call in progress: device count of non-flat queries (flat ones last)
     float *d_rows = nullptr;    // [n][d] fp32 (exact rescoring)
     void *d_frag = nullptr;     // [nblk][S][64][8] fp16, MFMA A-operand fragment order
     float *d_nc = nullptr;      // [nblk][32] ||c||^2 in accumulator-row order (+inf on padding rows)
@@ -78,7 +79,11 @@ struct NNIndex {
     std::mutex mu;
     long long last_queries = 0, last_fallback = 0;
     int last_splits = 0;
-    long last_flat_queries = 0; // queries of the last search whose orbit shortlist ran block 0 only
+    // flat_queries of the last search (tiler_search_stats): queries in all-flat shortlist workgroups, computed when the
+    // stats are read from the device count (last_flat_dev) and the launch shape; 0 when the search had no flat grouping
+    const int *last_flat_dev = nullptr;
+    long last_flat_nq = 0, last_flat_qpw = 0, last_flat_wgs = 0;
+    hipEvent_t done_event = nullptr;  // recorded at the end of every search on its stream (stats wait on it)
     int last_orbit = 0;         // 1: the last search ran the mirror-orbit path
     OrbitIndex *orbit = nullptr; // mirror-orbit index (orbit.hip), null when not applicable
     KdTree *kd = nullptr;       // KD_SPLIT_STD tree: ties resolve in ANN's first-found order (null: lowest index)

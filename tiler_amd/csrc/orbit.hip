@@ -675,7 +675,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                                                                          float *__restrict__ out_key,
                                                                          int *__restrict__ out_id, int red_end,
                                                                          const uint8_t *__restrict__ bmask,
-                                                                         int flat_wg0, const uint8_t *__restrict__ bmask0) {
+                                                                         int flat_wg0, const uint8_t *__restrict__ bmask0,
+                                                                         const int *__restrict__ flat_cnt) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * OS * 1024;
     constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
@@ -720,6 +721,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
     // only the nonzero k-steps; [p_begin, b_end): the pipelined full contraction
     // workgroups from flat_wg0 on hold flat query tiles only (q' block 0): every candidate block block-serially with
     // k-steps 0..2, only those streamed
+    // (flat_cnt: the device count of non-flat queries -> first all-flat workgroup; flat_wg0 bounds it)
+    if (flat_cnt) flat_wg0 = min(flat_wg0, (*flat_cnt + NW * QB * 32 - 1) / (NW * QB * 32));
     const bool flat = (int)blockIdx.x >= flat_wg0;
     const int nks = flat ? 3 : OS;
     if (flat) {
@@ -1308,10 +1311,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
             if ((double)tf < Tb) tf = nextafterf(tf, INFINITY);  // an upper bound in fp32
             t.thr[q] = tf;
             const int pidx = atomicAdd(t.fb_count, 1);
-            if (pidx < t.fb_max)
+            if (pidx < t.fb_max) {  // always (fb_max = nq)
                 t.fb_list[pidx] = (int)q;
-            else
+                t.t2_best[pidx] = ~0ull;
+            } else {
                 t.ex_list[atomicAdd(t.ex_count, 1)] = (int)q;
+            }
         }
         return;
     }
@@ -1466,47 +1471,81 @@ __global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a)
 // orbit of the dataset is scored again with the tier-1 contraction -- the same q' fragments (the query's own
 // column of its block), the same seeded d_0 and bound u = d_0 + |d_1| + |d_2| + |d_3| in fp32 -- and where the
 // bound key -2u reaches T_b (rounded up to fp32 by the rescore), the four mirror keys -2 V_m, V_m = sum_x
-// chi_x(m) d_x, are formed by the rescore's own butterfly (orbit_expand4) and every member whose key reaches
-// T_b is appended to the query's tier-2 buffer (duplicate rows included: rescore2 resolves equal distances in
-// ANN's order).  Any candidate that can reach the winner has real key <= T_r and so computed keys <= T_b
-// (DESIGN.md section 4), as in tier 1.  One wave = 32 tier-2 queries (compact), workgroups split the orbit
-// blocks; candidate fragments staged through LDS.  4x fewer MFMAs and bytes than the generic collect.
-static constexpr int OC_CB = 2;  // orbit blocks per LDS stage
-__global__ __launch_bounds__(256, 2) void nn_orbit_collect_kernel(const half8 *__restrict__ cfrag,
-                                                                  const float *__restrict__ cseed, int gblk, long G,
-                                                                  const int *__restrict__ member,
-                                                                  const half8 *__restrict__ qfrag, const int *fb_list,
-                                                                  const int *fb_count, int fb_max,
-                                                                  const float *__restrict__ thr, int blk_per_split,
-                                                                  int *ccnt, int *cbuf, int cap) {
+// chi_x(m) d_x, are formed by the rescore's own butterfly and every member whose key reaches T_b is scored: its
+// reference distance (sequential fp32) and its rank in ANN's visit order for this query (kd_rank) are packed into
+// one u64 and min-reduced into t2_best[j] by an atomic, so (distance, ANN order) picks the winner whatever the number
+// of candidates (duplicate rows included).  Any candidate that can reach the winner has real key <= T_r and so
+// computed keys <= T_b, as in tier 1.  The members are queued per wave in LDS and scored
+// lane-parallel, 64 at a time (the pair pass's idea), so near-tie floods keep every lane busy.  One wave = 32 tier-2
+// queries (compact), workgroups split the orbit blocks; candidate fragments staged through LDS by LDS-DMA.
+static constexpr int OC_CB = 2;    // orbit blocks per LDS stage
+static constexpr int OC_XQ = 512;  // per-wave queue of (tier-2 slot, candidate) awaiting the exact score
+struct OrbitCollectArgs {
+    const half8 *cfrag;
+    const float *cseed;
+    int gblk;
+    long G;
+    const int *member;
+    const half8 *qfrag;
+    const int *fb_list, *fb_count;
+    const float *thr;
+    int blk_per_split;
+    const float *rows;   // [n][192] fp32 candidate rows
+    const float *q;      // [nq][192] fp32 query rows
+    const KdOrder *ko;   // ANN tie order (nullptr: lowest index)
+    unsigned long long *best;
+};
+
+__device__ __forceinline__ unsigned long long t2_key(float d, unsigned rank) {
+    return ((unsigned long long)__float_as_uint(d) << 32) | rank;  // d >= 0: its bits order like the value
+}
+
+__global__ __launch_bounds__(256, 2) void nn_orbit_collect_kernel(OrbitCollectArgs a) {
     __shared__ __attribute__((aligned(16))) char smem[2 * (OC_CB * OS * 1024 + OC_CB * 128)];
+    __shared__ int2 xq[4][OC_XQ];
     constexpr int FRAG_BYTES = OC_CB * OS * 1024;
     constexpr int BUF_BYTES = FRAG_BYTES + OC_CB * 128;
     constexpr int PER_T = OC_CB * OS * 64 / 256;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-    const int count = min(*fb_count, fb_max);
-    const int b_begin = blockIdx.y * blk_per_split;
-    const int b_end = min(gblk, b_begin + blk_per_split);
+    const int count = *a.fb_count;  // every tier-2 query (fb_list has nq slots)
+    const int b_begin = blockIdx.y * a.blk_per_split;
+    const int b_end = min(a.gblk, b_begin + a.blk_per_split);
     const half8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
     const floatx16 zero = {0};
+    const unsigned long long below = (1ull << lane) - 1;
+    int nx = 0;  // queue fill (wave-uniform)
+    auto flush = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_wave_barrier();
+        for (int e0 = 0; e0 < nx; e0 += 64) {
+            const int e = e0 + lane;
+            if (e < nx) {
+                const int2 v = xq[w][e];
+                const float *qrow = a.q + (long)a.fb_list[v.x] * OD;
+                const float dist = exact_dist192_lean(qrow, a.rows + (long)v.y * OD);
+                atomicMin(a.best + v.x, t2_key(dist, kd_rank(a.ko, qrow, v.y)));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // every lane has read its entries before the queue refills
+        nx = 0;
+    };
     for (int grp = blockIdx.x; grp * 128 < count; grp += gridDim.x) {
         const int j = (grp * 4 + w) * 32 + (lane & 31);
-        const int q = j < count ? fb_list[j] : -1;
-        const float t = q >= 0 ? thr[q] : -INFINITY;
+        const int q = j < count ? a.fb_list[j] : -1;
+        const float t = q >= 0 ? a.thr[q] : -INFINITY;
         half8 bq[OS];
 #pragma unroll
-        for (int k = 0; k < OS; k++) bq[k] = q >= 0 ? qfrag[((long)(q >> 5) * OS + k) * 64 + (q & 31) + 32 * h] : zero8;
+        for (int k = 0; k < OS; k++) bq[k] = q >= 0 ? a.qfrag[((long)(q >> 5) * OS + k) * 64 + (q & 31) + 32 * h] : zero8;
         const int nstage = (b_end > b_begin) ? (b_end - b_begin + OC_CB - 1) / OC_CB : 0;
         // candidate fragments + seeds straight to LDS (LDS-DMA, as the shortlist's ring)
         auto issue = [&](int st, int buf) __attribute__((always_inline)) {
             const int blk0 = b_begin + st * OC_CB;
             const int lastv = min(OC_CB, b_end - blk0) * OS * 64 - 1;
-            const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * OS * 64;
+            const uint4 *src = reinterpret_cast<const uint4 *>(a.cfrag) + (long)blk0 * OS * 64;
             char *dst = smem + buf * BUF_BYTES + w * 1024;
 #pragma unroll
             for (int jj = 0; jj < PER_T; jj++) glds16_asm(src + min(w * 64 + lane + jj * 256, lastv), dst + jj * 256 * 16);
             if (w == 0 && lane < OC_CB * 8)
-                glds16_asm(reinterpret_cast<const uint4 *>(cseed) + (long)blk0 * 8 + min(lane, min(OC_CB, b_end - blk0) * 8 - 1),
+                glds16_asm(reinterpret_cast<const uint4 *>(a.cseed) + (long)blk0 * 8 + min(lane, min(OC_CB, b_end - blk0) * 8 - 1),
                            smem + buf * BUF_BYTES + FRAG_BYTES);
         };
         __syncthreads();  // the previous group's reads of both buffers are done
@@ -1529,64 +1568,107 @@ __global__ __launch_bounds__(256, 2) void nn_orbit_collect_kernel(const half8 *_
                     const half8 av = reinterpret_cast<const half8 *>(B)[(cb * OS + k) * 64 + lane];
                     d[k / 3] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[k], d[k / 3], 0, 0, 0);
                 }
-                if (q < 0) continue;
                 unsigned pass = 0;  // element r: the orbit bound reaches T_b
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
                     const float u = d[0][r] + fabsf(d[1][r]) + fabsf(d[2][r]) + fabsf(d[3][r]);
-                    pass |= (-2.0f * u <= t) ? 1u << r : 0u;
+                    pass |= (q >= 0 && -2.0f * u <= t) ? 1u << r : 0u;
                 }
-                if (!pass) continue;
-                while (pass) {  // rare: one reservation per passing orbit
-                    const int r = __builtin_ctz(pass);
-                    pass &= pass - 1;
+                if (!__any(pass)) continue;  // the usual case (wave-uniform)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const bool pr = (pass >> r) & 1;
+                    if (!__any(pr)) continue;
                     const long g = (long)blk * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (g >= G) continue;
-                    float dx[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // element r of each accumulator (selects, no scratch)
+                    int take = 0, m[4] = {-1, -1, -1, -1};
+                    if (pr && g < a.G) {
+                        const float a0 = d[0][r] + d[1][r], b0 = d[0][r] - d[1][r];
+                        const float c0 = d[2][r] + d[3][r], e0 = d[2][r] - d[3][r];
+                        const float V[4] = {a0 + c0, b0 + e0, a0 - c0, b0 - e0};
 #pragma unroll
-                    for (int i = 0; i < 16; i++)
-#pragma unroll
-                        for (int x = 0; x < 4; x++) dx[x] = i == r ? d[x][i] : dx[x];
-                    const float a0 = dx[0] + dx[1], b0 = dx[0] - dx[1];
-                    const float c0 = dx[2] + dx[3], e0 = dx[2] - dx[3];
-                    const float V[4] = {a0 + c0, b0 + e0, a0 - c0, b0 - e0};
-                    int m[4], take = 0;
-#pragma unroll
-                    for (int x = 0; x < 4; x++) {
-                        m[x] = member[g * 4 + x];
-                        take |= (m[x] >= 0 && -2.0f * V[x] <= t) ? 1 << x : 0;
-                    }
-                    if (!take) continue;
-                    int p = atomicAdd(&ccnt[j], __popc(take));
-#pragma unroll
-                    for (int x = 0; x < 4; x++)
-                        if ((take >> x) & 1) {
-                            if (p < cap) cbuf[(long)j * cap + p] = m[x];
-                            p++;
+                        for (int x = 0; x < 4; x++) {
+                            m[x] = a.member[g * 4 + x];
+                            take |= (m[x] >= 0 && -2.0f * V[x] <= t) ? 1 << x : 0;
                         }
+                    }
+#pragma unroll
+                    for (int x = 0; x < 4; x++) {  // append (j, member) in lane order
+                        const bool bx = (take >> x) & 1;
+                        const unsigned long long b = __ballot(bx);
+                        if (bx) xq[w][nx + __popcll(b & below)] = make_int2(j, m[x]);
+                        nx += __popcll(b);
+                    }
+                    if (nx > OC_XQ - 256) flush();  // room for the next element's <= 256 appends
                 }
             }
             dma_drain();
             __syncthreads();
         }
+        if (nx) flush();
     }
 }
 
-int orbit_collect(NNIndex *ix, const int *fb_list, const int *fb_count, int fb_max, const float *thr, int *ccnt,
-                  int *cbuf, int cap, int prev, hipStream_t stream) {
+// the tier-2 winners: decode t2_best[j] -> candidate, write the outputs (kd_done stays 0: kd_verify checks them)
+__global__ __launch_bounds__(256) void nn_orbit_t2_final_kernel(OrbitTail t, const float *__restrict__ qrows,
+                                                                const float *__restrict__ rows) {
+    const int count = *t.fb_count;
+    for (long j = (long)blockIdx.x * 256 + threadIdx.x; j < count; j += (long)gridDim.x * 256) {
+        const long q = t.fb_list[j];
+        const unsigned long long k = t.t2_best[j];
+        if (k == ~0ull) {  // nothing reached T_b: impossible for a finite query (the re-keyed entry does); exhaustive
+            t.ex_list[atomicAdd(t.ex_count, 1)] = (int)q;
+            continue;
+        }
+        const int c = kd_unrank(t.ko, qrows + q * OD, (unsigned)k);
+        t.out_idx[q] = c;
+        t.out_err[q] = __uint_as_float((unsigned)(k >> 32));
+        if (t.m_tile) {
+            t.m_tile[q] = t.tr_tile[c];
+            t.m_pal[q] = t.tr_pal[c];
+            const int at = t.tr_attr[c];
+            t.m_hm[q] = (at & 1) != 0;
+            t.m_vm[q] = (at & 2) != 0;
+        }
+    }
+    (void)rows;
+}
+
+int orbit_tier2(NNIndex *ix, const float *d_q, const OrbitTail &tail, int nq, hipStream_t stream) {
     OrbitIndex *o = ix->orbit;
-    // fixed grid (the tier-2 count stays on the device): many short splits so that a few hundred queries
-    // still spread over the chip; query groups of 128 sized from the previous call's count
+    // fixed grid, the tier-2 count stays on the device: many short candidate splits, and the x dimension strides
+    // over the query groups of 128, so 2 x 512 resident-sized workgroups serve 10 queries or all of them alike
     const int nsplit = std::min(o->gblk, 512);
     const int bps = (o->gblk + nsplit - 1) / nsplit;
-    const int groups = std::max(1, std::min(64, (prev + prev / 4 + 127) / 128 + 1));
-    KTimer tm("nn_collect", stream);
-    hipLaunchKernelGGL(nn_orbit_collect_kernel, dim3(groups, (o->gblk + bps - 1) / bps), dim3(256), 0, stream,
-                       (const half8 *)o->d_frag, o->d_seed, o->gblk, (long)o->G, o->d_member, (const half8 *)o->qfrag,
-                       fb_list, fb_count, fb_max, thr, bps, ccnt, cbuf, cap);
+    OrbitCollectArgs ca;
+    ca.cfrag = (const half8 *)o->d_frag;
+    ca.cseed = o->d_seed;
+    ca.gblk = o->gblk;
+    ca.G = o->G;
+    ca.member = o->d_member;
+    ca.qfrag = (const half8 *)o->qfrag;
+    ca.fb_list = tail.fb_list;
+    ca.fb_count = tail.fb_count;
+    ca.thr = tail.thr;
+    ca.blk_per_split = bps;
+    ca.rows = ix->d_rows;
+    ca.q = d_q;
+    ca.ko = tail.ko;
+    ca.best = tail.t2_best;
+    {
+        KTimer tm("nn_collect", stream);
+        hipLaunchKernelGGL(nn_orbit_collect_kernel, dim3(std::min(2, (nq + 127) / 128), (o->gblk + bps - 1) / bps),
+                           dim3(256), 0, stream, ca);
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    {
+        KTimer tm("nn_rescore2", stream);
+        hipLaunchKernelGGL(nn_orbit_t2_final_kernel, dim3((unsigned)std::min(256, (nq + 255) / 256)), dim3(256), 0,
+                           stream, tail, d_q, (const float *)ix->d_rows);
+    }
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }
+
 
 // ------------------------------------------------------------------------------------------
 // device: FrameTiling queries in one pass (DoFrameTiling main.pas:4023-4025): RGB tile -> Haar PsyV (fp64, one
@@ -2209,6 +2291,10 @@ int orbit_ensure_queries(OrbitIndex *o, int nq) {
     hipFree(o->qstat);
     hipFree(o->pair_cnt);
     hipFree(o->pair_cand);
+    o->qfrag = nullptr;  // a failed allocation below leaves nothing dangling
+    o->qstat = nullptr;
+    o->pair_cnt = o->pair_cand = nullptr;
+    o->cap_q = 0;
     TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cnt, (size_t)nq * sizeof(int)));
     TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cand, (size_t)nq * ORB_PSLOTS * sizeof(int)));
     TILER_HIP_CHECK(hipMalloc(&o->qfrag, (size_t)(nqblk + 1) * OS * 1024));
@@ -2290,18 +2376,13 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             }
         }
     }
-    // Flat query tiles (tail.flat_from.., FrameTiling moves them last): their q' has only block 0, so the workgroups
-    // made of them alone run the block-serial body with 3 of the 12 k-steps on every candidate block (d_1..d_3 are
-    // +-0 for them: the same bounds bit for bit).  Uses one candidate split.
+    // Flat query tiles (from *tail.flat_cnt on, FrameTiling moves them last): their q' has only block 0, so the
+    // workgroups made of them alone run the block-serial body with 3 of the 12 k-steps on every candidate block
+    // (d_1..d_3 are +-0 for them: the same bounds bit for bit).  The count stays on the device: the kernel derives its
+    // first all-flat workgroup from it, with any candidate split (the mixed launch is not used then).
     const int qpw_q = qpw * 32;  // queries per workgroup
-    int wf0 = wgs;
-    if (use_pipe && pmode == 0 && tail.flat_from < nq) {
-        wf0 = std::min(wgs, (std::max(0, tail.flat_from) + qpw_q - 1) / qpw_q);
-        if (wf0 < wgs) {
-            nsplit = 1;
-            mix_full = 0;
-        }
-    }
+    const int *flat_cnt = (use_pipe && pmode == 0) ? tail.flat_cnt : nullptr;
+    if (flat_cnt) mix_full = 0;
     const int bps = (o->gblk + nsplit - 1) / nsplit;
     nsplit = (o->gblk + bps - 1) / bps;
     if (orbit_ensure_queries(o, nq)) return -1;
@@ -2309,6 +2390,9 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     if (nkeys > o->cap_keys) {
         hipFree(o->key);
         hipFree(o->id);
+        o->key = nullptr;
+        o->id = nullptr;
+        o->cap_keys = 0;
         TILER_HIP_CHECK(hipMalloc((void **)&o->key, nkeys * sizeof(float)));
         TILER_HIP_CHECK(hipMalloc((void **)&o->id, nkeys * sizeof(int)));
         o->cap_keys = nkeys;
@@ -2328,7 +2412,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, MD>), dim3(wgs, nsplit),              \
                        dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
                        (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id, o->red_end, o->d_bmask,                \
-                       MD == 0 ? wf0 : 0x7fffffff, o->d_bmask0)
+                       0x7fffffff, o->d_bmask0, MD == 0 ? flat_cnt : nullptr)
 #ifdef TILER_EXPERIMENTS
 #define ORB_LAUNCH(NWV, QB, MD)                                                                                   \
     hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, NWV, QB, MD>), dim3(wgs, nsplit),                  \
@@ -2351,11 +2435,11 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         else if (use_pipe && pmode == 8)  // one wave per SIMD: 4 waves x 4 query blocks (9: x 3)
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 4, 0>), dim3(wgs, nsplit), dim3(256), lds,
                                stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
-                               nsplit, o->key, o->id, o->red_end, o->d_bmask, 0x7fffffff, o->d_bmask0);
+                               nsplit, o->key, o->id, o->red_end, o->d_bmask, 0x7fffffff, o->d_bmask0, nullptr);
         else if (use_pipe && pmode == 9)
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 3, 0>), dim3(wgs, nsplit), dim3(256), lds,
                                stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
-                               nsplit, o->key, o->id, o->red_end, o->d_bmask, 0x7fffffff, o->d_bmask0);
+                               nsplit, o->key, o->id, o->red_end, o->d_bmask, 0x7fffffff, o->d_bmask0, nullptr);
         else if (use_pipe && !mix_full)
             ORB_PIPE(0);
         else if (use_pipe)
@@ -2385,14 +2469,14 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, 0>), dim3(mix_full, 1),
                                dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,
                                (const half8 *)o->qfrag, nq, o->gblk, nsplit, o->key, o->id, o->red_end, o->d_bmask,
-                               0x7fffffff, o->d_bmask0);
+                               0x7fffffff, o->d_bmask0, nullptr);
             if (nq > q_off)
                 hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, 0>),
                                    dim3(wgs - mix_full, nsplit), dim3(ORB_NW * 64), lds, stream,
                                    (const half8 *)o->d_frag, o->d_seed, o->gblk,
                                    (const half8 *)o->qfrag + (size_t)qb_off * OS * 64, nq - q_off, bps, nsplit,
                                    o->key + (size_t)q_off * per_q, o->id + (size_t)q_off * per_q, o->red_end,
-                                   o->d_bmask, 0x7fffffff, o->d_bmask0);
+                                   o->d_bmask, 0x7fffffff, o->d_bmask0, nullptr);
         }
 #undef ORB_PIPE
     }
@@ -2469,7 +2553,10 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         o->last_rescored = h[1];
     }
     ix->last_splits = nsplit;
-    ix->last_flat_queries = wf0 < wgs ? (long)nq - (long)wf0 * qpw_q : 0;
+    ix->last_flat_dev = flat_cnt;  // flat_queries: derived from the device count when the stats are read
+    ix->last_flat_nq = nq;
+    ix->last_flat_qpw = qpw_q;
+    ix->last_flat_wgs = wgs;
     return 0;
 }
 

@@ -68,9 +68,11 @@ struct OrbitIndex {
 
 // generic tier-2 / tier-3 plumbing the orbit rescore feeds (owned by nn_search.hip)
 struct OrbitTail {
-    int *fb_list, *fb_count, *ex_list, *ex_count, fb_max;
+    int *fb_list, *fb_count, *ex_list, *ex_count, fb_max;  // fb_max = nq: every tier-2 query has a slot
     float *thr;                   // [nq] tier-2 threshold T_b (bound-key domain, fp32 rounded up), set by the rescore
-    int flat_from;                // queries >= flat_from are flat tiles: only isotypic block 0 of q' is nonzero
+    unsigned long long *t2_best;  // [nq] per tier-2 slot: min (distance bits << 32 | kd_rank), ~0 until scored
+    const int *flat_cnt;          // device [1] or null: queries >= *flat_cnt are flat tiles (only isotypic block 0 of
+                                  // q' is nonzero); read by the shortlist itself, so no host round trip
     int *out_idx;
     float *out_err;
     const int32_t *tr_tile, *tr_pal;
@@ -96,10 +98,11 @@ void orbit_counters(const NNIndex *ix, long long *expansions, long long *rescore
 int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, hipStream_t stream,
                  bool queries_prepared = false);
 int orbit_ensure_queries(OrbitIndex *o, int nq);
-// tier 2 of an orbit search: every orbit re-scored for the fb_list queries (device count, `prev` = the previous
-// call's count sizes the grid); members whose mirror key reaches thr[q] appended to cbuf[j][cap] / ccnt[j]
-int orbit_collect(NNIndex *ix, const int *fb_list, const int *fb_count, int fb_max, const float *thr, int *ccnt,
-                  int *cbuf, int cap, int prev, hipStream_t stream);
+// tier 2 of an orbit search, for every query the rescore listed (device count, fixed grid, no host read): every
+// orbit re-scored; each member whose mirror key reaches thr[q] gets its reference distance and ANN rank at once and
+// an atomic minimum into t2_best[j]; then the winners are decoded and written (tail's outputs).  No candidate
+// buffer, so no capacity to overflow: only non-finite / fp16-overflowing queries reach the exhaustive tier 3.
+int orbit_tier2(NNIndex *ix, const float *d_q, const OrbitTail &tail, int nq, hipStream_t stream);
 // FrameTiling queries in one kernel: RGB tiles -> Haar descriptors (qrows[Q][192] fp32) + q' fragments + stats
 // (+ rootbox[Q] = annBoxDistance to box[2][192] when box != null)
 // (perm: query i is tile perm[i] of d_rgb; null = identity)

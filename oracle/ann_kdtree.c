@@ -46,9 +46,11 @@ typedef struct {
 
 static int kd_new(kd_tree *t) { return t->nn++; }
 
+/* annMaxSpread (ANN.dll 0x1800158e0): enclosing rect, then the FIRST dimension whose spread exceeds the running
+ * maximum, which starts at 0 (so all-zero spreads give dimension 0) */
 static int max_spread(kd_tree *t, int *pidx, int n) {
     int best = 0;
-    float best_sp = -1.0f;
+    float best_sp = 0.0f;
     for (int dim = 0; dim < t->d; dim++) {
         float mn = t->data[(size_t)pidx[0] * t->d + dim], mx = mn;
         for (int i = 1; i < n; i++) {

@@ -1637,7 +1637,13 @@ int orbit_tier2(NNIndex *ix, const float *d_q, const OrbitTail &tail, int nq, hi
     OrbitIndex *o = ix->orbit;
     // fixed grid, the tier-2 count stays on the device: many short candidate splits, and the x dimension strides
     // over the query groups of 128, so 2 x 512 resident-sized workgroups serve 10 queries or all of them alike
-    const int nsplit = std::min(o->gblk, 512);
+#ifdef TILER_EXPERIMENTS
+    static const int t2x = getenv("TILER_T2_X") ? atoi(getenv("TILER_T2_X")) : 2;
+    static const int t2s = getenv("TILER_T2_NSPLIT") ? atoi(getenv("TILER_T2_NSPLIT")) : 512;
+#else
+    constexpr int t2x = 2, t2s = 512;
+#endif
+    const int nsplit = std::min(o->gblk, t2s);
     const int bps = (o->gblk + nsplit - 1) / nsplit;
     OrbitCollectArgs ca;
     ca.cfrag = (const half8 *)o->d_frag;
@@ -1656,7 +1662,7 @@ int orbit_tier2(NNIndex *ix, const float *d_q, const OrbitTail &tail, int nq, hi
     ca.best = tail.t2_best;
     {
         KTimer tm("nn_collect", stream);
-        hipLaunchKernelGGL(nn_orbit_collect_kernel, dim3(std::min(2, (nq + 127) / 128), (o->gblk + bps - 1) / bps),
+        hipLaunchKernelGGL(nn_orbit_collect_kernel, dim3(std::min(t2x, (nq + 127) / 128), (o->gblk + bps - 1) / bps),
                            dim3(256), 0, stream, ca);
     }
     TILER_HIP_CHECK(hipGetLastError());
@@ -1902,7 +1908,22 @@ __device__ __forceinline__ constexpr int haar_half_pos(int k) {
     return row * 8 + x;
 }
 
-template <bool FASTDIV, int H>
+// NT: the kernel's outputs (rows, fragments, statistics: 1,188 B per tile, never re-read by this kernel) are written
+// with non-temporal stores so they do not evict the tile pixels from L2 between the three component passes
+template <typename T>
+__device__ __forceinline__ void st_out(T *p, const T &v, bool nt) {
+    if (nt)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+__device__ __forceinline__ void st_out(float4 *p, const float4 &v, bool nt) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v w = {v.x, v.y, v.z, v.w};
+    st_out(reinterpret_cast<f4v *>(p), w, nt);
+}
+
+template <bool FASTDIV, int H, bool NT>
 __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut, float *st, float *sbox,
                                               double (*xch)[64][2], double (*sred)[64]) {
     const int lane = threadIdx.x & 63;
@@ -1959,7 +1980,8 @@ __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut,
             const int pc = threadIdx.x + 128 * t, tt = pc >> 4, c4 = pc & 15;
             if (t0 + tt < a.n) {
                 const float *q = st + tt * 65 + c4 * 4;
-                reinterpret_cast<float4 *>(a.out32 + (t0 + tt) * OD + c * 64)[c4] = make_float4(q[0], q[1], q[2], q[3]);
+                st_out(reinterpret_cast<float4 *>(a.out32 + (t0 + tt) * OD + c * 64) + c4, make_float4(q[0], q[1], q[2], q[3]),
+                       NT);
             }
         }
 #pragma unroll
@@ -1988,7 +2010,7 @@ __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut,
                 if (!isfinite(v) || fabs(v) > 65000.0) bad = 1;
                 if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
-            if (has_blk) a.frag[((i >> 5) * OS + s) * 64 + (i & 31) + 32 * H] = hv;
+            if (has_blk) st_out(a.frag + ((i >> 5) * OS + s) * 64 + (i & 31) + 32 * H, hv, NT);
             __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();  // st and xch are rewritten by the next component
@@ -2010,11 +2032,11 @@ __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut,
         q.flags = (bad || sred[3][lane] != 0.0 || !isfinite(n2)) ? 2 : 0;
         q.pad = 0;
         a.qstat[i] = q;
-        if (a.rootbox) a.rootbox[i] = rb;
+        if (a.rootbox) st_out(a.rootbox + i, rb, NT);
     }
 }
 
-template <bool FASTDIV>
+template <bool FASTDIV, bool NT>
 __global__ __launch_bounds__(128) void orbit_ft_query2_kernel(FtQueryArgs a) {
     __shared__ double lut[256];
     __shared__ float st[64 * 65];
@@ -2027,9 +2049,9 @@ __global__ __launch_bounds__(128) void orbit_ft_query2_kernel(FtQueryArgs a) {
         for (int i = threadIdx.x; i < 2 * OD; i += 128) sbox[i] = a.box[i];
     __syncthreads();
     if (threadIdx.x < 64)
-        ft_query_half<FASTDIV, 0>(a, lut, st, sbox, xch, sred);
+        ft_query_half<FASTDIV, 0, NT>(a, lut, st, sbox, xch, sred);
     else
-        ft_query_half<FASTDIV, 1>(a, lut, st, sbox, xch, sred);
+        ft_query_half<FASTDIV, 1, NT>(a, lut, st, sbox, xch, sred);
 }
 
 int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float *qrows, const float *box,
@@ -2075,10 +2097,17 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
         return 0;
     }
 #endif
-    if (gamma == -1)
-        hipLaunchKernelGGL(orbit_ft_query2_kernel<true>, grid, dim3(128), 0, stream, fa);
+#ifdef TILER_EXPERIMENTS
+    static const bool nt = !getenv("TILER_FTQ_NT") || atoi(getenv("TILER_FTQ_NT")) != 0;  // A/B: 0 = plain stores
+#else
+    constexpr bool nt = true;
+#endif
+    if (gamma == -1 && nt)
+        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, true>), grid, dim3(128), 0, stream, fa);
+    else if (gamma == -1)
+        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, false>), grid, dim3(128), 0, stream, fa);
     else
-        hipLaunchKernelGGL(orbit_ft_query2_kernel<false>, grid, dim3(128), 0, stream, fa);
+        hipLaunchKernelGGL((orbit_ft_query2_kernel<false, true>), grid, dim3(128), 0, stream, fa);
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -126,9 +126,14 @@ def _worker(rank, world, port, out_path):
                                               (res[3].astype(np.int32) << 17)).reshape(-1, Q)
         np.add.at(uc, res[0], 1)
     uc = td.allreduce(uc, "sum")
-    full = td.reduce_to(tm, 0)
-    assert (full is None) == (rank != 0)
+    # tilemaps onto rank 0 per keyframe (variable-size units, one buffer per sending rank)
+    plan = td.plan_keyframes(KF_FRAMES, Q, world)
+    owner = [r for u in range(len(KF_FRAMES)) for r in range(world) if u in plan[r]]
+    parts = {u: tm[starts[u]:starts[u + 1]].tobytes() for u in plan[rank]}
+    units = td.gather_units(parts, owner, 0)
+    assert (units is None) == (rank != 0)
     if rank == 0:
+        full = np.concatenate([np.frombuffer(b, np.int32).reshape(-1, Q, 2) for b in units])
         np.savez(out_path, merge_to=merge_to, uc=uc, tm=full)
     dist.destroy_process_group()
 
@@ -161,3 +166,54 @@ def test_sharded_steps_match_single_process(tmp_path):
         assert np.array_equal((blk[..., 1].ravel() >> 17) & 1, res[3])
         np.add.at(uc, res[0], 1)
     assert np.array_equal(got["uc"], uc)
+
+
+def _save_worker(rank, world, port, out_path):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch.distributed as dist
+
+    from tiler_amd import synth
+    from tiler_amd.encoder import DistributedEncoder
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    v = synth.video(71, 64, 48, kf_frames=(3, 2, 4, 1), n_palettes=4)
+    e = DistributedEncoder(v, device=-1)  # host-side only: SaveStream's collective path
+    own = sorted(e.plan[rank])
+    n_own = sum(int(v.kf_start[k + 1] - v.kf_start[k]) for k in own)
+    # a rank holds only its own keyframes' frames and tilemaps
+    assert e.kfs == own and e.frames == n_own and e.frame_rgb.shape[0] == n_own and e.tile.shape == (n_own, 48)
+    assert np.array_equal(e.frame_rgb, v.frame_rgb[e.frame_idx])
+    rng = np.random.default_rng(3)
+    sm_full = {"tile": rng.integers(0, e.palpix.shape[0], (v.frames, 48)), "pal": rng.integers(0, 4, (v.frames, 48)),
+               "hm": rng.integers(0, 2, (v.frames, 48)).astype(np.uint8),
+               "vm": rng.integers(0, 2, (v.frames, 48)).astype(np.uint8),
+               "smoothed": (rng.random((v.frames, 48)) < 0.3).astype(np.uint8)}
+    e.sm = {k: a[e.frame_idx] for k, a in sm_full.items()}
+    data = e.save_stream(64, 48, 24.0)
+    assert (data is None) == (rank != 0)
+    if rank == 0:
+        np.save(out_path, np.frombuffer(data, np.uint8))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_distributed_save_stream_bytes_and_per_rank_memory(tmp_path):
+    """SaveStream sharded: each of 2 gloo ranks holds only its keyframes' frames and tilemaps,
+    writes and compresses its own keyframe streams, and rank 0 assembles a .gtm byte-identical to the single-process
+    writer over the same SmoothedTileMaps (no dense whole-clip tilemap collective)."""
+    from tiler_amd import synth
+    from tiler_amd.encoder import Encoder
+    out = str(tmp_path / "g.npy")
+    mp.spawn(_save_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    v = synth.video(71, 64, 48, kf_frames=(3, 2, 4, 1), n_palettes=4)
+    e = Encoder(v)
+    rng = np.random.default_rng(3)
+    e.sm = {"tile": rng.integers(0, e.palpix.shape[0], (v.frames, 48)), "pal": rng.integers(0, 4, (v.frames, 48)),
+            "hm": rng.integers(0, 2, (v.frames, 48)).astype(np.uint8),
+            "vm": rng.integers(0, 2, (v.frames, 48)).astype(np.uint8),
+            "smoothed": (rng.random((v.frames, 48)) < 0.3).astype(np.uint8)}
+    assert np.load(out).tobytes() == e.save_stream(64, 48, 24.0)

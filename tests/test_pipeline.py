@@ -149,10 +149,11 @@ def _dist_worker(rank, world, port, out, quality):
     v = synth.video(61, 320, 240, kf_frames=(3, 2, 3), n_palettes=8)
     e = DistributedEncoder(v, device=0)
     sm = e.run_all(700, quality, 0.2)
-    if rank == 0:
-        data = e.save_stream(320, 240, 24.0)
-        np.savez(out, palpix=e.palpix, tile=e.tile, pal=e.pal, hm=e.hm, vm=e.vm, sm_tile=sm["tile"],
-                 sm_smoothed=sm["smoothed"], gtm=np.frombuffer(data, np.uint8))
+    data = e.save_stream(320, 240, 24.0)  # a collective: every rank calls it, rank 0 gets the bytes
+    assert e.frames == e.frame_idx.size < v.frames  # only this rank's keyframes are held
+    np.savez(out + f".{rank}.npz", frame_idx=e.frame_idx, palpix=e.palpix, tile=e.tile, pal=e.pal, hm=e.hm, vm=e.vm,
+             sm_tile=sm["tile"], sm_smoothed=sm["smoothed"],
+             gtm=np.frombuffer(data, np.uint8) if data is not None else np.zeros(0, np.uint8))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -170,15 +171,24 @@ def test_run_all_chain_two_ranks_match_single_process(gpu, tmp_path):
     s.close()
     out = str(tmp_path / "r.npz")
     mp.spawn(_dist_worker, args=(2, port, out, FT_MEDIUM), nprocs=2, join=True)
-    got = np.load(out)
     v = synth.video(61, 320, 240, kf_frames=(3, 2, 3), n_palettes=8)
     e = Encoder(v)
     sm = e.run_all(700, FT_MEDIUM, 0.2)
     data = e.save_stream(320, 240, 24.0)
-    for k, a in (("palpix", e.palpix), ("tile", e.tile), ("pal", e.pal), ("hm", e.hm), ("vm", e.vm),
-                 ("sm_tile", sm["tile"]), ("sm_smoothed", sm["smoothed"])):
-        assert np.array_equal(got[k], a), k
-    assert got["gtm"].tobytes() == data
+    seen = np.zeros(v.frames, bool)
+    for rank in range(2):
+        got = np.load(out + f".{rank}.npz")
+        fi = got["frame_idx"]
+        seen[fi] = True
+        assert np.array_equal(got["palpix"], e.palpix)  # the reduced tileset is replicated
+        for k, a in (("tile", e.tile), ("pal", e.pal), ("hm", e.hm), ("vm", e.vm), ("sm_tile", sm["tile"]),
+                     ("sm_smoothed", sm["smoothed"])):
+            assert np.array_equal(got[k], a[fi]), (rank, k)
+        if rank == 0:
+            assert got["gtm"].tobytes() == data
+        else:
+            assert got["gtm"].size == 0
+    assert seen.all()
 
 
 @pytest.mark.gpu

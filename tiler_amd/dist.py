@@ -10,8 +10,10 @@ The exchanges are the pipeline's own, each ONE fixed-layout tensor collective (n
     one bin, so exactly one rank writes its entry; every rank then applies MergeTiles identically and holds the
     reduced tileset (the north star's tileset all-gather);
   * before ReindexTiles: the UseCount histogram, int64 [T], all-reduced with SUM (main.pas:1208-1221);
-  * for SaveStream: the tilemaps, int32 [F][Q][4], each rank contributing its own keyframes' frames, reduced with
-    SUM onto the saving rank only.
+  * for SaveStream: each rank writes AND compresses its own keyframes' streams (LZCompress per keyframe is
+    independent); the stream lengths, int64 [KF], are all-reduced with SUM and each rank sends its streams to the
+    saving rank as one uint8 buffer (point-to-point, gather_units), which assembles the file.  No rank holds
+    another rank's frames or tilemaps at any point: per-rank memory is O(its keyframes) plus the tileset.
 Tensors live on the rank's GPU under nccl (RCCL reads HBM directly) and on the CPU under gloo.
 """
 from __future__ import annotations
@@ -80,10 +82,43 @@ def allreduce_sum(a: np.ndarray, device=None) -> np.ndarray:
     return allreduce(a, "sum", device)
 
 
-def reduce_to(a: np.ndarray, dst: int = 0, device=None) -> np.ndarray | None:
-    """SUM of every rank's `a` on rank `dst` only (None elsewhere): ranks contribute disjoint parts, zeros
-    elsewhere, so the sum is the assembled array."""
+def gather_units(parts: dict, owner_of, dst: int = 0, device=None) -> list | None:
+    """Variable-size byte units (e.g. compressed keyframe streams) onto rank `dst`, in unit order.  parts maps
+    unit -> bytes for the units this rank owns (owner_of[u] == rank); the lengths, int64 [n_units], are all-reduced
+    (SUM: one owner per unit), then every other rank sends its units concatenated in unit order as ONE uint8 tensor.
+    Returns the list of all units' bytes on dst, None elsewhere."""
+    import torch
     import torch.distributed as dist
-    t = _to_tensor(a, comm_device() if device is None else device)
-    dist.reduce(t, dst, op=dist.ReduceOp.SUM)
-    return t.cpu().numpy() if dist.get_rank() == dst else None
+    device = comm_device() if device is None else device
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = len(owner_of)
+    lens = np.zeros(n, np.int64)
+    for u, b in parts.items():
+        assert owner_of[u] == rank, (u, owner_of[u], rank)
+        lens[u] = len(b)
+    lens = allreduce(lens, "sum", device)
+    if rank != dst:
+        mine = [u for u in range(n) if owner_of[u] == rank]
+        total = int(sum(lens[u] for u in mine))
+        if total:
+            buf = np.frombuffer(b"".join(parts[u] for u in mine), np.uint8)
+            dist.send(torch.from_numpy(buf.copy()).to(device), dst)
+        return None
+    out = [parts.get(u) for u in range(n)]
+    for r in range(world):
+        if r == dst:
+            continue
+        units = [u for u in range(n) if owner_of[u] == r]
+        total = int(sum(lens[u] for u in units))
+        if not total:
+            for u in units:
+                out[u] = b""
+            continue
+        t = torch.empty(total, dtype=torch.uint8, device=device)
+        dist.recv(t, r)
+        buf = t.cpu().numpy().tobytes()
+        o = 0
+        for u in units:
+            out[u] = buf[o:o + int(lens[u])]
+            o += int(lens[u])
+    return out

@@ -15,7 +15,7 @@ import numpy as np
 
 from . import frame_tiling as ft
 from . import global_tiling as gt
-from .gtm import save_stream
+from . import gtm
 from .smooth import DEFAULT_STRENGTH, smooth_keyframe
 from .synth import Video, video_from_frames
 
@@ -43,11 +43,19 @@ def load_and_dither(frames, tm_w: int, tm_h: int, palettes_fn=None, n_palettes: 
 
 
 class Encoder:
-    def __init__(self, v: Video, palsize: int = 16):
+    """frames: the global frame indices this encoder holds the frames and tilemaps of (sorted, whole keyframes;
+    None = all).  The tileset (palpix, flags, Active, UseCount) is always the whole clip's.  Tilemap arrays are
+    [len(frames)][Q]: row r is frame frames[r]."""
+
+    def __init__(self, v: Video, palsize: int = 16, frames=None):
         F, Q = v.frames, v.tiles_per_frame
         self.palsize = palsize
-        self.frame_rgb = v.frame_rgb
+        self.n_frames = F
         self.kf_start = np.asarray(v.kf_start, np.int64)
+        own = np.arange(F) if frames is None else np.asarray(frames, np.int64)
+        self.frame_idx = own
+        # only the held frames are read (a memory-mapped Video pages in just these)
+        self.frame_rgb = v.frame_rgb if frames is None else np.ascontiguousarray(v.frame_rgb[own])
         self.palettes = np.asarray(v.palettes, np.int32)
         self.centroids = np.asarray(v.centroids, np.float64)
         self.n_palettes = self.palettes.shape[1]
@@ -59,11 +67,17 @@ class Encoder:
         self.active = np.ones(F * Q, np.uint8)
         self.use_count = np.ones(F * Q, np.int64)
         # TileMap: GlobalTileIndex = own tile, PalIdx = DitheringPalIndex, mirrors false
-        self.tile = np.arange(F * Q, dtype=np.int64).reshape(F, Q)
-        self.pal = self.dith_pal.reshape(F, Q).astype(np.int64)
-        self.hm = np.zeros((F, Q), np.uint8)
-        self.vm = np.zeros((F, Q), np.uint8)
+        self.tile = (own[:, None] * Q + np.arange(Q, dtype=np.int64)[None, :])
+        self.pal = self.dith_pal.reshape(F, Q)[own].astype(np.int64)
+        self.hm = np.zeros((own.size, Q), np.uint8)
+        self.vm = np.zeros((own.size, Q), np.uint8)
         self.sm = None
+        # the keyframes held (every frame of each), and their first tilemap row
+        self.kfs = [k for k in range(self.kf_start.size - 1)
+                    if np.isin(np.arange(self.kf_start[k], self.kf_start[k + 1]), own).all()]
+        self._row0 = {k: int(np.searchsorted(own, self.kf_start[k])) for k in self.kfs}
+        if sum(int(self.kf_start[k + 1] - self.kf_start[k]) for k in self.kfs) != own.size:
+            raise ValueError("an encoder holds whole keyframes only")
 
     @property
     def frames(self) -> int:
@@ -72,6 +86,11 @@ class Encoder:
     @property
     def tiles_per_frame(self) -> int:
         return self.tile.shape[1]
+
+    def rows(self, k: int) -> slice:
+        """Tilemap rows of keyframe k."""
+        r0 = self._row0[k]
+        return slice(r0, r0 + int(self.kf_start[k + 1] - self.kf_start[k]))
 
     # --- tile-list bookkeeping --------------------------------------------------------------------
     def finish_merge_tiles(self, merge_index):
@@ -128,27 +147,30 @@ class Encoder:
         (over the keyframe's current TileMap items), DoFrameTiling of all its frames, FinishFrameTiling."""
         gds = ft.prepare_global_ft(self.palpix, self.active)
         errs = np.zeros(self.tile.shape, np.float32)
+        Q = self.tiles_per_frame
         try:
-            for k in range(self.kf_start.size - 1):
-                f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
+            for k in self.kfs:
+                r = self.rows(k)
                 kt = ft.prepare_frame_tiling(self.palpix, self.thm, self.tvm, self.palettes[k], gds,
-                                             self.pal[f0:f1].ravel(), self.tile[f0:f1].ravel(), quality,
+                                             self.pal[r].ravel(), self.tile[r].ravel(), quality,
                                              self.centroids[k], use_wavelets, gamma)
                 try:
-                    t, p, h, v, e = kt.do_frame_tiling(self.frame_rgb[f0:f1])
+                    t, p, h, v, e = kt.do_frame_tiling(self.frame_rgb[r])
                 finally:
                     kt.finish_frame_tiling()
-                n = (f1 - f0, self.tiles_per_frame)
-                self.tile[f0:f1], self.pal[f0:f1] = t.reshape(n), p.reshape(n)
-                self.hm[f0:f1], self.vm[f0:f1], errs[f0:f1] = h.reshape(n), v.reshape(n), e.reshape(n)
+                n = (r.stop - r.start, Q)
+                self.tile[r], self.pal[r] = t.reshape(n), p.reshape(n)
+                self.hm[r], self.vm[r], errs[r] = h.reshape(n), v.reshape(n), e.reshape(n)
         finally:
             gds.kdt.close()
         return errs
 
+    def _use_count(self, T: int) -> np.ndarray:
+        return np.bincount(self.tile.ravel(), minlength=T).astype(np.int64)
+
     def do_reindex(self):
         """btnReindexClick main.pas:1199-1230: UseCount / Active from the TileMaps, then ReindexTiles."""
-        T = self.palpix.shape[0]
-        self.use_count = np.bincount(self.tile.ravel(), minlength=T).astype(np.int64)
+        self.use_count = self._use_count(self.palpix.shape[0])
         self.active = (self.use_count > 0).astype(np.uint8)
         self.reindex_tiles()
 
@@ -157,21 +179,34 @@ class Encoder:
         every position (frames of one keyframe only, main.pas:4081-4082) -> one GPU call per keyframe."""
         sm = {"tile": self.tile.copy(), "pal": self.pal.copy(), "hm": self.hm.copy(), "vm": self.vm.copy(),
               "smoothed": np.zeros(self.tile.shape, np.uint8)}
-        for k in range(self.kf_start.size - 1):
-            f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
-            t, p, h, v, s, _ = smooth_keyframe(sm["tile"][f0:f1], sm["pal"][f0:f1], sm["hm"][f0:f1],
-                                               sm["vm"][f0:f1], sm["smoothed"][f0:f1], self.palpix,
-                                               self.palettes[k], strength)
-            sm["tile"][f0:f1], sm["pal"][f0:f1], sm["hm"][f0:f1], sm["vm"][f0:f1] = t, p, h, v
-            sm["smoothed"][f0:f1] = s
+        for k in self.kfs:
+            r = self.rows(k)
+            t, p, h, v, s, _ = smooth_keyframe(sm["tile"][r], sm["pal"][r], sm["hm"][r], sm["vm"][r],
+                                               sm["smoothed"][r], self.palpix, self.palettes[k], strength)
+            sm["tile"][r], sm["pal"][r], sm["hm"][r], sm["vm"][r] = t, p, h, v
+            sm["smoothed"][r] = s
         self.sm = sm
         return sm
 
+    def _keyframe_streams(self, width: int, height: int, fps: float) -> dict:
+        """LZCompress'd command stream of every held keyframe (SaveStream main.pas:4724-4734), compressed
+        concurrently."""
+        sm = self.sm
+        if sm is None:
+            raise RuntimeError("SaveStream needs the SmoothedTileMaps: run do_smooth first")
+        raws = []
+        for k in self.kfs:
+            r = self.rows(k)
+            raws.append(gtm.keyframe_raw(k, self.palpix, self.thm, self.tvm, self.palettes[k], sm["tile"][r],
+                                         sm["pal"][r], sm["hm"][r], sm["vm"][r], sm["smoothed"][r], width, fps,
+                                         height, self.palsize))
+        return dict(zip(self.kfs, gtm.compress_streams(raws)))
+
     def save_stream(self, width: int, height: int, fps: float = 24.0) -> bytes:
         """btnSaveClick -> SaveStream main.pas:4529-4763 (the .gtm bytes; needs do_smooth first)."""
-        sm = self.sm
-        return save_stream(self.palpix, self.thm, self.tvm, self.kf_start, self.palettes, sm["tile"], sm["pal"],
-                           sm["hm"], sm["vm"], sm["smoothed"], width, height, fps, self.palsize)
+        comps = self._keyframe_streams(width, height, fps)
+        return gtm.assemble_stream([comps[k] for k in range(self.kf_start.size - 1)], self.kf_start, width, height,
+                                   fps)
 
     def run_all(self, desired: int, quality: int = ft.FT_MEDIUM, strength: float = DEFAULT_STRENGTH):
         """btnRunAllClick main.pas:1232-1272 from MakeUnique to Smooth."""
@@ -189,11 +224,12 @@ class DistributedEncoder(Encoder):
     Device: each rank binds its own GPU -- libANN.so through tiler_init(device) and torch through
     torch.cuda.set_device(device) -- with device = LOCAL_RANK (torchrun's one process per GPU) unless given.
     Work: palette bins (K-Modes) and keyframes (FrameTiling, then Smooth, same plan) are assigned longest-first
-    across the ranks; a rank computes only its own units.  Exchanges (fixed-layout tensors, tiler_amd.dist):
-    the K-Modes merge map (all-reduce MAX) so every rank holds the reduced tileset, the UseCount histogram
-    (all-reduce SUM) for ReindexTiles, and the tilemaps onto rank `save_rank` only (reduce SUM) for SaveStream.
-    Between steps a rank's tilemaps are current for its own keyframes only; after run_all (or gather()) rank
-    `save_rank` holds the whole single-process state."""
+    across the ranks; a rank computes only its own units.  Memory: a rank holds the tileset (replicated, the north
+    star's all-gathered tileset) and ONLY its own keyframes' frames and tilemaps ([own frames][Q]; `frame_idx`
+    maps rows to frames).  Exchanges (fixed-layout tensors, tiler_amd.dist): the K-Modes merge map (all-reduce
+    MAX) so every rank holds the reduced tileset, the UseCount histogram (all-reduce SUM) for ReindexTiles, and for
+    SaveStream each rank's compressed keyframe streams onto rank `save_rank` (gather_units).  save_stream is a
+    collective: every rank calls it, save_rank gets the .gtm bytes, the others None."""
 
     def __init__(self, v: Video, palsize: int = 16, device: int | None = None, save_rank: int = 0):
         import os
@@ -203,19 +239,25 @@ class DistributedEncoder(Encoder):
 
         from ._lib import check, load
         from . import dist as tdist
-        super().__init__(v, palsize)
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        kf_start = np.asarray(v.kf_start, np.int64)
+        nkf = kf_start.size - 1
+        kf_frames = [int(kf_start[k + 1] - kf_start[k]) for k in range(nkf)]
+        self.plan = tdist.plan_keyframes(kf_frames, v.tiles_per_frame, self.world)
+        self.owner_of = [0] * nkf
+        for r, units in enumerate(self.plan):
+            for k in units:
+                self.owner_of[k] = r
+        mine = sorted(self.plan[self.rank])
+        own = np.concatenate([np.arange(kf_start[k], kf_start[k + 1]) for k in mine]) if mine \
+            else np.zeros(0, np.int64)
+        super().__init__(v, palsize, frames=own)
         self.device = int(os.environ.get("LOCAL_RANK", "0")) if device is None else int(device)
-        check(load().tiler_init(self.device), "tiler_init")
-        if torch.cuda.is_available():
-            torch.cuda.set_device(self.device)
+        if self.device >= 0:  # device = -1: no GPU binding (host-side steps only, e.g. SaveStream in CPU tests)
+            check(load().tiler_init(self.device), "tiler_init")
+            if torch.cuda.is_available():
+                torch.cuda.set_device(self.device)
         self.save_rank = save_rank
-        nkf = self.kf_start.size - 1
-        kf_frames = [int(self.kf_start[k + 1] - self.kf_start[k]) for k in range(nkf)]
-        self.my_kf = tdist.plan_keyframes(kf_frames, self.tiles_per_frame, self.world)[self.rank]
-        self.my_frames = np.zeros(self.frames, bool)
-        for k in self.my_kf:
-            self.my_frames[int(self.kf_start[k]):int(self.kf_start[k + 1])] = True
 
     def do_global_tiling(self, desired: int, restart: int = gt.CRANDOM_KMODES_COUNT):
         from . import dist as tdist
@@ -233,87 +275,16 @@ class DistributedEncoder(Encoder):
         self.reindex_tiles()
         return plan.k_per_bin
 
-    def do_frame_tiling(self, quality: int = ft.FT_MEDIUM, use_wavelets: bool = True, gamma: int = -1):
-        """This rank's keyframes only (their TileMaps become current; the others' stay as they were)."""
-        gds = ft.prepare_global_ft(self.palpix, self.active)
-        errs = np.zeros(self.tile.shape, np.float32)
-        Q = self.tiles_per_frame
-        try:
-            for k in self.my_kf:
-                f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
-                kt = ft.prepare_frame_tiling(self.palpix, self.thm, self.tvm, self.palettes[k], gds,
-                                             self.pal[f0:f1].ravel(), self.tile[f0:f1].ravel(), quality,
-                                             self.centroids[k], use_wavelets, gamma)
-                try:
-                    t, p, h, v, e = kt.do_frame_tiling(self.frame_rgb[f0:f1])
-                finally:
-                    kt.finish_frame_tiling()
-                n = (f1 - f0, Q)
-                self.tile[f0:f1], self.pal[f0:f1] = t.reshape(n), p.reshape(n)
-                self.hm[f0:f1], self.vm[f0:f1], errs[f0:f1] = h.reshape(n), v.reshape(n), e.reshape(n)
-        finally:
-            gds.kdt.close()
-        return errs
-
-    def do_reindex(self):
-        """btnReindexClick main.pas:1199-1230 with the UseCount histogram all-reduced over the ranks' keyframes."""
+    def _use_count(self, T: int) -> np.ndarray:
+        """btnReindexClick main.pas:1208-1221: the UseCount histogram over every rank's keyframes."""
         from . import dist as tdist
-        T = self.palpix.shape[0]
-        local = np.bincount(self.tile[self.my_frames].ravel(), minlength=T).astype(np.int64)
-        self.use_count = tdist.allreduce(local, "sum")
-        self.active = (self.use_count > 0).astype(np.uint8)
-        self.tile = np.where(self.my_frames[:, None], self.tile, 0)  # other ranks' frames: not current here
-        self.reindex_tiles()
+        return tdist.allreduce(super()._use_count(T), "sum")
 
-    def do_smooth(self, strength: float = DEFAULT_STRENGTH):
-        sm = {"tile": self.tile.copy(), "pal": self.pal.copy(), "hm": self.hm.copy(), "vm": self.vm.copy(),
-              "smoothed": np.zeros(self.tile.shape, np.uint8)}
-        for k in self.my_kf:
-            f0, f1 = int(self.kf_start[k]), int(self.kf_start[k + 1])
-            t, p, h, v, s, _ = smooth_keyframe(sm["tile"][f0:f1], sm["pal"][f0:f1], sm["hm"][f0:f1],
-                                               sm["vm"][f0:f1], sm["smoothed"][f0:f1], self.palpix,
-                                               self.palettes[k], strength)
-            sm["tile"][f0:f1], sm["pal"][f0:f1], sm["hm"][f0:f1], sm["vm"][f0:f1] = t, p, h, v
-            sm["smoothed"][f0:f1] = s
-        self.sm = sm
-        return sm
-
-    def gather(self):
-        """Every rank's keyframes' TileMaps and SmoothedTileMaps onto rank save_rank (one reduce of int32
-        [F][Q][4]: tile, pal | hm << 16 | vm << 17, and the same for the smoothed items | smoothed << 18)."""
+    def save_stream(self, width: int, height: int, fps: float = 24.0) -> bytes | None:
+        """SaveStream as a collective: every rank writes and compresses its own keyframes' streams, rank
+        save_rank receives the others' and assembles the file (None on the other ranks)."""
         from . import dist as tdist
-        if self.n_palettes > 1 << 16:
-            raise ValueError("palette index does not fit the packed tilemap layout")
-        own = self.my_frames[:, None]
-        sm = self.sm
-        pk = np.zeros(self.tile.shape + (4,), np.int32)
-        pk[..., 0] = np.where(own, self.tile, 0)
-        pk[..., 1] = np.where(own, self.pal | (self.hm.astype(np.int64) << 16) | (self.vm.astype(np.int64) << 17), 0)
-        if sm is not None:
-            pk[..., 2] = np.where(own, sm["tile"], 0)
-            pk[..., 3] = np.where(own, sm["pal"] | (sm["hm"].astype(np.int64) << 16) |
-                                  (sm["vm"].astype(np.int64) << 17) | (sm["smoothed"].astype(np.int64) << 18), 0)
-        full = tdist.reduce_to(pk, self.save_rank)
-        if full is None:
+        comps = tdist.gather_units(self._keyframe_streams(width, height, fps), self.owner_of, self.save_rank)
+        if comps is None:
             return None
-        self.tile = full[..., 0].astype(np.int64)
-        self.pal = (full[..., 1] & 0xFFFF).astype(np.int64)
-        self.hm = ((full[..., 1] >> 16) & 1).astype(np.uint8)
-        self.vm = ((full[..., 1] >> 17) & 1).astype(np.uint8)
-        self.my_frames[:] = True
-        if sm is not None:
-            self.sm = {"tile": full[..., 2].astype(np.int64), "pal": (full[..., 3] & 0xFFFF).astype(np.int64),
-                       "hm": ((full[..., 3] >> 16) & 1).astype(np.uint8),
-                       "vm": ((full[..., 3] >> 17) & 1).astype(np.uint8),
-                       "smoothed": ((full[..., 3] >> 18) & 1).astype(np.uint8)}
-        return self.sm
-
-    def run_all(self, desired: int, quality: int = ft.FT_MEDIUM, strength: float = DEFAULT_STRENGTH):
-        """btnRunAllClick from MakeUnique to Smooth, then the tilemaps onto save_rank (None on the other ranks)."""
-        super().run_all(desired, quality, strength)
-        return self.gather()
-
-    def save_stream(self, width: int, height: int, fps: float = 24.0) -> bytes:
-        if self.rank != self.save_rank:
-            raise RuntimeError(f"SaveStream runs on rank {self.save_rank}, which holds the gathered tilemaps")
-        return super().save_stream(width, height, fps)
+        return gtm.assemble_stream(comps, self.kf_start, width, height, fps)

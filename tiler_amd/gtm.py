@@ -120,51 +120,48 @@ def keyframe_commands(tile, pal, hm, vm, smoothed, thm, tvm, palettes, palsize: 
     return bytes(z.b)
 
 
-def save_stream(palpix, thm, tvm, kf_start, palettes, sm_tile, sm_pal, sm_hm, sm_vm, sm_smoothed, width: int,
-                height: int, fps: float, palsize: int = 16, threads: int | None = None) -> bytes:
-    """SaveStream main.pas:4529-4763.  palpix [T][64] (active tiles, reindexed), thm/tvm [T], kf_start [KF+1],
-    palettes [KF][P][16], sm_* [F][Q] SmoothedTileMap; width/height in pixels.  Returns the .gtm bytes."""
+def keyframe_raw(k: int, palpix, thm, tvm, palettes_k, tile, pal, hm, vm, smoothed, width: int, fps: float,
+                 height: int, palsize: int = 16) -> bytes:
+    """The uncompressed command bytes of keyframe k (SaveStream main.pas:4724-4734): WriteTiles for k = 0 only
+    (SetDimensions + TileSet + 64 B per tile, 4603-4622), then WriteKFAttributes and the keyframe's frames
+    (tile/pal/hm/vm/smoothed: its [f][Q] SmoothedTileMap rows)."""
     palpix = np.ascontiguousarray(palpix, np.uint8).reshape(-1, 64)
     T = palpix.shape[0]
+    z = _Z()
+    if k == 0:  # WriteTiles
+        z.cmd(GT_SET_DIMENSIONS, 0)
+        z.word(width // 8)
+        z.word(height // 8)
+        z.dword(fpc_round(1000 * 1000 * 1000 / fps))
+        z.dword(T)
+        z.cmd(GT_TILE_SET, palsize)
+        z.dword(0)
+        z.dword(T - 1)
+        z.b += palpix.tobytes()
+    z.b += keyframe_commands(tile, pal, hm, vm, smoothed, thm, tvm, palettes_k, palsize)
+    return bytes(z.b)
+
+
+def compress_streams(raws, threads: int | None = None) -> list:
+    """LZCompress of independent keyframe streams, concurrently (the C encoder runs outside the GIL)."""
+    if not raws:
+        return []
+    workers = max(1, min(len(raws), threads or min(16, len(os.sched_getaffinity(0)))))
+    with ThreadPoolExecutor(workers) as ex:
+        return list(ex.map(lzma_encode, raws))
+
+
+def assemble_stream(comps, kf_start, width: int, height: int, fps: float) -> bytes:
+    """The .gtm file from the keyframes' compressed streams (in keyframe order): TGTMHeader (main.pas:103-114),
+    one TGTMKeyFrameInfo per keyframe (116-124) with the measured sizes (4735-4757), then the streams."""
     kf_start = np.asarray(kf_start, np.int64)
     KF = kf_start.size - 1
     F = int(kf_start[-1])
-    tmw, tmh = width // 8, height // 8
     header = {"AverageBytesPerSec": 0, "KFMaxBytesPerSec": 0}
     kfinfo = []
     for k in range(KF):
         kfinfo.append({"KFIndex": k, "FrameIndex": int(kf_start[k]), "RawSize": 0, "CompressedSize": 0,
                        "TimeCodeMillisecond": fpc_round(1000.0 * int(kf_start[k]) / fps)})
-
-    def hdr_bytes():
-        h = b"GTMv" + struct.pack("<9I", 40 - 8, 40 + 28 * KF, 1, width, height, KF, F,
-                                  header["AverageBytesPerSec"] & 0xFFFFFFFF, header["KFMaxBytesPerSec"] & 0xFFFFFFFF)
-        for ki in kfinfo:
-            h += b"GTMk" + struct.pack("<6I", 28 - 8, ki["KFIndex"], ki["FrameIndex"], ki["RawSize"],
-                                       ki["CompressedSize"], ki["TimeCodeMillisecond"])
-        return h
-
-    raws = []
-    for k in range(KF):
-        z = _Z()
-        if k == 0:  # WriteTiles
-            z.cmd(GT_SET_DIMENSIONS, 0)
-            z.word(tmw)
-            z.word(tmh)
-            z.dword(fpc_round(1000 * 1000 * 1000 / fps))
-            z.dword(T)
-            z.cmd(GT_TILE_SET, palsize)
-            z.dword(0)
-            z.dword(T - 1)
-            z.b += palpix.tobytes()
-        f0, f1 = int(kf_start[k]), int(kf_start[k + 1])
-        z.b += keyframe_commands(sm_tile[f0:f1], sm_pal[f0:f1], sm_hm[f0:f1], sm_vm[f0:f1], sm_smoothed[f0:f1],
-                                 thm, tvm, palettes[k], palsize)
-        raws.append(bytes(z.b))
-    # keyframe streams are independent: compress them concurrently (the C encoder runs outside the GIL)
-    workers = max(1, min(len(raws), threads or min(16, len(os.sched_getaffinity(0)))))
-    with ThreadPoolExecutor(workers) as ex:
-        comps = list(ex.map(lzma_encode, raws))
     body = bytearray()
     avg = 0
     last_kf = 0
@@ -179,4 +176,22 @@ def save_stream(palpix, thm, tvm, kf_start, palettes, sm_tile, sm_pal, sm_hm, sm
             header["KFMaxBytesPerSec"] = max(header["KFMaxBytesPerSec"], fpc_round(len(comp) * fps / kf_count))
         avg += len(comp)
     header["AverageBytesPerSec"] = fpc_round(avg * fps / F)
-    return hdr_bytes() + bytes(body)
+    h = b"GTMv" + struct.pack("<9I", 40 - 8, 40 + 28 * KF, 1, width, height, KF, F,
+                              header["AverageBytesPerSec"] & 0xFFFFFFFF, header["KFMaxBytesPerSec"] & 0xFFFFFFFF)
+    for ki in kfinfo:
+        h += b"GTMk" + struct.pack("<6I", 28 - 8, ki["KFIndex"], ki["FrameIndex"], ki["RawSize"],
+                                   ki["CompressedSize"], ki["TimeCodeMillisecond"])
+    return h + bytes(body)
+
+
+def save_stream(palpix, thm, tvm, kf_start, palettes, sm_tile, sm_pal, sm_hm, sm_vm, sm_smoothed, width: int,
+                height: int, fps: float, palsize: int = 16, threads: int | None = None) -> bytes:
+    """SaveStream main.pas:4529-4763.  palpix [T][64] (active tiles, reindexed), thm/tvm [T], kf_start [KF+1],
+    palettes [KF][P][16], sm_* [F][Q] SmoothedTileMap; width/height in pixels.  Returns the .gtm bytes."""
+    kf_start = np.asarray(kf_start, np.int64)
+    raws = []
+    for k in range(kf_start.size - 1):
+        f0, f1 = int(kf_start[k]), int(kf_start[k + 1])
+        raws.append(keyframe_raw(k, palpix, thm, tvm, palettes[k], sm_tile[f0:f1], sm_pal[f0:f1], sm_hm[f0:f1],
+                                 sm_vm[f0:f1], sm_smoothed[f0:f1], width, fps, height, palsize))
+    return assemble_stream(compress_streams(raws, threads), kf_start, width, height, fps)

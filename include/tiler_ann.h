@@ -130,6 +130,26 @@ int tiler_ft_set_maps(ann_kdtree *akd, const int32_t *tr_tile, const int32_t *tr
  * tilemap item {GlobalTileIndex, PalIdx, HMirror = attr&1, VMirror = attr&2} + err. Host buffers. */
 int tiler_frame_tiling(ann_kdtree *akd, const int32_t *rgb, int Q, int use_wavelets, int gamma, int32_t *out_tile,
                        int32_t *out_pal, uint8_t *out_hm, uint8_t *out_vm, float *out_err);
+/* PrepareFrameTiling (main.pas:3791-3967) for one keyframe, on the device: its tilemap items d_item_tile /
+ * d_item_pal [n_items] (TFrame.TileMap GlobalTileIndex / PalIdx of every frame tile; -1 = none) -> the distinct
+ * (PalIdx, tile) items -> UseOne's k = 8 preselection in global_ds (the handle over PrepareGlobalFT's 64-d rows, its
+ * TRTo maps set with tiler_ft_set_maps; ANN's tie order) -> used[palette][tile][attr] (results of equal err after
+ * the first skipped, main.pas:3832-3852; quality 0 Fast: the item's palette, 1 Medium: every palette p' with
+ * near[p' * n_palettes + p] != 0 -- the host's corr(p', p) < cFTPaletteTol * HighestCorr, BuildPaletteCorrTriangle
+ * main.pas:3855-3867 --, 2 Slow: all) -> DoPsyV's candidates in emission order -> their descriptors -> a new
+ * search handle over them with its TRTo maps set, ready for tiler_frame_tiling_dev.  The tileset d_palpix[n_tiles]
+ * [64], d_thm / d_tvm[n_tiles] (TTile.HMirror / VMirror) and d_palettes[n_palettes][16] are in HBM; near is a host
+ * array (Medium only).  Runs on stream (synchronising it twice: the distinct-item and candidate counts); info
+ * (optional) returns those counts.  Calls sharing global_ds are serialised.  NULL on error. */
+typedef struct {
+    int64_t items;      /* distinct (PalIdx, GlobalTileIndex) items searched */
+    int64_t candidates; /* KNNSize: candidate descriptors of the keyframe's dataset */
+} tiler_prepare_info;
+ann_kdtree *tiler_prepare_frame_tiling_dev(ann_kdtree *global_ds, const int32_t *d_item_tile,
+                                           const int32_t *d_item_pal, int64_t n_items, const uint8_t *d_palpix,
+                                           const uint8_t *d_thm, const uint8_t *d_tvm, int n_tiles,
+                                           const int32_t *d_palettes, int n_palettes, int quality, const uint8_t *near,
+                                           int use_wavelets, int gamma, void *stream, tiler_prepare_info *info);
 /* Same, every buffer in HBM, asynchronous on stream (the benchmarked path): no host synchronisation inside, every
  * data-dependent count (flat tiles, tier-2 / tier-3 queries) stays on the device. */
 int tiler_frame_tiling_dev(ann_kdtree *akd, const int32_t *d_rgb, int Q, int use_wavelets, int gamma,

@@ -216,3 +216,52 @@ def test_prepare_frame_tiling_used_table(gpu, oracle):
         ug = ft.mark_used(gds, tiles, items_p, items_t, P, q, corr_g, hi_g)
         uo = oracle.mark_used(ogds, ogt, oga, items_p, items_t, tiles, P, q, corr_o, hi_o)
         assert np.array_equal(ug, uo), q
+
+
+def test_prepare_frame_tiling_dev_matches_restatement(gpu, oracle):
+    """tiler_prepare_frame_tiling_dev (PrepareFrameTiling main.pas:3791-3967 on the device: distinct items by bitmap,
+    UseOne's k = 8 preselection, used bitmap, DoPsyV order, descriptors, index) for Fast / Medium / Slow: the
+    keyframe dataset has the restatement's size and the FrameTiling items over it equal oracle.frame_tiling over the
+    oracle's dataset (used table -> build_ft_dataset), bit for bit, with ANN's tie order.  Items include -1 (none)
+    and repeats; the scratch is reused across the three calls."""
+    import torch
+    from tiler_amd import frame_tiling as ft
+    rng = np.random.default_rng(18)
+    P, T = 8, 700
+    pals = synth.palettes(rng, P)
+    pals[1::2] = pals[0::2] ^ rng.integers(0, 2, pals[1::2].shape)  # near-identical pairs: Medium marks both
+    tiles, thm, tvm = synth.tileset(rng, T)
+    cent = synth.palette_centroids(pals)
+    items_t = rng.integers(0, T, 6000).astype(np.int32)
+    items_p = rng.integers(0, P, 6000).astype(np.int32)
+    items_t[::97] = -1
+    dev = torch.device("cuda", 0)
+    d = {k: torch.from_numpy(np.ascontiguousarray(a)).to(dev) for k, a in
+         (("t", items_t), ("p", items_p), ("tiles", tiles), ("thm", thm), ("tvm", tvm), ("pals", pals))}
+    frames = synth.frame_tiles(rng, 1500)
+    gds = ft.prepare_global_ft(tiles)
+    ogds, ogt, oga = oracle.prepare_global_ds(tiles)
+    corr_o, hi_o = oracle.palette_corr(cent)
+    near = ft.near_palettes(cent)
+    assert near.sum() > P  # some palette pairs are near
+    keep = items_t >= 0
+    try:
+        for q in (ft.FT_FAST, ft.FT_MEDIUM, ft.FT_SLOW):
+            kt, info = ft.prepare_frame_tiling_dev(gds, d["t"].data_ptr(), d["p"].data_ptr(), items_t.size,
+                                                   d["tiles"].data_ptr(), d["thm"].data_ptr(), d["tvm"].data_ptr(), T,
+                                                   d["pals"].data_ptr(), P, q, near)
+            torch.cuda.synchronize(dev)
+            uo = oracle.mark_used(ogds, ogt, oga, items_p[keep], items_t[keep], tiles, P, q, corr_o, hi_o)
+            assert info["items"] == np.unique(items_p[keep].astype(np.int64) * T + items_t[keep]).size, q
+            assert info["candidates"] == int(uo.sum()), q
+            ods, ot, op, oa = oracle.build_ft_dataset(uo, tiles, thm, tvm, pals)
+            g = ft.KeyframeTiler.__new__(ft.KeyframeTiler)
+            g.kdt, g.use_wavelets, g.gamma = kt, True, -1
+            got = g.do_frame_tiling(frames)
+            kt.close()
+            o = oracle.frame_tiling(frames, ods, ot, op, oa)
+            assert np.array_equal(got[4].view(np.uint32), o[4].view(np.uint32)), q
+            for a, b in zip(got[:4], o[:4]):
+                assert np.array_equal(a, b), (q, int(np.count_nonzero(a != b)))
+    finally:
+        gds.kdt.close()

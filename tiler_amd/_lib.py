@@ -37,6 +37,10 @@ class SearchStats(ctypes.Structure):
                 ("kd_replayed", ctypes.c_int64), ("flat_queries", ctypes.c_int64)]
 
 
+class PrepareInfo(ctypes.Structure):
+    _fields_ = [("items", ctypes.c_int64), ("candidates", ctypes.c_int64)]
+
+
 _SIGS = {
     "ann_kdtree_create": (c_void_p, [P(P(c_float)), c_int, c_int, c_int, c_int]),
     "ann_kdtree_create_dev": (c_void_p, [c_void_p, c_int, c_int, c_void_p]),
@@ -62,6 +66,9 @@ _SIGS = {
     "tiler_psyv_batch_dev": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                      c_void_p, c_void_p, c_void_p]),
     "tiler_ft_set_maps": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "tiler_prepare_frame_tiling_dev": (c_void_p, [c_void_p, c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p,
+                                                  c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
+                                                  c_void_p, P(PrepareInfo)]),
     "tiler_frame_tiling": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),
     "tiler_frame_tiling_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,

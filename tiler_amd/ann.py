@@ -51,6 +51,17 @@ class KDTree:
             raise TilerError("ann_kdtree_create failed: " + lib.tiler_last_error().decode())
         self.handle = h
 
+    @classmethod
+    def adopt(cls, handle: int, n: int, dd: int) -> "KDTree":
+        """Wrap a handle made by another entry point (tiler_prepare_frame_tiling_dev); destroyed on close."""
+        if not handle:
+            raise TilerError("null ann_kdtree handle: " + load().tiler_last_error().decode())
+        t = cls.__new__(cls)
+        t._lib = load()
+        t.n, t.dd = int(n), int(dd)
+        t.handle = handle
+        return t
+
     def close(self):
         if getattr(self, "handle", None):
             self._lib.ann_kdtree_destroy(self.handle)

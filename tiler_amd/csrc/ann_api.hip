@@ -15,6 +15,7 @@
 #include "../../include/tiler_ann.h"
 #include "dither.hpp"
 #include "palette.hpp"
+#include "prepare.hpp"
 #include "kmeans.hpp"
 #include "detmath.hpp"
 #include "keyframes.hpp"
@@ -172,6 +173,7 @@ struct ann_kdtree {
     int32_t *d_rgb = nullptr, *d_mt = nullptr, *d_mp = nullptr;
     uint8_t *d_mh = nullptr, *d_mv = nullptr;
     size_t cap_ft = 0;
+    PrepScratch *prep = nullptr;  // tiler_prepare_frame_tiling_dev scratch (on the global dataset's handle)
 };
 
 static int ensure_io(ann_kdtree *t, size_t nq, int d, int k) {
@@ -322,8 +324,50 @@ void ann_kdtree_destroy(ann_kdtree *t) {
     hipFree(t->d_mp);
     hipFree(t->d_mh);
     hipFree(t->d_mv);
+    if (t->prep) {
+        prep_scratch_free(t->prep);
+        delete t->prep;
+    }
     if (t->stream) hipStreamDestroy(t->stream);
     delete t;
+}
+
+ann_kdtree *tiler_prepare_frame_tiling_dev(ann_kdtree *global_ds, const int32_t *d_item_tile,
+                                           const int32_t *d_item_pal, int64_t n_items, const uint8_t *d_palpix,
+                                           const uint8_t *d_thm, const uint8_t *d_tvm, int n_tiles,
+                                           const int32_t *d_palettes, int n_palettes, int quality, const uint8_t *near,
+                                           int use_wavelets, int gamma, void *stream, tiler_prepare_info *info) {
+    if (!global_ds || !global_ds->ix || (n_items > 0 && (!d_item_tile || !d_item_pal)) || !d_palpix || !d_thm ||
+        !d_tvm || !d_palettes) {
+        set_error("tiler_prepare_frame_tiling_dev: invalid arguments");
+        return nullptr;
+    }
+    if (!ensure_init()) return nullptr;
+    ann_kdtree *t = new ann_kdtree();
+    if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_error("tiler_prepare_frame_tiling_dev: stream creation failed");
+        delete t;
+        return nullptr;
+    }
+    hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+    long nd = 0, nc = 0;
+    {
+        std::lock_guard<std::mutex> lk(global_ds->ix->mu);  // its k = 8 search scratch and the prepare scratch
+        if (!global_ds->prep) global_ds->prep = new PrepScratch();
+        t->ix = prepare_frame_tiling_dev(global_ds->ix, *global_ds->prep, d_item_tile, d_item_pal, (long)n_items,
+                                         d_palpix, d_thm, d_tvm, n_tiles, d_palettes, n_palettes, quality, near,
+                                         use_wavelets, gamma, s, &nd, &nc);
+    }
+    if (!t->ix) {
+        (void)hipStreamDestroy(t->stream);
+        delete t;
+        return nullptr;
+    }
+    if (info) {
+        info->items = nd;
+        info->candidates = nc;
+    }
+    return t;
 }
 
 int ann_kdtree_search_multi_batch(ann_kdtree *t, const float *q, int nq, int k, float eps, int *idxs, float *errs) {

@@ -41,7 +41,12 @@ def prepare_global_ft(tiles: np.ndarray, active: np.ndarray | None = None) -> Gl
     rows = np.stack([t0, t1, t2, t3], 1).reshape(-1, 64).astype(np.float32)
     tr_tile = np.repeat(idx.astype(np.int32), 4)
     tr_attrs = np.tile(np.array([0, 1, 3, 2], np.uint8), idx.size)
-    return GlobalDS(KDTree(rows), tr_tile, tr_attrs)
+    kdt = KDTree(rows)
+    if tr_tile.size:  # TRToTileIdx / TRToAttrs on the device too (tiler_prepare_frame_tiling_dev reads them)
+        v = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        check(load().tiler_ft_set_maps(kdt.handle, v(tr_tile), v(np.zeros_like(tr_tile)), v(tr_attrs)),
+              "tiler_ft_set_maps")
+    return GlobalDS(kdt, tr_tile, tr_attrs)
 
 
 def palette_corr(centroids: np.ndarray):
@@ -139,3 +144,35 @@ def prepare_frame_tiling(tiles, thm, tvm, palettes, gds: GlobalDS, item_pal, ite
     used = mark_used(gds, tiles, item_pal, item_tile, P, quality, corrs, highest)
     ds = ft_dataset_from_used(used, np.asarray(thm, np.uint8), np.asarray(tvm, np.uint8))
     return KeyframeTiler(tiles, thm, tvm, palettes, ds, use_wavelets, gamma)
+
+
+def near_palettes(palette_centroids, paltol: float = CFT_PALETTE_TOL) -> np.ndarray:
+    """Medium quality's palette pairs (UseOne main.pas:3838-3846): near[p', p] = corr(p', p) < tol * HighestCorr."""
+    corrs, highest = palette_corr(palette_centroids)
+    return np.ascontiguousarray((corrs < paltol * highest).astype(np.uint8))
+
+
+def prepare_frame_tiling_dev(gds: GlobalDS, d_item_tile: int, d_item_pal: int, n_items: int, d_palpix: int,
+                             d_thm: int, d_tvm: int, n_tiles: int, d_palettes: int, n_palettes: int,
+                             quality: int = FT_MEDIUM, near: np.ndarray | None = None, use_wavelets: bool = True,
+                             gamma: int = -1, stream: int = 0):
+    """PrepareFrameTiling main.pas:3791-3967 on the device (tiler_prepare_frame_tiling_dev): the keyframe's
+    tilemap items (HBM int32 pointers) -> UseOne's k = 8 preselection -> used -> DoPsyV dataset -> search handle.
+    Returns (KDTree over the keyframe's candidates with its maps set, {"items", "candidates"})."""
+    from ._lib import PrepareInfo
+    lib = load()
+    info = PrepareInfo()
+    nr = None
+    if quality == FT_MEDIUM:
+        if near is None:
+            raise ValueError("Medium quality needs the near-palette table (near_palettes)")
+        nr = np.ascontiguousarray(near, np.uint8)
+    vp = ctypes.c_void_p
+    h = lib.tiler_prepare_frame_tiling_dev(gds.kdt.handle, vp(d_item_tile), vp(d_item_pal), int(n_items),
+                                           vp(d_palpix), vp(d_thm), vp(d_tvm), int(n_tiles), vp(d_palettes),
+                                           int(n_palettes), int(quality),
+                                           nr.ctypes.data_as(vp) if nr is not None else None, int(use_wavelets),
+                                           int(gamma), vp(stream), ctypes.byref(info))
+    if not h:
+        check(-1, "tiler_prepare_frame_tiling_dev")
+    return KDTree.adopt(h, info.candidates, 192), {"items": int(info.items), "candidates": int(info.candidates)}

@@ -32,6 +32,11 @@ def oracle():
 def gpu():
     """The product library on a real device; a missing library or device is a test failure, not a skip."""
     import tiler_amd
+    try:  # torch's HIP runtime first (tests that hand torch-allocated HBM to libANN.so need it; bench.py's order)
+        import torch
+        torch.cuda.init()
+    except Exception:
+        pass
     lib = tiler_amd.load()
     rc = lib.tiler_init(0)
     assert rc == 0, f"tiler_init failed: {tiler_amd.last_error()}"

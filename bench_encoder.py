@@ -55,19 +55,23 @@ def frame_tiles_gpu(torch, g, n, dev):
     return (px[..., 2] << 16) | (px[..., 1] << 8) | px[..., 0]
 
 
-def keyframe_gpu(torch, g, F, Q, T, dev, change=0.3):
-    """[F, Q, 64] frames and [F, Q] tilemap items (tileset tiles; an item is re-drawn with its frame tile)."""
+def keyframe_gpu(torch, g, F, Q, T, dev, change=0.3, subset=0):
+    """[F, Q, 64] frames and [F, Q] tilemap items (tileset tiles; an item is re-drawn with its frame tile).
+    subset > 0: the keyframe's items come from `subset` random tiles of the set (a shot uses part of the tileset)."""
     fr = torch.empty((F, Q, 64), dtype=torch.int32, device=dev)
     it = torch.empty((F, Q), dtype=torch.int32, device=dev)
+    pool = torch.randperm(T, generator=g, device=dev)[:subset].int() if subset else None
+    draw = (lambda n: pool[torch.randint(0, subset, (n,), generator=g, device=dev)]) if subset else \
+        (lambda n: torch.randint(0, T, (n,), generator=g, device=dev, dtype=torch.int32))
     fr[0] = frame_tiles_gpu(torch, g, Q, dev)
-    it[0] = torch.randint(0, T, (Q,), generator=g, device=dev, dtype=torch.int32)
+    it[0] = draw(Q)
     for f in range(1, F):
         sel = torch.rand(Q, generator=g, device=dev) < change
         fr[f] = fr[f - 1]
         it[f] = it[f - 1]
         n = int(sel.sum().item())
         fr[f][sel] = frame_tiles_gpu(torch, g, n, dev)
-        it[f][sel] = torch.randint(0, T, (n,), generator=g, device=dev, dtype=torch.int32)
+        it[f][sel] = draw(n)
     return fr, it
 
 
@@ -80,6 +84,8 @@ def main():
     ap.add_argument("--tileset", type=int, default=65536)
     ap.add_argument("--palettes", type=int, default=128)
     ap.add_argument("--quality", type=int, default=1, help="0 Fast, 1 Medium (the reference default), 2 Slow")
+    ap.add_argument("--item-tiles", type=int, default=0,
+                    help="tiles a keyframe's items are drawn from (0: the whole tileset, uniformly)")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-smooth", action="store_true")
     ap.add_argument("--check-kf", type=int, default=1, help="keyframe re-checked against the restatement (-1: none)")
@@ -119,7 +125,7 @@ def main():
     g.manual_seed(args.seed)
     frames, items_t, items_p = [], [], []
     for k in range(nkf):
-        fr, it = keyframe_gpu(torch, g, starts[k + 1] - starts[k], Q, T, dev)
+        fr, it = keyframe_gpu(torch, g, starts[k + 1] - starts[k], Q, T, dev, subset=args.item_tiles)
         frames.append(fr)
         items_t.append(it)
         items_p.append(d_tpal[it.long()].int())
@@ -136,6 +142,7 @@ def main():
                       ("err", torch.float32))})
     sm = [None] * nkf
     times = {"prepare": [], "ft_smooth": []}
+    stats_kf = {}
     info_all = []
 
     def prepare(k, gds, stream):
@@ -169,6 +176,8 @@ def main():
             sm[k] = st
         s_ft.synchronize()
         times["ft_smooth"].append(time.perf_counter() - t0)
+        if k == args.check_kf or (k == 0 and args.check_kf < 0):
+            stats_kf.update(kt.stats())
 
     def run_clip():
         times["prepare"].clear()
@@ -210,7 +219,9 @@ def main():
     nkf = warm_n
     run_clip()
     nkf = _nkf
+    print("[bench_encoder] warm-up pass done", file=sys.stderr, flush=True)
     wall, t_global = run_clip()
+    print(f"[bench_encoder] clip: {wall:.3f} s", file=sys.stderr, flush=True)
     tiles_total = args.frames * Q
     value = tiles_total / wall / 1e6
     cand = [i["candidates"] for i in info_all]
@@ -223,9 +234,11 @@ def main():
            "ft_smooth_ms_avg": round(1e3 * float(np.mean(times["ft_smooth"])), 3),
            "items_avg": round(float(np.mean([i["items"] for i in info_all])), 1),
            "candidates_avg": round(float(np.mean(cand)), 1), "candidates_min": int(min(cand)),
-           "candidates_max": int(max(cand)), "data": "synthetic, generated in HBM before timing",
+           "candidates_max": int(max(cand)), "search_stats_one_keyframe": stats_kf,
+           "data": "synthetic, generated in HBM before timing",
            "config": {"workload": f"{W}x{H}, {args.frames} frames, {args.kf_len}-frame keyframes, {T}-tile set, "
-                                  f"{P} palettes"}}
+                                  f"{P} palettes, items from "
+                                  f"{args.item_tiles or T} tiles per keyframe"}}
 
     # ---- re-check one keyframe against the CPU restatement (after the timed region) ----
     ck = args.check_kf
@@ -237,11 +250,16 @@ def main():
         ip = items_p[ck].cpu().numpy().ravel()
         g_ds, g_tile, g_attr = oracle.prepare_global_ds(tiles)
         corrs, highest = oracle.palette_corr(cents)
+        say = lambda m: print(f"[bench_encoder] check: {m} ({time.perf_counter() - t0:.1f} s)", file=sys.stderr,
+                              flush=True)  # noqa: E731
         used = oracle.mark_used(g_ds, g_tile, g_attr, ip, it, tiles, P, args.quality, corrs, highest)
+        say("used table")
         ods, ot, op, oa = oracle.build_ft_dataset(used, tiles, thm, tvm, pals)
+        say("dataset")
         fr = frames[ck].cpu().numpy().reshape(-1, 64)
         pick = np.random.default_rng(5).choice(fr.shape[0], min(args.check_queries, fr.shape[0]), replace=False)
         o = oracle.frame_tiling(fr[pick], ods, ot, op, oa)
+        say("frame tiling")
         go = {nm: outs[ck][nm].cpu().numpy() for nm in ("tile", "pal", "hm", "vm", "err")}
         mism = int(np.count_nonzero((go["tile"][pick] != o[0]) | (go["pal"][pick] != o[1]) |
                                     (go["hm"][pick] != o[2]) | (go["vm"][pick] != o[3]) |

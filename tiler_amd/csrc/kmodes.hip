@@ -25,6 +25,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_cooperative_groups.h>
+
 #include "kmodes.hpp"
 
 namespace tiler {
@@ -696,6 +698,10 @@ __global__ __launch_bounds__(256) void kmb_init_modes2(KmBatch B, const int32_t 
     }
 }
 
+// each host work item (<= 64 centroids) runs as KM_ASUB workgroups of a quarter of its centroids: the late
+// chunk steps hold one large bin alone, where one workgroup per item left ~1 wave per SIMD (latency-bound)
+static constexpr int KM_ASUB = 4;
+
 // one 960-point chunk of each listed bin, applied in order (KModesIter kmodes.pas:869-911)
 struct KmSeqItem {
     int bin, p0, p1, pad;
@@ -707,6 +713,167 @@ __global__ __launch_bounds__(NT) void kmb_seq_strided(KmBatch B, const KmAsgItem
     const KmSeqItem it = *reinterpret_cast<const KmSeqItem *>(items + blockIdx.x);
     KmState s = bin_state(B, it.bin);
     bin_seq_body<NT>(s, it.p0, it.p1);
+}
+
+// ---- cooperative forms: one launch per phase instead of one per farthest-first round / chunk step ----
+// The farthest-first rounds and the chunk steps of an iteration are sequential by definition (round j + 1 needs
+// centre j + 1; chunk c + 1 is assigned against the modes chunk c leaves), and with one launch each the largest
+// bin's chain was launch-bound (C4: 5,035 rounds at ~40 us, 2 x 247 chunk launches per iteration).  One cooperative
+// launch (hipLaunchCooperativeKernel: every workgroup resident) runs the whole chain, a grid barrier between
+// dependent phases; the per-item work is that of the one-shot kernels (same items, same order-independent merges:
+// block maxima, atomicMin keys), so results are identical.
+namespace cg = cooperative_groups;
+static constexpr int KM_COOP_NT = 512;
+
+// farthest-first, every alive bin's item (bin, sub): mind update + the item's argmax candidate -> part[sub]
+__device__ void ff_coop_item(const KmBatch &B, const KmFfItem &it, int j, unsigned long long *best) {
+    constexpr int NT = KM_COOP_NT;
+    KmState s = bin_state(B, it.bin);
+    const int c = s.center[j];
+    uint32_t item[20];
+    load_row(s.X + (long)c * KM_A, item);
+    unsigned long long bv = 0;
+    int bi = -1;
+    for (long i = (long)it.sub * NT + threadIdx.x; i < s.n; i += (long)it.nsub * NT) {
+        uint32_t row[20];
+        load_row(s.X + i * KM_A, row);
+        const unsigned long long d = km_dissim(row, item);
+        unsigned long long m = s.mind[i];
+        if (d < m) {
+            m = d;
+            s.mind[i] = m;
+        }
+        if (!s.used[i] && m >= bv) {
+            bv = m;
+            bi = (int)i;
+        }
+    }
+    const unsigned long long v32 = bv > 0xFFFFFFFFull ? 0xFFFFFFFFull : bv;
+    best[threadIdx.x] = (bi < 0) ? 0ull : ((v32 << 32) | (unsigned)(bi + 1));
+    __syncthreads();
+    for (int o = NT / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) best[threadIdx.x] = max(best[threadIdx.x], best[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) s.part[it.sub] = best[0];
+    __syncthreads();  // best[] is reused by the next item
+}
+
+// farthest-first selection of centre j + 1 of bin r from its items' candidates
+__device__ void ff_coop_select(const KmBatch &B, int r, int nsub, int j, unsigned long long *best) {
+    constexpr int NT = KM_COOP_NT;
+    KmState s = bin_state(B, r);
+    unsigned long long bb = 0;
+    for (int i = threadIdx.x; i < nsub; i += NT) bb = max(bb, s.part[i]);
+    best[threadIdx.x] = bb;
+    __syncthreads();
+    for (int o = NT / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) best[threadIdx.x] = max(best[threadIdx.x], best[threadIdx.x + o]);
+        __syncthreads();
+    }
+    const unsigned long long w = best[0];
+    __syncthreads();
+    const int f = (w == 0) ? -1 : (int)(w & 0xFFFFFFFFull) - 1;
+    if (f < 0) {
+        if (threadIdx.x == 0) *s.err = 1;
+        return;
+    }
+    if (threadIdx.x < KM_A) s.cent[(long)(j + 1) * KM_A + threadIdx.x] = s.X[(long)f * KM_A + threadIdx.x];
+    if (threadIdx.x == 0) {
+        s.center[j + 1] = f;
+        s.used[f] = 1;
+    }
+}
+
+// InitFarthestFirst for every bin, rounds 0 .. Kmax - 1 (bins sorted by K descending: the alive ones are a prefix;
+// ff_end[a] = items of the first a bins)
+__global__ __launch_bounds__(KM_COOP_NT) void kmb_ff_coop(KmBatch B, const KmFfItem *items, const int *ff_end,
+                                                         int Kmax) {
+    __shared__ unsigned long long best[KM_COOP_NT];
+    cg::grid_group g = cg::this_grid();
+    int alive = B.nb;
+    for (int j = 0; j < Kmax; j++) {
+        while (alive > 0 && B.koff[alive] - B.koff[alive - 1] <= j) alive--;
+        const int nit = ff_end[alive];
+        for (int u = blockIdx.x; u < nit; u += gridDim.x) ff_coop_item(B, items[u], j, best);
+        g.sync();
+        for (int r = blockIdx.x; r < alive; r += gridDim.x)
+            if (j + 1 < B.koff[r + 1] - B.koff[r]) ff_coop_select(B, r, B.poff[r + 1] - B.poff[r], j, best);
+        g.sync();
+    }
+}
+
+// one assignment unit: up to NT points of an item vs the sub-th of KM_ASUB slices of its centroids
+template <int NT>
+__device__ void assign_unit(const KmBatch &B, KmAsgItem it, int sub, int nsub, uint4 *ct) {
+    const int per = (it.c1 - it.c0 + nsub - 1) / nsub;
+    it.c0 += sub * per;
+    it.c1 = min(it.c1, it.c0 + per);
+    if (it.c0 >= it.c1) return;  // uniform over the workgroup
+    KmState s = bin_state(B, it.bin);
+    const long i = it.p0 + threadIdx.x;
+    const bool valid = i < it.p1;
+    uint32_t item[20];
+    if (valid) load_row(s.X + i * KM_A, item);
+    unsigned long long best = ~0ull;
+    for (int t0 = it.c0; t0 < it.c1; t0 += 128) {
+        const int cnt = min(128, it.c1 - t0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < cnt * 5; e += NT) ct[e] = reinterpret_cast<const uint4 *>(s.cent + (long)t0 * KM_A)[e];
+        __syncthreads();
+        if (valid) {
+            for (int c = 0; c < cnt; c++) {
+                uint32_t row[20];
+#pragma unroll
+                for (int q = 0; q < 5; q++) {
+                    const uint4 v = ct[c * 5 + q];
+                    row[4 * q] = v.x;
+                    row[4 * q + 1] = v.y;
+                    row[4 * q + 2] = v.z;
+                    row[4 * q + 3] = v.w;
+                }
+                const unsigned long long d = km_dissim(row, item);
+                const unsigned long long key = (d << 32) | (0xFFFFFFFFu - (unsigned)(t0 + c));
+                best = key < best ? key : best;
+            }
+        }
+    }
+    if (valid) atomicMin(&s.akey[i], best);
+    __syncthreads();  // ct[] is reused by the next unit
+}
+
+// one KModesIter pass of every listed bin: per chunk step, the assignment units of every bin's chunk against the
+// current modes, barrier, each bin's chunk moves in order (bin_seq_body, one workgroup per bin), barrier
+struct KmStep {
+    int pos, na, ns, pad;  // items [pos, pos + na): assignment (KM_ASUB units each), [pos + na, + ns): seq
+};
+__global__ __launch_bounds__(KM_COOP_NT) void kmb_iter_coop(KmBatch B, const KmAsgItem *items, const KmStep *steps,
+                                                           int nsteps) {
+    __shared__ uint4 ct[128 * 5];
+    cg::grid_group g = cg::this_grid();
+    for (int st = 0; st < nsteps; st++) {
+        const KmStep sp = steps[st];
+        for (int u = blockIdx.x; u < sp.na * KM_ASUB; u += gridDim.x)
+            assign_unit<KM_COOP_NT>(B, items[sp.pos + u / KM_ASUB], u % KM_ASUB, KM_ASUB, ct);
+        g.sync();
+        for (int u = blockIdx.x; u < sp.ns; u += gridDim.x) {
+            const KmSeqItem it = *reinterpret_cast<const KmSeqItem *>(items + sp.pos + sp.na + u);
+            bin_seq_body<KM_COOP_NT>(bin_state(B, it.bin), it.p0, it.p1);
+            __syncthreads();
+        }
+        g.sync();
+    }
+}
+
+// resident workgroups of a cooperative K-Modes kernel (0: cooperative launch unavailable)
+static int coop_grid(const void *kernel) {
+    int dev = 0, coop = 0, ncu = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess || !coop ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, KM_COOP_NT, 0) != hipSuccess || per <= 0)
+        return 0;
+    return ncu * std::min(per, 2);
 }
 
 // ---- DoKModes medoid choice (main.pas:4231-4253): per cluster j with members, the member minimising
@@ -731,9 +898,6 @@ __global__ __launch_bounds__(256) void kmb_medoid(const uint8_t *X, const int32_
 // centroid splits of an assignment block: ~64 centroids per block, so a chunk of the largest bin alone
 // still spreads over the chip (results merge by atomicMin)
 static int csplit_of(int K) { return std::max(1, std::min(128, (K + 63) / 64)); }
-// each host work item (<= 64 centroids) runs as KM_ASUB workgroups of a quarter of its centroids: the late
-// chunk steps hold one large bin alone, where one workgroup per item left ~1 wave per SIMD (latency-bound)
-static constexpr int KM_ASUB = 4;
 
 int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const int32_t *h_k, const int32_t *h_start,
                      int n_modalities, int32_t *d_labels, uint8_t *d_centroids, int32_t *h_iter, uint64_t *h_cost,
@@ -794,7 +958,17 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
         max_items += (size_t)nch * ((KM_BIN + 255) / 256) * csplit_of(Kv[r]) + nch;
         max_items += (size_t)((nv[r] + 255) / 256) * csplit_of(Kv[r]);
     }
-    const size_t item_bytes = (max_items + (size_t)poff[nb] + 64) * sizeof(KmAsgItem);
+    int max_chunks = 0;
+    for (int r = 0; r < nb; r++) max_chunks = std::max(max_chunks, (nv[r] + KM_BIN - 1) / KM_BIN);
+    const size_t item_bytes = (max_items + (size_t)poff[nb] + 64) * sizeof(KmAsgItem) +
+                              ((size_t)max_chunks + 1) * sizeof(KmStep) + (size_t)(nb + 1) * 4 + 256;
+#ifdef TILER_EXPERIMENTS
+    static const bool no_coop = getenv("TILER_KM_COOP") && atoi(getenv("TILER_KM_COOP")) == 0;  // A/B
+#else
+    constexpr bool no_coop = false;
+#endif
+    const int g_ff = no_coop ? 0 : coop_grid((const void *)kmb_ff_coop);
+    const int g_it = no_coop ? 0 : coop_grid((const void *)kmb_iter_coop);
     TILER_HIP_CHECK(hipMalloc((void **)&buf, off + item_bytes));
     char *items = buf + o_items;
     KmBatch B;
@@ -856,12 +1030,28 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                 for (int sb = 0; sb < ns; sb++) ff.push_back({r, sb, ns, 0});
                 ff_end[r + 1] = (int)ff.size();
             }
-            if (upload(ff.data(), ff.size() * sizeof(KmFfItem))) goto fail;
-            KTimer tm("kmodes_init", st);
-            int alive = nb;
-            for (int j = 0; j < Kv[0]; j++) {
-                while (alive > 0 && Kv[alive - 1] <= j) alive--;
-                hipLaunchKernelGGL(kmb_ff_round, dim3(ff_end[alive]), dim3(256), 0, st, B, (const KmFfItem *)items, j);
+            if (g_ff > 0) {  // one cooperative launch for every round (items of KM_COOP_NT-point strides)
+                const size_t fb = ff.size() * sizeof(KmFfItem);
+                std::vector<char> up(fb + (nb + 1) * 4);
+                memcpy(up.data(), ff.data(), fb);
+                memcpy(up.data() + fb, ff_end.data(), (nb + 1) * 4);
+                if (upload(up.data(), up.size())) goto fail;
+                const KmFfItem *d_items = (const KmFfItem *)items;
+                const int *d_end = (const int *)(items + fb);
+                int kmax = Kv[0];
+                void *args[] = {&B, &d_items, &d_end, &kmax};
+                KTimer tm("kmodes_init", st);
+                if (hipLaunchCooperativeKernel((const void *)kmb_ff_coop, dim3(g_ff), dim3(KM_COOP_NT), args, 0, st) !=
+                    hipSuccess)
+                    goto fail;
+            } else {
+                if (upload(ff.data(), ff.size() * sizeof(KmFfItem))) goto fail;
+                KTimer tm("kmodes_init", st);
+                int alive = nb;
+                for (int j = 0; j < Kv[0]; j++) {
+                    while (alive > 0 && Kv[alive - 1] <= j) alive--;
+                    hipLaunchKernelGGL(kmb_ff_round, dim3(ff_end[alive]), dim3(256), 0, st, B, (const KmFfItem *)items, j);
+                }
             }
         }
         if (hipGetLastError() != hipSuccess) goto fail;
@@ -897,6 +1087,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                 // work list of this iteration: per chunk step c, the assign items then the seq items
                 std::vector<KmAsgItem> wl;
                 std::vector<std::pair<int, int>> steps;  // (assign items, seq items) per chunk step
+                const int qstep = g_it > 0 ? KM_COOP_NT : 256;  // points per assignment item
                 int maxch = 0;
                 for (int r : active) maxch = std::max(maxch, (nv[r] + KM_BIN - 1) / KM_BIN);
                 for (int c = 0; c < maxch; c++) {
@@ -905,9 +1096,9 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                         const int p0 = c * KM_BIN;
                         if (p0 >= nv[r]) continue;
                         const int p1 = std::min(nv[r], p0 + KM_BIN), cs = csplit_of(Kv[r]), per = (Kv[r] + cs - 1) / cs;
-                        for (int q0 = p0; q0 < p1; q0 += 256)
+                        for (int q0 = p0; q0 < p1; q0 += qstep)
                             for (int cc = 0; cc < cs; cc++, na++)
-                                wl.push_back({r, q0, std::min(p1, q0 + 256), cc * per, std::min(Kv[r], (cc + 1) * per), {0, 0, 0}});
+                                wl.push_back({r, q0, std::min(p1, q0 + qstep), cc * per, std::min(Kv[r], (cc + 1) * per), {0, 0, 0}});
                     }
                     for (int r : active) {
                         const int p0 = c * KM_BIN;
@@ -919,14 +1110,39 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     }
                     steps.push_back({na, ns});
                 }
-                if (upload(wl.data(), wl.size() * sizeof(KmAsgItem))) goto fail;
+                std::vector<KmStep> ksteps;
+                {
+                    int pos = 0;
+                    for (const auto &sp : steps) {
+                        ksteps.push_back({pos, sp.first, sp.second, 0});
+                        pos += sp.first + sp.second;
+                    }
+                }
+                const size_t wb = wl.size() * sizeof(KmAsgItem);
+                if (g_it > 0) {
+                    std::vector<char> up(wb + ksteps.size() * sizeof(KmStep));
+                    memcpy(up.data(), wl.data(), wb);
+                    memcpy(up.data() + wb, ksteps.data(), ksteps.size() * sizeof(KmStep));
+                    if (upload(up.data(), up.size())) goto fail;
+                } else if (upload(wl.data(), wb)) {
+                    goto fail;
+                }
                 for (int r : active) {
                     iters[r]++;
                     if (hipMemsetAsync(B.cost + r, 0, 8, st) != hipSuccess || hipMemsetAsync(B.moves + r, 0, 4, st) != hipSuccess)
                         goto fail;
                     if (hipMemsetAsync(B.akey + boff[r], 0xff, (size_t)nv[r] * 8, st) != hipSuccess) goto fail;
                 }
-                {
+                if (g_it > 0) {
+                    const KmAsgItem *d_items = (const KmAsgItem *)items;
+                    const KmStep *d_steps = (const KmStep *)(items + wb);
+                    int nst = (int)ksteps.size();
+                    void *args[] = {&B, &d_items, &d_steps, &nst};
+                    KTimer tm("kmodes_seq", st);
+                    if (hipLaunchCooperativeKernel((const void *)kmb_iter_coop, dim3(g_it), dim3(KM_COOP_NT), args, 0, st) !=
+                        hipSuccess)
+                        goto fail;
+                } else {
                     size_t pos = 0;
                     for (const auto &sp : steps) {
                         {

@@ -110,6 +110,6 @@ def test_smooth_c5_size_default_strength(gpu, oracle):
     cols = np.sort(rng.choice(Q, 6000, replace=False))
     sub = lambda a: np.ascontiguousarray(a[:, cols])  # noqa: E731
     o = oracle.smooth(sub(tile), sub(pal), sub(hm), sub(vm), sub(sm), palpix, pals, 0.02)
-    for a, b in zip(g, o):
-        assert np.array_equal(sub(np.asarray(a)), b)
+    for a, b in zip(g[:5], o[:5]):  # items and flags (tmpidx: None on both sides)
+        assert np.array_equal(sub(a), b)
     assert g[4].sum() > 0 and sub(np.asarray(g[4])).sum() > 0  # the default strength does merge here

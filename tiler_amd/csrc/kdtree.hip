@@ -1,27 +1,24 @@
 // kdtree.hip -- ANN 1.1.2 kd-tree (ANN_KD_STD) build over an HBM dataset + the pruning check / exact replay
 // that make the MFMA search return ANN's own answer among equal distances (kdtree.hpp).
 //
-// Build, level by level (every node of a level at once):
+// Build, level by level (every node of a level at once), entirely on the device (the shape is implicit, so the host
+// plans every level before any data exists; nothing comes back until the tree is done):
 //   big nodes (> KD_CH points): kd_spread_big_kernel, one wave per KD_CH-point chunk, per-dimension min / max
 //                      (annSpread) folded into the node with order-preserving integer atomics; kd_select_big_kernel
 //                      picks cut_dim = first maximum of max - min (fp32, annMaxSpread); kd_gather_kernel writes
 //                      the node's cut-dimension keys in pidx order, one wave per chunk
 //   small nodes:       kd_small_kernel, one wave per node does all three
-//   (host)             annMedianSplit's quickselect on each node's (key, index) pairs, bit for bit: the
-//                      permutation it leaves decides which of several equal keys go LO, and so the rest of the
-//                      tree; the nodes of a level run on a persistent host thread pool (a level is O(n) work)
-// The rows never leave HBM: per level only the n keys (4 B each) come to the host and the new order goes back.
+//   kd_median_big_kernel: annMedianSplit's quickselect on each node's (key, index) pairs by a workgroup, bit for bit
+//                      (Hoare's partition ranked in parallel): the permutation it leaves decides which of several equal
+//                      keys go LO, and so the rest of the tree
+//   subtrees of <= KD_SUB points: kd_subtree_waves_kernel, one workgroup each; then the cell bounds and positions
 #include <float.h>
 #include <math.h>
 #include <string.h>
 
 #include <algorithm>
-#include <atomic>
 #include <chrono>
-#include <condition_variable>
-#include <functional>
 #include <mutex>
-#include <thread>
 #include <vector>
 
 #include "kdorder_dev.hpp"
@@ -197,56 +194,207 @@ __global__ __launch_bounds__(256) void kd_small_kernel(const float *__restrict__
     for (int i = N.s + lane; i < N.e; i += 64) keys[i] = rows[(long)pidx[i] * dd + cd];
 }
 
-// annMedianSplit (kd_util.cpp) on one node's (key, index) pairs, key[i] = PA(i, cut_dim): the same pivot choice,
-// partition scans and swaps, then the largest low-side key moved to n_lo - 1; returns cut_val.
-static float median_split_host(float *key, int *idx, int n, int n_lo) {
-    auto sw = [&](int a, int b) {
-        std::swap(key[a], key[b]);
-        std::swap(idx[a], idx[b]);
-    };
-    int l = 0, r = n - 1;
-    while (l < r) {
-        int i = (r + l) / 2, k;
-        if (key[i] > key[r]) sw(i, r);
-        sw(l, i);
-        const float c = key[l];
-        i = l;
-        k = r;
-        for (;;) {
-            while (key[++i] < c) {
-            }
-            while (key[--k] > c) {
-            }
-            if (i < k)
-                sw(i, k);
-            else
-                break;
+// annMedianSplit (kd_util.cpp) on one big node's (key, index) pairs, key[i] = PA(i, cut_dim), by a whole workgroup
+// (round 3; until then a host thread ran it per node, with the keys round-tripped every level).  Sequentially:
+//     l = 0, r = n-1; while l < r: i = (l+r)/2; if key[i] > key[r] swap(i, r); swap(l, i); c = key[l];
+//       i = l, k = r; loop { while key[++i] < c; while key[--k] > c; if i < k swap(i, k) else break }; swap(l, k);
+//       k > n_lo -> r = k-1, k < n_lo -> l = k+1, else stop
+//     then the first maximum of key[0..n_lo) swapped to n_lo - 1; cut_val = (key[n_lo-1] + key[n_lo]) / 2.
+// Hoare's partition is data-parallel.  With the pivot c, the i-scan stops at the "left stoppers" of the ORIGINAL
+// array (p in (l, r] with key[p] >= c, ascending L_1 < L_2 < ...; key[r] >= c ends it) and the k-scan at the "right
+// stoppers" (p in [l, r) with key[p] <= c, descending R_1 > R_2 > ...; key[l] = c ends it): positions the scans
+// still have to cross are untouched by earlier swaps, and a swapped position stops the scan that reaches it next,
+// exactly at the point where the loop then ends.  So the loop swaps the pairs (L_j, R_j) with L_j < R_j -- a prefix
+// j < J, since L ascends and R descends -- and stops with k = R_J (J = 1) or max(R_J, L_{J-1}).  L_j < R_j iff the
+// number of right stoppers above L_j is >= j, which each lane decides from the ranks alone.  Per iteration: each wave
+// ranks a contiguous segment by ballots (two passes), writes the stoppers' positions by rank, the J-1 swaps run in
+// parallel (their positions are distinct), then swap(l, k).  Same comparisons, same permutation, same cut value.
+static constexpr int KD_MW = 16;  // waves per big-node workgroup
+__device__ __forceinline__ void kd_swap(float *kk, int *ii, int a, int b) {
+    const float tk = kk[a];
+    kk[a] = kk[b];
+    kk[b] = tk;
+    const int ti = ii[a];
+    ii[a] = ii[b];
+    ii[b] = ti;
+}
+
+__global__ __launch_bounds__(64 * KD_MW) void kd_median_big_kernel(float *__restrict__ keys, int *__restrict__ pidx,
+                                                                   const KdNodeDev *__restrict__ nodes,
+                                                                   const int *__restrict__ cut_dim,
+                                                                   int *__restrict__ lpos, int *__restrict__ rpos,
+                                                                   int *__restrict__ cd_out, float *__restrict__ cv_out) {
+    __shared__ int s_l, s_r;
+    __shared__ float s_c;
+    __shared__ int wl[KD_MW], wr[KD_MW], wp[KD_MW];
+    __shared__ float wv[KD_MW];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const KdNodeDev N = nodes[blockIdx.x];
+    float *kk = keys + N.s;
+    int *ii = pidx + N.s, *Lp = lpos + N.s, *Rp = rpos + N.s;
+    const int n = N.e - N.s, n_lo = n / 2;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    if (tid == 0) {
+        s_l = 0;
+        s_r = n - 1;
+    }
+    __syncthreads();
+    for (;;) {
+        const int l = s_l, r = s_r;  // uniform: read after the barrier
+        if (l >= r) break;
+        if (tid == 0) {
+            const int i = (r + l) / 2;
+            if (kk[i] > kk[r]) kd_swap(kk, ii, i, r);
+            kd_swap(kk, ii, l, i);
+            s_c = kk[l];
         }
-        sw(l, k);
-        if (k > n_lo)
-            r = k - 1;
-        else if (k < n_lo)
-            l = k + 1;
-        else
-            break;
-    }
-    if (n_lo > 0) {
-        float c = key[0];
-        int k = 0;
-        for (int i = 1; i < n_lo; i++)
-            if (key[i] > c) {
-                c = key[i];
-                k = i;
+        __syncthreads();
+        const float c = s_c;
+        const int seg = (r - l + KD_MW) / KD_MW;  // ceil((r - l + 1) / KD_MW)
+        const int a0 = l + w * seg, a1 = min(r + 1, a0 + seg);
+        int nl = 0, nr = 0;
+        for (int p0 = a0; p0 < a1; p0 += 64) {
+            const int p = p0 + lane;
+            const float v = p < a1 ? kk[p] : 0.0f;
+            nl += __popcll(__ballot(p < a1 && p > l && v >= c));
+            nr += __popcll(__ballot(p < a1 && p < r && v <= c));
+        }
+        if (lane == 0) {
+            wl[w] = nl;
+            wr[w] = nr;
+        }
+        __syncthreads();
+        int bl = 0, br = 0, tot_r = 0;
+        for (int x = 0; x < KD_MW; x++) {
+            if (x < w) {
+                bl += wl[x];
+                br += wr[x];
             }
-        sw(n_lo - 1, k);
+            tot_r += wr[x];
+        }
+        int np = 0;
+        for (int p0 = a0; p0 < a1; p0 += 64) {
+            const int p = p0 + lane;
+            const float v = p < a1 ? kk[p] : 0.0f;
+            const bool isl = p < a1 && p > l && v >= c, isr = p < a1 && p < r && v <= c;
+            const unsigned long long bL = __ballot(isl), bR = __ballot(isr);
+            const int jl = bl + __popcll(bL & below) + 1;  // rank from the left (1-based)
+            const int rb = br + __popcll(bR & below);      // right stoppers below p
+            if (isl) Lp[jl - 1] = p;
+            if (isr) Rp[tot_r - rb - 1] = p;  // rank from the right: tot_r - rb
+            if (isl && tot_r - rb - (isr ? 1 : 0) >= jl) np++;  // R_jl > p: pair jl is swapped
+            bl += __popcll(bL);
+            br += __popcll(bR);
+        }
+        for (int o = 32; o > 0; o >>= 1) np += __shfl_xor(np, o, 64);
+        if (lane == 0) wp[w] = np;
+        __syncthreads();
+        np = 0;
+        for (int x = 0; x < KD_MW; x++) np += wp[x];
+        for (int j = tid; j < np; j += 64 * KD_MW) kd_swap(kk, ii, Lp[j], Rp[j]);
+        __syncthreads();
+        if (tid == 0) {
+            int k = Rp[np];  // R_J, J = np + 1 (<= tot_r: position l is the last right stopper, never paired)
+            if (np > 0) k = max(k, Lp[np - 1]);
+            kd_swap(kk, ii, l, k);
+            if (k > n_lo)
+                s_r = k - 1;
+            else if (k < n_lo)
+                s_l = k + 1;
+            else
+                s_l = s_r = k;
+        }
+        __syncthreads();
     }
-    return (float)(((double)(key[n_lo - 1] + key[n_lo])) / 2.0);
+    // the first maximum of kk[0..n_lo) to n_lo - 1
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = tid; i < n_lo; i += 64 * KD_MW) {
+        const float v = kk[i];
+        if (v > bv || bi == 0x7fffffff) {  // a thread's indices ascend: strict > keeps its first
+            bv = v;
+            bi = i;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (oi != 0x7fffffff && (bi == 0x7fffffff || ov > bv || (ov == bv && oi < bi))) {
+            bv = ov;
+            bi = oi;
+        }
+    }
+    if (lane == 0) {
+        wv[w] = bv;
+        wp[w] = bi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int k = 0x7fffffff;
+        float c = -INFINITY;
+        for (int x = 0; x < KD_MW; x++)
+            if (wp[x] != 0x7fffffff && (k == 0x7fffffff || wv[x] > c || (wv[x] == c && wp[x] < k))) {
+                c = wv[x];
+                k = wp[x];
+            }
+        if (n_lo > 0) kd_swap(kk, ii, n_lo - 1, k);
+        const int m = N.s + n_lo;
+        cd_out[m] = cut_dim[blockIdx.x];
+        cv_out[m] = (float)(((double)(kk[n_lo - 1] + kk[n_lo])) / 2.0);
+    }
+}
+
+// ANNkd_split::cd_bnds of every internal node (rkd_tree: the LO child descends with bnd_box.hi[cd] = cv, the HI child
+// with .lo[cd] = cv; the node records lo[cd] / hi[cd] on entry): one thread per position p, two root walks -- find
+// the node split at p and its cut dimension, then apply the ancestors cutting that dimension, root first.
+__global__ __launch_bounds__(256) void kd_bounds_kernel(int n, int bs, const int *__restrict__ cd,
+                                                        const float *__restrict__ cv, const float *__restrict__ box,
+                                                        int dd, float *__restrict__ lo_out, float *__restrict__ hi_out) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    int s = 0, e = n;
+    bool found = false;
+    while (e - s > bs) {
+        const int m = s + (e - s) / 2;
+        if (p == m) {
+            found = true;
+            break;
+        }
+        if (p < m)
+            e = m;
+        else
+            s = m;
+    }
+    if (!found) return;
+    const int c = cd[p];
+    float lo = box[c], hi = box[dd + c];
+    s = 0;
+    e = n;
+    for (;;) {
+        const int m = s + (e - s) / 2;
+        if (m == p) break;
+        const bool same = cd[m] == c;
+        if (p < m) {
+            if (same) hi = cv[m];
+            e = m;
+        } else {
+            if (same) lo = cv[m];
+            s = m;
+        }
+    }
+    lo_out[p] = lo;
+    hi_out[p] = hi;
+}
+
+__global__ __launch_bounds__(256) void kd_pos_kernel(int n, const int *__restrict__ pidx, int *__restrict__ pos) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) pos[pidx ? pidx[i] : i] = i;  // pidx null: the identity (SkeletonTree's pidx[i] = i)
 }
 
 // A whole subtree of <= KD_SUB points per workgroup, entirely on the device: for every node (explicit stack) the
 // annSpread / annMaxSpread cut dimension (threads over dimensions, rows read coalesced), the node's keys into LDS
 // and annMedianSplit's quickselect by one thread on the LDS copy -- the same comparisons, swaps and cut value as
-// median_split_host -- so the subtree's permutation, cut dimensions and cut values are ANN's.
+// kd_median_big_kernel -- so the subtree's permutation, cut dimensions and cut values are ANN's.
 static constexpr int KD_SUB = 1024;
 
 #ifdef TILER_EXPERIMENTS  // round-1 subtree kernel, kept for A/B (TILER_KD_SUB_OLD)
@@ -541,75 +689,6 @@ void kd_tree_destroy(KdTree *t) {
     delete t;
 }
 
-// Persistent host workers for the per-level quickselects (thread start-up per level would cost more than a
-// deep level's work).  run(count, f): f(i) for every i < count, items claimed in order (callers sort big first).
-class HostPool {
-  public:
-    static HostPool &get() {
-        static HostPool p;
-        return p;
-    }
-    void run(int count, const std::function<void(int)> &f) {
-        if (count <= 0) return;
-        if (count == 1 || workers_.empty()) {
-            for (int i = 0; i < count; i++) f(i);
-            return;
-        }
-        std::unique_lock<std::mutex> lk(mu_);
-        fn_ = &f;
-        count_ = count;
-        next_.store(0);
-        busy_ = (int)workers_.size();
-        gen_++;
-        cv_.notify_all();
-        lk.unlock();
-        drain();
-        lk.lock();
-        done_cv_.wait(lk, [&] { return busy_ == 0; });
-        fn_ = nullptr;
-    }
-
-  private:
-    HostPool() {
-        const unsigned hc = std::thread::hardware_concurrency();
-        const int nt = (int)std::max(1u, std::min(16u, hc ? hc : 1u)) - 1;  // + the calling thread
-        for (int t = 0; t < nt; t++) workers_.emplace_back([this] { loop(); });
-    }
-    ~HostPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-            gen_++;
-        }
-        cv_.notify_all();
-        for (auto &w : workers_) w.join();
-    }
-    void drain() {
-        for (int i = next_.fetch_add(1); i < count_; i = next_.fetch_add(1)) (*fn_)(i);
-    }
-    void loop() {
-        unsigned long seen = 0;
-        for (;;) {
-            std::unique_lock<std::mutex> lk(mu_);
-            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-            if (stop_) return;
-            seen = gen_;
-            lk.unlock();
-            drain();
-            lk.lock();
-            if (--busy_ == 0) done_cv_.notify_all();
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex mu_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(int)> *fn_ = nullptr;
-    std::atomic<int> next_{0};
-    int count_ = 0, busy_ = 0;
-    unsigned long gen_ = 0;
-    bool stop_ = false;
-};
-
 // pinned host staging reused across builds (pinning is slow); builds are serialised by g_build_mu
 static std::mutex g_build_mu;
 struct Pinned {
@@ -626,7 +705,7 @@ struct Pinned {
         return p;
     }
 };
-static Pinned g_pin_pidx, g_pin_keys, g_pin_nodes, g_pin_ch, g_pin_cut;
+static Pinned g_pin_nodes, g_pin_ch;
 
 KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t stream) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -670,185 +749,164 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
     KD_CHECK(hipMalloc((void **)&t->d_hi, nn1 * 4));
     KD_CHECK(hipMalloc((void **)&t->d_box, (size_t)2 * std::max(dd, 1) * 4));
     KD_CHECK(hipMalloc((void **)&t->d_view, sizeof(KdOrder)));
-    std::vector<int> cdv(nn1, 0);
-    std::vector<float> cvv(nn1, 0.0f);
-    std::vector<float> box(2 * (size_t)std::max(dd, 1), 0.0f);
-    int *h_pidx;
-    float *h_keys;
-    KD_PIN(h_pidx, g_pin_pidx, nn1 * 4);
-    KD_PIN(h_keys, g_pin_keys, nn1 * 4);
-    for (int i = 0; i < n; i++) h_pidx[i] = i;  // SkeletonTree: pidx[i] = i
+    KD_CHECK(hipMemsetAsync(t->d_cd, 0, nn1 * 4, stream));
+    KD_CHECK(hipMemsetAsync(t->d_cv, 0, nn1 * 4, stream));
+    KD_CHECK(hipMemsetAsync(t->d_lo, 0, nn1 * 4, stream));
+    KD_CHECK(hipMemsetAsync(t->d_hi, 0, nn1 * 4, stream));
+    KD_CHECK(hipMemsetAsync(t->d_box, 0, (size_t)2 * std::max(dd, 1) * 4, stream));
+    hipLaunchKernelGGL(kd_pos_kernel, dim3((unsigned)((nn1 + 255) / 256)), dim3(256), 0, stream, n,
+                       (const int *)nullptr, t->d_pidx);  // SkeletonTree: pidx[i] = i
+    KD_CHECK(hipGetLastError());
     if (n > t->bs) {
-        float *d_keys = nullptr;
-        unsigned *d_omin = nullptr, *d_omax = nullptr;
-        int *d_cut = nullptr;
-        KdChunk *d_ch = nullptr;
-        KdNodeDev *d_nodes = nullptr;
-        const size_t max_nodes = (size_t)n / 2 + 1;
-        const size_t max_big = (size_t)n / KD_CH + 1;
-        const size_t max_ch = (size_t)n / KD_CH + max_big + 1;
-        KD_CHECK(hipMalloc((void **)&d_keys, nn1 * 4));
-        g.dev.push_back(d_keys);
-        KD_CHECK(hipMalloc((void **)&d_omin, max_big * dd * 4));
-        g.dev.push_back(d_omin);
-        KD_CHECK(hipMalloc((void **)&d_omax, max_big * dd * 4));
-        g.dev.push_back(d_omax);
-        KD_CHECK(hipMalloc((void **)&d_cut, max_nodes * 4));
-        g.dev.push_back(d_cut);
-        KD_CHECK(hipMalloc((void **)&d_ch, max_ch * sizeof(KdChunk)));
-        g.dev.push_back(d_ch);
-        KD_CHECK(hipMalloc((void **)&d_nodes, max_nodes * sizeof(KdNodeDev)));
-        g.dev.push_back(d_nodes);
-        KdChunk *h_ch;
-        KdNodeDev *h_nodes;
-        int *h_cut;
-        KD_PIN(h_ch, g_pin_ch, max_ch * sizeof(KdChunk));
-        KD_PIN(h_nodes, g_pin_nodes, max_nodes * sizeof(KdNodeDev));
-        KD_PIN(h_cut, g_pin_cut, max_nodes * 4);
-        KD_CHECK(hipMemcpyAsync(t->d_pidx, h_pidx, (size_t)n * 4, hipMemcpyHostToDevice, stream));
-        std::vector<std::pair<int, int>> level, next, deferred;  // deferred: subtrees built by kd_subtree_kernel
+        // The shape is implicit (node [s, e) splits at s + (e - s) / 2), so every level is planned here, before any
+        // data exists: the levels of nodes > KD_SUB points (each node by kd_median_big_kernel), then the subtrees
+        // of <= KD_SUB points (kd_subtree_waves_kernel).  Nothing comes back to the host until the tree is done.
+        std::vector<std::vector<std::pair<int, int>>> levels;
+        std::vector<std::pair<int, int>> level, next, deferred;
         (n <= KD_SUB ? deferred : level).emplace_back(0, n);
-        HostPool &pool = HostPool::get();
         while (!level.empty()) {
-            // nodes sorted by size, descending: the big ones (> KD_CH points) are a prefix
-            const int nn = (int)level.size();
-            int nbig = 0, nch = 0;
-            for (int i = 0; i < nn; i++) {
-                const int s = level[i].first, e = level[i].second;
-                h_nodes[i] = KdNodeDev{s, e};
-                if (e - s > KD_CH) {
-                    nbig = i + 1;
-                    for (int c = s; c < e; c += KD_CH) h_ch[nch++] = KdChunk{i, c, std::min(e, c + KD_CH)};
-                }
-            }
-            float *box_out = t->levels == 0 ? t->d_box : nullptr;
-            KD_CHECK(hipMemcpyAsync(d_nodes, h_nodes, (size_t)nn * sizeof(KdNodeDev), hipMemcpyHostToDevice, stream));
-            if (nbig > 0) {
-                KD_CHECK(hipMemcpyAsync(d_ch, h_ch, (size_t)nch * sizeof(KdChunk), hipMemcpyHostToDevice, stream));
-                KD_CHECK(hipMemsetAsync(d_omin, 0xff, (size_t)nbig * dd * 4, stream));
-                KD_CHECK(hipMemsetAsync(d_omax, 0x00, (size_t)nbig * dd * 4, stream));
-                hipLaunchKernelGGL(kd_spread_big_kernel, dim3((nch + 3) / 4), dim3(256), 0, stream, d_rows, dd,
-                                   (const int *)t->d_pidx, (const KdChunk *)d_ch, nch, d_omin, d_omax);
-                KD_CHECK(hipGetLastError());
-                hipLaunchKernelGGL(kd_select_big_kernel, dim3((nbig + 3) / 4), dim3(256), 0, stream, dd, nbig,
-                                   (const unsigned *)d_omin, (const unsigned *)d_omax, d_cut, box_out);
-                KD_CHECK(hipGetLastError());
-                hipLaunchKernelGGL(kd_gather_kernel, dim3((nch + 3) / 4), dim3(256), 0, stream, d_rows, dd,
-                                   (const int *)t->d_pidx, (const KdChunk *)d_ch, nch, (const int *)d_cut, d_keys);
-                KD_CHECK(hipGetLastError());
-                box_out = nullptr;
-            }
-            if (nn > nbig) {
-                hipLaunchKernelGGL(kd_small_kernel, dim3((nn - nbig + 3) / 4), dim3(256), 0, stream, d_rows, dd,
-                                   (const int *)t->d_pidx, (const KdNodeDev *)(d_nodes + nbig), nn - nbig,
-                                   d_cut + nbig, d_keys, box_out);
-                KD_CHECK(hipGetLastError());
-            }
-            KD_CHECK(hipMemcpyAsync(h_cut, d_cut, (size_t)nn * 4, hipMemcpyDeviceToHost, stream));
-            KD_CHECK(hipMemcpyAsync(h_keys, d_keys, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
-            KD_CHECK(hipStreamSynchronize(stream));
-            // annMedianSplit per node (biggest first), recording the split node m's cut
-            pool.run(nn, [&](int i) {
-                const int s = level[i].first, e = level[i].second, cnt = e - s, n_lo = cnt / 2;
-                const float cv = median_split_host(h_keys + s, h_pidx + s, cnt, n_lo);
-                cdv[s + n_lo] = h_cut[i];
-                cvv[s + n_lo] = cv;
-            });
+            levels.push_back(level);  // sorted by size, descending: the big ones (> KD_CH points) are a prefix
             next.clear();
-            for (int i = 0; i < nn; i++) {
-                const int s = level[i].first, e = level[i].second, m = s + (e - s) / 2;
+            for (const auto &nd : level) {
+                const int s = nd.first, e = nd.second, m = s + (e - s) / 2;
                 if (m - s > t->bs) (m - s <= KD_SUB ? deferred : next).emplace_back(s, m);
                 if (e - m > t->bs) (e - m <= KD_SUB ? deferred : next).emplace_back(m, e);
             }
             std::stable_sort(next.begin(), next.end(), [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
                 return a.second - a.first > b.second - b.first;
             });
-            KD_CHECK(hipMemcpyAsync(t->d_pidx, h_pidx, (size_t)n * 4, hipMemcpyHostToDevice, stream));
             level.swap(next);
+        }
+        const int nlev = (int)levels.size();
+        std::vector<int> node_off(nlev + 1, 0), ch_off(nlev + 1, 0), nbig(nlev, 0);
+        for (int L = 0; L < nlev; L++) {
+            int nch = 0;
+            for (size_t i = 0; i < levels[L].size(); i++) {
+                const int s = levels[L][i].first, e = levels[L][i].second;
+                if (e - s > KD_CH) {
+                    nbig[L] = (int)i + 1;
+                    nch += (e - s + KD_CH - 1) / KD_CH;
+                }
+            }
+            node_off[L + 1] = node_off[L] + (int)levels[L].size();
+            ch_off[L + 1] = ch_off[L] + nch;
+        }
+        const int n_nodes = node_off[nlev] + (int)deferred.size(), n_ch = ch_off[nlev];
+        KdNodeDev *h_nodes;
+        KdChunk *h_ch;
+        KD_PIN(h_nodes, g_pin_nodes, (size_t)std::max(n_nodes, 1) * sizeof(KdNodeDev));
+        KD_PIN(h_ch, g_pin_ch, (size_t)std::max(n_ch, 1) * sizeof(KdChunk));
+        int max_nn = 1, max_big = 1;
+        for (int L = 0; L < nlev; L++) {
+            int c = ch_off[L];
+            for (size_t i = 0; i < levels[L].size(); i++) {
+                const int s = levels[L][i].first, e = levels[L][i].second;
+                h_nodes[node_off[L] + i] = KdNodeDev{s, e};
+                if ((int)i < nbig[L])
+                    for (int x = s; x < e; x += KD_CH) h_ch[c++] = KdChunk{(int)i, x, std::min(e, x + KD_CH)};
+            }
+            max_nn = std::max(max_nn, (int)levels[L].size());
+            max_big = std::max(max_big, nbig[L]);
+        }
+        for (size_t i = 0; i < deferred.size(); i++)
+            h_nodes[node_off[nlev] + i] = KdNodeDev{deferred[i].first, deferred[i].second};
+        float *d_keys = nullptr;
+        unsigned *d_omin = nullptr, *d_omax = nullptr;
+        int *d_cut = nullptr, *d_lpos = nullptr, *d_rpos = nullptr;
+        KdChunk *d_ch = nullptr;
+        KdNodeDev *d_nodes = nullptr;
+        KD_CHECK(hipMalloc((void **)&d_nodes, (size_t)std::max(n_nodes, 1) * sizeof(KdNodeDev)));
+        g.dev.push_back(d_nodes);
+        KD_CHECK(hipMemcpyAsync(d_nodes, h_nodes, (size_t)n_nodes * sizeof(KdNodeDev), hipMemcpyHostToDevice, stream));
+        if (nlev > 0) {
+            KD_CHECK(hipMalloc((void **)&d_keys, nn1 * 4));
+            g.dev.push_back(d_keys);
+            KD_CHECK(hipMalloc((void **)&d_lpos, nn1 * 4));
+            g.dev.push_back(d_lpos);
+            KD_CHECK(hipMalloc((void **)&d_rpos, nn1 * 4));
+            g.dev.push_back(d_rpos);
+            KD_CHECK(hipMalloc((void **)&d_omin, (size_t)max_big * dd * 4));
+            g.dev.push_back(d_omin);
+            KD_CHECK(hipMalloc((void **)&d_omax, (size_t)max_big * dd * 4));
+            g.dev.push_back(d_omax);
+            KD_CHECK(hipMalloc((void **)&d_cut, (size_t)max_nn * 4));
+            g.dev.push_back(d_cut);
+            KD_CHECK(hipMalloc((void **)&d_ch, (size_t)std::max(n_ch, 1) * sizeof(KdChunk)));
+            g.dev.push_back(d_ch);
+            if (n_ch > 0)
+                KD_CHECK(hipMemcpyAsync(d_ch, h_ch, (size_t)n_ch * sizeof(KdChunk), hipMemcpyHostToDevice, stream));
+        }
+        for (int L = 0; L < nlev; L++) {
+            const int nn = (int)levels[L].size(), nb = nbig[L], nch = ch_off[L + 1] - ch_off[L];
+            const KdNodeDev *lv = d_nodes + node_off[L];
+            const KdChunk *lch = d_ch + ch_off[L];
+            float *box_out = L == 0 ? t->d_box : nullptr;
+            if (nb > 0) {
+                KD_CHECK(hipMemsetAsync(d_omin, 0xff, (size_t)nb * dd * 4, stream));
+                KD_CHECK(hipMemsetAsync(d_omax, 0x00, (size_t)nb * dd * 4, stream));
+                hipLaunchKernelGGL(kd_spread_big_kernel, dim3((nch + 3) / 4), dim3(256), 0, stream, d_rows, dd,
+                                   (const int *)t->d_pidx, lch, nch, d_omin, d_omax);
+                KD_CHECK(hipGetLastError());
+                hipLaunchKernelGGL(kd_select_big_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, dd, nb,
+                                   (const unsigned *)d_omin, (const unsigned *)d_omax, d_cut, box_out);
+                KD_CHECK(hipGetLastError());
+                hipLaunchKernelGGL(kd_gather_kernel, dim3((nch + 3) / 4), dim3(256), 0, stream, d_rows, dd,
+                                   (const int *)t->d_pidx, lch, nch, (const int *)d_cut, d_keys);
+                KD_CHECK(hipGetLastError());
+                box_out = nullptr;
+            }
+            if (nn > nb) {
+                hipLaunchKernelGGL(kd_small_kernel, dim3((nn - nb + 3) / 4), dim3(256), 0, stream, d_rows, dd,
+                                   (const int *)t->d_pidx, lv + nb, nn - nb, d_cut + nb, d_keys, box_out);
+                KD_CHECK(hipGetLastError());
+            }
+            hipLaunchKernelGGL(kd_median_big_kernel, dim3(nn), dim3(64 * KD_MW), 0, stream, d_keys, t->d_pidx, lv,
+                               (const int *)d_cut, d_lpos, d_rpos, t->d_cd, t->d_cv);
+            KD_CHECK(hipGetLastError());
             t->levels++;
         }
         if (!deferred.empty()) {
-            // the host levels' cuts first; the subtree kernel adds its nodes' entries and permutes its segments
-            KD_CHECK(hipMemcpyAsync(t->d_cd, cdv.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
-            KD_CHECK(hipMemcpyAsync(t->d_cv, cvv.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
-            if (t->levels == 0) {  // the whole tree is one subtree: the enclosing box comes from a root spread
-                h_nodes[0] = KdNodeDev{0, n};
-                KD_CHECK(hipMemcpyAsync(d_nodes, h_nodes, sizeof(KdNodeDev), hipMemcpyHostToDevice, stream));
+            const KdNodeDev *dn = d_nodes + node_off[nlev];
+            if (nlev == 0) {  // the whole tree is one subtree: the enclosing box comes from a root spread
+                int *d_cut1 = nullptr;
+                float *d_keys1 = nullptr;
+                KD_CHECK(hipMalloc((void **)&d_cut1, 4));
+                g.dev.push_back(d_cut1);
+                KD_CHECK(hipMalloc((void **)&d_keys1, nn1 * 4));
+                g.dev.push_back(d_keys1);
                 hipLaunchKernelGGL(kd_small_kernel, dim3(1), dim3(256), 0, stream, d_rows, dd, (const int *)t->d_pidx,
-                                   (const KdNodeDev *)d_nodes, 1, d_cut, d_keys, t->d_box);
+                                   dn, 1, d_cut1, d_keys1, t->d_box);
                 KD_CHECK(hipGetLastError());
             }
             const int nd = (int)deferred.size();
-            for (int i = 0; i < nd; i++) h_nodes[i] = KdNodeDev{deferred[i].first, deferred[i].second};
-            KD_CHECK(hipMemcpyAsync(d_nodes, h_nodes, (size_t)nd * sizeof(KdNodeDev), hipMemcpyHostToDevice, stream));
 #ifdef TILER_EXPERIMENTS
             if (getenv("TILER_KD_SUB_OLD"))  // A/B: one node at a time per workgroup
-                hipLaunchKernelGGL(kd_subtree_kernel, dim3(nd), dim3(256), 0, stream, d_rows, dd, t->d_pidx,
-                                   (const KdNodeDev *)d_nodes, t->bs, t->d_cd, t->d_cv);
+                hipLaunchKernelGGL(kd_subtree_kernel, dim3(nd), dim3(256), 0, stream, d_rows, dd, t->d_pidx, dn, t->bs,
+                                   t->d_cd, t->d_cv);
             else
 #endif
             hipLaunchKernelGGL(kd_subtree_waves_kernel, dim3(nd), dim3(64 * KD_SW), 0, stream, d_rows, dd, t->d_pidx,
-                               (const KdNodeDev *)d_nodes, t->bs, t->d_cd, t->d_cv);
+                               dn, t->bs, t->d_cd, t->d_cv);
             KD_CHECK(hipGetLastError());
-            KD_CHECK(hipMemcpyAsync(h_pidx, t->d_pidx, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
-            KD_CHECK(hipMemcpyAsync(cdv.data(), t->d_cd, nn1 * 4, hipMemcpyDeviceToHost, stream));
-            KD_CHECK(hipMemcpyAsync(cvv.data(), t->d_cv, nn1 * 4, hipMemcpyDeviceToHost, stream));
-            int maxd = 0;  // levels: the host ones + the deepest subtree's
-            for (const auto &dn : deferred) {
+            int maxd = 0;  // levels: the big ones + the deepest subtree's
+            for (const auto &d : deferred) {
                 int depth = 0;
-                for (int c = dn.second - dn.first; c > t->bs; c = (c + 1) / 2) depth++;
+                for (int c = d.second - d.first; c > t->bs; c = (c + 1) / 2) depth++;
                 maxd = std::max(maxd, depth);
             }
             t->levels += maxd;
         }
-        KD_CHECK(hipMemcpyAsync(box.data(), t->d_box, (size_t)2 * dd * 4, hipMemcpyDeviceToHost, stream));
-        KD_CHECK(hipStreamSynchronize(stream));
-    } else {
-        KD_CHECK(hipMemcpyAsync(t->d_pidx, h_pidx, nn1 * 4, hipMemcpyHostToDevice, stream));
+        hipLaunchKernelGGL(kd_bounds_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, t->bs,
+                           (const int *)t->d_cd, (const float *)t->d_cv, (const float *)t->d_box, dd, t->d_lo,
+                           t->d_hi);
+        KD_CHECK(hipGetLastError());
     }
-    // cell bounds along each node's cut dimension (rkd_tree: bnd_box.hi[cd] = cv for LO, .lo[cd] = cv for HI)
-    std::vector<float> lov(nn1, 0.0f), hiv(nn1, 0.0f);
-    if (n > t->bs) {
-        std::vector<float> lo(box.begin(), box.begin() + dd), hi(box.begin() + dd, box.begin() + 2 * dd);
-        struct Fr {
-            int s, e, stage;
-            float saved;
-        };
-        std::vector<Fr> st;
-        st.push_back({0, n, 0, 0.0f});
-        while (!st.empty()) {
-            Fr &f = st.back();
-            const int m = f.s + (f.e - f.s) / 2, cd = cdv[m];
-            if (f.stage == 0) {  // enter: record cd_bnds, descend LO with hi[cd] = cv
-                lov[m] = lo[cd];
-                hiv[m] = hi[cd];
-                f.saved = hi[cd];
-                hi[cd] = cvv[m];
-                f.stage = 1;
-                if (m - f.s > t->bs) st.push_back({f.s, m, 0, 0.0f});
-            } else if (f.stage == 1) {  // LO done: restore hi, descend HI with lo[cd] = cv
-                hi[cd] = f.saved;
-                f.saved = lo[cd];
-                lo[cd] = cvv[m];
-                f.stage = 2;
-                const int s2 = m, e2 = f.e;
-                if (e2 - s2 > t->bs) st.push_back({s2, e2, 0, 0.0f});
-            } else {
-                lo[cd] = f.saved;
-                st.pop_back();
-            }
-        }
-    }
-    std::vector<int> pos(nn1, 0);
-    for (int i = 0; i < n; i++) pos[h_pidx[i]] = i;
+    hipLaunchKernelGGL(kd_pos_kernel, dim3((unsigned)((nn1 + 255) / 256)), dim3(256), 0, stream, n,
+                       (const int *)t->d_pidx, t->d_pos);
+    KD_CHECK(hipGetLastError());
     const KdOrder view = t->view();
-    KD_CHECK(hipMemcpyAsync(t->d_pos, pos.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
-    KD_CHECK(hipMemcpyAsync(t->d_cd, cdv.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
-    KD_CHECK(hipMemcpyAsync(t->d_cv, cvv.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
-    KD_CHECK(hipMemcpyAsync(t->d_lo, lov.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
-    KD_CHECK(hipMemcpyAsync(t->d_hi, hiv.data(), nn1 * 4, hipMemcpyHostToDevice, stream));
     KD_CHECK(hipMemcpyAsync(t->d_view, &view, sizeof(KdOrder), hipMemcpyHostToDevice, stream));
-    KD_CHECK(hipStreamSynchronize(stream));
+    KD_CHECK(hipStreamSynchronize(stream));  // the scratch is freed on return; the caller gets a finished tree
 #undef KD_CHECK
 #undef KD_PIN
     t->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

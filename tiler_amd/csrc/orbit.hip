@@ -1908,22 +1908,34 @@ __device__ __forceinline__ constexpr int haar_half_pos(int k) {
     return row * 8 + x;
 }
 
-// NT: the kernel's outputs (rows, fragments, statistics: 1,188 B per tile, never re-read by this kernel) are written
-// with non-temporal stores so they do not evict the tile pixels from L2 between the three component passes
+// SM (store mode) of the kernel's outputs (rows, fragments, statistics: 1,188 B per tile, never re-read by this
+// kernel): 0 plain, 1 non-temporal (`nt`: the line still stays in the XCD's L2), 2 `sc1` (the line leaves L2 once
+// written), so the outputs do not evict the tile pixels from L2 between the three component passes
 template <typename T>
-__device__ __forceinline__ void st_out(T *p, const T &v, bool nt) {
-    if (nt)
+__device__ __forceinline__ void st_out(T *p, const T &v, int sm) {
+    static_assert(sizeof(T) == 16 || sizeof(T) == 4, "16- or 4-byte outputs");
+    if (sm == 2) {
+        if constexpr (sizeof(T) == 16) {
+            typedef unsigned u4v __attribute__((ext_vector_type(4)));
+            const u4v u = __builtin_bit_cast(u4v, v);
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(u) : "memory");
+        } else {
+            const unsigned u = __builtin_bit_cast(unsigned, v);
+            asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(u) : "memory");
+        }
+    } else if (sm == 1) {
         __builtin_nontemporal_store(v, p);
-    else
+    } else {
         *p = v;
+    }
 }
-__device__ __forceinline__ void st_out(float4 *p, const float4 &v, bool nt) {
+__device__ __forceinline__ void st_out(float4 *p, const float4 &v, int sm) {
     typedef float f4v __attribute__((ext_vector_type(4)));
     const f4v w = {v.x, v.y, v.z, v.w};
-    st_out(reinterpret_cast<f4v *>(p), w, nt);
+    st_out(reinterpret_cast<f4v *>(p), w, sm);
 }
 
-template <bool FASTDIV, int H, bool NT>
+template <bool FASTDIV, int H, int NT>
 __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut, float *st, float *sbox,
                                               double (*xch)[64][2], double (*sred)[64]) {
     const int lane = threadIdx.x & 63;
@@ -2036,7 +2048,7 @@ __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut,
     }
 }
 
-template <bool FASTDIV, bool NT>
+template <bool FASTDIV, int NT>
 __global__ __launch_bounds__(128) void orbit_ft_query2_kernel(FtQueryArgs a) {
     __shared__ double lut[256];
     __shared__ float st[64 * 65];
@@ -2098,16 +2110,18 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
     }
 #endif
 #ifdef TILER_EXPERIMENTS
-    static const bool nt = !getenv("TILER_FTQ_NT") || atoi(getenv("TILER_FTQ_NT")) != 0;  // A/B: 0 = plain stores
+    static const int nt = getenv("TILER_FTQ_NT") ? atoi(getenv("TILER_FTQ_NT")) : 1;  // A/B: 0 plain, 1 nt, 2 sc1
 #else
-    constexpr bool nt = true;
+    constexpr int nt = 1;
 #endif
-    if (gamma == -1 && nt)
-        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, true>), grid, dim3(128), 0, stream, fa);
+    if (gamma == -1 && nt == 2)
+        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 2>), grid, dim3(128), 0, stream, fa);
+    else if (gamma == -1 && nt == 1)
+        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 1>), grid, dim3(128), 0, stream, fa);
     else if (gamma == -1)
-        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, false>), grid, dim3(128), 0, stream, fa);
+        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 0>), grid, dim3(128), 0, stream, fa);
     else
-        hipLaunchKernelGGL((orbit_ft_query2_kernel<false, true>), grid, dim3(128), 0, stream, fa);
+        hipLaunchKernelGGL((orbit_ft_query2_kernel<false, 1>), grid, dim3(128), 0, stream, fa);
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -1946,6 +1946,7 @@ __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut,
     const bool has_blk = (i >> 5) < nqblk;
     const long ti = valid ? (a.perm ? (long)a.perm[i] : i) : (a.perm ? (long)a.perm[t0] : t0);
     const int4 *src = reinterpret_cast<const int4 *>(a.rgb + ti * 64) + 8 * H;
+    constexpr int SM = NT;  // output store mode (st_out)
     double nb = 0, h2q[4] = {0, 0, 0, 0}, e2q[4] = {0, 0, 0, 0};  // nb: wave 0 -> (root-box, as float), wave 1 -> n2
     float rb = 0.0f;
     int bad = 0;
@@ -1993,7 +1994,7 @@ __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut,
             if (t0 + tt < a.n) {
                 const float *q = st + tt * 65 + c4 * 4;
                 st_out(reinterpret_cast<float4 *>(a.out32 + (t0 + tt) * OD + c * 64) + c4, make_float4(q[0], q[1], q[2], q[3]),
-                       NT);
+                       SM);
             }
         }
 #pragma unroll
@@ -2022,7 +2023,7 @@ __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut,
                 if (!isfinite(v) || fabs(v) > 65000.0) bad = 1;
                 if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
-            if (has_blk) st_out(a.frag + ((i >> 5) * OS + s) * 64 + (i & 31) + 32 * H, hv, NT);
+            if (has_blk) st_out(a.frag + ((i >> 5) * OS + s) * 64 + (i & 31) + 32 * H, hv, SM);
             __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();  // st and xch are rewritten by the next component
@@ -2044,7 +2045,7 @@ __device__ __forceinline__ void ft_query_half(const FtQueryArgs &a, double *lut,
         q.flags = (bad || sred[3][lane] != 0.0 || !isfinite(n2)) ? 2 : 0;
         q.pad = 0;
         a.qstat[i] = q;
-        if (a.rootbox) st_out(a.rootbox + i, rb, NT);
+        if (a.rootbox) st_out(a.rootbox + i, rb, SM);
     }
 }
 
@@ -2114,14 +2115,16 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
 #else
     constexpr int nt = 1;
 #endif
-    if (gamma == -1 && nt == 2)
-        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 2>), grid, dim3(128), 0, stream, fa);
-    else if (gamma == -1 && nt == 1)
-        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 1>), grid, dim3(128), 0, stream, fa);
-    else if (gamma == -1)
-        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 0>), grid, dim3(128), 0, stream, fa);
-    else
+    if (gamma != -1)
         hipLaunchKernelGGL((orbit_ft_query2_kernel<false, 1>), grid, dim3(128), 0, stream, fa);
+#ifdef TILER_EXPERIMENTS
+    else if (nt == 0)
+        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 0>), grid, dim3(128), 0, stream, fa);
+    else if (nt == 2)
+        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 2>), grid, dim3(128), 0, stream, fa);
+#endif
+    else
+        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 1>), grid, dim3(128), 0, stream, fa);
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -278,8 +278,14 @@ def main():
                                   f"{args.item_tiles or T} tiles per keyframe"}}
 
     res["diag"] = diag
+    import hashlib
+    hsh = hashlib.blake2b(digest_size=8)
+    for k in range(nkf):  # every keyframe's FrameTiling items + errors (equal digest = identical outputs)
+        for nm in ("tile", "pal", "hm", "vm", "err"):
+            hsh.update(outs[k][nm].cpu().numpy().tobytes())
+    res["out_digest"] = hsh.hexdigest()
     print("[bench_encoder] " + json.dumps({k: res[k] for k in ("value", "wall_s", "prepare_ms_avg", "ft_smooth_ms_avg",
-                                                                "items_avg", "candidates_avg")}), file=sys.stderr,
+                                                                "items_avg", "candidates_avg", "out_digest")}), file=sys.stderr,
           flush=True)
 
     # ---- re-check one keyframe against the CPU restatement (after the timed region) ----

@@ -962,10 +962,14 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     for (int r = 0; r < nb; r++) max_chunks = std::max(max_chunks, (nv[r] + KM_BIN - 1) / KM_BIN);
     const size_t item_bytes = (max_items + (size_t)poff[nb] + 64) * sizeof(KmAsgItem) +
                               ((size_t)max_chunks + 1) * sizeof(KmStep) + (size_t)(nb + 1) * 4 + 256;
+    // The cooperative forms measured slower at C4 (r03g: 1.87 s -- farthest-first 573 ms, iterations 1,227 ms --
+    // against 0.99 s per launch: a grid-wide barrier per round / chunk step over every resident workgroup costs more
+    // than the launch it replaces), so the per-launch sequence is the default; TILER_KM_COOP=1 (experiment build)
+    // selects them for A/B.
 #ifdef TILER_EXPERIMENTS
-    static const bool no_coop = getenv("TILER_KM_COOP") && atoi(getenv("TILER_KM_COOP")) == 0;  // A/B
+    static const bool no_coop = !(getenv("TILER_KM_COOP") && atoi(getenv("TILER_KM_COOP")) == 1);
 #else
-    constexpr bool no_coop = false;
+    constexpr bool no_coop = true;
 #endif
     const int g_ff = no_coop ? 0 : coop_grid((const void *)kmb_ff_coop);
     const int g_it = no_coop ? 0 : coop_grid((const void *)kmb_iter_coop);

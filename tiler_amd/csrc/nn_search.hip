@@ -1071,36 +1071,19 @@ static int shortlist_variant() {
 
 // 16x16x32 shortlist for D = 161..192 float datasets: TILER_SHORTLIST=q16 (L16 = 4) / q16l6 (L16 = 6);
 // returns L16, or 0 for the 32x32x16 kernels
+// QB = 4 query blocks per wave; 5 (252 VGPRs) measured the same at 388k candidates (r03h: 80.6-81.2 vs 80.9-81.1 ms)
 static constexpr int SL16_NW = 8, SL16_QB = 4, SL16_CB = 8;
 static int shortlist16_L() {
     const int v = shortlist_variant();
     return v == 16 ? 4 : v == 166 ? 6 : 0;
 }
 
-// query blocks per wave (A/B switch TILER_SL16_QB=5 in the experiment build: each LDS fragment read feeds 5 MFMAs)
-static int sl16_qb() {
-#ifdef TILER_EXPERIMENTS
-    static const int v = getenv("TILER_SL16_QB") && atoi(getenv("TILER_SL16_QB")) == 5 ? 5 : SL16_QB;
-    return v;
-#else
-    return SL16_QB;
-#endif
-}
-
 template <int S, int L>
 static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     const int nqblk = (nq + 15) / 16;
-    const int qb = sl16_qb();
-    const dim3 grid((nqblk + SL16_NW * qb - 1) / (SL16_NW * qb), nsplit);
+    const dim3 grid((nqblk + SL16_NW * SL16_QB - 1) / (SL16_NW * SL16_QB), nsplit);
     const size_t lds = 2 * (SL16_CB * S * 1024 + SL16_CB * 64);
     KTimer tm("nn_shortlist", stream);
-#ifdef TILER_EXPERIMENTS
-    if (qb == 5)
-        hipLaunchKernelGGL((nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, 5>), grid, dim3(SL16_NW * 64), lds, stream,
-                           (const half8 *)ix->d_frag16, ix->d_seed16, ix->nblk16, (const half8 *)ix->scratch.qfrag16,
-                           nq, bps, nsplit, ix->perm, ix->scratch.key, ix->scratch.idx);
-    else
-#endif
     hipLaunchKernelGGL((nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB>), grid, dim3(SL16_NW * 64), lds, stream,
                        (const half8 *)ix->d_frag16, ix->d_seed16, ix->nblk16, (const half8 *)ix->scratch.qfrag16, nq,
                        bps, nsplit, ix->perm, ix->scratch.key, ix->scratch.idx);
@@ -1254,7 +1237,7 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     const int lpq = v16 ? 4 : 2;
     const int nblk = v16 ? ix->nblk16 : ix->nblk;
     const int max_split = 64 / (lpq * L);
-    const int qpwg = v16 ? SL16_NW * sl16_qb() * 16 : (ix->S == 12 ? 512 : 256);
+    const int qpwg = v16 ? SL16_NW * SL16_QB * 16 : (ix->S == 12 ? 512 : 256);
     const int wgs = (nq + qpwg - 1) / qpwg;
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
     nsplit = std::min(nsplit, nblk);

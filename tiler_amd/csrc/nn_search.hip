@@ -597,10 +597,39 @@ __device__ __forceinline__ void write_map(const RescoreArgs &a, long q, int best
     a.m_vm[q] = (at & 2) != 0;
 }
 
+// any() over this lane's group of W lanes (W divides 64)
+template <int W>
+__device__ __forceinline__ bool grp_any(bool p) {
+    const unsigned long long b = __ballot(p);
+    if constexpr (W == 64) {
+        return b != 0;
+    } else {
+        const int g = (int)(threadIdx.x & 63) / W;
+        return ((b >> (g * W)) & ((1ull << W) - 1)) != 0;
+    }
+}
+
+// lexicographic (v, i) minimum over a group of W lanes
+template <int W>
+__device__ __forceinline__ void grp_argmin(float &v, int &i) {
+#pragma unroll
+    for (int o = W / 2; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(v, o, 64);
+        const int oi = __shfl_xor(i, o, 64);
+        const bool take = (ov < v) || (ov == v && (unsigned)oi < (unsigned)i);
+        v = take ? ov : v;
+        i = take ? oi : i;
+    }
+}
+
+// W lanes per query: 64 (one wave), or 16 when the query has at most 16 list entries (the 16x16x32 shortlist with
+// one split: 4 lanes x L = 4), four queries per wave -- the entries' exact distances (192 dependent fp32 adds
+// each) then fill the wave instead of a quarter of it
+template <int W>
 __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
-    const int lane = threadIdx.x & 63;
-    const long q = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= a.nq) return;
+    const int lane = threadIdx.x & (W - 1);
+    const long q = (long)blockIdx.x * (256 / W) + (threadIdx.x / W);
+    if (q >= a.nq) return;  // whole groups
     const int E = a.nsplit * a.lpq * a.L;  // list entries per query
     float key = INFINITY;
     int idx = -1;
@@ -623,7 +652,7 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
         for (int r = 0; r < a.k; r++) {
             float mv = taken ? INFINITY : v;
             int mi = taken ? 0x7fffffff : who;
-            wave_argmin(mv, mi);
+            grp_argmin<W>(mv, mi);
             kk = mv;
             if (lane == mi) taken = true;
         }
@@ -654,7 +683,7 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
     // global order), but under ANN's kd order a lane's dropped equal-key entry can rank first
     if (!exact || a.L < a.k || a.ko) {
         const bool last = lane < E && (lane % a.L) == a.L - 1;
-        if (__any(last && idx >= 0 && (double)key <= T)) fallback = true;
+        if (grp_any<W>(last && idx >= 0 && (double)key <= T)) fallback = true;
     }
     const bool cand = (idx >= 0) && ((double)key <= T);
     float dist = INFINITY;
@@ -682,7 +711,7 @@ __global__ __launch_bounds__(256) void nn_rescore_kernel(RescoreArgs a) {
     for (int r = 0; r < a.k; r++) {
         float mv = taken ? INFINITY : dist;
         int mi = taken ? 0x7fffffff : di;
-        kd_argmin<64>(a.ko, qrow, mv, mi);
+        kd_argmin<W>(a.ko, qrow, mv, mi);
         if (!taken && di == mi && mi != 0x7fffffff) taken = true;
         if (lane == 0) {
             const bool ok = mi != 0x7fffffff;
@@ -1330,7 +1359,10 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     TILER_HIP_CHECK(hipMemsetAsync(s.ccnt, 0, (size_t)std::min(nq, TIER2_MAX) * sizeof(int), stream));
     {
         KTimer t_rs("nn_rescore", stream);
-        hipLaunchKernelGGL(nn_rescore_kernel, dim3((nq + 3) / 4), dim3(256), 0, stream, ra);
+        if (ra.nsplit * ra.lpq * ra.L <= 16)
+            hipLaunchKernelGGL(nn_rescore_kernel<16>, dim3((nq + 15) / 16), dim3(256), 0, stream, ra);
+        else
+            hipLaunchKernelGGL(nn_rescore_kernel<64>, dim3((nq + 3) / 4), dim3(256), 0, stream, ra);
     }
     TILER_HIP_CHECK(hipGetLastError());
     return search_tail(ix, ra, nq, stream, nullptr);

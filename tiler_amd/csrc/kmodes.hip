@@ -25,7 +25,6 @@
 #include <string>
 #include <vector>
 
-#include <hip/hip_cooperative_groups.h>
 
 #include "kmodes.hpp"
 
@@ -715,165 +714,137 @@ __global__ __launch_bounds__(NT) void kmb_seq_strided(KmBatch B, const KmAsgItem
     bin_seq_body<NT>(s, it.p0, it.p1);
 }
 
-// ---- cooperative forms: one launch per phase instead of one per farthest-first round / chunk step ----
-// The farthest-first rounds and the chunk steps of an iteration are sequential by definition (round j + 1 needs
-// centre j + 1; chunk c + 1 is assigned against the modes chunk c leaves), and with one launch each the largest
-// bin's chain was launch-bound (C4: 5,035 rounds at ~40 us, 2 x 247 chunk launches per iteration).  One cooperative
-// launch (hipLaunchCooperativeKernel: every workgroup resident) runs the whole chain, a grid barrier between
-// dependent phases; the per-item work is that of the one-shot kernels (same items, same order-independent merges:
-// block maxima, atomicMin keys), so results are identical.
-namespace cg = cooperative_groups;
-static constexpr int KM_COOP_NT = 512;
+// ---- farthest-first as ONE persistent launch (round 3) ----
+// InitFarthestFirst is 5,035 rounds at C4 (the largest bin's K), each dependent on the last, and one launch per round
+// cost ~40 us (20 us median, r03i trace).  Here one workgroup per CU runs every round: the items of the alive bins
+// (same (bin, sub) list, points strided by KM_FF_NT), the last item of a bin to finish selects its next centre (the
+// per-launch kernel's counter protocol), then a grid barrier.  The barrier is two-level -- 8 arrival counters (one
+// 128-byte line each, workgroups by blockIdx % 8) -> a top counter -> a generation word every workgroup polls -- with
+// monotonic counts inside the call (zeroed per call) and the agent-scope release / acquire of cdna_hip_programming.md
+// Guideline 16; cooperative_groups' grid sync (26-100 us per call on ROCm 7.2) made the r03 cooperative form slower
+// than the launches it replaced.  Item u is always processed by workgroup u % G, so a point's min-distance word is
+// only ever touched by one workgroup and its rows stay in that XCD's L2.  Every spin is bounded: a barrier that waits
+// ~0.5 s sets *fail, every workgroup leaves, and the host reruns the rounds with the per-launch kernel (the state
+// is re-initialised), so a result never depends on residency.  Same updates, same partition-independent argmax
+// (value, then the largest index), so the centres are those of the per-launch rounds.
+static constexpr int KM_FF_NT = 512;
 
-// farthest-first, every alive bin's item (bin, sub): mind update + the item's argmax candidate -> part[sub]
-__device__ void ff_coop_item(const KmBatch &B, const KmFfItem &it, int j, unsigned long long *best) {
-    constexpr int NT = KM_COOP_NT;
-    KmState s = bin_state(B, it.bin);
-    const int c = s.center[j];
-    uint32_t item[20];
-    load_row(s.X + (long)c * KM_A, item);
-    unsigned long long bv = 0;
-    int bi = -1;
-    for (long i = (long)it.sub * NT + threadIdx.x; i < s.n; i += (long)it.nsub * NT) {
-        uint32_t row[20];
-        load_row(s.X + i * KM_A, row);
-        const unsigned long long d = km_dissim(row, item);
-        unsigned long long m = s.mind[i];
-        if (d < m) {
-            m = d;
-            s.mind[i] = m;
-        }
-        if (!s.used[i] && m >= bv) {
-            bv = m;
-            bi = (int)i;
-        }
-    }
-    const unsigned long long v32 = bv > 0xFFFFFFFFull ? 0xFFFFFFFFull : bv;
-    best[threadIdx.x] = (bi < 0) ? 0ull : ((v32 << 32) | (unsigned)(bi + 1));
+__device__ __forceinline__ bool km_grid_sync(unsigned *bar, unsigned epoch, unsigned *fail) {
+    __shared__ int s_ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its stores have left
     __syncthreads();
-    for (int o = NT / 2; o > 0; o >>= 1) {
-        if (threadIdx.x < o) best[threadIdx.x] = max(best[threadIdx.x], best[threadIdx.x + o]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) s.part[it.sub] = best[0];
-    __syncthreads();  // best[] is reused by the next item
-}
-
-// farthest-first selection of centre j + 1 of bin r from its items' candidates
-__device__ void ff_coop_select(const KmBatch &B, int r, int nsub, int j, unsigned long long *best) {
-    constexpr int NT = KM_COOP_NT;
-    KmState s = bin_state(B, r);
-    unsigned long long bb = 0;
-    for (int i = threadIdx.x; i < nsub; i += NT) bb = max(bb, s.part[i]);
-    best[threadIdx.x] = bb;
-    __syncthreads();
-    for (int o = NT / 2; o > 0; o >>= 1) {
-        if (threadIdx.x < o) best[threadIdx.x] = max(best[threadIdx.x], best[threadIdx.x + o]);
-        __syncthreads();
-    }
-    const unsigned long long w = best[0];
-    __syncthreads();
-    const int f = (w == 0) ? -1 : (int)(w & 0xFFFFFFFFull) - 1;
-    if (f < 0) {
-        if (threadIdx.x == 0) *s.err = 1;
-        return;
-    }
-    if (threadIdx.x < KM_A) s.cent[(long)(j + 1) * KM_A + threadIdx.x] = s.X[(long)f * KM_A + threadIdx.x];
     if (threadIdx.x == 0) {
-        s.center[j + 1] = f;
-        s.used[f] = 1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int G = (int)gridDim.x, g = (int)(blockIdx.x & 7);
+        const unsigned ng = (unsigned)((G - g + 7) >> 3), ngroups = (unsigned)min(G, 8);
+        int ok = 1;
+        if (__hip_atomic_fetch_add(bar + 32 * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch * ng - 1u &&
+            __hip_atomic_fetch_add(bar + 256, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch * ngroups - 1u)
+            __hip_atomic_store(bar + 288, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (unsigned spins = 0; __hip_atomic_load(bar + 288, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch;) {
+            if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || ++spins > (1u << 20)) {
+                __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        s_ok = ok;
     }
+    __syncthreads();
+    return s_ok != 0;
 }
 
-// InitFarthestFirst for every bin, rounds 0 .. Kmax - 1 (bins sorted by K descending: the alive ones are a prefix;
-// ff_end[a] = items of the first a bins)
-__global__ __launch_bounds__(KM_COOP_NT) void kmb_ff_coop(KmBatch B, const KmFfItem *items, const int *ff_end,
-                                                         int Kmax) {
-    __shared__ unsigned long long best[KM_COOP_NT];
-    cg::grid_group g = cg::this_grid();
+// (value, largest index) maximum of a packed u64 over the workgroup; red[] holds one word per wave
+__device__ __forceinline__ unsigned long long km_block_max(unsigned long long v, unsigned long long *red) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long ov = ((unsigned long long)__shfl_xor((unsigned)(v >> 32), o, 64) << 32) |
+                                      (unsigned)__shfl_xor((unsigned)v, o, 64);
+        v = ov > v ? ov : v;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    unsigned long long m = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) m = red[w] > m ? red[w] : m;
+    __syncthreads();  // red[] is reused
+    return m;
+}
+
+__global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist(KmBatch B, const KmFfItem *items, const int *ff_end,
+                                                           int Kmax, unsigned *bar, unsigned *fail) {
+    __shared__ unsigned long long red[KM_FF_NT / 64];
+    __shared__ int last;
     int alive = B.nb;
     for (int j = 0; j < Kmax; j++) {
         while (alive > 0 && B.koff[alive] - B.koff[alive - 1] <= j) alive--;
         const int nit = ff_end[alive];
-        for (int u = blockIdx.x; u < nit; u += gridDim.x) ff_coop_item(B, items[u], j, best);
-        g.sync();
-        for (int r = blockIdx.x; r < alive; r += gridDim.x)
-            if (j + 1 < B.koff[r + 1] - B.koff[r]) ff_coop_select(B, r, B.poff[r + 1] - B.poff[r], j, best);
-        g.sync();
-    }
-}
-
-// one assignment unit: up to NT points of an item vs the sub-th of KM_ASUB slices of its centroids
-template <int NT>
-__device__ void assign_unit(const KmBatch &B, KmAsgItem it, int sub, int nsub, uint4 *ct) {
-    const int per = (it.c1 - it.c0 + nsub - 1) / nsub;
-    it.c0 += sub * per;
-    it.c1 = min(it.c1, it.c0 + per);
-    if (it.c0 >= it.c1) return;  // uniform over the workgroup
-    KmState s = bin_state(B, it.bin);
-    const long i = it.p0 + threadIdx.x;
-    const bool valid = i < it.p1;
-    uint32_t item[20];
-    if (valid) load_row(s.X + i * KM_A, item);
-    unsigned long long best = ~0ull;
-    for (int t0 = it.c0; t0 < it.c1; t0 += 128) {
-        const int cnt = min(128, it.c1 - t0);
-        __syncthreads();
-        for (int e = threadIdx.x; e < cnt * 5; e += NT) ct[e] = reinterpret_cast<const uint4 *>(s.cent + (long)t0 * KM_A)[e];
-        __syncthreads();
-        if (valid) {
-            for (int c = 0; c < cnt; c++) {
+        for (int u = blockIdx.x; u < nit; u += gridDim.x) {
+            const KmFfItem it = items[u];
+            KmState s = bin_state(B, it.bin);
+            const int c = s.center[j];
+            uint32_t item[20];
+            load_row(s.X + (long)c * KM_A, item);
+            unsigned long long bv = 0;
+            int bi = -1;
+            for (long i = (long)it.sub * KM_FF_NT + threadIdx.x; i < s.n; i += (long)it.nsub * KM_FF_NT) {
                 uint32_t row[20];
-#pragma unroll
-                for (int q = 0; q < 5; q++) {
-                    const uint4 v = ct[c * 5 + q];
-                    row[4 * q] = v.x;
-                    row[4 * q + 1] = v.y;
-                    row[4 * q + 2] = v.z;
-                    row[4 * q + 3] = v.w;
-                }
+                load_row(s.X + i * KM_A, row);
                 const unsigned long long d = km_dissim(row, item);
-                const unsigned long long key = (d << 32) | (0xFFFFFFFFu - (unsigned)(t0 + c));
-                best = key < best ? key : best;
+                unsigned long long m = s.mind[i];
+                if (d < m) {  // cmovb: strict-less (kmodes.pas:555-558)
+                    m = d;
+                    s.mind[i] = m;
+                }
+                if (!s.used[i] && m >= bv) {  // ascending i within a thread: '>=' keeps the last
+                    bv = m;
+                    bi = (int)i;
+                }
+            }
+            const unsigned long long v32 = bv > 0xFFFFFFFFull ? 0xFFFFFFFFull : bv;
+            const unsigned long long best = km_block_max(bi < 0 ? 0ull : ((v32 << 32) | (unsigned)(bi + 1)), red);
+            if (j + 1 >= s.K) continue;  // the bin's last round: no selection (uniform)
+            if (threadIdx.x == 0) {
+                s.part[it.sub] = best;
+                __threadfence();
+                last = atomicAdd(&B.ffdone[it.bin], 1) == it.nsub - 1;
+            }
+            __syncthreads();
+            if (!last) continue;  // uniform
+            __threadfence();
+            unsigned long long bb = 0;
+            for (int i = threadIdx.x; i < it.nsub; i += KM_FF_NT)
+                bb = max(bb, __hip_atomic_load(&s.part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            const unsigned long long w = km_block_max(bb, red);
+            const int f = (w == 0) ? -1 : (int)(w & 0xFFFFFFFFull) - 1;
+            if (threadIdx.x == 0) __hip_atomic_store(&B.ffdone[it.bin], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (f < 0) {
+                if (threadIdx.x == 0) *s.err = 1;
+                continue;
+            }
+            if (threadIdx.x < KM_A) s.cent[(long)(j + 1) * KM_A + threadIdx.x] = s.X[(long)f * KM_A + threadIdx.x];
+            if (threadIdx.x == 0) {
+                s.center[j + 1] = f;
+                s.used[f] = 1;
             }
         }
-    }
-    if (valid) atomicMin(&s.akey[i], best);
-    __syncthreads();  // ct[] is reused by the next unit
-}
-
-// one KModesIter pass of every listed bin: per chunk step, the assignment units of every bin's chunk against the
-// current modes, barrier, each bin's chunk moves in order (bin_seq_body, one workgroup per bin), barrier
-struct KmStep {
-    int pos, na, ns, pad;  // items [pos, pos + na): assignment (KM_ASUB units each), [pos + na, + ns): seq
-};
-__global__ __launch_bounds__(KM_COOP_NT) void kmb_iter_coop(KmBatch B, const KmAsgItem *items, const KmStep *steps,
-                                                           int nsteps) {
-    __shared__ uint4 ct[128 * 5];
-    cg::grid_group g = cg::this_grid();
-    for (int st = 0; st < nsteps; st++) {
-        const KmStep sp = steps[st];
-        for (int u = blockIdx.x; u < sp.na * KM_ASUB; u += gridDim.x)
-            assign_unit<KM_COOP_NT>(B, items[sp.pos + u / KM_ASUB], u % KM_ASUB, KM_ASUB, ct);
-        g.sync();
-        for (int u = blockIdx.x; u < sp.ns; u += gridDim.x) {
-            const KmSeqItem it = *reinterpret_cast<const KmSeqItem *>(items + sp.pos + sp.na + u);
-            bin_seq_body<KM_COOP_NT>(bin_state(B, it.bin), it.p0, it.p1);
-            __syncthreads();
-        }
-        g.sync();
+        if (j + 1 < Kmax && !km_grid_sync(bar, (unsigned)(j + 1), fail)) return;
     }
 }
 
-// resident workgroups of a cooperative K-Modes kernel (0: cooperative launch unavailable)
-static int coop_grid(const void *kernel) {
-    int dev = 0, coop = 0, ncu = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess || !coop ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, KM_COOP_NT, 0) != hipSuccess || per <= 0)
-        return 0;
-    return ncu * std::min(per, 2);
+// resident workgroups for kmb_ff_persist: one per CU (0: not placeable -> per-launch rounds)
+static int ff_persist_grid() {
+    static const int g = [] {
+        int dev = 0, ncu = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)kmb_ff_persist, KM_FF_NT, 0) != hipSuccess ||
+            per <= 0 || ncu <= 0)
+            return 0;
+        return ncu;
+    }();
+    return g;
 }
 
 // ---- DoKModes medoid choice (main.pas:4231-4253): per cluster j with members, the member minimising
@@ -949,7 +920,8 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                  o_csize = carve((size_t)Ktot * 4), o_mind = carve((size_t)N * 8), o_used = carve(N),
                  o_part = carve((size_t)poff[nb] * 8), o_center = carve((size_t)Ktot * 4), o_akey = carve((size_t)N * 8),
                  o_seed = carve(nb * 4), o_cost = carve(nb * 8), o_moves = carve(nb * 4), o_err = carve(nb * 4),
-                 o_ffd = carve(nb * 4), o_rand = carve((size_t)Ktot * KM_A * 4), o_items = carve(0);
+                 o_ffd = carve(nb * 4), o_rand = carve((size_t)Ktot * KM_A * 4), o_bar = carve(1280),
+                 o_items = carve(0);
     char *buf = nullptr;
     // the largest work list: one iteration's chunk items for every bin
     size_t max_items = 0;
@@ -958,21 +930,16 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
         max_items += (size_t)nch * ((KM_BIN + 255) / 256) * csplit_of(Kv[r]) + nch;
         max_items += (size_t)((nv[r] + 255) / 256) * csplit_of(Kv[r]);
     }
-    int max_chunks = 0;
-    for (int r = 0; r < nb; r++) max_chunks = std::max(max_chunks, (nv[r] + KM_BIN - 1) / KM_BIN);
     const size_t item_bytes = (max_items + (size_t)poff[nb] + 64) * sizeof(KmAsgItem) +
-                              ((size_t)max_chunks + 1) * sizeof(KmStep) + (size_t)(nb + 1) * 4 + 256;
-    // The cooperative forms measured slower at C4 (r03g: 1.87 s -- farthest-first 573 ms, iterations 1,227 ms --
-    // against 0.99 s per launch: a grid-wide barrier per round / chunk step over every resident workgroup costs more
-    // than the launch it replaces), so the per-launch sequence is the default; TILER_KM_COOP=1 (experiment build)
-    // selects them for A/B.
+                              (size_t)(nb + 1) * 4 + 256;
+    // farthest-first: one persistent launch for every round (kmb_ff_persist) unless it cannot be placed;
+    // TILER_KM_FF=0 (experiment build) selects the per-launch rounds for A/B
 #ifdef TILER_EXPERIMENTS
-    static const bool no_coop = !(getenv("TILER_KM_COOP") && atoi(getenv("TILER_KM_COOP")) == 1);
+    static const bool ff_launches = getenv("TILER_KM_FF") && atoi(getenv("TILER_KM_FF")) == 0;
 #else
-    constexpr bool no_coop = true;
+    constexpr bool ff_launches = false;
 #endif
-    const int g_ff = no_coop ? 0 : coop_grid((const void *)kmb_ff_coop);
-    const int g_it = no_coop ? 0 : coop_grid((const void *)kmb_iter_coop);
+    const int g_ff = ff_launches ? 0 : ff_persist_grid();
     TILER_HIP_CHECK(hipMalloc((void **)&buf, off + item_bytes));
     char *items = buf + o_items;
     KmBatch B;
@@ -1020,11 +987,6 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
             if (hipMemcpyAsync(B.seed, seeds.data(), nb * 4, hipMemcpyHostToDevice, st) != hipSuccess) goto fail;
             if (hipStreamSynchronize(st) != hipSuccess) goto fail;
         }
-        if (hipMemsetAsync(B.err, 0, nb * 4, st) != hipSuccess || hipMemsetAsync(B.ffdone, 0, nb * 4, st) != hipSuccess ||
-            hipMemsetAsync(B.mind, 0xff, (size_t)N * 8, st) != hipSuccess || hipMemsetAsync(B.used, 0, N, st) != hipSuccess ||
-            hipMemsetAsync(B.cent, 0xff, (size_t)Ktot * KM_A, st) != hipSuccess)
-            goto fail;
-        hipLaunchKernelGGL(kmb_ff_start, dim3((nb + 63) / 64), dim3(64), 0, st, B, (const int32_t *)(buf + o_start));
         // InitFarthestFirst, all bins round by round
         {
             std::vector<KmFfItem> ff;
@@ -1034,22 +996,40 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                 for (int sb = 0; sb < ns; sb++) ff.push_back({r, sb, ns, 0});
                 ff_end[r + 1] = (int)ff.size();
             }
-            if (g_ff > 0) {  // one cooperative launch for every round (items of KM_COOP_NT-point strides)
-                const size_t fb = ff.size() * sizeof(KmFfItem);
+            const size_t fb = ff.size() * sizeof(KmFfItem);
+            {
                 std::vector<char> up(fb + (nb + 1) * 4);
                 memcpy(up.data(), ff.data(), fb);
                 memcpy(up.data() + fb, ff_end.data(), (nb + 1) * 4);
                 if (upload(up.data(), up.size())) goto fail;
-                const KmFfItem *d_items = (const KmFfItem *)items;
-                const int *d_end = (const int *)(items + fb);
-                int kmax = Kv[0];
-                void *args[] = {&B, &d_items, &d_end, &kmax};
-                KTimer tm("kmodes_init", st);
-                if (hipLaunchCooperativeKernel((const void *)kmb_ff_coop, dim3(g_ff), dim3(KM_COOP_NT), args, 0, st) !=
-                    hipSuccess)
+            }
+            auto ff_init = [&]() -> int {  // the state every farthest-first run starts from
+                if (hipMemsetAsync(B.err, 0, nb * 4, st) != hipSuccess || hipMemsetAsync(B.ffdone, 0, nb * 4, st) != hipSuccess ||
+                    hipMemsetAsync(B.mind, 0xff, (size_t)N * 8, st) != hipSuccess || hipMemsetAsync(B.used, 0, N, st) != hipSuccess ||
+                    hipMemsetAsync(B.cent, 0xff, (size_t)Ktot * KM_A, st) != hipSuccess)
+                    return -1;
+                hipLaunchKernelGGL(kmb_ff_start, dim3((nb + 63) / 64), dim3(64), 0, st, B, (const int32_t *)(buf + o_start));
+                return hipGetLastError() == hipSuccess ? 0 : -1;
+            };
+            if (ff_init()) goto fail;
+            bool done = false;
+            if (g_ff > 0) {
+                unsigned *bar = (unsigned *)(buf + o_bar), *ffail = bar + 300;
+                if (hipMemsetAsync(bar, 0, 1280, st) != hipSuccess) goto fail;  // counters, generation, fail word
+                {
+                    KTimer tm("kmodes_init", st);
+                    hipLaunchKernelGGL(kmb_ff_persist, dim3(g_ff), dim3(KM_FF_NT), 0, st, B, (const KmFfItem *)items,
+                                       (const int *)(items + fb), Kv[0], bar, ffail);
+                }
+                unsigned hf = 1;
+                if (hipGetLastError() != hipSuccess ||
+                    hipMemcpyAsync(&hf, ffail, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess)
                     goto fail;
-            } else {
-                if (upload(ff.data(), ff.size() * sizeof(KmFfItem))) goto fail;
+                done = hf == 0;
+                if (!done && ff_init()) goto fail;  // a barrier gave up: rerun the rounds one launch each
+            }
+            if (!done) {
                 KTimer tm("kmodes_init", st);
                 int alive = nb;
                 for (int j = 0; j < Kv[0]; j++) {
@@ -1091,7 +1071,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                 // work list of this iteration: per chunk step c, the assign items then the seq items
                 std::vector<KmAsgItem> wl;
                 std::vector<std::pair<int, int>> steps;  // (assign items, seq items) per chunk step
-                const int qstep = g_it > 0 ? KM_COOP_NT : 256;  // points per assignment item
+                const int qstep = 256;  // points per assignment item
                 int maxch = 0;
                 for (int r : active) maxch = std::max(maxch, (nv[r] + KM_BIN - 1) / KM_BIN);
                 for (int c = 0; c < maxch; c++) {
@@ -1114,39 +1094,14 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     }
                     steps.push_back({na, ns});
                 }
-                std::vector<KmStep> ksteps;
-                {
-                    int pos = 0;
-                    for (const auto &sp : steps) {
-                        ksteps.push_back({pos, sp.first, sp.second, 0});
-                        pos += sp.first + sp.second;
-                    }
-                }
-                const size_t wb = wl.size() * sizeof(KmAsgItem);
-                if (g_it > 0) {
-                    std::vector<char> up(wb + ksteps.size() * sizeof(KmStep));
-                    memcpy(up.data(), wl.data(), wb);
-                    memcpy(up.data() + wb, ksteps.data(), ksteps.size() * sizeof(KmStep));
-                    if (upload(up.data(), up.size())) goto fail;
-                } else if (upload(wl.data(), wb)) {
-                    goto fail;
-                }
+                if (upload(wl.data(), wl.size() * sizeof(KmAsgItem))) goto fail;
                 for (int r : active) {
                     iters[r]++;
                     if (hipMemsetAsync(B.cost + r, 0, 8, st) != hipSuccess || hipMemsetAsync(B.moves + r, 0, 4, st) != hipSuccess)
                         goto fail;
                     if (hipMemsetAsync(B.akey + boff[r], 0xff, (size_t)nv[r] * 8, st) != hipSuccess) goto fail;
                 }
-                if (g_it > 0) {
-                    const KmAsgItem *d_items = (const KmAsgItem *)items;
-                    const KmStep *d_steps = (const KmStep *)(items + wb);
-                    int nst = (int)ksteps.size();
-                    void *args[] = {&B, &d_items, &d_steps, &nst};
-                    KTimer tm("kmodes_seq", st);
-                    if (hipLaunchCooperativeKernel((const void *)kmb_iter_coop, dim3(g_it), dim3(KM_COOP_NT), args, 0, st) !=
-                        hipSuccess)
-                        goto fail;
-                } else {
+                {
                     size_t pos = 0;
                     for (const auto &sp : steps) {
                         {

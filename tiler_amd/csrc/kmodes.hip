@@ -720,8 +720,11 @@ __global__ __launch_bounds__(NT) void kmb_seq_strided(KmBatch B, const KmAsgItem
 // (same (bin, sub) list, points strided by KM_FF_NT), the last item of a bin to finish selects its next centre (the
 // per-launch kernel's counter protocol), then a grid barrier.  The barrier is two-level -- 8 arrival counters (one
 // 128-byte line each, workgroups by blockIdx % 8) -> a top counter -> a generation word every workgroup polls -- with
-// monotonic counts inside the call (zeroed per call) and the agent-scope release / acquire of cdna_hip_programming.md
-// Guideline 16; cooperative_groups' grid sync (26-100 us per call on ROCm 7.2) made the r03 cooperative form slower
+// monotonic counts inside the call (zeroed per call).  Hand-offs follow cdna_hip_programming.md Guideline 16 R1: every
+// word another workgroup reads in this launch (a bin's centre index, the used flags, the per-item candidates) is
+// stored AND loaded `sc1` (agent-scope atomics), drained before the counter add, so no release / acquire fence runs
+// (an agent release writes back the XCD's dirty L2 lines and the acquire drops the CU's L1: r03k's first form with
+// them took 56 us per round); rows and min-distances are read-only or owner-only.  cooperative_groups' grid sync (26-100 us per call on ROCm 7.2) made the r03 cooperative form slower
 // than the launches it replaced.  Item u is always processed by workgroup u % G, so a point's min-distance word is
 // only ever touched by one workgroup and its rows stay in that XCD's L2.  Every spin is bounded: a barrier that waits
 // ~0.5 s sets *fail, every workgroup leaves, and the host reruns the rounds with the per-launch kernel (the state
@@ -731,11 +734,9 @@ static constexpr int KM_FF_NT = 512;
 
 __device__ __forceinline__ bool km_grid_sync(unsigned *bar, unsigned epoch, unsigned *fail) {
     __shared__ int s_ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its stores have left
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores have left (R1 drain)
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int G = (int)gridDim.x, g = (int)(blockIdx.x & 7);
         const unsigned ng = (unsigned)((G - g + 7) >> 3), ngroups = (unsigned)min(G, 8);
         int ok = 1;
@@ -750,9 +751,9 @@ __device__ __forceinline__ bool km_grid_sync(unsigned *bar, unsigned epoch, unsi
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         s_ok = ok;
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below the poll
     __syncthreads();
     return s_ok != 0;
 }
@@ -783,7 +784,7 @@ __global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist(KmBatch B, const KmFf
         for (int u = blockIdx.x; u < nit; u += gridDim.x) {
             const KmFfItem it = items[u];
             KmState s = bin_state(B, it.bin);
-            const int c = s.center[j];
+            const int c = __hip_atomic_load(s.center + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             uint32_t item[20];
             load_row(s.X + (long)c * KM_A, item);
             unsigned long long bv = 0;
@@ -797,7 +798,8 @@ __global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist(KmBatch B, const KmFf
                     m = d;
                     s.mind[i] = m;
                 }
-                if (!s.used[i] && m >= bv) {  // ascending i within a thread: '>=' keeps the last
+                const bool used = __hip_atomic_load(s.used + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                if (!used && m >= bv) {  // ascending i within a thread: '>=' keeps the last
                     bv = m;
                     bi = (int)i;
                 }
@@ -806,13 +808,13 @@ __global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist(KmBatch B, const KmFf
             const unsigned long long best = km_block_max(bi < 0 ? 0ull : ((v32 << 32) | (unsigned)(bi + 1)), red);
             if (j + 1 >= s.K) continue;  // the bin's last round: no selection (uniform)
             if (threadIdx.x == 0) {
-                s.part[it.sub] = best;
-                __threadfence();
-                last = atomicAdd(&B.ffdone[it.bin], 1) == it.nsub - 1;
+                __hip_atomic_store(s.part + it.sub, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the candidate has left before the count
+                last = __hip_atomic_fetch_add(B.ffdone + it.bin, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       it.nsub - 1;
             }
             __syncthreads();
             if (!last) continue;  // uniform
-            __threadfence();
             unsigned long long bb = 0;
             for (int i = threadIdx.x; i < it.nsub; i += KM_FF_NT)
                 bb = max(bb, __hip_atomic_load(&s.part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -823,10 +825,11 @@ __global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist(KmBatch B, const KmFf
                 if (threadIdx.x == 0) *s.err = 1;
                 continue;
             }
+            // the centre's row for the later kernels (nothing in this launch reads it: items read X[center])
             if (threadIdx.x < KM_A) s.cent[(long)(j + 1) * KM_A + threadIdx.x] = s.X[(long)f * KM_A + threadIdx.x];
             if (threadIdx.x == 0) {
-                s.center[j + 1] = f;
-                s.used[f] = 1;
+                __hip_atomic_store(s.center + j + 1, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(s.used + f, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         if (j + 1 < Kmax && !km_grid_sync(bar, (unsigned)(j + 1), fail)) return;

@@ -719,7 +719,8 @@ __global__ __launch_bounds__(NT) void kmb_seq_strided(KmBatch B, const KmAsgItem
 // cost ~40 us (20 us median, r03i trace).  Here one workgroup per CU runs every round: the items of the alive bins
 // (same (bin, sub) list, points strided by KM_FF_NT), the last item of a bin to finish selects its next centre (the
 // per-launch kernel's counter protocol), then a grid barrier.  The barrier is two-level -- 8 arrival counters (one
-// 128-byte line each, workgroups by blockIdx % 8) -> a top counter -> a generation word every workgroup polls -- with
+// 128-byte line each, workgroups by blockIdx % 8) -> a top counter -> 8 generation words (one per group, each polled
+// by its group only) -- with
 // monotonic counts inside the call (zeroed per call).  Hand-offs follow cdna_hip_programming.md Guideline 16 R1: every
 // word another workgroup reads in this launch (a bin's centre index, the used flags, the per-item candidates) is
 // stored AND loaded `sc1` (agent-scope atomics), drained before the counter add, so no release / acquire fence runs
@@ -740,10 +741,11 @@ __device__ __forceinline__ bool km_grid_sync(unsigned *bar, unsigned epoch, unsi
         const int G = (int)gridDim.x, g = (int)(blockIdx.x & 7);
         const unsigned ng = (unsigned)((G - g + 7) >> 3), ngroups = (unsigned)min(G, 8);
         int ok = 1;
+        // group g's generation word: its own 128-byte line, polled by that group's workgroups only
         if (__hip_atomic_fetch_add(bar + 32 * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch * ng - 1u &&
             __hip_atomic_fetch_add(bar + 256, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch * ngroups - 1u)
-            __hip_atomic_store(bar + 288, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (unsigned spins = 0; __hip_atomic_load(bar + 288, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch;) {
+            for (int x = 0; x < 8; x++) __hip_atomic_store(bar + 288 + 32 * x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (unsigned spins = 0; __hip_atomic_load(bar + 288 + 32 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch;) {
             if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || ++spins > (1u << 20)) {
                 __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 ok = 0;
@@ -923,7 +925,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                  o_csize = carve((size_t)Ktot * 4), o_mind = carve((size_t)N * 8), o_used = carve(N),
                  o_part = carve((size_t)poff[nb] * 8), o_center = carve((size_t)Ktot * 4), o_akey = carve((size_t)N * 8),
                  o_seed = carve(nb * 4), o_cost = carve(nb * 8), o_moves = carve(nb * 4), o_err = carve(nb * 4),
-                 o_ffd = carve(nb * 4), o_rand = carve((size_t)Ktot * KM_A * 4), o_bar = carve(1280),
+                 o_ffd = carve(nb * 4), o_rand = carve((size_t)Ktot * KM_A * 4), o_bar = carve(2304),
                  o_items = carve(0);
     char *buf = nullptr;
     // the largest work list: one iteration's chunk items for every bin
@@ -1017,8 +1019,8 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
             if (ff_init()) goto fail;
             bool done = false;
             if (g_ff > 0) {
-                unsigned *bar = (unsigned *)(buf + o_bar), *ffail = bar + 300;
-                if (hipMemsetAsync(bar, 0, 1280, st) != hipSuccess) goto fail;  // counters, generation, fail word
+                unsigned *bar = (unsigned *)(buf + o_bar), *ffail = bar + 544;
+                if (hipMemsetAsync(bar, 0, 2304, st) != hipSuccess) goto fail;  // counters, generations, fail word
                 {
                     KTimer tm("kmodes_init", st);
                     hipLaunchKernelGGL(kmb_ff_persist, dim3(g_ff), dim3(KM_FF_NT), 0, st, B, (const KmFfItem *)items,

@@ -237,7 +237,8 @@ __global__ __launch_bounds__(256) void km_init_modes2(KmState s, const int32_t *
 }
 
 // ---- the sequential part of one bin (KModesIter kmodes.pas:869-911), one workgroup of KM_SEQ_NT ----
-static constexpr int KM_SEQ_NT = 512;  // 6 groups of 80 attribute lanes (320..1024 measured: 512 best)
+static constexpr int KM_SEQ_NT = 512;  // 32 moves of 16 lanes (round 2: 6 of 80 lanes; 320..1024 threads: 512 best)
+static constexpr int KM_SEQ_W = 16;    // lanes per move: 5 attributes per lane
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -280,6 +281,58 @@ __device__ void move_point_cat(const KmState &s, int ip, int to, int from, int a
     }
 }
 
+// The same MovePointCat with W lanes per move (W divides 80 into KM_A / W attributes per lane: a = l + W k).  Every
+// attribute's update touches only its own count row and mode byte, so a lane's attributes are independent: their
+// loads are issued together (one dependent round trip for all of them, not one per attribute), then the stores,
+// then the mode checks that read the updated counts -- each attribute sees exactly the reads and writes of the
+// sequential form.
+template <int W>
+__device__ void move_point_cat_w(const KmState &s, int ip, int to, int from, int l) {
+    constexpr int NA = KM_A / W;
+    static_assert(KM_A % W == 0, "W must divide the attribute count");
+    int cur[NA], tcv[NA], fcv[NA], ctv[NA], cfv[NA];
+    int32_t *tc[NA], *fc[NA];
+#pragma unroll
+    for (int k = 0; k < NA; k++) cur[k] = s.X[(long)ip * KM_A + l + W * k];
+#pragma unroll
+    for (int k = 0; k < NA; k++) {
+        const int a = l + W * k;
+        tc[k] = s.freq + ((long)to * KM_A + a) * s.M;
+        fc[k] = s.freq + ((long)from * KM_A + a) * s.M;
+        tcv[k] = tc[k][cur[k]];
+        fcv[k] = fc[k][cur[k]];
+        ctv[k] = s.cent[(long)to * KM_A + a];
+        cfv[k] = s.cent[(long)from * KM_A + a];
+    }
+#pragma unroll
+    for (int k = 0; k < NA; k++) {
+        tc[k][cur[k]] = tcv[k] + 1;
+        fc[k][cur[k]] = fcv[k] - 1;
+    }
+#pragma unroll
+    for (int k = 0; k < NA; k++) {
+        const int a = l + W * k;
+        const int tct = ctv[k] == cur[k] ? tcv[k] + 1 : tc[k][ctv[k]];  // tc[*ct] after the increment
+        if (tct < tcv[k] + 1) s.cent[(long)to * KM_A + a] = (uint8_t)cur[k];
+        if (cfv[k] == cur[k]) {  // the source mode lost a count: GetMaxValueIndex (first max) over the updated row
+            int bi = -1, bv = INT32_MIN;
+            for (int m = 0; m < s.M; m++) {
+                const int v = fc[k][m];
+                if (v > bv) {
+                    bv = v;
+                    bi = m;
+                }
+            }
+            s.cent[(long)from * KM_A + a] = (uint8_t)bi;
+        }
+    }
+    if (l == 0) {
+        s.memb[ip] = to;
+        s.csize[to]++;
+        s.csize[from]--;
+    }
+}
+
 // One 960-point chunk applied in order.  The chunk's assignment keys and labels are staged in LDS, the cost
 // is a parallel sum, and only the points that move are visited, in order (an ordered compaction; a rescue
 // that relabels a later point of the chunk rebuilds the list from there).  MovePointCat of a point touches
@@ -287,9 +340,10 @@ __device__ void move_point_cat(const KmState &s, int ip, int to, int from, int a
 // pairs are pairwise disjoint commute exactly: they are applied together, KM_SEQ_G at a time, by groups of
 // 80 lanes.  A move that empties its cluster (size 1 before it) runs alone and is followed by the rescue
 // (GetMaxClusterMembers + a random member, kmodes.pas:886-906), exactly as the reference orders it.
-template <int NT>
+template <int NT, int W>
 __device__ void bin_seq_body(KmState s, int p0, int p1) {
-    constexpr int KM_SEQ_G = NT / KM_A;  // moves applied concurrently
+    constexpr int KM_SEQ_G = NT / W;  // moves applied concurrently (W lanes each)
+    static_assert(KM_SEQ_G <= 64, "the group is chosen by one wave");
     __shared__ int sh_i[4];
     __shared__ unsigned long long sh_best[NT];
     __shared__ int sh_cnt[NT];
@@ -361,48 +415,60 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
                 c_sz[tid] = sz;
             }
             __syncthreads();
-            // 2. the longest prefix of them that can run together (in list order)
-            if (tid == 0) {
-                int ng = 0, adv = 0, single = 0;
-                for (int k = 0; k < KM_SEQ_G && c_t[k] >= 0; k++) {
-                    const int cl = c_cl[k], old = c_old[k];
-                    if (cl == old) {  // relabelled by an earlier rescue: no longer a move
-                        adv++;
-                        continue;
+            // 2. the longest prefix of them that can run together (in list order), chosen by wave 0 with ballots:
+            // entries whose label already equals their target are skipped (counted in the advance), the first move
+            // that empties its cluster or shares a cluster with an earlier move of the prefix ends it; a move that
+            // empties its cluster at the head runs alone (then the rescue)
+            if (tid < 64) {
+                const int k = tid;
+                const bool valid = k < KM_SEQ_G && c_t[k] >= 0;
+                const int cl = valid ? c_cl[k] : -1, old = valid ? c_old[k] : -2;
+                const bool mv = valid && cl != old;
+                bool clash = false;
+                if (mv)
+                    for (int j = 0; j < k; j++) {
+                        const int cj = c_cl[j], oj = c_old[j];
+                        if (c_t[j] >= 0 && cj != oj) clash |= cj == cl || cj == old || oj == cl || oj == old;
                     }
-                    if (c_sz[k] <= 1) {  // empties its cluster -> alone, then the rescue
-                        if (ng == 0) {
-                            g_t[0] = c_t[k];
-                            g_cl[0] = cl;
-                            g_old[0] = old;
-                            ng = 1;
-                            adv++;
-                            single = 1;
-                        }
-                        break;
+                const unsigned long long stopm = __ballot(mv && (c_sz[k < KM_SEQ_G ? k : 0] <= 1 || clash));
+                const unsigned long long invm = __ballot(!valid);  // lanes >= KM_SEQ_G are invalid: never empty
+                const int first_inv = __builtin_ctzll(invm);
+                const int first_stop = stopm ? __builtin_ctzll(stopm) : 64;
+                const int end = min(first_stop, first_inv);
+                const unsigned long long below_end = end >= 64 ? ~0ull : ((1ull << end) - 1ull);
+                const unsigned long long mvm = __ballot(mv) & below_end;
+                const int ng = __popcll(mvm);
+                if (ng == 0 && first_stop < first_inv) {  // an emptying move at the head: alone
+                    if (k == first_stop) {
+                        g_t[0] = c_t[k];
+                        g_cl[0] = cl;
+                        g_old[0] = old;
+                        g_n = 1;
+                        g_adv = first_stop + 1;
+                        g_single = 1;
                     }
-                    bool clash = false;
-                    for (int j = 0; j < ng; j++)
-                        clash |= g_cl[j] == cl || g_cl[j] == old || g_old[j] == cl || g_old[j] == old;
-                    if (clash) break;
-                    g_t[ng] = c_t[k];
-                    g_cl[ng] = cl;
-                    g_old[ng] = old;
-                    ng++;
-                    adv++;
+                } else {
+                    if (mv && k < end) {
+                        const int r = __popcll(mvm & ((1ull << k) - 1ull));
+                        g_t[r] = c_t[k];
+                        g_cl[r] = cl;
+                        g_old[r] = old;
+                    }
+                    if (k == 0) {
+                        g_n = ng;
+                        g_adv = end;
+                        g_single = 0;
+                    }
                 }
-                g_n = ng;
-                g_adv = adv;
-                g_single = single;
             }
             __syncthreads();
             const int ng = g_n;
             li += g_adv;
             moves += ng;
-            // 3. apply them: lanes [80 j, 80 j + 80) move point j of the group
+            // 3. apply them: lanes [W j, W j + W) move point j of the group
             {
-                const int j = tid / KM_A, a = tid - j * KM_A;
-                if (j < ng) move_point_cat(s, p0 + g_t[j], g_cl[j], g_old[j], a);
+                const int j = tid / W, l = tid - j * W;
+                if (j < ng) move_point_cat_w<W>(s, p0 + g_t[j], g_cl[j], g_old[j], l);
                 if (tid < ng) smemb[g_t[tid]] = g_cl[tid];
             }
             __syncthreads();
@@ -707,11 +773,11 @@ struct KmSeqItem {
 };
 
 // seq items live in the same work list as the assign items (one KmAsgItem slot each)
-template <int NT>
+template <int NT, int W>
 __global__ __launch_bounds__(NT) void kmb_seq_strided(KmBatch B, const KmAsgItem *items) {
     const KmSeqItem it = *reinterpret_cast<const KmSeqItem *>(items + blockIdx.x);
     KmState s = bin_state(B, it.bin);
-    bin_seq_body<NT>(s, it.p0, it.p1);
+    bin_seq_body<NT, W>(s, it.p0, it.p1);
 }
 
 // ---- farthest-first as ONE persistent launch (round 3) ----
@@ -1118,8 +1184,15 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                         // seq items are KmSeqItem views of KmAsgItem slots: stride 32 bytes
                         {
                             KTimer tm("kmodes_seq", st);
-                            hipLaunchKernelGGL(kmb_seq_strided<KM_SEQ_NT>, dim3(sp.second), dim3(KM_SEQ_NT), 0, st, B,
-                                               (const KmAsgItem *)items + pos);
+#ifdef TILER_EXPERIMENTS
+                            static const bool w80 = getenv("TILER_KM_SEQ_W") && atoi(getenv("TILER_KM_SEQ_W")) == 80;
+                            if (w80)  // A/B: round 2's 80 lanes per move (6 moves at a time)
+                                hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, 80>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
+                                                   st, B, (const KmAsgItem *)items + pos);
+                            else
+#endif
+                            hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, KM_SEQ_W>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
+                                               st, B, (const KmAsgItem *)items + pos);
                         }
                         pos += sp.second;
                     }

@@ -714,6 +714,126 @@ __global__ __launch_bounds__(256) void kmb_assign(KmBatch B, const KmAsgItem *it
     if (valid) atomicMin(&s.akey[i], best);
 }
 
+// ---- assignment with at most 16 modalities (round 3) ----
+// The histograms index freq[.][.][M] by byte value, so with M <= 16 every byte of X (and of every mode) is < 16.
+// Then the asm's int8 |r - x| is the plain |r - x| <= 15 and W0 / W4 never wrap (a0 + 256 a1 + S_lo <= 15 + 3,840 +
+// 480 < 2^16):   dis = 2048 #mismatch + (a0 + a8) + 256 (a1 + a9) + sum_{k=16..79} |r_k - x_k|   (= km_dissim).
+// A byte differs iff one of its 4 bit planes differs, so #mismatch is, per 32 bytes, the popcount of the OR of the
+// 4 planes' XORs (3 words) instead of a nonzero-byte count per dword, and the L1 is one v_sad_u8 chain over bytes
+// 16..79 plus two over the packed words (byte 0 | byte 8 << 8) and (byte 1 | byte 9 << 8): ~40 VALU per pair
+// instead of ~155.  Prepared row, KM_PW words: [0, 16) bytes 16..79, [16, 28) planes (word 16 + 3p + k = bit p of
+// bytes 32k .. 32k + 31), 28 the low word, 29 the high word, 30-31 zero.  Points are prepared once per call
+// (X never changes), centroids per stage in LDS (the sequential passes change modes).
+static constexpr int KM_PW = 32;
+static constexpr int KM_A16_CT = 64;  // centroids per LDS stage
+
+__device__ __forceinline__ uint32_t km_prep_word(const uint32_t *row, int w) {
+    if (w < 16) return row[4 + w];
+    if (w < 28) {
+        const int p = (w - 16) / 3, k = (w - 16) % 3;
+        uint32_t r = 0;
+        for (int j = 0; j < 8 && 8 * k + j < 20; j++) {
+            // bits p of the 4 bytes of dword 8k + j -> 4 consecutive bits: (b0 | b1 << 8 | b2 << 16 | b3 << 24) *
+            // 0x01020408 puts b_i at bit 24 + i and nothing else in bits 24..31
+            const uint32_t v = (row[8 * k + j] >> p) & 0x01010101u;
+            r |= ((v * 0x01020408u) >> 24) << (4 * j);
+        }
+        return r;
+    }
+    if (w == 28) return (row[0] & 0xFFu) | ((row[2] & 0xFFu) << 8);
+    if (w == 29) return ((row[0] >> 8) & 0xFFu) | (((row[2] >> 8) & 0xFFu) << 8);
+    return 0;
+}
+
+__device__ __forceinline__ unsigned km_dissim16(const uint32_t *__restrict__ r, const uint32_t *__restrict__ x) {
+    unsigned l1 = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) l1 = __builtin_amdgcn_sad_u8(r[w], x[w], l1);
+    l1 = __builtin_amdgcn_sad_u8(r[28], x[28], l1);
+    const unsigned hi = __builtin_amdgcn_sad_u8(r[29], x[29], 0u);
+    unsigned mism = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+        mism += __popc((r[16 + k] ^ x[16 + k]) | (r[19 + k] ^ x[19 + k]) | (r[22 + k] ^ x[22 + k]) | (r[25 + k] ^ x[25 + k]));
+    return (mism << 11) + l1 + (hi << 8);
+}
+
+// prepared point rows of the (bin-permuted) X; *bad |= 1 if some byte is >= 16
+__global__ __launch_bounds__(256) void kmb_prep_points(const uint8_t *X, long N, uint4 *Xp, unsigned *bad) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < N; i += (long)gridDim.x * 256) {
+        uint32_t row[20];
+        load_row(X + i * KM_A, row);
+        uint32_t big = 0;
+#pragma unroll
+        for (int d = 0; d < 20; d++) big |= row[d] & 0xF0F0F0F0u;
+        if (big) atomicOr(bad, 1u);
+        uint32_t o[KM_PW];
+#pragma unroll
+        for (int w = 0; w < KM_PW; w++) o[w] = km_prep_word(row, w);
+#pragma unroll
+        for (int q = 0; q < KM_PW / 4; q++) Xp[i * (KM_PW / 4) + q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    }
+}
+
+// kmb_assign with km_dissim16; inside a workgroup the argmin runs on 32-bit keys (dis << 13 | 8191 - local index:
+// dis < 2^18, at most 8,192 centroids per workgroup -- host-checked), merged into the u64 key by atomicMin as before
+__global__ __launch_bounds__(256) void kmb_assign16(KmBatch B, const KmAsgItem *items, const uint4 *__restrict__ Xp) {
+    __shared__ uint4 raw[KM_A16_CT * 5];
+    __shared__ uint4 ct[KM_A16_CT * (KM_PW / 4)];
+    KmAsgItem it = items[blockIdx.x];
+    {
+        const int per = (it.c1 - it.c0 + (int)gridDim.y - 1) / (int)gridDim.y;
+        it.c0 += (int)blockIdx.y * per;
+        it.c1 = min(it.c1, it.c0 + per);
+        if (it.c0 >= it.c1) return;
+    }
+    KmState s = bin_state(B, it.bin);
+    const long i = it.p0 + threadIdx.x;
+    const bool valid = i < it.p1;
+    uint32_t x[KM_PW];
+    if (valid) {
+        const uint4 *src = Xp + ((long)B.boff[it.bin] + i) * (KM_PW / 4);
+#pragma unroll
+        for (int q = 0; q < KM_PW / 4; q++) {
+            const uint4 v = src[q];
+            x[4 * q] = v.x;
+            x[4 * q + 1] = v.y;
+            x[4 * q + 2] = v.z;
+            x[4 * q + 3] = v.w;
+        }
+    }
+    unsigned best = ~0u;
+    for (int t0 = it.c0; t0 < it.c1; t0 += KM_A16_CT) {
+        const int cnt = min(KM_A16_CT, it.c1 - t0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < cnt * 5; e += 256) raw[e] = reinterpret_cast<const uint4 *>(s.cent + (long)t0 * KM_A)[e];
+        __syncthreads();
+        for (int e = threadIdx.x; e < cnt * KM_PW; e += 256)
+            reinterpret_cast<uint32_t *>(ct)[e] =
+                km_prep_word(reinterpret_cast<const uint32_t *>(raw + (e / KM_PW) * 5), e % KM_PW);
+        __syncthreads();
+        if (valid) {
+            const unsigned kb = 8191u - (unsigned)(t0 - it.c0);
+            for (int c = 0; c < cnt; c++) {
+                uint32_t r[KM_PW];
+#pragma unroll
+                for (int q = 0; q < KM_PW / 4; q++) {
+                    const uint4 v = ct[c * (KM_PW / 4) + q];
+                    r[4 * q] = v.x;
+                    r[4 * q + 1] = v.y;
+                    r[4 * q + 2] = v.z;
+                    r[4 * q + 3] = v.w;
+                }
+                best = min(best, (km_dissim16(r, x) << 13) | (kb - (unsigned)c));
+            }
+        }
+    }
+    if (valid) {
+        const unsigned c = (unsigned)it.c0 + 8191u - (best & 8191u);
+        atomicMin(&s.akey[i], ((unsigned long long)(best >> 13) << 32) | (0xFFFFFFFFu - c));
+    }
+}
+
 // initial labels + histograms (ComputeKModes kmodes.pas:984-1008), all points of all bins
 __global__ __launch_bounds__(256) void kmb_init_hist(KmBatch B, long N) {
     for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < N; g += (long)gridDim.x * 256) {
@@ -992,7 +1112,14 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                  o_part = carve((size_t)poff[nb] * 8), o_center = carve((size_t)Ktot * 4), o_akey = carve((size_t)N * 8),
                  o_seed = carve(nb * 4), o_cost = carve(nb * 8), o_moves = carve(nb * 4), o_err = carve(nb * 4),
                  o_ffd = carve(nb * 4), o_rand = carve((size_t)Ktot * KM_A * 4), o_bar = carve(2304),
-                 o_items = carve(0);
+                 o_bad = carve(4);
+    // assignment with <= 16 modalities (kmb_assign16): prepared point rows, at most 8,192 centroids per workgroup
+    bool use16 = M <= 16;
+    for (int r = 0; r < nb; r++) use16 = use16 && (Kv[r] + csplit_of(Kv[r]) - 1) / csplit_of(Kv[r]) <= 8192;
+#ifdef TILER_EXPERIMENTS
+    if (getenv("TILER_KM_A16") && atoi(getenv("TILER_KM_A16")) == 0) use16 = false;  // A/B: the general kernel
+#endif
+    const size_t o_Xp = carve(use16 ? (size_t)N * KM_PW * 4 : 0), o_items = carve(0);
     char *buf = nullptr;
     // the largest work list: one iteration's chunk items for every bin
     size_t max_items = 0;
@@ -1056,7 +1183,17 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
         {
             std::vector<unsigned> seeds(nb, 0x42381337u);  // ComputeKModes kmodes.pas:930, per call (= per bin)
             if (hipMemcpyAsync(B.seed, seeds.data(), nb * 4, hipMemcpyHostToDevice, st) != hipSuccess) goto fail;
+            unsigned bad = 0;
+            if (use16) {
+                if (hipMemsetAsync(buf + o_bad, 0, 4, st) != hipSuccess) goto fail;
+                hipLaunchKernelGGL(kmb_prep_points, dim3((unsigned)std::min<long>(4096, (N + 255) / 256)), dim3(256), 0, st,
+                                   B.X, N, (uint4 *)(buf + o_Xp), (unsigned *)(buf + o_bad));
+                if (hipGetLastError() != hipSuccess ||
+                    hipMemcpyAsync(&bad, buf + o_bad, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+                    goto fail;
+            }
             if (hipStreamSynchronize(st) != hipSuccess) goto fail;
+            use16 = use16 && bad == 0;  // a byte >= 16 (outside the declared modalities): the general kernel
         }
         // InitFarthestFirst, all bins round by round
         {
@@ -1122,7 +1259,11 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
             if (hipMemsetAsync(B.akey, 0xff, (size_t)N * 8, st) != hipSuccess) goto fail;
             if (upload(as.data(), as.size() * sizeof(KmAsgItem))) goto fail;
             KTimer tm("kmodes_assign", st);
-            hipLaunchKernelGGL(kmb_assign, dim3((unsigned)as.size(), KM_ASUB), dim3(256), 0, st, B, (const KmAsgItem *)items);
+            if (use16)
+                hipLaunchKernelGGL(kmb_assign16, dim3((unsigned)as.size(), KM_ASUB), dim3(256), 0, st, B,
+                                   (const KmAsgItem *)items, (const uint4 *)(buf + o_Xp));
+            else
+                hipLaunchKernelGGL(kmb_assign, dim3((unsigned)as.size(), KM_ASUB), dim3(256), 0, st, B, (const KmAsgItem *)items);
         }
         if (hipMemsetAsync(B.csize, 0, (size_t)Ktot * 4, st) != hipSuccess ||
             hipMemsetAsync(B.freq, 0, (size_t)Ktot * KM_A * M * 4, st) != hipSuccess)
@@ -1177,8 +1318,12 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     for (const auto &sp : steps) {
                         {
                             KTimer tm("kmodes_assign", st);
-                            hipLaunchKernelGGL(kmb_assign, dim3(sp.first, KM_ASUB), dim3(256), 0, st, B,
-                                               (const KmAsgItem *)items + pos);
+                            if (use16)
+                                hipLaunchKernelGGL(kmb_assign16, dim3(sp.first, KM_ASUB), dim3(256), 0, st, B,
+                                                   (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
+                            else
+                                hipLaunchKernelGGL(kmb_assign, dim3(sp.first, KM_ASUB), dim3(256), 0, st, B,
+                                                   (const KmAsgItem *)items + pos);
                         }
                         pos += sp.first;
                         // seq items are KmSeqItem views of KmAsgItem slots: stride 32 bytes

@@ -95,6 +95,7 @@ struct KmState {
     unsigned long long *cost;  // [1]
     int *moves;                // [1]
     int *err;                  // [1]
+    int *dbg;                  // experiment build: [8] sequential-pass counters of the bin, or nullptr
 };
 
 // ---- farthest-first (InitFarthestFirst kmodes.pas:698-776) ----
@@ -286,14 +287,15 @@ __device__ void move_point_cat(const KmState &s, int ip, int to, int from, int a
 // loads are issued together (one dependent round trip for all of them, not one per attribute), then the stores,
 // then the mode checks that read the updated counts -- each attribute sees exactly the reads and writes of the
 // sequential form.
+// xrow: the point's row already staged in LDS (the move pass prefetches its candidates' rows), or nullptr
 template <int W>
-__device__ void move_point_cat_w(const KmState &s, int ip, int to, int from, int l) {
+__device__ void move_point_cat_w(const KmState &s, int ip, int to, int from, int l, const uint8_t *xrow = nullptr) {
     constexpr int NA = KM_A / W;
     static_assert(KM_A % W == 0, "W must divide the attribute count");
     int cur[NA], tcv[NA], fcv[NA], ctv[NA], cfv[NA];
     int32_t *tc[NA], *fc[NA];
 #pragma unroll
-    for (int k = 0; k < NA; k++) cur[k] = s.X[(long)ip * KM_A + l + W * k];
+    for (int k = 0; k < NA; k++) cur[k] = xrow ? xrow[l + W * k] : s.X[(long)ip * KM_A + l + W * k];
 #pragma unroll
     for (int k = 0; k < NA; k++) {
         const int a = l + W * k;
@@ -309,6 +311,39 @@ __device__ void move_point_cat_w(const KmState &s, int ip, int to, int from, int
         tc[k][cur[k]] = tcv[k] + 1;
         fc[k][cur[k]] = fcv[k] - 1;
     }
+    if (s.M == 16) {
+        // what the two mode rules read after the updates -- tc[*ct] and, where the source mode lost a count, the
+        // whole updated source row (64 B) -- is loaded in ONE round trip for all NA attributes (round 2 walked the row
+        // with one dependent load per value: the rule fires on most groups, ~16 round trips each)
+        int tct[NA];
+        int4 fr[NA][4];
+#pragma unroll
+        for (int k = 0; k < NA; k++) {
+            tct[k] = ctv[k] == cur[k] ? tcv[k] + 1 : tc[k][ctv[k]];
+            if (cfv[k] == cur[k]) {
+                const int4 *r4 = reinterpret_cast<const int4 *>(fc[k]);  // 64-byte rows (M = 16)
+#pragma unroll
+                for (int q = 0; q < 4; q++) fr[k][q] = r4[q];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NA; k++) {
+            const int a = l + W * k;
+            if (tct[k] < tcv[k] + 1) s.cent[(long)to * KM_A + a] = (uint8_t)cur[k];
+            if (cfv[k] == cur[k]) {  // GetMaxValueIndex (kmodes.pas:149-161): first maximum
+                const int v[16] = {fr[k][0].x, fr[k][0].y, fr[k][0].z, fr[k][0].w, fr[k][1].x, fr[k][1].y, fr[k][1].z, fr[k][1].w,
+                                   fr[k][2].x, fr[k][2].y, fr[k][2].z, fr[k][2].w, fr[k][3].x, fr[k][3].y, fr[k][3].z, fr[k][3].w};
+                int bi = 0, bv = v[0];
+#pragma unroll
+                for (int m = 1; m < 16; m++)
+                    if (v[m] > bv) {
+                        bv = v[m];
+                        bi = m;
+                    }
+                s.cent[(long)from * KM_A + a] = (uint8_t)bi;
+            }
+        }
+    } else
 #pragma unroll
     for (int k = 0; k < NA; k++) {
         const int a = l + W * k;
@@ -352,7 +387,8 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
     __shared__ int slist[KM_BIN];
     __shared__ int slen;
     __shared__ int c_t[KM_SEQ_G], c_cl[KM_SEQ_G], c_old[KM_SEQ_G], c_sz[KM_SEQ_G];
-    __shared__ int g_t[KM_SEQ_G], g_cl[KM_SEQ_G], g_old[KM_SEQ_G];
+    __shared__ int g_t[KM_SEQ_G], g_cl[KM_SEQ_G], g_old[KM_SEQ_G], g_k[KM_SEQ_G];
+    __shared__ uint4 c_x[KM_SEQ_G * 5];  // the candidates' rows, fetched with their cluster sizes
     __shared__ int g_n, g_adv, g_single;
     const int n = p1 - p0, tid = threadIdx.x;
     unsigned long long cpart = 0;
@@ -372,7 +408,7 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
     }
     __syncthreads();
     const unsigned long long cost = sh_best[0];
-    int moves = 0;
+    int moves = 0, ngroups = 0, nsingle = 0, nresc = 0, nrebuild = 0;
     int from_pos = 0;
     auto target = [&](int t) { return (int)(0xFFFFFFFFu - (unsigned)(skey[t] & 0xFFFFFFFFull)); };
     for (;;) {
@@ -414,6 +450,10 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
                 c_old[tid] = old;
                 c_sz[tid] = sz;
             }
+            for (int e = tid; e < KM_SEQ_G * 5; e += NT) {  // rows of the candidates (the apply step reads LDS)
+                const int k = li + e / 5;
+                if (k < len) c_x[e] = reinterpret_cast<const uint4 *>(s.X + (long)(p0 + slist[k]) * KM_A)[e % 5];
+            }
             __syncthreads();
             // 2. the longest prefix of them that can run together (in list order), chosen by wave 0 with ballots:
             // entries whose label already equals their target are skipped (counted in the advance), the first move
@@ -443,6 +483,7 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
                         g_t[0] = c_t[k];
                         g_cl[0] = cl;
                         g_old[0] = old;
+                        g_k[0] = k;
                         g_n = 1;
                         g_adv = first_stop + 1;
                         g_single = 1;
@@ -453,6 +494,7 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
                         g_t[r] = c_t[k];
                         g_cl[r] = cl;
                         g_old[r] = old;
+                        g_k[r] = k;
                     }
                     if (k == 0) {
                         g_n = ng;
@@ -465,16 +507,20 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
             const int ng = g_n;
             li += g_adv;
             moves += ng;
+            ngroups++;
+            nsingle += g_single;
             // 3. apply them: lanes [W j, W j + W) move point j of the group
             {
                 const int j = tid / W, l = tid - j * W;
-                if (j < ng) move_point_cat_w<W>(s, p0 + g_t[j], g_cl[j], g_old[j], l);
+                if (j < ng)
+                    move_point_cat_w<W>(s, p0 + g_t[j], g_cl[j], g_old[j], l, reinterpret_cast<const uint8_t *>(c_x + g_k[j] * 5));
                 if (tid < ng) smemb[g_t[tid]] = g_cl[tid];
             }
             __syncthreads();
             if (!g_single) continue;
             const int t = g_t[0], old = g_old[0];
             if (s.csize[old] != 0) continue;
+            nresc++;
             // GetMaxClusterMembers (kmodes.pas:631-669): largest cluster, ties -> last
             unsigned long long b = 0;
             for (int c = tid; c < s.K; c += NT) {
@@ -525,6 +571,7 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
             if (qp - p0 > t && qp < p1) {  // a later point of this chunk was relabelled: rebuild from t + 1
                 from_pos = t + 1;
                 rebuilt = true;
+                nrebuild++;
             }
         }
         if (!rebuilt) break;
@@ -532,6 +579,15 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
     if (tid == 0) {
         s.cost[0] += cost;
         s.moves[0] += moves;
+        if (s.dbg) {
+            atomicAdd(s.dbg + 0, ngroups);
+            atomicAdd(s.dbg + 1, moves);
+            atomicAdd(s.dbg + 2, nsingle);
+            atomicAdd(s.dbg + 3, nresc);
+            atomicAdd(s.dbg + 4, nrebuild);
+            atomicMax(s.dbg + 5, ngroups);
+            atomicAdd(s.dbg + 6, 1);
+        }
     }
 }
 
@@ -553,6 +609,7 @@ struct KmBatch {
     unsigned *seed;               // [nb]
     unsigned long long *cost;     // [nb]
     int *moves, *err, *ffdone;    // [nb]
+    int *dbg;                     // experiment build (TILER_KM_STATS): [nb][8] counters, or nullptr
 };
 
 __device__ __forceinline__ KmState bin_state(const KmBatch &B, int b) {
@@ -575,6 +632,7 @@ __device__ __forceinline__ KmState bin_state(const KmBatch &B, int b) {
     s.cost = B.cost + b;
     s.moves = B.moves + b;
     s.err = B.err + b;
+    s.dbg = B.dbg ? B.dbg + 8 * b : nullptr;
     return s;
 }
 
@@ -1161,6 +1219,11 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     B.moves = (int *)(buf + o_moves);
     B.err = (int *)(buf + o_err);
     B.ffdone = (int *)(buf + o_ffd);
+    B.dbg = nullptr;
+#ifdef TILER_EXPERIMENTS
+    static const bool km_stats = getenv("TILER_KM_STATS") != nullptr;
+    if (km_stats) TILER_HIP_CHECK(hipMalloc((void **)&B.dbg, (size_t)nb * 8 * 4));
+#endif
     int32_t *rand_rows = (int32_t *)(buf + o_rand);
     int rc = -1;
     std::vector<char> hitems;
@@ -1348,6 +1411,23 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     hipMemcpyAsync(herr.data(), B.err, nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                     hipStreamSynchronize(st) != hipSuccess)
                     goto fail;
+#ifdef TILER_EXPERIMENTS
+                if (B.dbg) {  // per iteration: summed counters, the largest bin's, the bin with most groups
+                    std::vector<int> hd((size_t)nb * 8);
+                    if (hipMemcpy(hd.data(), B.dbg, hd.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) goto fail;
+                    long tot[8] = {0};
+                    int wb = -1;
+                    for (int r : active) {
+                        for (int k = 0; k < 8; k++) tot[k] += hd[r * 8 + k];
+                        if (wb < 0 || hd[r * 8 + 0] > hd[wb * 8 + 0]) wb = r;
+                    }
+                    fprintf(stderr, "km_stats iter %d active %zu: groups %ld moves %ld single %ld rescues %ld rebuilds %ld chunks %ld | "
+                            "bin0 (n %d K %d) groups %d moves %d maxg/chunk %d | most groups: bin %d (n %d K %d) groups %d moves %d maxg/chunk %d\n",
+                            iters[active[0]], active.size(), tot[0], tot[1], tot[2], tot[3], tot[4], tot[6], nv[0], Kv[0], hd[0], hd[1], hd[5],
+                            wb, nv[wb], Kv[wb], hd[wb * 8], hd[wb * 8 + 1], hd[wb * 8 + 5]);
+                    if (hipMemset(B.dbg, 0, (size_t)nb * 8 * 4) != hipSuccess) goto fail;
+                }
+#endif
                 std::vector<int> still;
                 for (int r : active) {
                     if (herr[r]) {
@@ -1380,6 +1460,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     } while (0);
 fail:
     if (rc == -1) set_error("kmodes: HIP failure");
+    if (B.dbg) (void)hipFree(B.dbg);
     (void)hipFree(buf);
     return rc < 0 ? -1 : 0;
 }

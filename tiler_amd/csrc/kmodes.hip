@@ -645,6 +645,17 @@ __device__ __forceinline__ int bin_of(const int32_t *off, int nb, long i) {  // 
     return lo;
 }
 
+// start of a KModesIter for the bins act[blockIdx.y]: cost, moves, assignment keys
+__global__ __launch_bounds__(256) void kmb_iter_reset(KmBatch B, const int *act) {
+    const int r = act[blockIdx.y];
+    const long p0 = B.boff[r], n = B.boff[r + 1] - p0;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) B.akey[p0 + i] = ~0ull;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        B.cost[r] = 0;
+        B.moves[r] = 0;
+    }
+}
+
 // farthest-first start (kmodes.pas:698-710): one thread per bin
 __global__ void kmb_ff_start(KmBatch B, const int32_t *start) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1369,12 +1380,19 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     }
                     steps.push_back({na, ns});
                 }
-                if (upload(wl.data(), wl.size() * sizeof(KmAsgItem))) goto fail;
-                for (int r : active) {
-                    iters[r]++;
-                    if (hipMemsetAsync(B.cost + r, 0, 8, st) != hipSuccess || hipMemsetAsync(B.moves + r, 0, 4, st) != hipSuccess)
-                        goto fail;
-                    if (hipMemsetAsync(B.akey + boff[r], 0xff, (size_t)nv[r] * 8, st) != hipSuccess) goto fail;
+                {  // the work list, then the active bins (one reset launch, not three memsets per bin)
+                    const size_t wb = wl.size() * sizeof(KmAsgItem);
+                    hitems.resize(wb + active.size() * 4);
+                    memcpy(hitems.data(), wl.data(), wb);
+                    memcpy(hitems.data() + wb, active.data(), active.size() * 4);
+                    if (upload(hitems.data(), hitems.size())) goto fail;
+                    int maxn = 0;
+                    for (int r : active) {
+                        iters[r]++;
+                        maxn = std::max(maxn, nv[r]);
+                    }
+                    hipLaunchKernelGGL(kmb_iter_reset, dim3((unsigned)std::min(64, (maxn + 255) / 256), (unsigned)active.size()),
+                                       dim3(256), 0, st, B, (const int *)(items + wb));
                 }
                 {
                     size_t pos = 0;

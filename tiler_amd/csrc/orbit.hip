@@ -894,7 +894,16 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
         for (int s = 0; s < OS; s += 2) {
             half8 n0, n1;
             const bool more = s + 2 < OS || cb + 1 < CB;
-            if (s + 2 < OS) {
+            if (MODE == 14 || MODE == 15) {  // timing: no A-fragment LDS reads (the stage's first pair reused; invalid)
+                n0 = a0;
+                n1 = a1;
+                if (s + 2 >= OS && cb + 1 < CB) {
+                    sd0 = SD[(cb + 1) * 8 + 0];
+                    sd1 = SD[(cb + 1) * 8 + 1];
+                    sd2 = SD[(cb + 1) * 8 + 2];
+                    sd3 = SD[(cb + 1) * 8 + 3];
+                }
+            } else if (s + 2 < OS) {
                 n0 = A[(cb * OS + s + 2) * 64];
                 n1 = A[(cb * OS + s + 3) * 64];
             } else if (cb + 1 < CB) {  // next block of this stage: first pair and seeds
@@ -958,8 +967,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                             if (t >= (ss == 10 ? 0 : M3 / 2) && t < (ss == 10 ? M3 / 2 : M3))
                                 Sc[t / 4][t % 4] = Sc[t / 4][t % 4] + mx4(T2, t, true);
                     }
-                } else if (MODE == 11 || MODE == 12) {  // timing experiment: every MFMA chain live + (11) as many VALU adds on registers no MFMA touches (12: none)
-                    const int nd = MODE == 12 ? 0 : ss <= 2 ? 11 : ss <= 4 ? 10 : (ss >= 6 && ss <= 8) ? 11 : ss >= 10 ? 16 : 0;
+                } else if (MODE == 11 || MODE == 12 || MODE == 14) {  // timing experiment: every MFMA chain live + (11) as many VALU adds on registers no MFMA touches (12: none)
+                    const int nd = (MODE == 12 || MODE == 14) ? 0 : ss <= 2 ? 11 : ss <= 4 ? 10 : (ss >= 6 && ss <= 8) ? 11 : ss >= 10 ? 16 : 0;
 #pragma unroll
                     for (int i = 0; i < nd; i++) asm volatile("v_add_f32 %0, %0, |%1|" : "+v"(dm[i & 15]) : "v"(dm[(i + 5) & 15]));
 #pragma unroll
@@ -971,7 +980,7 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                 } else if (MODE == 2) {  // timing experiment: MFMA + loads only (results invalid)
                 } else if (ss <= 2)  // previous block: + |d_3| (RB) -- before step 3's MFMA writes RB
                     acc_abs(T2, RB, ss == 0 ? 0 : ss == 1 ? C1 : C2, ss == 0 ? C1 : ss == 1 ? C2 : N3);
-                if (!LOOSE && MODE != 2 && (MODE < 11 || MODE == 13) && (ss == 3 || ss == 4)) {  // previous block: its max for the list test
+                if (!LOOSE && MODE != 2 && (MODE < 11 || MODE == 13 || MODE == 15) && (ss == 3 || ss == 4)) {  // previous block: its max for the list test
 #pragma unroll
                     for (int q = 0; q < QB; q++) {  // query blocks [0, (QB+1)/2) at step 3, the rest at step 4
                         if ((ss == 3) != (q < (QB + 1) / 2)) continue;
@@ -982,9 +991,9 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                         asm volatile("" ::"v"(pmx[q]));
                     }
                 }
-                if (!LOOSE && MODE != 2 && (MODE < 11 || MODE == 13) && ss >= 6 && ss <= 8)  // this block: + |d_1| (RB, complete after step 5) -- before step 9
+                if (!LOOSE && MODE != 2 && (MODE < 11 || MODE == 13 || MODE == 15) && ss >= 6 && ss <= 8)  // this block: + |d_1| (RB, complete after step 5) -- before step 9
                     acc_abs(P, RB, ss == 6 ? 0 : ss == 7 ? C1 : C2, ss == 6 ? C1 : ss == 7 ? C2 : N3);
-                if (!LOOSE && MODE != 2 && MODE < 11 && ss >= 10)  // this block: + |d_2| (T2, complete after step 8)
+                if (!LOOSE && MODE != 2 && (MODE < 11 || MODE == 15) && ss >= 10)  // this block: + |d_2| (T2, complete after step 8)
                     acc_abs(P, T2, ss == 10 ? 0 : N3 / 2, ss == 10 ? N3 / 2 : N3);
                 if (MODE == 13 && ss >= 9)  // experiment: the |d_2| adds in thirds over steps 9..11 (after step 9's MFMAs)
                     acc_abs(P, T2, ss == 9 ? 0 : ss == 10 ? C1 : C2, ss == 9 ? C1 : ss == 10 ? C2 : N3);
@@ -1073,7 +1082,7 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
             }
         }
     }
-    if (MODE == 11 || MODE == 12)  // timing modes: the dummy adds stay live; the lists stay empty (as MODE 2)
+    if (MODE == 11 || MODE == 12 || MODE == 14)  // timing modes: the dummy adds stay live; the lists stay empty (as MODE 2)
 #pragma unroll
         for (int i = 0; i < 16; i++) asm volatile("" ::"v"(dm[i]));
 }
@@ -2482,6 +2491,10 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             ORB_PIPE(12);
         else if (use_pipe && pmode == 13)  // |d_2| adds spread over k-steps 9..11 (valid)
             ORB_PIPE(13);
+        else if (use_pipe && pmode == 14)  // timing: as 12 without the A-fragment LDS reads (results invalid)
+            ORB_PIPE(14);
+        else if (use_pipe && pmode == 15)  // timing: as 1 (bound, no list updates) without the A-fragment LDS reads (invalid)
+            ORB_PIPE(15);
         else if (use_pipe && pmode == 8)  // one wave per SIMD: 4 waves x 4 query blocks (9: x 3)
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 4, 0>), dim3(wgs, nsplit), dim3(256), lds,
                                stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,

@@ -42,11 +42,11 @@ class KDTree:
                 raise ValueError("dataset must be [n, dd]")
             self.n, self.dd = data.shape
             self._rows = data
-            rowp = (ctypes.POINTER(ctypes.c_float) * max(1, self.n))()
-            base = data.ctypes.data
-            for i in range(self.n):
-                rowp[i] = ctypes.cast(base + 4 * self.dd * i, ctypes.POINTER(ctypes.c_float))
-            h = lib.ann_kdtree_create(rowp, self.n, self.dd, bs, split)
+            # the float** row table (ANNpointArray) as one uint64 array: a per-row ctypes loop cost ~0.2 s at 262k rows
+            rowp = np.uint64(data.ctypes.data) + np.arange(max(1, self.n), dtype=np.uint64) * np.uint64(4 * self.dd)
+            self._rowp = rowp
+            h = lib.ann_kdtree_create(rowp.ctypes.data_as(ctypes.POINTER(ctypes.POINTER(ctypes.c_float))), self.n,
+                                      self.dd, bs, split)
         if not h:
             raise TilerError("ann_kdtree_create failed: " + lib.tiler_last_error().decode())
         self.handle = h

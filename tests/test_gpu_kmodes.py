@@ -33,6 +33,21 @@ def test_kmodes_bit_exact(gpu, oracle, n, k, protos, noise):
     assert np.array_equal(gl, ol) and np.array_equal(gc, oc)
 
 
+@pytest.mark.parametrize("modalities,vmax", [(64, 64), (200, 200), (8, 8)])
+def test_kmodes_other_modalities(gpu, oracle, modalities, vmax):
+    """Byte values beyond 15 (64 / 200 modalities) run the general assignment (kmb_assign: the asm's int8 |r - x|
+    and the W0 / W4 wrap do matter there) and the general mode-rule walk; 8 modalities the <= 16 forms."""
+    rng = np.random.default_rng(modalities)
+    protos = rng.integers(0, vmax, (80, 80)).astype(np.uint8)
+    X = protos[rng.integers(0, 80, 1500)].copy()
+    flip = rng.random(X.shape) < 0.2
+    X[flip] = rng.integers(0, vmax, int(flip.sum()))
+    gl, gc, gi, gcost = compute_kmodes(X, 60, 3, n_modalities=modalities)
+    ol, oc, oi, ocost = oracle.kmodes(X, 60, 3, modalities=modalities)
+    assert (gi, gcost) == (oi, ocost)
+    assert np.array_equal(gl, ol) and np.array_equal(gc, oc)
+
+
 def test_kmodes_duplicates_force_rescue(gpu, oracle):
     rng = np.random.default_rng(77)
     X = _dataset(rng, 800, 5, 0.0)  # 5 distinct rows only: farthest-first picks duplicates, clusters empty

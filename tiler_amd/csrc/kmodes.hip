@@ -240,6 +240,7 @@ __global__ __launch_bounds__(256) void km_init_modes2(KmState s, const int32_t *
 // ---- the sequential part of one bin (KModesIter kmodes.pas:869-911), one workgroup of KM_SEQ_NT ----
 static constexpr int KM_SEQ_NT = 512;  // 32 moves of 16 lanes (round 2: 6 of 80 lanes; 320..1024 threads: 512 best)
 static constexpr int KM_SEQ_W = 16;    // lanes per move: 5 attributes per lane
+static constexpr int KM_CLASH_TAB = 8192;  // buckets of the move pass's cluster-clash table (power of two; exact for K <= 8192)
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -390,6 +391,8 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
     __shared__ int g_t[KM_SEQ_G], g_cl[KM_SEQ_G], g_old[KM_SEQ_G], g_k[KM_SEQ_G];
     __shared__ uint4 c_x[KM_SEQ_G * 5];  // the candidates' rows, fetched with their cluster sizes
     __shared__ int g_n, g_adv, g_single;
+    __shared__ int g_tab[KM_CLASH_TAB];  // cluster hash -> smallest candidate index of the group touching it (64: none)
+    for (int i = threadIdx.x; i < KM_CLASH_TAB; i += NT) g_tab[i] = 64;  // (the first barrier below orders it)
     const int n = p1 - p0, tid = threadIdx.x;
     unsigned long long cpart = 0;
     for (int t = tid; t < n; t += NT) {
@@ -464,12 +467,20 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
                 const bool valid = k < KM_SEQ_G && c_t[k] >= 0;
                 const int cl = valid ? c_cl[k] : -1, old = valid ? c_old[k] : -2;
                 const bool mv = valid && cl != old;
-                bool clash = false;
-                if (mv)
-                    for (int j = 0; j < k; j++) {
-                        const int cj = c_cl[j], oj = c_old[j];
-                        if (c_t[j] >= 0 && cj != oj) clash |= cj == cl || cj == old || oj == cl || oj == old;
-                    }
+                // "shares a cluster with an earlier move": every move enters the smallest index touching each of its
+                // two clusters into a table indexed by cluster mod KM_CLASH_TAB (LDS atomics of one wave are applied in
+                // order, before the reads below); with K > KM_CLASH_TAB a bucket shared by two clusters only ends the
+                // prefix earlier (still a set of pairwise disjoint moves).  Round 2 compared each lane with every earlier one, one LDS round trip each.
+                const int h1 = cl & (KM_CLASH_TAB - 1), h2 = old & (KM_CLASH_TAB - 1);
+                if (mv) {
+                    atomicMin(&g_tab[h1], k);
+                    atomicMin(&g_tab[h2], k);
+                }
+                const bool clash = mv && (g_tab[h1] < k || g_tab[h2] < k);
+                if (mv) {  // back to empty (after every lane's reads: one wave, in order)
+                    g_tab[h1] = 64;
+                    g_tab[h2] = 64;
+                }
                 const unsigned long long stopm = __ballot(mv && (c_sz[k < KM_SEQ_G ? k : 0] <= 1 || clash));
                 const unsigned long long invm = __ballot(!valid);  // lanes >= KM_SEQ_G are invalid: never empty
                 const int first_inv = __builtin_ctzll(invm);

@@ -48,6 +48,18 @@ def test_kmodes_other_modalities(gpu, oracle, modalities, vmax):
     assert np.array_equal(gl, ol) and np.array_equal(gc, oc)
 
 
+def test_kmodes_more_clusters_than_clash_table(gpu, oracle):
+    """K = 8,500 > the move pass's 8,192-bucket clash table (kmodes.hip KM_CLASH_TAB): clusters share buckets, which
+    may only end a group of concurrent moves early; labels, centroids, iterations and cost stay bit-exact."""
+    rng = np.random.default_rng(8500)
+    X = _dataset(rng, 20000, 2000, 0.3)  # 5 iterations with moves (about 10 s of the oracle on 8 threads)
+    start = 20000 - 1 - int(np.argmin(X.astype(np.int64).sum(1)[::-1]))
+    gl, gc, gi, gcost = compute_kmodes(X, 8500, start)
+    ol, oc, oi, ocost = oracle.kmodes(X, 8500, start, threads=_oracle_threads())
+    assert (gi, gcost) == (oi, ocost)
+    assert np.array_equal(gl, ol) and np.array_equal(gc, oc)
+
+
 def test_kmodes_duplicates_force_rescue(gpu, oracle):
     rng = np.random.default_rng(77)
     X = _dataset(rng, 800, 5, 0.0)  # 5 distinct rows only: farthest-first picks duplicates, clusters empty

@@ -415,23 +415,39 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
     int from_pos = 0;
     auto target = [&](int t) { return (int)(0xFFFFFFFFu - (unsigned)(skey[t] & 0xFFFFFFFFull)); };
     for (;;) {
-        // ordered list of the chunk positions >= from_pos whose best cluster differs from their label
-        // (wave 0: contiguous segments per lane, exclusive scan of the counts by shuffles)
+        // ordered list of the chunk positions >= from_pos whose best cluster differs from their label: every thread
+        // flags its positions (t = from_pos + r * NT + tid), ballots rank them inside each wave, one wave scans the
+        // per-(round, wave) counts (round 2: wave 0 walked contiguous segments, two dependent LDS reads per position)
         __syncthreads();
-        if (tid < 64) {
-            const int rem = n - from_pos, seg = (rem + 63) / 64;
-            const int a0 = from_pos + tid * seg, a1 = min(n, a0 + seg);
-            int mine = 0;
-            for (int t = a0; t < a1; t++) mine += target(t) != smemb[t];
-            int incl = mine;
-            for (int o = 1; o < 64; o <<= 1) {
-                const int v = __shfl_up(incl, o, 64);
-                if (tid >= o) incl += v;
+        {
+            constexpr int NWV = NT / 64, MAXR = (KM_BIN + NT - 1) / NT;
+            static_assert(MAXR * NWV <= 64, "one wave scans the counts");
+            const int lane = tid & 63, wv = tid >> 6;
+            unsigned long long bal[MAXR];
+#pragma unroll
+            for (int r = 0; r < MAXR; r++) {
+                const int t = from_pos + r * NT + tid;
+                bal[r] = __ballot(t < n && target(t) != smemb[t]);
+                if (lane == 0) sh_cnt[r * NWV + wv] = __popcll(bal[r]);
             }
-            int w = incl - mine;
-            for (int t = a0; t < a1; t++)
-                if (target(t) != smemb[t]) slist[w++] = t;
-            if (tid == 63) slen = incl;
+            __syncthreads();
+            if (tid < 64) {  // exclusive scan over (round, wave) in position order
+                const int c = tid < MAXR * NWV ? sh_cnt[tid] : 0;
+                int incl = c;
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int v = __shfl_up(incl, o, 64);
+                    if (tid >= o) incl += v;
+                }
+                if (tid < MAXR * NWV) sh_cnt[NT - 64 + tid] = incl - c;
+                if (tid == 63) slen = incl;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < MAXR; r++) {
+                const int t = from_pos + r * NT + tid;
+                if ((bal[r] >> lane) & 1)
+                    slist[sh_cnt[NT - 64 + r * NWV + wv] + __popcll(bal[r] & ((1ull << lane) - 1ull))] = t;
+            }
         }
         __syncthreads();
         const int len = slen;

@@ -96,6 +96,8 @@ struct KmState {
     int *moves;                // [1]
     int *err;                  // [1]
     int *dbg;                  // experiment build: [8] sequential-pass counters of the bin, or nullptr
+    int4 *mvl;                 // [2 * KM_BIN] this chunk's moves in order (point, to, from, 1 = first of its group)
+    int *mvn;                  // [1] their count
 };
 
 // ---- farthest-first (InitFarthestFirst kmodes.pas:698-776) ----
@@ -288,6 +290,79 @@ __device__ void move_point_cat(const KmState &s, int ip, int to, int from, int a
 // loads are issued together (one dependent round trip for all of them, not one per attribute), then the stores,
 // then the mode checks that read the updated counts -- each attribute sees exactly the reads and writes of the
 // sequential form.
+// The attribute updates of MovePointCat (kmodes.pas:778-807) for the NA attributes a = a0 + l + W k of one lane, every
+// load of a kind issued together (one dependent round trip for all of them), then the stores, then the mode rules on
+// the updated counts; no membership / size updates (the decision pass made them).
+template <int W, int NA>
+__device__ __forceinline__ void apply_point_attrs(const KmState &s, int ip, int to, int from, int a0) {
+    int cur[NA], tcv[NA], fcv[NA], ctv[NA], cfv[NA];
+    int32_t *tc[NA], *fc[NA];
+#pragma unroll
+    for (int k = 0; k < NA; k++) cur[k] = s.X[(long)ip * KM_A + a0 + W * k];
+#pragma unroll
+    for (int k = 0; k < NA; k++) {
+        const int a = a0 + W * k;
+        tc[k] = s.freq + ((long)to * KM_A + a) * s.M;
+        fc[k] = s.freq + ((long)from * KM_A + a) * s.M;
+        tcv[k] = tc[k][cur[k]];
+        fcv[k] = fc[k][cur[k]];
+        ctv[k] = s.cent[(long)to * KM_A + a];
+        cfv[k] = s.cent[(long)from * KM_A + a];
+    }
+#pragma unroll
+    for (int k = 0; k < NA; k++) {
+        tc[k][cur[k]] = tcv[k] + 1;
+        fc[k][cur[k]] = fcv[k] - 1;
+    }
+    if (s.M == 16) {
+        int tct[NA];
+        int4 fr[NA][4];
+#pragma unroll
+        for (int k = 0; k < NA; k++) {
+            tct[k] = ctv[k] == cur[k] ? tcv[k] + 1 : tc[k][ctv[k]];
+            if (cfv[k] == cur[k]) {
+                const int4 *r4 = reinterpret_cast<const int4 *>(fc[k]);  // 64-byte rows (M = 16)
+#pragma unroll
+                for (int q = 0; q < 4; q++) fr[k][q] = r4[q];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NA; k++) {
+            const int a = a0 + W * k;
+            if (tct[k] < tcv[k] + 1) s.cent[(long)to * KM_A + a] = (uint8_t)cur[k];
+            if (cfv[k] == cur[k]) {  // GetMaxValueIndex (kmodes.pas:149-161): first maximum
+                const int v[16] = {fr[k][0].x, fr[k][0].y, fr[k][0].z, fr[k][0].w, fr[k][1].x, fr[k][1].y, fr[k][1].z, fr[k][1].w,
+                                   fr[k][2].x, fr[k][2].y, fr[k][2].z, fr[k][2].w, fr[k][3].x, fr[k][3].y, fr[k][3].z, fr[k][3].w};
+                int bi = 0, bv = v[0];
+#pragma unroll
+                for (int m = 1; m < 16; m++)
+                    if (v[m] > bv) {
+                        bv = v[m];
+                        bi = m;
+                    }
+                s.cent[(long)from * KM_A + a] = (uint8_t)bi;
+            }
+        }
+    } else
+#pragma unroll
+    for (int k = 0; k < NA; k++) {
+        const int a = a0 + W * k;
+        const int tct = ctv[k] == cur[k] ? tcv[k] + 1 : tc[k][ctv[k]];
+        if (tct < tcv[k] + 1) s.cent[(long)to * KM_A + a] = (uint8_t)cur[k];
+        if (cfv[k] == cur[k]) {
+            int bi = -1, bv = INT32_MIN;
+            for (int m = 0; m < s.M; m++) {
+                const int v = fc[k][m];
+                if (v > bv) {
+                    bv = v;
+                    bi = m;
+                }
+            }
+            s.cent[(long)from * KM_A + a] = (uint8_t)bi;
+        }
+    }
+}
+
 // xrow: the point's row already staged in LDS (the move pass prefetches its candidates' rows), or nullptr
 template <int W>
 __device__ void move_point_cat_w(const KmState &s, int ip, int to, int from, int l, const uint8_t *xrow = nullptr) {
@@ -376,7 +451,10 @@ __device__ void move_point_cat_w(const KmState &s, int ip, int to, int from, int
 // pairs are pairwise disjoint commute exactly: they are applied together, KM_SEQ_G at a time, by groups of
 // 80 lanes.  A move that empties its cluster (size 1 before it) runs alone and is followed by the rescue
 // (GetMaxClusterMembers + a random member, kmodes.pas:886-906), exactly as the reference orders it.
-template <int NT, int W>
+// DECIDE: the decision pass -- the same move sequence (every decision reads only labels, targets and cluster sizes:
+// none reads a count or a mode), with the labels and sizes updated and every move appended in order to s.mvl (group
+// starts flagged) instead of applied; kmb_seq_apply then applies the attribute updates over many workgroups.
+template <int NT, int W, bool DECIDE = false>
 __device__ void bin_seq_body(KmState s, int p0, int p1) {
     constexpr int KM_SEQ_G = NT / W;  // moves applied concurrently (W lanes each)
     static_assert(KM_SEQ_G <= 64, "the group is chosen by one wave");
@@ -391,9 +469,13 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
     __shared__ int g_t[KM_SEQ_G], g_cl[KM_SEQ_G], g_old[KM_SEQ_G], g_k[KM_SEQ_G];
     __shared__ uint4 c_x[KM_SEQ_G * 5];  // the candidates' rows, fetched with their cluster sizes
     __shared__ int g_n, g_adv, g_single;
+    int nlist = 0;  // DECIDE: moves appended (uniform)
     __shared__ int g_tab[KM_CLASH_TAB];  // cluster hash -> smallest candidate index of the group touching it (64: none)
     for (int i = threadIdx.x; i < KM_CLASH_TAB; i += NT) g_tab[i] = 64;  // (the first barrier below orders it)
     const int n = p1 - p0, tid = threadIdx.x;
+    // experiment build (s.dbg): shader-clock sums of the phases (wave 0's view): staging, list builds, candidate
+    // fetch, group choice, apply, rescue
+    unsigned long long tm_[6] = {0, 0, 0, 0, 0, 0}, tm0 = s.dbg ? __builtin_amdgcn_s_memtime() : 0, tma = 0;
     unsigned long long cpart = 0;
     for (int t = tid; t < n; t += NT) {
         const unsigned long long k = s.akey[p0 + t];
@@ -411,6 +493,10 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
     }
     __syncthreads();
     const unsigned long long cost = sh_best[0];
+    if (s.dbg) {
+        tma = __builtin_amdgcn_s_memtime();
+        tm_[0] += tma - tm0;
+    }
     int moves = 0, ngroups = 0, nsingle = 0, nresc = 0, nrebuild = 0;
     int from_pos = 0;
     auto target = [&](int t) { return (int)(0xFFFFFFFFu - (unsigned)(skey[t] & 0xFFFFFFFFull)); };
@@ -451,6 +537,11 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
         }
         __syncthreads();
         const int len = slen;
+        if (s.dbg) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            tm_[1] += t - tma;
+            tma = t;
+        }
         bool rebuilt = false;
         int li = 0;
         while (li < len && !rebuilt) {
@@ -469,11 +560,17 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
                 c_old[tid] = old;
                 c_sz[tid] = sz;
             }
-            for (int e = tid; e < KM_SEQ_G * 5; e += NT) {  // rows of the candidates (the apply step reads LDS)
-                const int k = li + e / 5;
-                if (k < len) c_x[e] = reinterpret_cast<const uint4 *>(s.X + (long)(p0 + slist[k]) * KM_A)[e % 5];
-            }
+            if (!DECIDE)
+                for (int e = tid; e < KM_SEQ_G * 5; e += NT) {  // rows of the candidates (the apply step reads LDS)
+                    const int k = li + e / 5;
+                    if (k < len) c_x[e] = reinterpret_cast<const uint4 *>(s.X + (long)(p0 + slist[k]) * KM_A)[e % 5];
+                }
             __syncthreads();
+            if (s.dbg) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                tm_[2] += t - tma;
+                tma = t;
+            }
             // 2. the longest prefix of them that can run together (in list order), chosen by wave 0 with ballots:
             // entries whose label already equals their target are skipped (counted in the advance), the first move
             // that empties its cluster or shares a cluster with an earlier move of the prefix ends it; a move that
@@ -531,19 +628,39 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
                 }
             }
             __syncthreads();
+            if (s.dbg) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                tm_[3] += t - tma;
+                tma = t;
+            }
             const int ng = g_n;
             li += g_adv;
             moves += ng;
             ngroups++;
             nsingle += g_single;
             // 3. apply them: lanes [W j, W j + W) move point j of the group
-            {
+            if (DECIDE) {  // labels and sizes now (cluster-disjoint moves: no two threads touch one size), the move listed
+                if (tid < ng) {
+                    const int ip = p0 + g_t[tid], to = g_cl[tid], from = g_old[tid];
+                    s.memb[ip] = to;
+                    s.csize[to]++;
+                    s.csize[from]--;
+                    s.mvl[nlist + tid] = make_int4(ip, to, from, tid == 0 ? 1 : 0);
+                    smemb[g_t[tid]] = to;
+                }
+                nlist += ng;
+            } else {
                 const int j = tid / W, l = tid - j * W;
                 if (j < ng)
                     move_point_cat_w<W>(s, p0 + g_t[j], g_cl[j], g_old[j], l, reinterpret_cast<const uint8_t *>(c_x + g_k[j] * 5));
                 if (tid < ng) smemb[g_t[tid]] = g_cl[tid];
             }
             __syncthreads();
+            if (s.dbg) {
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                tm_[4] += t - tma;
+                tma = t;
+            }
             if (!g_single) continue;
             const int t = g_t[0], old = g_old[0];
             if (s.csize[old] != 0) continue;
@@ -592,7 +709,17 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
             }
             __syncthreads();
             const int qp = sh_i[3];
-            if (tid < KM_A) move_point_cat(s, qp, old, from, tid);
+            if (DECIDE) {
+                if (tid == 0) {
+                    s.memb[qp] = old;
+                    s.csize[old]++;
+                    s.csize[from]--;
+                    s.mvl[nlist] = make_int4(qp, old, from, 1);
+                }
+                nlist++;
+            } else if (tid < KM_A) {
+                move_point_cat(s, qp, old, from, tid);
+            }
             if (tid == 0 && qp >= p0 && qp < p1) smemb[qp - p0] = old;
             __syncthreads();
             if (qp - p0 > t && qp < p1) {  // a later point of this chunk was relabelled: rebuild from t + 1
@@ -600,10 +727,16 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
                 rebuilt = true;
                 nrebuild++;
             }
+            if (s.dbg) {
+                const unsigned long long tt = __builtin_amdgcn_s_memtime();
+                tm_[5] += tt - tma;
+                tma = tt;
+            }
         }
         if (!rebuilt) break;
     }
     if (tid == 0) {
+        if (DECIDE) *s.mvn = nlist;
         s.cost[0] += cost;
         s.moves[0] += moves;
         if (s.dbg) {
@@ -614,6 +747,8 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
             atomicAdd(s.dbg + 4, nrebuild);
             atomicMax(s.dbg + 5, ngroups);
             atomicAdd(s.dbg + 6, 1);
+            unsigned long long *t64 = reinterpret_cast<unsigned long long *>(s.dbg + 8);  // [8..19]: 6 u64 clock sums
+            for (int q = 0; q < 6; q++) atomicAdd(t64 + q, tm_[q]);
         }
     }
 }
@@ -637,6 +772,8 @@ struct KmBatch {
     unsigned long long *cost;     // [nb]
     int *moves, *err, *ffdone;    // [nb]
     int *dbg;                     // experiment build (TILER_KM_STATS): [nb][8] counters, or nullptr
+    int4 *mvl;                    // [nb][2 * KM_BIN] move lists of the decision pass
+    int *mvn;                     // [nb]
 };
 
 __device__ __forceinline__ KmState bin_state(const KmBatch &B, int b) {
@@ -659,7 +796,9 @@ __device__ __forceinline__ KmState bin_state(const KmBatch &B, int b) {
     s.cost = B.cost + b;
     s.moves = B.moves + b;
     s.err = B.err + b;
-    s.dbg = B.dbg ? B.dbg + 8 * b : nullptr;
+    s.dbg = B.dbg ? B.dbg + 24 * b : nullptr;
+    s.mvl = B.mvl + (long)b * 2 * KM_BIN;
+    s.mvn = B.mvn + b;
     return s;
 }
 
@@ -989,11 +1128,66 @@ struct KmSeqItem {
 };
 
 // seq items live in the same work list as the assign items (one KmAsgItem slot each)
-template <int NT, int W>
+template <int NT, int W, bool DECIDE = false>
 __global__ __launch_bounds__(NT) void kmb_seq_strided(KmBatch B, const KmAsgItem *items) {
     const KmSeqItem it = *reinterpret_cast<const KmSeqItem *>(items + blockIdx.x);
     KmState s = bin_state(B, it.bin);
-    bin_seq_body<NT, W>(s, it.p0, it.p1);
+    bin_seq_body<NT, W, DECIDE>(s, it.p0, it.p1);
+}
+
+// The attribute updates of one chunk's move list (kmb_seq_strided<.., true>), attributes split over NSLICE
+// workgroups per bin (blockIdx.y): each applies the list in order, group after group, the moves of a group (pairwise
+// cluster-disjoint) at once, one lane per (move, attribute).  Every (cluster, attribute) sees its updates in the
+// reference's order; attributes are independent of each other.  Round 2 applied them on the deciding workgroup alone
+// (one CU's memory traffic: ~10 us per group of ~26 moves, each touching 160 count rows).
+static constexpr int KM_APPLY_SLICES = 10;
+template <int NSLICE>
+__global__ __launch_bounds__(32 * (KM_A / NSLICE)) void kmb_seq_apply(KmBatch B, const KmAsgItem *items) {
+    constexpr int W = KM_A / NSLICE, NT = 32 * W;  // one attribute per lane, 32 moves per pass
+    static_assert(KM_A % NSLICE == 0 && NT % 64 == 0, "attribute slices");
+    __shared__ int gs[2 * KM_BIN + 1];  // group starts
+    __shared__ int ngr;
+    const KmSeqItem it = *reinterpret_cast<const KmSeqItem *>(items + blockIdx.x);
+    KmState s = bin_state(B, it.bin);
+    const int n = *s.mvn, tid = threadIdx.x;
+    if (n == 0) return;  // uniform
+    // group starts in list order: ballot ranks per wave, wave totals through LDS (one wave scans them)
+    __shared__ int wtot[2 * KM_BIN / 64 + 2];
+    const int nw = (n + 63) / 64;
+    for (int i0 = 0; i0 < nw * 64; i0 += NT) {
+        const int i = i0 + tid;
+        const bool f = i < n && s.mvl[i].w != 0;
+        const unsigned long long b = __ballot(f);
+        if ((tid & 63) == 0 && i < nw * 64) wtot[i >> 6] = __popcll(b);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int w = 0; w < nw; w++) {
+            const int c = wtot[w];
+            wtot[w] = acc;
+            acc += c;
+        }
+        ngr = acc;
+        gs[acc] = n;
+    }
+    __syncthreads();
+    for (int i0 = 0; i0 < nw * 64; i0 += NT) {
+        const int i = i0 + tid;
+        const bool f = i < n && s.mvl[i].w != 0;
+        const unsigned long long b = __ballot(f);
+        if (f) gs[wtot[i >> 6] + __popcll(b & ((1ull << (tid & 63)) - 1ull))] = i;
+    }
+    __syncthreads();
+    const int G = ngr, j = tid / W, l = tid - j * W, a0 = blockIdx.y * W + l;
+    for (int g = 0; g < G; g++) {
+        const int m = gs[g] + j;
+        if (m < gs[g + 1]) {
+            const int4 mv = s.mvl[m];
+            apply_point_attrs<W, 1>(s, mv.x, mv.y, mv.z, a0);
+        }
+        __syncthreads();  // the next group may touch these clusters' rows
+    }
 }
 
 // ---- farthest-first as ONE persistent launch (round 3) ----
@@ -1208,7 +1402,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                  o_part = carve((size_t)poff[nb] * 8), o_center = carve((size_t)Ktot * 4), o_akey = carve((size_t)N * 8),
                  o_seed = carve(nb * 4), o_cost = carve(nb * 8), o_moves = carve(nb * 4), o_err = carve(nb * 4),
                  o_ffd = carve(nb * 4), o_rand = carve((size_t)Ktot * KM_A * 4), o_bar = carve(2304),
-                 o_bad = carve(4);
+                 o_bad = carve(4), o_mvl = carve((size_t)nb * 2 * KM_BIN * 16), o_mvn = carve((size_t)nb * 4);
     // assignment with <= 16 modalities (kmb_assign16): prepared point rows, at most 8,192 centroids per workgroup
     bool use16 = M <= 16;
     for (int r = 0; r < nb; r++) use16 = use16 && (Kv[r] + csplit_of(Kv[r]) - 1) / csplit_of(Kv[r]) <= 8192;
@@ -1257,10 +1451,12 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     B.moves = (int *)(buf + o_moves);
     B.err = (int *)(buf + o_err);
     B.ffdone = (int *)(buf + o_ffd);
+    B.mvl = (int4 *)(buf + o_mvl);
+    B.mvn = (int *)(buf + o_mvn);
     B.dbg = nullptr;
 #ifdef TILER_EXPERIMENTS
     static const bool km_stats = getenv("TILER_KM_STATS") != nullptr;
-    if (km_stats) TILER_HIP_CHECK(hipMalloc((void **)&B.dbg, (size_t)nb * 8 * 4));
+    if (km_stats) TILER_HIP_CHECK(hipMalloc((void **)&B.dbg, (size_t)nb * 24 * 4));
 #endif
     int32_t *rand_rows = (int32_t *)(buf + o_rand);
     int rc = -1;
@@ -1439,13 +1635,21 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                             KTimer tm("kmodes_seq", st);
 #ifdef TILER_EXPERIMENTS
                             static const bool w80 = getenv("TILER_KM_SEQ_W") && atoi(getenv("TILER_KM_SEQ_W")) == 80;
-                            if (w80)  // A/B: round 2's 80 lanes per move (6 moves at a time)
+                            static const bool oldseq = getenv("TILER_KM_APPLY") && atoi(getenv("TILER_KM_APPLY")) == 0;
+                            if (w80)  // A/B: round 2's 80 lanes per move (6 moves at a time), applied in place
                                 hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, 80>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
+                                                   st, B, (const KmAsgItem *)items + pos);
+                            else if (oldseq)  // A/B: decided and applied by one workgroup per bin
+                                hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, KM_SEQ_W>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
                                                    st, B, (const KmAsgItem *)items + pos);
                             else
 #endif
-                            hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, KM_SEQ_W>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
-                                               st, B, (const KmAsgItem *)items + pos);
+                            {  // the decisions (one workgroup per bin), then the attribute updates over KM_APPLY_SLICES each
+                                hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, KM_SEQ_W, true>), dim3(sp.second),
+                                                   dim3(KM_SEQ_NT), 0, st, B, (const KmAsgItem *)items + pos);
+                                hipLaunchKernelGGL((kmb_seq_apply<KM_APPLY_SLICES>), dim3(sp.second, KM_APPLY_SLICES),
+                                                   dim3(32 * (KM_A / KM_APPLY_SLICES)), 0, st, B, (const KmAsgItem *)items + pos);
+                            }
                         }
                         pos += sp.second;
                     }
@@ -1458,19 +1662,24 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     goto fail;
 #ifdef TILER_EXPERIMENTS
                 if (B.dbg) {  // per iteration: summed counters, the largest bin's, the bin with most groups
-                    std::vector<int> hd((size_t)nb * 8);
+                    std::vector<int> hd((size_t)nb * 24);
                     if (hipMemcpy(hd.data(), B.dbg, hd.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) goto fail;
                     long tot[8] = {0};
                     int wb = -1;
                     for (int r : active) {
-                        for (int k = 0; k < 8; k++) tot[k] += hd[r * 8 + k];
-                        if (wb < 0 || hd[r * 8 + 0] > hd[wb * 8 + 0]) wb = r;
+                        for (int k = 0; k < 8; k++) tot[k] += hd[r * 24 + k];
+                        if (wb < 0 || hd[r * 24 + 0] > hd[wb * 24 + 0]) wb = r;
                     }
                     fprintf(stderr, "km_stats iter %d active %zu: groups %ld moves %ld single %ld rescues %ld rebuilds %ld chunks %ld | "
                             "bin0 (n %d K %d) groups %d moves %d maxg/chunk %d | most groups: bin %d (n %d K %d) groups %d moves %d maxg/chunk %d\n",
                             iters[active[0]], active.size(), tot[0], tot[1], tot[2], tot[3], tot[4], tot[6], nv[0], Kv[0], hd[0], hd[1], hd[5],
-                            wb, nv[wb], Kv[wb], hd[wb * 8], hd[wb * 8 + 1], hd[wb * 8 + 5]);
-                    if (hipMemset(B.dbg, 0, (size_t)nb * 8 * 4) != hipSuccess) goto fail;
+                            wb, nv[wb], Kv[wb], hd[wb * 24], hd[wb * 24 + 1], hd[wb * 24 + 5]);
+                    {
+                        const unsigned long long *c0 = reinterpret_cast<const unsigned long long *>(hd.data() + 8);
+                        fprintf(stderr, "km_clock iter %d bin0 Mcycles: staging %.2f lists %.2f fetch %.2f choose %.2f apply %.2f rescue %.2f\n",
+                                iters[active[0]], c0[0] / 1e6, c0[1] / 1e6, c0[2] / 1e6, c0[3] / 1e6, c0[4] / 1e6, c0[5] / 1e6);
+                    }
+                    if (hipMemset(B.dbg, 0, (size_t)nb * 24 * 4) != hipSuccess) goto fail;
                 }
 #endif
                 std::vector<int> still;

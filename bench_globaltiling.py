@@ -96,7 +96,7 @@ def run(args) -> dict:
     t_km = time.perf_counter() - t1
     lib.tiler_timing_enable(0)
     phases = {}
-    for name in ("kmodes_init", "kmodes_assign", "kmodes_seq"):
+    for name in ("kmodes_init", "kmodes_assign", "kmodes_seq", "kmodes_apply"):
         n = ctypes.c_int(0)
         ms = lib.tiler_timing_get(name.encode(), ctypes.byref(n))
         phases[name] = {"ms_total": round(ms, 2), "launches": n.value}

@@ -1644,12 +1644,32 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                                                    st, B, (const KmAsgItem *)items + pos);
                             else
 #endif
-                            {  // the decisions (one workgroup per bin), then the attribute updates over KM_APPLY_SLICES each
+                                // the decisions (one workgroup per bin), then the attribute updates over KM_APPLY_SLICES each
                                 hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, KM_SEQ_W, true>), dim3(sp.second),
                                                    dim3(KM_SEQ_NT), 0, st, B, (const KmAsgItem *)items + pos);
-                                hipLaunchKernelGGL((kmb_seq_apply<KM_APPLY_SLICES>), dim3(sp.second, KM_APPLY_SLICES),
-                                                   dim3(32 * (KM_A / KM_APPLY_SLICES)), 0, st, B, (const KmAsgItem *)items + pos);
-                            }
+                        }
+#ifdef TILER_EXPERIMENTS
+                        if (!(getenv("TILER_KM_SEQ_W") && atoi(getenv("TILER_KM_SEQ_W")) == 80) &&
+                            !(getenv("TILER_KM_APPLY") && atoi(getenv("TILER_KM_APPLY")) == 0))
+#endif
+                        {
+                            KTimer tm("kmodes_apply", st);
+#ifdef TILER_EXPERIMENTS
+                            static const int sl = getenv("TILER_KM_SLICES") ? atoi(getenv("TILER_KM_SLICES")) : KM_APPLY_SLICES;
+#define KM_APPLY_AB(NS)                                                                                              \
+    hipLaunchKernelGGL((kmb_seq_apply<NS>), dim3(sp.second, NS), dim3(32 * (KM_A / NS)), 0, st, B,                  \
+                       (const KmAsgItem *)items + pos)
+                            if (sl == 5)
+                                KM_APPLY_AB(5);
+                            else if (sl == 20)
+                                KM_APPLY_AB(20);
+                            else if (sl == 40)
+                                KM_APPLY_AB(40);
+                            else
+#undef KM_APPLY_AB
+#endif
+                            hipLaunchKernelGGL((kmb_seq_apply<KM_APPLY_SLICES>), dim3(sp.second, KM_APPLY_SLICES),
+                                               dim3(32 * (KM_A / KM_APPLY_SLICES)), 0, st, B, (const KmAsgItem *)items + pos);
                         }
                         pos += sp.second;
                     }

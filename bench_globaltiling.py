@@ -5,7 +5,8 @@ DoGlobalTiling (main.pas:4256-4370) on the SURVEY.md 8(d) synthetic workload: 1,
 65,536 prototypes with 10 % per-byte perturbation, DitheringPalIndex bins with Zipf(1.1) sizes over
 128 palettes, desired 65,536 tiles.  The K-Modes of every bin (DoKModes main.pas:4195-4254, run
 concurrently by ProcThreadPool at main.pas:4339) is ONE tiler_kmodes_batch call on the GPU; the
-timed step is that call + the medoid batch (inputs resident in HBM).  A bounded CPU baseline runs the
+timed step is that call (after one untimed run, kernel timers off) + the medoid batch (inputs resident in
+HBM).  A bounded CPU baseline runs the
 oracle's restatement (pinned to the reference asm) on the smallest bins and checks them bit-exact.
 
 Prints one JSON line.  Not the headline metric (bench.py is); a secondary measurement of §8 rows a9-a13.
@@ -86,14 +87,22 @@ def run(args) -> dict:
     vp = ctypes.c_void_p
     p = lambda a: a.ctypes.data_as(vp)  # noqa: E731
     stream = torch.cuda.current_stream(dev).cuda_stream
-    torch.cuda.synchronize(dev)
+    def kmodes_batch():
+        check(lib.tiler_kmodes_batch_dev(vp(d_X.data_ptr()), p(off), len(run), p(ks), p(st), 16,
+                                         vp(d_lab.data_ptr()), vp(d_cent.data_ptr()), p(iters), p(costs),
+                                         vp(stream)), "tiler_kmodes_batch_dev")
+        torch.cuda.synchronize(dev)
+
+    # one untimed run (module load, workspace growth), then the timed run with the per-phase HIP event
+    # timers OFF (an event pair between two dependent launches costs several microseconds, ~50 ms over the
+    # 6,422 chunk steps), then a third run with them on for the phase breakdown only
+    kmodes_batch()
+    t1 = time.perf_counter()
+    kmodes_batch()
+    t_km = time.perf_counter() - t1
     lib.tiler_timing_reset()
     lib.tiler_timing_enable(1)
-    t1 = time.perf_counter()
-    check(lib.tiler_kmodes_batch_dev(vp(d_X.data_ptr()), p(off), len(run), p(ks), p(st), 16, vp(d_lab.data_ptr()),
-                                     vp(d_cent.data_ptr()), p(iters), p(costs), vp(stream)), "tiler_kmodes_batch_dev")
-    torch.cuda.synchronize(dev)
-    t_km = time.perf_counter() - t1
+    kmodes_batch()
     lib.tiler_timing_enable(0)
     phases = {}
     for name in ("kmodes_init", "kmodes_assign", "kmodes_seq", "kmodes_apply"):

@@ -20,6 +20,7 @@ import math
 import os
 import sys
 import time
+import zlib
 
 import numpy as np
 
@@ -168,6 +169,7 @@ def run(args) -> dict:
                    "largest_bin": int(np.diff(off).max()), "largest_k": int(ks.max())},
         "kmodes_s": round(t_km, 3), "medoids_s": round(t_med, 3), "host_prep_s": round(host_prep, 2),
         "iterations": {"max": int(iters.max()), "mean": round(float(iters.mean()), 2)}, "phases": phases,
+        "digest": "%08x" % zlib.crc32(cent.tobytes(), zlib.crc32(labels.tobytes())),  # A/B runs: same bins
         "cpu_baseline": cpu,
     }
     del d_X, d_lab, d_cent

@@ -1011,20 +1011,23 @@ __global__ __launch_bounds__(256) void kmb_prep_points(const uint8_t *X, long N,
 }
 
 // kmb_assign with km_dissim16; inside a workgroup the argmin runs on 32-bit keys (dis << 13 | 8191 - local index:
-// dis < 2^18, at most 8,192 centroids per workgroup -- host-checked), merged into the u64 key by atomicMin as before
-__global__ __launch_bounds__(256) void kmb_assign16(KmBatch B, const KmAsgItem *items, const uint4 *__restrict__ Xp) {
-    __shared__ uint4 raw[KM_A16_CT * 5];
-    __shared__ uint4 ct[KM_A16_CT * (KM_PW / 4)];
-    KmAsgItem it = items[blockIdx.x];
-    {
-        const int per = (it.c1 - it.c0 + (int)gridDim.y - 1) / (int)gridDim.y;
-        it.c0 += (int)blockIdx.y * per;
-        it.c1 = min(it.c1, it.c0 + per);
-        if (it.c0 >= it.c1) return;
-    }
+// dis < 2^18, at most 8,192 centroids per workgroup -- host-checked), merged into the u64 key by atomicMin as before.
+// G groups of 256 threads per workgroup, each one point per thread over its own slice of the item's centroids (the
+// item split over gridDim.y * G slices): the late chunk steps (960 points x 5,035 centroids, 1,264 slices) cost
+// ~6 ns per dispatched workgroup beyond their work (r03zl: 4 -> 16 slices per item +143 ms), so fewer, larger
+// workgroups.  r03zk: P points per thread instead (fewer waves, same LDS-broadcast reads per pair) was slower.
+template <int G, bool PF = false>
+__global__ __launch_bounds__(256 * G) void kmb_assign16(KmBatch B, const KmAsgItem *items, const uint4 *__restrict__ Xp) {
+    __shared__ uint4 raw[G][KM_A16_CT * 5];
+    __shared__ uint4 ct[G][KM_A16_CT * (KM_PW / 4)];
+    const KmAsgItem it = items[blockIdx.x];
+    const int g = threadIdx.x >> 8, tid = threadIdx.x & 255;
+    const int per = (it.c1 - it.c0 + (int)gridDim.y * G - 1) / ((int)gridDim.y * G);
+    const int gc0 = it.c0 + ((int)blockIdx.y * G + g) * per, gc1 = min(it.c1, gc0 + per);
+    if (G == 1 && gc0 >= gc1) return;
     KmState s = bin_state(B, it.bin);
-    const long i = it.p0 + threadIdx.x;
-    const bool valid = i < it.p1;
+    const long i = it.p0 + tid;
+    const bool valid = i < it.p1 && gc0 < gc1;
     uint32_t x[KM_PW];
     if (valid) {
         const uint4 *src = Xp + ((long)B.boff[it.bin] + i) * (KM_PW / 4);
@@ -1038,22 +1041,22 @@ __global__ __launch_bounds__(256) void kmb_assign16(KmBatch B, const KmAsgItem *
         }
     }
     unsigned best = ~0u;
-    for (int t0 = it.c0; t0 < it.c1; t0 += KM_A16_CT) {
-        const int cnt = min(KM_A16_CT, it.c1 - t0);
+    for (int t = 0; t < per; t += KM_A16_CT) {  // the same trip count in every group (barriers inside)
+        const int t0 = gc0 + t, cnt = max(0, min(KM_A16_CT, gc1 - t0));
         __syncthreads();
-        for (int e = threadIdx.x; e < cnt * 5; e += 256) raw[e] = reinterpret_cast<const uint4 *>(s.cent + (long)t0 * KM_A)[e];
+        for (int e = tid; e < cnt * 5; e += 256) raw[g][e] = reinterpret_cast<const uint4 *>(s.cent + (long)t0 * KM_A)[e];
         __syncthreads();
-        for (int e = threadIdx.x; e < cnt * KM_PW; e += 256)
-            reinterpret_cast<uint32_t *>(ct)[e] =
-                km_prep_word(reinterpret_cast<const uint32_t *>(raw + (e / KM_PW) * 5), e % KM_PW);
+        for (int e = tid; e < cnt * KM_PW; e += 256)
+            reinterpret_cast<uint32_t *>(ct[g])[e] =
+                km_prep_word(reinterpret_cast<const uint32_t *>(raw[g] + (e / KM_PW) * 5), e % KM_PW);
         __syncthreads();
-        if (valid) {
-            const unsigned kb = 8191u - (unsigned)(t0 - it.c0);
+        if (valid && !PF) {
+            const unsigned kb = 8191u - (unsigned)t;
             for (int c = 0; c < cnt; c++) {
                 uint32_t r[KM_PW];
 #pragma unroll
                 for (int q = 0; q < KM_PW / 4; q++) {
-                    const uint4 v = ct[c * (KM_PW / 4) + q];
+                    const uint4 v = ct[g][c * (KM_PW / 4) + q];
                     r[4 * q] = v.x;
                     r[4 * q + 1] = v.y;
                     r[4 * q + 2] = v.z;
@@ -1061,10 +1064,29 @@ __global__ __launch_bounds__(256) void kmb_assign16(KmBatch B, const KmAsgItem *
                 }
                 best = min(best, (km_dissim16(r, x) << 13) | (kb - (unsigned)c));
             }
+        } else if (valid && cnt > 0) {  // PF: the next centroid's row read from LDS while this one is compared
+            const unsigned kb = 8191u - (unsigned)t;
+            uint4 nx[KM_PW / 4];
+#pragma unroll
+            for (int q = 0; q < KM_PW / 4; q++) nx[q] = ct[g][q];
+            for (int c = 0; c < cnt; c++) {
+                uint32_t r[KM_PW];
+#pragma unroll
+                for (int q = 0; q < KM_PW / 4; q++) {
+                    r[4 * q] = nx[q].x;
+                    r[4 * q + 1] = nx[q].y;
+                    r[4 * q + 2] = nx[q].z;
+                    r[4 * q + 3] = nx[q].w;
+                }
+                const int cn = c + 1 < cnt ? c + 1 : c;
+#pragma unroll
+                for (int q = 0; q < KM_PW / 4; q++) nx[q] = ct[g][cn * (KM_PW / 4) + q];
+                best = min(best, (km_dissim16(r, x) << 13) | (kb - (unsigned)c));
+            }
         }
     }
     if (valid) {
-        const unsigned c = (unsigned)it.c0 + 8191u - (best & 8191u);
+        const unsigned c = (unsigned)gc0 + 8191u - (best & 8191u);
         atomicMin(&s.akey[i], ((unsigned long long)(best >> 13) << 32) | (0xFFFFFFFFu - c));
     }
 }
@@ -1121,6 +1143,7 @@ __global__ __launch_bounds__(256) void kmb_init_modes2(KmBatch B, const int32_t 
 // each host work item (<= 64 centroids) runs as KM_ASUB workgroups of a quarter of its centroids: the late
 // chunk steps hold one large bin alone, where one workgroup per item left ~1 wave per SIMD (latency-bound)
 static constexpr int KM_ASUB = 4;
+static constexpr int KM_A16_G = 1;  // 256-thread groups per kmb_assign16 workgroup
 
 // one 960-point chunk of each listed bin, applied in order (KModesIter kmodes.pas:869-911)
 struct KmSeqItem {
@@ -1557,7 +1580,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
             if (upload(as.data(), as.size() * sizeof(KmAsgItem))) goto fail;
             KTimer tm("kmodes_assign", st);
             if (use16)
-                hipLaunchKernelGGL(kmb_assign16, dim3((unsigned)as.size(), KM_ASUB), dim3(256), 0, st, B,
+                hipLaunchKernelGGL(kmb_assign16<KM_A16_G>, dim3((unsigned)as.size(), KM_ASUB / KM_A16_G), dim3(256 * KM_A16_G), 0, st, B,
                                    (const KmAsgItem *)items, (const uint4 *)(buf + o_Xp));
             else
                 hipLaunchKernelGGL(kmb_assign, dim3((unsigned)as.size(), KM_ASUB), dim3(256), 0, st, B, (const KmAsgItem *)items);
@@ -1622,8 +1645,27 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     for (const auto &sp : steps) {
                         {
                             KTimer tm("kmodes_assign", st);
+#ifdef TILER_EXPERIMENTS
+                            static const int asub = getenv("TILER_KM_ASUB") ? atoi(getenv("TILER_KM_ASUB")) : KM_ASUB;
+                            static const int a16g = getenv("TILER_KM_A16G") ? atoi(getenv("TILER_KM_A16G")) : KM_A16_G;
+                            static const bool a16pf = getenv("TILER_KM_A16PF") && atoi(getenv("TILER_KM_A16PF")) == 1;
+                            if (use16 && a16pf)  // A/B: LDS row of the next centroid prefetched
+                                hipLaunchKernelGGL((kmb_assign16<1, true>), dim3(sp.first, asub), dim3(256), 0, st, B,
+                                                   (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
+                            else if (use16 && (asub != KM_ASUB || a16g != KM_A16_G)) {  // A/B: slices per item, groups per workgroup
+                                if (a16g == 2)
+                                    hipLaunchKernelGGL(kmb_assign16<2>, dim3(sp.first, asub / 2), dim3(512), 0, st, B,
+                                                       (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
+                                else if (a16g == 4)
+                                    hipLaunchKernelGGL(kmb_assign16<4>, dim3(sp.first, asub / 4), dim3(1024), 0, st, B,
+                                                       (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
+                                else
+                                    hipLaunchKernelGGL(kmb_assign16<1>, dim3(sp.first, asub), dim3(256), 0, st, B,
+                                                       (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
+                            } else
+#endif
                             if (use16)
-                                hipLaunchKernelGGL(kmb_assign16, dim3(sp.first, KM_ASUB), dim3(256), 0, st, B,
+                                hipLaunchKernelGGL(kmb_assign16<KM_A16_G>, dim3(sp.first, KM_ASUB / KM_A16_G), dim3(256 * KM_A16_G), 0, st, B,
                                                    (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
                             else
                                 hipLaunchKernelGGL(kmb_assign, dim3(sp.first, KM_ASUB), dim3(256), 0, st, B,

@@ -1012,10 +1012,12 @@ __global__ __launch_bounds__(256) void kmb_prep_points(const uint8_t *X, long N,
 
 // kmb_assign with km_dissim16; inside a workgroup the argmin runs on 32-bit keys (dis << 13 | 8191 - local index:
 // dis < 2^18, at most 8,192 centroids per workgroup -- host-checked), merged into the u64 key by atomicMin as before.
-// G groups of 256 threads per workgroup, each one point per thread over its own slice of the item's centroids (the
-// item split over gridDim.y * G slices): the late chunk steps (960 points x 5,035 centroids, 1,264 slices) cost
-// ~6 ns per dispatched workgroup beyond their work (r03zl: 4 -> 16 slices per item +143 ms), so fewer, larger
-// workgroups.  r03zk: P points per thread instead (fewer waves, same LDS-broadcast reads per pair) was slower.
+// G groups of 256 threads per workgroup (each one point per thread over its own slice of the item's centroids, the
+// item split over gridDim.y * G slices) and PF (the next centroid's LDS row read while this one is compared) are
+// experiment-build A/B forms only.  C4 assignment time (r03zk-zn, 6,423 launches): 4 slices of 256 threads 142 ms;
+// 1 / 2 / 8 / 16 slices 176 / 152 / 184 / 289 ms; 2 or 4 groups per workgroup 163 / 223 ms; PF 147 ms; 2 or 4 points
+// per thread (fewer waves, half / a quarter of the broadcast LDS reads per pair) 162 / 200 ms.  Neither fewer point
+// re-reads nor fewer LDS reads per pair pays: the late steps (960 points x 5,035 centroids) are latency-bound waves.
 template <int G, bool PF = false>
 __global__ __launch_bounds__(256 * G) void kmb_assign16(KmBatch B, const KmAsgItem *items, const uint4 *__restrict__ Xp) {
     __shared__ uint4 raw[G][KM_A16_CT * 5];

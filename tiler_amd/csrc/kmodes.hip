@@ -1339,13 +1339,81 @@ __global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist(KmBatch B, const KmFf
     }
 }
 
+// Farthest-first with the selection after the barrier (round 3, r03zo): every item of round j stores its candidate
+// (sc1) into the round's parity half of the part slots and arrives; after the barrier EVERY item of a bin reduces
+// that bin's candidates itself (the same partition-independent maximum, so the same centre) instead of the last item
+// to finish selecting and publishing it.  Gone per round: the ffdone count, the selector's candidate loads, the
+// centre's sc1 publication and its load -- three dependent device-scope round trips of the ~11 on a round's
+// critical path.  The slots alternate halves by round parity: round j + 1's stores cannot reach a half that a slow
+// workgroup still reads for round j (it has not arrived at barrier j + 1 yet).  The used flag of a point is written
+// and read only by the thread that scans it (item u always on workgroup u % G, point i on lane i % KM_FF_NT), centres
+// and their rows for the later kernels by the bin's sub-0 item (plain stores: nothing in this launch reads them).
+__global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist2(KmBatch B, const KmFfItem *items, const int *ff_end,
+                                                            int Kmax, unsigned *bar, unsigned *fail) {
+    __shared__ unsigned long long red[KM_FF_NT / 64];
+    int alive = B.nb;
+    const long half = B.poff[B.nb];
+    for (int j = 0; j < Kmax; j++) {
+        while (alive > 0 && B.koff[alive] - B.koff[alive - 1] <= j) alive--;
+        const int nit = ff_end[alive];
+        for (int u = blockIdx.x; u < nit; u += gridDim.x) {
+            const KmFfItem it = items[u];
+            KmState s = bin_state(B, it.bin);
+            int c;
+            if (j == 0) {
+                c = s.center[0];  // kmb_ff_start (an earlier launch)
+            } else {
+                const unsigned long long *pp = s.part + ((j - 1) & 1) * half;
+                unsigned long long bb = 0;
+                for (int i = threadIdx.x; i < it.nsub; i += KM_FF_NT)
+                    bb = max(bb, __hip_atomic_load(&pp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                const unsigned long long w = km_block_max(bb, red);
+                c = (w == 0) ? -1 : (int)(w & 0xFFFFFFFFull) - 1;
+                if (c < 0) {
+                    if (it.sub == 0 && threadIdx.x == 0) *s.err = 1;
+                    c = 0;  // the call fails (host checks err); keep the rounds well-defined
+                } else {
+                    if (it.sub == 0) {
+                        if (threadIdx.x < KM_A) s.cent[(long)j * KM_A + threadIdx.x] = s.X[(long)c * KM_A + threadIdx.x];
+                        if (threadIdx.x == 0) s.center[j] = c;
+                    }
+                    if ((c / KM_FF_NT) % it.nsub == it.sub && c % KM_FF_NT == (int)threadIdx.x) s.used[c] = 1;
+                }
+            }
+            uint32_t item[20];
+            load_row(s.X + (long)c * KM_A, item);
+            unsigned long long bv = 0;
+            int bi = -1;
+            for (long i = (long)it.sub * KM_FF_NT + threadIdx.x; i < s.n; i += (long)it.nsub * KM_FF_NT) {
+                uint32_t row[20];
+                load_row(s.X + i * KM_A, row);
+                const unsigned long long d = km_dissim(row, item);
+                unsigned long long m = s.mind[i];
+                if (d < m) {  // cmovb: strict-less (kmodes.pas:555-558)
+                    m = d;
+                    s.mind[i] = m;
+                }
+                if (!s.used[i] && m >= bv) {  // ascending i within a thread: '>=' keeps the last
+                    bv = m;
+                    bi = (int)i;
+                }
+            }
+            const unsigned long long v32 = bv > 0xFFFFFFFFull ? 0xFFFFFFFFull : bv;
+            const unsigned long long best = km_block_max(bi < 0 ? 0ull : ((v32 << 32) | (unsigned)(bi + 1)), red);
+            if (j + 1 >= s.K) continue;  // the bin's last round: no selection (uniform)
+            if (threadIdx.x == 0) __hip_atomic_store(s.part + (j & 1) * half + it.sub, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (j + 1 < Kmax && !km_grid_sync(bar, (unsigned)(j + 1), fail)) return;
+    }
+}
+
 // resident workgroups for kmb_ff_persist: one per CU (0: not placeable -> per-launch rounds)
 static int ff_persist_grid() {
     static const int g = [] {
         int dev = 0, ncu = 0, per = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)kmb_ff_persist, KM_FF_NT, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)kmb_ff_persist2, KM_FF_NT, 0) != hipSuccess ||
             per <= 0 || ncu <= 0)
             return 0;
         return ncu;
@@ -1424,7 +1492,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                  o_poff = carve((nb + 1) * 4), o_start = carve(nb * 4), o_memb = carve((size_t)N * 4),
                  o_cent = carve((size_t)Ktot * KM_A), o_freq = carve((size_t)Ktot * KM_A * M * 4),
                  o_csize = carve((size_t)Ktot * 4), o_mind = carve((size_t)N * 8), o_used = carve(N),
-                 o_part = carve((size_t)poff[nb] * 8), o_center = carve((size_t)Ktot * 4), o_akey = carve((size_t)N * 8),
+                 o_part = carve((size_t)poff[nb] * 16), o_center = carve((size_t)Ktot * 4), o_akey = carve((size_t)N * 8),
                  o_seed = carve(nb * 4), o_cost = carve(nb * 8), o_moves = carve(nb * 4), o_err = carve(nb * 4),
                  o_ffd = carve(nb * 4), o_rand = carve((size_t)Ktot * KM_A * 4), o_bar = carve(2304),
                  o_bad = carve(4), o_mvl = carve((size_t)nb * 2 * KM_BIN * 16), o_mvn = carve((size_t)nb * 4);
@@ -1445,8 +1513,8 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     }
     const size_t item_bytes = (max_items + (size_t)poff[nb] + 64) * sizeof(KmAsgItem) +
                               (size_t)(nb + 1) * 4 + 256;
-    // farthest-first: one persistent launch for every round (kmb_ff_persist) unless it cannot be placed;
-    // TILER_KM_FF=0 (experiment build) selects the per-launch rounds for A/B
+    // farthest-first: one persistent launch for every round (kmb_ff_persist2) unless it cannot be placed;
+    // TILER_KM_FF=0 (experiment build) selects the per-launch rounds for A/B, TILER_KM_FF=1 the r03k persistent form
 #ifdef TILER_EXPERIMENTS
     static const bool ff_launches = getenv("TILER_KM_FF") && atoi(getenv("TILER_KM_FF")) == 0;
 #else
@@ -1548,7 +1616,15 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                 if (hipMemsetAsync(bar, 0, 2304, st) != hipSuccess) goto fail;  // counters, generations, fail word
                 {
                     KTimer tm("kmodes_init", st);
-                    hipLaunchKernelGGL(kmb_ff_persist, dim3(g_ff), dim3(KM_FF_NT), 0, st, B, (const KmFfItem *)items,
+#ifdef TILER_EXPERIMENTS
+                    static const bool ff1 = getenv("TILER_KM_FF") && atoi(getenv("TILER_KM_FF")) == 1;
+                    if (ff1)  // A/B: the last item of a bin selects and publishes the centre (r03k-r03zn)
+                        hipLaunchKernelGGL(kmb_ff_persist, dim3(g_ff), dim3(KM_FF_NT), 0, st, B, (const KmFfItem *)items,
+                                           (const int *)(items + fb), Kv[0], bar, ffail);
+                    else
+#endif
+                    // every item selects the centre after the barrier (r03zo: C4 122 -> 102 ms)
+                    hipLaunchKernelGGL(kmb_ff_persist2, dim3(g_ff), dim3(KM_FF_NT), 0, st, B, (const KmFfItem *)items,
                                        (const int *)(items + fb), Kv[0], bar, ffail);
                 }
                 unsigned hf = 1;

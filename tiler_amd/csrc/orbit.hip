@@ -1437,71 +1437,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
 // query; each lane sums its candidate in the reference order (sequential fp32, every op rounded), the
 // query's lanes pick (distance, index) lexicographically and the first writes the tilemap item.  Running
 // these 192-step chains here instead of one lane per candidate inside the half-wave rescore keeps the
-// rescore's instruction stream short (it is latency-bound) and fills the lanes.
-// STAGED (r03zr A/B): the workgroup's 64 query rows and up to 256 candidate rows pass through LDS in 32-float
-// column chunks, loaded coalesced (a row chunk is 128 contiguous bytes: 8 lanes), each lane then sums its chunk from
-// LDS in the same sequential order -- instead of every lane walking two 768-byte rows of its own (64 distinct lines
-// per load instruction).
-static constexpr int ORB_PCH = 32;  // floats per staged column chunk
-template <bool STAGED>
+// rescore's instruction stream short (it is latency-bound) and fills the lanes.  r03zr: staging the rows through LDS in
+// coalesced 32-float column chunks (12 barriers, every slot's row loaded) took 1.00 ms vs 0.50 ms for this per-lane walk.
 __global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a) {
     const long gid = (long)blockIdx.x * 256 + threadIdx.x;
     const long q = gid / ORB_PSLOTS;
     const int s = (int)(gid % ORB_PSLOTS);
     float bd = INFINITY;
-    if (STAGED) {
-        __shared__ float qs[256 / ORB_PSLOTS][ORB_PCH + 1];
-        __shared__ float cs[256][ORB_PCH + 1];
-        __shared__ int cidx[256];
-        const long q0 = (long)blockIdx.x * (256 / ORB_PSLOTS);
-        const int n0 = q < a.nq ? a.pair_cnt[q] : 0;
-        const bool act = s < n0;
-        const int c0 = act ? a.pair_cand[q * ORB_PSLOTS + s] : -1;
-        cidx[threadIdx.x] = c0;
-        if (__syncthreads_or(act)) {
-            float dist = 0.0f;
-            for (int k = 0; k < OD; k += ORB_PCH) {
-                for (int e = threadIdx.x; e < (256 / ORB_PSLOTS) * (ORB_PCH / 4); e += 256) {  // query chunks
-                    const int r = e / (ORB_PCH / 4), v = e % (ORB_PCH / 4);
-                    if (q0 + r < a.nq) {
-                        const float4 x = reinterpret_cast<const float4 *>(a.q + (q0 + r) * OD + k)[v];
-                        qs[r][4 * v] = x.x;
-                        qs[r][4 * v + 1] = x.y;
-                        qs[r][4 * v + 2] = x.z;
-                        qs[r][4 * v + 3] = x.w;
-                    }
-                }
-                for (int e = threadIdx.x; e < 256 * (ORB_PCH / 4); e += 256) {  // candidate chunks
-                    const int r = e / (ORB_PCH / 4), v = e % (ORB_PCH / 4), c = cidx[r];
-                    if (c >= 0) {
-                        const float4 y = reinterpret_cast<const float4 *>(a.rows + (long)c * OD + k)[v];
-                        cs[r][4 * v] = y.x;
-                        cs[r][4 * v + 1] = y.y;
-                        cs[r][4 * v + 2] = y.z;
-                        cs[r][4 * v + 3] = y.w;
-                    }
-                }
-                __syncthreads();
-                if (act) {
-                    const float *xr = qs[threadIdx.x / ORB_PSLOTS], *yr = cs[threadIdx.x];
-#pragma unroll
-                    for (int d = 0; d < ORB_PCH; d++) {
-                        const float t = xr[d] - yr[d];
-                        dist = dist + t * t;
-                    }
-                }
-                __syncthreads();
-            }
-            if (act) bd = dist;  // a slot without a candidate keeps INFINITY (never the group's minimum)
-        }
-    }
     if (q >= a.nq) return;  // whole groups: 256 % ORB_PSLOTS == 0
     const int n = a.pair_cnt[q];
     if (n == 0) return;  // uniform over the group
     int bi = 0x7fffffff, bg = -1;
     if (s < n) {
         int c = a.pair_cand[q * ORB_PSLOTS + s];
-        if (!STAGED) bd = exact_dist192_lean(a.q + q * OD, a.rows + (long)c * OD);
+        bd = exact_dist192_lean(a.q + q * OD, a.rows + (long)c * OD);
         if (a.grp_of) {
             bg = a.grp_of[c];
             class_first(a, a.q + q * OD, c, bg);  // same row, same distance
@@ -2657,13 +2606,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         static_assert(256 % ORB_PSLOTS == 0, "pair groups must not straddle blocks");
         KTimer tm("nn_pairs", stream);
         const long lanes = (long)nq * ORB_PSLOTS;
-#ifdef TILER_EXPERIMENTS
-        static const bool staged = getenv("TILER_PAIRS_LDS") && atoi(getenv("TILER_PAIRS_LDS")) == 1;
-        if (staged)  // A/B: rows staged through LDS in column chunks
-            hipLaunchKernelGGL(nn_orbit_pairs_kernel<true>, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, ra);
-        else
-#endif
-        hipLaunchKernelGGL(nn_orbit_pairs_kernel<false>, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, ra);
+        hipLaunchKernelGGL(nn_orbit_pairs_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, ra);
     }
     TILER_HIP_CHECK(hipGetLastError());
     if (want_stats) {

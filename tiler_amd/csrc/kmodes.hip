@@ -595,8 +595,8 @@ __device__ void bin_seq_body(KmState s, int p0, int p1) {
                     g_tab[h2] = 64;
                 }
                 const unsigned long long stopm = __ballot(mv && (c_sz[k < KM_SEQ_G ? k : 0] <= 1 || clash));
-                const unsigned long long invm = __ballot(!valid);  // lanes >= KM_SEQ_G are invalid: never empty
-                const int first_inv = __builtin_ctzll(invm);
+                const unsigned long long invm = __ballot(!valid);  // lanes >= KM_SEQ_G are invalid (none when KM_SEQ_G = 64)
+                const int first_inv = invm ? __builtin_ctzll(invm) : 64;  // a full 64-candidate window: none invalid
                 const int first_stop = stopm ? __builtin_ctzll(stopm) : 64;
                 const int end = min(first_stop, first_inv);
                 const unsigned long long below_end = end >= 64 ? ~0ull : ((1ull << end) - 1ull);
@@ -1761,6 +1761,9 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                                                    st, B, (const KmAsgItem *)items + pos);
                             else if (oldseq)  // A/B: decided and applied by one workgroup per bin
                                 hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, KM_SEQ_W>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
+                                                   st, B, (const KmAsgItem *)items + pos);
+                            else if (getenv("TILER_KM_DW") && atoi(getenv("TILER_KM_DW")) == 8)  // A/B: 64-candidate window
+                                hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, 8, true>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
                                                    st, B, (const KmAsgItem *)items + pos);
                             else
 #endif

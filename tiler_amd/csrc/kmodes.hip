@@ -1206,8 +1206,7 @@ __global__ __launch_bounds__(32 * (KM_A / NSLICE)) void kmb_seq_apply(KmBatch B,
     __syncthreads();
     const int G = ngr, j = tid / W, l = tid - j * W, a0 = blockIdx.y * W + l;
     for (int g = 0; g < G; g++) {
-        const int m = gs[g] + j;
-        if (m < gs[g + 1]) {
+        for (int m = gs[g] + j; m < gs[g + 1]; m += NT / W) {  // a group's moves are cluster-disjoint: any batching
             const int4 mv = s.mvl[m];
             apply_point_attrs<W, 1>(s, mv.x, mv.y, mv.z, a0);
         }

@@ -1761,6 +1761,9 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                             else if (oldseq)  // A/B: decided and applied by one workgroup per bin
                                 hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, KM_SEQ_W>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
                                                    st, B, (const KmAsgItem *)items + pos);
+                            else if (getenv("TILER_KM_DNT") && atoi(getenv("TILER_KM_DNT")) == 1024)  // A/B: 16 waves, 51-candidate window
+                                hipLaunchKernelGGL((kmb_seq_strided<1024, 20, true>), dim3(sp.second), dim3(1024), 0,
+                                                   st, B, (const KmAsgItem *)items + pos);
                             else if (getenv("TILER_KM_DNT") && atoi(getenv("TILER_KM_DNT")) == 256)  // A/B: 4 waves, same window
                                 hipLaunchKernelGGL((kmb_seq_strided<256, 8, true>), dim3(sp.second), dim3(256), 0,
                                                    st, B, (const KmAsgItem *)items + pos);

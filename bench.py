@@ -54,6 +54,9 @@ def main():
     ap.add_argument("--no-dither", action="store_true")
     ap.add_argument("--no-globaltiling", action="store_true", help="skip the C4 K-Modes secondary line")
     ap.add_argument("--no-palettes", action="store_true", help="skip the palette-generation secondary line")
+    ap.add_argument("--no-encoder", action="store_true", help="skip the sustained 1000-frame encoder lines")
+    ap.add_argument("--no-per-call", action="store_true", help="skip the per-tile ann_kdtree_search line")
+    ap.add_argument("--per-call-queries", type=int, default=8192)
     ap.add_argument("--palette-frames", type=int, default=8, help="frames of the palette-generation line")
     ap.add_argument("--clip-frames", type=int, default=1000, help="keyframe-detection clip length (C3: 1000)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -446,6 +449,32 @@ def main():
         ga.cpu_seconds = min(10.0, args.cpu_seconds)
         gtl = bench_globaltiling.run(ga)
 
+    # ---- secondary: the reference's unmodified per-tile call pattern (main.pas:4027 from every ProcThreadPool worker,
+    # main.pas:972) on this keyframe's ONE handle: ann_kdtree_search per query, one thread (latency) and 16 threads
+    # (the library coalesces concurrent callers into batches); every answer checked against the batched search ----
+    per_call = None
+    if rank == 0 and world == 1 and not args.no_per_call:
+        per_call = per_call_line(lib, kdt, frames, args.per_call_queries)
+
+    # ---- secondary: the encoder's whole FrameTiling pass over the 1000-frame C3 clip with REAL PrepareFrameTiling
+    # candidate sets (bench_encoder.py: PrepareGlobalFT, per keyframe Prepare at Medium quality + FrameTiling + Smooth),
+    # items shot-local (16k tiles per keyframe) and from the whole tileset ----
+    enc_local = enc_all = None
+    if rank == 0 and world == 1 and not args.no_encoder and args.config == "c3":
+        import bench_encoder
+        for name, item_tiles in (("local", 16384), ("all", 0)):
+            ea = bench_encoder.parser().parse_args(["--item-tiles", str(item_tiles)])
+            ea.check_kf = -1 if args.no_cpu else 1
+            r = bench_encoder.run(ea)
+            print(f"[bench] encoder_{name}: {r['value']} Mtiles/s, parity {r.get('parity')}", file=sys.stderr,
+                  flush=True)
+            r.pop("diag", None)
+            if name == "local":
+                enc_local = r
+            else:
+                enc_all = r
+            torch.cuda.empty_cache()
+
     # ---- CPU baseline (rank 0, N=1): the oracle restatement, bounded sample, same workload ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -462,12 +491,66 @@ def main():
                        "parallelism": f"keyframes sharded, {world} GPU(s)"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "search_stats": stats, "out_digest": out_digest,
             "secondary": {"prepare": prep, "smooth": smooth, "keyframes": keyframes, "dither": dither,
-                          "palettes": palettes_line, "globaltiling": gtl},
+                          "palettes": palettes_line, "globaltiling": gtl, "per_tile_calls": per_call,
+                          "encoder_local": enc_local, "encoder_all": enc_all},
         }
         print(json.dumps(res))
     kdt.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def per_call_line(lib, kdt, frames, nq_conc: int) -> dict:
+    """ann_kdtree_search once per query, as DoFrameTiling calls it (main.pas:4023-4027), on the keyframe's handle:
+    latency of lone calls, then calls/s with 16 threads calling concurrently on the same handle.  The queries are
+    the keyframe's frame tiles' descriptors (fp32, made on the GPU); every answer must equal the batched search's."""
+    import ctypes
+    import threading
+    from tiler_amd.psyv import psyv_batch
+    nq = min(nq_conc, frames.reshape(-1, 64).shape[0])
+    _, qd = psyv_batch(rgb=frames.reshape(-1, 64)[:nq], flags=2, want64=False, want32=True)
+    bi, be = kdt.search_batch(qd)
+    ref_i, ref_e = bi.astype(np.int64), be
+    err = np.zeros(1, np.float32)
+    vp = ctypes.c_void_p
+    lat = []
+    one = np.zeros(nq, np.int64)
+    for i in range(64):  # lone calls: the full per-call path (H2D, search chain, D2H, sync)
+        q = np.ascontiguousarray(qd[i])
+        t0 = time.perf_counter()
+        one[i] = lib.ann_kdtree_search(kdt.handle, q.ctypes.data_as(vp), 0.0, err.ctypes.data_as(vp))
+        lat.append(time.perf_counter() - t0)
+    threads = 16
+    got = np.full(nq, -2, np.int64)
+    gerr = np.zeros(nq, np.float32)
+    c0 = kdt.combine_stats()
+
+    def worker(t):
+        e = np.zeros(1, np.float32)
+        for i in range(t, nq, threads):
+            got[i] = lib.ann_kdtree_search(kdt.handle, qd[i].ctypes.data_as(vp), 0.0, e.ctypes.data_as(vp))
+            gerr[i] = e[0]
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    tc = time.perf_counter() - t0
+    c1 = kdt.combine_stats()
+    batches = c1["batches"] - c0["batches"]
+    mism = int(np.count_nonzero(got != ref_i) + np.count_nonzero(gerr.view(np.uint32) != ref_e.view(np.uint32)) +
+               np.count_nonzero(one[:64] != ref_i[:64]))
+    lat_ms = np.array(lat) * 1e3
+    return {"value": round(nq / tc, 1), "unit": "calls/s (16 threads, one handle)", "queries": nq,
+            "threads": threads, "latency_ms": {"median": round(float(np.median(lat_ms)), 3),
+                                               "p90": round(float(np.percentile(lat_ms, 90)), 3)},
+            "lone_calls_per_s": round(1e3 / float(np.median(lat_ms)), 1),
+            "batches": int(batches), "avg_batch": round(nq / max(1, batches), 2), "max_batch": c1["max_batch"],
+            "mismatches_vs_batched": mism,
+            "what": "ann_kdtree_search (extern.pas:65) per frame tile on the C3 keyframe handle; concurrent callers "
+                    "are coalesced into batches inside libANN.so (ann_api.hip Combiner)"}
 
 
 def pmc_traffic(kernel: str):

@@ -33,6 +33,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+PEAK_F16_TFLOPS = 2500.0   # MI355X dense fp16 MFMA (MI355X_MICROARCH.md; sparsity excluded)
+GENERIC_KERNEL = "nn_shortlist16_kernel<S=6,L=4,CB=8,NW=8,QB=4>"
+
 
 def frame_tiles_gpu(torch, g, n, dev):
     """synth.frame_tiles' mix on the GPU: [n, 64] int32 0x00BBGGRR."""
@@ -75,7 +78,7 @@ def keyframe_gpu(torch, g, F, Q, T, dev, change=0.3, subset=0):
     return fr, it
 
 
-def main():
+def parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--kf-len", type=int, default=24)
@@ -90,9 +93,14 @@ def main():
     ap.add_argument("--no-smooth", action="store_true")
     ap.add_argument("--check-kf", type=int, default=1, help="keyframe re-checked against the restatement (-1: none)")
     ap.add_argument("--check-queries", type=int, default=1500)
+    ap.add_argument("--check-items", type=int, default=1000, help="items whose k = 8 search is re-checked")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, visible cores)")
     ap.add_argument("--seed", type=int, default=20261017)
-    args = ap.parse_args()
+    return ap
 
+
+def run(args) -> dict:
+    """The sustained clip; also bench.py's `secondary.encoder_*` lines."""
     import torch
 
     import tiler_amd
@@ -101,8 +109,9 @@ def main():
     from tiler_amd._lib import check
 
     lib = tiler_amd.load()
-    check(lib.tiler_init(0), "tiler_init")
-    dev = torch.device("cuda", 0)
+    devi = torch.cuda.current_device() if torch.cuda.is_initialized() else 0
+    check(lib.tiler_init(devi), "tiler_init")
+    dev = torch.device("cuda", devi)
     vp = ctypes.c_void_p
     W, H, T, P = args.width, args.height, args.tileset, args.palettes
     Q = (W // 8) * (H // 8)
@@ -179,7 +188,9 @@ def main():
         if k == args.check_kf or (k == 0 and args.check_kf < 0):
             stats_kf.update(kt.stats())
 
-    def run_clip():
+    kept = {}
+
+    def run_clip(keep=False):
         times["prepare"].clear()
         times["ft_smooth"].clear()
         info_all.clear()
@@ -191,7 +202,10 @@ def main():
             for k in range(nkf):
                 kt = prepare(k, gds, s_prep)
                 ft_smooth(k, kt)
-                kt.close()
+                if k == args.check_kf and keep:
+                    kept["kt"] = kt
+                else:
+                    kt.close()
         else:
             box = {}
             worker = threading.Thread(target=lambda: box.__setitem__(0, prepare(0, gds, s_prep)))
@@ -200,14 +214,17 @@ def main():
             for k in range(nkf):
                 worker.join()
                 kt = box.pop(k)
-                if prev is not None:
+                if prev is not None and prev is not kept.get("kt"):
                     prev.close()  # keyframe k-1 is finished and nothing else is in flight: its frees cost nothing
                 if k + 1 < nkf:
                     worker = threading.Thread(target=lambda k1=k + 1: box.__setitem__(k1, prepare(k1, gds, s_prep)))
                     worker.start()
                 ft_smooth(k, kt)
+                if k == args.check_kf and keep:
+                    kept["kt"] = kt  # the re-checked keyframe's candidate set is read back after the timed region
                 prev = kt
-            prev.close()
+            if prev is not kept.get("kt"):
+                prev.close()
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
         gds.kdt.close()
@@ -243,6 +260,7 @@ def main():
     lib.tiler_timing_enable(0)
     diag["ft_smooth_ms"] = round(1e3 * times["ft_smooth"][-1], 3)
     diag["ft_kernels"] = kernel_times()
+    diag["ft_search_stats"] = kt0.stats()
     kt0.close()
     gds0.kdt.close()
     times["prepare"].clear()
@@ -257,7 +275,7 @@ def main():
     run_clip()
     nkf = _nkf
     print("[bench_encoder] warm-up pass done", file=sys.stderr, flush=True)
-    wall, t_global = run_clip()
+    wall, t_global = run_clip(keep=True)
     print(f"[bench_encoder] clip: {wall:.3f} s", file=sys.stderr, flush=True)
     tiles_total = args.frames * Q
     value = tiles_total / wall / 1e6
@@ -278,6 +296,29 @@ def main():
                                   f"{args.item_tiles or T} tiles per keyframe"}}
 
     res["diag"] = diag
+    # roofline of the FrameTiling search kernel on keyframe 0 (diag, HIP events on its stream): the generic 16x16x32
+    # shortlist issues 2*M*D flops per query (M = the keyframe's candidates, D = 192; real candidate sets have no
+    # mirror-orbit structure); flat query tiles grouped last issue only k-step 0 (flat_queries)
+    fk = diag["ft_kernels"]
+    orbit_kf = bool(diag.get("ft_search_stats", {}).get("orbit_search"))
+    sl = fk.get("nn_orbit" if orbit_kf else "nn_shortlist")
+    q0 = (starts[1] - starts[0]) * Q
+    m0 = diag["candidates"]
+    if sl and not orbit_kf:
+        nflat = diag.get("ft_search_stats", {}).get("flat_queries", 0) or 0
+        s16 = 6
+        flops = 2.0 * (-(-m0 // 16) * 16) * 32 * (s16 * (q0 - nflat) + nflat)
+        ach = flops / (sl["ms"] * 1e-3) / 1e12
+        res["roofline"] = {"bound": "mfma", "kernel": GENERIC_KERNEL, "achieved": round(ach, 2), "peak": PEAK_F16_TFLOPS,
+                           "unit": "TFLOP/s", "frac": round(ach / PEAK_F16_TFLOPS, 4), "kernel_ms": sl["ms"],
+                           "flops_per_launch": flops, "queries": q0, "flat_queries": nflat, "candidates": m0,
+                           "bruteforce_flops": 2.0 * m0 * 192 * q0,
+                           "note": "issued MFMA flops (candidates padded to 16-row blocks; 6 k-steps of 32 per query, "
+                                   "1 for flat query tiles grouped last) / the kernel's HIP-event time on keyframe 0; "
+                                   "dense fp16 peak"}
+    elif sl:
+        res["roofline"] = {"bound": "mfma", "kernel": "nn_orbit_shortlist_pipe_kernel", "kernel_ms": sl["ms"],
+                           "note": "orbit path (candidate set with mirror orbits)"}
     import hashlib
     hsh = hashlib.blake2b(digest_size=8)
     for k in range(nkf):  # every keyframe's FrameTiling items + errors (equal digest = identical outputs)
@@ -288,40 +329,77 @@ def main():
                                                                 "items_avg", "candidates_avg", "out_digest")}), file=sys.stderr,
           flush=True)
 
-    # ---- re-check one keyframe against the CPU restatement (after the timed region) ----
+    # ---- re-check one keyframe against the CPU restatement (after the timed region), bounded ----
+    # The reference's Prepare (UseOne's k = 8 kd search of every item in 64-d, main.pas:3830) takes minutes on the
+    # host, so the chain is checked link by link: (1) the k = 8 search of a sample of the keyframe's items against the
+    # restated ANN search; (2) the device Prepare's candidate set (tiler_ft_get_maps on the keyframe's own handle from
+    # the timed run) against the host UseOne over the k = 8 results of ALL the keyframe's items (frame_tiling.mark_used,
+    # DoPsyV emission order) -- every used cell, in order; (3) a sample of its FrameTiling items against the restated
+    # ANN search over THAT candidate set (the CPU rate is timed here); (4) a column sample of its Smooth.
     ck = args.check_kf
-    stop_beat = threading.Event()
-
-    def heartbeat():  # the restatement's k = 8 kd searches run for minutes: keep the log moving
-        t0 = time.perf_counter()
-        while not stop_beat.wait(30):
-            print(f"[bench_encoder] check running ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
-
-    threading.Thread(target=heartbeat, daemon=True).start()
-    if 0 <= ck < nkf:
+    if 0 <= ck < nkf and "kt" in kept:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle as oracle
+        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         t0 = time.perf_counter()
-        it = items_t[ck].cpu().numpy().ravel()
-        ip = items_p[ck].cpu().numpy().ravel()
-        g_ds, g_tile, g_attr = oracle.prepare_global_ds(tiles)
-        corrs, highest = oracle.palette_corr(cents)
         say = lambda m: print(f"[bench_encoder] check: {m} ({time.perf_counter() - t0:.1f} s)", file=sys.stderr,
                               flush=True)  # noqa: E731
-        used = oracle.mark_used(g_ds, g_tile, g_attr, ip, it, tiles, P, args.quality, corrs, highest)
-        say("used table")
-        ods, ot, op, oa = oracle.build_ft_dataset(used, tiles, thm, tvm, pals)
-        say("dataset")
+        kt_ck = kept.pop("kt")
+        g_tile, g_pal, g_attr = kt_ck.maps()
+        kt_ck.close()
+        it = items_t[ck].cpu().numpy().ravel()
+        ip = items_p[ck].cpu().numpy().ravel()
+        chk = {"keyframe": ck, "candidates_gpu": int(g_tile.size)}
+        # (1) k = 8 searches of sampled distinct items, GPU (batched, same global handle kind) vs restated ANN
+        gdsc = ftm.prepare_global_ft(tiles)
+        keys = np.unique(ip.astype(np.int64) * T + it.astype(np.int64))
+        ks = np.random.default_rng(4).choice(keys, min(args.check_items, keys.size), replace=False)
+        qk = tiles[(ks % T)].astype(np.float32)
+        gi8, ge8 = gdsc.kdt.search_batch(qk, k=8)
+        o_ds, _, _ = oracle.prepare_global_ds(tiles)
+        okd = oracle.KDTree(o_ds)
+        oi8, oe8 = okd.search_batch(qk, threads=threads, k=8)
+        okd.close()
+        chk["knn8_items"] = int(ks.size)
+        chk["knn8_mismatches"] = int(np.count_nonzero(np.any((gi8 != oi8) | (ge8.view(np.uint32) !=
+                                                                          oe8.view(np.uint32)), axis=1)))
+        say("k = 8 sample")
+        # (2) the whole candidate set: host UseOne over the k = 8 results of every item vs the device Prepare
+        corrs, highest = ftm.palette_corr(cents)
+        used = ftm.mark_used(gdsc, tiles, ip, it, P, args.quality, corrs, highest)
+        gdsc.kdt.close()
+        hds = synth.ft_dataset_from_used(used, thm, tvm)
+        chk["candidates_host"] = int(hds.tile_of.size)
+        chk["candidate_set_equal"] = bool(np.array_equal(hds.tile_of, g_tile) and np.array_equal(hds.pal_of, g_pal)
+                                          and np.array_equal(hds.attrs, g_attr))
+        say("candidate set")
+        # (3) FrameTiling items vs the restated search over the device's candidate set
+        used_g = np.zeros((P, T, 4), np.uint8)
+        used_g[g_pal, g_tile, g_attr] = 1
+        ods, ot, op, oa = oracle.build_ft_dataset(used_g, tiles, thm, tvm, pals)
         fr = frames[ck].cpu().numpy().reshape(-1, 64)
         pick = np.random.default_rng(5).choice(fr.shape[0], min(args.check_queries, fr.shape[0]), replace=False)
-        o = oracle.frame_tiling(fr[pick], ods, ot, op, oa)
-        say("frame tiling")
+        t1 = time.perf_counter()
+        okd = oracle.KDTree(ods)
+        build_s = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        qd = oracle.psyv_batch(pick.size, rgb=fr[pick], flags=2).astype(np.float32)
+        ki, ke = okd.search_batch(qd, threads=threads)
+        cpu_s = time.perf_counter() - t1
+        okd.close()
         go = {nm: outs[ck][nm].cpu().numpy() for nm in ("tile", "pal", "hm", "vm", "err")}
-        mism = int(np.count_nonzero((go["tile"][pick] != o[0]) | (go["pal"][pick] != o[1]) |
-                                    (go["hm"][pick] != o[2]) | (go["vm"][pick] != o[3]) |
-                                    (go["err"][pick].view(np.uint32) != o[4].view(np.uint32))))
-        chk = {"keyframe": ck, "candidates_gpu": cand[ck], "candidates_oracle": int(used.sum()),
-               "ft_queries": int(pick.size), "ft_mismatches": mism}
+        mism = int(np.count_nonzero((go["tile"][pick] != ot[ki]) | (go["pal"][pick] != op[ki]) |
+                                    (go["hm"][pick] != (oa[ki] & 1)) | (go["vm"][pick] != (oa[ki] >> 1)) |
+                                    (go["err"][pick].view(np.uint32) != ke.view(np.uint32))))
+        chk["ft_queries"] = int(pick.size)
+        chk["ft_mismatches"] = mism
+        res["cpu_baseline"] = {"value": round(pick.size / cpu_s / 1e6, 6), "unit": "Mtiles/s", "cores": threads,
+                               "kind": "port",
+                               "sample": f"{pick.size} frame tiles of keyframe {ck} vs its {ods.shape[0]} candidates: "
+                                         f"fp64 descriptor + ANN 1.1.2 kd-tree search (oracle/ann_kdtree.c, ANN_KD_STD, "
+                                         f"bucket 1, eps 0), tree build {build_s:.1f} s untimed, {threads} threads; "
+                                         f"the per-keyframe Prepare and Smooth are not in this rate"}
+        say("frame tiling")
         if sm[ck] is not None:
             F = starts[ck + 1] - starts[ck]
             cols = np.sort(np.random.default_rng(6).choice(Q, min(2000, Q), replace=False))
@@ -332,10 +410,17 @@ def main():
             chk["smooth_positions"] = int(cols.size)
             chk["smooth_mismatches"] = int(sum(np.count_nonzero(a != b) for a, b in zip(gs, so)))
         chk["check_s"] = round(time.perf_counter() - t0, 2)
+        chk["mismatches_total"] = (chk["knn8_mismatches"] + chk["ft_mismatches"] + chk.get("smooth_mismatches", 0) +
+                                   (0 if chk["candidate_set_equal"] else 1))
         res["parity"] = chk
-    stop_beat.set()
-    print(json.dumps(res), flush=True)
+    for k in range(nkf):
+        sm[k] = None
+    outs.clear()
+    frames.clear()
+    items_t.clear()
+    items_p.clear()
+    return res
 
 
 if __name__ == "__main__":
-    main()
+    print(json.dumps(run(parser().parse_args())), flush=True)

@@ -26,7 +26,10 @@
  *     (extern.pas:66) and never calls it; its tie order is not reproduced;
  *   - the dataset rows are copied to device memory at create (ANN borrows pa until destroy);
  *   - no process abort: errors return -1 (or NULL) and tiler_last_error() explains;
- *   - every entry point is thread-safe; concurrent calls on one handle are serialised.
+ *   - every entry point is thread-safe.  Concurrent single-query calls on one handle (ann_kdtree_search /
+ *     _pri_search / _search_multi from many threads: the reference's ProcThreadPool pattern, main.pas:972, 4027,
+ *     3830) are coalesced: callers that arrive while a batch is in flight are searched together as the next batch,
+ *     each woken with its own answer (identical to a lone call's); other calls on one handle are serialised.
  * The search runs on the GPU only.  There is no CPU fallback: if the HIP runtime or a gfx950
  * device is missing every call fails with -1 / NULL.
  */
@@ -90,6 +93,8 @@ typedef struct {
                                  workgroup with non-flat ones are not counted.  0 for searches without flat grouping. */
 } tiler_search_stats;
 int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
+/* Coalescing counters of the single-query entry points on this handle: calls, batches searched, largest batch. */
+int tiler_combine_stats(ann_kdtree *akd, int64_t *calls, int64_t *batches, int32_t *max_batch);
 /* Leaf position of every dataset point in ANN's kd-tree (the order of its depth-first scan with every near
  * child LO): pos[n].  -1 when the handle was created with TILER_SPLIT_INDEX_ORDER. */
 int tiler_kdtree_positions(ann_kdtree *akd, int32_t *pos);
@@ -126,6 +131,8 @@ int tiler_psyv_batch_dev(int n, const int32_t *rgb, const uint8_t *palpix, const
  * Attach the keyframe dataset's row -> (tile, palette, attrs) maps (TTilingDataset.TRTo*, main.pas:181-189)
  * to a handle created over the keyframe's candidate descriptors. */
 int tiler_ft_set_maps(ann_kdtree *akd, const int32_t *tr_tile, const int32_t *tr_pal, const uint8_t *tr_attr);
+/* Read them back (host arrays of the handle's n rows), e.g. the candidate set tiler_prepare_frame_tiling_dev built. */
+int tiler_ft_get_maps(ann_kdtree *akd, int32_t *tr_tile, int32_t *tr_pal, uint8_t *tr_attr);
 /* For Q frame tiles (RGB): query descriptor (UseWavelets, gamma, no mirror) -> fp32 -> exact NN ->
  * tilemap item {GlobalTileIndex, PalIdx, HMirror = attr&1, VMirror = attr&2} + err. Host buffers. */
 int tiler_frame_tiling(ann_kdtree *akd, const int32_t *rgb, int Q, int use_wavelets, int gamma, int32_t *out_tile,
@@ -140,7 +147,9 @@ int tiler_frame_tiling(ann_kdtree *akd, const int32_t *rgb, int Q, int use_wavel
  * search handle over them with its TRTo maps set, ready for tiler_frame_tiling_dev.  The tileset d_palpix[n_tiles]
  * [64], d_thm / d_tvm[n_tiles] (TTile.HMirror / VMirror) and d_palettes[n_palettes][16] are in HBM; near is a host
  * array (Medium only).  Runs on stream (synchronising it twice: the distinct-item and candidate counts); info
- * (optional) returns those counts.  Calls sharing global_ds are serialised.  NULL on error. */
+ * (optional) returns those counts.  Calls sharing global_ds are serialised on the host and ordered on the device: a
+ * call on another stream waits (hipStreamWaitEvent) until the previous call's work that reads the shared scratch has
+ * run, so concurrent prepares on different streams are safe.  NULL on error. */
 typedef struct {
     int64_t items;      /* distinct (PalIdx, GlobalTileIndex) items searched */
     int64_t candidates; /* KNNSize: candidate descriptors of the keyframe's dataset */

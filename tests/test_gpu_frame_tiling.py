@@ -196,6 +196,41 @@ def test_frame_tiling_flat_tiles_last_matches_small_batches(gpu):
     kt.finish_frame_tiling()
 
 
+def test_frame_tiling_flat_tiles_last_generic_path(gpu, oracle):
+    """The same grouping on the generic 16x16x32 shortlist (candidate sets without mirror orbits: one orientation per
+    (palette, tile), as real PrepareFrameTiling output mostly is): both operands' fragments carry the three PsyV DC
+    dimensions in k-step 0 (dc_first_dim), so the flat workgroups contract k-step 0 only.  The >= 8192-tile batch
+    must equal per-frame batches (no grouping) and the oracle (restated ANN search) bit for bit."""
+    from tiler_amd.frame_tiling import KeyframeTiler
+    rng = np.random.default_rng(29)
+    P, T = 16, 6000
+    tiles, thm, tvm = synth.tileset(rng, T)
+    pals = synth.palettes(rng, P)
+    used = np.zeros((P, T, 4), np.uint8)
+    for _ in range(2):  # two (palette, orientation) cells per tile, never a whole mirror orbit
+        used[rng.integers(0, P, T), np.arange(T), rng.integers(0, 4, T)] = 1
+    ds = synth.ft_dataset_from_used(used, thm, tvm)
+    kt = KeyframeTiler(tiles, thm, tvm, pals, ds)
+    frames = synth.keyframe_frames(rng, 8, 1200)
+    flat = (frames.reshape(-1, 64) == frames.reshape(-1, 64)[:, :1]).all(axis=1)
+    assert frames.shape[0] * 1200 >= 8192 and 0 < flat.sum() < flat.size
+    big = kt.do_frame_tiling(frames.reshape(-1, 64))
+    st = kt.kdt.stats()
+    assert st["orbit_search"] == 0 and st["flat_queries"] > 0
+    for f in range(frames.shape[0]):
+        g = kt.do_frame_tiling(frames[f])
+        for a, b in zip(g[:4], big[:4]):
+            assert np.array_equal(a, b[f * 1200:(f + 1) * 1200])
+        assert np.array_equal(g[4].view(np.uint32), big[4][f * 1200:(f + 1) * 1200].view(np.uint32))
+    kt.finish_frame_tiling()
+    ods, ot, op, oa = oracle.build_ft_dataset(used, tiles, thm, tvm, pals)
+    pick = np.concatenate([np.nonzero(flat)[0][:300], np.nonzero(~flat)[0][:300]])
+    o = oracle.frame_tiling(frames.reshape(-1, 64)[pick], ods, ot, op, oa)
+    for a, b in zip(big[:4], o[:4]):
+        assert np.array_equal(a[pick], b)
+    assert np.array_equal(big[4][pick].view(np.uint32), o[4].view(np.uint32))
+
+
 def test_prepare_frame_tiling_used_table(gpu, oracle):
     """UseOne (k=8 preselection + distinct-err walk) for Fast / Medium / Slow, main.pas:3802-3853."""
     from tiler_amd import frame_tiling as ft

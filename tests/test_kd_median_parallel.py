@@ -66,8 +66,8 @@ def _parallel(key, idx, n_lo):
         c = key[l]
         p = np.arange(l, r + 1)
         v = key[l:r + 1]
-        isl = (p > l) & (v >= c)
-        isr = (p < r) & (v <= c)
+        isl = (p > l) & ~(v < c)   # where `while key[++i] < c` stops (NaN keys / a NaN pivot stop it too)
+        isr = (p < r) & ~(v > c)   # where `while key[--k] > c` stops
         tot_r = int(isr.sum())
         jl = np.cumsum(isl)                  # rank from the left (1-based) at left stoppers
         rb = np.cumsum(isr) - isr            # right stoppers below p
@@ -89,9 +89,37 @@ def _parallel(key, idx, n_lo):
             l = k + 1
         else:
             break
-    if n_lo > 0:
-        sw(n_lo - 1, int(np.argmax(key[:n_lo])))  # the first maximum
+    if n_lo > 0:  # the first maximum, NaN keys skipped; a NaN key[0] is never replaced (kd_median_big_kernel)
+        head = key[:n_lo]
+        ok = ~np.isnan(head)
+        m = 0 if (np.isnan(head[0]) or not ok.any()) else int(np.flatnonzero(ok)[np.argmax(head[ok])])
+        sw(n_lo - 1, m)
     return key, idx, np.float32((np.float64(np.float32(key[n_lo - 1] + key[n_lo]))) / 2.0)
+
+
+def _same(a, b):
+    return (np.array_equal(a[0], b[0], equal_nan=True) and np.array_equal(a[1], b[1]) and
+            (a[2] == b[2] or (np.isnan(a[2]) and np.isnan(b[2]))))
+
+
+def test_parallel_hoare_with_nan_and_inf_keys():
+    """Non-finite keys: NaN stops both scans in the sequential loop (its `<` / `>` tests fail), a NaN
+    pivot makes every position a stopper; the ranked form must make the same swaps and never index past the
+    stoppers it counted.  +-inf are ordinary ordered keys."""
+    rng = np.random.default_rng(7)
+    with np.errstate(invalid="ignore"):
+        for t in range(1500):
+            n = int(rng.integers(2, 300))
+            key = rng.integers(0, int(rng.integers(1, 9)), n).astype(np.float32)
+            frac = [0.02, 0.2, 0.6, 1.0][t % 4]
+            key[rng.random(n) < frac] = np.nan
+            if t % 5 == 0:
+                key[rng.random(n) < 0.1] = np.inf
+                key[rng.random(n) < 0.1] = -np.inf
+            if t % 7 == 0:
+                key[(n - 1) // 2] = np.nan  # the first pivot
+            idx = np.arange(n, dtype=np.int64)
+            assert _same(_sequential(key, idx, n // 2), _parallel(key, idx, n // 2)), (t, n)
 
 
 def test_parallel_hoare_ranking_equals_annmediansplit():

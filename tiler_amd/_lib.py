@@ -54,6 +54,7 @@ _SIGS = {
     "ann_kdtree_search_multi_batch": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p]),
     "ann_kdtree_search_batch_dev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "ann_kdtree_get_stats": (c_int, [c_void_p, P(SearchStats)]),
+    "tiler_combine_stats": (c_int, [c_void_p, P(ctypes.c_int64), P(ctypes.c_int64), P(ctypes.c_int32)]),
     "tiler_init": (c_int, [c_int]),
     "tiler_shutdown": (c_int, []),
     "tiler_last_error": (c_char_p, []),
@@ -66,6 +67,7 @@ _SIGS = {
     "tiler_psyv_batch_dev": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                      c_void_p, c_void_p, c_void_p]),
     "tiler_ft_set_maps": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "tiler_ft_get_maps": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "tiler_prepare_frame_tiling_dev": (c_void_p, [c_void_p, c_void_p, c_void_p, ctypes.c_int64, c_void_p, c_void_p,
                                                   c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
                                                   c_void_p, P(PrepareInfo)]),

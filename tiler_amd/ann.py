@@ -120,6 +120,21 @@ class KDTree:
                 "tie_order": s.tie_order, "kd_levels": s.kd_levels, "kd_build_ms": round(s.kd_build_ms, 3),
                 "kd_replayed": s.kd_replayed, "flat_queries": s.flat_queries}
 
+    def combine_stats(self) -> dict:
+        """Coalescing of concurrent single-query calls on this handle (tiler_combine_stats)."""
+        c, b, m = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
+        check(self._lib.tiler_combine_stats(self.handle, ctypes.byref(c), ctypes.byref(b), ctypes.byref(m)),
+              "tiler_combine_stats")
+        return {"calls": c.value, "batches": b.value, "max_batch": m.value}
+
+    def maps(self):
+        """The TRTo* maps of the handle (tiler_ft_get_maps): (tile_of, pal_of, attrs) per dataset row."""
+        t = np.zeros(max(self.n, 1), np.int32)
+        p = np.zeros(max(self.n, 1), np.int32)
+        a = np.zeros(max(self.n, 1), np.uint8)
+        check(self._lib.tiler_ft_get_maps(self.handle, _ptr(t), _ptr(p), _ptr(a)), "tiler_ft_get_maps")
+        return t[:self.n], p[:self.n], a[:self.n]
+
     def positions(self) -> np.ndarray:
         """Leaf position of every point in ANN's kd-tree (tiler_kdtree_positions)."""
         pos = np.zeros(self.n, np.int32)

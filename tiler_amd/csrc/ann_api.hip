@@ -8,6 +8,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -163,8 +165,37 @@ bool ensure_init() {
 
 using namespace tiler;
 
+// Concurrent single-query callers of one handle (the reference's pattern: ann_kdtree_search per tile from every
+// ProcThreadPool worker, main.pas:4027 / 972, and ann_kdtree_search_multi per item, main.pas:3830) are coalesced: a
+// caller queues its query; the first caller that finds no batch in flight becomes the leader, takes every queued query
+// of its k (callers that arrived while the previous batch ran), searches them as ONE batch and wakes each caller on its
+// own slot.  Batching never changes an answer (every query's result is exact and independent of the others).  The
+// leader stops once its own query is answered and hands the queue to a waiting caller.
+struct CombineReq {
+    const float *q = nullptr;
+    int k = 1;
+    int *idx = nullptr;
+    float *err = nullptr;
+    int rc = 0;
+    bool done = false;
+    std::string msg;
+};
+struct Combiner {
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<CombineReq *> pending;
+    bool busy = false;
+    // pinned staging of the batch in flight (only the leader touches them)
+    float *h_q = nullptr, *h_err = nullptr;
+    int *h_idx = nullptr;
+    size_t cap_q = 0, cap_r = 0;
+    long long batches = 0, calls = 0;  // counters (tiler_combine_stats)
+    int max_batch = 0;
+};
+
 struct ann_kdtree {
     NNIndex *ix = nullptr;
+    Combiner comb;
     hipStream_t stream = nullptr;
     float *d_q = nullptr;
     int *d_idx = nullptr;
@@ -328,6 +359,9 @@ void ann_kdtree_destroy(ann_kdtree *t) {
         prep_scratch_free(t->prep);
         delete t->prep;
     }
+    hipHostFree(t->comb.h_q);
+    hipHostFree(t->comb.h_idx);
+    hipHostFree(t->comb.h_err);
     if (t->stream) hipStreamDestroy(t->stream);
     delete t;
 }
@@ -404,10 +438,114 @@ int ann_kdtree_search_batch(ann_kdtree *t, const float *q, int nq, float eps, in
     return ann_kdtree_search_multi_batch(t, q, nq, 1, eps, idx, err);
 }
 
+static constexpr int COMBINE_MAX = 8192;  // queries per coalesced batch
+
+// one coalesced batch: pack the queries into pinned memory, one search, unpack (the leader, outside c.m)
+static int combine_run(ann_kdtree *t, std::vector<CombineReq *> &b, int k) {
+    Combiner &c = t->comb;
+    NNIndex *ix = t->ix;
+    const int nq = (int)b.size(), d = ix->d;
+    std::lock_guard<std::mutex> lk(ix->mu);
+    if (ix->n == 0) {
+        for (CombineReq *r : b)
+            for (int i = 0; i < k; i++) {
+                r->idx[i] = -1;
+                r->err[i] = FLT_MAX;
+            }
+        return 0;
+    }
+    if ((size_t)nq * d > c.cap_q) {
+        hipHostFree(c.h_q);
+        c.h_q = nullptr;
+        c.cap_q = 0;
+        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_q, (size_t)nq * d * sizeof(float), hipHostMallocDefault));
+        c.cap_q = (size_t)nq * d;
+    }
+    if ((size_t)nq * k > c.cap_r) {
+        hipHostFree(c.h_idx);
+        hipHostFree(c.h_err);
+        c.h_idx = nullptr;
+        c.h_err = nullptr;
+        c.cap_r = 0;
+        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_idx, (size_t)nq * k * sizeof(int), hipHostMallocDefault));
+        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_err, (size_t)nq * k * sizeof(float), hipHostMallocDefault));
+        c.cap_r = (size_t)nq * k;
+    }
+    for (int j = 0; j < nq; j++) memcpy(c.h_q + (size_t)j * d, b[j]->q, (size_t)d * sizeof(float));
+    if (ensure_io(t, nq, d, k)) return -1;
+    TILER_HIP_CHECK(hipMemcpyAsync(t->d_q, c.h_q, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, t->stream));
+    if (nn_search_dev(ix, t->d_q, nq, k, t->d_idx, t->d_err, nullptr, t->stream)) return -1;
+    TILER_HIP_CHECK(hipMemcpyAsync(c.h_idx, t->d_idx, (size_t)nq * k * sizeof(int), hipMemcpyDeviceToHost, t->stream));
+    TILER_HIP_CHECK(hipMemcpyAsync(c.h_err, t->d_err, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, t->stream));
+    TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
+    for (int j = 0; j < nq; j++) {
+        memcpy(b[j]->idx, c.h_idx + (size_t)j * k, (size_t)k * sizeof(int));
+        memcpy(b[j]->err, c.h_err + (size_t)j * k, (size_t)k * sizeof(float));
+    }
+    return 0;
+}
+
+static int combined_search(ann_kdtree *t, const float *q, int k, int *idx, float *err) {
+    if (!t || !t->ix || !q || !idx || !err) {
+        set_error("ann_kdtree_search: invalid arguments");
+        return -1;
+    }
+    if (k < 1 || k > 32) {
+        set_error("ann_kdtree_search: k must be in 1..32");
+        return -1;
+    }
+    if (!ensure_init()) return -1;
+    Combiner &c = t->comb;
+    CombineReq me;
+    me.q = q;
+    me.k = k;
+    me.idx = idx;
+    me.err = err;
+    std::unique_lock<std::mutex> lk(c.m);
+    c.pending.push_back(&me);
+    c.calls++;
+    while (!me.done) {
+        if (c.busy) {
+            c.cv.wait(lk);
+            continue;
+        }
+        c.busy = true;  // lead: batches until this caller's own query is answered
+        while (!me.done) {
+            std::vector<CombineReq *> b;
+            const int bk = c.pending.front()->k;
+            for (auto it = c.pending.begin(); it != c.pending.end() && (int)b.size() < COMBINE_MAX;) {
+                if ((*it)->k == bk) {
+                    b.push_back(*it);
+                    it = c.pending.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+            c.batches++;
+            c.max_batch = std::max(c.max_batch, (int)b.size());
+            lk.unlock();
+            const int rc = combine_run(t, b, bk);
+            const std::string msg = rc ? std::string(last_error()) : std::string();
+            lk.lock();
+            for (CombineReq *r : b) {
+                r->rc = rc;
+                r->msg = msg;
+                r->done = true;
+            }
+            c.cv.notify_all();
+        }
+        c.busy = false;
+        if (!c.pending.empty()) c.cv.notify_all();  // a waiting caller takes over the queue
+    }
+    if (me.rc) set_error(me.msg);
+    return me.rc;
+}
+
 int ann_kdtree_search(ann_kdtree *t, float *q, float eps, float *err) {
+    (void)eps;  // the exact answer satisfies every eps bound
     int idx = -1;
     float e = 0.0f;
-    if (ann_kdtree_search_multi_batch(t, q, 1, 1, eps, &idx, &e)) return -1;
+    if (combined_search(t, q, 1, &idx, &e)) return -1;
     if (err) *err = e;
     return idx;
 }
@@ -415,7 +553,20 @@ int ann_kdtree_search(ann_kdtree *t, float *q, float eps, float *err) {
 int ann_kdtree_pri_search(ann_kdtree *t, float *q, float eps, float *err) { return ann_kdtree_search(t, q, eps, err); }
 
 int ann_kdtree_search_multi(ann_kdtree *t, int *idxs, float *errs, int cnt, float *q, float eps) {
-    return ann_kdtree_search_multi_batch(t, q, 1, cnt, eps, idxs, errs);
+    (void)eps;
+    return combined_search(t, q, cnt, idxs, errs);
+}
+
+int tiler_combine_stats(ann_kdtree *t, int64_t *calls, int64_t *batches, int32_t *max_batch) {
+    if (!t) {
+        set_error("tiler_combine_stats: null handle");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(t->comb.m);
+    if (calls) *calls = t->comb.calls;
+    if (batches) *batches = t->comb.batches;
+    if (max_batch) *max_batch = t->comb.max_batch;
+    return 0;
 }
 
 int ann_kdtree_search_batch_dev(ann_kdtree *t, const float *d_q, int nq, int k, int *d_idx, float *d_err,
@@ -569,6 +720,26 @@ int tiler_ft_set_maps(ann_kdtree *t, const int32_t *tr_tile, const int32_t *tr_p
     TILER_HIP_CHECK(hipMemcpy(ix->d_tr_tile, tr_tile, (size_t)ix->n * 4, hipMemcpyHostToDevice));
     TILER_HIP_CHECK(hipMemcpy(ix->d_tr_pal, tr_pal, (size_t)ix->n * 4, hipMemcpyHostToDevice));
     TILER_HIP_CHECK(hipMemcpy(ix->d_tr_attr, tr_attr, (size_t)ix->n, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int tiler_ft_get_maps(ann_kdtree *t, int32_t *tr_tile, int32_t *tr_pal, uint8_t *tr_attr) {
+    if (!t || !t->ix || !tr_tile || !tr_pal || !tr_attr) {
+        set_error("tiler_ft_get_maps: invalid arguments");
+        return -1;
+    }
+    if (!t->ix->d_tr_tile) {
+        set_error("tiler_ft_get_maps: the handle has no maps");
+        return -1;
+    }
+    if (!ensure_init()) return -1;
+    NNIndex *ix = t->ix;
+    std::lock_guard<std::mutex> lk(ix->mu);
+    TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
+    TILER_HIP_CHECK(hipDeviceSynchronize());  // maps may have been written on the creator's stream
+    TILER_HIP_CHECK(hipMemcpy(tr_tile, ix->d_tr_tile, (size_t)ix->n * 4, hipMemcpyDeviceToHost));
+    TILER_HIP_CHECK(hipMemcpy(tr_pal, ix->d_tr_pal, (size_t)ix->n * 4, hipMemcpyDeviceToHost));
+    TILER_HIP_CHECK(hipMemcpy(tr_attr, ix->d_tr_attr, (size_t)ix->n, hipMemcpyDeviceToHost));
     return 0;
 }
 

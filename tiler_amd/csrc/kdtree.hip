@@ -256,8 +256,8 @@ __global__ __launch_bounds__(64 * KD_MW) void kd_median_big_kernel(float *__rest
         for (int p0 = a0; p0 < a1; p0 += 64) {
             const int p = p0 + lane;
             const float v = p < a1 ? kk[p] : 0.0f;
-            nl += __popcll(__ballot(p < a1 && p > l && v >= c));
-            nr += __popcll(__ballot(p < a1 && p < r && v <= c));
+            nl += __popcll(__ballot(p < a1 && p > l && !(v < c)));
+            nr += __popcll(__ballot(p < a1 && p < r && !(v > c)));
         }
         if (lane == 0) {
             wl[w] = nl;
@@ -276,7 +276,9 @@ __global__ __launch_bounds__(64 * KD_MW) void kd_median_big_kernel(float *__rest
         for (int p0 = a0; p0 < a1; p0 += 64) {
             const int p = p0 + lane;
             const float v = p < a1 ? kk[p] : 0.0f;
-            const bool isl = p < a1 && p > l && v >= c, isr = p < a1 && p < r && v <= c;
+            // a stopper is where the scan's loop test FAILS: !(key < c) / !(key > c), so a NaN key (or a NaN pivot)
+            // stops both scans exactly as the sequential loop's comparisons do (and position l always stops the k-scan)
+            const bool isl = p < a1 && p > l && !(v < c), isr = p < a1 && p < r && !(v > c);
             const unsigned long long bL = __ballot(isl), bR = __ballot(isr);
             const int jl = bl + __popcll(bL & below) + 1;  // rank from the left (1-based)
             const int rb = br + __popcll(bR & below);      // right stoppers below p
@@ -306,12 +308,14 @@ __global__ __launch_bounds__(64 * KD_MW) void kd_median_big_kernel(float *__rest
         }
         __syncthreads();
     }
-    // the first maximum of kk[0..n_lo) to n_lo - 1
+    // the first maximum of kk[0..n_lo) to n_lo - 1.  Sequentially m = 0, then m = i where key[i] > key[m]: a NaN key
+    // never replaces m, and a NaN key[0] is never replaced -- so NaN keys are skipped here and key[0] = NaN decides
+    // below
     float bv = -INFINITY;
     int bi = 0x7fffffff;
     for (int i = tid; i < n_lo; i += 64 * KD_MW) {
         const float v = kk[i];
-        if (v > bv || bi == 0x7fffffff) {  // a thread's indices ascend: strict > keeps its first
+        if (v == v && (v > bv || bi == 0x7fffffff)) {  // a thread's indices ascend: strict > keeps its first
             bv = v;
             bi = i;
         }
@@ -337,6 +341,7 @@ __global__ __launch_bounds__(64 * KD_MW) void kd_median_big_kernel(float *__rest
                 c = wv[x];
                 k = wp[x];
             }
+        if (n_lo > 0 && (k == 0x7fffffff || kk[0] != kk[0])) k = 0;  // key[0] NaN (or every key NaN): m stays 0
         if (n_lo > 0) kd_swap(kk, ii, n_lo - 1, k);
         const int m = N.s + n_lo;
         cd_out[m] = cut_dim[blockIdx.x];

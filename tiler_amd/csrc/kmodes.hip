@@ -100,145 +100,6 @@ struct KmState {
     int *mvn;                  // [1] their count
 };
 
-// ---- farthest-first (InitFarthestFirst kmodes.pas:698-776) ----
-// update mindist with the centre chosen last, then per-block argmax over unused points ('>=' -> last)
-__global__ __launch_bounds__(256) void km_ff_update(KmState s, int j) {
-    __shared__ unsigned long long best[256];
-    const int c = s.center[j];
-    uint32_t item[20];
-    load_row(s.X + (long)c * KM_A, item);
-    unsigned long long bk = 0;  // (value, index) max packed: value in high bits is not possible (u64 values)
-    unsigned long long bv = 0;
-    int bi = -1;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < s.n; i += (long)gridDim.x * 256) {
-        uint32_t row[20];
-        load_row(s.X + i * KM_A, row);
-        const unsigned long long d = km_dissim(row, item);
-        unsigned long long m = s.mind[i];
-        if (d < m) {  // cmovb: strict-less (kmodes.pas:555-558); the 'used' skip is a no-op (567)
-            m = d;
-            s.mind[i] = m;
-        }
-        if (!s.used[i] && m >= bv) {  // ascending i within a thread: '>=' keeps the last
-            bv = m;
-            bi = (int)i;
-        }
-    }
-    (void)bk;
-    // block reduce (value max, ties -> larger index); value fits 32 bits (dis < 2^19) unless UINT64_MAX
-    const unsigned long long v32 = bv > 0xFFFFFFFFull ? 0xFFFFFFFFull : bv;
-    best[threadIdx.x] = (bi < 0) ? 0ull : ((v32 << 32) | (unsigned)(bi + 1));
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) best[threadIdx.x] = max(best[threadIdx.x], best[threadIdx.x + o]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) s.part[blockIdx.x] = best[0];
-}
-
-__global__ __launch_bounds__(256) void km_ff_select(KmState s, int j, int nblk) {
-    __shared__ unsigned long long best[256];
-    unsigned long long b = 0;
-    for (int i = threadIdx.x; i < nblk; i += 256) b = max(b, s.part[i]);
-    best[threadIdx.x] = b;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) best[threadIdx.x] = max(best[threadIdx.x], best[threadIdx.x + o]);
-        __syncthreads();
-    }
-    const unsigned long long w = best[0];
-    const int f = (w == 0) ? -1 : (int)(w & 0xFFFFFFFFull) - 1;
-    if (f < 0) {
-        if (threadIdx.x == 0) *s.err = 1;
-        return;
-    }
-    if (threadIdx.x < KM_A) s.cent[(long)j * KM_A + threadIdx.x] = s.X[(long)f * KM_A + threadIdx.x];
-    if (threadIdx.x == 0) {
-        s.center[j] = f;
-        s.used[f] = 1;
-    }
-}
-
-// ---- assignment: akey[i] = min over centroids of (dis << 32 | ~c)  (argmin, ties -> last centroid) ----
-// grid: (points / 256, centroid splits); centroids staged through LDS in tiles of 128
-__global__ __launch_bounds__(256) void km_assign(KmState s, int p0, int p1, int csplit) {
-    __shared__ uint4 ct[128 * 5];
-    const long i = p0 + (long)blockIdx.x * 256 + threadIdx.x;
-    const bool valid = i < p1;
-    uint32_t item[20];
-    if (valid) load_row(s.X + i * KM_A, item);
-    const int per = (s.K + csplit - 1) / csplit;
-    const int c0 = blockIdx.y * per, c1 = min(s.K, c0 + per);
-    unsigned long long best = ~0ull;
-    for (int t0 = c0; t0 < c1; t0 += 128) {
-        const int cnt = min(128, c1 - t0);
-        __syncthreads();
-        for (int e = threadIdx.x; e < cnt * 5; e += 256)
-            ct[e] = reinterpret_cast<const uint4 *>(s.cent + (long)t0 * KM_A)[e];
-        __syncthreads();
-        if (valid) {
-            for (int c = 0; c < cnt; c++) {
-                uint32_t row[20];
-#pragma unroll
-                for (int q = 0; q < 5; q++) {
-                    const uint4 v = ct[c * 5 + q];
-                    row[4 * q] = v.x;
-                    row[4 * q + 1] = v.y;
-                    row[4 * q + 2] = v.z;
-                    row[4 * q + 3] = v.w;
-                }
-                const unsigned long long d = km_dissim(row, item);
-                const unsigned long long key = (d << 32) | (0xFFFFFFFFu - (unsigned)(t0 + c));
-                best = key < best ? key : best;
-            }
-        }
-    }
-    if (valid) atomicMin(&s.akey[i], best);
-}
-
-__global__ void km_fill_u64(unsigned long long *p, long n, unsigned long long v) {
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = v;
-}
-
-// initial labels + histograms (ComputeKModes kmodes.pas:984-1008)
-__global__ __launch_bounds__(256) void km_init_hist(KmState s) {
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < s.n; i += (long)gridDim.x * 256) {
-        const int c = (int)(0xFFFFFFFFu - (unsigned)(s.akey[i] & 0xFFFFFFFFull));
-        s.memb[i] = c;
-        atomicAdd(&s.csize[c], 1);
-        for (int a = 0; a < KM_A; a++) atomicAdd(&s.freq[((long)c * KM_A + a) * s.M + s.X[i * KM_A + a]], 1);
-    }
-}
-
-// modes (kmodes.pas:1010-1021): empty clusters take X[RandInt(n)][a] per attribute in (k, a) order
-__global__ __launch_bounds__(256) void km_init_modes(KmState s, int32_t *rand_rows) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        unsigned seed = *s.seed;
-        for (int k = 0; k < s.K; k++)
-            if (s.csize[k] == 0)
-                for (int a = 0; a < KM_A; a++) rand_rows[(long)k * KM_A + a] = (int)km_randint((unsigned)s.n, &seed);
-        *s.seed = seed;
-    }
-}
-
-__global__ __launch_bounds__(256) void km_init_modes2(KmState s, const int32_t *rand_rows) {
-    for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < (long)s.K * KM_A; e += (long)gridDim.x * 256) {
-        const int k = (int)(e / KM_A), a = (int)(e % KM_A);
-        if (s.csize[k] == 0) {
-            s.cent[e] = s.X[(long)rand_rows[e] * KM_A + a];
-        } else {
-            const int32_t *f = s.freq + e * s.M;
-            int bi = -1, bv = INT32_MIN;
-            for (int m = 0; m < s.M; m++)
-                if (f[m] > bv) {
-                    bv = f[m];
-                    bi = m;
-                }
-            s.cent[e] = (uint8_t)bi;  // GetMaxValueIndex: first max (kmodes.pas:149-161)
-        }
-    }
-}
-
 // ---- the sequential part of one bin (KModesIter kmodes.pas:869-911), one workgroup of KM_SEQ_NT ----
 static constexpr int KM_SEQ_NT = 512;  // 32 moves of 16 lanes (round 2: 6 of 80 lanes; 320..1024 threads: 512 best)
 static constexpr int KM_SEQ_W = 16;    // lanes per move: 5 attributes per lane

@@ -285,7 +285,16 @@ struct Prep16Args {
     half8 *frag;    // [ceil(n/16)][S][64][8]
     float *seed;    // dataset: [ceil(n/16)][16] -||c||^2/2 by A row (-inf on padding rows); queries: null
     int perm;
+    int dcfirst;    // 1 (d = 192, both operands alike): the three PsyV DC dimensions 0, 64, 128 in k-step 0
 };
+
+// Fragment position k -> descriptor dimension.  A flat tile's Haar PsyV (one colour) is exactly zero but in the Y, U
+// and V DC (dimensions 0, 64, 128); swapping 64 <-> 1 and 128 <-> 2 on BOTH sides (the contraction is invariant under
+// a common permutation) puts all three into k-step 0, so a workgroup of flat queries needs k-step 0 only: the other
+// k-steps would add exactly +-0 products to every accumulator.
+__device__ __forceinline__ int dc_first_dim(int k) {
+    return k == 1 ? 64 : k == 64 ? 1 : k == 2 ? 128 : k == 128 ? 2 : k;
+}
 
 __global__ __launch_bounds__(256) void prep16_kernel(Prep16Args a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
@@ -299,7 +308,8 @@ __global__ __launch_bounds__(256) void prep16_kernel(Prep16Args a) {
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 const int k = s * 32 + 8 * g + j;
-                const float v = (valid && k < a.d) ? a.rows[row * a.d + k] : 0.0f;
+                const int kd = a.dcfirst ? dc_first_dim(k) : k;
+                const float v = (valid && k < a.d) ? a.rows[row * a.d + kd] : 0.0f;
                 const float vs = v * a.scale;
                 _Float16 vh = (_Float16)vs;
                 if (fabsf((float)vh) < 6.103515625e-05f) vh = (_Float16)0.0f;  // as prep_rows_kernel
@@ -316,13 +326,16 @@ __global__ __launch_bounds__(256) void prep16_kernel(Prep16Args a) {
     }
 }
 
-template <int S, int L, int CB, int NW, int QB>
-__global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 *__restrict__ cfrag,
-                                                                const float *__restrict__ cseed, int nblk,
-                                                                const half8 *__restrict__ qfrag, int nq,
-                                                                int blk_per_split, int nsplit, int perm,
-                                                                float *__restrict__ out_key,
-                                                                int *__restrict__ out_idx) {
+// FLAT: a workgroup whose queries are all flat tiles (grouped last by nn_frame_tiling_dev; their fragments are zero
+// beyond k-step 0, dc_first_dim): per candidate block only k-step 0 is streamed (1 of S KB) and contracted, the
+// same keys bit for bit.
+// MODE (timing experiments of the experiment build only; results invalid when != 0): 1 no list insertion, 2 no
+// epilogue, 3 no epilogue and no A-fragment reads inside the stage (the MFMA + stream floor)
+template <int S, int L, int CB, int NW, int QB, bool FLAT, int MODE = 0>
+__device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag, const float *__restrict__ cseed,
+                                                 int nblk, const half8 *__restrict__ qfrag, int nq, int blk_per_split,
+                                                 int nsplit, int perm, float *__restrict__ out_key,
+                                                 int *__restrict__ out_idx) {
     typedef float floatx4 __attribute__((ext_vector_type(4)));
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * S * 1024;
@@ -367,7 +380,11 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 
         const int nb = min(CB, b_end - blk0);
         const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64 + w * 64 + lane;
         char *dst = smem + buf * BUF_BYTES + w * 1024;
-        if (nb == CB) {
+        if constexpr (FLAT) {  // wave w: k-step 0 of block w (the last block again past the end: never read)
+            static_assert(CB == NW, "one k-step-0 piece per wave");
+            glds16_asm(reinterpret_cast<const uint4 *>(cfrag) + (long)(blk0 + min(w, nb - 1)) * S * 64 + lane,
+                       smem + buf * BUF_BYTES + w * S * 1024);
+        } else if (nb == CB) {
 #pragma unroll
             for (int j = 0; j < PER_T; j++) glds16_asm(src + j * NT, dst + j * NT * 16);
         } else {
@@ -398,11 +415,18 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 
             const int blk = b_begin + st * CB + cb;
             if (blk < b_end) {
                 floatx4 acc[QB];
+                if constexpr (FLAT) {
+                    const half8 af = A[(cb * S) * 64];
+#pragma unroll
+                    for (int q = 0; q < QB; q++)
+                        acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bq[q][0], sd[cb], 0, 0, 0);
+                } else {
 #pragma unroll
                 for (int s = 0; s < S; s += 2) {
                     half8 n0, n1;
-                    const bool more = s + 2 < S || cb + 1 < CB;
-                    if (s + 2 < S) {
+                    const bool more = MODE != 3 && (s + 2 < S || cb + 1 < CB);
+                    if constexpr (MODE == 3) {
+                    } else if (s + 2 < S) {
                         n0 = A[(cb * S + s + 2) * 64];
                         n1 = A[(cb * S + s + 3) * 64];
                     } else if (cb + 1 < CB) {
@@ -422,12 +446,22 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 
                         a1 = n1;
                     }
                 }
+                }
+                if constexpr (MODE >= 2) {
+#pragma unroll
+                    for (int q = 0; q < QB; q++) li[q][0] += __float_as_int(acc[q][0]) & 1;  // keeps the MFMAs live
+                    continue;
+                }
                 // epilogue: acc = q.c - ||c||^2/2, key = -2 acc; one wave-uniform branch per block
                 bool need = false;
 #pragma unroll
                 for (int q = 0; q < QB; q++) {
                     const float m = fmaxf(fmaxf(acc[q][0], acc[q][1]), fmaxf(acc[q][2], acc[q][3]));
                     need |= m > -0.5f * lk[q][L - 1];
+                }
+                if constexpr (MODE == 1) {
+                    li[0][0] += need ? 1 : 0;
+                    continue;
                 }
                 if (__builtin_expect(__any(need), 0)) {
                     const int base = blk * 16;
@@ -456,6 +490,22 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 
             }
         }
     }
+}
+
+// flat_cnt (or null): device count of the batch's non-flat queries, the flat ones placed after them
+template <int S, int L, int CB, int NW, int QB, int MODE = 0>
+__global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 *__restrict__ cfrag,
+                                                                const float *__restrict__ cseed, int nblk,
+                                                                const half8 *__restrict__ qfrag, int nq,
+                                                                int blk_per_split, int nsplit, int perm,
+                                                                float *__restrict__ out_key,
+                                                                int *__restrict__ out_idx, const int *flat_cnt) {
+    if (flat_cnt && (long)blockIdx.x * (NW * QB * 16) >= (long)*flat_cnt)
+        shortlist16_body<S, L, CB, NW, QB, true, MODE>(cfrag, cseed, nblk, qfrag, nq, blk_per_split, nsplit, perm,
+                                                       out_key, out_idx);
+    else
+        shortlist16_body<S, L, CB, NW, QB, false, MODE>(cfrag, cseed, nblk, qfrag, nq, blk_per_split, nsplit, perm,
+                                                        out_key, out_idx);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -958,7 +1008,7 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hip
         ix->nblk16 = (int)((n + 15) / 16);
         TILER_HIP_CHECK_NULL(hipMalloc(&ix->d_frag16, (size_t)ix->nblk16 * ix->S16 * 1024));
         TILER_HIP_CHECK_NULL(hipMalloc((void **)&ix->d_seed16, (size_t)ix->nblk16 * 16 * sizeof(float)));
-        Prep16Args p16{d_rows, n, d, ix->S16, scale, (half8 *)ix->d_frag16, ix->d_seed16, 1};
+        Prep16Args p16{d_rows, n, d, ix->S16, scale, (half8 *)ix->d_frag16, ix->d_seed16, 1, d == 192 ? 1 : 0};
         hipLaunchKernelGGL(prep16_kernel, dim3((unsigned)std::min<long>(4096, (ix->nblk16 + 3) / 4)), dim3(256), 0,
                            stream, p16);
         TILER_HIP_CHECK_NULL(hipGetLastError());
@@ -1084,6 +1134,18 @@ static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream
 // D=192 generic shortlist variant (A/B switch TILER_SHORTLIST, datasets without mirror orbits; C3 keyframe,
 // one box): "q16" (default): nn_shortlist16_kernel, 16x16x32 MFMA, L16 = 4 (51.6 ms); "q16l6": L16 = 6
 // (53.4 ms, fewer tier-2 queries); "w8": nn_shortlist_kernel, 32x32x16, 8 waves x 2 query blocks (63.9 ms)
+#ifdef TILER_EXPERIMENTS
+// TILER_SL16_MODE=1..3: timing modes of the 16x16x32 shortlist (shortlist16_body MODE); the search then stops after
+// the shortlist with idx = 0, err = 0 (nothing downstream may use such results)
+static int sl16_mode() {
+    static int m = [] {
+        const char *e = getenv("TILER_SL16_MODE");
+        return e ? atoi(e) : 0;
+    }();
+    return m;
+}
+#endif
+
 static int shortlist_variant() {
 #ifdef TILER_EXPERIMENTS
     static int v = [] {
@@ -1113,10 +1175,27 @@ static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
     const dim3 grid((nqblk + SL16_NW * SL16_QB - 1) / (SL16_NW * SL16_QB), nsplit);
     const size_t lds = 2 * (SL16_CB * S * 1024 + SL16_CB * 64);
     KTimer tm("nn_shortlist", stream);
+#ifdef TILER_EXPERIMENTS
+    const int mode = sl16_mode();
+    if (mode) {
+        auto k = mode == 1 ? nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 1>
+                 : mode == 2 ? nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 2>
+                             : nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 3>;
+        hipLaunchKernelGGL(k, grid, dim3(SL16_NW * 64), lds, stream, (const half8 *)ix->d_frag16, ix->d_seed16,
+                           ix->nblk16, (const half8 *)ix->scratch.qfrag16, nq, bps, nsplit, ix->perm, ix->scratch.key,
+                           ix->scratch.idx, ix->flat_cnt);
+    } else
+#endif
     hipLaunchKernelGGL((nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB>), grid, dim3(SL16_NW * 64), lds, stream,
                        (const half8 *)ix->d_frag16, ix->d_seed16, ix->nblk16, (const half8 *)ix->scratch.qfrag16, nq,
-                       bps, nsplit, ix->perm, ix->scratch.key, ix->scratch.idx);
+                       bps, nsplit, ix->perm, ix->scratch.key, ix->scratch.idx, ix->flat_cnt);
     TILER_HIP_CHECK(hipGetLastError());
+    if (ix->flat_cnt) {  // flat_queries of the stats: derived from the device count when they are read
+        ix->last_flat_dev = ix->flat_cnt;
+        ix->last_flat_nq = nq;
+        ix->last_flat_qpw = SL16_NW * SL16_QB * 16;
+        ix->last_flat_wgs = grid.x;
+    }
     return 0;
 }
 
@@ -1227,6 +1306,12 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         TILER_HIP_CHECK(hipMemsetAsync(s.kd_count, 0, sizeof(int), stream));
     }
     if (search_core(ix, ra, d_q, nq, k, stream, orbit_prepared)) return -1;
+#ifdef TILER_EXPERIMENTS
+    if (ix->S16 > 0 && !ix->orbit && sl16_mode()) {  // timing mode: no verify over the invalid results
+        TILER_HIP_CHECK(hipEventRecord(ix->done_event, stream));
+        return 0;
+    }
+#endif
     if (!ix->kd) {
         TILER_HIP_CHECK(hipEventRecord(ix->done_event, stream));
         return 0;
@@ -1323,7 +1408,7 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     }
     TILER_HIP_CHECK(hipGetLastError());
     if (v16) {
-        Prep16Args p16{d_q, nq, ix->d, ix->S16, ix->scale, (half8 *)s.qfrag16, nullptr, 0};
+        Prep16Args p16{d_q, nq, ix->d, ix->S16, ix->scale, (half8 *)s.qfrag16, nullptr, 0, ix->d == 192 ? 1 : 0};
         {
             KTimer t_prep("nn_prep", stream);
             hipLaunchKernelGGL(prep16_kernel, dim3((unsigned)std::min<long>(4096, ((nq + 15) / 16 + 3) / 4)),
@@ -1341,6 +1426,13 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     } else if (dispatch_shortlist<8>(ix, nq, nsplit, bps, stream)) {
         return -1;
     }
+#ifdef TILER_EXPERIMENTS
+    if (v16 && sl16_mode()) {
+        TILER_HIP_CHECK(hipMemsetAsync(ra.out_idx, 0, (size_t)nq * k * sizeof(int), stream));
+        TILER_HIP_CHECK(hipMemsetAsync(ra.out_err, 0, (size_t)nq * k * sizeof(float), stream));
+        return 0;
+    }
+#endif
     ra.qstat = s.qstat;
     ra.key = s.key;
     ra.idx = s.idx;
@@ -1494,16 +1586,19 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
     }
     const bool fuse_rb = ix->kd && use_wavelets && ix->kd->dd == 192;
     if (fuse_rb && ensure_scratch(ix, Q, 0)) return -1;
-    if (ix->orbit && use_wavelets) {
 #ifdef TILER_EXPERIMENTS
-        static const bool noflat = getenv("TILER_NO_FLAT") != nullptr;  // A/B: tiles in their own order
+    static const bool noflat = getenv("TILER_NO_FLAT") != nullptr;  // A/B: tiles in their own order
 #else
-        constexpr bool noflat = false;
+    constexpr bool noflat = false;
 #endif
+    // flat grouping on the generic path (datasets without mirror orbits: real PrepareFrameTiling candidate sets):
+    // the 16x16x32 shortlist's flat workgroups contract k-step 0 only (dc_first_dim)
+    const bool flat_generic = !ix->orbit && use_wavelets && ix->S16 > 0 && shortlist16_L() > 0 && Q >= 8192;
+    if (flat_generic || (ix->orbit && use_wavelets)) {
         // flat tiles last (see ft_flat_flag_kernel) when the shortlist is long enough to repay the ~0.1 ms of
         // grouping: C3 (2,048 group blocks) -0.6..-1.1 ms per step; C2 (512 blocks, whose ragged last round the mixed
         // split already fills) +0.08 ms (profiles/flat_c2_ab.sh), so not there
-        if (!noflat && Q >= 8192 && ((const OrbitIndex *)ix->orbit)->gblk >= 1024) {
+        if (!noflat && Q >= 8192 && (flat_generic || ((const OrbitIndex *)ix->orbit)->gblk >= 1024)) {
             const int nb = (Q + 255) / 256;
             if ((size_t)Q > s.cap_flat) {
                 hipFree(s.fperm);
@@ -1540,9 +1635,27 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
             FtMaps fm;
             if (maps) fm = FtMaps{s.ftile, s.fpal, s.fhm, s.fvm};
             ix->flat_cnt = s.fcnt;  // the shortlist reads the non-flat count on the device (no host sync)
-            int rc = orbit_ft_queries(ix, d_rgb, Q, gamma, s.qrows, fuse_rb ? ix->kd->d_box : nullptr,
+            int rc = 0;
+            if (flat_generic) {
+                PsyvArgs pa;
+                pa.n = Q;
+                pa.rgb = d_rgb;
+                pa.perm = s.fperm;
+                pa.flags = PSYV_WAVELETS;
+                pa.gamma = gamma;
+                pa.out32 = s.qrows;
+                if (fuse_rb) {
+                    pa.box = ix->kd->d_box;
+                    pa.rootbox = s.kd_rootbox;
+                }
+                rc = launch_psyv(pa, stream);
+                if (!rc) rc = nn_search_dev(ix, s.qrows, Q, 1, s.fidx, s.ferr, maps ? &fm : nullptr, stream, fuse_rb);
+            } else {
+                rc = orbit_ft_queries(ix, d_rgb, Q, gamma, s.qrows, fuse_rb ? ix->kd->d_box : nullptr,
                                       fuse_rb ? s.kd_rootbox : nullptr, stream, s.fperm);
-            if (!rc) rc = nn_search_dev(ix, s.qrows, Q, 1, s.fidx, s.ferr, maps ? &fm : nullptr, stream, fuse_rb, true);
+                if (!rc)
+                    rc = nn_search_dev(ix, s.qrows, Q, 1, s.fidx, s.ferr, maps ? &fm : nullptr, stream, fuse_rb, true);
+            }
             ix->flat_cnt = nullptr;
             if (rc) return -1;
             hipLaunchKernelGGL(ft_unpermute_kernel, dim3(nb), dim3(256), 0, stream, Q, (const int *)s.fperm,
@@ -1552,6 +1665,8 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
             TILER_HIP_CHECK(hipGetLastError());
             return 0;
         }
+    }
+    if (ix->orbit && use_wavelets) {
         // one kernel: descriptors + the orbit search's q' fragments and statistics (+ the kd root box)
         if (orbit_ft_queries(ix, d_rgb, Q, gamma, s.qrows, fuse_rb ? ix->kd->d_box : nullptr,
                              fuse_rb ? s.kd_rootbox : nullptr, stream))

@@ -175,6 +175,7 @@ void prep_scratch_free(PrepScratch *s) {
     hipFree(s->attrs);
     hipFree(s->flags);
     hipHostFree(s->h_total);
+    if (s->done) hipEventDestroy(s->done);
     *s = PrepScratch{};
 }
 
@@ -206,6 +207,9 @@ NNIndex *prepare_frame_tiling_dev(NNIndex *global, PrepScratch &s, const int32_t
     }
     if (!s.h_total) TILER_HIP_CHECK_NULL(hipHostMalloc((void **)&s.h_total, 2 * sizeof(int), hipHostMallocDefault));
     if (!s.total) TILER_HIP_CHECK_NULL(hipMalloc((void **)&s.total, 2 * sizeof(int)));
+    if (!s.done) TILER_HIP_CHECK_NULL(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    // the previous prepare's map copies (queued on its own stream) still read tile_of / pal_of / attrs
+    TILER_HIP_CHECK_NULL(hipStreamWaitEvent(stream, s.done, 0));
     // 1. distinct (pal, tile) items in key order
     const long nkw = ((long)P * T + 31) / 32;
     const long nuw = ((long)P * T * 4 + 31) / 32;
@@ -300,6 +304,7 @@ NNIndex *prepare_frame_tiling_dev(NNIndex *global, PrepScratch &s, const int32_t
         nn_index_destroy(ix);
         return nullptr;
     }
+    TILER_HIP_CHECK_NULL(hipEventRecord(s.done, stream));
     if (n_distinct) *n_distinct = nq;
     if (n_cand) *n_cand = M;
     return ix;

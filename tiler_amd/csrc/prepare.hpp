@@ -19,6 +19,9 @@ struct PrepScratch {
     int32_t *tile_of = nullptr, *pal_of = nullptr;  // [cand] DoPsyV emission order
     uint8_t *attrs = nullptr, *flags = nullptr;     // [cand]
     int *h_total = nullptr;        // pinned [2]
+    // recorded on the caller's stream after the last read of this scratch (the TRTo* map copies); the next prepare,
+    // possibly on another stream, waits on it before it writes the scratch again
+    hipEvent_t done = nullptr;
     size_t cap_bits = 0, cap_items = 0, cap_used = 0, cap_cand = 0, cap_near = 0, cap_blk = 0;
 };
 void prep_scratch_free(PrepScratch *s);

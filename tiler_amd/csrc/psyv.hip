@@ -71,7 +71,8 @@ __global__ __launch_bounds__(64) void psyv_rgb_haar_kernel(PsyvArgs a) {
     const long t0 = (long)blockIdx.x * 64;
     const long i = t0 + lane;
     const bool valid = i < a.n;
-    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + (valid ? i : t0) * 64);
+    const long ti = valid ? i : t0;
+    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + (a.perm ? (long)a.perm[ti] : ti) * 64);
 #pragma unroll 1
     for (int c = 0; c < 3; c++) {
         double p[64];
@@ -192,6 +193,10 @@ int launch_psyv(PsyvArgs args, hipStream_t stream) {
     KTimer tm("psyv", stream);
     if (args.rootbox && !(args.rgb && !args.flags_per && args.flags == PSYV_WAVELETS)) {
         set_error("psyv: the fused root-box output exists on the RGB Haar query path only");
+        return -1;
+    }
+    if (args.perm && !(args.rgb && !args.flags_per && (args.flags & ~PSYV_QWEIGHT) == PSYV_WAVELETS)) {
+        set_error("psyv: a query permutation exists on the RGB Haar query path only");
         return -1;
     }
     if (args.rgb && !args.flags_per && (args.flags & ~PSYV_QWEIGHT) == PSYV_WAVELETS) {

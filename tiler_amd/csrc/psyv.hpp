@@ -23,6 +23,8 @@ struct PsyvArgs {
     // enclosing box, kdtree.hpp) -> rootbox[n], fused so the FrameTiling search's pruning check needs no re-read
     const float *box = nullptr;
     float *rootbox = nullptr;
+    // optional (RGB Haar query path only): descriptor i is made of tile rgb[perm[i]] (FrameTiling's flat grouping)
+    const int *perm = nullptr;
     // filled by launch_psyv from the shared LUTs
     const double *gamma_lut = nullptr, *dct_lut = nullptr, *qmul = nullptr, *ratio = nullptr, *lab_lin = nullptr;
     double haar_f = 0, u_mul = 0, v_mul = 0;

@@ -198,8 +198,8 @@ class Encoder:
         for k in self.kfs:
             r = self.rows(k)
             raws.append(gtm.keyframe_raw(k, self.palpix, self.thm, self.tvm, self.palettes[k], sm["tile"][r],
-                                         sm["pal"][r], sm["hm"][r], sm["vm"][r], sm["smoothed"][r], width, fps,
-                                         height, self.palsize))
+                                         sm["pal"][r], sm["hm"][r], sm["vm"][r], sm["smoothed"][r], width=width,
+                                         height=height, fps=fps, palsize=self.palsize))
         return dict(zip(self.kfs, gtm.compress_streams(raws)))
 
     def save_stream(self, width: int, height: int, fps: float = 24.0) -> bytes:

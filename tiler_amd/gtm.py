@@ -120,8 +120,8 @@ def keyframe_commands(tile, pal, hm, vm, smoothed, thm, tvm, palettes, palsize: 
     return bytes(z.b)
 
 
-def keyframe_raw(k: int, palpix, thm, tvm, palettes_k, tile, pal, hm, vm, smoothed, width: int, fps: float,
-                 height: int, palsize: int = 16) -> bytes:
+def keyframe_raw(k: int, palpix, thm, tvm, palettes_k, tile, pal, hm, vm, smoothed, *, width: int, height: int,
+                 fps: float, palsize: int = 16) -> bytes:
     """The uncompressed command bytes of keyframe k (SaveStream main.pas:4724-4734): WriteTiles for k = 0 only
     (SetDimensions + TileSet + 64 B per tile, 4603-4622), then WriteKFAttributes and the keyframe's frames
     (tile/pal/hm/vm/smoothed: its [f][Q] SmoothedTileMap rows)."""
@@ -193,5 +193,6 @@ def save_stream(palpix, thm, tvm, kf_start, palettes, sm_tile, sm_pal, sm_hm, sm
     for k in range(kf_start.size - 1):
         f0, f1 = int(kf_start[k]), int(kf_start[k + 1])
         raws.append(keyframe_raw(k, palpix, thm, tvm, palettes[k], sm_tile[f0:f1], sm_pal[f0:f1], sm_hm[f0:f1],
-                                 sm_vm[f0:f1], sm_smoothed[f0:f1], width, fps, height, palsize))
+                                 sm_vm[f0:f1], sm_smoothed[f0:f1], width=width, height=height, fps=fps,
+                                 palsize=palsize))
     return assemble_stream(compress_streams(raws, threads), kf_start, width, height, fps)

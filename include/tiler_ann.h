@@ -93,6 +93,10 @@ typedef struct {
                                  workgroup with non-flat ones are not counted.  0 for searches without flat grouping. */
 } tiler_search_stats;
 int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
+/* Search batches of at most max_k1 queries (k = 1; default 64) or max_k8 (k <= 8; default 16) -- the coalesced
+ * per-tile calls -- run an exhaustive exact scan spread over the whole GPU instead of the MFMA shortlist and its
+ * tiers (same answers; 0 disables it, e.g. to test those tiers on small batches).  Process-wide.  0 / -1. */
+int tiler_set_scan_limits(int max_k1, int max_k8);
 /* Coalescing counters of the single-query entry points on this handle: calls, batches searched, largest batch. */
 int tiler_combine_stats(ann_kdtree *akd, int64_t *calls, int64_t *batches, int32_t *max_batch);
 /* Leaf position of every dataset point in ANN's kd-tree (the order of its depth-first scan with every near

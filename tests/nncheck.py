@@ -10,19 +10,33 @@ import numpy as np
 INDEX_ORDER = 100
 
 
+SCAN_DEFAULT = (64, 16)  # tiler_set_scan_limits defaults (include/tiler_ann.h)
+
+
 def check_nn(gpu, oracle, data, qs, k=1, bs=1):
-    """k nearest neighbours of qs under both tie rules; returns the kd-order handle's stats."""
+    """k nearest neighbours of qs under both tie rules; returns the kd-order handle's stats.  A batch small enough for
+    the exhaustive small-batch scan is searched twice under the kd order: by that scan and, with it disabled, by the
+    MFMA shortlist and its tiers (whose stats are returned); both must equal the oracle."""
     data = np.ascontiguousarray(data, np.float32)
     qs = np.ascontiguousarray(qs, np.float32).reshape(-1, data.shape[1])
-    with gpu.KDTree(data, bs=bs) as kdt:
-        gi, ge = kdt.search_batch(qs, k=k)
-        st = kdt.stats()
+    lib = gpu.load()
+    small = qs.shape[0] <= (SCAN_DEFAULT[0] if k == 1 else SCAN_DEFAULT[1] if k <= 8 else 0)
+    runs = []
+    try:
+        for limits in ((SCAN_DEFAULT, (0, 0)) if small else (SCAN_DEFAULT,)):
+            assert lib.tiler_set_scan_limits(*limits) == 0
+            with gpu.KDTree(data, bs=bs) as kdt:
+                gi, ge = kdt.search_batch(qs, k=k)
+                runs.append((gi, ge, kdt.stats()))
+    finally:
+        lib.tiler_set_scan_limits(*SCAN_DEFAULT)
     okd = oracle.KDTree(data, bs=bs)
     oi, oe = okd.search_batch(qs, k=k)
     okd.close()
-    assert np.array_equal(ge.view(np.uint32), oe.view(np.uint32)), "kd order: distance mismatch"
-    bad = np.nonzero(np.any((gi != oi).reshape(qs.shape[0], -1), axis=1))[0]
-    assert bad.size == 0, f"kd order: {bad.size} of {qs.shape[0]} queries differ (first {bad[:8]})"
+    for gi, ge, st in runs:
+        assert np.array_equal(ge.view(np.uint32), oe.view(np.uint32)), "kd order: distance mismatch"
+        bad = np.nonzero(np.any((gi != oi).reshape(qs.shape[0], -1), axis=1))[0]
+        assert bad.size == 0, f"kd order: {bad.size} of {qs.shape[0]} queries differ (first {bad[:8]})"
     with gpu.KDTree(data, split=INDEX_ORDER) as kdt:
         gi2, ge2 = kdt.search_batch(qs, k=k)
         assert kdt.stats()["tie_order"] == 1

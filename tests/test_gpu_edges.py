@@ -104,8 +104,8 @@ def test_nonfinite_dataset_builds_and_searches(gpu):
     data[rng.random(n) < 0.15, 0] = np.nan
     data[rng.random(n) < 0.02, 5] = np.inf
     data[n // 2, 0] = np.nan  # the first pivot of the root's quickselect
-    q = rng.normal(0, 1, (64, d)).astype(np.float32)
-    q[:, 0] = rng.integers(0, 1000, 64).astype(np.float32)
+    q = rng.normal(0, 1, (96, d)).astype(np.float32)  # > 64: the MFMA path (not the small-batch scan)
+    q[:, 0] = rng.integers(0, 1000, 96).astype(np.float32)
     with gpu.KDTree(data) as kdt:
         pos = kdt.positions()
         gi, ge = kdt.search_batch(q)

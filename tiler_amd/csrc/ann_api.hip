@@ -557,6 +557,15 @@ int ann_kdtree_search_multi(ann_kdtree *t, int *idxs, float *errs, int cnt, floa
     return combined_search(t, q, cnt, idxs, errs);
 }
 
+int tiler_set_scan_limits(int max_k1, int max_k8) {
+    if (max_k1 < 0 || max_k8 < 0) {
+        set_error("tiler_set_scan_limits: negative limit");
+        return -1;
+    }
+    nn_set_scan_limits(max_k1, max_k8);
+    return 0;
+}
+
 int tiler_combine_stats(ann_kdtree *t, int64_t *calls, int64_t *batches, int32_t *max_batch) {
     if (!t) {
         set_error("tiler_combine_stats: null handle");

@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "nn_search.hpp"
 #include "kdorder_dev.hpp"
@@ -331,7 +332,14 @@ __global__ __launch_bounds__(256) void prep16_kernel(Prep16Args a) {
 // same keys bit for bit.
 // MODE (timing experiments of the experiment build only; results invalid when != 0): 1 no list insertion, 2 no
 // epilogue, 3 no epilogue and no A-fragment reads inside the stage (the MFMA + stream floor)
-template <int S, int L, int CB, int NW, int QB, bool FLAT, int MODE = 0>
+template <int N>
+__device__ __forceinline__ void vm_wait() {  // s_waitcnt vmcnt(N): all but this wave's N youngest vector-memory ops
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// VAR bit 0: per query block, a wave-uniform test before its 4 per-element list tests, thresholds kept in registers
+// (the same comparisons, so the same lists); bit 1: a 3-buffer LDS ring (two stages in flight instead of one)
+template <int S, int L, int CB, int NW, int QB, bool FLAT, int MODE = 0, int VAR = 0>
 __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag, const float *__restrict__ cseed,
                                                  int nblk, const half8 *__restrict__ qfrag, int nq, int blk_per_split,
                                                  int nsplit, int perm, float *__restrict__ out_key,
@@ -397,11 +405,25 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
                        smem + buf * BUF_BYTES + FRAG_BYTES);
     };
 
+    constexpr int NBUF = (VAR & 2) ? 3 : 2;
+    // a stage's DMA instructions per wave (the seed piece is wave 0's): the counted wait of the 3-buffer ring
+    auto wait_all_but_next = [&]() {
+        if (w == 0) vm_wait<(FLAT ? 1 : PER_T) + 1>();
+        else vm_wait<(FLAT ? 1 : PER_T)>();
+    };
+    float th[QB];  // VAR & 1: -0.5 * lk[q][L - 1] (and the window bound), kept current
+#pragma unroll
+    for (int q = 0; q < QB; q++) th[q] = -INFINITY;
     if (nstage > 0) issue(0, 0);
-    dma_drain();
+    if (NBUF == 3 && nstage > 1) {
+        issue(1, 1);
+        wait_all_but_next();
+    } else {
+        dma_drain();
+    }
     __syncthreads();
     for (int st = 0; st < nstage; st++) {
-        const char *B = smem + (st & 1) * BUF_BYTES;
+        const char *B = smem + (st % NBUF) * BUF_BYTES;
         const half8 *A = reinterpret_cast<const half8 *>(B) + lane;
         const floatx4 *SD = reinterpret_cast<const floatx4 *>(B + FRAG_BYTES) + g;
         floatx4 sd[CB];
@@ -409,7 +431,7 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
         for (int cb = 0; cb < CB; cb++) sd[cb] = SD[cb * 4];
         half8 a0 = A[0], a1 = A[64];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (st + 1 < nstage) issue(st + 1, (st + 1) & 1);
+        if (st + NBUF - 1 < nstage) issue(st + NBUF - 1, (st + NBUF - 1) % NBUF);
 #pragma unroll
         for (int cb = 0; cb < CB; cb++) {
             const int blk = b_begin + st * CB + cb;
@@ -454,10 +476,11 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
                 }
                 // epilogue: acc = q.c - ||c||^2/2, key = -2 acc; one wave-uniform branch per block
                 bool need = false;
+                float m[QB];
 #pragma unroll
                 for (int q = 0; q < QB; q++) {
-                    const float m = fmaxf(fmaxf(acc[q][0], acc[q][1]), fmaxf(acc[q][2], acc[q][3]));
-                    need |= m > -0.5f * lk[q][L - 1];
+                    m[q] = fmaxf(fmaxf(acc[q][0], acc[q][1]), fmaxf(acc[q][2], acc[q][3]));
+                    need |= m[q] > ((VAR & 1) ? th[q] : -0.5f * lk[q][L - 1]);
                 }
                 if constexpr (MODE == 1) {
                     li[0][0] += need ? 1 : 0;
@@ -465,16 +488,31 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
                 }
                 if (__builtin_expect(__any(need), 0)) {
                     const int base = blk * 16;
+                    if constexpr ((VAR & 1) != 0) {
 #pragma unroll
-                    for (int q = 0; q < QB; q++)
+                        for (int q = 0; q < QB; q++)
+                            if (__any(m[q] > th[q]))
 #pragma unroll
-                        for (int i = 0; i < 4; i++)
-                            if (acc[q][i] > -0.5f * lk[q][L - 1])
-                                list_insert<L>(lk[q], li[q], -2.0f * acc[q][i], base + rel[i]);
+                                for (int i = 0; i < 4; i++)
+                                    if (acc[q][i] > th[q]) {
+                                        list_insert<L>(lk[q], li[q], -2.0f * acc[q][i], base + rel[i]);
+                                        th[q] = -0.5f * lk[q][L - 1];
+                                    }
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < QB; q++)
+#pragma unroll
+                            for (int i = 0; i < 4; i++)
+                                if (acc[q][i] > -0.5f * lk[q][L - 1])
+                                    list_insert<L>(lk[q], li[q], -2.0f * acc[q][i], base + rel[i]);
+                    }
                 }
             }
         }
-        dma_drain();
+        if (NBUF == 3 && st + 2 < nstage)
+            wait_all_but_next();  // stage st + 1 landed, st + 2 may still be in flight
+        else
+            dma_drain();
         __syncthreads();
     }
     // partial lists: [q][split][g][L]
@@ -493,7 +531,7 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
 }
 
 // flat_cnt (or null): device count of the batch's non-flat queries, the flat ones placed after them
-template <int S, int L, int CB, int NW, int QB, int MODE = 0>
+template <int S, int L, int CB, int NW, int QB, int MODE = 0, int VAR = 0>
 __global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 *__restrict__ cfrag,
                                                                 const float *__restrict__ cseed, int nblk,
                                                                 const half8 *__restrict__ qfrag, int nq,
@@ -501,11 +539,11 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 
                                                                 float *__restrict__ out_key,
                                                                 int *__restrict__ out_idx, const int *flat_cnt) {
     if (flat_cnt && (long)blockIdx.x * (NW * QB * 16) >= (long)*flat_cnt)
-        shortlist16_body<S, L, CB, NW, QB, true, MODE>(cfrag, cseed, nblk, qfrag, nq, blk_per_split, nsplit, perm,
-                                                       out_key, out_idx);
+        shortlist16_body<S, L, CB, NW, QB, true, MODE, VAR>(cfrag, cseed, nblk, qfrag, nq, blk_per_split, nsplit, perm,
+                                                            out_key, out_idx);
     else
-        shortlist16_body<S, L, CB, NW, QB, false, MODE>(cfrag, cseed, nblk, qfrag, nq, blk_per_split, nsplit, perm,
-                                                        out_key, out_idx);
+        shortlist16_body<S, L, CB, NW, QB, false, MODE, VAR>(cfrag, cseed, nblk, qfrag, nq, blk_per_split, nsplit,
+                                                             perm, out_key, out_idx);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -924,6 +962,168 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(RescoreArgs a, int list_n
 }
 
 // ------------------------------------------------------------------------------------------
+// 4. small batches (the reference's per-tile calls: ann_kdtree_search per frame tile, main.pas:4027, coalesced by the
+// library into batches of a few queries): an exhaustive exact scan spread over the whole GPU.  Grid = candidate
+// splits; each workgroup scans its contiguous candidate range for ALL the batch's queries (staged in LDS), one
+// candidate per thread at a time, each query's fp32 distance summed in dimension order (the reference's sequential
+// sum), the K best per (thread, query) by (distance, tie order); then the workgroup's K best per query -> partials
+// [q][split][K].  nn_scan_merge_kernel picks the k best of each query's partials.  No MFMA, no tiers: the shortlist's
+// fixed costs (a 512-query workgroup per split, fragment prep, rescore) dominated a call of one query (0.6 ms).
+// ------------------------------------------------------------------------------------------
+static constexpr int SCAN_D_MAX = 256;
+template <int QN, int K>
+__global__ __launch_bounds__(256) void nn_scan_small_kernel(RescoreArgs a, int nsplit, float *__restrict__ pd,
+                                                            int *__restrict__ pi) {
+    __shared__ __attribute__((aligned(16))) float sq[QN * SCAN_D_MAX];
+    __shared__ float rd[4][K];
+    __shared__ int ri[4][K];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int qg = blockIdx.y * QN;  // this workgroup's group of queries
+    const int nq = min(a.nq - qg, QN), d = a.d;
+    for (int i = tid; i < nq * d; i += 256)
+        sq[(i / d) * SCAN_D_MAX + i % d] = a.q[(long)(qg + i / d) * d + i % d];
+    __syncthreads();
+    const long c0 = (long)a.n * blockIdx.x / nsplit, c1 = (long)a.n * (blockIdx.x + 1) / nsplit;
+    float bd[QN][K];
+    int bi[QN][K];
+#pragma unroll
+    for (int q = 0; q < QN; q++)
+#pragma unroll
+        for (int r = 0; r < K; r++) {
+            bd[q][r] = INFINITY;
+            bi[q][r] = 0x7fffffff;
+        }
+    for (long j = c0 + tid; j < c1; j += 256) {
+        const float *c = a.rows + j * d;
+        float dist[QN];
+#pragma unroll
+        for (int q = 0; q < QN; q++) dist[q] = 0.0f;
+        for (int d0 = 0; d0 < d; d0 += 4) {  // d % 4 == 0 (checked on the host)
+            const float4 cv = *reinterpret_cast<const float4 *>(c + d0);
+#pragma unroll
+            for (int q = 0; q < QN; q++) {
+                const float4 qv = *reinterpret_cast<const float4 *>(sq + q * SCAN_D_MAX + d0);
+                float t;
+                t = qv.x - cv.x; dist[q] = dist[q] + t * t;
+                t = qv.y - cv.y; dist[q] = dist[q] + t * t;
+                t = qv.z - cv.z; dist[q] = dist[q] + t * t;
+                t = qv.w - cv.w; dist[q] = dist[q] + t * t;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < QN; q++) {
+            if (q >= nq) break;
+            const float *qr = sq + q * SCAN_D_MAX;
+            if (!kd_less(a.ko, qr, dist[q], (int)j, bd[q][K - 1], bi[q][K - 1])) continue;
+            int p = K - 1;  // j ascends in this thread: insertion keeps (distance, tie order)
+            while (p > 0 && kd_less(a.ko, qr, dist[q], (int)j, bd[q][p - 1], bi[q][p - 1])) {
+                bd[q][p] = bd[q][p - 1];
+                bi[q][p] = bi[q][p - 1];
+                p--;
+            }
+            bd[q][p] = dist[q];
+            bi[q][p] = (int)j;
+        }
+    }
+    // per query: the workgroup's K best, K rounds of (distance, tie order) argmin over the threads' sorted lists
+    for (int q = 0; q < nq; q++) {
+        const float *qr = sq + q * SCAN_D_MAX;
+        int ptr = 0;
+        for (int r = 0; r < K; r++) {
+            float v = INFINITY;
+            int vi = 0x7fffffff;
+#pragma unroll
+            for (int x = 0; x < K; x++)
+                if (x == ptr) {
+                    v = bd[q][x];
+                    vi = bi[q][x];
+                }
+            float mv = v;
+            int mi = vi;
+            kd_argmin<64>(a.ko, qr, mv, mi);
+            if (lane == 0) {
+                rd[w][r] = mv;
+                ri[w][r] = mi;
+            }
+            if (vi == mi && mi != 0x7fffffff) ptr++;  // this wave's winner leaves its list
+        }
+        __syncthreads();
+        if (w == 0) {  // merge the 4 waves' sorted K-lists: lane l < 4 holds wave l's list head
+            int hp = 0;
+            for (int r = 0; r < K; r++) {
+                float v = INFINITY;
+                int vi = 0x7fffffff;
+                if (lane < 4 && hp < K) {
+                    v = rd[lane][hp];
+                    vi = ri[lane][hp];
+                }
+                float mv = v;
+                int mi = vi;
+                kd_argmin<64>(a.ko, qr, mv, mi);
+                if (lane < 4 && vi == mi && mi != 0x7fffffff) hp++;
+                if (lane == 0) {
+                    const long o = ((long)(qg + q) * nsplit + blockIdx.x) * K + r;
+                    pd[o] = mv;
+                    pi[o] = mi;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// one wave per query: the k best of its nsplit * K partials (each split's list sorted) -> out, tilemap item
+template <int K>
+__global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int nsplit, const float *__restrict__ pd,
+                                                           const int *__restrict__ pi) {
+    const int q = blockIdx.x, lane = threadIdx.x;
+    const float *qr = a.q + (long)q * a.d;
+    // each lane owns the splits lane, lane + 64, ...: its running K best of their entries
+    float bd[K];
+    int bi[K];
+#pragma unroll
+    for (int r = 0; r < K; r++) {
+        bd[r] = INFINITY;
+        bi[r] = 0x7fffffff;
+    }
+    for (int sp = lane; sp < nsplit; sp += 64)
+        for (int r = 0; r < K; r++) {
+            const float v = pd[((long)q * nsplit + sp) * K + r];
+            const int vi = pi[((long)q * nsplit + sp) * K + r];
+            if (vi == 0x7fffffff || !kd_less(a.ko, qr, v, vi, bd[K - 1], bi[K - 1])) break;  // the split's list is sorted
+            int p = K - 1;
+            while (p > 0 && kd_less(a.ko, qr, v, vi, bd[p - 1], bi[p - 1])) {
+                bd[p] = bd[p - 1];
+                bi[p] = bi[p - 1];
+                p--;
+            }
+            bd[p] = v;
+            bi[p] = vi;
+        }
+    int ptr = 0;
+    for (int r = 0; r < a.k; r++) {
+        float v = INFINITY;
+        int vi = 0x7fffffff;
+#pragma unroll
+        for (int x = 0; x < K; x++)
+            if (x == ptr) {
+                v = bd[x];
+                vi = bi[x];
+            }
+        float mv = v;
+        int mi = vi;
+        kd_argmin<64>(a.ko, qr, mv, mi);
+        if (vi == mi && mi != 0x7fffffff) ptr++;
+        if (lane == 0) {
+            const bool ok = mi != 0x7fffffff;
+            a.out_idx[(long)q * a.k + r] = ok ? mi : -1;
+            a.out_err[(long)q * a.k + r] = ok ? mv : FLT_MAX;
+            if (r == 0) write_map(a, q, ok ? mi : -1);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
 static int pick_S(int d) {
@@ -1146,6 +1346,17 @@ static int sl16_mode() {
 }
 #endif
 
+#ifdef TILER_EXPERIMENTS
+// TILER_SL16_VAR=1..3: variants of the 16x16x32 shortlist (shortlist16_body VAR), valid results
+static int sl16_var() {  // -1: unset (the shipped VAR)
+    static int v = [] {
+        const char *e = getenv("TILER_SL16_VAR");
+        return e ? atoi(e) : -1;
+    }();
+    return v;
+}
+#endif
+
 static int shortlist_variant() {
 #ifdef TILER_EXPERIMENTS
     static int v = [] {
@@ -1164,6 +1375,9 @@ static int shortlist_variant() {
 // returns L16, or 0 for the 32x32x16 kernels
 // QB = 4 query blocks per wave; 5 (252 VGPRs) measured the same at 388k candidates (r03h: 80.6-81.2 vs 80.9-81.1 ms)
 static constexpr int SL16_NW = 8, SL16_QB = 4, SL16_CB = 8;
+// shortlist16_body VAR of the shipped kernel: the per-query-block insertion gate (r04c/r04e: -2..-3 % shortlist time,
+// same digests; the 3-buffer ring, VAR 2, measured no gain)
+static constexpr int SL16_VAR = 1;
 static int shortlist16_L() {
     const int v = shortlist_variant();
     return v == 16 ? 4 : v == 166 ? 6 : 0;
@@ -1173,22 +1387,30 @@ template <int S, int L>
 static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     const int nqblk = (nq + 15) / 16;
     const dim3 grid((nqblk + SL16_NW * SL16_QB - 1) / (SL16_NW * SL16_QB), nsplit);
-    const size_t lds = 2 * (SL16_CB * S * 1024 + SL16_CB * 64);
+    const size_t buf = SL16_CB * S * 1024 + SL16_CB * 64;
+    auto go = [&](auto kern, int nbuf) {
+        hipLaunchKernelGGL(kern, grid, dim3(SL16_NW * 64), nbuf * buf, stream, (const half8 *)ix->d_frag16,
+                           ix->d_seed16, ix->nblk16, (const half8 *)ix->scratch.qfrag16, nq, bps, nsplit, ix->perm,
+                           ix->scratch.key, ix->scratch.idx, ix->flat_cnt);
+    };
     KTimer tm("nn_shortlist", stream);
 #ifdef TILER_EXPERIMENTS
     const int mode = sl16_mode();
+    const int var = sl16_var();
     if (mode) {
-        auto k = mode == 1 ? nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 1>
-                 : mode == 2 ? nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 2>
-                             : nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 3>;
-        hipLaunchKernelGGL(k, grid, dim3(SL16_NW * 64), lds, stream, (const half8 *)ix->d_frag16, ix->d_seed16,
-                           ix->nblk16, (const half8 *)ix->scratch.qfrag16, nq, bps, nsplit, ix->perm, ix->scratch.key,
-                           ix->scratch.idx, ix->flat_cnt);
+        if (mode == 1) go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 1>, 2);
+        else if (mode == 2) go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 2>, 2);
+        else go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 3>, 2);
+    } else if (var >= 0) {
+        switch (var) {
+            case 0: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 0>, 2); break;
+            case 1: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 1>, 2); break;
+            case 2: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 2>, 3); break;
+            default: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 3>, 3); break;
+        }
     } else
 #endif
-    hipLaunchKernelGGL((nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB>), grid, dim3(SL16_NW * 64), lds, stream,
-                       (const half8 *)ix->d_frag16, ix->d_seed16, ix->nblk16, (const half8 *)ix->scratch.qfrag16, nq,
-                       bps, nsplit, ix->perm, ix->scratch.key, ix->scratch.idx, ix->flat_cnt);
+    go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, SL16_VAR>, 2);
     TILER_HIP_CHECK(hipGetLastError());
     if (ix->flat_cnt) {  // flat_queries of the stats: derived from the device count when they are read
         ix->last_flat_dev = ix->flat_cnt;
@@ -1261,6 +1483,17 @@ static int launch_exact(RescoreArgs ra, int list_n, int grid, hipStream_t stream
 }
 
 static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream, const OrbitTail *orbit);
+
+// generic tier-2 slots of a search: whole chunks covering 1.5x the largest tier-2 count of the recent searches (this
+// index's last count, or the last one seen on any index: an encoder builds a new index per keyframe), >= 1 chunk
+static std::atomic<int> g_t2_recent{0};
+static int tier2_slots(NNIndex *ix, int nq) {
+    const int own = ix->h_fb_count ? ((volatile int *)ix->h_fb_count)[0] : 0;
+    const int prev = std::max(own < (1 << 30) ? own : 0, g_t2_recent.load(std::memory_order_relaxed));
+    const long want = (long)prev + prev / 2 + 1;
+    const long chunks = std::max(1L, (want + TIER2_MAX - 1) / TIER2_MAX);
+    return (int)std::min<long>(nq, chunks * TIER2_MAX);
+}
 static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream,
                        bool orbit_prepared);
 
@@ -1335,8 +1568,51 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     return 0;
 }
 
+// the small-batch path (nn_scan_small_kernel): groups of up to 16 queries (k = 1) or 4 (k <= 8) per workgroup row,
+// batches of up to SCAN_MAX1 / SCAN_MAX8 queries
+static constexpr int SCAN_QN1 = 16, SCAN_QN8 = 4;
+static std::atomic<int> g_scan_max1{64}, g_scan_max8{16};  // tiler_set_scan_limits
+void nn_set_scan_limits(int max_k1, int max_k8) {
+    g_scan_max1.store(std::max(0, max_k1));
+    g_scan_max8.store(std::max(0, max_k8));
+}
+static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t stream) {
+    const int nsplit = (int)std::max<long>(1, std::min<long>(1024, ((long)ix->n + 255) / 256));
+    const int K = k == 1 ? 1 : 8;
+    if (ensure_scratch(ix, nq, (long)nq * nsplit * K)) return -1;
+    SearchScratch &s = ix->scratch;
+    ix->last_splits = 0;
+    ix->last_fallback = 0;
+    TILER_HIP_CHECK(hipMemsetAsync(s.fb_count, 0, 16, stream));  // the stats' tier counts: none
+    KTimer tm("nn_scan", stream);
+    // the per-query work is unrolled over QN: the smallest instance that holds a group
+    const int qn = K == 1 ? (nq == 1 ? 1 : nq <= 4 ? 4 : SCAN_QN1) : (nq == 1 ? 1 : SCAN_QN8);
+    const dim3 grid(nsplit, (nq + qn - 1) / qn);
+    auto scan = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, ra, nsplit, s.key, s.idx);
+    };
+    if (K == 1) {
+        if (qn == 1) scan(nn_scan_small_kernel<1, 1>);
+        else if (qn == 4) scan(nn_scan_small_kernel<4, 1>);
+        else scan(nn_scan_small_kernel<SCAN_QN1, 1>);
+        hipLaunchKernelGGL(nn_scan_merge_kernel<1>, dim3(nq), dim3(64), 0, stream, ra, nsplit, (const float *)s.key,
+                           (const int *)s.idx);
+    } else {
+        if (qn == 1) scan(nn_scan_small_kernel<1, 8>);
+        else scan(nn_scan_small_kernel<SCAN_QN8, 8>);
+        hipLaunchKernelGGL(nn_scan_merge_kernel<8>, dim3(nq), dim3(64), 0, stream, ra, nsplit, (const float *)s.key,
+                           (const int *)s.idx);
+    }
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream,
                        bool orbit_prepared) {
+    if (ix->d <= SCAN_D_MAX && ix->d % 4 == 0 &&
+        ((k == 1 && nq <= g_scan_max1.load(std::memory_order_relaxed)) ||
+         (k <= 8 && nq <= g_scan_max8.load(std::memory_order_relaxed))))
+        return scan_small(ix, ra, nq, k, stream);
     const bool mfma = ix->S > 0 && k <= 8;
     if (!mfma) {
         ix->last_splits = 0;
@@ -1447,7 +1723,10 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     ra.ccnt = s.ccnt;
     ra.cbuf = s.cbuf;
     ra.cap = TIER2_CAP;
-    ra.fb_max = nq;  // every overflowed query gets a tier-2 slot; the collect runs in chunks of TIER2_MAX
+    // tier-2 slots: the collect runs in chunks of TIER2_MAX, as many as the recent tier-2 counts call for (each
+    // chunk costs two launches even when empty); an overflowed query beyond the slots goes to the exact tier 3, so
+    // the count only shapes the work, never the result
+    ra.fb_max = tier2_slots(ix, nq);
     TILER_HIP_CHECK(hipMemsetAsync(s.ccnt, 0, (size_t)std::min(nq, TIER2_MAX) * sizeof(int), stream));
     {
         KTimer t_rs("nn_rescore", stream);
@@ -1469,7 +1748,7 @@ static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t s
     if (orbit) {
         if (orbit_tier2(ix, ra.q, *orbit, nq, stream)) return -1;
     } else {
-        for (int jbase = 0; jbase < nq; jbase += TIER2_MAX) {
+        for (int jbase = 0; jbase < ra.fb_max; jbase += TIER2_MAX) {
             if (dispatch_collect(ix, nq, jbase, stream)) return -1;
             KTimer t_r2("nn_rescore2", stream);
             hipLaunchKernelGGL(nn_rescore2_kernel,
@@ -1480,6 +1759,10 @@ static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t s
     }
     if (launch_exact(ra, 0, std::min(nq, 1024), stream)) return -1;
     TILER_HIP_CHECK(hipMemcpyAsync(ix->h_fb_count, s.fb_count, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
+    if (!orbit) {  // the previous search's count on this index (already landed: the host waited for it)
+        const int c = ((volatile int *)ix->h_fb_count)[0];
+        if (c >= 0 && c < (1 << 30)) g_t2_recent.store(c, std::memory_order_relaxed);
+    }
     return 0;
 }
 

@@ -106,6 +106,9 @@ struct FtMaps {
 int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
                   hipStream_t stream, bool rootbox_ready = false, bool orbit_prepared = false);
 
+// batches of at most max_k1 queries (k = 1) / max_k8 (k <= 8) take the exhaustive small-batch scan; 0 disables it
+void nn_set_scan_limits(int max_k1, int max_k8);
+
 // frame tiling: RGB tiles -> descriptors (fp32) -> search -> tilemap items
 int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int *d_idx,
                         float *d_err, const FtMaps *maps, hipStream_t stream);

@@ -1647,13 +1647,20 @@ __global__ __launch_bounds__(256) void nn_orbit_t2_final_kernel(OrbitTail t, con
 
 int orbit_tier2(NNIndex *ix, const float *d_q, const OrbitTail &tail, int nq, hipStream_t stream) {
     OrbitIndex *o = ix->orbit;
-    // fixed grid, the tier-2 count stays on the device: many short candidate splits, and the x dimension strides
-    // over the query groups of 128, so 2 x 512 resident-sized workgroups serve 10 queries or all of them alike
+    // the tier-2 count stays on the device (no host round trip): many short candidate splits, and the x dimension
+    // strides over the query groups of 128, so any count is served.  x is sized from the count the previous search
+    // on this index left in the pinned h_fb_count (a heuristic only: a stale or racing value changes the grid, never
+    // the result): one group per workgroup column when the count repeats (C3: ~1k tier-2 queries -> 10 columns,
+    // 0.21 -> ~0.11 ms), 2 columns at least
+    const int prev = ix->h_fb_count ? std::max(0, (int)((volatile int *)ix->h_fb_count)[0]) : 0;
+    const int t2x_auto = std::max(2, std::min(64, (prev + prev / 4 + 127) / 128 + 1));
 #ifdef TILER_EXPERIMENTS
-    static const int t2x = getenv("TILER_T2_X") ? atoi(getenv("TILER_T2_X")) : 2;
+    static const int t2x_env = getenv("TILER_T2_X") ? atoi(getenv("TILER_T2_X")) : 0;
+    const int t2x = t2x_env > 0 ? t2x_env : t2x_auto;
     static const int t2s = getenv("TILER_T2_NSPLIT") ? atoi(getenv("TILER_T2_NSPLIT")) : 512;
 #else
-    constexpr int t2x = 2, t2s = 512;
+    const int t2x = t2x_auto;
+    constexpr int t2s = 512;
 #endif
     const int nsplit = std::min(o->gblk, t2s);
     const int bps = (o->gblk + nsplit - 1) / nsplit;

@@ -27,6 +27,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+KM_VALU_PER_PAIR = 61  # kmb_assign16's VALU instructions per (point, centroid) pair (ISA count, DESIGN.md K-Modes)
+
 
 def parser():
     ap = argparse.ArgumentParser()
@@ -110,6 +112,20 @@ def run(args) -> dict:
         n = ctypes.c_int(0)
         ms = lib.tiler_timing_get(name.encode(), ctypes.byref(n))
         phases[name] = {"ms_total": round(ms, 2), "launches": n.value}
+    pairs, steps = ctypes.c_int64(0), ctypes.c_int64(0)
+    check(lib.tiler_kmodes_last_stats(ctypes.byref(pairs), ctypes.byref(steps)), "tiler_kmodes_last_stats")
+    # roofline of the assignment: the (point, centroid) dissimilarities it evaluates per second over
+    # its busy time (HIP events), against the VALU-issue bound of its kernel: kmb_assign16 spends 61 VALU
+    # instructions per pair (ISA count, DESIGN.md K-Modes), one wave64 VALU instruction per 2 cycles per SIMD
+    asg_s = phases["kmodes_assign"]["ms_total"] * 1e-3
+    valu_bound = 1024 * 2.4e9 / 2 * 64 / KM_VALU_PER_PAIR
+    roofline = {"bound": "valu", "kernel": "kmb_assign16", "unit": "pairs/s", "pairs": int(pairs.value),
+                "chunk_steps": int(steps.value), "busy_ms": phases["kmodes_assign"]["ms_total"],
+                "achieved": round(pairs.value / asg_s, 1) if asg_s else None, "peak": valu_bound,
+                "frac": round(pairs.value / asg_s / valu_bound, 4) if asg_s else None,
+                "note": f"peak = 1,024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction x 64 lanes / "
+                        f"{KM_VALU_PER_PAIR} instructions per pair; the launches' busy time from HIP event pairs "
+                        f"(one run with the timers on)"}
     labels = d_lab.cpu().numpy()
     cent = d_cent.cpu().numpy()
     t2 = time.perf_counter()
@@ -169,6 +185,7 @@ def run(args) -> dict:
                    "largest_bin": int(np.diff(off).max()), "largest_k": int(ks.max())},
         "kmodes_s": round(t_km, 3), "medoids_s": round(t_med, 3), "host_prep_s": round(host_prep, 2),
         "iterations": {"max": int(iters.max()), "mean": round(float(iters.mean()), 2)}, "phases": phases,
+        "roofline": roofline,
         "digest": "%08x" % zlib.crc32(cent.tobytes(), zlib.crc32(labels.tobytes())),  # A/B runs: same bins
         "cpu_baseline": cpu,
     }

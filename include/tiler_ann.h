@@ -201,6 +201,13 @@ int tiler_kmodes_batch(const uint8_t *X, const int32_t *bin_off, int nbins, cons
 int tiler_kmodes_batch_dev(const uint8_t *d_X, const int32_t *bin_off, int nbins, const int32_t *k,
                            const int32_t *start, int n_modalities, int32_t *d_labels, uint8_t *d_centroids,
                            int32_t *n_iter, uint64_t *cost, void *stream);
+/* Work counters of the last tiler_kmodes_batch[_dev] call (process-wide): the (point, centroid) dissimilarities its
+ * assignment launches evaluated (the initial assignment + every chunk step's), and its dependent chunk steps. */
+int tiler_kmodes_last_stats(int64_t *assign_pairs, int64_t *chunk_steps);
+/* Test hook (process-wide): on != 0 makes the persistent farthest-first launch give up at its first grid barrier,
+ * as a barrier that times out on a contended GPU would, so every batch takes the recovery path (state re-initialised,
+ * the rounds re-run one launch each).  Results are identical either way.  0. */
+int tiler_debug_kmodes_ff_fallback(int on);
 /* Medoids of every bin's clusters (as tiler_kmodes_medoids per bin): medoid[sum k] bin-local rows. */
 int tiler_kmodes_medoids_batch(const uint8_t *X, const int32_t *bin_off, int nbins, const int32_t *k,
                                const int32_t *labels, const uint8_t *centroids, int32_t *medoid, int32_t *counts);

@@ -33,6 +33,40 @@ def test_kmodes_bit_exact(gpu, oracle, n, k, protos, noise):
     assert np.array_equal(gl, ol) and np.array_equal(gc, oc)
 
 
+def test_kmodes_batch_ff_fallback_bit_exact(gpu, oracle):
+    """the recovery path of the persistent farthest-first (a grid barrier that gives up sets the fail word,
+    every workgroup leaves, the host re-initialises the state and re-runs the rounds one launch each), forced through
+    tiler_debug_kmodes_ff_fallback: a batch of bins must give the restatement's labels, centroids, iterations and cost,
+    and the same outputs as the persistent path."""
+    from tiler_amd.kmodes import compute_kmodes_batch
+    rng = np.random.default_rng(77)
+    sizes, ks = [2500, 1800, 900, 400], [120, 95, 40, 17]
+    X = np.concatenate([_dataset(rng, n, 150, 0.12) for n in sizes])
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    k = np.array(ks, np.int32)
+    starts = np.array([int(np.argmin(X[off[b]:off[b + 1]].astype(np.int64).sum(1))) for b in range(len(sizes))], np.int32)
+    import ctypes
+    lib = gpu.load()
+    assert lib.tiler_debug_kmodes_ff_fallback(1) == 0
+    lib.tiler_timing_reset()
+    lib.tiler_timing_enable(1)
+    try:
+        fl, fc, fi, fcost = compute_kmodes_batch(X, off, k, starts)
+    finally:
+        lib.tiler_debug_kmodes_ff_fallback(0)
+        lib.tiler_timing_enable(0)
+    n_init = ctypes.c_int(0)
+    lib.tiler_timing_get(b"kmodes_init", ctypes.byref(n_init))
+    assert n_init.value == 2  # the persistent launch, then the recovery's per-launch rounds
+    pl, pc, pi, pcost = compute_kmodes_batch(X, off, k, starts)
+    assert np.array_equal(fl, pl) and np.array_equal(fc, pc) and np.array_equal(fi, pi) and np.array_equal(fcost, pcost)
+    koff = np.concatenate([[0], np.cumsum(ks)])
+    for b in range(len(sizes)):
+        ol, oc, oi, ocost = oracle.kmodes(X[off[b]:off[b + 1]], ks[b], int(starts[b]))
+        assert (int(fi[b]), int(fcost[b])) == (oi, ocost), b
+        assert np.array_equal(fl[off[b]:off[b + 1]], ol) and np.array_equal(fc[koff[b]:koff[b + 1]], oc), b
+
+
 @pytest.mark.parametrize("modalities,vmax", [(64, 64), (200, 200), (8, 8)])
 def test_kmodes_other_modalities(gpu, oracle, modalities, vmax):
     """Byte values beyond 15 (64 / 200 modalities) run the general assignment (kmb_assign: the asm's int8 |r - x|

@@ -975,6 +975,19 @@ int tiler_kmodes_batch_dev(const uint8_t *d_X, const int32_t *bin_off, int nbins
                             (hipStream_t)stream);
 }
 
+int tiler_debug_kmodes_ff_fallback(int on) {
+    kmodes_force_ff_fallback(on);
+    return 0;
+}
+
+int tiler_kmodes_last_stats(int64_t *assign_pairs, int64_t *chunk_steps) {
+    long long p = 0, c = 0;
+    kmodes_last_stats(&p, &c);
+    if (assign_pairs) *assign_pairs = p;
+    if (chunk_steps) *chunk_steps = c;
+    return 0;
+}
+
 int tiler_kmodes_medoids_batch(const uint8_t *X, const int32_t *bin_off, int nbins, const int32_t *k,
                                const int32_t *labels, const uint8_t *centroids, int32_t *medoid, int32_t *counts) {
     if (!ensure_init()) return -1;

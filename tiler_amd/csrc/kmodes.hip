@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -1136,69 +1137,6 @@ __device__ __forceinline__ unsigned long long km_block_max(unsigned long long v,
     return m;
 }
 
-__global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist(KmBatch B, const KmFfItem *items, const int *ff_end,
-                                                           int Kmax, unsigned *bar, unsigned *fail) {
-    __shared__ unsigned long long red[KM_FF_NT / 64];
-    __shared__ int last;
-    int alive = B.nb;
-    for (int j = 0; j < Kmax; j++) {
-        while (alive > 0 && B.koff[alive] - B.koff[alive - 1] <= j) alive--;
-        const int nit = ff_end[alive];
-        for (int u = blockIdx.x; u < nit; u += gridDim.x) {
-            const KmFfItem it = items[u];
-            KmState s = bin_state(B, it.bin);
-            const int c = __hip_atomic_load(s.center + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t item[20];
-            load_row(s.X + (long)c * KM_A, item);
-            unsigned long long bv = 0;
-            int bi = -1;
-            for (long i = (long)it.sub * KM_FF_NT + threadIdx.x; i < s.n; i += (long)it.nsub * KM_FF_NT) {
-                uint32_t row[20];
-                load_row(s.X + i * KM_A, row);
-                const unsigned long long d = km_dissim(row, item);
-                unsigned long long m = s.mind[i];
-                if (d < m) {  // cmovb: strict-less (kmodes.pas:555-558)
-                    m = d;
-                    s.mind[i] = m;
-                }
-                const bool used = __hip_atomic_load(s.used + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-                if (!used && m >= bv) {  // ascending i within a thread: '>=' keeps the last
-                    bv = m;
-                    bi = (int)i;
-                }
-            }
-            const unsigned long long v32 = bv > 0xFFFFFFFFull ? 0xFFFFFFFFull : bv;
-            const unsigned long long best = km_block_max(bi < 0 ? 0ull : ((v32 << 32) | (unsigned)(bi + 1)), red);
-            if (j + 1 >= s.K) continue;  // the bin's last round: no selection (uniform)
-            if (threadIdx.x == 0) {
-                __hip_atomic_store(s.part + it.sub, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the candidate has left before the count
-                last = __hip_atomic_fetch_add(B.ffdone + it.bin, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                       it.nsub - 1;
-            }
-            __syncthreads();
-            if (!last) continue;  // uniform
-            unsigned long long bb = 0;
-            for (int i = threadIdx.x; i < it.nsub; i += KM_FF_NT)
-                bb = max(bb, __hip_atomic_load(&s.part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            const unsigned long long w = km_block_max(bb, red);
-            const int f = (w == 0) ? -1 : (int)(w & 0xFFFFFFFFull) - 1;
-            if (threadIdx.x == 0) __hip_atomic_store(&B.ffdone[it.bin], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (f < 0) {
-                if (threadIdx.x == 0) *s.err = 1;
-                continue;
-            }
-            // the centre's row for the later kernels (nothing in this launch reads it: items read X[center])
-            if (threadIdx.x < KM_A) s.cent[(long)(j + 1) * KM_A + threadIdx.x] = s.X[(long)f * KM_A + threadIdx.x];
-            if (threadIdx.x == 0) {
-                __hip_atomic_store(s.center + j + 1, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(s.used + f, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if (j + 1 < Kmax && !km_grid_sync(bar, (unsigned)(j + 1), fail)) return;
-    }
-}
-
 // Farthest-first with the selection after the barrier (round 3, r03zo): every item of round j stores its candidate
 // (sc1) into the round's parity half of the part slots and arrives; after the barrier EVERY item of a bin reduces
 // that bin's candidates itself (the same partition-independent maximum, so the same centre) instead of the last item
@@ -1267,7 +1205,7 @@ __global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist2(KmBatch B, const KmF
     }
 }
 
-// resident workgroups for kmb_ff_persist: one per CU (0: not placeable -> per-launch rounds)
+// resident workgroups for kmb_ff_persist2: one per CU (0: not placeable -> per-launch rounds)
 static int ff_persist_grid() {
     static const int g = [] {
         int dev = 0, ncu = 0, per = 0;
@@ -1303,6 +1241,15 @@ __global__ __launch_bounds__(256) void kmb_medoid(const uint8_t *X, const int32_
 // centroid splits of an assignment block: ~64 centroids per block, so a chunk of the largest bin alone
 // still spreads over the chip (results merge by atomicMin)
 static int csplit_of(int K) { return std::max(1, std::min(128, (K + 63) / 64)); }
+
+// counters of the last batch (tiler_kmodes_last_stats): assignment (point, centroid) pairs and dependent chunk steps
+static std::atomic<long long> g_km_last_pairs{0}, g_km_last_steps{0};
+static std::atomic<int> g_km_force_ff_fail{0};  // tiler_debug_kmodes_ff_fallback
+void kmodes_force_ff_fallback(int on) { g_km_force_ff_fail.store(on != 0); }
+void kmodes_last_stats(long long *pairs, long long *steps) {
+    if (pairs) *pairs = g_km_last_pairs.load();
+    if (steps) *steps = g_km_last_steps.load();
+}
 
 int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const int32_t *h_k, const int32_t *h_start,
                      int n_modalities, int32_t *d_labels, uint8_t *d_centroids, int32_t *h_iter, uint64_t *h_cost,
@@ -1341,6 +1288,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     }
     const long N = boff[nb], Ktot = koff[nb];
     const int M = n_modalities;
+    long long km_pairs = 0, km_steps = 0;  // tiler_kmodes_last_stats
     // device workspace
     size_t off = 0;
     auto carve = [&](size_t bytes) {
@@ -1359,9 +1307,6 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     // assignment with <= 16 modalities (kmb_assign16): prepared point rows, at most 8,192 centroids per workgroup
     bool use16 = M <= 16;
     for (int r = 0; r < nb; r++) use16 = use16 && (Kv[r] + csplit_of(Kv[r]) - 1) / csplit_of(Kv[r]) <= 8192;
-#ifdef TILER_EXPERIMENTS
-    if (getenv("TILER_KM_A16") && atoi(getenv("TILER_KM_A16")) == 0) use16 = false;  // A/B: the general kernel
-#endif
     const size_t o_Xp = carve(use16 ? (size_t)N * KM_PW * 4 : 0), o_items = carve(0);
     char *buf = nullptr;
     // the largest work list: one iteration's chunk items for every bin
@@ -1373,14 +1318,8 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     }
     const size_t item_bytes = (max_items + (size_t)poff[nb] + 64) * sizeof(KmAsgItem) +
                               (size_t)(nb + 1) * 4 + 256;
-    // farthest-first: one persistent launch for every round (kmb_ff_persist2) unless it cannot be placed;
-    // TILER_KM_FF=0 (experiment build) selects the per-launch rounds for A/B, TILER_KM_FF=1 the r03k persistent form
-#ifdef TILER_EXPERIMENTS
-    static const bool ff_launches = getenv("TILER_KM_FF") && atoi(getenv("TILER_KM_FF")) == 0;
-#else
-    constexpr bool ff_launches = false;
-#endif
-    const int g_ff = ff_launches ? 0 : ff_persist_grid();
+    // farthest-first: one persistent launch for every round (kmb_ff_persist2) unless it cannot be placed
+    const int g_ff = ff_persist_grid();
     TILER_HIP_CHECK(hipMalloc((void **)&buf, off + item_bytes));
     char *items = buf + o_items;
     KmBatch B;
@@ -1474,15 +1413,11 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
             if (g_ff > 0) {
                 unsigned *bar = (unsigned *)(buf + o_bar), *ffail = bar + 544;
                 if (hipMemsetAsync(bar, 0, 2304, st) != hipSuccess) goto fail;  // counters, generations, fail word
+                if (g_km_force_ff_fail.load() &&  // test hook: every barrier gives up at once (round 0 runs)
+                    hipMemsetAsync(ffail, 0x01, 1, st) != hipSuccess)
+                    goto fail;
                 {
                     KTimer tm("kmodes_init", st);
-#ifdef TILER_EXPERIMENTS
-                    static const bool ff1 = getenv("TILER_KM_FF") && atoi(getenv("TILER_KM_FF")) == 1;
-                    if (ff1)  // A/B: the last item of a bin selects and publishes the centre (r03k-r03zn)
-                        hipLaunchKernelGGL(kmb_ff_persist, dim3(g_ff), dim3(KM_FF_NT), 0, st, B, (const KmFfItem *)items,
-                                           (const int *)(items + fb), Kv[0], bar, ffail);
-                    else
-#endif
                     // every item selects the centre after the barrier (r03zo: C4 122 -> 102 ms)
                     hipLaunchKernelGGL(kmb_ff_persist2, dim3(g_ff), dim3(KM_FF_NT), 0, st, B, (const KmFfItem *)items,
                                        (const int *)(items + fb), Kv[0], bar, ffail);
@@ -1514,6 +1449,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     for (int c = 0; c < cs; c++)
                         as.push_back({r, p0, std::min(nv[r], p0 + 256), c * per, std::min(Kv[r], (c + 1) * per), {0, 0, 0}});
             }
+            for (const KmAsgItem &it : as) km_pairs += (long long)(it.p1 - it.p0) * (it.c1 - it.c0);
             if (hipMemsetAsync(B.akey, 0xff, (size_t)N * 8, st) != hipSuccess) goto fail;
             if (upload(as.data(), as.size() * sizeof(KmAsgItem))) goto fail;
             KTimer tm("kmodes_assign", st);
@@ -1564,6 +1500,15 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     }
                     steps.push_back({na, ns});
                 }
+                {
+                    size_t q = 0;
+                    for (const auto &sp : steps) {  // (point, centroid) pairs the assignment launches evaluate
+                        for (int i = 0; i < sp.first; i++, q++)
+                            km_pairs += (long long)(wl[q].p1 - wl[q].p0) * (wl[q].c1 - wl[q].c0);
+                        q += sp.second;
+                        km_steps++;
+                    }
+                }
                 {  // the work list, then the active bins (one reset launch, not three memsets per bin)
                     const size_t wb = wl.size() * sizeof(KmAsgItem);
                     hitems.resize(wb + active.size() * 4);
@@ -1583,25 +1528,6 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     for (const auto &sp : steps) {
                         {
                             KTimer tm("kmodes_assign", st);
-#ifdef TILER_EXPERIMENTS
-                            static const int asub = getenv("TILER_KM_ASUB") ? atoi(getenv("TILER_KM_ASUB")) : KM_ASUB;
-                            static const int a16g = getenv("TILER_KM_A16G") ? atoi(getenv("TILER_KM_A16G")) : KM_A16_G;
-                            static const bool a16pf = getenv("TILER_KM_A16PF") && atoi(getenv("TILER_KM_A16PF")) == 1;
-                            if (use16 && a16pf)  // A/B: LDS row of the next centroid prefetched
-                                hipLaunchKernelGGL((kmb_assign16<1, true>), dim3(sp.first, asub), dim3(256), 0, st, B,
-                                                   (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
-                            else if (use16 && (asub != KM_ASUB || a16g != KM_A16_G)) {  // A/B: slices per item, groups per workgroup
-                                if (a16g == 2)
-                                    hipLaunchKernelGGL(kmb_assign16<2>, dim3(sp.first, asub / 2), dim3(512), 0, st, B,
-                                                       (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
-                                else if (a16g == 4)
-                                    hipLaunchKernelGGL(kmb_assign16<4>, dim3(sp.first, asub / 4), dim3(1024), 0, st, B,
-                                                       (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
-                                else
-                                    hipLaunchKernelGGL(kmb_assign16<1>, dim3(sp.first, asub), dim3(256), 0, st, B,
-                                                       (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
-                            } else
-#endif
                             if (use16)
                                 hipLaunchKernelGGL(kmb_assign16<KM_A16_G>, dim3(sp.first, KM_ASUB / KM_A16_G), dim3(256 * KM_A16_G), 0, st, B,
                                                    (const KmAsgItem *)items + pos, (const uint4 *)(buf + o_Xp));
@@ -1613,50 +1539,12 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                         // seq items are KmSeqItem views of KmAsgItem slots: stride 32 bytes
                         {
                             KTimer tm("kmodes_seq", st);
-#ifdef TILER_EXPERIMENTS
-                            static const bool w80 = getenv("TILER_KM_SEQ_W") && atoi(getenv("TILER_KM_SEQ_W")) == 80;
-                            static const bool oldseq = getenv("TILER_KM_APPLY") && atoi(getenv("TILER_KM_APPLY")) == 0;
-                            if (w80)  // A/B: round 2's 80 lanes per move (6 moves at a time), applied in place
-                                hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, 80>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
-                                                   st, B, (const KmAsgItem *)items + pos);
-                            else if (oldseq)  // A/B: decided and applied by one workgroup per bin
-                                hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, KM_SEQ_W>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
-                                                   st, B, (const KmAsgItem *)items + pos);
-                            else if (getenv("TILER_KM_DNT") && atoi(getenv("TILER_KM_DNT")) == 1024)  // A/B: 16 waves, 51-candidate window
-                                hipLaunchKernelGGL((kmb_seq_strided<1024, 20, true>), dim3(sp.second), dim3(1024), 0,
-                                                   st, B, (const KmAsgItem *)items + pos);
-                            else if (getenv("TILER_KM_DNT") && atoi(getenv("TILER_KM_DNT")) == 256)  // A/B: 4 waves, same window
-                                hipLaunchKernelGGL((kmb_seq_strided<256, 8, true>), dim3(sp.second), dim3(256), 0,
-                                                   st, B, (const KmAsgItem *)items + pos);
-                            else if (getenv("TILER_KM_DW") && atoi(getenv("TILER_KM_DW")) == 8)  // A/B: 64-candidate window
-                                hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, 8, true>), dim3(sp.second), dim3(KM_SEQ_NT), 0,
-                                                   st, B, (const KmAsgItem *)items + pos);
-                            else
-#endif
-                                // the decisions (one workgroup per bin), then the attribute updates over KM_APPLY_SLICES each
-                                hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, KM_SEQ_W, true>), dim3(sp.second),
-                                                   dim3(KM_SEQ_NT), 0, st, B, (const KmAsgItem *)items + pos);
+                            // the decisions (one workgroup per bin), then the attribute updates over KM_APPLY_SLICES each
+                            hipLaunchKernelGGL((kmb_seq_strided<KM_SEQ_NT, KM_SEQ_W, true>), dim3(sp.second),
+                                               dim3(KM_SEQ_NT), 0, st, B, (const KmAsgItem *)items + pos);
                         }
-#ifdef TILER_EXPERIMENTS
-                        if (!(getenv("TILER_KM_SEQ_W") && atoi(getenv("TILER_KM_SEQ_W")) == 80) &&
-                            !(getenv("TILER_KM_APPLY") && atoi(getenv("TILER_KM_APPLY")) == 0))
-#endif
                         {
                             KTimer tm("kmodes_apply", st);
-#ifdef TILER_EXPERIMENTS
-                            static const int sl = getenv("TILER_KM_SLICES") ? atoi(getenv("TILER_KM_SLICES")) : KM_APPLY_SLICES;
-#define KM_APPLY_AB(NS)                                                                                              \
-    hipLaunchKernelGGL((kmb_seq_apply<NS>), dim3(sp.second, NS), dim3(32 * (KM_A / NS)), 0, st, B,                  \
-                       (const KmAsgItem *)items + pos)
-                            if (sl == 5)
-                                KM_APPLY_AB(5);
-                            else if (sl == 20)
-                                KM_APPLY_AB(20);
-                            else if (sl == 40)
-                                KM_APPLY_AB(40);
-                            else
-#undef KM_APPLY_AB
-#endif
                             hipLaunchKernelGGL((kmb_seq_apply<KM_APPLY_SLICES>), dim3(sp.second, KM_APPLY_SLICES),
                                                dim3(32 * (KM_A / KM_APPLY_SLICES)), 0, st, B, (const KmAsgItem *)items + pos);
                         }
@@ -1719,6 +1607,8 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                 goto fail;
         }
         if (hipStreamSynchronize(st) != hipSuccess) goto fail;
+        g_km_last_pairs.store(km_pairs);
+        g_km_last_steps.store(km_steps);
         rc = 0;
     } while (0);
 fail:

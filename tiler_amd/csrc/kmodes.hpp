@@ -17,6 +17,10 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                      hipStream_t st);
 int kmodes_batch_host(const uint8_t *X, const int32_t *boff, int nb, const int32_t *k, const int32_t *start,
                       int n_modalities, int32_t *labels, uint8_t *centroids, int32_t *n_iter, uint64_t *cost);
+// the last batch's assignment (point, centroid) pairs and its dependent chunk steps
+void kmodes_last_stats(long long *pairs, long long *steps);
+// test hook: the persistent farthest-first's barriers give up at once, so the host's recovery path runs
+void kmodes_force_ff_fallback(int on);
 int kmodes_medoids_batch_host(const uint8_t *X, const int32_t *boff, int nb, const int32_t *k, const int32_t *labels,
                               const uint8_t *centroids, int32_t *medoid, int32_t *counts);
 }  // namespace tiler

@@ -1654,14 +1654,8 @@ int orbit_tier2(NNIndex *ix, const float *d_q, const OrbitTail &tail, int nq, hi
     // 0.21 -> ~0.11 ms), 2 columns at least
     const int prev = ix->h_fb_count ? std::max(0, (int)((volatile int *)ix->h_fb_count)[0]) : 0;
     const int t2x_auto = std::max(2, std::min(64, (prev + prev / 4 + 127) / 128 + 1));
-#ifdef TILER_EXPERIMENTS
-    static const int t2x_env = getenv("TILER_T2_X") ? atoi(getenv("TILER_T2_X")) : 0;
-    const int t2x = t2x_env > 0 ? t2x_env : t2x_auto;
-    static const int t2s = getenv("TILER_T2_NSPLIT") ? atoi(getenv("TILER_T2_NSPLIT")) : 512;
-#else
     const int t2x = t2x_auto;
     constexpr int t2s = 512;
-#endif
     const int nsplit = std::min(o->gblk, t2s);
     const int bps = (o->gblk + nsplit - 1) / nsplit;
     OrbitCollectArgs ca;
@@ -1717,142 +1711,6 @@ struct FtQueryArgs {
     const int *perm;     // query i reads tile perm[i] (null: tile i)
 };
 
-template <bool FASTDIV>
-__global__ __launch_bounds__(64) void orbit_ft_query_kernel(FtQueryArgs a) {
-    __shared__ double lut[256];
-    __shared__ float st[64 * 65];  // one component of the 64 tiles: row-major per lane, stride 65 (conflict-free)
-    __shared__ float sbox[2 * OD];
-    const int lane = threadIdx.x;
-    const double *__restrict__ glut = a.gamma_lut + 256 * (a.gamma + 1);
-    for (int i = lane; i < 256; i += 64) lut[i] = glut[i];
-    if (a.box)
-        for (int i = lane; i < 2 * OD; i += 64) sbox[i] = a.box[i];
-    __syncthreads();
-    const long t0 = (long)blockIdx.x * 64;
-    const long i = t0 + lane;
-    const bool valid = i < a.n;
-    const long nqblk = (a.n + 31) / 32;
-    const bool has_blk = (i >> 5) < nqblk;
-    const long ti = valid ? (a.perm ? (long)a.perm[i] : i) : (a.perm ? (long)a.perm[t0] : t0);
-    const int4 *src = reinterpret_cast<const int4 *>(a.rgb + ti * 64);
-    double n2 = 0, h2q[4] = {0, 0, 0, 0}, e2q[4] = {0, 0, 0, 0};
-    int bad = 0;
-    float rb = 0.0f;
-    const float *row = st + lane * 65;
-#pragma unroll 1
-    for (int c = 0; c < 3; c++) {
-        double p[64];
-#pragma unroll
-        for (int k4 = 0; k4 < 16; k4++) {
-            const int4 v = src[k4];
-            const int cc[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int r = cc[e] & 0xff, g = (cc[e] >> 8) & 0xff, b = (cc[e] >> 16) & 0xff;
-                // gamma -1: r / 255.0 in registers (no LDS gather: bank conflicts on random bytes); else the LUT
-                const double fr = FASTDIV ? div255(r) : lut[r], fg = FASTDIV ? div255(g) : lut[g],
-                             fb = FASTDIV ? div255(b) : lut[b];
-                const double cy = div10000<FASTDIV>(2126.0 * fr + 7152.0 * fg + 722.0 * fb);
-                p[4 * k4 + e] = c == 0 ? cy : c == 1 ? (fb - cy) * a.u_mul : (fr - cy) * a.v_mul;
-            }
-        }
-#ifdef TILER_EXPERIMENTS
-        if (a.xmode != 1)
-#endif
-            haar_regs(p, a.haar_f);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 64; k++) st[lane * 65 + k] = (float)p[k];
-        if (a.box) {
-#pragma unroll 4
-            for (int k = 0; k < 64; k++) {  // annBoxDistance, dimension order
-                const float v = row[k];
-                const float lo = sbox[c * 64 + k], hi = sbox[OD + c * 64 + k];
-                const float t = fmaxf(lo - v, 0.0f) + fmaxf(v - hi, 0.0f);  // lo <= hi: one term at most; + 0 exact
-                rb = rb + t * t;
-            }
-        }
-        __syncthreads();
-        // fp32 rows: 16 lanes per tile store its 256-byte component segment
-#pragma unroll
-        for (int t = 0; t < 16; t++) {
-            const int pc = lane + 64 * t, tt = pc >> 4, c4 = pc & 15;
-            if (t0 + tt < a.n) {
-                const float *q = st + tt * 65 + c4 * 4;
-                reinterpret_cast<float4 *>(a.out32 + (t0 + tt) * OD + c * 64)[c4] = make_float4(q[0], q[1], q[2], q[3]);
-            }
-        }
-        if (valid) {
-#pragma unroll 8
-            for (int k = 0; k < 64; k++) {
-                const double orig = (double)row[k] * (double)a.scale;
-                n2 += orig * orig;
-            }
-        }
-        // orbit transform of this component: k-steps s = 3x + c, 16 outputs each (orbit_prep_kernel's math).  The
-        // tables are the same for every component up to the 64c shift (tools/gen_orbit_map.py asserts it), so
-        // with x and j unrolled every term is an LDS read at an immediate offset of the lane's staged row.
-#ifdef TILER_EXPERIMENTS
-        if (a.xmode == 2) continue;
-#endif
-#pragma unroll 1
-        for (int x = 0; x < 4; x++) {
-            const int s = 3 * x + c;
-            half8 hv[2];
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                // the output's packed table word (one scalar load per block of 16): sources, signs, count.  All
-                // four terms are read unconditionally and absent ones add +0 (v is never -0: exact), so the 64
-                // LDS reads of a block have no control dependence and issue back to back.
-                const unsigned w = orbitgen::PACK[x * 16 + j];
-                const int cnt = (int)(w >> 28);
-                double v = 0.0;
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    const double r = (double)row[(w >> (6 * t)) & 63];
-                    const double sr = ((w >> (24 + t)) & 1) ? -r : r;
-                    v = v + (t < cnt ? sr : 0.0);
-                }
-                v = valid ? v * ((cnt == 1 ? 1.0 : 0.5) * (double)a.scale) : 0.0;
-                _Float16 vh = (_Float16)(float)v;
-                if (fabs((double)(float)vh) < 6.103515625e-05) vh = (_Float16)0.0f;  // no fp16 subnormal operands
-                hv[j >> 3][j & 7] = vh;
-                const double dh = (double)(float)vh;
-#ifdef TILER_EXPERIMENTS
-                if (a.xmode != 3) {
-#endif
-                h2q[j & 3] += dh * dh;  // four partial sums per norm: bound inputs, any order is rigorous
-                e2q[j & 3] += (v - dh) * (v - dh);
-                if (!isfinite(v) || fabs(v) > 65000.0) bad = 1;
-#ifdef TILER_EXPERIMENTS
-                }
-#endif
-                if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // 4 outputs in flight at most
-            }
-#ifdef TILER_EXPERIMENTS
-            if (has_blk && a.xmode != 5) {
-#else
-            if (has_blk) {
-#endif
-                half8 *f = a.frag + ((i >> 5) * OS + s) * 64 + (i & 31);
-                f[0] = hv[0];
-                f[32] = hv[1];
-            }
-            __builtin_amdgcn_sched_barrier(0);  // one block of 16 outputs at a time (bounded live range)
-        }
-    }
-    const double h2 = (h2q[0] + h2q[1]) + (h2q[2] + h2q[3]), e2 = (e2q[0] + e2q[1]) + (e2q[2] + e2q[3]);
-    if (valid) {
-        OrbitStat q;
-        q.n2 = n2;
-        q.hn = sqrt(h2);
-        q.en = sqrt(e2);
-        q.flags = (bad || !isfinite(n2)) ? 2 : 0;
-        q.pad = 0;
-        a.qstat[i] = q;
-        if (a.rootbox) a.rootbox[i] = rb;
-    }
-}
 
 // The same pass with TWO waves per 64-tile block: wave h holds input rows 4h..4h+3 of every tile (32 fp64 values per
 // lane instead of 64, so the block keeps about half the registers and twice the waves per SIMD hide the loads).
@@ -2119,29 +1977,9 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
 #endif
     const dim3 grid((unsigned)((Q + 63) / 64));
     KTimer tm("psyv", stream);
-#ifdef TILER_EXPERIMENTS
-    if (getenv("TILER_FTQ_ONEWAVE")) {  // A/B: the one-wave-per-block kernel
-        if (gamma == -1)
-            hipLaunchKernelGGL(orbit_ft_query_kernel<true>, grid, dim3(64), 0, stream, fa);
-        else
-            hipLaunchKernelGGL(orbit_ft_query_kernel<false>, grid, dim3(64), 0, stream, fa);
-        TILER_HIP_CHECK(hipGetLastError());
-        return 0;
-    }
-#endif
-#ifdef TILER_EXPERIMENTS
-    [[maybe_unused]] static const int nt = getenv("TILER_FTQ_NT") ? atoi(getenv("TILER_FTQ_NT")) : 1;  // A/B: 0 plain, 1 nt, 2 sc1
-#else
-    [[maybe_unused]] constexpr int nt = 1;
-#endif
+    // output stores non-temporal (template 1; r03g: plain 0.426 ms, nt 0.396-0.399, sc1 0.414 at C3)
     if (gamma != -1)
         hipLaunchKernelGGL((orbit_ft_query2_kernel<false, 1>), grid, dim3(128), 0, stream, fa);
-#ifdef TILER_EXPERIMENTS
-    else if (nt == 0)
-        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 0>), grid, dim3(128), 0, stream, fa);
-    else if (nt == 2)
-        hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 2>), grid, dim3(128), 0, stream, fa);
-#endif
     else
         hipLaunchKernelGGL((orbit_ft_query2_kernel<true, 1>), grid, dim3(128), 0, stream, fa);
     TILER_HIP_CHECK(hipGetLastError());
@@ -2570,16 +2408,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.nq = nq;
     ra.L = ORB_L;
     ra.nsplit = nsplit;
-#ifdef TILER_EXPERIMENTS
-    static const int p1 = [] {
-        const char *e = getenv("TILER_ORBIT_P1");
-        const int v = e ? atoi(e) : 2;
-        return v < 1 ? 1 : v > 2 ? 2 : v;
-    }();
-#else
-    constexpr int p1 = 2;
-#endif
-    ra.p1 = p1;
+    ra.p1 = 2;
     ra.pair_cnt = o->pair_cnt;
     ra.pair_cand = o->pair_cand;
     ra.scale2 = (double)ix->scale * (double)ix->scale;
@@ -2588,13 +2417,6 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.Hp = o->Hp;
     ra.Ecp = o->Ecp;
     ra.t = tail;
-#ifdef TILER_EXPERIMENTS
-    if (getenv("TILER_KD_EXP") && atoi(getenv("TILER_KD_EXP")) == 2) {  // timing: index-order compares (invalid)
-        ra.t.ko = nullptr;
-        ra.gorder = nullptr;
-        ra.grp_of = nullptr;
-    }
-#endif
     static const bool want_stats = [] {
         const char *e = getenv("TILER_ORBIT_STATS");
         return e && e[0] == '1';

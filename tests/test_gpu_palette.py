@@ -58,7 +58,7 @@ def test_quantize_edges(gpu, oracle):
 
 def test_quantize_clustered_long_recount_lists(gpu, oracle):
     """Few dominant colours with small noise: many entries share a nearest neighbour, so the merges' recount
-    lists grow past the block-wide threshold (the wave-parallel path)."""
+    lists are long (the batched recount_next over many entries at once)."""
     rng = np.random.default_rng(11)
     base = rng.integers(0, 256, (6, 3))
     n = 1500
@@ -66,6 +66,20 @@ def test_quantize_clustered_long_recount_lists(gpu, oracle):
     rgb = px[..., 0] | (px[..., 1] << 8) | (px[..., 2] << 16)
     pal_of = rng.integers(0, 3, n).astype(np.int32)
     _check(oracle, rgb, pal_of, 3)
+
+
+@pytest.mark.parametrize("cap", [1, 3, 64])
+def test_quantize_list_overflow(gpu, oracle, cap):
+    """tiler_debug_dl3_list_cap: with at most `cap` recount entries per LDS batch, the merges' lists spill to the
+    global overflow and run in several batches; palettes stay bit-exact."""
+    from tiler_amd import load
+    lib = load()
+    rgb, pal_of, pairs = _case(5, (2,), 90, 3)
+    assert lib.tiler_debug_dl3_list_cap(cap) == 0
+    try:
+        _check(oracle, rgb, pal_of, pairs)
+    finally:
+        lib.tiler_debug_dl3_list_cap(0)
 
 
 @pytest.mark.parametrize("gamma", [-1, 0])

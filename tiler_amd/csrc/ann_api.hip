@@ -851,6 +851,11 @@ int tiler_quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_
                                  use_count, colors, (hipStream_t)stream);
 }
 
+int tiler_debug_dl3_list_cap(int cap) {
+    dl3_set_list_cap(cap);
+    return 0;
+}
+
 int tiler_prepare_dither_tiles_dev(long n_tiles, const int32_t *d_rgb, int n_palettes, int gamma, int use_wavelets,
                                    int max_iter, uint32_t seed, int32_t *d_labels, double *d_centroids,
                                    int *iterations, void *stream) {

@@ -9,10 +9,11 @@
 //      32-bit wrapping sums (MSVC `ulong`, as the reference DLL) -- the tile order does not matter to a histogram;
 //   2. pass 1 of reduce_table3 (recount_next for every entry: the O(n^2 / 2) nearest-merge search) with one wave
 //      per entry over the whole grid;
-//   3. pass 2 (the sequential merges) with one 1024-thread workgroup per pair: each merge's scans (the minimum
-//      error, the index fix-ups, recount_dist) run block-parallel in the reference's phase order, each
-//      recount_next as a block- or wave-wide first-minimum search; results are those of the sequential loops
-//      because every phase only writes entries it owns.
+//   3. pass 2 (the sequential merges) with one 1024-thread workgroup per pair: each merge is the minimum error
+//      over chunk minima, one pass over the table that applies every entry's fix-ups (re-point, the updates of
+//      recount_dist(c1) and recount_dist(c2)) or lists it for recount_next, and one batched, load-balanced scan
+//      for all listed recount_next; results are those of the sequential loops because each entry's steps only
+//      depend on its own state and on table data the merge does not change (dl3_merge_pass).
 // calc_err is evaluated exactly as quantizer.c:512-541 in IEEE single precision: integer cell means, squares of
 // integers (exact), sqrt through double (innocuous for sqrt: 53 >= 2 * 24 + 2) rounded once to float.
 #include <hipcub/hipcub.hpp>
@@ -21,6 +22,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "palette.hpp"
@@ -32,7 +34,6 @@ namespace {
 
 constexpr int DL3_T = 1024;        // pass-2 workgroup
 constexpr int DL3_W = DL3_T / 64;  // its waves
-constexpr int DL3_BLOCK_LIST = 8;  // a recount list up to this length runs block-wide per item, longer wave-wide
 
 struct Dl3Sum {
     uint32_t r, g, b, n;
@@ -50,21 +51,19 @@ struct Dl3Expand {  // one pixel 0x00BBGGRR -> its CUBE3 contribution (build_tab
     }
 };
 
-// the colour tables of all pairs; entry e of pair p at seg[p] + local index.  Two 16-byte records per entry: every
-// scan of pass 2 reads only S (one dwordx4 per entry, several in flight per lane), calc_err also V.
+// the colour tables of all pairs; entry e of pair p at seg[p] + local index, split by access: the nearest-merge
+// scans read QN alone (8 bytes per entry), the per-merge pass QN and EC, calc_err also V.
 struct Dl3Tab {
-    uint4 *S;  // x = Q (rr | gg << 8 | bb << 16, setrgb), y = N (pixel_count), z = E (err, float bits), w = C (cc)
-    uint4 *V;  // x, y, z = CUBE3 r, g, b (32-bit, wrapping); w unused
+    uint2 *QN;  // x = Q (rr | gg << 8 | bb << 16, setrgb), y = N (pixel_count)
+    uint2 *EC;  // x = E (err, float bits), y = C (cc)
+    uint4 *V;   // x, y, z = CUBE3 r, g, b (32-bit, wrapping); w unused
 };
-constexpr int DL3_U = 6;  // records loaded per lane before any is used
-
-__device__ __forceinline__ float dl3_e(const uint4 &s) { return __uint_as_float(s.z); }
+constexpr int DL3_U = 6;   // records loaded per lane before any is used
+constexpr int DL3_UM = 4;  // the same in the merge pass (two records per entry)
 
 __device__ __forceinline__ void dl3_set_ec(const Dl3Tab &t, int i, float e, int c) {
-    *reinterpret_cast<uint2 *>(reinterpret_cast<uint32_t *>(t.S + i) + 2) = make_uint2(__float_as_uint(e), (uint32_t)c);
+    t.EC[i] = make_uint2(__float_as_uint(e), (uint32_t)c);
 }
-
-__device__ __forceinline__ void dl3_set_c(const Dl3Tab &t, int i, int c) { reinterpret_cast<uint32_t *>(t.S + i)[3] = c; }
 
 __device__ __forceinline__ uint32_t dl3_setrgb(uint32_t r, uint32_t g, uint32_t b, uint32_t n) {  // quantizer.c:472-478
     const int v = (int)n, v2 = v >> 1;
@@ -82,9 +81,9 @@ struct Dl3Entry {
     uint32_t r, g, b, n, q;
 };
 
-__device__ __forceinline__ Dl3Entry dl3_entry(const uint4 &s, const uint4 &v) { return Dl3Entry{v.x, v.y, v.z, s.y, s.x}; }
+__device__ __forceinline__ Dl3Entry dl3_entry(const uint2 &qn, const uint4 &v) { return Dl3Entry{v.x, v.y, v.z, qn.y, qn.x}; }
 
-__device__ __forceinline__ Dl3Entry dl3_load(const Dl3Tab &t, int i) { return dl3_entry(t.S[i], t.V[i]); }
+__device__ __forceinline__ Dl3Entry dl3_load(const Dl3Tab &t, int i) { return dl3_entry(t.QN[i], t.V[i]); }
 
 __device__ __forceinline__ float dl3_calc_err(const Dl3Entry &a, const Dl3Entry &b) {  // quantizer.c:512-541
     const uint32_t P1 = a.n, P2 = b.n, P3 = P1 + P2;
@@ -100,15 +99,16 @@ __device__ __forceinline__ float dl3_calc_err(const Dl3Entry &a, const Dl3Entry 
     return d1 + d2;
 }
 
-// A rigorous lower bound of the COMPUTED calc_err(a, b): sqrt(d1) + sqrt(d2) >= |Q_a - Q_b| (triangle inequality
-// through the merged mean), so the exact value is >= min(P_a, P_b) * |Q_a - Q_b|, and the float evaluation (four
-// roundings of non-negative terms, the counts' conversion) loses at most a factor (1 - 2^-24)^5.  A candidate whose
-// bound exceeds the current best strictly can neither win nor tie, so skipping it leaves every result unchanged.
-__device__ __forceinline__ double dl3_lower_bound(uint32_t qa, uint32_t na, uint32_t qb, uint32_t nb) {
+// True when the COMPUTED calc_err(a, b) is certainly > e, so the candidate can neither win nor tie.  The exact value
+// is >= m * |Q_a - Q_b| with m = min(P_a, P_b) (sqrt(d1) + sqrt(d2) >= |Q_a - Q_b|, the triangle inequality through
+// the merged mean), the float evaluation loses at most (1 - 2^-24)^5, so computed^2 >= m^2 * dd * (1 - 6e-7).  The
+// test's own float evaluation (dd exact, m rounded once, three products, e * e) is within (1 +- 2^-24)^6, so with
+// the factor 1 - 1e-5 a true result implies computed^2 > e^2.  e = inf (or e * e overflowing) never prunes.
+__device__ __forceinline__ bool dl3_cannot(uint32_t qa, uint32_t na, uint32_t qb, uint32_t nb, float e) {
     const int dr = (int)(qa & 255) - (int)(qb & 255), dg = (int)((qa >> 8) & 255) - (int)((qb >> 8) & 255);
     const int db = (int)((qa >> 16) & 255) - (int)((qb >> 16) & 255);
-    const double dd = (double)(dr * dr + dg * dg + db * db);
-    return __builtin_sqrt(dd) * (double)(na < nb ? na : nb) * (1.0 - 1e-6);
+    const float m = (float)(na < nb ? na : nb);
+    return (float)(dr * dr + dg * dg + db * db) * m * m * 0.99999f > e * e;
 }
 
 // first minimum: smaller error, equal errors -> smaller index (the reference's ascending scan with `<`)
@@ -157,25 +157,26 @@ struct Dl3Chunks {
 };
 
 __device__ __forceinline__ void dl3_mark(Dl3Chunks *ch, int i) {
-    if (!ch) return;
     const int c = i >> ch->sh;
     const unsigned m = 1u << (c & 31);
     if (!(atomicOr(&ch->bits[c >> 5], m) & m)) ch->dirty[atomicAdd(&ch->n, 1)] = c;
 }
 
-// recount_next(i) over j in (i, tot) (quantizer.c:543-560), lanes striding by STRIDE: this lane's first minimum
-// (its j ascend, `<` keeps the earlier of equal errors)
-template <int STRIDE>
-__device__ __forceinline__ void dl3_recount_scan(const Dl3Tab &t, const Dl3Entry &a, int i, int tot, int lane, float &e,
-                                                 int &j) {
-    for (int k0 = i + 1 + lane; k0 < tot; k0 += STRIDE * DL3_U) {
-        uint4 r[DL3_U];
+// recount_next(i) (quantizer.c:543-560) by one wave over j in (i, tot): each lane's first minimum (its j ascend,
+// `<` keeps the earlier of equal errors), then the wave's; lane 0 stores it (cc = 0 for an empty range)
+__device__ void dl3_recount_wave(const Dl3Tab &t, int i, int tot) {
+    const Dl3Entry a = dl3_load(t, i);
+    float e = HUGE_VALF;
+    int j = INT32_MAX;
+    const int lane = (int)(threadIdx.x & 63);
+    for (int k0 = i + 1 + lane; k0 < tot; k0 += 64 * DL3_U) {
+        uint2 r[DL3_U];
 #pragma unroll
-        for (int u = 0; u < DL3_U; u++) r[u] = t.S[min(k0 + u * STRIDE, tot - 1)];
+        for (int u = 0; u < DL3_U; u++) r[u] = t.QN[min(k0 + u * 64, tot - 1)];
 #pragma unroll
         for (int u = 0; u < DL3_U; u++) {
-            const int k = k0 + u * STRIDE;
-            if (k >= tot || dl3_lower_bound(a.q, a.n, r[u].x, r[u].y) > (double)e) continue;  // cannot win or tie
+            const int k = k0 + u * 64;
+            if (k >= tot || dl3_cannot(a.q, a.n, r[u].x, r[u].y, e)) continue;
             const float cur = dl3_calc_err(a, dl3_entry(r[u], t.V[k]));
             if (cur < e) {
                 e = cur;
@@ -183,31 +184,8 @@ __device__ __forceinline__ void dl3_recount_scan(const Dl3Tab &t, const Dl3Entry
             }
         }
     }
-}
-
-// recount_next(i) by the whole block / one wave
-__device__ void dl3_recount_block(const Dl3Tab &t, int i, int tot, float *sh_e, int *sh_j, Dl3Chunks *ch = nullptr) {
-    const Dl3Entry a = dl3_load(t, i);
-    float e = HUGE_VALF;
-    int j = INT32_MAX;
-    dl3_recount_scan<DL3_T>(t, a, i, tot, (int)threadIdx.x, e, j);
-    dl3_block_min(e, j, sh_e, sh_j);
-    if (threadIdx.x == 0) {
-        dl3_set_ec(t, i, e, j == INT32_MAX ? 0 : j);
-        dl3_mark(ch, i);
-    }
-}
-
-__device__ void dl3_recount_wave(const Dl3Tab &t, int i, int tot, Dl3Chunks *ch = nullptr) {
-    const Dl3Entry a = dl3_load(t, i);
-    float e = HUGE_VALF;
-    int j = INT32_MAX;
-    dl3_recount_scan<64>(t, a, i, tot, (int)(threadIdx.x & 63), e, j);
     dl3_wave_min(e, j);
-    if ((threadIdx.x & 63) == 0) {
-        dl3_set_ec(t, i, e, j == INT32_MAX ? 0 : j);
-        dl3_mark(ch, i);
-    }
+    if (lane == 0) dl3_set_ec(t, i, e, j == INT32_MAX ? 0 : j);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -253,7 +231,7 @@ __global__ __launch_bounds__(256) void dl3_init_kernel(const Dl3Sum *__restrict_
     if (e >= seg[P]) return;
     const Dl3Sum s = agg[e];
     t.V[e] = make_uint4(s.r, s.g, s.b, 0u);
-    t.S[e] = make_uint4(dl3_setrgb(s.r, s.g, s.b, s.n), s.n, 0u, 0u);  // E, C: pass 1
+    t.QN[e] = make_uint2(dl3_setrgb(s.r, s.g, s.b, s.n), s.n);  // EC: pass 1
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -266,7 +244,7 @@ __global__ __launch_bounds__(256) void dl3_pass1_kernel(const uint32_t *__restri
         const int p = (int)(ukeys[e] >> (3 * bpc));
         const int s = seg[p], n = seg[p + 1] - s, i = e - s;
         Dl3Tab u = t;
-        u.S += s, u.V += s;
+        u.QN += s, u.EC += s, u.V += s;
         if (i == n - 1) {  // the last entry (quantizer.c:598-599)
             if ((threadIdx.x & 63) == 0) dl3_set_ec(u, i, HUGE_VALF, n);
         } else {
@@ -282,51 +260,104 @@ struct Dl3Args {
     Dl3Tab t;
     const int *seg;
     int quant_to;
-    int *list;       // [entries] recount lists (a pair's slice at its seg offset)
+    int *list;       // [entries] recount-list overflow (a pair's slice at its seg offset)
+    int lcap;        // recount-list entries held in LDS per batch (DL3_LCAP; smaller only by the test hook)
     int32_t *pal;    // [P][quant_to] 0x00BBGGRR
 };
 
-// the collected recount list: short lists block-wide per item, long ones one item per wave
-__device__ void dl3_run_list(const Dl3Tab &t, const int *list, int k, int tot, float *sh_e, int *sh_j,
-                             Dl3Chunks *ch) {
-    if (k <= DL3_BLOCK_LIST) {
-        for (int q = 0; q < k; q++) dl3_recount_block(t, list[q], tot, sh_e, sh_j, ch);
-    } else {
-        for (int q = threadIdx.x >> 6; q < k; q += DL3_W) dl3_recount_wave(t, list[q], tot, ch);
-    }
-    __syncthreads();
+// One merge's recount list, batched: every listed entry's recount_next scan is cut into units of 64 candidates,
+// the units of the whole batch are split evenly over the waves, and each candidate that survives the bound is
+// folded into its entry's slot by a 64-bit LDS atomic minimum of (err bits, index) -- the first minimum, as err >= 0
+// orders like its bits.  Every scan reads only table data no step of the merge writes (QN, V), so the order of the
+// candidates does not matter, and the slot's current value is an achieved error, hence a valid pruning bound.
+constexpr int DL3_LCAP = 1024;
+constexpr unsigned long long DL3_NONE = (0x7f800000ull << 32) | 0xffffffffull;  // (inf, no index)
+struct Dl3List {
+    int item[DL3_LCAP];
+    uint2 qn[DL3_LCAP];
+    unsigned long long slot[DL3_LCAP];
+    int pre[DL3_LCAP + 1];  // exclusive prefix of the items' unit counts
+    int wsum[DL3_W];
+    int n;                  // listed entries (those >= DL3_LCAP in the global overflow)
+};
+
+__device__ __forceinline__ void dl3_push(Dl3List *L, int *glist, int i, int lcap) {
+    const int k = atomicAdd(&L->n, 1);
+    if (k < lcap)
+        L->item[k] = i;
+    else
+        glist[k] = i;
 }
 
-// recount_dist(c) (quantizer.c:562-581)
-__device__ void dl3_recount_dist(const Dl3Tab &t, int *list, int c, int tot, float *sh_e, int *sh_j, int *sh_n,
-                                 Dl3Chunks *ch) {
-    dl3_recount_block(t, c, tot, sh_e, sh_j, ch);
-    if (threadIdx.x == 0) *sh_n = 0;
-    __syncthreads();
-    const Dl3Entry b = dl3_load(t, c);
-    for (int i0 = threadIdx.x; i0 < c; i0 += DL3_T * DL3_U) {
-        uint4 r[DL3_U];
+__device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, const int *glist, int K, int tot, Dl3Chunks *ch,
+                                 int lcap) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int base = 0; base < K; base += lcap) {
+        const int nb = min(lcap, K - base);
+        int units = 0;
+        if (tid < nb) {
+            const int i = base ? glist[base + tid] : L->item[tid];
+            if (base) L->item[tid] = i;  // the previous batch's readers passed its last barrier
+            L->qn[tid] = t.QN[i];
+            L->slot[tid] = DL3_NONE;
+            units = (tot - 1 - i + 63) >> 6;
+        }
+        int v = units;  // block-wide exclusive scan of the unit counts
 #pragma unroll
-        for (int u = 0; u < DL3_U; u++) r[u] = t.S[min(i0 + u * DL3_T, c - 1)];
-#pragma unroll
-        for (int u = 0; u < DL3_U; u++) {
-            const int i = i0 + u * DL3_T;
-            if (i >= c) break;
-            if ((int)r[u].w == c) {
-                list[atomicAdd(sh_n, 1)] = i;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int x = __shfl_up(v, o);
+            if (lane >= o) v += x;
+        }
+        if (lane == 63) L->wsum[w] = v;
+        __syncthreads();
+        int off = 0;
+        for (int k = 0; k < w; k++) off += L->wsum[k];
+        if (tid < nb) L->pre[tid + 1] = off + v;
+        if (tid == 0) L->pre[0] = 0;
+        __syncthreads();
+        const int U = L->pre[nb];
+        const int ua = (int)((long)U * w / DL3_W), ub = (int)((long)U * (w + 1) / DL3_W);
+        int q = 0;  // the item of unit ua: the last q with pre[q] <= ua
+        for (int lo = 0, hi = nb; lo < hi;) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (L->pre[mid] <= ua) {
+                lo = mid;
+                q = mid;
             } else {
-                const float ei = dl3_e(r[u]);
-                if (dl3_lower_bound(r[u].x, r[u].y, b.q, b.n) > (double)ei) continue;  // no update possible
-                const float cur = dl3_calc_err(dl3_entry(r[u], t.V[i]), b);
-                if (cur < ei) {
-                    dl3_set_ec(t, i, cur, c);
-                    dl3_mark(ch, i);
-                }
+                hi = mid - 1;
             }
         }
+        for (int u0 = ua; u0 < ub; u0 += DL3_U) {
+            uint2 r[DL3_U];
+            int qq[DL3_U], jj[DL3_U];
+#pragma unroll
+            for (int u = 0; u < DL3_U; u++) {
+                const int uu = u0 + u;
+                while (q < nb - 1 && L->pre[q + 1] <= uu) q++;
+                qq[u] = q;
+                jj[u] = uu < ub ? L->item[q] + 1 + ((uu - L->pre[q]) << 6) + lane : tot;
+                r[u] = t.QN[min(jj[u], tot - 1)];
+            }
+#pragma unroll
+            for (int u = 0; u < DL3_U; u++) {
+                if (jj[u] >= tot) continue;
+                const float eb = __uint_as_float((uint32_t)(L->slot[qq[u]] >> 32));
+                const uint2 a = L->qn[qq[u]];
+                if (dl3_cannot(a.x, a.y, r[u].x, r[u].y, eb)) continue;
+                const float cur = dl3_calc_err(dl3_entry(a, t.V[L->item[qq[u]]]), dl3_entry(r[u], t.V[jj[u]]));
+                if (cur <= eb)
+                    atomicMin(&L->slot[qq[u]], ((unsigned long long)__float_as_uint(cur) << 32) | (uint32_t)jj[u]);
+            }
+        }
+        __syncthreads();
+        if (tid < nb) {
+            const unsigned long long k = L->slot[tid];
+            const int i = L->item[tid];
+            dl3_set_ec(t, i, __uint_as_float((uint32_t)(k >> 32)), (uint32_t)k == 0xffffffffu ? 0 : (int)(uint32_t)k);
+            dl3_mark(ch, i);
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    dl3_run_list(t, list, *sh_n, tot, sh_e, sh_j, ch);
 }
 
 // the first minimum of chunk c over entries below tot, by one wave (lane 0 stores it)
@@ -335,12 +366,12 @@ __device__ void dl3_chunk_min(const Dl3Tab &t, Dl3Chunks *ch, int c, int tot) {
     float v = HUGE_VALF;
     int j = INT32_MAX;
     for (int i0 = b + (int)(threadIdx.x & 63); i0 < e; i0 += 64 * DL3_U) {
-        uint4 r[DL3_U];
+        uint2 r[DL3_U];
 #pragma unroll
-        for (int u = 0; u < DL3_U; u++) r[u] = t.S[min(i0 + u * 64, e - 1)];
+        for (int u = 0; u < DL3_U; u++) r[u] = t.EC[min(i0 + u * 64, e - 1)];
 #pragma unroll
         for (int u = 0; u < DL3_U; u++) {
-            const float x = dl3_e(r[u]);
+            const float x = __uint_as_float(r[u].x);
             if (i0 + u * 64 < e && x < v) {
                 v = x;
                 j = i0 + u * 64;
@@ -354,22 +385,94 @@ __device__ void dl3_chunk_min(const Dl3Tab &t, Dl3Chunks *ch, int c, int tot) {
     }
 }
 
+// One merge's fix-ups (quantizer.c:631-642) as one pass with each entry in its own lane.  The reference's loops --
+// re-point i < c1 from the moved entry to c1; recount_next(i) for i > c1 pointing at it; recount_dist(c1); then
+// recount_dist(c2) unless c2 was the last entry -- only ever change entry i from entry i's own state and table data
+// none of them writes (QN, V are final once the merge is applied), so each entry's sequence of steps can run on its
+// own.  A recount_next makes every later step of the same entry a no-op: its scan over (i, tot) already covers c1
+// and c2 whenever a later step would compare against them (c1 < c2, and those steps only visit i < c1 or i < c2),
+// and a repeated recount gives the same result.  So an entry either joins the recount list, or takes the updates
+// with calc_err(i, c1) then calc_err(i, c2) (strictly smaller only, as the reference).
+__device__ void dl3_merge_pass(const Dl3Tab &t, Dl3List *L, int *glist, int c1, int c2, int tot, Dl3Chunks *ch,
+                               int lcap) {
+    const bool c2v = c2 != tot;
+    const uint2 q1 = t.QN[c1], q2 = t.QN[c2v ? c2 : c1];
+    const uint4 v1 = t.V[c1], v2 = t.V[c2v ? c2 : c1];
+    const Dl3Entry b1 = dl3_entry(q1, v1), b2 = dl3_entry(q2, v2);
+    for (int i0 = threadIdx.x; i0 < tot; i0 += DL3_T * DL3_UM) {
+        uint2 rq[DL3_UM], re[DL3_UM];
+#pragma unroll
+        for (int u = 0; u < DL3_UM; u++) {
+            const int i = min(i0 + u * DL3_T, tot - 1);
+            rq[u] = t.QN[i];
+            re[u] = t.EC[i];
+        }
+#pragma unroll
+        for (int u = 0; u < DL3_UM; u++) {
+            const int i = i0 + u * DL3_T;
+            if (i >= tot) break;
+            int c = (int)re[u].y;
+            float e = __uint_as_float(re[u].x);
+            bool rc = false, wr = false;
+            if (i == c1) {
+                rc = true;
+            } else if (i > c1) {
+                rc = c == tot;
+            } else {
+                if (c == tot) {
+                    c = c1;
+                    wr = true;
+                }
+                if (c == c1) {
+                    rc = true;
+                } else if (!dl3_cannot(rq[u].x, rq[u].y, b1.q, b1.n, e)) {
+                    const float cur = dl3_calc_err(dl3_entry(rq[u], t.V[i]), b1);
+                    if (cur < e) {
+                        e = cur;
+                        c = c1;
+                        wr = true;
+                    }
+                }
+            }
+            if (!rc && c2v && i <= c2) {
+                if (i == c2 || c == c2) {
+                    rc = true;
+                } else if (!dl3_cannot(rq[u].x, rq[u].y, b2.q, b2.n, e)) {
+                    const float cur = dl3_calc_err(dl3_entry(rq[u], t.V[i]), b2);
+                    if (cur < e) {
+                        e = cur;
+                        c = c2;
+                        wr = true;
+                    }
+                }
+            }
+            if (rc) {
+                dl3_push(L, glist, i, lcap);
+            } else if (wr) {
+                dl3_set_ec(t, i, e, c);
+                dl3_mark(ch, i);
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
     __shared__ float sh_e[DL3_W];
     __shared__ int sh_j[DL3_W];
-    __shared__ int sh_n;
     __shared__ Dl3Chunks chs;
+    __shared__ Dl3List lst;
     Dl3Chunks *ch = &chs;
+    Dl3List *L = &lst;
     const int p = blockIdx.x;
     const int s = a.seg[p], n = a.seg[p + 1] - s;
     if (n <= a.quant_to) {  // nothing to merge
         for (int i = threadIdx.x; i < a.quant_to; i += DL3_T)
-            a.pal[(long)p * a.quant_to + i] = i < n ? (int32_t)a.t.S[s + i].x : 0;
+            a.pal[(long)p * a.quant_to + i] = i < n ? (int32_t)a.t.QN[s + i].x : 0;
         return;
     }
     Dl3Tab t = a.t;
-    t.S += s, t.V += s;
-    int *list = a.list + s;
+    t.QN += s, t.EC += s, t.V += s;
+    int *glist = a.list + s;
     int sh = 0;
     while (((n + (1 << sh) - 1) >> sh) > DL3_MAXCH) sh++;
     if (threadIdx.x == 0) {
@@ -390,69 +493,30 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
         for (int c = threadIdx.x; c < nch; c += DL3_T) dl3_min(e, j, ch->e[c], ch->j[c]);
         dl3_block_min(e, j, sh_e, sh_j);
         if (j != INT32_MAX) c1 = j;
-        const int c2 = (int)t.S[c1].w;
+        const int c2 = (int)t.EC[c1].y;
         __syncthreads();  // every thread has read C[c1] and the chunk minima before they change
         tot--;
         if (threadIdx.x == 0) {  // merge c1 into c2, the last entry into c1 (quantizer.c:619-629)
-            const uint4 s1 = t.S[c1], v1 = t.V[c1], s2 = t.S[c2], v2 = t.V[c2];
-            const uint32_t r = v2.x + v1.x, g = v2.y + v1.y, b = v2.z + v1.z, nn = s2.y + s1.y;
+            const uint2 q1 = t.QN[c1], q2 = t.QN[c2];
+            const uint4 v1 = t.V[c1], v2 = t.V[c2];
+            const uint32_t r = v2.x + v1.x, g = v2.y + v1.y, b = v2.z + v1.z, nn = q2.y + q1.y;
             t.V[c2] = make_uint4(r, g, b, 0u);
-            t.S[c2] = make_uint4(dl3_setrgb(r, g, b, nn), nn, s2.z, s2.w);
-            const uint4 sl = t.S[tot], vl = t.V[tot];  // (after the c2 update: c2 may be the last entry)
-            t.V[c1] = vl;
-            t.S[c1] = sl;
+            t.QN[c2] = make_uint2(dl3_setrgb(r, g, b, nn), nn);
+            // (after the c2 update: c2 may be the last entry)
+            t.V[c1] = t.V[tot];
+            t.QN[c1] = t.QN[tot];
+            t.EC[c1] = t.EC[tot];
             dl3_set_ec(t, tot - 1, HUGE_VALF, tot);
-            sh_n = 0;
+            L->n = 0;
             dl3_mark(ch, c1);
             dl3_mark(ch, tot - 1);
             dl3_mark(ch, tot);  // the removed entry leaves its chunk
         }
         __syncthreads();
-        // One pass for three of the reference's loops, each entry in its own lane (quantizer.c:631-641):
-        //   i > c1 pointing at the moved entry -> recount_next(i);
-        //   i < c1 pointing at the moved entry -> re-point to c1, then recount_dist(c1)'s loop: pointing at c1 ->
-        //   recount_next(i), else the update with calc_err(i, c1);
-        // plus recount_next(c1) itself.  The recounts only write their own entry and read table data no loop
-        // writes, and the updates below c1 read nothing the recounts above c1 write, so this equals the sequence.
-        {
-            const Dl3Entry b1 = dl3_load(t, c1);
-            for (int i0 = threadIdx.x; i0 < tot; i0 += DL3_T * DL3_U) {
-                uint4 r[DL3_U];
-#pragma unroll
-                for (int u = 0; u < DL3_U; u++) r[u] = t.S[min(i0 + u * DL3_T, tot - 1)];
-#pragma unroll
-                for (int u = 0; u < DL3_U; u++) {
-                    const int i = i0 + u * DL3_T;
-                    if (i >= tot) break;
-                    if (i == c1) continue;
-                    int ci = (int)r[u].w;
-                    if (i > c1) {
-                        if (ci == tot) list[atomicAdd(&sh_n, 1)] = i;
-                        continue;
-                    }
-                    if (ci == tot) {
-                        ci = c1;
-                        dl3_set_c(t, i, c1);
-                    }
-                    if (ci == c1) {
-                        list[atomicAdd(&sh_n, 1)] = i;
-                    } else {
-                        const float ei = dl3_e(r[u]);
-                        if (dl3_lower_bound(r[u].x, r[u].y, b1.q, b1.n) > (double)ei) continue;  // no update possible
-                        const float cur = dl3_calc_err(dl3_entry(r[u], t.V[i]), b1);
-                        if (cur < ei) {
-                            dl3_set_ec(t, i, cur, c1);
-                            dl3_mark(ch, i);
-                        }
-                    }
-                }
-            }
-            if (threadIdx.x == 0) list[atomicAdd(&sh_n, 1)] = c1;
-        }
+        dl3_merge_pass(t, L, glist, c1, c2, tot, ch, a.lcap);
         __syncthreads();
-        dl3_run_list(t, list, sh_n, tot, sh_e, sh_j, ch);
-        if (c2 != tot) dl3_recount_dist(t, list, c2, tot, sh_e, sh_j, &sh_n, ch);
-        // refresh the marked chunks (every mark above is complete: the list runs end in a barrier)
+        dl3_recount_list(t, L, glist, L->n, tot, ch, a.lcap);
+        // refresh the marked chunks (every mark above is complete: the list run ends in a barrier)
         const int nd = ch->n;
         for (int q = threadIdx.x >> 6; q < nd; q += DL3_W) dl3_chunk_min(t, ch, ch->dirty[q], tot);
         __syncthreads();
@@ -461,12 +525,19 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
         __syncthreads();
     }
     for (int i = threadIdx.x; i < a.quant_to; i += DL3_T)  // set_palette3 + copy_pal (calloc'd beyond tot)
-        a.pal[(long)p * a.quant_to + i] = i < tot ? (int32_t)t.S[i].x : 0;
+        a.pal[(long)p * a.quant_to + i] = i < tot ? (int32_t)t.QN[i].x : 0;
 }
 
 // ---------------------------------------------------------------------------------------------------------------
 // host: CompareCMULHS (TFPList.Sort) and FinishQuantizePalette's order
 // ---------------------------------------------------------------------------------------------------------------
+}  // namespace
+
+static std::atomic<int> g_dl3_lcap{DL3_LCAP};  // tiler_debug_dl3_list_cap
+void dl3_set_list_cap(int cap) { g_dl3_lcap.store(cap > 0 ? cap : DL3_LCAP); }
+
+namespace {
+
 int muldiv_win(int a, int b, int c) {  // Windows MulDiv (unit windows in main.pas's uses): rounded half away from 0
     if (c == 0) return -1;
     if (c < 0) {
@@ -639,7 +710,8 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     int *d_seg = (int *)take(4 * (P + 2));
     int *d_uc = (int *)take(4 * (P + 2));
     Dl3Tab t;
-    t.S = (uint4 *)take(4 * b_keys);
+    t.QN = (uint2 *)take(2 * b_keys);
+    t.EC = (uint2 *)take(2 * b_keys);
     t.V = (uint4 *)take(4 * b_keys);
     int *d_list = (int *)k0;  // the sort buffers are free once the table exists
     int32_t *d_pal = (int32_t *)take(4 * (size_t)P * palsize);
@@ -687,6 +759,7 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
             ra.seg = d_seg;
             ra.quant_to = palsize;
             ra.list = d_list;
+            ra.lcap = std::max(1, std::min(DL3_LCAP, g_dl3_lcap.load()));
             ra.pal = d_pal;
             hipLaunchKernelGGL(dl3_reduce_kernel, dim3(P), dim3(DL3_T), 0, stream, ra);
             if (hipGetLastError() != hipSuccess) break;

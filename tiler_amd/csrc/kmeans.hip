@@ -12,8 +12,8 @@
 //   * Lloyd iterations until no label changes (or max_iter assignments): a centroid is the mean of its members in
 //     point order, summed in runs of 256 members (sequential inside a run, run sums in order) and divided by the
 //     count; an empty cluster keeps its centroid.
-// Layout: X [n][d] row-major for the assignment (a wave per point block, lane = centroid, the centroid chunk in
-// LDS as [d][64]); X^T [d][n] for the seeding's per-point distance (lane = point, coalesced).
+// Layout: X [n][d] row-major (centroid means, seeding rows); X^T [d][n] for the per-point distances of the seeding
+// and the assignment (lane = point, coalesced).
 #include <hipcub/hipcub.hpp>
 #include <math.h>
 #include <stdint.h>
@@ -32,9 +32,7 @@ namespace tiler {
 namespace {
 
 constexpr int KM_MAXD = 192;    // descriptor dimension bound (cTileDCTSize)
-constexpr int KM_CH = 64;       // centroids per LDS chunk (lane = centroid)
-constexpr int KM_PTS = 4;       // points per wave step (independent distance chains per lane)
-constexpr int KM_WG_PTS = 256;  // points per assignment workgroup
+constexpr int KM_CH = 32;       // centroids per LDS chunk of the assignment (distance chains per lane)
 constexpr int KM_RUN = 256;     // members per centroid partial sum
 constexpr int KM_SEL_T = 1024;  // seeding selection workgroup
 
@@ -152,76 +150,53 @@ __global__ __launch_bounds__(256) void km_copy_row_kernel(const double *__restri
     for (int k = threadIdx.x; k < d; k += 256) dst[k] = X[row * d + k];
 }
 
-// Lloyd assignment: workgroup = KM_WG_PTS points, the centroids chunk by chunk through LDS ([d][64]); a wave takes
-// KM_PTS points at a time, lane = centroid, each lane's distance chains in dimension order
-__global__ __launch_bounds__(256) void km_assign_kernel(const double *__restrict__ X, long n, int d,
+// Lloyd assignment: lane = point (X^T [d][n]: one coalesced load per dimension), the centroids KM_CH at a time
+// through LDS as [d][KM_CH] (each read a broadcast of two centroids' values), every lane keeping KM_CH distance
+// chains in dimension order; the first minimum over chunks, then over a chunk's centroids in index order (ties ->
+// the lowest centroid).  Per (dimension, centroid): sub, mul, add in fp64 (no contraction) -- the bound is the fp64
+// VALU rate; per dimension a lane issues 3 * KM_CH of them against KM_CH / 2 LDS reads and one global load.
+__global__ __launch_bounds__(256) void km_assign_kernel(const double *__restrict__ XT, long n, int d,
                                                         const double *__restrict__ cent, int k,
                                                         int32_t *__restrict__ labels, int *__restrict__ changed) {
-    __shared__ double sc[KM_MAXD * KM_CH];
-    __shared__ double best_d[KM_WG_PTS];
-    __shared__ int best_c[KM_WG_PTS];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const long p0 = (long)blockIdx.x * KM_WG_PTS;
-    for (int q = threadIdx.x; q < KM_WG_PTS; q += 256) {
-        best_d[q] = HUGE_VAL;
-        best_c[q] = -1;
-    }
+    __shared__ double2 sc[KM_MAXD * KM_CH / 2];  // sc[dd * KM_CH / 2 + jp] = (c[2 jp][dd], c[2 jp + 1][dd])
+    const long p = (long)blockIdx.x * 256 + threadIdx.x;
+    const long pc = p < n ? p : n - 1;
+    double best = HUGE_VAL;
+    int bc = -1;
     for (int c0 = 0; c0 < k; c0 += KM_CH) {
         const int nc = k - c0 < KM_CH ? k - c0 : KM_CH;
         __syncthreads();
         for (int idx = threadIdx.x; idx < d * KM_CH; idx += 256) {
             const int dd = idx / KM_CH, cc = idx % KM_CH;
-            sc[idx] = cc < nc ? cent[(long)(c0 + cc) * d + dd] : 0.0;
+            reinterpret_cast<double *>(sc)[idx] = cc < nc ? cent[(long)(c0 + cc) * d + dd] : 0.0;
         }
         __syncthreads();
-        for (int q = wave * KM_PTS; q < KM_WG_PTS; q += 4 * KM_PTS) {
-            double acc[KM_PTS];
-            const double *xr[KM_PTS];
+        double acc[KM_CH];
 #pragma unroll
-            for (int j = 0; j < KM_PTS; j++) {
-                acc[j] = 0.0;
-                const long p = p0 + q + j;
-                xr[j] = X + (p < n ? p : n - 1) * d;
+        for (int j = 0; j < KM_CH; j++) acc[j] = 0.0;
+        double x = XT[pc];
+        for (int dd = 0; dd < d; dd++) {
+            const double xn = XT[(long)(dd + 1 < d ? dd + 1 : dd) * n + pc];  // the next dimension in flight
+#pragma unroll
+            for (int jp = 0; jp < KM_CH / 2; jp++) {
+                const double2 cv = sc[dd * (KM_CH / 2) + jp];
+                const double t0 = x - cv.x, t1 = x - cv.y;
+                acc[2 * jp] = acc[2 * jp] + t0 * t0;
+                acc[2 * jp + 1] = acc[2 * jp + 1] + t1 * t1;
             }
-            for (int dd = 0; dd < d; dd++) {
-                const double cv = sc[dd * KM_CH + lane];
-#pragma unroll
-                for (int j = 0; j < KM_PTS; j++) {
-                    const double t = xr[j][dd] - cv;
-                    acc[j] = acc[j] + t * t;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < KM_PTS; j++) {
-                double e = lane < nc ? acc[j] : HUGE_VAL;
-                int c = lane < nc ? c0 + lane : 0x7fffffff;
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) {
-                    const double e2 = __shfl_xor(e, o);
-                    const int c2 = __shfl_xor(c, o);
-                    if (e2 < e || (e2 == e && c2 < c)) {
-                        e = e2;
-                        c = c2;
-                    }
-                }
-                if (lane == 0 && e < best_d[q + j]) {  // earlier chunks win ties (lower centroid index)
-                    best_d[q + j] = e;
-                    best_c[q + j] = c;
-                }
-            }
+            x = xn;
         }
-    }
-    __syncthreads();
-    for (int q = threadIdx.x; q < KM_WG_PTS; q += 256) {
-        const long p = p0 + q;
-        if (p < n) {
-            const int c = best_c[q];
-            if (labels[p] != c) {
-                labels[p] = c;
-                atomicAdd(changed, 1);
+#pragma unroll
+        for (int j = 0; j < KM_CH; j++)
+            if (j < nc && acc[j] < best) {
+                best = acc[j];
+                bc = c0 + j;
             }
-        }
     }
+    const bool ch = p < n && labels[p] != bc;
+    if (ch) labels[p] = bc;
+    const unsigned long long m = __ballot(ch);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(changed, (int)__popcll(m));
 }
 
 __global__ void km_iota_kernel(int32_t *v, long n) {
@@ -338,7 +313,7 @@ int kmeans_dev(const double *d_X, long n, int d, int k, int max_iter, uint32_t s
         }
         if (!ok) break;
         if (hipMemsetAsync(d_labels, 0xff, 4 * nn, stream) != hipSuccess) break;  // -1: every first label changes
-        const unsigned g_assign = (unsigned)((n + KM_WG_PTS - 1) / KM_WG_PTS);
+        const unsigned g_assign = (unsigned)((n + 255) / 256);
         bool fail = false;
         while (it < max_iter) {
             {
@@ -347,7 +322,7 @@ int kmeans_dev(const double *d_X, long n, int d, int k, int max_iter, uint32_t s
                     fail = true;
                     break;
                 }
-                hipLaunchKernelGGL(km_assign_kernel, dim3(g_assign), dim3(256), 0, stream, d_X, n, d, d_cent, k, d_labels,
+                hipLaunchKernelGGL(km_assign_kernel, dim3(g_assign), dim3(256), 0, stream, XT, n, d, d_cent, k, d_labels,
                                    d_changed);
             }
             int changed = 0;

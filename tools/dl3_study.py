@@ -33,7 +33,18 @@ def dump(path):
     lib = tiler_amd.load()
     lib.tiler_init(0)
     pf = frames()
+    prepare_dither_tiles(pf.reshape(-1, 64), P)  # warm
+    lib.tiler_timing_reset()
+    lib.tiler_timing_enable(1)
+    t0 = time.perf_counter()
     lab, _, it = prepare_dither_tiles(pf.reshape(-1, 64), P)
+    tk = time.perf_counter() - t0
+    lib.tiler_timing_enable(0)
+    kp = {}
+    for name in ("kmeans", "kmeans_assign", "kmeans_update"):
+        n = ctypes.c_int(0)
+        kp[name] = round(lib.tiler_timing_get(name.encode(), ctypes.byref(n)), 2)
+    print({"prepare_dither_s": round(tk, 3), "kmeans_iterations": it, "kmeans_ms": kp})
     quantize_palettes(pf.reshape(-1, 64), lab, P)  # warm
     lib.tiler_timing_reset()
     lib.tiler_timing_enable(1)

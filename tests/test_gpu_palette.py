@@ -68,11 +68,11 @@ def test_quantize_clustered_long_recount_lists(gpu, oracle):
     _check(oracle, rgb, pal_of, 3)
 
 
-@pytest.mark.parametrize("cap,grid", [(1, 0), (3, 0), (64, 0), (0, 0), (1, 1), (3, 1)])
+@pytest.mark.parametrize("cap,grid", [(1, 0), (3, 0), (64, 0), (0, 1), (1, 1), (3, 1)])
 def test_quantize_list_overflow(gpu, oracle, cap, grid):
     """tiler_debug_dl3: with at most `cap` recount entries per LDS batch the merges' lists spill to the global
-    overflow (and, without the grid, run in several batches); grid = 0 is the batched linear recount of tables above
-    65,536 colours.  Palettes stay bit-exact."""
+    overflow (and, without the grid, run in several batches); grid = 1 is the colour-grid path (an alternative kept
+    for A/B), 0 the default batched linear scans.  Palettes stay bit-exact."""
     from tiler_amd import load
     lib = load()
     rgb, pal_of, pairs = _case(5, (2,), 90, 3)
@@ -80,7 +80,7 @@ def test_quantize_list_overflow(gpu, oracle, cap, grid):
     try:
         _check(oracle, rgb, pal_of, pairs)
     finally:
-        lib.tiler_debug_dl3(0, 1)
+        lib.tiler_debug_dl3(0, 0)
 
 
 @pytest.mark.parametrize("gamma", [-1, 0])

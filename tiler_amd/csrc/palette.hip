@@ -62,6 +62,7 @@ struct Dl3Tab {
 };
 constexpr int DL3_U = 6;   // records loaded per lane before any is used
 constexpr int DL3_UM = 4;  // the same in the merge pass (two records per entry)
+constexpr int DL3_UL = 12;  // candidates per lane in flight in the batched recount
 constexpr int DL3_UP = 2;  // members per lane in flight in the grid merge pass
 
 __device__ __forceinline__ void dl3_set_ec(const Dl3Tab &t, int i, float e, int c) {
@@ -154,6 +155,7 @@ constexpr int DL3_MAXCH = 4096;
 struct Dl3Chunks {
     float e[DL3_MAXCH];
     int j[DL3_MAXCH];
+    int c[DL3_MAXCH];  // cc of entry j (so the merge's c2 needs no table read)
     unsigned bits[DL3_MAXCH / 32];
     int dirty[DL3_MAXCH];
     int n, sh;  // dirty count; log2 of the chunk size
@@ -283,6 +285,7 @@ struct Dl3List {
 };
 struct Dl3Batch {  // the batched recount's per-item state (tables that do not use the grid)
     uint2 qn[DL3_LCAP];
+    uint4 v[DL3_LCAP];
     unsigned long long slot[DL3_LCAP];
     int pre[DL3_LCAP + 1];  // exclusive prefix of the items' unit counts
     int wsum[DL3_W];
@@ -306,6 +309,7 @@ __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const
             const int i = base ? glist[base + tid] : L->item[tid];
             if (base) L->item[tid] = i;  // the previous batch's readers passed its last barrier
             B->qn[tid] = t.QN[i];
+            B->v[tid] = t.V[i];
             B->slot[tid] = DL3_NONE;
             units = (tot - 1 - i + 63) >> 6;
         }
@@ -334,26 +338,31 @@ __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const
                 hi = mid - 1;
             }
         }
-        for (int u0 = ua; u0 < ub; u0 += DL3_U) {
-            uint2 r[DL3_U];
-            int qq[DL3_U], jj[DL3_U];
+        // DL3_UL candidates per lane in flight; each candidate's (item, index) is recomputed after the loads from
+        // the unit cursor (LDS) instead of being held in registers
+        for (int u0 = ua; u0 < ub; u0 += DL3_UL) {
+            uint2 r[DL3_UL];
+            const int q0 = q;
 #pragma unroll
-            for (int u = 0; u < DL3_U; u++) {
+            for (int u = 0; u < DL3_UL; u++) {
                 const int uu = u0 + u;
                 while (q < nb - 1 && B->pre[q + 1] <= uu) q++;
-                qq[u] = q;
-                jj[u] = uu < ub ? L->item[q] + 1 + ((uu - B->pre[q]) << 6) + lane : tot;
-                r[u] = t.QN[min(jj[u], tot - 1)];
+                const int jj = uu < ub ? L->item[q] + 1 + ((uu - B->pre[q]) << 6) + lane : tot;
+                r[u] = t.QN[min(jj, tot - 1)];
             }
+            q = q0;
 #pragma unroll
-            for (int u = 0; u < DL3_U; u++) {
-                if (jj[u] >= tot) continue;
-                const float eb = __uint_as_float((uint32_t)(B->slot[qq[u]] >> 32));
-                const uint2 a = B->qn[qq[u]];
+            for (int u = 0; u < DL3_UL; u++) {
+                const int uu = u0 + u;
+                while (q < nb - 1 && B->pre[q + 1] <= uu) q++;
+                const int jj = uu < ub ? L->item[q] + 1 + ((uu - B->pre[q]) << 6) + lane : tot;
+                if (jj >= tot) continue;
+                const float eb = __uint_as_float((uint32_t)(B->slot[q] >> 32));
+                const uint2 a = B->qn[q];
                 if (dl3_cannot(a.x, a.y, r[u].x, r[u].y, eb)) continue;
-                const float cur = dl3_calc_err(dl3_entry(a, t.V[L->item[qq[u]]]), dl3_entry(r[u], t.V[jj[u]]));
+                const float cur = dl3_calc_err(dl3_entry(a, B->v[q]), dl3_entry(r[u], t.V[jj]));
                 if (cur <= eb)
-                    atomicMin(&B->slot[qq[u]], ((unsigned long long)__float_as_uint(cur) << 32) | (uint32_t)jj[u]);
+                    atomicMin(&B->slot[q], ((unsigned long long)__float_as_uint(cur) << 32) | (uint32_t)jj);
             }
         }
         __syncthreads();
@@ -710,7 +719,7 @@ __device__ void dl3_recount_grid(const Dl3Tab &t, Dl3Grid *G, const uint4 *mem, 
 __device__ void dl3_chunk_min(const Dl3Tab &t, Dl3Chunks *ch, int c, int tot) {
     const int b = c << ch->sh, e = min(tot, b + (1 << ch->sh));
     float v = HUGE_VALF;
-    int j = INT32_MAX;
+    int j = INT32_MAX, cc = 0;
     for (int i0 = b + (int)(threadIdx.x & 63); i0 < e; i0 += 64 * DL3_U) {
         uint2 r[DL3_U];
 #pragma unroll
@@ -721,13 +730,24 @@ __device__ void dl3_chunk_min(const Dl3Tab &t, Dl3Chunks *ch, int c, int tot) {
             if (i0 + u * 64 < e && x < v) {
                 v = x;
                 j = i0 + u * 64;
+                cc = (int)r[u].y;
             }
         }
     }
-    dl3_wave_min(v, j);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {  // dl3_wave_min carrying the winner's cc
+        const float v2 = __shfl_xor(v, o);
+        const int j2 = __shfl_xor(j, o), c2 = __shfl_xor(cc, o);
+        if (v2 < v || (v2 == v && j2 < j)) {
+            v = v2;
+            j = j2;
+            cc = c2;
+        }
+    }
     if ((threadIdx.x & 63) == 0) {
         ch->e[c] = v;
         ch->j[c] = j;
+        ch->c[c] = cc;
     }
 }
 
@@ -793,17 +813,6 @@ __device__ __forceinline__ void dl3_fixup(const Dl3Tab &t, Dl3List *L, int *glis
     }
 }
 
-__device__ __forceinline__ Dl3Merge dl3_merge_ctx(const Dl3Tab &t, int c1, int c2, int tot) {
-    Dl3Merge m;
-    m.c1 = c1;
-    m.c2 = c2;
-    m.tot = tot;
-    m.c2v = c2 != tot;
-    m.b1 = dl3_load(t, c1);
-    m.b2 = dl3_load(t, m.c2v ? c2 : c1);
-    return m;
-}
-
 // One merge's fix-ups (quantizer.c:631-642) as one pass with each entry in its own lane.  The reference's loops --
 // re-point i < c1 from the moved entry to c1; recount_next(i) for i > c1 pointing at it; recount_dist(c1); then
 // recount_dist(c2) unless c2 was the last entry -- only ever change entry i from entry i's own state and table data
@@ -812,9 +821,8 @@ __device__ __forceinline__ Dl3Merge dl3_merge_ctx(const Dl3Tab &t, int c1, int c
 // and c2 whenever a later step would compare against them (c1 < c2, and those steps only visit i < c1 or i < c2),
 // and a repeated recount gives the same result.  So an entry either joins the recount list, or takes the updates
 // with calc_err(i, c1) then calc_err(i, c2) (strictly smaller only, as the reference).
-__device__ void dl3_merge_pass(const Dl3Tab &t, Dl3List *L, int *glist, int c1, int c2, int tot, Dl3Chunks *ch,
-                               int lcap) {
-    const Dl3Merge m = dl3_merge_ctx(t, c1, c2, tot);
+__device__ void dl3_merge_pass(const Dl3Tab &t, Dl3List *L, int *glist, const Dl3Merge &m, Dl3Chunks *ch, int lcap) {
+    const int tot = m.tot;
     for (int i0 = threadIdx.x; i0 < tot; i0 += DL3_T * DL3_UM) {
         uint2 rq[DL3_UM], re[DL3_UM];
 #pragma unroll
@@ -836,10 +844,9 @@ __device__ void dl3_merge_pass(const Dl3Tab &t, Dl3List *L, int *glist, int c1, 
 // also staged in LDS for this merge's recounts), the last entry (always recounted: it points past the table), and
 // the members of the cells dl3_box_live keeps for the merge's points (old c1, old c2, old last, new c1, new c2),
 // found block by block, one wave per live block.  Every other entry's fix-ups are no-ops (dl3_box_live).
-__device__ void dl3_merge_pass_grid(const Dl3Tab &t, Dl3List *L, int *glist, int c1, int c2, int tot, Dl3Chunks *ch,
+__device__ void dl3_merge_pass_grid(const Dl3Tab &t, Dl3List *L, int *glist, const Dl3Merge &m, Dl3Chunks *ch,
                                     int lcap, Dl3Grid *G, const uint4 *mem) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const Dl3Merge m = dl3_merge_ctx(t, c1, c2, tot);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, tot = m.tot;
     if (tid < G->nx) {
         const int x = G->x[tid];
         const uint2 qn = t.QN[x];
@@ -911,11 +918,13 @@ __device__ void dl3_merge_pass_grid(const Dl3Tab &t, Dl3List *L, int *glist, int
 #define DL3_PROF(k)
 #endif
 
+template <bool GRID>
 __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
     __shared__ float sh_e[DL3_W];
     __shared__ int sh_j[DL3_W];
     __shared__ Dl3Chunks chs;
     __shared__ Dl3List lst;
+    __shared__ Dl3Merge sm;  // this merge's c1, c2 and their new entries (thread 0 -> everyone)
     __shared__ union {
         Dl3Batch b;
         Dl3Grid g;
@@ -935,7 +944,7 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
     t.QN += s, t.EC += s, t.V += s;
     int *glist = a.list + s;
     uint4 *mem = a.members + 2 * (size_t)s;
-    const bool use_grid = a.grid && n <= DL3_GMAX;
+    const bool use_grid = GRID && n <= DL3_GMAX;
     int sh = 0;
     while (((n + (1 << sh) - 1) >> sh) > DL3_MAXCH) sh++;
     if (threadIdx.x == 0) {
@@ -959,32 +968,47 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
         const int nch = (tot + (1 << sh) - 1) >> sh;
         for (int c = threadIdx.x; c < nch; c += DL3_T) dl3_min(e, j, ch->e[c], ch->j[c]);
         dl3_block_min(e, j, sh_e, sh_j);
-        if (j != INT32_MAX) c1 = j;
-        const int c2 = (int)t.EC[c1].y;
-        __syncthreads();  // every thread has read C[c1] and the chunk minima before they change
+        int c2;
+        if (j != INT32_MAX) {
+            c1 = j;
+            c2 = ch->c[j >> sh];  // the chunk minimum's cc
+        } else {
+            c2 = (int)t.EC[c1].y;
+        }
+        __syncthreads();  // every thread has read the chunk minima before they change
         tot--;
-        if (threadIdx.x == 0) {  // merge c1 into c2, the last entry into c1 (quantizer.c:619-629)
-            const uint2 q1 = t.QN[c1], q2 = t.QN[c2];
-            if (use_grid) {  // the fix-ups' query points: old c1, old c2, old last (then new c1, new c2 below)
-                G->pts[0] = q1;
-                G->pts[1] = q2;
-                G->pts[2] = t.QN[tot];
-            }
-            const uint4 v1 = t.V[c1], v2 = t.V[c2];
+        if (threadIdx.x == 0) {  // merge c1 into c2, the last entry into c1 (quantizer.c:619-629): one round of loads
+            const uint2 q1 = t.QN[c1], q2 = t.QN[c2], ql = t.QN[tot];
+            const uint4 v1 = t.V[c1], v2 = t.V[c2], vl = t.V[tot];
+            const uint2 el = t.EC[tot];
             const uint32_t r = v2.x + v1.x, g = v2.y + v1.y, b = v2.z + v1.z, nn = q2.y + q1.y;
-            t.V[c2] = make_uint4(r, g, b, 0u);
-            t.QN[c2] = make_uint2(dl3_setrgb(r, g, b, nn), nn);
-            // (after the c2 update: c2 may be the last entry)
-            t.V[c1] = t.V[tot];
-            t.QN[c1] = t.QN[tot];
-            t.EC[c1] = t.EC[tot];
+            const uint2 qm = make_uint2(dl3_setrgb(r, g, b, nn), nn);
+            const uint4 vm = make_uint4(r, g, b, 0u);
+            t.V[c2] = vm;
+            t.QN[c2] = qm;
+            // the last entry moves into c1 (after the c2 update: c2 may be the last entry)
+            const bool c2last = c2 == tot;
+            const uint2 qc1 = c2last ? qm : ql;
+            const uint4 vc1 = c2last ? vm : vl;
+            t.V[c1] = vc1;
+            t.QN[c1] = qc1;
+            t.EC[c1] = el;
             dl3_set_ec(t, tot - 1, HUGE_VALF, tot);
             L->n = 0;
-            if (use_grid) {
-                G->pts[3] = t.QN[c1];
-                G->pts[4] = t.QN[c2 != tot ? c2 : c1];
+            sm.c1 = c1;
+            sm.c2 = c2;
+            sm.tot = tot;
+            sm.c2v = !c2last;
+            sm.b1 = dl3_entry(qc1, vc1);
+            sm.b2 = c2last ? sm.b1 : dl3_entry(qm, vm);
+            if (use_grid) {  // the fix-ups' query points: old c1, old c2, old last, new c1, new c2
+                G->pts[0] = q1;
+                G->pts[1] = q2;
+                G->pts[2] = ql;
+                G->pts[3] = qc1;
+                G->pts[4] = c2last ? qc1 : qm;
                 dl3_grid_touch(G, c1);
-                if (c2 != tot) dl3_grid_touch(G, c2);
+                if (!c2last) dl3_grid_touch(G, c2);
             }
             dl3_mark(ch, c1);
             dl3_mark(ch, tot - 1);
@@ -993,10 +1017,13 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
         __syncthreads();
         if (use_grid && G->rebuild) dl3_grid_build(t, G, mem, tot);
         DL3_PROF(0)
-        if (use_grid)
-            dl3_merge_pass_grid(t, L, glist, c1, c2, tot, ch, a.lcap, G, mem);
-        else
-            dl3_merge_pass(t, L, glist, c1, c2, tot, ch, a.lcap);
+        {
+            const Dl3Merge m = sm;
+            if (use_grid)
+                dl3_merge_pass_grid(t, L, glist, m, ch, a.lcap, G, mem);
+            else
+                dl3_merge_pass(t, L, glist, m, ch, a.lcap);
+        }
         __syncthreads();
         DL3_PROF(1)
 #ifdef TILER_EXPERIMENTS
@@ -1033,7 +1060,7 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
 }  // namespace
 
 static std::atomic<int> g_dl3_lcap{DL3_LCAP};  // tiler_debug_dl3
-static std::atomic<int> g_dl3_grid{1};
+static std::atomic<int> g_dl3_grid{0};
 void dl3_debug(int list_cap, int grid) {
     g_dl3_lcap.store(list_cap > 0 ? list_cap : DL3_LCAP);
     g_dl3_grid.store(grid != 0);
@@ -1273,7 +1300,10 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
                 hipSuccess)
                 break;
 #endif
-            hipLaunchKernelGGL(dl3_reduce_kernel, dim3(P), dim3(DL3_T), 0, stream, ra);
+            if (ra.grid)
+                hipLaunchKernelGGL(dl3_reduce_kernel<true>, dim3(P), dim3(DL3_T), 0, stream, ra);
+            else
+                hipLaunchKernelGGL(dl3_reduce_kernel<false>, dim3(P), dim3(DL3_T), 0, stream, ra);
             if (hipGetLastError() != hipSuccess) break;
 #ifdef TILER_EXPERIMENTS
             if (getenv("TILER_DL3_PROF")) {  // the largest pair's phase split

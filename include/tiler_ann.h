@@ -253,10 +253,9 @@ int tiler_quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_
                                 int n_palettes, int palsize, int lookup_bpc, int32_t *palettes, int32_t *use_count,
                                 int32_t *colors, void *stream);
 /* Test hook (process-wide) for the DLv3 merges: at most list_cap listed recount_next entries are kept in LDS
- * (list_cap <= 0 or above the built-in 1024 restores 1024; a smaller cap runs the global-memory overflow and the
- * multi-batch path on small tables); grid = 1 makes tables of up to 65,536 colours take the colour-grid scans
- * (measured slower), 0 the default batched linear scans.  Results are identical for every setting.  0. */
-int tiler_debug_dl3(int list_cap, int grid);
+ * (list_cap <= 0 or above the built-in 1024 restores 1024); a smaller cap runs the global-memory overflow and the
+ * multi-batch path on small tables.  Results are identical for every cap.  0. */
+int tiler_debug_dl3(int list_cap);
 /* PrepareDitherTiles for one keyframe (main.pas:2097-2152): ComputeTilePsyVisFeatures(UseLAB, use_wavelets,
  * gamma) of its n_tiles RGB tiles (frame order), then the k-means of yakmo_create(n_palettes, 1, MaxInt, k-means++,
  * seed, no normalisation) -> labels[n_tiles] (DitheringPalIndex), centroids[n_palettes][192] (PaletteCentroids),

@@ -68,19 +68,18 @@ def test_quantize_clustered_long_recount_lists(gpu, oracle):
     _check(oracle, rgb, pal_of, 3)
 
 
-@pytest.mark.parametrize("cap,grid", [(1, 0), (3, 0), (64, 0), (0, 1), (1, 1), (3, 1)])
-def test_quantize_list_overflow(gpu, oracle, cap, grid):
+@pytest.mark.parametrize("cap", [1, 3, 64])
+def test_quantize_list_overflow(gpu, oracle, cap):
     """tiler_debug_dl3: with at most `cap` recount entries per LDS batch the merges' lists spill to the global
-    overflow (and, without the grid, run in several batches); grid = 1 is the colour-grid path (an alternative kept
-    for A/B), 0 the default batched linear scans.  Palettes stay bit-exact."""
+    overflow and run in several batches; palettes stay bit-exact."""
     from tiler_amd import load
     lib = load()
     rgb, pal_of, pairs = _case(5, (2,), 90, 3)
-    assert lib.tiler_debug_dl3(cap, grid) == 0
+    assert lib.tiler_debug_dl3(cap) == 0
     try:
         _check(oracle, rgb, pal_of, pairs)
     finally:
-        lib.tiler_debug_dl3(0, 0)
+        lib.tiler_debug_dl3(0)
 
 
 @pytest.mark.parametrize("gamma", [-1, 0])

@@ -88,7 +88,7 @@ _SIGS = {
     "tiler_kmodes_medoids_batch": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                            c_void_p]),
     "tiler_debug_kmodes_ff_fallback": (c_int, [c_int]),
-    "tiler_debug_dl3": (c_int, [c_int, c_int]),
+    "tiler_debug_dl3": (c_int, [c_int]),
     "tiler_kmodes_last_stats": (c_int, [P(ctypes.c_int64), P(ctypes.c_int64)]),
     "tiler_kmodes_compute": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),

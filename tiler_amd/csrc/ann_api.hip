@@ -851,8 +851,8 @@ int tiler_quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_
                                  use_count, colors, (hipStream_t)stream);
 }
 
-int tiler_debug_dl3(int list_cap, int grid) {
-    dl3_debug(list_cap, grid);
+int tiler_debug_dl3(int list_cap) {
+    dl3_debug(list_cap);
     return 0;
 }
 

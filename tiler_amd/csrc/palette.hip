@@ -62,8 +62,6 @@ struct Dl3Tab {
 };
 constexpr int DL3_U = 6;   // records loaded per lane before any is used
 constexpr int DL3_UM = 4;  // the same in the merge pass (two records per entry)
-constexpr int DL3_UL = 12;  // candidates per lane in flight in the batched recount
-constexpr int DL3_UP = 2;  // members per lane in flight in the grid merge pass
 
 __device__ __forceinline__ void dl3_set_ec(const Dl3Tab &t, int i, float e, int c) {
     t.EC[i] = make_uint2(__float_as_uint(e), (uint32_t)c);
@@ -266,9 +264,7 @@ struct Dl3Args {
     const int *seg;
     int quant_to;
     int *list;       // [entries] recount-list overflow (a pair's slice at its seg offset)
-    uint4 *members;  // [entries][2] the grid's cell-sorted copies (j, Q, N; r, g, b) (a pair's slice at 2 seg)
     int lcap;        // recount-list entries held in LDS per batch (DL3_LCAP; smaller only by the test hook)
-    int grid;        // tables up to DL3_GMAX entries recount through the grid (0 only by the test hook)
     int32_t *pal;    // [P][quant_to] 0x00BBGGRR
 };
 
@@ -283,7 +279,7 @@ struct Dl3List {
     int item[DL3_LCAP];
     int n;  // listed entries (those >= lcap in the global overflow)
 };
-struct Dl3Batch {  // the batched recount's per-item state (tables that do not use the grid)
+struct Dl3Batch {  // the batched recount's per-item state
     uint2 qn[DL3_LCAP];
     uint4 v[DL3_LCAP];
     unsigned long long slot[DL3_LCAP];
@@ -338,31 +334,26 @@ __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const
                 hi = mid - 1;
             }
         }
-        // DL3_UL candidates per lane in flight; each candidate's (item, index) is recomputed after the loads from
-        // the unit cursor (LDS) instead of being held in registers
-        for (int u0 = ua; u0 < ub; u0 += DL3_UL) {
-            uint2 r[DL3_UL];
-            const int q0 = q;
+        for (int u0 = ua; u0 < ub; u0 += DL3_U) {
+            uint2 r[DL3_U];
+            int qq[DL3_U], jj[DL3_U];
 #pragma unroll
-            for (int u = 0; u < DL3_UL; u++) {
+            for (int u = 0; u < DL3_U; u++) {
                 const int uu = u0 + u;
                 while (q < nb - 1 && B->pre[q + 1] <= uu) q++;
-                const int jj = uu < ub ? L->item[q] + 1 + ((uu - B->pre[q]) << 6) + lane : tot;
-                r[u] = t.QN[min(jj, tot - 1)];
+                qq[u] = q;
+                jj[u] = uu < ub ? L->item[q] + 1 + ((uu - B->pre[q]) << 6) + lane : tot;
+                r[u] = t.QN[min(jj[u], tot - 1)];
             }
-            q = q0;
 #pragma unroll
-            for (int u = 0; u < DL3_UL; u++) {
-                const int uu = u0 + u;
-                while (q < nb - 1 && B->pre[q + 1] <= uu) q++;
-                const int jj = uu < ub ? L->item[q] + 1 + ((uu - B->pre[q]) << 6) + lane : tot;
-                if (jj >= tot) continue;
-                const float eb = __uint_as_float((uint32_t)(B->slot[q] >> 32));
-                const uint2 a = B->qn[q];
+            for (int u = 0; u < DL3_U; u++) {
+                if (jj[u] >= tot) continue;
+                const float eb = __uint_as_float((uint32_t)(B->slot[qq[u]] >> 32));
+                const uint2 a = B->qn[qq[u]];
                 if (dl3_cannot(a.x, a.y, r[u].x, r[u].y, eb)) continue;
-                const float cur = dl3_calc_err(dl3_entry(a, B->v[q]), dl3_entry(r[u], t.V[jj]));
+                const float cur = dl3_calc_err(dl3_entry(a, B->v[qq[u]]), dl3_entry(r[u], t.V[jj[u]]));
                 if (cur <= eb)
-                    atomicMin(&B->slot[q], ((unsigned long long)__float_as_uint(cur) << 32) | (uint32_t)jj);
+                    atomicMin(&B->slot[qq[u]], ((unsigned long long)__float_as_uint(cur) << 32) | (uint32_t)jj[u]);
             }
         }
         __syncthreads();
@@ -377,343 +368,9 @@ __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const
 }
 
 #ifdef TILER_EXPERIMENTS
-// per pair: phase wall-clock ticks (100 MHz), merges, list entries; grid-recount split (experiment build only)
-__device__ unsigned long long g_dl3_prof[1024][16];
-#define DL3_GPROF(k, v) \
-    if (lane == 0 && blockIdx.x < 1024) atomicAdd(&g_dl3_prof[blockIdx.x][k], (unsigned long long)(v));
-#else
-#define DL3_GPROF(k, v)
+// per pair: phase wall-clock ticks (100 MHz), merges, list entries (experiment build only)
+__device__ unsigned long long g_dl3_prof[1024][6];
 #endif
-
-// The colour grid of the recount_next scans: 16 x 16 x 16 cells over Q (cells of 16^3 colour values) in 4 x 4 x 4
-// blocks of 4^3 cells, built over the whole table every so often; members are (j, Q, N, r, g, b) copies sorted by
-// cell.  Entries whose Q or N changed since the build (each merge changes c2, and moves the last entry into c1) are
-// "changed": skipped in the cells and kept in a short list every scan visits.  For a cell or block,
-// dist(Q_i, its box) * min(P_i, its members' min N) <= every member's bound (dl3_cannot), so a scan visits i's own
-// and the 26 neighbouring cells plus the changed list, then the blocks, then the cells of the surviving blocks that
-// the bound cannot exclude.  Candidates are folded by (err, index) first minimum, so the order of visits does not
-// change any result.  recount_next over a short range (<= DL3_SHORT candidates) scans it directly.
-constexpr int DL3_GC = 4096;     // cells
-constexpr int DL3_GMAX = 65536;  // tables up to this many entries use the grid (the changed bitset is in LDS)
-constexpr int DL3_XCAP = 128;    // changed entries before a rebuild
-constexpr int DL3_SHORT = 256;
-constexpr int DL3_WCAP = 64;     // cells a wave collects before scanning their members
-constexpr int DL3_NPTS = 5;      // the merge's query points (dl3_merge_pass_grid)
-struct Dl3Grid {
-    int end[DL3_GC];           // members of cell c: [c ? end[c - 1] : 0, end[c])
-    uint32_t minp[DL3_GC];     // smallest N of the cell's members at the build
-    int bcnt[64];              // members per block
-    uint32_t bminp[64];
-    uint32_t changed[DL3_GMAX / 32];
-    int x[DL3_XCAP];           // the changed entries, and their current QN / V (loaded by every merge pass)
-    uint2 xqn[DL3_XCAP];
-    uint4 xv[DL3_XCAP];
-    uint32_t gminp;            // smallest N of all members at the build
-    // upper bounds of err and err / N over the members of each cell / block (not the last entry, not the changed
-    // ones): set at the build, raised by every later write of a member's err (float bits: err >= 0)
-    uint32_t maxe[DL3_GC], maxep[DL3_GC], bmaxe[64], bmaxep[64];
-    uint2 pts[DL3_NPTS];       // this merge's query points (Q, N)
-    int wb[DL3_W][DL3_WCAP];   // per wave: collected cells' first member, and the exclusive prefix of their sizes
-    int wp[DL3_W][DL3_WCAP + 1];
-    int wsum[DL3_W];
-    int nx, rebuild;
-};
-
-__device__ __forceinline__ int dl3_cell(uint32_t q) { return ((q >> 4) & 15) | ((q >> 8) & 0xf0) | ((q >> 12) & 0xf00); }
-
-__device__ __forceinline__ int dl3_block_of(int c) { return ((c >> 2) & 3) | ((c >> 4) & 0xc) | ((c >> 6) & 0x30); }
-
-// block-wide (re)build over entries [0, tot)
-__device__ void dl3_grid_build(const Dl3Tab &t, Dl3Grid *G, uint4 *mem, int tot) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int c = tid; c < DL3_GC; c += DL3_T) {
-        G->end[c] = 0;
-        G->minp[c] = 0xffffffffu;
-    }
-    for (int c = tid; c < DL3_GC; c += DL3_T) G->maxe[c] = G->maxep[c] = 0u;
-    if (tid < 64) {
-        G->bcnt[tid] = 0;
-        G->bminp[tid] = 0xffffffffu;
-        G->bmaxe[tid] = G->bmaxep[tid] = 0u;
-    }
-    for (int k = tid; k < (tot + 31) / 32; k += DL3_T) G->changed[k] = 0;
-    __syncthreads();  // every thread has read G->rebuild
-    if (tid == 0) {
-        G->nx = G->rebuild = 0;
-        G->gminp = 0xffffffffu;
-    }
-    for (int j = tid; j < tot; j += DL3_T) {
-        const uint2 qn = t.QN[j];
-        const int c = dl3_cell(qn.x);
-        atomicAdd(&G->end[c], 1);
-        atomicMin(&G->minp[c], qn.y);
-        if (j < tot - 1) {  // the last entry's err is HUGE_VALF; it is visited explicitly
-            const float e = __uint_as_float(t.EC[j].x);
-            atomicMax(&G->maxe[c], __float_as_uint(e));
-            atomicMax(&G->maxep[c], __float_as_uint(e / (float)qn.y));
-        }
-    }
-    __syncthreads();
-    constexpr int PER = DL3_GC / DL3_T;  // cells per thread in the scan
-    int v[PER], sum = 0;
-#pragma unroll
-    for (int u = 0; u < PER; u++) {
-        const int c = tid * PER + u;
-        sum += (v[u] = G->end[c]);
-        if (v[u]) {
-            const int b = dl3_block_of(c);
-            atomicAdd(&G->bcnt[b], v[u]);
-            atomicMin(&G->bminp[b], G->minp[c]);
-            atomicMin(&G->gminp, G->minp[c]);
-            atomicMax(&G->bmaxe[b], G->maxe[c]);
-            atomicMax(&G->bmaxep[b], G->maxep[c]);
-        }
-    }
-    int inc = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int x = __shfl_up(inc, o);
-        if (lane >= o) inc += x;
-    }
-    if (lane == 63) G->wsum[w] = inc;
-    __syncthreads();
-    int off = inc - sum;
-    for (int k = 0; k < w; k++) off += G->wsum[k];
-#pragma unroll
-    for (int u = 0; u < PER; u++) {
-        G->end[tid * PER + u] = off;  // the cell's first position; the scatter moves it to its end
-        off += v[u];
-    }
-    __syncthreads();
-    for (int j = tid; j < tot; j += DL3_T) {
-        const uint2 qn = t.QN[j];
-        const uint4 vv = t.V[j];
-        const int pos = atomicAdd(&G->end[dl3_cell(qn.x)], 1);
-        mem[2 * pos] = make_uint4((uint32_t)j, qn.x, qn.y, 0u);
-        mem[2 * pos + 1] = vv;
-    }
-    __syncthreads();
-}
-
-__device__ __forceinline__ void dl3_grid_touch(Dl3Grid *G, int i) {  // one thread: entry i's Q / N changed
-    const uint32_t m = 1u << (i & 31);
-    if (G->changed[i >> 5] & m) return;
-    G->changed[i >> 5] |= m;
-    G->x[G->nx++] = i;
-    if (G->nx > DL3_XCAP - 2) G->rebuild = 1;
-}
-
-__device__ __forceinline__ int dl3_gap(int v, int lo, int hi) { return v < lo ? lo - v : (v > hi ? v - hi : 0); }
-
-// a member's err was written (not the last entry, not a changed one)
-__device__ __forceinline__ void dl3_stat(Dl3Grid *G, uint32_t q, uint32_t n, float e) {
-    const int c = dl3_cell(q), b = dl3_block_of(c);
-    const uint32_t eb = __float_as_uint(e), pb = __float_as_uint(e / (float)n);
-    atomicMax(&G->maxe[c], eb);
-    atomicMax(&G->maxep[c], pb);
-    atomicMax(&G->bmaxe[b], eb);
-    atomicMax(&G->bmaxep[b], pb);
-}
-
-// Can a member i of the box [lo, lo + size)^3 need this merge's fix-ups?  Only if it points at one of the merge's
-// old entries x (old c1, c2, last) -- then err_i = calc_err(i, x) -- or calc_err(i, x) < err_i for a new one (new
-// c1, c2); either way min(P_i, P_x) * |Q_i - Q_x| * (1 - 6e-7) <= err_i (dl3_cannot), i.e.
-// |Q_i - Q_x| <= max(err_i / P_i, err_i / P_x) up to that factor.  With the box's bounds of err and err / N the
-// box is out for every point when dist^2 * 0.9998 exceeds both maxep^2 and (maxe / P_x)^2 (the factor covers the
-// float evaluation of both sides with a wide margin; an infinite bound keeps the box).
-__device__ __forceinline__ bool dl3_box_live(const Dl3Grid *G, int lr, int lg, int lb, int size, uint32_t maxe,
-                                             uint32_t maxep) {
-    const float me = __uint_as_float(maxe), mp = __uint_as_float(maxep);
-#pragma unroll
-    for (int k = 0; k < DL3_NPTS; k++) {
-        const uint2 x = G->pts[k];
-        const int gr = dl3_gap((int)(x.x & 255), lr, lr + size - 1), gg = dl3_gap((int)((x.x >> 8) & 255), lg, lg + size - 1);
-        const int gb = dl3_gap((int)((x.x >> 16) & 255), lb, lb + size - 1);
-        const float d2 = (float)(gr * gr + gg * gg + gb * gb) * 0.9998f, n = (float)x.y;
-        if (!(d2 > mp * mp) || !(d2 * n * n > me * me)) return true;
-    }
-    return false;
-}
-
-// as dl3_cannot for every member of a box: dd = squared distance from Q_a to the box, nb = its members' min N
-__device__ __forceinline__ bool dl3_cannot_dd(int dd, uint32_t na, uint32_t nb, float e) {
-    const float m = (float)(na < nb ? na : nb);
-    return (float)dd * m * m * 0.99999f > e * e;
-}
-
-// append this lane's cell (cn members from cb; cn = 0: none) to the wave's collection (wave-uniform call)
-__device__ __forceinline__ void dl3_collect(int *wb, int *wp, int lane, int cb, int cn, int &nc, int &nt) {
-    const unsigned long long bal = __ballot(cn > 0);
-    int p = cn;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int x = __shfl_up(p, o);
-        if (lane >= o) p += x;
-    }
-    if (cn > 0) {
-        const int pos = nc + (int)__popcll(bal & ((1ull << lane) - 1ull));
-        wb[pos] = cb;
-        wp[pos] = nt + p - cn;
-    }
-    nc += (int)__popcll(bal);
-    nt += __shfl(p, 63);
-}
-
-// the collection's member index of position k (< nt): the last cell q with wp[q] <= k
-__device__ __forceinline__ int dl3_member_at(const int *wb, const int *wp, int nc, int k) {
-    int lo = 0, hi = nc - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (wp[mid] <= k)
-            lo = mid;
-        else
-            hi = mid - 1;
-    }
-    return wb[lo] + k - wp[lo];
-}
-
-// recount_next(i) by one wave through the grid; lane 0 stores the result and marks its chunk
-__device__ void dl3_recount_grid(const Dl3Tab &t, Dl3Grid *G, const uint4 *mem, int i, int tot, Dl3Chunks *ch) {
-    const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
-#ifdef TILER_EXPERIMENTS
-    unsigned long long t0 = wall_clock64(), t1 = t0, t2 = t0;
-#endif
-    const Dl3Entry a = dl3_load(t, i);
-    float e = HUGE_VALF;
-    int j = INT32_MAX;
-    auto eval = [&](int k, const Dl3Entry &b) {
-        if (dl3_cannot(a.q, a.n, b.q, b.n, e)) return;
-        dl3_min(e, j, dl3_calc_err(a, b), k);
-    };
-    auto member_ok = [&](int jj) { return jj > i && jj < tot && !((G->changed[jj >> 5] >> (jj & 31)) & 1u); };
-    int *wb = G->wb[w], *wp = G->wp[w];
-    // scan the members of the collected cells [0, nc) (nt members), DL3_UM per lane in flight
-    auto flush = [&](int nc, int nt) {
-        DL3_GPROF(10, 1)
-        DL3_GPROF(11, nt)
-        for (int k0 = 0; k0 < nt; k0 += 64 * DL3_UM) {
-            uint4 m0[DL3_UM];
-            int ix[DL3_UM];
-#pragma unroll
-            for (int u = 0; u < DL3_UM; u++) {
-                const int k = k0 + u * 64 + lane;
-                m0[u].x = 0x7fffffffu;
-                ix[u] = 0;
-                if (k < nt) {
-                    ix[u] = dl3_member_at(wb, wp, nc, k);
-                    m0[u] = mem[2 * ix[u]];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < DL3_UM; u++) {
-                const int jj = (int)m0[u].x;
-                if (!member_ok(jj) || dl3_cannot(a.q, a.n, m0[u].y, m0[u].z, e)) continue;
-                const uint4 v = mem[2 * ix[u] + 1];  // the member's r, g, b: only for the survivors
-                dl3_min(e, j, dl3_calc_err(a, Dl3Entry{v.x, v.y, v.z, m0[u].z, m0[u].y}), jj);
-            }
-        }
-    };
-    auto collect = [&](int cb, int cn, int &nc, int &nt) { dl3_collect(wb, wp, lane, cb, cn, nc, nt); };
-    if (tot - 1 - i <= DL3_SHORT) {
-        for (int k0 = i + 1 + lane; k0 < tot; k0 += 64 * DL3_UM) {
-            uint2 r[DL3_UM];
-#pragma unroll
-            for (int u = 0; u < DL3_UM; u++) r[u] = t.QN[min(k0 + u * 64, tot - 1)];
-#pragma unroll
-            for (int u = 0; u < DL3_UM; u++) {
-                const int k = k0 + u * 64;
-                if (k < tot && !dl3_cannot(a.q, a.n, r[u].x, r[u].y, e))
-                    dl3_min(e, j, dl3_calc_err(a, dl3_entry(r[u], t.V[k])), k);
-            }
-        }
-    } else {
-        const int ar = a.q & 255, ag = (a.q >> 8) & 255, ab = (a.q >> 16) & 255;
-        const int cx = ar >> 4, cy = ag >> 4, cz = ab >> 4;
-        // round 1: the changed entries (their data in LDS), and the 27 cells around i's own (lanes 0..26)
-        const int nx = G->nx;
-        for (int k = lane; k < nx; k += 64) {
-            const int jj = G->x[k];
-            if (jj > i && jj < tot) eval(jj, dl3_entry(G->xqn[k], G->xv[k]));
-        }
-        int nc = 0, nt = 0;
-        {
-            int cb = 0, cn = 0;
-            if (lane < 27) {
-                const int x = cx + lane % 3 - 1, y = cy + (lane / 3) % 3 - 1, z = cz + lane / 9 - 1;
-                if (x >= 0 && x < 16 && y >= 0 && y < 16 && z >= 0 && z < 16) {
-                    const int c = x | (y << 4) | (z << 8);
-                    cb = c ? G->end[c - 1] : 0;
-                    cn = G->end[c] - cb;
-                }
-            }
-            collect(cb, cn, nc, nt);
-            flush(nc, nt);
-        }
-        dl3_wave_min(e, j);
-#ifdef TILER_EXPERIMENTS
-        t1 = wall_clock64();
-#endif
-        // every member outside the 27 cells is at least `gap` from Q_i on some axis (the grid's edges aside) and
-        // has N >= the build's minimum
-        int gap = 256;
-        if (cx > 0) gap = min(gap, ar - ((cx - 1) << 4) + 1);
-        if (cx < 15) gap = min(gap, ((cx + 2) << 4) - ar);
-        if (cy > 0) gap = min(gap, ag - ((cy - 1) << 4) + 1);
-        if (cy < 15) gap = min(gap, ((cy + 2) << 4) - ag);
-        if (cz > 0) gap = min(gap, ab - ((cz - 1) << 4) + 1);
-        if (cz < 15) gap = min(gap, ((cz + 2) << 4) - ab);
-        if (!dl3_cannot_dd(gap * gap, a.n, G->gminp, e)) {
-            // round 2: blocks (lane = block) the bound cannot exclude, then their cells outside round 1's
-            const int bx = lane & 3, by = (lane >> 2) & 3, bz = lane >> 4;
-            const int bd = dl3_gap(ar, bx << 6, (bx << 6) + 63), bg = dl3_gap(ag, by << 6, (by << 6) + 63);
-            const int bb = dl3_gap(ab, bz << 6, (bz << 6) + 63);
-            unsigned long long live =
-                __ballot(G->bcnt[lane] > 0 && !dl3_cannot_dd(bd * bd + bg * bg + bb * bb, a.n, G->bminp[lane], e));
-            nc = nt = 0;
-            DL3_GPROF(12, __popcll(live))
-            while (live) {
-                const int blk = (int)__builtin_ctzll(live);
-                live &= live - 1;
-                const int x = ((blk & 3) << 2) | (lane & 3), y = (((blk >> 2) & 3) << 2) | ((lane >> 2) & 3);
-                const int z = ((blk >> 4) << 2) | (lane >> 4);
-                const int c = x | (y << 4) | (z << 8);
-                int cb = 0, cn = 0;
-                if (max(abs(x - cx), max(abs(y - cy), abs(z - cz))) >= 2) {
-                    const int b0 = c ? G->end[c - 1] : 0, n0 = G->end[c] - b0;
-                    const int gx = dl3_gap(ar, x << 4, (x << 4) + 15), gy = dl3_gap(ag, y << 4, (y << 4) + 15);
-                    const int gz = dl3_gap(ab, z << 4, (z << 4) + 15);
-                    if (n0 > 0 && !dl3_cannot_dd(gx * gx + gy * gy + gz * gz, a.n, G->minp[c], e)) {
-                        cb = b0;
-                        cn = n0;
-                    }
-                }
-                if (nc + 64 > DL3_WCAP) {  // room for this block's cells
-                    flush(nc, nt);
-                    dl3_wave_min(e, j);
-                    nc = nt = 0;
-                }
-                collect(cb, cn, nc, nt);
-            }
-            flush(nc, nt);
-        }
-    }
-    dl3_wave_min(e, j);
-#ifdef TILER_EXPERIMENTS
-    t2 = wall_clock64();
-    if (tot - 1 - i <= DL3_SHORT) {
-        DL3_GPROF(6, 1)
-        DL3_GPROF(7, t2 - t0)
-    } else {
-        DL3_GPROF(8, t1 - t0)
-        DL3_GPROF(9, t2 - t1)
-    }
-#endif
-    if (lane == 0) {
-        dl3_set_ec(t, i, e, j == INT32_MAX ? 0 : j);
-        dl3_mark(ch, i);
-        if (i < tot - 1 && !((G->changed[i >> 5] >> (i & 31)) & 1u)) dl3_stat(G, a.q, a.n, e);
-    }
-}
 
 // the first minimum of chunk c over entries below tot, by one wave (lane 0 stores it)
 __device__ void dl3_chunk_min(const Dl3Tab &t, Dl3Chunks *ch, int c, int tot) {
@@ -751,14 +408,6 @@ __device__ void dl3_chunk_min(const Dl3Tab &t, Dl3Chunks *ch, int c, int tot) {
     }
 }
 
-// One merge's fix-ups (quantizer.c:631-642) as one pass with each entry in its own lane.  The reference's loops --
-// re-point i < c1 from the moved entry to c1; recount_next(i) for i > c1 pointing at it; recount_dist(c1); then
-// recount_dist(c2) unless c2 was the last entry -- only ever change entry i from entry i's own state and table data
-// none of them writes (QN, V are final once the merge is applied), so each entry's sequence of steps can run on its
-// own.  A recount_next makes every later step of the same entry a no-op: its scan over (i, tot) already covers c1
-// and c2 whenever a later step would compare against them (c1 < c2, and those steps only visit i < c1 or i < c2),
-// and a repeated recount gives the same result.  So an entry either joins the recount list, or takes the updates
-// with calc_err(i, c1) then calc_err(i, c2) (strictly smaller only, as the reference).
 struct Dl3Merge {  // one merge's fix-up context
     int c1, c2, tot;
     bool c2v;
@@ -768,7 +417,7 @@ struct Dl3Merge {  // one merge's fix-up context
 // entry i's fix-ups (qn, ec: its QN and EC; getv() its V): the list, or the updates written (G: stats to raise)
 template <class GetV>
 __device__ __forceinline__ void dl3_fixup(const Dl3Tab &t, Dl3List *L, int *glist, int lcap, Dl3Chunks *ch,
-                                          Dl3Grid *G, const Dl3Merge &m, int i, uint2 qn, uint2 ec, GetV getv) {
+                                          const Dl3Merge &m, int i, uint2 qn, uint2 ec, GetV getv) {
     int c = (int)ec.y;
     float e = __uint_as_float(ec.x);
     bool rc = false, wr = false;
@@ -809,7 +458,6 @@ __device__ __forceinline__ void dl3_fixup(const Dl3Tab &t, Dl3List *L, int *glis
     } else if (wr) {
         dl3_set_ec(t, i, e, c);
         dl3_mark(ch, i);
-        if (G) dl3_stat(G, qn.x, qn.y, e);
     }
 }
 
@@ -835,74 +483,7 @@ __device__ void dl3_merge_pass(const Dl3Tab &t, Dl3List *L, int *glist, const Dl
         for (int u = 0; u < DL3_UM; u++) {
             const int i = i0 + u * DL3_T;
             if (i >= tot) break;
-            dl3_fixup(t, L, glist, lcap, ch, nullptr, m, i, rq[u], re[u], [&]() { return t.V[i]; });
-        }
-    }
-}
-
-// The same through the grid: only entries that can need a fix-up are visited -- the changed entries (their data
-// also staged in LDS for this merge's recounts), the last entry (always recounted: it points past the table), and
-// the members of the cells dl3_box_live keeps for the merge's points (old c1, old c2, old last, new c1, new c2),
-// found block by block, one wave per live block.  Every other entry's fix-ups are no-ops (dl3_box_live).
-__device__ void dl3_merge_pass_grid(const Dl3Tab &t, Dl3List *L, int *glist, const Dl3Merge &m, Dl3Chunks *ch,
-                                    int lcap, Dl3Grid *G, const uint4 *mem) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, tot = m.tot;
-    if (tid < G->nx) {
-        const int x = G->x[tid];
-        const uint2 qn = t.QN[x];
-        const uint4 v = t.V[x];
-        const uint2 ec = t.EC[x];
-        G->xqn[tid] = qn;
-        G->xv[tid] = v;
-        if (x < tot - 1) dl3_fixup(t, L, glist, lcap, ch, nullptr, m, x, qn, ec, [&]() { return v; });
-    }
-    if (tid == DL3_T - 1) dl3_push(L, glist, tot - 1, lcap);
-    int *wb = G->wb[w], *wp = G->wp[w];
-    const int bx = lane & 3, by = (lane >> 2) & 3, bz = lane >> 4;
-    unsigned long long live =
-        __ballot(G->bcnt[lane] > 0 && dl3_box_live(G, bx << 6, by << 6, bz << 6, 64, G->bmaxe[lane], G->bmaxep[lane]));
-    for (int r = 0; live; r++) {
-        const int blk = (int)__builtin_ctzll(live);
-        live &= live - 1;
-        if ((r & (DL3_W - 1)) != w) continue;
-        const int x = ((blk & 3) << 2) | (lane & 3), y = (((blk >> 2) & 3) << 2) | ((lane >> 2) & 3);
-        const int z = ((blk >> 4) << 2) | (lane >> 4);
-        const int c = x | (y << 4) | (z << 8);
-        const int b0 = c ? G->end[c - 1] : 0, n0 = G->end[c] - b0;
-        const bool keep = n0 > 0 && dl3_box_live(G, x << 4, y << 4, z << 4, 16, G->maxe[c], G->maxep[c]);
-        int nc = 0, nt = 0;
-        dl3_collect(wb, wp, lane, keep ? b0 : 0, keep ? n0 : 0, nc, nt);
-        for (int k0 = 0; k0 < nt; k0 += 64 * DL3_UP) {
-            uint4 m0[DL3_UP];
-            uint2 ec[DL3_UP];
-            int ix[DL3_UP];
-#pragma unroll
-            for (int u = 0; u < DL3_UP; u++) {
-                const int k = k0 + u * 64 + lane;
-                m0[u].x = 0x7fffffffu;
-                ix[u] = 0;
-                if (k < nt) {
-                    ix[u] = dl3_member_at(wb, wp, nc, k);
-                    m0[u] = mem[2 * ix[u]];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < DL3_UP; u++) {
-                const int i = (int)m0[u].x;
-                if (i < tot - 1 && !((G->changed[i >> 5] >> (i & 31)) & 1u))
-                    ec[u] = t.EC[i];
-                else
-                    m0[u].x = 0x7fffffffu;
-            }
-#pragma unroll
-            for (int u = 0; u < DL3_UP; u++) {
-                const int i = (int)m0[u].x;
-                if (i != 0x7fffffff) {
-                    const uint4 *vp = mem + 2 * ix[u] + 1;
-                    dl3_fixup(t, L, glist, lcap, ch, G, m, i, make_uint2(m0[u].y, m0[u].z), ec[u],
-                              [&]() { return *vp; });
-                }
-            }
+            dl3_fixup(t, L, glist, lcap, ch, m, i, rq[u], re[u], [&]() { return t.V[i]; });
         }
     }
 }
@@ -918,21 +499,16 @@ __device__ void dl3_merge_pass_grid(const Dl3Tab &t, Dl3List *L, int *glist, con
 #define DL3_PROF(k)
 #endif
 
-template <bool GRID>
 __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
     __shared__ float sh_e[DL3_W];
     __shared__ int sh_j[DL3_W];
     __shared__ Dl3Chunks chs;
     __shared__ Dl3List lst;
     __shared__ Dl3Merge sm;  // this merge's c1, c2 and their new entries (thread 0 -> everyone)
-    __shared__ union {
-        Dl3Batch b;
-        Dl3Grid g;
-    } u;  // a table uses one of the two recount paths
+    __shared__ Dl3Batch bat;
     Dl3Chunks *ch = &chs;
     Dl3List *L = &lst;
-    Dl3Batch *B = &u.b;
-    Dl3Grid *G = &u.g;
+    Dl3Batch *B = &bat;
     const int p = blockIdx.x;
     const int s = a.seg[p], n = a.seg[p + 1] - s;
     if (n <= a.quant_to) {  // nothing to merge
@@ -943,8 +519,6 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
     Dl3Tab t = a.t;
     t.QN += s, t.EC += s, t.V += s;
     int *glist = a.list + s;
-    uint4 *mem = a.members + 2 * (size_t)s;
-    const bool use_grid = GRID && n <= DL3_GMAX;
     int sh = 0;
     while (((n + (1 << sh) - 1) >> sh) > DL3_MAXCH) sh++;
     if (threadIdx.x == 0) {
@@ -955,7 +529,6 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
     __syncthreads();
     for (int c = threadIdx.x >> 6; c < ((n + (1 << sh) - 1) >> sh); c += DL3_W) dl3_chunk_min(t, ch, c, n);
     __syncthreads();
-    if (use_grid) dl3_grid_build(t, G, mem, n);
     int tot = n, c1 = 0;
 #ifdef TILER_EXPERIMENTS
     unsigned long long prof_t = wall_clock64();
@@ -1001,42 +574,22 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
             sm.c2v = !c2last;
             sm.b1 = dl3_entry(qc1, vc1);
             sm.b2 = c2last ? sm.b1 : dl3_entry(qm, vm);
-            if (use_grid) {  // the fix-ups' query points: old c1, old c2, old last, new c1, new c2
-                G->pts[0] = q1;
-                G->pts[1] = q2;
-                G->pts[2] = ql;
-                G->pts[3] = qc1;
-                G->pts[4] = c2last ? qc1 : qm;
-                dl3_grid_touch(G, c1);
-                if (!c2last) dl3_grid_touch(G, c2);
-            }
             dl3_mark(ch, c1);
             dl3_mark(ch, tot - 1);
             dl3_mark(ch, tot);  // the removed entry leaves its chunk
         }
         __syncthreads();
-        if (use_grid && G->rebuild) dl3_grid_build(t, G, mem, tot);
         DL3_PROF(0)
         {
             const Dl3Merge m = sm;
-            if (use_grid)
-                dl3_merge_pass_grid(t, L, glist, m, ch, a.lcap, G, mem);
-            else
-                dl3_merge_pass(t, L, glist, m, ch, a.lcap);
+            dl3_merge_pass(t, L, glist, m, ch, a.lcap);
         }
         __syncthreads();
         DL3_PROF(1)
 #ifdef TILER_EXPERIMENTS
         if (threadIdx.x == 0 && p < 1024) g_dl3_prof[p][5] += L->n;
 #endif
-        if (use_grid) {
-            const int K = L->n;
-            for (int q = threadIdx.x >> 6; q < K; q += DL3_W)
-                dl3_recount_grid(t, G, mem, q < a.lcap ? L->item[q] : glist[q], tot, ch);
-            __syncthreads();
-        } else {
-            dl3_recount_list(t, L, B, glist, L->n, tot, ch, a.lcap);
-        }
+        dl3_recount_list(t, L, B, glist, L->n, tot, ch, a.lcap);
         DL3_PROF(2)
         // refresh the marked chunks (every mark above is complete: the list run ends in a barrier)
         const int nd = ch->n;
@@ -1060,10 +613,8 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
 }  // namespace
 
 static std::atomic<int> g_dl3_lcap{DL3_LCAP};  // tiler_debug_dl3
-static std::atomic<int> g_dl3_grid{0};
-void dl3_debug(int list_cap, int grid) {
+void dl3_debug(int list_cap) {
     g_dl3_lcap.store(list_cap > 0 ? list_cap : DL3_LCAP);
-    g_dl3_grid.store(grid != 0);
 }
 
 namespace {
@@ -1222,7 +773,7 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     const size_t np = (size_t)std::max(npix, 1);
     const size_t b_keys = 4 * np, b_sum = sizeof(Dl3Sum) * np, b_tmp = std::max(tmp_sort, tmp_red) + 256;
     const size_t bytes = 4 * b_keys /* keys, vals x2 */ + b_keys /* ukeys */ + b_sum + b_tmp + 4 * (P + 2) * 2 +
-                         16 * b_keys /* table, grid members (the list reuses a sort buffer) */ + 4 * (size_t)P * palsize + 4096;
+                         8 * b_keys /* table (the list reuses a sort buffer) */ + 4 * (size_t)P * palsize + 4096;
     char *ws = nullptr;
     TILER_HIP_CHECK(hipMalloc((void **)&ws, bytes));
     char *cur = ws;
@@ -1243,7 +794,6 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     t.QN = (uint2 *)take(2 * b_keys);
     t.EC = (uint2 *)take(2 * b_keys);
     t.V = (uint4 *)take(4 * b_keys);
-    uint4 *members = (uint4 *)take(8 * b_keys);
     int *d_list = (int *)k0;  // the sort buffers are free once the table exists
     int32_t *d_pal = (int32_t *)take(4 * (size_t)P * palsize);
     int rc = -1;
@@ -1290,24 +840,19 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
             ra.seg = d_seg;
             ra.quant_to = palsize;
             ra.list = d_list;
-            ra.members = members;
             ra.lcap = std::max(1, std::min(DL3_LCAP, g_dl3_lcap.load()));
-            ra.grid = g_dl3_grid.load();
             ra.pal = d_pal;
 #ifdef TILER_EXPERIMENTS
-            static unsigned long long zero[1024][16];
+            static unsigned long long zero[1024][6];
             if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dl3_prof), zero, sizeof(zero), 0, hipMemcpyHostToDevice, stream) !=
                 hipSuccess)
                 break;
 #endif
-            if (ra.grid)
-                hipLaunchKernelGGL(dl3_reduce_kernel<true>, dim3(P), dim3(DL3_T), 0, stream, ra);
-            else
-                hipLaunchKernelGGL(dl3_reduce_kernel<false>, dim3(P), dim3(DL3_T), 0, stream, ra);
+            hipLaunchKernelGGL(dl3_reduce_kernel, dim3(P), dim3(DL3_T), 0, stream, ra);
             if (hipGetLastError() != hipSuccess) break;
 #ifdef TILER_EXPERIMENTS
             if (getenv("TILER_DL3_PROF")) {  // the largest pair's phase split
-                static unsigned long long pr[1024][16];
+                static unsigned long long pr[1024][6];
                 if (hipMemcpyFromSymbolAsync(pr, HIP_SYMBOL(g_dl3_prof), sizeof(pr), 0, hipMemcpyDeviceToHost, stream) !=
                         hipSuccess ||
                     hipStreamSynchronize(stream) != hipSuccess)
@@ -1318,11 +863,6 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
                 fprintf(stderr, "dl3 pair %d colors %d merges %llu list/merge %.2f us: argmin+merge %.1f pass %.1f list %.1f chunks %.1f\n",
                         best, seg[best + 1] - seg[best], pr[best][4], (double)pr[best][5] / std::max(1ull, pr[best][4]),
                         pr[best][0] / 100.0, pr[best][1] / 100.0, pr[best][2] / 100.0, pr[best][3] / 100.0);
-                const double ng = std::max(1.0, (double)pr[best][5] - pr[best][6]);
-                fprintf(stderr, "  short %llu avg %.2f us | grid %.0f: round1 %.2f us round2 %.2f us, flushes %.2f, members %.1f, "
-                        "live blocks %.2f per recount\n", pr[best][6], pr[best][7] / 100.0 / std::max(1ull, pr[best][6]),
-                        ng, pr[best][8] / 100.0 / ng, pr[best][9] / 100.0 / ng, pr[best][10] / ng, pr[best][11] / ng,
-                        pr[best][12] / ng);
             }
 #endif
         }

@@ -2,7 +2,7 @@
 """Study of DLv3 pass 2 (palette.hip dl3_reduce_kernel) on bench.py's palette workload (8 frames of a 1080p shot,
 128 palettes).  Not part of the product.
 
-  python tools/dl3_study.py dump OUT.npz [grid] (GPU box) DitheringPalIndex of the 8 frames (k-means, GPU) + per-pair
+  python tools/dl3_study.py dump OUT.npz      (GPU box) DitheringPalIndex of the 8 frames (k-means, GPU) + per-pair
                                                DLv3 table sizes and the phase times
   python tools/dl3_study.py analyze OUT.npz   (host) per-pair sizes, and the restatement's time on the largest pairs
 """
@@ -32,8 +32,6 @@ def dump(path):
     from tiler_amd.palette import prepare_dither_tiles, quantize_palettes
     lib = tiler_amd.load()
     lib.tiler_init(0)
-    if len(sys.argv) > 3 and sys.argv[3] == "grid":
-        lib.tiler_debug_dl3(0, 1)
     pf = frames()
     prepare_dither_tiles(pf.reshape(-1, 64), P)  # warm
     lib.tiler_timing_reset()

@@ -60,8 +60,14 @@ struct Dl3Tab {
     uint2 *EC;  // x = E (err, float bits), y = C (cc)
     uint4 *V;   // x, y, z = CUBE3 r, g, b (32-bit, wrapping); w unused
 };
-constexpr int DL3_U = 6;   // records loaded per lane before any is used
-constexpr int DL3_UM = 4;  // the same in the merge pass (two records per entry)
+#ifndef DL3_U_V
+#define DL3_U_V 6
+#endif
+#ifndef DL3_UM_V
+#define DL3_UM_V 4
+#endif
+constexpr int DL3_U = DL3_U_V;    // records loaded per lane before any is used
+constexpr int DL3_UM = DL3_UM_V;  // the same in the merge pass (two records per entry)
 
 __device__ __forceinline__ void dl3_set_ec(const Dl3Tab &t, int i, float e, int c) {
     t.EC[i] = make_uint2(__float_as_uint(e), (uint32_t)c);

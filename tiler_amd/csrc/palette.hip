@@ -58,7 +58,7 @@ struct Dl3Expand {  // one pixel 0x00BBGGRR -> its CUBE3 contribution (build_tab
 struct Dl3Tab {
     uint2 *QN;  // x = Q (rr | gg << 8 | bb << 16, setrgb), y = N (pixel_count)
     uint2 *EC;  // x = E (err, float bits), y = C (cc)
-    uint4 *V;   // x, y, z = CUBE3 r, g, b (32-bit, wrapping); w unused
+    uint4 *V;   // x, y, z = CUBE3 r, g, b (32-bit, wrapping); w = N
 };
 #ifndef DL3_U_V
 #define DL3_U_V 6
@@ -89,9 +89,9 @@ struct Dl3Entry {
     uint32_t r, g, b, n, q;
 };
 
-__device__ __forceinline__ Dl3Entry dl3_entry(const uint2 &qn, const uint4 &v) { return Dl3Entry{v.x, v.y, v.z, qn.y, qn.x}; }
+__device__ __forceinline__ Dl3Entry dl3_entry(uint32_t q, const uint4 &v) { return Dl3Entry{v.x, v.y, v.z, v.w, q}; }
 
-__device__ __forceinline__ Dl3Entry dl3_load(const Dl3Tab &t, int i) { return dl3_entry(t.QN[i], t.V[i]); }
+__device__ __forceinline__ Dl3Entry dl3_load(const Dl3Tab &t, int i) { return dl3_entry(t.QN[i].x, t.V[i]); }
 
 __device__ __forceinline__ float dl3_calc_err(const Dl3Entry &a, const Dl3Entry &b) {  // quantizer.c:512-541
     const uint32_t P1 = a.n, P2 = b.n, P3 = P1 + P2;
@@ -117,6 +117,15 @@ __device__ __forceinline__ bool dl3_cannot(uint32_t qa, uint32_t na, uint32_t qb
     const int db = (int)((qa >> 16) & 255) - (int)((qb >> 16) & 255);
     const float m = (float)(na < nb ? na : nb);
     return (float)(dr * dr + dg * dg + db * db) * m * m * 0.99999f > e * e;
+}
+
+// The scans' first test, cheaper than dl3_cannot: |Q_a - Q_b|_2 >= |Q_a - Q_b|_1 / sqrt(3) (three channels), and the L1
+// distance of the packed bytes is one v_sad_u8.  e3 = e * e * 3.00003 (dl3_e3); L1 (<= 765) converts exactly, m is
+// rounded once, so a true result implies (m * L1)^2 / 3 > e^2 (1 + 9e-6) and, as for dl3_cannot, computed calc_err > e.
+__device__ __forceinline__ float dl3_e3(float e) { return e * e * 3.00003f; }
+__device__ __forceinline__ bool dl3_cannot_l1(uint32_t qa, float na, uint32_t qb, uint32_t nb, float e3) {
+    const float t = (float)__builtin_amdgcn_sad_u8(qa, qb, 0u) * fminf(na, (float)nb);
+    return t * t > e3;
 }
 
 // first minimum: smaller error, equal errors -> smaller index (the reference's ascending scan with `<`)
@@ -182,11 +191,13 @@ __device__ void dl3_recount_wave(const Dl3Tab &t, int i, int tot) {
         uint2 r[DL3_U];
 #pragma unroll
         for (int u = 0; u < DL3_U; u++) r[u] = t.QN[min(k0 + u * 64, tot - 1)];
+        const float e3 = dl3_e3(e), naf = (float)a.n;
 #pragma unroll
         for (int u = 0; u < DL3_U; u++) {
             const int k = k0 + u * 64;
-            if (k >= tot || dl3_cannot(a.q, a.n, r[u].x, r[u].y, e)) continue;
-            const float cur = dl3_calc_err(a, dl3_entry(r[u], t.V[k]));
+            if (k >= tot || dl3_cannot_l1(a.q, naf, r[u].x, r[u].y, e3) || dl3_cannot(a.q, a.n, r[u].x, r[u].y, e))
+                continue;
+            const float cur = dl3_calc_err(a, dl3_entry(r[u].x, t.V[k]));
             if (cur < e) {
                 e = cur;
                 j = k;
@@ -239,7 +250,7 @@ __global__ __launch_bounds__(256) void dl3_init_kernel(const Dl3Sum *__restrict_
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e >= seg[P]) return;
     const Dl3Sum s = agg[e];
-    t.V[e] = make_uint4(s.r, s.g, s.b, 0u);
+    t.V[e] = make_uint4(s.r, s.g, s.b, s.n);
     t.QN[e] = make_uint2(dl3_setrgb(s.r, s.g, s.b, s.n), s.n);  // EC: pass 1
 }
 
@@ -301,8 +312,14 @@ __device__ __forceinline__ void dl3_push(Dl3List *L, int *glist, int i, int lcap
         glist[k] = i;
 }
 
+struct Dl3Merge {  // one merge's fix-up context
+    int c1, c2, tot;
+    bool c2v;
+    Dl3Entry b1, b2;  // the new c1 and c2
+};
+
 __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const int *glist, int K, int tot,
-                                 Dl3Chunks *ch, int lcap) {
+                                 Dl3Chunks *ch, int lcap, const Dl3Merge &m) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     for (int base = 0; base < K; base += lcap) {
         const int nb = min(lcap, K - base);
@@ -310,9 +327,24 @@ __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const
         if (tid < nb) {
             const int i = base ? glist[base + tid] : L->item[tid];
             if (base) L->item[tid] = i;  // the previous batch's readers passed its last barrier
-            B->qn[tid] = t.QN[i];
-            B->v[tid] = t.V[i];
-            B->slot[tid] = DL3_NONE;
+            const uint2 qn = t.QN[i];
+            const uint4 v = t.V[i];
+            B->qn[tid] = qn;
+            B->v[tid] = v;
+            // the slot starts at the merge's new entries when they lie in (i, tot): candidates like any other (so
+            // the result is unchanged), and the merged c2 is usually near what i pointed at, so the scan prunes from
+            // its first candidate on
+            unsigned long long k0 = DL3_NONE;
+            const Dl3Entry ai = dl3_entry(qn.x, v);
+            if (m.c2v && m.c2 > i) {
+                const unsigned long long k = ((unsigned long long)__float_as_uint(dl3_calc_err(ai, m.b2)) << 32) | (uint32_t)m.c2;
+                k0 = k < k0 ? k : k0;
+            }
+            if (m.c1 > i) {
+                const unsigned long long k = ((unsigned long long)__float_as_uint(dl3_calc_err(ai, m.b1)) << 32) | (uint32_t)m.c1;
+                k0 = k < k0 ? k : k0;
+            }
+            B->slot[tid] = k0;
             units = (tot - 1 - i + 63) >> 6;
         }
         int v = units;  // block-wide exclusive scan of the unit counts
@@ -340,27 +372,34 @@ __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const
                 hi = mid - 1;
             }
         }
-        for (int u0 = ua; u0 < ub; u0 += DL3_U) {
+        // the wave's units item by item, up to DL3_U units a step: the item, its bound and the step's shape are
+        // wave-uniform; per candidate one load, the L1 test (dl3_cannot_l1), and for the few that pass it the exact
+        // bound and calc_err.  The scan's VALU is what bounds it (a 64-lane op issues over 4 cycles).
+        for (int u0 = ua; u0 < ub;) {
+            while (q < nb - 1 && B->pre[q + 1] <= u0) q++;
+            const int nu = min(DL3_U, min(ub, B->pre[q + 1]) - u0);
+            const int j0 = L->item[q] + 1 + ((u0 - B->pre[q]) << 6) + lane;
             uint2 r[DL3_U];
-            int qq[DL3_U], jj[DL3_U];
+#pragma unroll
+            for (int u = 0; u < DL3_U; u++) r[u] = t.QN[min(j0 + (u << 6), tot - 1)];
+            const uint2 a = B->qn[q];
+            const float naf = (float)a.y;
+            float eb = __uint_as_float((uint32_t)(B->slot[q] >> 32));
+            float e3 = dl3_e3(eb);
 #pragma unroll
             for (int u = 0; u < DL3_U; u++) {
-                const int uu = u0 + u;
-                while (q < nb - 1 && B->pre[q + 1] <= uu) q++;
-                qq[u] = q;
-                jj[u] = uu < ub ? L->item[q] + 1 + ((uu - B->pre[q]) << 6) + lane : tot;
-                r[u] = t.QN[min(jj[u], tot - 1)];
+                const int j = j0 + (u << 6);
+                if (u >= nu || j >= tot || dl3_cannot_l1(a.x, naf, r[u].x, r[u].y, e3) ||
+                    dl3_cannot(a.x, a.y, r[u].x, r[u].y, eb))
+                    continue;
+                const float cur = dl3_calc_err(dl3_entry(a.x, B->v[q]), dl3_entry(r[u].x, t.V[j]));
+                if (cur <= eb) {
+                    atomicMin(&B->slot[q], ((unsigned long long)__float_as_uint(cur) << 32) | (uint32_t)j);
+                    eb = cur;  // an achieved value: still a valid bound for this lane
+                    e3 = dl3_e3(eb);
+                }
             }
-#pragma unroll
-            for (int u = 0; u < DL3_U; u++) {
-                if (jj[u] >= tot) continue;
-                const float eb = __uint_as_float((uint32_t)(B->slot[qq[u]] >> 32));
-                const uint2 a = B->qn[qq[u]];
-                if (dl3_cannot(a.x, a.y, r[u].x, r[u].y, eb)) continue;
-                const float cur = dl3_calc_err(dl3_entry(a, B->v[qq[u]]), dl3_entry(r[u], t.V[jj[u]]));
-                if (cur <= eb)
-                    atomicMin(&B->slot[qq[u]], ((unsigned long long)__float_as_uint(cur) << 32) | (uint32_t)jj[u]);
-            }
+            u0 += nu;
         }
         __syncthreads();
         if (tid < nb) {
@@ -414,13 +453,8 @@ __device__ void dl3_chunk_min(const Dl3Tab &t, Dl3Chunks *ch, int c, int tot) {
     }
 }
 
-struct Dl3Merge {  // one merge's fix-up context
-    int c1, c2, tot;
-    bool c2v;
-    Dl3Entry b1, b2;  // the new c1 and c2
-};
 
-// entry i's fix-ups (qn, ec: its QN and EC; getv() its V): the list, or the updates written (G: stats to raise)
+// entry i's fix-ups (qn, ec: its QN and EC; getv() its V): the list, or the updates written
 template <class GetV>
 __device__ __forceinline__ void dl3_fixup(const Dl3Tab &t, Dl3List *L, int *glist, int lcap, Dl3Chunks *ch,
                                           const Dl3Merge &m, int i, uint2 qn, uint2 ec, GetV getv) {
@@ -438,8 +472,9 @@ __device__ __forceinline__ void dl3_fixup(const Dl3Tab &t, Dl3List *L, int *glis
         }
         if (c == m.c1) {
             rc = true;
-        } else if (!dl3_cannot(qn.x, qn.y, m.b1.q, m.b1.n, e)) {
-            const float cur = dl3_calc_err(dl3_entry(qn, getv()), m.b1);
+        } else if (!dl3_cannot_l1(m.b1.q, (float)m.b1.n, qn.x, qn.y, dl3_e3(e)) &&
+                   !dl3_cannot(qn.x, qn.y, m.b1.q, m.b1.n, e)) {
+            const float cur = dl3_calc_err(dl3_entry(qn.x, getv()), m.b1);
             if (cur < e) {
                 e = cur;
                 c = m.c1;
@@ -450,8 +485,9 @@ __device__ __forceinline__ void dl3_fixup(const Dl3Tab &t, Dl3List *L, int *glis
     if (!rc && m.c2v && i <= m.c2) {
         if (i == m.c2 || c == m.c2) {
             rc = true;
-        } else if (!dl3_cannot(qn.x, qn.y, m.b2.q, m.b2.n, e)) {
-            const float cur = dl3_calc_err(dl3_entry(qn, getv()), m.b2);
+        } else if (!dl3_cannot_l1(m.b2.q, (float)m.b2.n, qn.x, qn.y, dl3_e3(e)) &&
+                   !dl3_cannot(qn.x, qn.y, m.b2.q, m.b2.n, e)) {
+            const float cur = dl3_calc_err(dl3_entry(qn.x, getv()), m.b2);
             if (cur < e) {
                 e = cur;
                 c = m.c2;
@@ -557,20 +593,20 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
         __syncthreads();  // every thread has read the chunk minima before they change
         tot--;
         if (threadIdx.x == 0) {  // merge c1 into c2, the last entry into c1 (quantizer.c:619-629): one round of loads
-            const uint2 q1 = t.QN[c1], q2 = t.QN[c2], ql = t.QN[tot];
+            const uint32_t ql = t.QN[tot].x;
             const uint4 v1 = t.V[c1], v2 = t.V[c2], vl = t.V[tot];
             const uint2 el = t.EC[tot];
-            const uint32_t r = v2.x + v1.x, g = v2.y + v1.y, b = v2.z + v1.z, nn = q2.y + q1.y;
-            const uint2 qm = make_uint2(dl3_setrgb(r, g, b, nn), nn);
-            const uint4 vm = make_uint4(r, g, b, 0u);
+            const uint32_t r = v2.x + v1.x, g = v2.y + v1.y, b = v2.z + v1.z, nn = v2.w + v1.w;
+            const uint32_t qm = dl3_setrgb(r, g, b, nn);
+            const uint4 vm = make_uint4(r, g, b, nn);
             t.V[c2] = vm;
-            t.QN[c2] = qm;
+            t.QN[c2] = make_uint2(qm, nn);
             // the last entry moves into c1 (after the c2 update: c2 may be the last entry)
             const bool c2last = c2 == tot;
-            const uint2 qc1 = c2last ? qm : ql;
+            const uint32_t qc1 = c2last ? qm : ql;
             const uint4 vc1 = c2last ? vm : vl;
             t.V[c1] = vc1;
-            t.QN[c1] = qc1;
+            t.QN[c1] = make_uint2(qc1, vc1.w);
             t.EC[c1] = el;
             dl3_set_ec(t, tot - 1, HUGE_VALF, tot);
             L->n = 0;
@@ -595,7 +631,7 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
 #ifdef TILER_EXPERIMENTS
         if (threadIdx.x == 0 && p < 1024) g_dl3_prof[p][5] += L->n;
 #endif
-        dl3_recount_list(t, L, B, glist, L->n, tot, ch, a.lcap);
+        dl3_recount_list(t, L, B, glist, L->n, tot, ch, a.lcap, sm);
         DL3_PROF(2)
         // refresh the marked chunks (every mark above is complete: the list run ends in a barrier)
         const int nd = ch->n;

@@ -56,7 +56,7 @@ struct Dl3Expand {  // one pixel 0x00BBGGRR -> its CUBE3 contribution (build_tab
 // the colour tables of all pairs; entry e of pair p at seg[p] + local index, split by access: the nearest-merge
 // scans read QN alone (8 bytes per entry), the per-merge pass QN and EC, calc_err also V.
 struct Dl3Tab {
-    uint2 *QN;  // x = Q (rr | gg << 8 | bb << 16, setrgb), y = N (pixel_count)
+    uint2 *QN;  // x = Q (rr | gg << 8 | bb << 16, setrgb), y = (float)N, bits (the scans' bounds; V.w is exact)
     uint2 *EC;  // x = E (err, float bits), y = C (cc)
     uint4 *V;   // x, y, z = CUBE3 r, g, b (32-bit, wrapping); w = N
 };
@@ -89,6 +89,8 @@ struct Dl3Entry {
     uint32_t r, g, b, n, q;
 };
 
+__device__ __forceinline__ uint2 dl3_qn(uint32_t q, uint32_t n) { return make_uint2(q, __float_as_uint((float)n)); }
+
 __device__ __forceinline__ Dl3Entry dl3_entry(uint32_t q, const uint4 &v) { return Dl3Entry{v.x, v.y, v.z, v.w, q}; }
 
 __device__ __forceinline__ Dl3Entry dl3_load(const Dl3Tab &t, int i) { return dl3_entry(t.QN[i].x, t.V[i]); }
@@ -112,10 +114,10 @@ __device__ __forceinline__ float dl3_calc_err(const Dl3Entry &a, const Dl3Entry 
 // the merged mean), the float evaluation loses at most (1 - 2^-24)^5, so computed^2 >= m^2 * dd * (1 - 6e-7).  The
 // test's own float evaluation (dd exact, m rounded once, three products, e * e) is within (1 +- 2^-24)^6, so with
 // the factor 1 - 1e-5 a true result implies computed^2 > e^2.  e = inf (or e * e overflowing) never prunes.
-__device__ __forceinline__ bool dl3_cannot(uint32_t qa, uint32_t na, uint32_t qb, uint32_t nb, float e) {
+__device__ __forceinline__ bool dl3_cannot(uint32_t qa, float na, uint32_t qb, float nb, float e) {
     const int dr = (int)(qa & 255) - (int)(qb & 255), dg = (int)((qa >> 8) & 255) - (int)((qb >> 8) & 255);
     const int db = (int)((qa >> 16) & 255) - (int)((qb >> 16) & 255);
-    const float m = (float)(na < nb ? na : nb);
+    const float m = fminf(na, nb);  // the counts as floats: rounded once each, as the margin allows
     return (float)(dr * dr + dg * dg + db * db) * m * m * 0.99999f > e * e;
 }
 
@@ -123,8 +125,8 @@ __device__ __forceinline__ bool dl3_cannot(uint32_t qa, uint32_t na, uint32_t qb
 // distance of the packed bytes is one v_sad_u8.  e3 = e * e * 3.00003 (dl3_e3); L1 (<= 765) converts exactly, m is
 // rounded once, so a true result implies (m * L1)^2 / 3 > e^2 (1 + 9e-6) and, as for dl3_cannot, computed calc_err > e.
 __device__ __forceinline__ float dl3_e3(float e) { return e * e * 3.00003f; }
-__device__ __forceinline__ bool dl3_cannot_l1(uint32_t qa, float na, uint32_t qb, uint32_t nb, float e3) {
-    const float t = (float)__builtin_amdgcn_sad_u8(qa, qb, 0u) * fminf(na, (float)nb);
+__device__ __forceinline__ bool dl3_cannot_l1(uint32_t qa, float na, uint32_t qb, float nb, float e3) {
+    const float t = (float)__builtin_amdgcn_sad_u8(qa, qb, 0u) * fminf(na, nb);
     return t * t > e3;
 }
 
@@ -189,13 +191,15 @@ __device__ void dl3_recount_wave(const Dl3Tab &t, int i, int tot) {
     const int lane = (int)(threadIdx.x & 63);
     for (int k0 = i + 1 + lane; k0 < tot; k0 += 64 * DL3_U) {
         uint2 r[DL3_U];
+        const uint2 *p = t.QN + k0;  // loads past tot stay inside the table allocation (its slack)
 #pragma unroll
-        for (int u = 0; u < DL3_U; u++) r[u] = t.QN[min(k0 + u * 64, tot - 1)];
+        for (int u = 0; u < DL3_U; u++) r[u] = p[u * 64];
         const float e3 = dl3_e3(e), naf = (float)a.n;
 #pragma unroll
         for (int u = 0; u < DL3_U; u++) {
             const int k = k0 + u * 64;
-            if (k >= tot || dl3_cannot_l1(a.q, naf, r[u].x, r[u].y, e3) || dl3_cannot(a.q, a.n, r[u].x, r[u].y, e))
+            const float nb = __uint_as_float(r[u].y);
+            if (k >= tot || dl3_cannot_l1(a.q, naf, r[u].x, nb, e3) || dl3_cannot(a.q, naf, r[u].x, nb, e))
                 continue;
             const float cur = dl3_calc_err(a, dl3_entry(r[u].x, t.V[k]));
             if (cur < e) {
@@ -251,7 +255,7 @@ __global__ __launch_bounds__(256) void dl3_init_kernel(const Dl3Sum *__restrict_
     if (e >= seg[P]) return;
     const Dl3Sum s = agg[e];
     t.V[e] = make_uint4(s.r, s.g, s.b, s.n);
-    t.QN[e] = make_uint2(dl3_setrgb(s.r, s.g, s.b, s.n), s.n);  // EC: pass 1
+    t.QN[e] = dl3_qn(dl3_setrgb(s.r, s.g, s.b, s.n), s.n);  // EC: pass 1
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -284,6 +288,11 @@ struct Dl3Args {
     int lcap;        // recount-list entries held in LDS per batch (DL3_LCAP; smaller only by the test hook)
     int32_t *pal;    // [P][quant_to] 0x00BBGGRR
 };
+
+#ifdef TILER_EXPERIMENTS
+// per pair: phase wall-clock ticks (100 MHz), merges, list entries, recount candidates past the L1 test and past the exact bound (experiment build only)
+__device__ unsigned long long g_dl3_prof[1024][8];
+#endif
 
 // One merge's recount list, batched: every listed entry's recount_next scan is cut into units of 64 candidates,
 // the units of the whole batch are split evenly over the waves, and each candidate that survives the bound is
@@ -380,18 +389,25 @@ __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const
             const int nu = min(DL3_U, min(ub, B->pre[q + 1]) - u0);
             const int j0 = L->item[q] + 1 + ((u0 - B->pre[q]) << 6) + lane;
             uint2 r[DL3_U];
+            const uint2 *pj = t.QN + j0;  // one address, immediate offsets; loads past tot stay inside the slack
 #pragma unroll
-            for (int u = 0; u < DL3_U; u++) r[u] = t.QN[min(j0 + (u << 6), tot - 1)];
+            for (int u = 0; u < DL3_U; u++) r[u] = pj[u << 6];
             const uint2 a = B->qn[q];
-            const float naf = (float)a.y;
+            const float naf = __uint_as_float(a.y);
             float eb = __uint_as_float((uint32_t)(B->slot[q] >> 32));
             float e3 = dl3_e3(eb);
 #pragma unroll
             for (int u = 0; u < DL3_U; u++) {
                 const int j = j0 + (u << 6);
-                if (u >= nu || j >= tot || dl3_cannot_l1(a.x, naf, r[u].x, r[u].y, e3) ||
-                    dl3_cannot(a.x, a.y, r[u].x, r[u].y, eb))
-                    continue;
+                const float nb = __uint_as_float(r[u].y);
+                if (u >= nu || j >= tot || dl3_cannot_l1(a.x, naf, r[u].x, nb, e3)) continue;
+#ifdef TILER_EXPERIMENTS
+                if (blockIdx.x < 1024) atomicAdd(&g_dl3_prof[blockIdx.x][6], 1ull);
+#endif
+                if (dl3_cannot(a.x, naf, r[u].x, nb, eb)) continue;
+#ifdef TILER_EXPERIMENTS
+                if (blockIdx.x < 1024) atomicAdd(&g_dl3_prof[blockIdx.x][7], 1ull);
+#endif
                 const float cur = dl3_calc_err(dl3_entry(a.x, B->v[q]), dl3_entry(r[u].x, t.V[j]));
                 if (cur <= eb) {
                     atomicMin(&B->slot[q], ((unsigned long long)__float_as_uint(cur) << 32) | (uint32_t)j);
@@ -411,11 +427,6 @@ __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const
         __syncthreads();
     }
 }
-
-#ifdef TILER_EXPERIMENTS
-// per pair: phase wall-clock ticks (100 MHz), merges, list entries (experiment build only)
-__device__ unsigned long long g_dl3_prof[1024][6];
-#endif
 
 // the first minimum of chunk c over entries below tot, by one wave (lane 0 stores it)
 __device__ void dl3_chunk_min(const Dl3Tab &t, Dl3Chunks *ch, int c, int tot) {
@@ -472,8 +483,8 @@ __device__ __forceinline__ void dl3_fixup(const Dl3Tab &t, Dl3List *L, int *glis
         }
         if (c == m.c1) {
             rc = true;
-        } else if (!dl3_cannot_l1(m.b1.q, (float)m.b1.n, qn.x, qn.y, dl3_e3(e)) &&
-                   !dl3_cannot(qn.x, qn.y, m.b1.q, m.b1.n, e)) {
+        } else if (!dl3_cannot_l1(m.b1.q, (float)m.b1.n, qn.x, __uint_as_float(qn.y), dl3_e3(e)) &&
+                   !dl3_cannot(qn.x, __uint_as_float(qn.y), m.b1.q, (float)m.b1.n, e)) {
             const float cur = dl3_calc_err(dl3_entry(qn.x, getv()), m.b1);
             if (cur < e) {
                 e = cur;
@@ -485,8 +496,8 @@ __device__ __forceinline__ void dl3_fixup(const Dl3Tab &t, Dl3List *L, int *glis
     if (!rc && m.c2v && i <= m.c2) {
         if (i == m.c2 || c == m.c2) {
             rc = true;
-        } else if (!dl3_cannot_l1(m.b2.q, (float)m.b2.n, qn.x, qn.y, dl3_e3(e)) &&
-                   !dl3_cannot(qn.x, qn.y, m.b2.q, m.b2.n, e)) {
+        } else if (!dl3_cannot_l1(m.b2.q, (float)m.b2.n, qn.x, __uint_as_float(qn.y), dl3_e3(e)) &&
+                   !dl3_cannot(qn.x, __uint_as_float(qn.y), m.b2.q, (float)m.b2.n, e)) {
             const float cur = dl3_calc_err(dl3_entry(qn.x, getv()), m.b2);
             if (cur < e) {
                 e = cur;
@@ -600,13 +611,13 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
             const uint32_t qm = dl3_setrgb(r, g, b, nn);
             const uint4 vm = make_uint4(r, g, b, nn);
             t.V[c2] = vm;
-            t.QN[c2] = make_uint2(qm, nn);
+            t.QN[c2] = dl3_qn(qm, nn);
             // the last entry moves into c1 (after the c2 update: c2 may be the last entry)
             const bool c2last = c2 == tot;
             const uint32_t qc1 = c2last ? qm : ql;
             const uint4 vc1 = c2last ? vm : vl;
             t.V[c1] = vc1;
-            t.QN[c1] = make_uint2(qc1, vc1.w);
+            t.QN[c1] = dl3_qn(qc1, vc1.w);
             t.EC[c1] = el;
             dl3_set_ec(t, tot - 1, HUGE_VALF, tot);
             L->n = 0;
@@ -815,7 +826,7 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     const size_t np = (size_t)std::max(npix, 1);
     const size_t b_keys = 4 * np, b_sum = sizeof(Dl3Sum) * np, b_tmp = std::max(tmp_sort, tmp_red) + 256;
     const size_t bytes = 4 * b_keys /* keys, vals x2 */ + b_keys /* ukeys */ + b_sum + b_tmp + 4 * (P + 2) * 2 +
-                         8 * b_keys /* table (the list reuses a sort buffer) */ + 4 * (size_t)P * palsize + 4096;
+                         8 * b_keys + 8192 /* table (the list reuses a sort buffer) */ + 4 * (size_t)P * palsize + 4096;
     char *ws = nullptr;
     TILER_HIP_CHECK(hipMalloc((void **)&ws, bytes));
     char *cur = ws;
@@ -833,7 +844,7 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     int *d_seg = (int *)take(4 * (P + 2));
     int *d_uc = (int *)take(4 * (P + 2));
     Dl3Tab t;
-    t.QN = (uint2 *)take(2 * b_keys);
+    t.QN = (uint2 *)take(2 * b_keys + 8 * 1024);  // + slack for the scans' unclamped loads
     t.EC = (uint2 *)take(2 * b_keys);
     t.V = (uint4 *)take(4 * b_keys);
     int *d_list = (int *)k0;  // the sort buffers are free once the table exists
@@ -885,7 +896,7 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
             ra.lcap = std::max(1, std::min(DL3_LCAP, g_dl3_lcap.load()));
             ra.pal = d_pal;
 #ifdef TILER_EXPERIMENTS
-            static unsigned long long zero[1024][6];
+            static unsigned long long zero[1024][8];
             if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dl3_prof), zero, sizeof(zero), 0, hipMemcpyHostToDevice, stream) !=
                 hipSuccess)
                 break;
@@ -894,7 +905,7 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
             if (hipGetLastError() != hipSuccess) break;
 #ifdef TILER_EXPERIMENTS
             if (getenv("TILER_DL3_PROF")) {  // the largest pair's phase split
-                static unsigned long long pr[1024][6];
+                static unsigned long long pr[1024][8];
                 if (hipMemcpyFromSymbolAsync(pr, HIP_SYMBOL(g_dl3_prof), sizeof(pr), 0, hipMemcpyDeviceToHost, stream) !=
                         hipSuccess ||
                     hipStreamSynchronize(stream) != hipSuccess)
@@ -905,6 +916,8 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
                 fprintf(stderr, "dl3 pair %d colors %d merges %llu list/merge %.2f us: argmin+merge %.1f pass %.1f list %.1f chunks %.1f\n",
                         best, seg[best + 1] - seg[best], pr[best][4], (double)pr[best][5] / std::max(1ull, pr[best][4]),
                         pr[best][0] / 100.0, pr[best][1] / 100.0, pr[best][2] / 100.0, pr[best][3] / 100.0);
+                fprintf(stderr, "  recount candidates per merge: past L1 %.1f, past the exact bound %.1f\n",
+                        (double)pr[best][6] / std::max(1ull, pr[best][4]), (double)pr[best][7] / std::max(1ull, pr[best][4]));
             }
 #endif
         }

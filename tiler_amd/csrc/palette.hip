@@ -66,6 +66,9 @@ struct Dl3Tab {
 #ifndef DL3_UM_V
 #define DL3_UM_V 4
 #endif
+#ifndef DL3_PROBE
+#define DL3_PROBE 1  // recount: each listed entry's first 64 candidates before the bulk scan (0: A/B builds only)
+#endif
 constexpr int DL3_U = DL3_U_V;    // records loaded per lane before any is used
 constexpr int DL3_UM = DL3_UM_V;  // the same in the merge pass (two records per entry)
 
@@ -384,8 +387,32 @@ __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const
         // the wave's units item by item, up to DL3_U units a step: the item, its bound and the step's shape are
         // wave-uniform; per candidate one load, the L1 test (dl3_cannot_l1), and for the few that pass it the exact
         // bound and calc_err.  The scan's VALU is what bounds it (a 64-lane op issues over 4 cycles).
+#if DL3_PROBE
+        // probe: every item's first unit (its next 64 entries: neighbours in the table's colour-cell order, so
+        // usually close) scanned first, one wave per item, so the slots hold a tight bound before the bulk scan
+        for (int qq = w; qq < nb; qq += DL3_W) {
+            const int u0 = B->pre[qq];
+            if (u0 >= B->pre[qq + 1]) continue;  // empty range (uniform)
+            const int j = L->item[qq] + 1 + lane;
+            const uint2 rr = t.QN[j];
+            const uint2 a = B->qn[qq];
+            const float naf = __uint_as_float(a.y), eb = __uint_as_float((uint32_t)(B->slot[qq] >> 32));
+            const float nb2 = __uint_as_float(rr.y);
+            if (j < tot && !dl3_cannot_l1(a.x, naf, rr.x, nb2, dl3_e3(eb)) && !dl3_cannot(a.x, naf, rr.x, nb2, eb)) {
+                const float cur = dl3_calc_err(dl3_entry(a.x, B->v[qq]), dl3_entry(rr.x, t.V[j]));
+                if (cur <= eb) atomicMin(&B->slot[qq], ((unsigned long long)__float_as_uint(cur) << 32) | (uint32_t)j);
+            }
+        }
+        __syncthreads();
+#endif
         for (int u0 = ua; u0 < ub;) {
             while (q < nb - 1 && B->pre[q + 1] <= u0) q++;
+#if DL3_PROBE
+            if (u0 == B->pre[q]) {  // the probed unit
+                u0++;
+                continue;
+            }
+#endif
             const int nu = min(DL3_U, min(ub, B->pre[q + 1]) - u0);
             const int j0 = L->item[q] + 1 + ((u0 - B->pre[q]) << 6) + lane;
             uint2 r[DL3_U];
@@ -523,18 +550,20 @@ __device__ __forceinline__ void dl3_fixup(const Dl3Tab &t, Dl3List *L, int *glis
 // and a repeated recount gives the same result.  So an entry either joins the recount list, or takes the updates
 // with calc_err(i, c1) then calc_err(i, c2) (strictly smaller only, as the reference).
 __device__ void dl3_merge_pass(const Dl3Tab &t, Dl3List *L, int *glist, const Dl3Merge &m, Dl3Chunks *ch, int lcap) {
-    const int tot = m.tot;
-    for (int i0 = threadIdx.x; i0 < tot; i0 += DL3_T * DL3_UM) {
+    const int tot = m.tot, lane = threadIdx.x & 63;
+    // wave-contiguous blocks of 64 * DL3_UM entries (one address per block, immediate offsets; loads past tot stay
+    // inside the tables' slack), blocks round robin over the waves
+    for (int i0 = (int)(threadIdx.x >> 6) * 64 * DL3_UM + lane; i0 < tot; i0 += DL3_T * DL3_UM) {
         uint2 rq[DL3_UM], re[DL3_UM];
+        const uint2 *pq = t.QN + i0, *pe = t.EC + i0;
 #pragma unroll
         for (int u = 0; u < DL3_UM; u++) {
-            const int i = min(i0 + u * DL3_T, tot - 1);
-            rq[u] = t.QN[i];
-            re[u] = t.EC[i];
+            rq[u] = pq[u * 64];
+            re[u] = pe[u * 64];
         }
 #pragma unroll
         for (int u = 0; u < DL3_UM; u++) {
-            const int i = i0 + u * DL3_T;
+            const int i = i0 + u * 64;
             if (i >= tot) break;
             dl3_fixup(t, L, glist, lcap, ch, m, i, rq[u], re[u], [&]() { return t.V[i]; });
         }
@@ -826,7 +855,7 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     const size_t np = (size_t)std::max(npix, 1);
     const size_t b_keys = 4 * np, b_sum = sizeof(Dl3Sum) * np, b_tmp = std::max(tmp_sort, tmp_red) + 256;
     const size_t bytes = 4 * b_keys /* keys, vals x2 */ + b_keys /* ukeys */ + b_sum + b_tmp + 4 * (P + 2) * 2 +
-                         8 * b_keys + 8192 /* table (the list reuses a sort buffer) */ + 4 * (size_t)P * palsize + 4096;
+                         8 * b_keys + 16384 /* table (the list reuses a sort buffer) */ + 4 * (size_t)P * palsize + 4096;
     char *ws = nullptr;
     TILER_HIP_CHECK(hipMalloc((void **)&ws, bytes));
     char *cur = ws;
@@ -845,7 +874,7 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     int *d_uc = (int *)take(4 * (P + 2));
     Dl3Tab t;
     t.QN = (uint2 *)take(2 * b_keys + 8 * 1024);  // + slack for the scans' unclamped loads
-    t.EC = (uint2 *)take(2 * b_keys);
+    t.EC = (uint2 *)take(2 * b_keys + 8 * 1024);  // + slack for the pass's unclamped loads
     t.V = (uint4 *)take(4 * b_keys);
     int *d_list = (int *)k0;  // the sort buffers are free once the table exists
     int32_t *d_pal = (int32_t *)take(4 * (size_t)P * palsize);

@@ -5,6 +5,7 @@
 # items (~388k).  Same box, one call; results of modes != 0 are invalid.
 set -eu
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
+bash profiles/exp_lib.sh
 mkdir -p gpurun_out/r04b
 cp tiler_amd/lib/experiments/libANN.so tiler_amd/lib/libANN.so
 for it in 16384 0; do

@@ -4,6 +4,7 @@
 # registers, 2 three-buffer LDS ring, 3 both; 0 the shipped kernel).  Valid results: digests must match var 0.
 set -eu
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
+bash profiles/exp_lib.sh
 mkdir -p gpurun_out/r04e
 cp tiler_amd/lib/experiments/libANN.so tiler_amd/lib/libANN.so
 for it in 16384 0; do

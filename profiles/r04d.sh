@@ -7,6 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r04d
 mkdir -p "$OUT"
 cd "$R"
+bash "$R/profiles/exp_lib.sh"
 cp tiler_amd/lib/experiments/libANN.so tiler_amd/lib/libANN.so
 cd /tmp
 export TMPDIR=/tmp

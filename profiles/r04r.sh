@@ -6,6 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r04r
 mkdir -p "$OUT"
 cd "$R"
+bash "$R/profiles/exp_lib.sh"
 timeout -k 10 300 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_palette.py > "$OUT/pal_tests.log" 2>&1 || { tail -30 "$OUT/pal_tests.log"; exit 1; }
 tail -1 "$OUT/pal_tests.log"
 timeout -k 10 120 python3 -u tools/dl3_study.py dump "$OUT/ship.npz"

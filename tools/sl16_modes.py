@@ -24,11 +24,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--item-tiles", type=int, default=16384)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--lib", default="")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
-    if args.lib:
-        os.environ["TILER_LIB"] = args.lib
     import torch
     import tiler_amd
     from tiler_amd import frame_tiling as ftm

@@ -1655,7 +1655,13 @@ int orbit_tier2(NNIndex *ix, const float *d_q, const OrbitTail &tail, int nq, hi
     const int prev = ix->h_fb_count ? std::max(0, (int)((volatile int *)ix->h_fb_count)[0]) : 0;
     const int t2x_auto = std::max(2, std::min(64, (prev + prev / 4 + 127) / 128 + 1));
     const int t2x = t2x_auto;
-    constexpr int t2s = 512;
+#ifndef ORB_T2_WG
+#define ORB_T2_WG 1024
+#endif
+    // candidate splits: about ORB_T2_WG workgroups in all (128..512 splits); r04t at C3: a fixed 512 splits (one per
+    // 4 blocks) gave ~5,600 tiny workgroups, 0.152 ms -> 0.119 ms with ~1,000 (C2 0.059 -> 0.047), digests unchanged
+    const int t2s = ORB_T2_WG > 0 ? std::max(128, std::min(512, ORB_T2_WG / std::max(1, std::min(t2x, (nq + 127) / 128))))
+                                  : 512;
     const int nsplit = std::min(o->gblk, t2s);
     const int bps = (o->gblk + nsplit - 1) / nsplit;
     OrbitCollectArgs ca;

@@ -47,7 +47,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (rank 0)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, visible cores)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host cores this process may use "
+                    "(benchutil.host_cores: affinity mask, cgroup quota, the box's advertised share)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-smooth", action="store_true")
     ap.add_argument("--no-keyframes", action="store_true")
@@ -61,10 +62,26 @@ def main():
     ap.add_argument("--clip-frames", type=int, default=1000, help="keyframe-detection clip length (C3: 1000)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI, the product); gloo only to rehearse the N>1 control flow")
+    ap.add_argument("--rank-check", action="store_true",
+                    help="launcher self-test without a GPU: the ranks rendezvous over gloo, all-reduce their ranks "
+                         "and rank 0 prints the world it saw (tests/test_bench_launch.py)")
     args = ap.parse_args()
+
+    # --gpus N: one process per GPU.  Under an external launcher (torch.distributed.run) WORLD_SIZE must agree;
+    # without one this process starts the N ranks itself BEFORE touching the GPU and relays rank 0's line.
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}: refusing to time a different world",
+              file=sys.stderr)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
+
+    if args.rank_check:
+        return rank_check()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -190,7 +207,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_tiles = QK * args.steps * world
+    ranks_seen = dist.get_world_size() if world > 1 else 1
+    total_tiles = QK * args.steps * ranks_seen
     value = total_tiles / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
 
@@ -482,7 +500,8 @@ def main():
 
     if rank == 0:
         res = {
-            "metric": METRIC, "value": round(value, 4), "unit": "Mtiles/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC, "value": round(value, 4), "unit": "Mtiles/s", "n_gpus": world, "ranks_seen": ranks_seen,
+            "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded, SURVEY.md 8(d))",
             "config": {"workload": f"{args.config.upper()}: {W}x{H} 8x8 tiles ({Q} tiles/frame), keyframe of {F} "
@@ -498,6 +517,63 @@ def main():
     kdt.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def rank_check() -> None:
+    """--rank-check: rendezvous the ranks over gloo (CPU only), all-reduce (rank + 1) and print the world seen."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    seen, total = 1, 1
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([rank + 1], dtype=torch.int64)
+        dist.all_reduce(t)
+        seen, total = dist.get_world_size(), int(t.item())
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks_seen": seen, "rank_sum": total,
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}))
+
+
+def launch_ranks(n: int) -> int:
+    """Start `n` ranks of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in each one's environment, as
+    torch.distributed.run would set them; rank r binds GPU r), relay rank 0's stdout and return the worst exit
+    status.  The parent never initialises the GPU, so the children are plain child processes, not an exec.
+    If a rank fails, the others are stopped (by their own PIDs) so nobody waits at a barrier forever."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = []
+    import threading
+    reader = threading.Thread(target=lambda: out0.extend(procs[0].stdout.read().decode().splitlines()), daemon=True)
+    reader.start()
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+                if codes[i] not in (None, 0):
+                    for q in procs:
+                        if q.poll() is None:
+                            q.kill()
+        time.sleep(0.2)
+    reader.join(timeout=30)
+    for ln in out0:
+        print(ln, flush=True)
+    bad = [c for c in codes if c]
+    if bad:
+        print(f"bench.py: rank exit codes {codes}", file=sys.stderr)
+    return (bad[0] if bad[0] > 0 else 128 - bad[0]) if bad else 0
 
 
 def per_call_line(lib, kdt, frames, nq_conc: int) -> dict:
@@ -577,7 +653,9 @@ def cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
-    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    from benchutil import host_cores
+    hc = host_cores()
+    threads = args.cpu_threads or hc["usable"]
     P, T = pals.shape[0], tiles.shape[0]
     used = np.zeros((P, T, 4), np.uint8)
     used[ds.pal_of, ds.tile_of, ds.attrs] = 1
@@ -620,6 +698,7 @@ def cpu_baseline(args, tiles, thm, tvm, pals, ds, frames, out_tile, out_pal, out
     li, _ = pyoracle.nn_batch(ods, qd_all, threads=threads)
     tie_decided = int(np.count_nonzero((ot[li] != ot[ki_all]) | (oa[li] != oa[ki_all]) | (op[li] != op[ki_all])))
     return {"value": round(done / spent / 1e6, 6), "unit": "Mtiles/s", "cores": threads, "kind": "port",
+            "host_cores": hc,
             "sample": f"{done} query tiles of the keyframe (first {front} and last {q0.shape[0] - back}) vs the full "
                       f"{ods.shape[0]}-candidate set: fp64 "
                       f"descriptor + ANN 1.1.2 kd-tree (ANN_KD_STD, bucket 1, eps 0; oracle/ann_kdtree.c; "

@@ -10,7 +10,7 @@ cd "$R"
 TILER_BENCH_ONE_DEVICE=1 timeout -k 10 300 python3 bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 --no-cpu \
   --no-smooth --no-keyframes --no-dither --no-palettes --no-globaltiling --no-encoder --no-per-call \
   > "$OUT/bench_n2_rehearsal.json" 2> "$OUT/bench_n2_rehearsal.err"
-echo "n2 rehearsal done"; cat "$OUT/bench_n2_rehearsal.json" | head -c 400; echo
+echo "n2 rehearsal done"; head -c 400 "$OUT/bench_n2_rehearsal.json"; echo
 STEPS=3 bash profiles/run_profile.sh "$TAG"
 python3 profiles/summarize.py "$OUT" "$OUT/pmc_traffic.json" > "$OUT/summary.json"
 echo "summary done"

@@ -104,9 +104,29 @@ int tiler_combine_stats(ann_kdtree *akd, int64_t *calls, int64_t *batches, int32
 int tiler_kdtree_positions(ann_kdtree *akd, int32_t *pos);
 
 /* ---- runtime ---- */
-/* Binds the library to one HIP device (one process per GPU: device = LOCAL_RANK).  Optional; the first call
- * of any other entry point binds device 0.  Re-binding to another device once bound fails with -1. */
+/* Binds the library to one HIP device (one process per GPU: device = LOCAL_RANK), or with TILER_ALL_DEVICES to
+ * every visible gfx950 device (one process driving the node: the unmodified FreePascal encoder, whose keyframes run
+ * concurrently in one process, main.pas:972 / 3961 / 4005-4011).  Optional; the first call of any other entry point
+ * binds device 0.  Re-binding differently once bound fails with -1.
+ * With all devices bound: ann_kdtree_create puts each new handle on the least loaded device (live dataset bytes,
+ * ties to the lowest device), so concurrent keyframes' handles spread over the GPUs with no call-site change;
+ * device-buffer entry points (_dev, ann_kdtree_create_dev*) run on the device their buffers live on, and a handle
+ * used there from another device (e.g. the global 64-d dataset in tiler_prepare_frame_tiling_dev) is replicated to
+ * it on first use (rows peer-copied over xGMI, the identical index built there); every other call of a handle runs
+ * on the handle's device.  Host entry points without a handle run on the caller's current device if bound. */
+#define TILER_ALL_DEVICES (-1)
 int tiler_init(int device);
+int tiler_device_count(void);                              /* devices bound (binds device 0 if none yet) */
+int tiler_kdtree_device(ann_kdtree *akd);                  /* the device a handle lives on */
+/* Copy a handle's index to device (TILER_ALL_DEVICES: to every bound device) now instead of on first use. 0 / -1. */
+int tiler_kdtree_replicate(ann_kdtree *akd, int device);
+/* The placement rule alone (host only, no device needed): dev_out[i] = the device ann_kdtree_create would give the
+ * i-th of n handles of bytes[i] dataset bytes created in order on ndev empty devices (none destroyed).  0 / -1. */
+int tiler_placement_plan(int ndev, const int64_t *bytes, int n, int32_t *dev_out);
+/* Test hook (process-wide): on != 0 makes the first device-buffer call of a handle (and tiler_kdtree_replicate) build
+ * its copy even on the handle's own device, so the replication path (peer copy, index rebuild, maps copy, routing)
+ * runs on a one-GPU box; results are identical either way.  Only with TILER_ALL_DEVICES.  0. */
+int tiler_debug_force_replicas(int on);
 int tiler_shutdown(void);
 const char *tiler_last_error(void); /* thread-local message of the last failure */
 int tiler_set_gamma(double g0, double g1); /* gGamma main.pas:586 / 1441-1447; rebuilds gGammaCorLut */

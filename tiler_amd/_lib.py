@@ -57,6 +57,11 @@ _SIGS = {
     "tiler_set_scan_limits": (c_int, [c_int, c_int]),
     "tiler_combine_stats": (c_int, [c_void_p, P(ctypes.c_int64), P(ctypes.c_int64), P(ctypes.c_int32)]),
     "tiler_init": (c_int, [c_int]),
+    "tiler_device_count": (c_int, []),
+    "tiler_kdtree_device": (c_int, [c_void_p]),
+    "tiler_kdtree_replicate": (c_int, [c_void_p, c_int]),
+    "tiler_placement_plan": (c_int, [c_int, c_void_p, c_int, c_void_p]),
+    "tiler_debug_force_replicas": (c_int, [c_int]),
     "tiler_shutdown": (c_int, []),
     "tiler_last_error": (c_char_p, []),
     "tiler_set_gamma": (c_int, [c_double, c_double]),

@@ -135,6 +135,14 @@ class KDTree:
         check(self._lib.tiler_ft_get_maps(self.handle, _ptr(t), _ptr(p), _ptr(a)), "tiler_ft_get_maps")
         return t[:self.n], p[:self.n], a[:self.n]
 
+    def device(self) -> int:
+        """The device the handle lives on (tiler_kdtree_device)."""
+        return check(self._lib.tiler_kdtree_device(self.handle), "tiler_kdtree_device")
+
+    def replicate(self, device: int = -1):
+        """Copy the index to `device` now (-1 = every bound device; tiler_kdtree_replicate)."""
+        check(self._lib.tiler_kdtree_replicate(self.handle, device), "tiler_kdtree_replicate")
+
     def positions(self) -> np.ndarray:
         """Leaf position of every point in ANN's kd-tree (tiler_kdtree_positions)."""
         pos = np.zeros(self.n, np.int32)

@@ -8,6 +8,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -35,11 +36,22 @@ const char *last_error() { return g_err.c_str(); }
 
 static std::mutex g_init_mu;
 static bool g_ready = false;
-static int g_device = 0;
-static Luts g_luts;
+static bool g_all = false;     // tiler_init(TILER_ALL_DEVICES): every visible gfx950 device bound
+static int g_device = 0;       // the primary device (the only one unless g_all)
+static constexpr int MAX_DEV = 64;
+static bool g_bound[MAX_DEV] = {};
+static Luts g_luts[MAX_DEV];
 static double g_gamma[2] = {2.0, 0.6};
+// live dataset bytes of the handles on each device: ann_kdtree_create places a new handle on the least loaded one
+static std::mutex g_place_mu;
+static long long g_dev_load[MAX_DEV] = {};
 
-const Luts &luts() { return g_luts; }
+static bool bound(int d) { return d >= 0 && d < MAX_DEV && g_bound[d]; }
+const Luts &luts() {  // the current device's tables (every bound device has its own copy)
+    int d = -1;
+    (void)hipGetDevice(&d);
+    return g_luts[bound(d) ? d : g_device];
+}
 
 // ---- kernel timing --------------------------------------------------------------------------
 struct TimedPair {
@@ -71,7 +83,7 @@ KTimer::~KTimer() {
 
 // InitLuts main.pas:592-642; constants main.pas:63-98, 2675-2676, 2816, 3000-3009 -- all on the host,
 // identical expressions to the CPU restatement, so device and oracle share the same bits.
-static int upload_gamma_lut() {
+static int upload_gamma_lut(Luts &L) {
     std::vector<double> g(3 * 256), lin(3 * 256);
     for (int gi = -1; gi <= 1; gi++)
         for (int i = 0; i < 256; i++) g[(gi + 1) * 256 + i] = (gi >= 0) ? pow(i / 255.0, g_gamma[gi]) : i / 255.0;
@@ -79,12 +91,12 @@ static int upload_gamma_lut() {
         const double v = g[k];
         lin[k] = v > 0.04045 ? fpc_power_frac((v + 0.055) / 1.055, 2.4) : v / 12.92;
     }
-    TILER_HIP_CHECK(hipMemcpy(g_luts.d_gamma, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
-    TILER_HIP_CHECK(hipMemcpy(g_luts.d_lab_lin, lin.data(), lin.size() * sizeof(double), hipMemcpyHostToDevice));
+    TILER_HIP_CHECK(hipMemcpy(L.d_gamma, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
+    TILER_HIP_CHECK(hipMemcpy(L.d_lab_lin, lin.data(), lin.size() * sizeof(double), hipMemcpyHostToDevice));
     return 0;
 }
 
-static int build_luts() {
+static int build_luts(Luts &L) {
     static const int qden[3][64] = {
         {16, 11, 10, 16, 24, 40, 51, 61, 12, 12, 14, 19, 26, 58, 60, 55, 14, 13, 16, 24, 40, 57, 69, 56,
          14, 17, 22, 29, 51, 87, 80, 62, 18, 22, 37, 56, 68, 109, 103, 77, 24, 35, 55, 64, 81, 104, 113, 92,
@@ -110,27 +122,42 @@ static int build_luts() {
     const double sh = sqrt(0.5);
     for (int v = 0; v < 8; v++)
         for (int u = 0; u < 8; u++) ratio[v * 8 + u] = (u == 0 && v == 0) ? 0.5 : ((u == 0 || v == 0) ? sh : 1.0);
-    TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_gamma, 3 * 256 * sizeof(double)));
-    TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_dct, 4096 * sizeof(double)));
-    TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_qmul, 192 * sizeof(double)));
-    TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_ratio, 64 * sizeof(double)));
-    TILER_HIP_CHECK(hipMalloc((void **)&g_luts.d_lab_lin, 3 * 256 * sizeof(double)));
-    TILER_HIP_CHECK(hipMemcpy(g_luts.d_dct, dct.data(), 4096 * sizeof(double), hipMemcpyHostToDevice));
-    TILER_HIP_CHECK(hipMemcpy(g_luts.d_qmul, qm.data(), 192 * sizeof(double), hipMemcpyHostToDevice));
-    TILER_HIP_CHECK(hipMemcpy(g_luts.d_ratio, ratio.data(), 64 * sizeof(double), hipMemcpyHostToDevice));
-    g_luts.haar_f = 1.0 / sqrt(2.0);
-    g_luts.u_mul = 0.5 / (1.0 - 722.0 / 10000.0);
-    g_luts.v_mul = 0.5 / (1.0 - 2126.0 / 10000.0);
-    return upload_gamma_lut();
+    TILER_HIP_CHECK(hipMalloc((void **)&L.d_gamma, 3 * 256 * sizeof(double)));
+    TILER_HIP_CHECK(hipMalloc((void **)&L.d_dct, 4096 * sizeof(double)));
+    TILER_HIP_CHECK(hipMalloc((void **)&L.d_qmul, 192 * sizeof(double)));
+    TILER_HIP_CHECK(hipMalloc((void **)&L.d_ratio, 64 * sizeof(double)));
+    TILER_HIP_CHECK(hipMalloc((void **)&L.d_lab_lin, 3 * 256 * sizeof(double)));
+    TILER_HIP_CHECK(hipMemcpy(L.d_dct, dct.data(), 4096 * sizeof(double), hipMemcpyHostToDevice));
+    TILER_HIP_CHECK(hipMemcpy(L.d_qmul, qm.data(), 192 * sizeof(double), hipMemcpyHostToDevice));
+    TILER_HIP_CHECK(hipMemcpy(L.d_ratio, ratio.data(), 64 * sizeof(double), hipMemcpyHostToDevice));
+    L.haar_f = 1.0 / sqrt(2.0);
+    L.u_mul = 0.5 / (1.0 - 722.0 / 10000.0);
+    L.v_mul = 0.5 / (1.0 - 2126.0 / 10000.0);
+    return upload_gamma_lut(L);
+}
+
+static int bind_device(int device) {
+    hipDeviceProp_t prop;
+    TILER_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error(std::string("tiler: device ") + std::to_string(device) + " is " + prop.gcnArchName +
+                  ", libANN.so is built for gfx950 only");
+        return -1;
+    }
+    TILER_HIP_CHECK(hipSetDevice(device));
+    if (build_luts(g_luts[device])) return -1;
+    g_bound[device] = true;
+    return 0;
 }
 
 static int init_locked(int device) {
     if (g_ready) {
-        if (device == g_device) return 0;
+        if (device == TILER_ALL_DEVICES ? g_all : (!g_all && device == g_device)) return 0;
         // already bound (explicitly, or implicitly to device 0 by an earlier call): handles, LUTs and scratch live
-        // on that device, so a silent switch would run later calls on the wrong GPU
-        set_error("tiler_init: the library is already bound to device " + std::to_string(g_device) +
-                  "; call tiler_init(" + std::to_string(device) + ") before any other entry point");
+        // on that device (those devices), so a silent switch would run later calls on the wrong GPU
+        set_error("tiler_init: the library is already bound to " +
+                  (g_all ? std::string("all devices") : "device " + std::to_string(g_device)) + "; call tiler_init(" +
+                  std::to_string(device) + ") before any other entry point");
         return -1;
     }
     int count = 0;
@@ -138,27 +165,97 @@ static int init_locked(int device) {
         set_error("tiler: no HIP device visible (libANN.so runs on MI355X / gfx950 only, no CPU path)");
         return -1;
     }
+    count = std::min(count, MAX_DEV);
+    if (device == TILER_ALL_DEVICES) {
+        // one process driving every GPU of the node (the reference encoder is one process, main.pas:972): each
+        // device gets its own tables; handles are placed per device (ann_kdtree_create) and peers can copy directly
+        for (int d = 0; d < count; d++)
+            if (bind_device(d)) return -1;
+        for (int a = 0; a < count; a++) {
+            TILER_HIP_CHECK(hipSetDevice(a));
+            for (int b = 0; b < count; b++) {
+                int ok = 0;
+                if (a != b && hipDeviceCanAccessPeer(&ok, a, b) == hipSuccess && ok) {
+                    const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+                    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+                }
+            }
+        }
+        g_all = true;
+        g_device = 0;
+        TILER_HIP_CHECK(hipSetDevice(0));
+        g_ready = true;
+        return 0;
+    }
     if (device < 0 || device >= count) {
         set_error("tiler: device index out of range");
         return -1;
     }
-    hipDeviceProp_t prop;
-    TILER_HIP_CHECK(hipGetDeviceProperties(&prop, device));
-    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-        set_error(std::string("tiler: device is ") + prop.gcnArchName + ", libANN.so is built for gfx950 only");
-        return -1;
-    }
-    TILER_HIP_CHECK(hipSetDevice(device));
+    if (bind_device(device)) return -1;
     g_device = device;
-    if (build_luts()) return -1;
     g_ready = true;
     return 0;
 }
 
+// Every entry point: bind on first use; the calling thread's current device is kept when the library is bound to it
+// (all devices: the caller selects one with hipSetDevice, or the entry point follows its handle), else the primary.
 bool ensure_init() {
     std::lock_guard<std::mutex> lk(g_init_mu);
     if (!g_ready && init_locked(0)) return false;
+    int cur = -1;
+    if (g_all && hipGetDevice(&cur) == hipSuccess && bound(cur)) return true;
     return hipSetDevice(g_device) == hipSuccess;
+}
+
+// the device a pointer lives on (device memory; host / unknown pointers: the current device)
+static int ptr_device(const void *p) {
+    int cur = g_device;
+    (void)hipGetDevice(&cur);
+    if (!g_all || !p) return cur;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return cur;
+    }
+    return (a.type == hipMemoryTypeDevice && bound(a.device)) ? a.device : cur;
+}
+
+// runs the scope on device d and restores the caller's current device afterwards
+struct DevScope {
+    int prev = -1;
+    explicit DevScope(int d) {
+        int c = -1;
+        if (hipGetDevice(&c) == hipSuccess && c != d && hipSetDevice(d) == hipSuccess) prev = c;
+    }
+    ~DevScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// least-loaded device for a new dataset of `bytes`: the placement rule of ann_kdtree_create (ties: lowest device)
+static int pick_device(const long long *load, int ndev) {
+    int best = 0;
+    for (int d = 1; d < ndev; d++)
+        if (load[d] < load[best]) best = d;
+    return best;
+}
+static int place_handle(long long bytes) {
+    if (!g_all) return g_device;
+    std::lock_guard<std::mutex> lk(g_place_mu);
+    long long load[MAX_DEV];
+    int map[MAX_DEV], n = 0;
+    for (int d = 0; d < MAX_DEV; d++)
+        if (g_bound[d]) {
+            load[n] = g_dev_load[d];
+            map[n++] = d;
+        }
+    const int d = map[pick_device(load, n)];
+    g_dev_load[d] += bytes;
+    return d;
+}
+static void unplace_handle(int dev, long long bytes) {
+    std::lock_guard<std::mutex> lk(g_place_mu);
+    if (dev >= 0 && dev < MAX_DEV) g_dev_load[dev] -= bytes;
 }
 
 }  // namespace tiler
@@ -205,7 +302,16 @@ struct ann_kdtree {
     uint8_t *d_mh = nullptr, *d_mv = nullptr;
     size_t cap_ft = 0;
     PrepScratch *prep = nullptr;  // tiler_prepare_frame_tiling_dev scratch (on the global dataset's handle)
+    int dev = 0;                  // the device the handle's index, stream and buffers live on
+    hipEvent_t maps_ev = nullptr; // recorded after tiler_prepare_frame_tiling_dev wrote the TRTo maps (on its stream)
+    long long placed = 0;         // dataset bytes counted in g_dev_load[dev]
+    // copies of this handle's index on other devices (tiler_kdtree_replicate, or made on first use by a device entry
+    // point whose buffers live there): rows peer-copied over xGMI, the same index built there
+    std::mutex rep_mu;
+    ann_kdtree *rep[MAX_DEV] = {};
 };
+
+static void handle_free(ann_kdtree *t);
 
 static int ensure_io(ann_kdtree *t, size_t nq, int d, int k) {
     const size_t need = nq * (size_t)std::max(d, k);
@@ -270,7 +376,12 @@ int tiler_set_gamma(double g0, double g1) {
     std::lock_guard<std::mutex> lk(g_init_mu);
     g_gamma[0] = g0;
     g_gamma[1] = g1;
-    return upload_gamma_lut();
+    for (int d = 0; d < MAX_DEV; d++)
+        if (g_bound[d]) {
+            DevScope ds(d);
+            if (upload_gamma_lut(g_luts[d])) return -1;
+        }
+    return 0;
 }
 
 static bool split_ok(int bs, int split, const char *who) {
@@ -301,16 +412,26 @@ ann_kdtree *ann_kdtree_create(float **pa, int n, int dd, int bs, int split) {
         }
         memcpy(&h[(size_t)i * dd], pa[i], sizeof(float) * dd);
     }
+    // host rows: the handle goes to the least loaded bound device (one device unless tiler_init(TILER_ALL_DEVICES))
+    const long long bytes = (long long)h.size() * 4;
+    const int dev = place_handle(bytes);
+    DevScope ds(dev);
     ann_kdtree *t = new ann_kdtree();
-    TILER_HIP_CHECK_NULL(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
+    t->dev = dev;
+    t->placed = bytes;
     float *d_rows = nullptr;
-    TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_rows, std::max<size_t>(1, h.size()) * sizeof(float)));
-    if (n > 0)
-        TILER_HIP_CHECK_NULL(hipMemcpyAsync(d_rows, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, t->stream));
+    if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void **)&d_rows, std::max<size_t>(1, h.size()) * sizeof(float)) != hipSuccess ||
+        (n > 0 && hipMemcpyAsync(d_rows, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, t->stream) !=
+                      hipSuccess)) {
+        set_error("ann_kdtree_create: device allocation or copy failed");
+        if (d_rows) (void)hipFree(d_rows);
+        handle_free(t);
+        return nullptr;
+    }
     t->ix = nn_index_create_dev(d_rows, n, dd, bs, split, t->stream);
     if (!t->ix) {
-        hipStreamDestroy(t->stream);
-        delete t;
+        handle_free(t);
         return nullptr;
     }
     return t;
@@ -327,7 +448,15 @@ ann_kdtree *ann_kdtree_create_dev_ex(const float *d_rows_in, int n, int dd, int 
         return nullptr;
     }
     if (!split_ok(bs, split, "ann_kdtree_create_dev")) return nullptr;
+    const int dev = ptr_device(d_rows_in);  // device rows: the handle lives where they are
+    DevScope ds(dev);
     ann_kdtree *t = new ann_kdtree();
+    t->dev = dev;
+    t->placed = (long long)n * dd * 4;
+    {
+        std::lock_guard<std::mutex> lk(g_place_mu);
+        g_dev_load[dev] += t->placed;
+    }
     TILER_HIP_CHECK_NULL(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
     float *d_rows = nullptr;
@@ -336,34 +465,153 @@ ann_kdtree *ann_kdtree_create_dev_ex(const float *d_rows_in, int n, int dd, int 
     if (n > 0) TILER_HIP_CHECK_NULL(hipMemcpyAsync(d_rows, d_rows_in, bytes, hipMemcpyDeviceToDevice, s));
     t->ix = nn_index_create_dev(d_rows, n, dd, bs, split, s);
     if (!t->ix) {
-        (void)hipStreamDestroy(t->stream);
-        delete t;
+        handle_free(t);
         return nullptr;
     }
     return t;
 }
 
-void ann_kdtree_destroy(ann_kdtree *t) {
+// release a handle (its replicas first); the caller's device is restored
+static void handle_free(ann_kdtree *t) {
     if (!t) return;
-    if (t->stream) hipStreamSynchronize(t->stream);
+    for (int d = 0; d < MAX_DEV; d++)
+        if (t->rep[d]) handle_free(t->rep[d]);
+    DevScope ds(t->dev);
+    if (t->stream) (void)hipStreamSynchronize(t->stream);
     nn_index_destroy(t->ix);
-    hipFree(t->d_q);
-    hipFree(t->d_idx);
-    hipFree(t->d_err);
-    hipFree(t->d_rgb);
-    hipFree(t->d_mt);
-    hipFree(t->d_mp);
-    hipFree(t->d_mh);
-    hipFree(t->d_mv);
+    (void)hipFree(t->d_q);
+    (void)hipFree(t->d_idx);
+    (void)hipFree(t->d_err);
+    (void)hipFree(t->d_rgb);
+    (void)hipFree(t->d_mt);
+    (void)hipFree(t->d_mp);
+    (void)hipFree(t->d_mh);
+    (void)hipFree(t->d_mv);
     if (t->prep) {
         prep_scratch_free(t->prep);
         delete t->prep;
     }
-    hipHostFree(t->comb.h_q);
-    hipHostFree(t->comb.h_idx);
-    hipHostFree(t->comb.h_err);
-    if (t->stream) hipStreamDestroy(t->stream);
+    (void)hipHostFree(t->comb.h_q);
+    (void)hipHostFree(t->comb.h_idx);
+    (void)hipHostFree(t->comb.h_err);
+    if (t->maps_ev) (void)hipEventDestroy(t->maps_ev);
+    if (t->stream) (void)hipStreamDestroy(t->stream);
+    unplace_handle(t->dev, t->placed);
     delete t;
+}
+
+void ann_kdtree_destroy(ann_kdtree *t) { handle_free(t); }
+
+// the copy of t's index on device dev (t itself when it lives there), made on first use: rows (and the TRTo maps)
+// peer-copied from t's device over xGMI, the index built there exactly as at create (same rows, same kd-tree)
+static std::atomic<int> g_force_replicas{0};  // tiler_debug_force_replicas: copies even on the handle's own device
+static ann_kdtree *replica_of(ann_kdtree *t, int dev) {
+    if (!t || (t->dev == dev && !g_force_replicas.load())) return t;
+    if (!bound(dev)) {
+        set_error("tiler: device " + std::to_string(dev) + " is not bound (tiler_init(-1) binds every device)");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(t->rep_mu);
+    if (t->rep[dev]) return t->rep[dev];
+    NNIndex *src = t->ix;
+    std::lock_guard<std::mutex> ilk(src->mu);
+    DevScope ds(dev);
+    ann_kdtree *r = new ann_kdtree();
+    r->dev = dev;
+    r->placed = (long long)src->n * src->d * 4;
+    {
+        std::lock_guard<std::mutex> pl(g_place_mu);
+        g_dev_load[dev] += r->placed;
+    }
+    float *d_rows = nullptr;
+    const size_t bytes = (size_t)src->n * src->d * sizeof(float);
+    // the source's own stream has finished building it (creates return with the index queued on it)
+    if (hipStreamSynchronize(t->stream) != hipSuccess || (src->done_event && hipEventSynchronize(src->done_event) != hipSuccess) ||
+        hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void **)&d_rows, std::max<size_t>(4, bytes)) != hipSuccess ||
+        (bytes && hipMemcpyPeerAsync(d_rows, dev, src->d_rows, t->dev, bytes, r->stream) != hipSuccess)) {
+        set_error("tiler: replica allocation or peer copy failed");
+        if (d_rows) (void)hipFree(d_rows);
+        handle_free(r);
+        return nullptr;
+    }
+    r->ix = nn_index_create_dev(d_rows, src->n, src->d, src->bs, src->split, r->stream);
+    if (!r->ix) {
+        handle_free(r);
+        return nullptr;
+    }
+    if (src->d_tr_tile) {
+        const size_t n = std::max(1, src->n);
+        NNIndex *ix = r->ix;
+        if (hipMalloc((void **)&ix->d_tr_tile, n * 4) != hipSuccess || hipMalloc((void **)&ix->d_tr_pal, n * 4) != hipSuccess ||
+            hipMalloc((void **)&ix->d_tr_attr, n) != hipSuccess ||
+            hipMemcpyPeerAsync(ix->d_tr_tile, dev, src->d_tr_tile, t->dev, (size_t)src->n * 4, r->stream) != hipSuccess ||
+            hipMemcpyPeerAsync(ix->d_tr_pal, dev, src->d_tr_pal, t->dev, (size_t)src->n * 4, r->stream) != hipSuccess ||
+            hipMemcpyPeerAsync(ix->d_tr_attr, dev, src->d_tr_attr, t->dev, (size_t)src->n, r->stream) != hipSuccess) {
+            set_error("tiler: replica maps copy failed");
+            handle_free(r);
+            return nullptr;
+        }
+    }
+    if (hipStreamSynchronize(r->stream) != hipSuccess) {
+        set_error("tiler: replica build failed");
+        handle_free(r);
+        return nullptr;
+    }
+    t->rep[dev] = r;
+    return r;
+}
+
+// the handle to run a device-buffer call on: t's copy on the device of the call's buffer p
+static ann_kdtree *handle_for(ann_kdtree *t, const void *p) { return g_all ? replica_of(t, ptr_device(p)) : t; }
+
+int tiler_kdtree_replicate(ann_kdtree *t, int device) {
+    if (!t || !t->ix) {
+        set_error("tiler_kdtree_replicate: null handle");
+        return -1;
+    }
+    if (!ensure_init()) return -1;
+    for (int d = 0; d < MAX_DEV; d++)
+        if (g_bound[d] && (device == TILER_ALL_DEVICES || device == d) && !replica_of(t, d)) return -1;
+    if (device != TILER_ALL_DEVICES && !bound(device)) {
+        set_error("tiler_kdtree_replicate: device not bound");
+        return -1;
+    }
+    return 0;
+}
+
+int tiler_debug_force_replicas(int on) {
+    g_force_replicas.store(on != 0);
+    return 0;
+}
+
+int tiler_kdtree_device(ann_kdtree *t) {
+    if (!t) {
+        set_error("tiler_kdtree_device: null handle");
+        return -1;
+    }
+    return t->dev;
+}
+
+int tiler_device_count(void) {
+    if (!ensure_init()) return -1;
+    int n = 0;
+    for (int d = 0; d < MAX_DEV; d++) n += g_bound[d] ? 1 : 0;
+    return n;
+}
+
+int tiler_placement_plan(int ndev, const int64_t *bytes, int n, int32_t *dev_out) {
+    if (ndev <= 0 || ndev > MAX_DEV || n < 0 || (n > 0 && (!bytes || !dev_out))) {
+        set_error("tiler_placement_plan: invalid arguments");
+        return -1;
+    }
+    long long load[MAX_DEV] = {};
+    for (int i = 0; i < n; i++) {
+        const int d = pick_device(load, ndev);
+        dev_out[i] = d;
+        load[d] += bytes[i];
+    }
+    return 0;
 }
 
 ann_kdtree *tiler_prepare_frame_tiling_dev(ann_kdtree *global_ds, const int32_t *d_item_tile,
@@ -377,7 +625,14 @@ ann_kdtree *tiler_prepare_frame_tiling_dev(ann_kdtree *global_ds, const int32_t 
         return nullptr;
     }
     if (!ensure_init()) return nullptr;
+    // the keyframe's handle lives where its buffers are; the global dataset's copy on that device serves its k = 8
+    // preselection (peer-copied on first use when the keyframe runs on another GPU)
+    const int dev = ptr_device(d_palpix);
+    ann_kdtree *gds = replica_of(global_ds, dev);
+    if (!gds) return nullptr;
+    DevScope ds(dev);
     ann_kdtree *t = new ann_kdtree();
+    t->dev = dev;
     if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) {
         set_error("tiler_prepare_frame_tiling_dev: stream creation failed");
         delete t;
@@ -386,16 +641,21 @@ ann_kdtree *tiler_prepare_frame_tiling_dev(ann_kdtree *global_ds, const int32_t 
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
     long nd = 0, nc = 0;
     {
-        std::lock_guard<std::mutex> lk(global_ds->ix->mu);  // its k = 8 search scratch and the prepare scratch
-        if (!global_ds->prep) global_ds->prep = new PrepScratch();
-        t->ix = prepare_frame_tiling_dev(global_ds->ix, *global_ds->prep, d_item_tile, d_item_pal, (long)n_items,
-                                         d_palpix, d_thm, d_tvm, n_tiles, d_palettes, n_palettes, quality, near,
-                                         use_wavelets, gamma, s, &nd, &nc);
+        std::lock_guard<std::mutex> lk(gds->ix->mu);  // its k = 8 search scratch and the prepare scratch
+        if (!gds->prep) gds->prep = new PrepScratch();
+        t->ix = prepare_frame_tiling_dev(gds->ix, *gds->prep, d_item_tile, d_item_pal, (long)n_items, d_palpix, d_thm,
+                                         d_tvm, n_tiles, d_palettes, n_palettes, quality, near, use_wavelets, gamma, s,
+                                         &nd, &nc);
     }
-    if (!t->ix) {
-        (void)hipStreamDestroy(t->stream);
-        delete t;
+    if (!t->ix || hipEventCreateWithFlags(&t->maps_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(t->maps_ev, s) != hipSuccess) {
+        handle_free(t);
         return nullptr;
+    }
+    t->placed = (long long)nc * 192 * 4;
+    {
+        std::lock_guard<std::mutex> pl(g_place_mu);
+        g_dev_load[dev] += t->placed;
     }
     if (info) {
         info->items = nd;
@@ -415,6 +675,7 @@ int ann_kdtree_search_multi_batch(ann_kdtree *t, const float *q, int nq, int k, 
         return -1;
     }
     if (!ensure_init()) return -1;
+    DevScope ds(t->dev);
     std::lock_guard<std::mutex> lk(t->ix->mu);
     if (nq == 0) return 0;
     NNIndex *ix = t->ix;
@@ -445,6 +706,7 @@ static int combine_run(ann_kdtree *t, std::vector<CombineReq *> &b, int k) {
     Combiner &c = t->comb;
     NNIndex *ix = t->ix;
     const int nq = (int)b.size(), d = ix->d;
+    DevScope ds(t->dev);
     std::lock_guard<std::mutex> lk(ix->mu);
     if (ix->n == 0) {
         for (CombineReq *r : b)
@@ -458,7 +720,7 @@ static int combine_run(ann_kdtree *t, std::vector<CombineReq *> &b, int k) {
         hipHostFree(c.h_q);
         c.h_q = nullptr;
         c.cap_q = 0;
-        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_q, (size_t)nq * d * sizeof(float), hipHostMallocDefault));
+        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_q, (size_t)nq * d * sizeof(float), hipHostMallocPortable));
         c.cap_q = (size_t)nq * d;
     }
     if ((size_t)nq * k > c.cap_r) {
@@ -467,8 +729,8 @@ static int combine_run(ann_kdtree *t, std::vector<CombineReq *> &b, int k) {
         c.h_idx = nullptr;
         c.h_err = nullptr;
         c.cap_r = 0;
-        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_idx, (size_t)nq * k * sizeof(int), hipHostMallocDefault));
-        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_err, (size_t)nq * k * sizeof(float), hipHostMallocDefault));
+        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_idx, (size_t)nq * k * sizeof(int), hipHostMallocPortable));
+        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_err, (size_t)nq * k * sizeof(float), hipHostMallocPortable));
         c.cap_r = (size_t)nq * k;
     }
     for (int j = 0; j < nq; j++) memcpy(c.h_q + (size_t)j * d, b[j]->q, (size_t)d * sizeof(float));
@@ -585,6 +847,8 @@ int ann_kdtree_search_batch_dev(ann_kdtree *t, const float *d_q, int nq, int k, 
         return -1;
     }
     if (!ensure_init()) return -1;
+    if (!(t = handle_for(t, d_q))) return -1;
+    DevScope ds(t->dev);
     std::lock_guard<std::mutex> lk(t->ix->mu);
     return nn_search_dev(t->ix, d_q, nq, k, d_idx, d_err, nullptr, (hipStream_t)stream);
 }
@@ -594,6 +858,7 @@ int ann_kdtree_get_stats(ann_kdtree *t, tiler_search_stats *out) {
         set_error("ann_kdtree_get_stats: invalid arguments");
         return -1;
     }
+    DevScope ds(t->dev);
     std::lock_guard<std::mutex> lk(t->ix->mu);
     // everything below was written by the last search on ITS stream (the caller's, for the _dev entry points)
     if (t->ix->done_event) TILER_HIP_CHECK(hipEventSynchronize(t->ix->done_event));
@@ -637,6 +902,7 @@ int tiler_kdtree_positions(ann_kdtree *t, int32_t *pos) {
         set_error("tiler_kdtree_positions: handle has no kd-tree (KD_SPLIT_INDEX_ORDER)");
         return -1;
     }
+    DevScope ds(t->dev);
     std::lock_guard<std::mutex> lk(t->ix->mu);
     return kd_tree_positions(t->ix->kd, pos);
 }
@@ -645,6 +911,7 @@ int tiler_psyv_batch_dev(int n, const int32_t *rgb, const uint8_t *palpix, const
                          const int32_t *palettes, const int32_t *pal_of, const uint8_t *flags_per, int flags, int gamma,
                          double *out64, float *out32, void *stream) {
     if (!ensure_init()) return -1;
+    DevScope ds(ptr_device(rgb ? (const void *)rgb : (const void *)palpix));
     PsyvArgs a;
     a.n = n;
     a.rgb = rgb;
@@ -711,12 +978,8 @@ int tiler_psyv_batch(int n, const int32_t *rgb, int n_tiles, const uint8_t *palp
     return rc;
 }
 
-int tiler_ft_set_maps(ann_kdtree *t, const int32_t *tr_tile, const int32_t *tr_pal, const uint8_t *tr_attr) {
-    if (!t || !t->ix || !tr_tile || !tr_pal || !tr_attr) {
-        set_error("tiler_ft_set_maps: invalid arguments");
-        return -1;
-    }
-    if (!ensure_init()) return -1;
+static int set_maps_one(ann_kdtree *t, const int32_t *tr_tile, const int32_t *tr_pal, const uint8_t *tr_attr) {
+    DevScope ds(t->dev);
     NNIndex *ix = t->ix;
     std::lock_guard<std::mutex> lk(ix->mu);
     const size_t n = std::max(1, ix->n);
@@ -732,6 +995,19 @@ int tiler_ft_set_maps(ann_kdtree *t, const int32_t *tr_tile, const int32_t *tr_p
     return 0;
 }
 
+int tiler_ft_set_maps(ann_kdtree *t, const int32_t *tr_tile, const int32_t *tr_pal, const uint8_t *tr_attr) {
+    if (!t || !t->ix || !tr_tile || !tr_pal || !tr_attr) {
+        set_error("tiler_ft_set_maps: invalid arguments");
+        return -1;
+    }
+    if (!ensure_init()) return -1;
+    if (set_maps_one(t, tr_tile, tr_pal, tr_attr)) return -1;
+    std::lock_guard<std::mutex> lk(t->rep_mu);  // the copies on other devices get the same maps
+    for (int d = 0; d < MAX_DEV; d++)
+        if (t->rep[d] && set_maps_one(t->rep[d], tr_tile, tr_pal, tr_attr)) return -1;
+    return 0;
+}
+
 int tiler_ft_get_maps(ann_kdtree *t, int32_t *tr_tile, int32_t *tr_pal, uint8_t *tr_attr) {
     if (!t || !t->ix || !tr_tile || !tr_pal || !tr_attr) {
         set_error("tiler_ft_get_maps: invalid arguments");
@@ -742,14 +1018,30 @@ int tiler_ft_get_maps(ann_kdtree *t, int32_t *tr_tile, int32_t *tr_pal, uint8_t 
         return -1;
     }
     if (!ensure_init()) return -1;
+    DevScope ds(t->dev);
     NNIndex *ix = t->ix;
     std::lock_guard<std::mutex> lk(ix->mu);
-    TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
-    TILER_HIP_CHECK(hipDeviceSynchronize());  // maps may have been written on the creator's stream
+    // maps written by tiler_prepare_frame_tiling_dev on the caller's stream: wait for that work only (the other
+    // streams of the device keep running); tiler_ft_set_maps copies synchronously
+    if (t->maps_ev) TILER_HIP_CHECK(hipEventSynchronize(t->maps_ev));
     TILER_HIP_CHECK(hipMemcpy(tr_tile, ix->d_tr_tile, (size_t)ix->n * 4, hipMemcpyDeviceToHost));
     TILER_HIP_CHECK(hipMemcpy(tr_pal, ix->d_tr_pal, (size_t)ix->n * 4, hipMemcpyDeviceToHost));
     TILER_HIP_CHECK(hipMemcpy(tr_attr, ix->d_tr_attr, (size_t)ix->n, hipMemcpyDeviceToHost));
     return 0;
+}
+
+// FrameTiling on handle t itself (its device; the entry points pick the handle)
+static int frame_tiling_on(ann_kdtree *t, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int32_t *d_tile,
+                           int32_t *d_pal, uint8_t *d_hm, uint8_t *d_vm, float *d_err, void *stream) {
+    if (!t->ix->d_tr_tile) {
+        set_error("tiler_frame_tiling: call tiler_ft_set_maps first");
+        return -1;
+    }
+    DevScope ds(t->dev);
+    std::lock_guard<std::mutex> lk(t->ix->mu);
+    if (ensure_io(t, Q, 1, 1)) return -1;
+    FtMaps m{d_tile, d_pal, d_hm, d_vm};
+    return nn_frame_tiling_dev(t->ix, d_rgb, Q, use_wavelets, gamma, t->d_idx, d_err, &m, (hipStream_t)stream);
 }
 
 int tiler_frame_tiling_dev(ann_kdtree *t, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int32_t *d_tile,
@@ -758,15 +1050,9 @@ int tiler_frame_tiling_dev(ann_kdtree *t, const int32_t *d_rgb, int Q, int use_w
         set_error("tiler_frame_tiling: null handle");
         return -1;
     }
-    if (!t->ix->d_tr_tile) {
-        set_error("tiler_frame_tiling: call tiler_ft_set_maps first");
-        return -1;
-    }
     if (!ensure_init()) return -1;
-    std::lock_guard<std::mutex> lk(t->ix->mu);
-    if (ensure_io(t, Q, 1, 1)) return -1;
-    FtMaps m{d_tile, d_pal, d_hm, d_vm};
-    return nn_frame_tiling_dev(t->ix, d_rgb, Q, use_wavelets, gamma, t->d_idx, d_err, &m, (hipStream_t)stream);
+    if (!(t = handle_for(t, d_rgb))) return -1;
+    return frame_tiling_on(t, d_rgb, Q, use_wavelets, gamma, d_tile, d_pal, d_hm, d_vm, d_err, stream);
 }
 
 int tiler_frame_tiling(ann_kdtree *t, const int32_t *rgb, int Q, int use_wavelets, int gamma, int32_t *out_tile,
@@ -777,6 +1063,7 @@ int tiler_frame_tiling(ann_kdtree *t, const int32_t *rgb, int Q, int use_wavelet
     }
     if (Q == 0) return 0;
     if (!ensure_init()) return -1;
+    DevScope ds(t->dev);
     if ((size_t)Q > t->cap_ft) {
         hipFree(t->d_rgb);
         hipFree(t->d_mt);
@@ -795,8 +1082,7 @@ int tiler_frame_tiling(ann_kdtree *t, const int32_t *rgb, int Q, int use_wavelet
         if (ensure_io(t, Q, 1, 1)) return -1;
     }
     TILER_HIP_CHECK(hipMemcpyAsync(t->d_rgb, rgb, (size_t)Q * 256, hipMemcpyHostToDevice, t->stream));
-    if (tiler_frame_tiling_dev(t, t->d_rgb, Q, use_wavelets, gamma, t->d_mt, t->d_mp, t->d_mh, t->d_mv, t->d_err,
-                               t->stream))
+    if (frame_tiling_on(t, t->d_rgb, Q, use_wavelets, gamma, t->d_mt, t->d_mp, t->d_mh, t->d_mv, t->d_err, t->stream))
         return -1;
     TILER_HIP_CHECK(hipMemcpyAsync(out_tile, t->d_mt, (size_t)Q * 4, hipMemcpyDeviceToHost, t->stream));
     TILER_HIP_CHECK(hipMemcpyAsync(out_pal, t->d_mp, (size_t)Q * 4, hipMemcpyDeviceToHost, t->stream));
@@ -818,6 +1104,7 @@ int tiler_smooth_keyframe_dev(int F, int Q, int32_t *d_tile, int32_t *d_tmpidx, 
                               uint8_t *d_vm, uint8_t *d_smoothed, const uint8_t *d_palpix, const int32_t *d_palettes,
                               double strength, void *stream) {
     if (!ensure_init()) return -1;
+    DevScope ds(ptr_device(d_tile));
     return smooth_keyframe_dev(F, Q, d_tile, d_tmpidx, d_pal, d_hm, d_vm, d_smoothed, d_palpix, d_palettes, strength,
                                (hipStream_t)stream);
 }
@@ -831,6 +1118,7 @@ int tiler_dither_tiles(int n, const int32_t *rgb, const int32_t *pal_of, const i
 int tiler_dither_tiles_dev(int n, const int32_t *d_rgb, const int32_t *d_pal_of, const int32_t *d_palettes,
                            int n_palettes, int palsize, uint8_t *d_palpix, uint8_t *d_hm, uint8_t *d_vm, void *stream) {
     if (!ensure_init()) return -1;
+    DevScope ds(ptr_device(d_rgb));
     return dither_tiles_tk_dev(n, d_rgb, d_pal_of, d_palettes, n_palettes, palsize, d_palpix, d_hm, d_vm,
                                (hipStream_t)stream);
 }
@@ -847,6 +1135,7 @@ int tiler_quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_
                                 int n_palettes, int palsize, int lookup_bpc, int32_t *palettes, int32_t *use_count,
                                 int32_t *colors, void *stream) {
     if (!ensure_init()) return -1;
+    DevScope ds(ptr_device(d_rgb));
     return quantize_palettes_dev(n_tiles, d_rgb, d_pal_of, d_active, n_palettes, palsize, lookup_bpc, palettes,
                                  use_count, colors, (hipStream_t)stream);
 }
@@ -860,6 +1149,7 @@ int tiler_prepare_dither_tiles_dev(long n_tiles, const int32_t *d_rgb, int n_pal
                                    int max_iter, uint32_t seed, int32_t *d_labels, double *d_centroids,
                                    int *iterations, void *stream) {
     if (!ensure_init()) return -1;
+    DevScope ds(ptr_device(d_rgb));
     return prepare_dither_dev(n_tiles, d_rgb, n_palettes, gamma, use_wavelets, max_iter <= 0 ? 0x7fffffff : max_iter,
                               seed, d_labels, d_centroids, iterations, (hipStream_t)stream);
 }
@@ -943,6 +1233,7 @@ int tiler_interframe_correlation(const int32_t *rgb, int F, int tm_w, int tm_h, 
 
 int tiler_interframe_correlation_dev(const int32_t *d_rgb, int F, int tm_w, int tm_h, double *corr, void *stream) {
     if (!ensure_init()) return -1;
+    DevScope ds(ptr_device(d_rgb));
     return interframe_corr_dev(d_rgb, F, tm_w, tm_h, corr, (hipStream_t)stream);
 }
 
@@ -976,6 +1267,7 @@ int tiler_kmodes_batch_dev(const uint8_t *d_X, const int32_t *bin_off, int nbins
         set_error("kmodes: null buffer");
         return -1;
     }
+    DevScope ds(ptr_device(d_X));
     return kmodes_batch_dev(d_X, bin_off, nbins, k, start, n_modalities, d_labels, d_centroids, n_iter, cost,
                             (hipStream_t)stream);
 }

@@ -694,8 +694,9 @@ void kd_tree_destroy(KdTree *t) {
     delete t;
 }
 
-// pinned host staging reused across builds (pinning is slow); builds are serialised by g_build_mu
-static std::mutex g_build_mu;
+// pinned host staging reused across builds (pinning is slow); builds on one device are serialised by its mutex
+static constexpr int KD_MAX_DEV = 64;
+static std::mutex g_build_mu[KD_MAX_DEV];
 struct Pinned {
     void *p = nullptr;
     size_t cap = 0;
@@ -704,17 +705,19 @@ struct Pinned {
             if (p) (void)hipHostFree(p);
             p = nullptr;
             cap = 0;
-            if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+            if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) return nullptr;
             cap = bytes;
         }
         return p;
     }
 };
-static Pinned g_pin_nodes, g_pin_ch;
+static Pinned g_pin_nodes[KD_MAX_DEV], g_pin_ch[KD_MAX_DEV];
 
 KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t stream) {
     const auto t0 = std::chrono::steady_clock::now();
-    std::lock_guard<std::mutex> build_lk(g_build_mu);
+    int kdev = 0;
+    if (hipGetDevice(&kdev) != hipSuccess || kdev < 0 || kdev >= KD_MAX_DEV) kdev = 0;
+    std::lock_guard<std::mutex> build_lk(g_build_mu[kdev]);
     KdTree *t = new KdTree();
     t->n = n;
     t->dd = dd;
@@ -799,8 +802,8 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
         const int n_nodes = node_off[nlev] + (int)deferred.size(), n_ch = ch_off[nlev];
         KdNodeDev *h_nodes;
         KdChunk *h_ch;
-        KD_PIN(h_nodes, g_pin_nodes, (size_t)std::max(n_nodes, 1) * sizeof(KdNodeDev));
-        KD_PIN(h_ch, g_pin_ch, (size_t)std::max(n_ch, 1) * sizeof(KdChunk));
+        KD_PIN(h_nodes, g_pin_nodes[kdev], (size_t)std::max(n_nodes, 1) * sizeof(KdNodeDev));
+        KD_PIN(h_ch, g_pin_ch[kdev], (size_t)std::max(n_ch, 1) * sizeof(KdChunk));
         int max_nn = 1, max_big = 1;
         for (int L = 0; L < nlev; L++) {
             int c = ch_off[L];

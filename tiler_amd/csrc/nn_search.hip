@@ -1151,7 +1151,7 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hip
     }
     ix->S = pick_S(d);
     ix->nblk = (n + 31) / 32;
-    TILER_HIP_CHECK_NULL(hipHostMalloc((void **)&ix->h_fb_count, sizeof(int) * 2, hipHostMallocDefault));
+    TILER_HIP_CHECK_NULL(hipHostMalloc((void **)&ix->h_fb_count, sizeof(int) * 2, hipHostMallocPortable));
     ix->h_fb_count[0] = 1 << 30;  // first call: full tier-2 grid
     ix->h_fb_count[1] = 0;
     if (ix->S == 0 || n == 0) return ix;

@@ -205,7 +205,7 @@ NNIndex *prepare_frame_tiling_dev(NNIndex *global, PrepScratch &s, const int32_t
         set_error("prepare_frame_tiling: invalid arguments");
         return nullptr;
     }
-    if (!s.h_total) TILER_HIP_CHECK_NULL(hipHostMalloc((void **)&s.h_total, 2 * sizeof(int), hipHostMallocDefault));
+    if (!s.h_total) TILER_HIP_CHECK_NULL(hipHostMalloc((void **)&s.h_total, 2 * sizeof(int), hipHostMallocPortable));
     if (!s.total) TILER_HIP_CHECK_NULL(hipMalloc((void **)&s.total, 2 * sizeof(int)));
     if (!s.done) TILER_HIP_CHECK_NULL(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
     // the previous prepare's map copies (queued on its own stream) still read tile_of / pal_of / attrs

@@ -99,6 +99,12 @@ int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
 int tiler_set_scan_limits(int max_k1, int max_k8);
 /* Coalescing counters of the single-query entry points on this handle: calls, batches searched, largest batch. */
 int tiler_combine_stats(ann_kdtree *akd, int64_t *calls, int64_t *batches, int32_t *max_batch);
+/* Test / bench hook: the reference's per-call pattern timed natively (no interpreter between the calls): the first
+ * min(nq, 64) queries as lone calls on one thread (median latency -> *lone_us), then all nq from `threads` native
+ * threads calling ann_kdtree_search (k = 1) or ann_kdtree_search_multi (k > 1) once per query on this one handle
+ * (query i on thread i % threads) -> *wall_s.  q[nq][dd] host rows; idx / err [nq][k] receive every answer.  0 / -1. */
+int tiler_debug_percall_bench(ann_kdtree *akd, const float *q, int nq, int k, int threads, int32_t *idx, float *err,
+                              double *wall_s, double *lone_us);
 /* Leaf position of every dataset point in ANN's kd-tree (the order of its depth-first scan with every near
  * child LO): pos[n].  -1 when the handle was created with TILER_SPLIT_INDEX_ORDER. */
 int tiler_kdtree_positions(ann_kdtree *akd, int32_t *pos);

@@ -11,7 +11,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-BENCH="python3 $R/bench.py --steps $STEPS --warmup 1 --no-cpu --no-smooth --no-palettes --no-globaltiling"
+BENCH="python3 $R/bench.py --steps $STEPS --warmup 1 --no-cpu --no-smooth --no-palettes --no-globaltiling --no-keyframes --no-dither --no-encoder --no-per-call"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- $BENCH > "$OUT/trace.log" 2>&1
 echo "trace done"
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \

@@ -108,3 +108,37 @@ def test_concurrent_errors_reach_every_caller(gpu):
                     kdt.search_multi(q[i], 40)
         _run_threads(one, 64)
     assert np.array_equal(out, np.arange(64))
+
+
+def test_native_percall_harness_exact(gpu, oracle):
+    """tiler_debug_percall_bench: the per-call pattern from 16 native threads (no interpreter between calls), k = 1 on
+    a keyframe handle and k = 8 on the global 64-d handle; every answer equals the restated ANN search."""
+    import ctypes
+    vp = ctypes.c_void_p
+    lib = gpu.load()
+    rng = np.random.default_rng(44)
+    tiles, thm, tvm = synth.tileset(rng, 2000)
+    pals = synth.palettes(rng, 8)
+    used = synth.used_one_palette(rng.integers(0, 8, 2000).astype(np.int32), 8)
+    ods, *_ = oracle.build_ft_dataset(used, tiles, thm, tvm, pals)
+    q1 = oracle.psyv_batch(3000, rgb=synth.frame_tiles(rng, 3000), flags=2).astype(np.float32)
+    gds, _, _ = oracle.prepare_global_ds(tiles)
+    q8 = tiles[rng.integers(0, 2000, 1000)].astype(np.float32)
+    for data, q, k in ((ods, q1, 1), (gds, q8, 8)):
+        idx = np.full((q.shape[0], k), -7, np.int32)
+        err = np.zeros((q.shape[0], k), np.float32)
+        wall, lone = ctypes.c_double(0), ctypes.c_double(0)
+        with gpu.KDTree(data) as kdt:
+            rc = lib.tiler_debug_percall_bench(kdt.handle, q.ctypes.data_as(vp), q.shape[0], k, THREADS,
+                                               idx.ctypes.data_as(vp), err.ctypes.data_as(vp), ctypes.byref(wall),
+                                               ctypes.byref(lone))
+            assert rc == 0, gpu.last_error()
+            cs = kdt.combine_stats()
+        okd = oracle.KDTree(data)
+        oi, oe = okd.search_batch(q, k=k)
+        okd.close()
+        oi, oe = oi.reshape(-1, k), oe.reshape(-1, k)
+        assert np.array_equal(idx, oi) and np.array_equal(err.view(np.uint32), oe.view(np.uint32)), k
+        assert cs["calls"] == q.shape[0] + min(64, q.shape[0]) and cs["batches"] < cs["calls"]
+        print(f"k={k}: {q.shape[0] / wall.value:.0f} calls/s on {THREADS} native threads, lone {lone.value:.1f} us, "
+              f"avg batch {cs['calls'] / cs['batches']:.1f}")

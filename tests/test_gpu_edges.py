@@ -121,3 +121,29 @@ def test_nonfinite_dataset_builds_and_searches(gpu):
     assert ((gi >= 0) & (gi < n)).all()
     assert np.array_equal(dist[np.arange(q.shape[0]), gi].view(np.uint32), ge.view(np.uint32))
     assert np.all(np.isnan(ge) | (ge >= best))
+
+
+def test_tier2_overflow_on_fresh_index_exact(gpu, oracle):
+    """a fresh index sizes its generic tier-2 slots from the recent count of OTHER indexes.  Here an
+    index whose searches need no tier 2 runs first, then a fresh index where every one of 70,000 queries ties 16
+    identical copies (its lane lists fill with equal keys: all go to tier 2, more than the 65,536 slots of one
+    chunk).  Whatever the slots, every answer must be exact (the overflow goes to the exhaustive tier 3): a sample of
+    3,000 queries equals the restated lowest-index scan."""
+    rng = np.random.default_rng(71)
+    plain = rng.normal(0, 1, (20000, 192)).astype(np.float32)
+    with gpu.KDTree(plain, split=INDEX_ORDER) as kdt:
+        kdt.search_batch(plain[:4096] + 0.5)
+        assert kdt.stats()["fallback_queries"] < 1000
+    base = rng.normal(0, 1, (2048, 192)).astype(np.float32)
+    data = np.tile(base, (16, 1))
+    pick = rng.integers(0, 2048, 70000)
+    q = base[pick] + rng.normal(0, 1e-3, (70000, 192)).astype(np.float32)
+    with gpu.KDTree(data, split=INDEX_ORDER) as kdt:
+        gi, ge = kdt.search_batch(q)
+        st = kdt.stats()
+    assert st["orbit_search"] == 0 and st["fallback_queries"] + st["exhaustive_queries"] > 65536, st
+    s = np.random.default_rng(5).choice(q.shape[0], 3000, replace=False)
+    oi, oe = oracle.nn_batch(data, q[s])
+    assert np.array_equal(gi[s], oi)
+    assert np.array_equal(ge[s].view(np.uint32), oe.view(np.uint32))
+    assert (gi < 2048).all()  # the lowest-index copy

@@ -9,6 +9,9 @@
 #include <string.h>
 
 #include <atomic>
+#include <algorithm>
+#include <chrono>
+#include <thread>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -283,8 +286,8 @@ struct Combiner {
     std::deque<CombineReq *> pending;
     bool busy = false;
     // pinned staging of the batch in flight (only the leader touches them)
-    float *h_q = nullptr, *h_err = nullptr;
-    int *h_idx = nullptr;
+    float *h_q = nullptr;
+    int *h_idx = nullptr;  // [2][cap_r / 2]: indices, then distances
     size_t cap_q = 0, cap_r = 0;
     long long batches = 0, calls = 0;  // counters (tiler_combine_stats)
     int max_batch = 0;
@@ -493,7 +496,6 @@ static void handle_free(ann_kdtree *t) {
     }
     (void)hipHostFree(t->comb.h_q);
     (void)hipHostFree(t->comb.h_idx);
-    (void)hipHostFree(t->comb.h_err);
     if (t->maps_ev) (void)hipEventDestroy(t->maps_ev);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     unplace_handle(t->dev, t->placed);
@@ -723,26 +725,32 @@ static int combine_run(ann_kdtree *t, std::vector<CombineReq *> &b, int k) {
         TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_q, (size_t)nq * d * sizeof(float), hipHostMallocPortable));
         c.cap_q = (size_t)nq * d;
     }
-    if ((size_t)nq * k > c.cap_r) {
+    const size_t nr = (size_t)nq * k;
+    if (2 * nr > c.cap_r) {  // one pinned block: indices then distances (one copy back per batch)
         hipHostFree(c.h_idx);
-        hipHostFree(c.h_err);
         c.h_idx = nullptr;
-        c.h_err = nullptr;
         c.cap_r = 0;
-        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_idx, (size_t)nq * k * sizeof(int), hipHostMallocPortable));
-        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_err, (size_t)nq * k * sizeof(float), hipHostMallocPortable));
-        c.cap_r = (size_t)nq * k;
+        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_idx, 2 * nr * sizeof(int), hipHostMallocPortable));
+        c.cap_r = 2 * nr;
     }
     for (int j = 0; j < nq; j++) memcpy(c.h_q + (size_t)j * d, b[j]->q, (size_t)d * sizeof(float));
-    if (ensure_io(t, nq, d, k)) return -1;
+    if (ensure_io(t, nq, d, k)) return -1;  // d_idx holds nq * max(d, k) >= 2 * nq * k ints (d >= 2 k here)
+    int *r_idx = t->d_idx;
+    float *r_err = reinterpret_cast<float *>(t->d_idx + nr);
+    if ((size_t)nq * std::max(d, k) < 2 * nr) r_err = t->d_err;  // tiny d: the separate buffer (two copies)
     TILER_HIP_CHECK(hipMemcpyAsync(t->d_q, c.h_q, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, t->stream));
-    if (nn_search_dev(ix, t->d_q, nq, k, t->d_idx, t->d_err, nullptr, t->stream)) return -1;
-    TILER_HIP_CHECK(hipMemcpyAsync(c.h_idx, t->d_idx, (size_t)nq * k * sizeof(int), hipMemcpyDeviceToHost, t->stream));
-    TILER_HIP_CHECK(hipMemcpyAsync(c.h_err, t->d_err, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToHost, t->stream));
+    if (nn_search_dev(ix, t->d_q, nq, k, r_idx, r_err, nullptr, t->stream)) return -1;
+    float *h_err = reinterpret_cast<float *>(c.h_idx + nr);
+    if (r_err == reinterpret_cast<float *>(r_idx + nr)) {
+        TILER_HIP_CHECK(hipMemcpyAsync(c.h_idx, r_idx, 2 * nr * sizeof(int), hipMemcpyDeviceToHost, t->stream));
+    } else {
+        TILER_HIP_CHECK(hipMemcpyAsync(c.h_idx, r_idx, nr * sizeof(int), hipMemcpyDeviceToHost, t->stream));
+        TILER_HIP_CHECK(hipMemcpyAsync(h_err, r_err, nr * sizeof(float), hipMemcpyDeviceToHost, t->stream));
+    }
     TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
     for (int j = 0; j < nq; j++) {
         memcpy(b[j]->idx, c.h_idx + (size_t)j * k, (size_t)k * sizeof(int));
-        memcpy(b[j]->err, c.h_err + (size_t)j * k, (size_t)k * sizeof(float));
+        memcpy(b[j]->err, h_err + (size_t)j * k, (size_t)k * sizeof(float));
     }
     return 0;
 }
@@ -837,6 +845,57 @@ int tiler_combine_stats(ann_kdtree *t, int64_t *calls, int64_t *batches, int32_t
     if (calls) *calls = t->comb.calls;
     if (batches) *batches = t->comb.batches;
     if (max_batch) *max_batch = t->comb.max_batch;
+    return 0;
+}
+
+int tiler_debug_percall_bench(ann_kdtree *t, const float *q, int nq, int k, int threads, int32_t *idx, float *err,
+                              double *wall_s, double *lone_us) {
+    if (!t || !t->ix || nq < 0 || (nq > 0 && (!q || !idx || !err)) || k < 1 || k > 32 || threads < 1 || threads > 256) {
+        set_error("tiler_debug_percall_bench: invalid arguments");
+        return -1;
+    }
+    const int d = t->ix->d;
+    auto call = [&](int i) -> int {
+        float *qi = const_cast<float *>(q + (size_t)i * d);
+        if (k == 1) {
+            const int r = ann_kdtree_search(t, qi, 0.0f, err + i);
+            idx[i] = r;
+            return r < 0 && t->ix->n > 0 ? -1 : 0;
+        }
+        return ann_kdtree_search_multi(t, idx + (size_t)i * k, err + (size_t)i * k, k, qi, 0.0f);
+    };
+    // lone calls: one caller, one query at a time (the latency of the whole per-call path)
+    const int nl = std::min(nq, 64);
+    std::vector<double> lat;
+    for (int i = 0; i < nl; i++) {
+        const auto a = std::chrono::steady_clock::now();
+        if (call(i)) return -1;
+        lat.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count());
+    }
+    std::sort(lat.begin(), lat.end());
+    if (lone_us) *lone_us = lat.empty() ? 0.0 : lat[lat.size() / 2];
+    // `threads` native callers on the one handle, query i on thread i % threads (a pool's workers)
+    std::atomic<int> bad{0};
+    std::string msg;
+    std::mutex msg_mu;
+    const auto a = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int w = 0; w < threads; w++)
+        th.emplace_back([&, w]() {
+            for (int i = w; i < nq; i += threads)
+                if (call(i)) {
+                    bad.store(1);
+                    std::lock_guard<std::mutex> lk(msg_mu);
+                    msg = last_error();
+                    return;
+                }
+        });
+    for (auto &x : th) x.join();
+    if (wall_s) *wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+    if (bad.load()) {
+        set_error("tiler_debug_percall_bench: " + msg);
+        return -1;
+    }
     return 0;
 }
 

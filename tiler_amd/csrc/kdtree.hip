@@ -1049,9 +1049,14 @@ __global__ __launch_bounds__(64) void kd_replay_kernel(KdOrder o, KdFixArgs a) {
 // one wave per query: coalesced row read, the outside-the-box terms in parallel, then their sequential fp32 sum
 // in dimension order (a term inside the box is +0 and leaves the running sum unchanged, so only the others are
 // added, by one lane, in order)
+// done / count (or null): the search's per-query verify flags and replay count, cleared here (saves two memsets)
 __global__ __launch_bounds__(256) void kd_rootbox_kernel(KdOrder o, const float *__restrict__ q, int nq,
-                                                         float *__restrict__ out) {
+                                                         float *__restrict__ out, uint8_t *__restrict__ done,
+                                                         int *__restrict__ count) {
     const int lane = threadIdx.x & 63;
+    if (count && blockIdx.x == 0 && threadIdx.x == 0) *count = 0;
+    if (done)
+        for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nq; i += (long)gridDim.x * 256) done[i] = 0;
     for (long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6); i < nq; i += (long)gridDim.x * 4) {
         float rb = 0.0f;
         for (int d0 = 0; d0 < o.dd; d0 += 64) {
@@ -1080,11 +1085,12 @@ __global__ __launch_bounds__(256) void kd_rootbox_kernel(KdOrder o, const float 
     }
 }
 
-int kd_root_boxes(const KdTree *t, const float *d_q, int nq, float *rootbox, hipStream_t stream) {
+int kd_root_boxes(const KdTree *t, const float *d_q, int nq, float *rootbox, hipStream_t stream, uint8_t *done,
+                  int *count) {
     if (!t || nq <= 0) return 0;
     KTimer tm("kd_verify", stream);
     hipLaunchKernelGGL(kd_rootbox_kernel, dim3((unsigned)std::min<long>(8192, (nq + 3) / 4)), dim3(256), 0, stream,
-                       t->view(), d_q, nq, rootbox);
+                       t->view(), d_q, nq, rootbox, done, count);
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }

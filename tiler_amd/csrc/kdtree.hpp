@@ -59,7 +59,9 @@ struct KdFixArgs {
     const uint8_t *done = nullptr;          // [nq] or null: 1 = already checked (the pair pass), skip
 };
 // rootbox[q] = annBoxDistance(q, box) for nq fp32 rows q[nq][dd] (queries whose descriptor kernel did not fuse it)
-int kd_root_boxes(const KdTree *t, const float *d_q, int nq, float *rootbox, hipStream_t stream);
+// annBoxDistance of every query to the root box; done[nq] / count (optional) are zeroed by the same launch
+int kd_root_boxes(const KdTree *t, const float *d_q, int nq, float *rootbox, hipStream_t stream,
+                  uint8_t *done = nullptr, int *count = nullptr);
 int kd_verify_and_replay(const KdTree *t, const KdFixArgs &a, hipStream_t stream);
 
 }  // namespace tiler

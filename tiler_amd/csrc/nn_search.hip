@@ -1485,11 +1485,15 @@ static int launch_exact(RescoreArgs ra, int list_n, int grid, hipStream_t stream
 static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t stream, const OrbitTail *orbit);
 
 // generic tier-2 slots of a search: whole chunks covering 1.5x the largest tier-2 count of the recent searches (this
-// index's last count, or the last one seen on any index: an encoder builds a new index per keyframe), >= 1 chunk
+// index's last count, or the last one seen on any index: an encoder builds a new index per keyframe), >= 1 chunk.
+// A fresh index (the 1 << 30 sentinel: no search of its own yet) takes 3x the recent count of the other indexes, a
+// margin for an unrelated one.  Queries past the slots go to the exhaustive tier 3: exact either way, slower.
 static std::atomic<int> g_t2_recent{0};
 static int tier2_slots(NNIndex *ix, int nq) {
     const int own = ix->h_fb_count ? ((volatile int *)ix->h_fb_count)[0] : 0;
-    const int prev = std::max(own < (1 << 30) ? own : 0, g_t2_recent.load(std::memory_order_relaxed));
+    const bool fresh = own >= (1 << 30);
+    const int recent = g_t2_recent.load(std::memory_order_relaxed);
+    const int prev = fresh ? 2 * recent : std::max(own, recent);
     const long want = (long)prev + prev / 2 + 1;
     const long chunks = std::max(1L, (want + TIER2_MAX - 1) / TIER2_MAX);
     return (int)std::min<long>(nq, chunks * TIER2_MAX);
@@ -1534,9 +1538,12 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     if (!ix->done_event) TILER_HIP_CHECK(hipEventCreateWithFlags(&ix->done_event, hipEventDisableTiming));
     if (ix->kd) {  // ANN's tie order: the pruning check needs every query's box distance and a clean slate
         if (ensure_scratch(ix, nq, 0)) return -1;
-        if (!rootbox_ready && kd_root_boxes(ix->kd, d_q, nq, s.kd_rootbox, stream)) return -1;
-        TILER_HIP_CHECK(hipMemsetAsync(s.kd_done, 0, (size_t)nq, stream));
-        TILER_HIP_CHECK(hipMemsetAsync(s.kd_count, 0, sizeof(int), stream));
+        if (!rootbox_ready) {  // the box distances, with the verify flags and the replay count cleared in the same launch
+            if (kd_root_boxes(ix->kd, d_q, nq, s.kd_rootbox, stream, s.kd_done, s.kd_count)) return -1;
+        } else {
+            TILER_HIP_CHECK(hipMemsetAsync(s.kd_done, 0, (size_t)nq, stream));
+            TILER_HIP_CHECK(hipMemsetAsync(s.kd_count, 0, sizeof(int), stream));
+        }
     }
     if (search_core(ix, ra, d_q, nq, k, stream, orbit_prepared)) return -1;
 #ifdef TILER_EXPERIMENTS
@@ -1581,9 +1588,8 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
     const int K = k == 1 ? 1 : 8;
     if (ensure_scratch(ix, nq, (long)nq * nsplit * K)) return -1;
     SearchScratch &s = ix->scratch;
-    ix->last_splits = 0;
+    ix->last_splits = 0;  // the stats report no tier-2 / tier-3 queries for a scan (fb_count is not read)
     ix->last_fallback = 0;
-    TILER_HIP_CHECK(hipMemsetAsync(s.fb_count, 0, 16, stream));  // the stats' tier counts: none
     KTimer tm("nn_scan", stream);
     // the per-query work is unrolled over QN: the smallest instance that holds a group
     const int qn = K == 1 ? (nq == 1 ? 1 : nq <= 4 ? 4 : SCAN_QN1) : (nq == 1 ? 1 : SCAN_QN8);
@@ -1759,7 +1765,8 @@ static int search_tail(NNIndex *ix, const RescoreArgs &ra, int nq, hipStream_t s
     }
     if (launch_exact(ra, 0, std::min(nq, 1024), stream)) return -1;
     TILER_HIP_CHECK(hipMemcpyAsync(ix->h_fb_count, s.fb_count, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
-    if (!orbit) {  // the previous search's count on this index (already landed: the host waited for it)
+    if (!orbit) {  // a heuristic only: the copy above is still in flight, so this reads the previous search's count
+        // on this index (or, racing the DMA, this one's; the sentinel on a fresh index is skipped)
         const int c = ((volatile int *)ix->h_fb_count)[0];
         if (c >= 0 && c < (1 << 30)) g_t2_recent.store(c, std::memory_order_relaxed);
     }

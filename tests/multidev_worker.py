@@ -27,6 +27,7 @@ import pyoracle  # noqa: E402
 import tiler_amd  # noqa: E402
 from tiler_amd import frame_tiling as ft  # noqa: E402
 from tiler_amd import synth  # noqa: E402
+from tiler_amd._lib import check  # noqa: E402
 
 THREADS = 16
 
@@ -138,7 +139,7 @@ def main():
         o = [torch.empty(Q, dtype=t, device=dev) for t in (torch.int32, torch.int32, torch.uint8, torch.uint8,
                                                             torch.float32)]
         vp = ctypes.c_void_p
-        tiler_amd.check(lib.tiler_frame_tiling_dev(kt.handle, vp(d_rgb.data_ptr()), Q, 1, -1,
+        check(lib.tiler_frame_tiling_dev(kt.handle, vp(d_rgb.data_ptr()), Q, 1, -1,
                                                    *[vp(x.data_ptr()) for x in o], None), "tiler_frame_tiling_dev")
         torch.cuda.synchronize(dev)
         host = ft.KeyframeTiler.__new__(ft.KeyframeTiler)  # the host entry point runs on the handle itself
@@ -172,12 +173,12 @@ def main():
     kt = kdts[3]
     kt.replicate(-1)
     vp = ctypes.c_void_p
-    tiler_amd.check(lib.tiler_ft_set_maps(kt.handle, ot.ctypes.data_as(vp), op.ctypes.data_as(vp),
+    check(lib.tiler_ft_set_maps(kt.handle, ot.ctypes.data_as(vp), op.ctypes.data_as(vp),
                                           oa.ctypes.data_as(vp)), "tiler_ft_set_maps")
     Q = frames.shape[0]
     o = [torch.empty(Q, dtype=t, device=dev) for t in (torch.int32, torch.int32, torch.uint8, torch.uint8,
                                                         torch.float32)]
-    tiler_amd.check(lib.tiler_frame_tiling_dev(kt.handle, vp(d_rgb.data_ptr()), Q, 1, -1,
+    check(lib.tiler_frame_tiling_dev(kt.handle, vp(d_rgb.data_ptr()), Q, 1, -1,
                                                *[vp(x.data_ptr()) for x in o], None), "tiler_frame_tiling_dev")
     torch.cuda.synchronize(dev)
     ref = pyoracle.frame_tiling(frames, ods, ot, op, oa)

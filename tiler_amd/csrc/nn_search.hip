@@ -432,6 +432,69 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
         half8 a0 = A[0], a1 = A[64];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (st + NBUF - 1 < nstage) issue(st + NBUF - 1, (st + NBUF - 1) % NBUF);
+        if constexpr (!FLAT && MODE == 0 && (VAR & 4) != 0) {
+            // Software-pipelined stage: block cb + 1's contraction is issued before block cb's epilogue (two
+            // accumulator sets), so the epilogue's VALU runs beside this wave's own MFMAs; every element is compared
+            // once and its mask both gates the wave-uniform branch and selects the list insertions (the same tests
+            // as VAR 1, so the same lists).
+            const int nb = min(CB, b_end - (b_begin + st * CB));  // >= 1: st < nstage
+            floatx4 acc2[2][QB];
+            auto contract = [&](int cb, floatx4(&ac)[QB]) {  // a0 / a1: block cb's first fragment pair on entry,
+#pragma unroll                                                   // block cb + 1's on exit
+                for (int s = 0; s < S; s += 2) {
+                    half8 n0, n1;
+                    const bool more = s + 2 < S || cb + 1 < CB;
+                    if (s + 2 < S) {
+                        n0 = A[(cb * S + s + 2) * 64];
+                        n1 = A[(cb * S + s + 3) * 64];
+                    } else if (cb + 1 < CB) {
+                        n0 = A[((cb + 1) * S) * 64];
+                        n1 = A[((cb + 1) * S + 1) * 64];
+                    }
+#pragma unroll
+                    for (int q = 0; q < QB; q++)
+                        ac[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bq[q][s], s == 0 ? sd[cb] : ac[q], 0, 0, 0);
+#pragma unroll
+                    for (int q = 0; q < QB; q++)
+                        ac[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bq[q][s + 1], ac[q], 0, 0, 0);
+                    if (more) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2 * QB, 0);
+                    if (more) {
+                        a0 = n0;
+                        a1 = n1;
+                    }
+                }
+            };
+            auto epilogue = [&](int cb, const floatx4(&ac)[QB]) {
+                bool p[QB][4], need = false;
+#pragma unroll
+                for (int q = 0; q < QB; q++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        p[q][i] = ac[q][i] > th[q];
+                        need |= p[q][i];
+                    }
+                if (__builtin_expect(__any(need), 0)) {
+                    const int base = (b_begin + st * CB + cb) * 16;
+#pragma unroll
+                    for (int q = 0; q < QB; q++)
+                        if (__any(p[q][0] | p[q][1] | p[q][2] | p[q][3])) {
+#pragma unroll
+                            for (int i = 0; i < 4; i++)
+                                if (p[q][i]) list_insert<L>(lk[q], li[q], -2.0f * ac[q][i], base + rel[i]);
+                            th[q] = -0.5f * lk[q][L - 1];
+                        }
+                }
+            };
+            contract(0, acc2[0]);
+#pragma unroll
+            for (int cb = 0; cb < CB; cb++) {
+                if (cb < nb) {
+                    if (cb + 1 < nb) contract(cb + 1, acc2[(cb + 1) & 1]);
+                    epilogue(cb, acc2[cb & 1]);
+                }
+            }
+        } else
 #pragma unroll
         for (int cb = 0; cb < CB; cb++) {
             const int blk = b_begin + st * CB + cb;
@@ -1406,6 +1469,7 @@ static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
             case 0: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 0>, 2); break;
             case 1: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 1>, 2); break;
             case 2: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 2>, 3); break;
+            case 5: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 5>, 2); break;
             default: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 3>, 3); break;
         }
     } else

@@ -97,6 +97,9 @@ int ann_kdtree_get_stats(ann_kdtree *akd, tiler_search_stats *out);
  * per-tile calls -- run an exhaustive exact scan spread over the whole GPU instead of the MFMA shortlist and its
  * tiers (same answers; 0 disables it, e.g. to test those tiers on small batches).  Process-wide.  0 / -1. */
 int tiler_set_scan_limits(int max_k1, int max_k8);
+/* Test hook (process-wide): on != 0 makes ANN's pruning check vouch for no result, so every query of every kd-order
+ * search takes the exact replay of annkSearch (kd_replay_kernel); answers are identical either way.  0. */
+int tiler_debug_force_replay(int on);
 /* Coalescing counters of the single-query entry points on this handle: calls, batches searched, largest batch. */
 int tiler_combine_stats(ann_kdtree *akd, int64_t *calls, int64_t *batches, int32_t *max_batch);
 /* Test / bench hook: the reference's per-call pattern timed natively (no interpreter between the calls): the first

@@ -54,8 +54,7 @@ def test_no_cpu_fallback_without_gpu():
 
 # env switches of the timing-experiment build (`make EXPERIMENTS=1`): some select kernels whose results are invalid
 EXPERIMENT_SWITCHES = ["TILER_ORBIT", "TILER_ORBIT_QB", "TILER_ORBIT_NW", "TILER_ORBIT_MODE", "TILER_ORBIT_PIPE",
-                       "TILER_ORBIT_PMODE", "TILER_SHORTLIST", "TILER_KF_MODE", "TILER_SL16_MODE", "TILER_SL16_VAR",
-                       "TILER_KM_STATS", "TILER_DL3_PROF"]
+                       "TILER_ORBIT_PMODE", "TILER_SHORTLIST", "TILER_SL16_MODE", "TILER_SL16_VAR"]
 
 
 def test_shipped_library_ignores_experiment_switches():

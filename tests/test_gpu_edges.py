@@ -147,3 +147,31 @@ def test_tier2_overflow_on_fresh_index_exact(gpu, oracle):
     assert np.array_equal(gi[s], oi)
     assert np.array_equal(ge[s].view(np.uint32), oe.view(np.uint32))
     assert (gi < 2048).all()  # the lowest-index copy
+
+
+def test_forced_replay_exact(gpu, oracle):
+    """tiler_debug_force_replay: ANN's pruning check vouches for nothing, so every kd-order query -- the coalesced
+    small-batch path (scan, merge + check, replay) and the MFMA path (verify kernel, replay) -- runs the exact
+    annkSearch replay; every answer must still equal the restated search, k = 1 and k = 8."""
+    lib = gpu.load()
+    rng = np.random.default_rng(81)
+    tiles, thm, tvm = synth.tileset(rng, 400)
+    pals = synth.palettes(rng, 4)
+    used = synth.used_one_palette(rng.integers(0, 4, 400).astype(np.int32), 4)
+    ods, *_ = oracle.build_ft_dataset(used, tiles, thm, tvm, pals)
+    q = oracle.psyv_batch(300, rgb=synth.frame_tiles(rng, 300), flags=2).astype(np.float32)
+    gen = rng.normal(0, 1, (3000, 192)).astype(np.float32)
+    gq = gen[rng.integers(0, 3000, 200)] + rng.normal(0, 0.05, (200, 192)).astype(np.float32)
+    ints = rng.integers(0, 16, (2000, 64)).astype(np.float32)
+    iq = ints[rng.integers(0, 2000, 100)]
+    assert lib.tiler_debug_force_replay(1) == 0
+    try:
+        for nq in (5, 300):  # the scan path (<= 64 queries) and the MFMA path
+            check_nn(gpu, oracle, ods, q[:nq])
+        st = check_nn(gpu, oracle, gen, gq)
+        assert st["kd_replayed"] == gq.shape[0], st
+        check_nn(gpu, oracle, ints, iq[:10], k=8)
+        st8 = check_nn(gpu, oracle, ints, iq, k=8)
+        assert st8["kd_replayed"] > 0, st8
+    finally:
+        lib.tiler_debug_force_replay(0)

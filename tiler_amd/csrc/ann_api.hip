@@ -280,15 +280,25 @@ struct CombineReq {
     bool done = false;
     std::string msg;
 };
+// One batch in flight: its own stream, pinned staging, device buffers and search scratch, so that two batches can be
+// in flight on one handle (the second one's upload and kernels overlap the first one's; only small-batch scans run
+// concurrently: they touch nothing of the index but its read-only data and the scratch swapped in for them).
+struct CombineSlot {
+    hipStream_t stream = nullptr;
+    float *h_q = nullptr;
+    int *h_res = nullptr;  // [2][cap_r / 2]: indices, then distances
+    float *d_q = nullptr;
+    int *d_res = nullptr;
+    size_t cap_q = 0, cap_r = 0;
+    SearchScratch scratch;
+    bool busy = false;
+};
 struct Combiner {
+    static constexpr int SLOTS = 2;
     std::mutex m;
     std::condition_variable cv;
     std::deque<CombineReq *> pending;
-    bool busy = false;
-    // pinned staging of the batch in flight (only the leader touches them)
-    float *h_q = nullptr;
-    int *h_idx = nullptr;  // [2][cap_r / 2]: indices, then distances
-    size_t cap_q = 0, cap_r = 0;
+    CombineSlot slot[SLOTS];
     long long batches = 0, calls = 0;  // counters (tiler_combine_stats)
     int max_batch = 0;
 };
@@ -494,8 +504,15 @@ static void handle_free(ann_kdtree *t) {
         prep_scratch_free(t->prep);
         delete t->prep;
     }
-    (void)hipHostFree(t->comb.h_q);
-    (void)hipHostFree(t->comb.h_idx);
+    for (CombineSlot &cs : t->comb.slot) {
+        if (cs.stream) (void)hipStreamSynchronize(cs.stream);
+        nn_scratch_free(cs.scratch);
+        (void)hipFree(cs.d_q);
+        (void)hipFree(cs.d_res);
+        (void)hipHostFree(cs.h_q);
+        (void)hipHostFree(cs.h_res);
+        if (cs.stream) (void)hipStreamDestroy(cs.stream);
+    }
     if (t->maps_ev) (void)hipEventDestroy(t->maps_ev);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     unplace_handle(t->dev, t->placed);
@@ -704,12 +721,12 @@ int ann_kdtree_search_batch(ann_kdtree *t, const float *q, int nq, float eps, in
 static constexpr int COMBINE_MAX = 8192;  // queries per coalesced batch
 
 // one coalesced batch: pack the queries into pinned memory, one search, unpack (the leader, outside c.m)
-static int combine_run(ann_kdtree *t, std::vector<CombineReq *> &b, int k) {
-    Combiner &c = t->comb;
+static int combine_run(ann_kdtree *t, CombineSlot &cs, std::vector<CombineReq *> &b, int k) {
     NNIndex *ix = t->ix;
     const int nq = (int)b.size(), d = ix->d;
+    const size_t nr = (size_t)nq * k;
     DevScope ds(t->dev);
-    std::lock_guard<std::mutex> lk(ix->mu);
+    std::unique_lock<std::mutex> lk(ix->mu);
     if (ix->n == 0) {
         for (CombineReq *r : b)
             for (int i = 0; i < k; i++) {
@@ -718,38 +735,44 @@ static int combine_run(ann_kdtree *t, std::vector<CombineReq *> &b, int k) {
             }
         return 0;
     }
-    if ((size_t)nq * d > c.cap_q) {
-        hipHostFree(c.h_q);
-        c.h_q = nullptr;
-        c.cap_q = 0;
-        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_q, (size_t)nq * d * sizeof(float), hipHostMallocPortable));
-        c.cap_q = (size_t)nq * d;
+    if (!cs.stream) TILER_HIP_CHECK(hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+    if ((size_t)nq * d > cs.cap_q) {
+        (void)hipHostFree(cs.h_q);
+        (void)hipFree(cs.d_q);
+        cs.h_q = nullptr;
+        cs.d_q = nullptr;
+        cs.cap_q = 0;
+        TILER_HIP_CHECK(hipHostMalloc((void **)&cs.h_q, (size_t)nq * d * sizeof(float), hipHostMallocPortable));
+        TILER_HIP_CHECK(hipMalloc((void **)&cs.d_q, (size_t)nq * d * sizeof(float)));
+        cs.cap_q = (size_t)nq * d;
     }
-    const size_t nr = (size_t)nq * k;
-    if (2 * nr > c.cap_r) {  // one pinned block: indices then distances (one copy back per batch)
-        hipHostFree(c.h_idx);
-        c.h_idx = nullptr;
-        c.cap_r = 0;
-        TILER_HIP_CHECK(hipHostMalloc((void **)&c.h_idx, 2 * nr * sizeof(int), hipHostMallocPortable));
-        c.cap_r = 2 * nr;
+    if (2 * nr > cs.cap_r) {  // indices then distances, one block: one copy back per batch
+        (void)hipHostFree(cs.h_res);
+        (void)hipFree(cs.d_res);
+        cs.h_res = nullptr;
+        cs.d_res = nullptr;
+        cs.cap_r = 0;
+        TILER_HIP_CHECK(hipHostMalloc((void **)&cs.h_res, 2 * nr * sizeof(int), hipHostMallocPortable));
+        TILER_HIP_CHECK(hipMalloc((void **)&cs.d_res, 2 * nr * sizeof(int)));
+        cs.cap_r = 2 * nr;
     }
-    for (int j = 0; j < nq; j++) memcpy(c.h_q + (size_t)j * d, b[j]->q, (size_t)d * sizeof(float));
-    if (ensure_io(t, nq, d, k)) return -1;  // d_idx holds nq * max(d, k) >= 2 * nq * k ints (d >= 2 k here)
-    int *r_idx = t->d_idx;
-    float *r_err = reinterpret_cast<float *>(t->d_idx + nr);
-    if ((size_t)nq * std::max(d, k) < 2 * nr) r_err = t->d_err;  // tiny d: the separate buffer (two copies)
-    TILER_HIP_CHECK(hipMemcpyAsync(t->d_q, c.h_q, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, t->stream));
-    if (nn_search_dev(ix, t->d_q, nq, k, r_idx, r_err, nullptr, t->stream)) return -1;
-    float *h_err = reinterpret_cast<float *>(c.h_idx + nr);
-    if (r_err == reinterpret_cast<float *>(r_idx + nr)) {
-        TILER_HIP_CHECK(hipMemcpyAsync(c.h_idx, r_idx, 2 * nr * sizeof(int), hipMemcpyDeviceToHost, t->stream));
-    } else {
-        TILER_HIP_CHECK(hipMemcpyAsync(c.h_idx, r_idx, nr * sizeof(int), hipMemcpyDeviceToHost, t->stream));
-        TILER_HIP_CHECK(hipMemcpyAsync(h_err, r_err, nr * sizeof(float), hipMemcpyDeviceToHost, t->stream));
-    }
-    TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
+    for (int j = 0; j < nq; j++) memcpy(cs.h_q + (size_t)j * d, b[j]->q, (size_t)d * sizeof(float));
+    int *r_idx = cs.d_res;
+    float *r_err = reinterpret_cast<float *>(cs.d_res + nr);
+    TILER_HIP_CHECK(hipMemcpyAsync(cs.d_q, cs.h_q, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, cs.stream));
+    const bool small = nn_search_is_small(ix, nq, k);
+    std::swap(ix->scratch, cs.scratch);  // this batch's scratch
+    const int rc = nn_search_dev(ix, cs.d_q, nq, k, r_idx, r_err, nullptr, cs.stream);
+    std::swap(ix->scratch, cs.scratch);
+    if (rc) return -1;
+    TILER_HIP_CHECK(hipMemcpyAsync(cs.h_res, cs.d_res, 2 * nr * sizeof(int), hipMemcpyDeviceToHost, cs.stream));
+    // a small-batch scan is queued: the other slot may queue its batch while this one runs; any other search keeps
+    // the index (its orbit / tier buffers) until it has finished
+    if (small) lk.unlock();
+    TILER_HIP_CHECK(hipStreamSynchronize(cs.stream));
+    const float *h_err = reinterpret_cast<const float *>(cs.h_res + nr);
     for (int j = 0; j < nq; j++) {
-        memcpy(b[j]->idx, c.h_idx + (size_t)j * k, (size_t)k * sizeof(int));
+        memcpy(b[j]->idx, cs.h_res + (size_t)j * k, (size_t)k * sizeof(int));
         memcpy(b[j]->err, h_err + (size_t)j * k, (size_t)k * sizeof(float));
     }
     return 0;
@@ -775,12 +798,16 @@ static int combined_search(ann_kdtree *t, const float *q, int k, int *idx, float
     c.pending.push_back(&me);
     c.calls++;
     while (!me.done) {
-        if (c.busy) {
+        int si = -1;
+        for (int i = 0; i < Combiner::SLOTS && si < 0; i++)
+            if (!c.slot[i].busy) si = i;
+        if (si < 0 || c.pending.empty()) {  // both slots leading, or this caller's query is in a batch already
             c.cv.wait(lk);
             continue;
         }
-        c.busy = true;  // lead: batches until this caller's own query is answered
-        while (!me.done) {
+        CombineSlot &cs = c.slot[si];
+        cs.busy = true;  // lead: batches until this caller's own query is answered or nothing is left to take
+        while (!me.done && !c.pending.empty()) {
             std::vector<CombineReq *> b;
             const int bk = c.pending.front()->k;
             for (auto it = c.pending.begin(); it != c.pending.end() && (int)b.size() < COMBINE_MAX;) {
@@ -794,7 +821,7 @@ static int combined_search(ann_kdtree *t, const float *q, int k, int *idx, float
             c.batches++;
             c.max_batch = std::max(c.max_batch, (int)b.size());
             lk.unlock();
-            const int rc = combine_run(t, b, bk);
+            const int rc = combine_run(t, cs, b, bk);
             const std::string msg = rc ? std::string(last_error()) : std::string();
             lk.lock();
             for (CombineReq *r : b) {
@@ -804,8 +831,8 @@ static int combined_search(ann_kdtree *t, const float *q, int k, int *idx, float
             }
             c.cv.notify_all();
         }
-        c.busy = false;
-        if (!c.pending.empty()) c.cv.notify_all();  // a waiting caller takes over the queue
+        cs.busy = false;
+        c.cv.notify_all();  // a waiting caller takes over the queue (or finds its answer)
     }
     if (me.rc) set_error(me.msg);
     return me.rc;
@@ -833,6 +860,11 @@ int tiler_set_scan_limits(int max_k1, int max_k8) {
         return -1;
     }
     nn_set_scan_limits(max_k1, max_k8);
+    return 0;
+}
+
+int tiler_debug_force_replay(int on) {
+    nn_set_force_replay(on);
     return 0;
 }
 

@@ -402,151 +402,12 @@ __global__ __launch_bounds__(256) void kd_pos_kernel(int n, const int *__restric
 // kd_median_big_kernel -- so the subtree's permutation, cut dimensions and cut values are ANN's.
 static constexpr int KD_SUB = 1024;
 
-#ifdef TILER_EXPERIMENTS  // round-1 subtree kernel, kept for A/B (TILER_KD_SUB_OLD)
-__global__ __launch_bounds__(256) void kd_subtree_kernel(const float *__restrict__ rows, int dd, int *__restrict__ pidx,
-                                                         const KdNodeDev *__restrict__ roots, int bs,
-                                                         int *__restrict__ cd_out, float *__restrict__ cv_out) {
-    __shared__ float key[KD_SUB];
-    __shared__ int idx[KD_SUB];
-    __shared__ float red_v[4];
-    __shared__ int red_d[4];
-    __shared__ int stk_s[64], stk_e[64];
-    __shared__ int sp, cur_s, cur_e, cur_cd;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const KdNodeDev R = roots[blockIdx.x];
-    const int S = R.s, m_all = R.e - R.s;
-    for (int i = tid; i < m_all; i += 256) idx[i] = pidx[S + i];
-    if (tid == 0) {
-        sp = 1;
-        stk_s[0] = 0;
-        stk_e[0] = m_all;
-    }
-    __syncthreads();
-    while (sp > 0) {
-        if (tid == 0) {
-            sp--;
-            cur_s = stk_s[sp];
-            cur_e = stk_e[sp];
-        }
-        __syncthreads();
-        const int s = cur_s, e = cur_e;
-        // annMaxSpread: first dimension of maximum spread (0 when every spread is 0)
-        float best = -INFINITY;
-        int bd = 0x7fffffff;
-        for (int d = tid; d < dd; d += 256) {
-            float mn = INFINITY, mx = -INFINITY;
-            for (int i = s; i < e; i++) {
-                const float v = rows[(long)idx[i] * dd + d];
-                mn = fminf(mn, v);
-                mx = fmaxf(mx, v);
-            }
-            const float spr = mx - mn;
-            if (spr > best || (spr == best && d < bd)) {
-                best = spr;
-                bd = d;
-            }
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-            const float ob = __shfl_xor(best, o, 64);
-            const int od = __shfl_xor(bd, o, 64);
-            if (ob > best || (ob == best && od < bd)) {
-                best = ob;
-                bd = od;
-            }
-        }
-        if (lane == 0) {
-            red_v[w] = best;
-            red_d[w] = bd;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            float b = red_v[0];
-            int d0 = red_d[0];
-            for (int k = 1; k < 4; k++)
-                if (red_v[k] > b || (red_v[k] == b && red_d[k] < d0)) {
-                    b = red_v[k];
-                    d0 = red_d[k];
-                }
-            cur_cd = b > 0.0f ? d0 : 0;
-        }
-        __syncthreads();
-        const int cd = cur_cd;
-        for (int i = s + tid; i < e; i += 256) key[i] = rows[(long)idx[i] * dd + cd];
-        __syncthreads();
-        if (tid == 0) {  // annMedianSplit on key[s..e) / idx[s..e)
-            float *kk = key + s;
-            int *ii = idx + s;
-            const int n = e - s, n_lo = n / 2;
-            auto sw = [&](int a, int b) {
-                const float tk = kk[a];
-                kk[a] = kk[b];
-                kk[b] = tk;
-                const int ti = ii[a];
-                ii[a] = ii[b];
-                ii[b] = ti;
-            };
-            int l = 0, r = n - 1;
-            while (l < r) {
-                int i = (r + l) / 2, k;
-                if (kk[i] > kk[r]) sw(i, r);
-                sw(l, i);
-                const float c = kk[l];
-                i = l;
-                k = r;
-                for (;;) {
-                    while (kk[++i] < c) {
-                    }
-                    while (kk[--k] > c) {
-                    }
-                    if (i < k)
-                        sw(i, k);
-                    else
-                        break;
-                }
-                sw(l, k);
-                if (k > n_lo)
-                    r = k - 1;
-                else if (k < n_lo)
-                    l = k + 1;
-                else
-                    break;
-            }
-            if (n_lo > 0) {
-                float c = kk[0];
-                int k = 0;
-                for (int i = 1; i < n_lo; i++)
-                    if (kk[i] > c) {
-                        c = kk[i];
-                        k = i;
-                    }
-                sw(n_lo - 1, k);
-            }
-            const int m = s + n_lo;
-            cd_out[S + m] = cd;
-            cv_out[S + m] = (float)(((double)(kk[n_lo - 1] + kk[n_lo])) / 2.0);
-            if (e - m > bs) {
-                stk_s[sp] = m;
-                stk_e[sp] = e;
-                sp++;
-            }
-            if (m - s > bs) {
-                stk_s[sp] = s;
-                stk_e[sp] = m;
-                sp++;
-            }
-        }
-        __syncthreads();
-    }
-    for (int i = tid; i < m_all; i += 256) pidx[S + i] = idx[i];
-}
-
-#endif
 
 // The same subtrees with the nodes of each level spread over the workgroup's 16 waves (round 2): one wave per node --
 // spreads with lanes over dimensions and a wave reduction (annMaxSpread's first maximum), the cut dimension's keys
 // gathered by the lanes, then lane 0's annMedianSplit quickselect on the LDS copy, exactly the operations of
-// kd_subtree_kernel.  Nodes of one level own disjoint ranges of key/idx and distinct output slots, so running them
-// concurrently changes nothing; kd_subtree_kernel walked them one at a time with a block barrier per node.
+// the round-1 one-node-per-workgroup kernel.  Nodes of one level own disjoint ranges of key/idx and distinct output slots, so running them
+// concurrently changes nothing; that kernel walked them one at a time with a block barrier per node.
 static constexpr int KD_SW = 16;
 __global__ __launch_bounds__(64 * KD_SW) void kd_subtree_waves_kernel(const float *__restrict__ rows, int dd,
                                                                      int *__restrict__ pidx,
@@ -562,7 +423,7 @@ __global__ __launch_bounds__(64 * KD_SW) void kd_subtree_waves_kernel(const floa
     for (int i = tid; i < m_all; i += 64 * KD_SW) idx[i] = pidx[S + i];
     if (tid == 0) {
         lvl[0][0] = make_int2(0, m_all);
-        nlvl[0] = 1;  // the root is processed even when it is a leaf (as kd_subtree_kernel; its cut is never read)
+        nlvl[0] = 1;  // the root is processed even when it is a leaf (as the round-1 kernel did; its cut is never read)
         nlvl[1] = 0;
     }
     __syncthreads();
@@ -601,7 +462,7 @@ __global__ __launch_bounds__(64 * KD_SW) void kd_subtree_waves_kernel(const floa
             for (int i = s + lane; i < e; i += 64) key[i] = rows[(long)idx[i] * dd + cd];
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the keys are in LDS before lane 0 reads them
             __builtin_amdgcn_wave_barrier();
-            if (lane == 0) {  // annMedianSplit on key[s..e) / idx[s..e), as kd_subtree_kernel
+            if (lane == 0) {  // annMedianSplit on key[s..e) / idx[s..e), as the round-1 kernel did
                 float *kk = key + s;
                 int *ii = idx + s;
                 const int n = e - s, n_lo = n / 2;
@@ -887,12 +748,6 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
                 KD_CHECK(hipGetLastError());
             }
             const int nd = (int)deferred.size();
-#ifdef TILER_EXPERIMENTS
-            if (getenv("TILER_KD_SUB_OLD"))  // A/B: one node at a time per workgroup
-                hipLaunchKernelGGL(kd_subtree_kernel, dim3(nd), dim3(256), 0, stream, d_rows, dd, t->d_pidx, dn, t->bs,
-                                   t->d_cd, t->d_cv);
-            else
-#endif
             hipLaunchKernelGGL(kd_subtree_waves_kernel, dim3(nd), dim3(64 * KD_SW), 0, stream, d_rows, dd, t->d_pidx,
                                dn, t->bs, t->d_cd, t->d_cv);
             KD_CHECK(hipGetLastError());
@@ -953,7 +808,7 @@ __global__ __launch_bounds__(256) void kd_verify_kernel(KdOrder o, KdFixArgs a) 
         const float dc = a.err[q * a.k + j];
         ok = fb < Dk || (fb <= Dk && dc == Dk);
     }
-    if (!ok) a.list[atomicAdd(a.count, 1)] = (int)q;
+    if (!ok || a.force_replay) a.list[atomicAdd(a.count, 1)] = (int)q;
 }
 
 // annkSearch replayed exactly (kd_search.cpp): depth-first, near child first, far child iff its box distance
@@ -1091,6 +946,26 @@ int kd_root_boxes(const KdTree *t, const float *d_q, int nq, float *rootbox, hip
     KTimer tm("kd_verify", stream);
     hipLaunchKernelGGL(kd_rootbox_kernel, dim3((unsigned)std::min<long>(8192, (nq + 3) / 4)), dim3(256), 0, stream,
                        t->view(), d_q, nq, rootbox, done, count);
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// the replay alone, for queries some earlier kernel already checked and listed in a.list / *a.count
+int kd_replay_listed(const KdTree *t, const KdFixArgs &a, hipStream_t stream) {
+    if (!t || a.nq <= 0) return 0;
+    if (a.k > 32) {
+        set_error("kd replay: k > 32");
+        return -1;
+    }
+    const KdOrder o = t->view();
+    KTimer tm("kd_replay", stream);
+    const dim3 grid(std::min(64, (a.nq + 63) / 64));  // grid-stride over the device-side count
+    if (a.k <= 1)
+        hipLaunchKernelGGL(kd_replay_kernel<1>, grid, dim3(64), 0, stream, o, a);
+    else if (a.k <= 8)
+        hipLaunchKernelGGL(kd_replay_kernel<8>, grid, dim3(64), 0, stream, o, a);
+    else
+        hipLaunchKernelGGL(kd_replay_kernel<32>, grid, dim3(64), 0, stream, o, a);
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }

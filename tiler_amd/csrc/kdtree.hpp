@@ -57,11 +57,14 @@ struct KdFixArgs {
     int *list = nullptr, *count = nullptr;  // [nq], [1]: queries sent to the replay (count zeroed by the caller)
     const float *rootbox = nullptr;         // [nq] annBoxDistance of every query (kd_root_boxes)
     const uint8_t *done = nullptr;          // [nq] or null: 1 = already checked (the pair pass), skip
+    int force_replay = 0;                   // test hook (tiler_debug_force_replay): vouch for nothing
 };
 // rootbox[q] = annBoxDistance(q, box) for nq fp32 rows q[nq][dd] (queries whose descriptor kernel did not fuse it)
 // annBoxDistance of every query to the root box; done[nq] / count (optional) are zeroed by the same launch
 int kd_root_boxes(const KdTree *t, const float *d_q, int nq, float *rootbox, hipStream_t stream,
                   uint8_t *done = nullptr, int *count = nullptr);
 int kd_verify_and_replay(const KdTree *t, const KdFixArgs &a, hipStream_t stream);
+// the exact replay of the queries already listed in a.list / *a.count (the small-batch merge checks them itself)
+int kd_replay_listed(const KdTree *t, const KdFixArgs &a, hipStream_t stream);
 
 }  // namespace tiler

@@ -310,34 +310,11 @@ int interframe_corr_dev(const int32_t *d_rgb, int F, int tm_w, int tm_h, double 
         }
         {
             KTimer tm("kf_corr", stream);
-#ifdef TILER_EXPERIMENTS
-            // experiment build only (make EXPERIMENTS=1): TILER_KF_MODE 0 = producer/consumer kernel, 3 = lane
-            // kernel (A/B reference); timing experiments (results invalid): 1 = lane kernel without the neighbour
-            // move, 2 = lane kernel with split chains, 4 = producer/consumer with the consumer idle, 5 = with the
-            // producers idle
-            static const int mode = getenv("TILER_KF_MODE") ? atoi(getenv("TILER_KF_MODE")) : 0;
-            const dim3 grid((F + KF_FRAMES_PER_WAVE - 1) / KF_FRAMES_PER_WAVE);
-#else
-            constexpr int mode = 0;  // the shipped library has no result-changing switches
-#endif
-            if (mode == 0) {
+            {
                 const int per = 15;  // frames per workgroup (one DPP row; see the kernel)
                 hipLaunchKernelGGL((pearson_chain_pc_kernel<0, 3, 3, 2, 1>), dim3((F + per - 1) / per), dim3(256), 0,
                                    stream, d_rgb, F, tm_w, tm_h, d_sums, d_d2, d_num);
             }
-#ifdef TILER_EXPERIMENTS
-            else if (mode >= 4) {
-                auto kern = mode == 4   ? pearson_chain_pc_kernel<4, 3, 3, 2, 1>
-                            : mode == 5 ? pearson_chain_pc_kernel<5, 3, 3, 2, 1>
-                                        : pearson_chain_pc_kernel<0, 3, 3, 2, 1>;
-                const int per = 15;  // frames per workgroup (one DPP row; see the kernel)
-                hipLaunchKernelGGL(kern, dim3((F + per - 1) / per), dim3(256), 0, stream, d_rgb, F, tm_w, tm_h, d_sums, d_d2, d_num);
-            } else {
-                auto kern = mode == 1 ? pearson_chain_kernel<8, 1> : mode == 2 ? pearson_chain_kernel<8, 2>
-                                                                   : pearson_chain_kernel<8, 0>;
-                hipLaunchKernelGGL(kern, grid, dim3(64), 0, stream, d_rgb, F, tm_w, tm_h, d_sums, d_d2, d_num);
-            }
-#endif
             if (hipGetLastError() != hipSuccess) break;
         }
         if (hipMemcpyAsync(h.data(), d_d2, (size_t)F * 16, hipMemcpyDeviceToHost, stream) != hipSuccess) break;

@@ -96,7 +96,7 @@ struct KmState {
     unsigned long long *cost;  // [1]
     int *moves;                // [1]
     int *err;                  // [1]
-    int *dbg;                  // experiment build: [8] sequential-pass counters of the bin, or nullptr
+    int *dbg;                  // [8] sequential-pass counters of the bin (study hook; null in the library)
     int4 *mvl;                 // [2 * KM_BIN] this chunk's moves in order (point, to, from, 1 = first of its group)
     int *mvn;                  // [1] their count
 };
@@ -633,7 +633,7 @@ struct KmBatch {
     unsigned *seed;               // [nb]
     unsigned long long *cost;     // [nb]
     int *moves, *err, *ffdone;    // [nb]
-    int *dbg;                     // experiment build (TILER_KM_STATS): [nb][8] counters, or nullptr
+    int *dbg;                     // [nb][24] sequential-pass counters (study hook; null in the library)
     int4 *mvl;                    // [nb][2 * KM_BIN] move lists of the decision pass
     int *mvn;                     // [nb]
 };
@@ -1346,10 +1346,6 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     B.mvl = (int4 *)(buf + o_mvl);
     B.mvn = (int *)(buf + o_mvn);
     B.dbg = nullptr;
-#ifdef TILER_EXPERIMENTS
-    static const bool km_stats = getenv("TILER_KM_STATS") != nullptr;
-    if (km_stats) TILER_HIP_CHECK(hipMalloc((void **)&B.dbg, (size_t)nb * 24 * 4));
-#endif
     int32_t *rand_rows = (int32_t *)(buf + o_rand);
     int rc = -1;
     std::vector<char> hitems;
@@ -1557,28 +1553,6 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     hipMemcpyAsync(herr.data(), B.err, nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                     hipStreamSynchronize(st) != hipSuccess)
                     goto fail;
-#ifdef TILER_EXPERIMENTS
-                if (B.dbg) {  // per iteration: summed counters, the largest bin's, the bin with most groups
-                    std::vector<int> hd((size_t)nb * 24);
-                    if (hipMemcpy(hd.data(), B.dbg, hd.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) goto fail;
-                    long tot[8] = {0};
-                    int wb = -1;
-                    for (int r : active) {
-                        for (int k = 0; k < 8; k++) tot[k] += hd[r * 24 + k];
-                        if (wb < 0 || hd[r * 24 + 0] > hd[wb * 24 + 0]) wb = r;
-                    }
-                    fprintf(stderr, "km_stats iter %d active %zu: groups %ld moves %ld single %ld rescues %ld rebuilds %ld chunks %ld | "
-                            "bin0 (n %d K %d) groups %d moves %d maxg/chunk %d | most groups: bin %d (n %d K %d) groups %d moves %d maxg/chunk %d\n",
-                            iters[active[0]], active.size(), tot[0], tot[1], tot[2], tot[3], tot[4], tot[6], nv[0], Kv[0], hd[0], hd[1], hd[5],
-                            wb, nv[wb], Kv[wb], hd[wb * 24], hd[wb * 24 + 1], hd[wb * 24 + 5]);
-                    {
-                        const unsigned long long *c0 = reinterpret_cast<const unsigned long long *>(hd.data() + 8);
-                        fprintf(stderr, "km_clock iter %d bin0 Mcycles: staging %.2f lists %.2f fetch %.2f choose %.2f apply %.2f rescue %.2f\n",
-                                iters[active[0]], c0[0] / 1e6, c0[1] / 1e6, c0[2] / 1e6, c0[3] / 1e6, c0[4] / 1e6, c0[5] / 1e6);
-                    }
-                    if (hipMemset(B.dbg, 0, (size_t)nb * 24 * 4) != hipSuccess) goto fail;
-                }
-#endif
                 std::vector<int> still;
                 for (int r : active) {
                     if (herr[r]) {

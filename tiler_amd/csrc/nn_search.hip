@@ -737,6 +737,9 @@ struct RescoreArgs {
     int32_t *m_tile, *m_pal;
     uint8_t *m_hm, *m_vm;
     const KdOrder *ko;   // tie order: ANN's kd-tree first-found (device view) or nullptr = the lowest index
+    int *kd_list, *kd_count;  // small-batch scan with a kd-tree of > bs points: the merge kernel runs ANN's pruning
+                              // check itself (kd_verify_kernel's test) and lists the queries for kd_replay_kernel
+    int force_replay;         // test hook (tiler_debug_force_replay): the check vouches for nothing
 };
 
 __device__ __forceinline__ void write_map(const RescoreArgs &a, long q, int best) {
@@ -1043,6 +1046,7 @@ __global__ __launch_bounds__(256) void nn_scan_small_kernel(RescoreArgs a, int n
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int qg = blockIdx.y * QN;  // this workgroup's group of queries
     const int nq = min(a.nq - qg, QN), d = a.d;
+    if (a.kd_count && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.kd_count = 0;  // the merge kernel appends
     for (int i = tid; i < nq * d; i += 256)
         sq[(i / d) * SCAN_D_MAX + i % d] = a.q[(long)(qg + i / d) * d + i % d];
     __syncthreads();
@@ -1184,6 +1188,27 @@ __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int ns
             if (r == 0) write_map(a, q, ok ? mi : -1);
         }
     }
+    // ANN's pruning along every result's path (kd_verify_kernel's test, one lane): vouched for, or listed for the
+    // exact replay.  Saves the root-box and verify launches of a coalesced per-tile batch.
+    if (a.kd_count && lane == 0) {
+        const KdOrder o = *a.ko;
+        const float Dk = a.out_err[(long)q * a.k + a.k - 1];
+        if (a.out_idx[(long)q * a.k] >= 0 && Dk < FLT_MAX) {
+            const float rb = kd_root_box(o, qr);
+            bool vouch = true;
+            for (int j = 0; j < a.k && vouch; j++) {
+                const int c = a.out_idx[(long)q * a.k + j];
+                if ((unsigned)c >= (unsigned)o.n) {
+                    vouch = false;
+                    break;
+                }
+                const float fb = kd_path_far_box(o, qr, o.pos[c], rb);
+                const float dc = a.out_err[(long)q * a.k + j];
+                vouch = fb < Dk || (fb <= Dk && dc == Dk);
+            }
+            if (!vouch || a.force_replay) a.kd_list[atomicAdd(a.kd_count, 1)] = q;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1281,20 +1306,7 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hip
     return ix;
 }
 
-void nn_index_destroy(NNIndex *ix) {
-    if (!ix) return;
-    orbit_destroy(ix->orbit);
-    kd_tree_destroy(ix->kd);
-    hipFree(ix->d_rows);
-    hipFree(ix->d_frag);
-    hipFree(ix->d_nc);
-    hipFree(ix->d_seed);
-    hipFree(ix->d_frag16);
-    hipFree(ix->d_seed16);
-    hipFree(ix->d_tr_tile);
-    hipFree(ix->d_tr_pal);
-    hipFree(ix->d_tr_attr);
-    SearchScratch &s = ix->scratch;
+void nn_scratch_free(SearchScratch &s) {
     hipFree(s.qfrag);
     hipFree(s.qfrag16);
     hipFree(s.qstat);
@@ -1322,6 +1334,23 @@ void nn_index_destroy(NNIndex *ix) {
     hipFree(s.fpal);
     hipFree(s.fhm);
     hipFree(s.fvm);
+    s = SearchScratch();
+}
+
+void nn_index_destroy(NNIndex *ix) {
+    if (!ix) return;
+    orbit_destroy(ix->orbit);
+    kd_tree_destroy(ix->kd);
+    hipFree(ix->d_rows);
+    hipFree(ix->d_frag);
+    hipFree(ix->d_nc);
+    hipFree(ix->d_seed);
+    hipFree(ix->d_frag16);
+    hipFree(ix->d_seed16);
+    hipFree(ix->d_tr_tile);
+    hipFree(ix->d_tr_pal);
+    hipFree(ix->d_tr_attr);
+    nn_scratch_free(ix->scratch);
     hipHostFree(ix->h_fb_count);
     if (ix->done_event) hipEventDestroy(ix->done_event);
     delete ix;
@@ -1366,10 +1395,6 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         s.cap_q = nq;
     }
     if (!s.kd_count) TILER_HIP_CHECK(hipMalloc((void **)&s.kd_count, 16));
-    if (!s.ccnt) {
-        TILER_HIP_CHECK(hipMalloc((void **)&s.ccnt, (size_t)TIER2_MAX * sizeof(int)));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.cbuf, (size_t)TIER2_MAX * TIER2_CAP * sizeof(int)));
-    }
     if ((size_t)nkeys > s.cap_keys) {
         hipFree(s.key);
         hipFree(s.idx);
@@ -1564,6 +1589,8 @@ static int tier2_slots(NNIndex *ix, int nq) {
 }
 static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream,
                        bool orbit_prepared);
+static bool scan_small_takes(const NNIndex *ix, int nq, int k);
+static std::atomic<int> g_force_replay{0};  // tiler_debug_force_replay
 
 int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
                   hipStream_t stream, bool rootbox_ready, bool orbit_prepared) {
@@ -1600,6 +1627,29 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     ix->last_flat_dev = nullptr;
     SearchScratch &s = ix->scratch;
     if (!ix->done_event) TILER_HIP_CHECK(hipEventCreateWithFlags(&ix->done_event, hipEventDisableTiming));
+    if (ix->kd && scan_small_takes(ix, nq, k)) {  // the coalesced per-tile batches: scan, merge + pruning check, replay
+        if (ensure_scratch(ix, nq, 0)) return -1;
+        const bool prune = ix->kd->n > ix->kd->bs;  // a single bucket: no pruning, position order is exact
+        ra.kd_list = prune ? s.kd_list : nullptr;
+        ra.kd_count = prune ? s.kd_count : nullptr;
+        ra.force_replay = g_force_replay.load(std::memory_order_relaxed);
+        if (search_core(ix, ra, d_q, nq, k, stream, orbit_prepared)) return -1;
+        if (prune) {
+            KdFixArgs fa{ix->d_rows, d_q, nq, k, d_idx, d_err};
+            fa.tr_tile = ra.tr_tile;
+            fa.tr_pal = ra.tr_pal;
+            fa.tr_attr = ra.tr_attr;
+            fa.m_tile = ra.m_tile;
+            fa.m_pal = ra.m_pal;
+            fa.m_hm = ra.m_hm;
+            fa.m_vm = ra.m_vm;
+            fa.list = s.kd_list;
+            fa.count = s.kd_count;
+            if (kd_replay_listed(ix->kd, fa, stream)) return -1;
+        }
+        TILER_HIP_CHECK(hipEventRecord(ix->done_event, stream));
+        return 0;
+    }
     if (ix->kd) {  // ANN's tie order: the pruning check needs every query's box distance and a clean slate
         if (ensure_scratch(ix, nq, 0)) return -1;
         if (!rootbox_ready) {  // the box distances, with the verify flags and the replay count cleared in the same launch
@@ -1634,6 +1684,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     fa.m_vm = ra.m_vm;
     fa.list = s.kd_list;
     fa.count = s.kd_count;
+    fa.force_replay = g_force_replay.load(std::memory_order_relaxed);
     if (kd_verify_and_replay(ix->kd, fa, stream)) return -1;
     TILER_HIP_CHECK(hipEventRecord(ix->done_event, stream));  // what tiler_search_stats reads is final here
     return 0;
@@ -1646,6 +1697,13 @@ static std::atomic<int> g_scan_max1{64}, g_scan_max8{16};  // tiler_set_scan_lim
 void nn_set_scan_limits(int max_k1, int max_k8) {
     g_scan_max1.store(std::max(0, max_k1));
     g_scan_max8.store(std::max(0, max_k8));
+}
+void nn_set_force_replay(int on) { g_force_replay.store(on != 0); }
+bool nn_search_is_small(const NNIndex *ix, int nq, int k) { return scan_small_takes(ix, nq, k); }
+static bool scan_small_takes(const NNIndex *ix, int nq, int k) {
+    return ix->d <= SCAN_D_MAX && ix->d % 4 == 0 &&
+           ((k == 1 && nq <= g_scan_max1.load(std::memory_order_relaxed)) ||
+            (k <= 8 && nq <= g_scan_max8.load(std::memory_order_relaxed)));
 }
 static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t stream) {
     const int nsplit = (int)std::max<long>(1, std::min<long>(1024, ((long)ix->n + 255) / 256));
@@ -1679,10 +1737,7 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
 
 static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, int k, hipStream_t stream,
                        bool orbit_prepared) {
-    if (ix->d <= SCAN_D_MAX && ix->d % 4 == 0 &&
-        ((k == 1 && nq <= g_scan_max1.load(std::memory_order_relaxed)) ||
-         (k <= 8 && nq <= g_scan_max8.load(std::memory_order_relaxed))))
-        return scan_small(ix, ra, nq, k, stream);
+    if (scan_small_takes(ix, nq, k)) return scan_small(ix, ra, nq, k, stream);
     const bool mfma = ix->S > 0 && k <= 8;
     if (!mfma) {
         ix->last_splits = 0;
@@ -1790,6 +1845,10 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     ra.ex_list = s.ex_list;
     ra.ex_count = s.fb_count + 1;
     ra.thr = s.thr;
+    if (!s.ccnt) {  // the generic tier 2's collect buffers (256 MB), on the first search that can need them
+        TILER_HIP_CHECK(hipMalloc((void **)&s.ccnt, (size_t)TIER2_MAX * sizeof(int)));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.cbuf, (size_t)TIER2_MAX * TIER2_CAP * sizeof(int)));
+    }
     ra.ccnt = s.ccnt;
     ra.cbuf = s.cbuf;
     ra.cap = TIER2_CAP;

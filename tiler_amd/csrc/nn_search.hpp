@@ -95,6 +95,11 @@ struct NNIndex {
 // ANN's kd-tree with bucket size bs for the tie order, TILER_SPLIT_INDEX_ORDER resolves ties to the lowest index
 NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hipStream_t stream);
 void nn_index_destroy(NNIndex *ix);
+// release a SearchScratch's device buffers (an index's own, or a coalescer slot's)
+void nn_scratch_free(SearchScratch &s);
+// the search nn_search_dev runs for nq queries of k: the small-batch scan (true), which touches nothing of the index
+// but its read-only data and the scratch, or the shortlist path
+bool nn_search_is_small(const NNIndex *ix, int nq, int k);
 
 struct FtMaps {
     int32_t *tile = nullptr, *pal = nullptr;
@@ -108,6 +113,8 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
 
 // batches of at most max_k1 queries (k = 1) / max_k8 (k <= 8) take the exhaustive small-batch scan; 0 disables it
 void nn_set_scan_limits(int max_k1, int max_k8);
+// test hook: every kd pruning check lists its query for the exact replay (results unchanged)
+void nn_set_force_replay(int on);
 
 // frame tiling: RGB tiles -> descriptors (fp32) -> search -> tilemap items
 int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int *d_idx,

@@ -292,10 +292,6 @@ struct Dl3Args {
     int32_t *pal;    // [P][quant_to] 0x00BBGGRR
 };
 
-#ifdef TILER_EXPERIMENTS
-// per pair: phase wall-clock ticks (100 MHz), merges, list entries, recount candidates past the L1 test and past the exact bound (experiment build only)
-__device__ unsigned long long g_dl3_prof[1024][8];
-#endif
 
 // One merge's recount list, batched: every listed entry's recount_next scan is cut into units of 64 candidates,
 // the units of the whole batch are split evenly over the waves, and each candidate that survives the bound is
@@ -428,13 +424,7 @@ __device__ void dl3_recount_list(const Dl3Tab &t, Dl3List *L, Dl3Batch *B, const
                 const int j = j0 + (u << 6);
                 const float nb = __uint_as_float(r[u].y);
                 if (u >= nu || j >= tot || dl3_cannot_l1(a.x, naf, r[u].x, nb, e3)) continue;
-#ifdef TILER_EXPERIMENTS
-                if (blockIdx.x < 1024) atomicAdd(&g_dl3_prof[blockIdx.x][6], 1ull);
-#endif
                 if (dl3_cannot(a.x, naf, r[u].x, nb, eb)) continue;
-#ifdef TILER_EXPERIMENTS
-                if (blockIdx.x < 1024) atomicAdd(&g_dl3_prof[blockIdx.x][7], 1ull);
-#endif
                 const float cur = dl3_calc_err(dl3_entry(a.x, B->v[q]), dl3_entry(r[u].x, t.V[j]));
                 if (cur <= eb) {
                     atomicMin(&B->slot[q], ((unsigned long long)__float_as_uint(cur) << 32) | (uint32_t)j);
@@ -570,16 +560,6 @@ __device__ void dl3_merge_pass(const Dl3Tab &t, Dl3List *L, int *glist, const Dl
     }
 }
 
-#ifdef TILER_EXPERIMENTS
-#define DL3_PROF(k)                                                     \
-    if (threadIdx.x == 0 && p < 1024) {                                 \
-        const unsigned long long nw = wall_clock64();                   \
-        g_dl3_prof[p][k] += nw - prof_t;                                \
-        prof_t = nw;                                                    \
-    }
-#else
-#define DL3_PROF(k)
-#endif
 
 __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
     __shared__ float sh_e[DL3_W];
@@ -612,9 +592,6 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
     for (int c = threadIdx.x >> 6; c < ((n + (1 << sh) - 1) >> sh); c += DL3_W) dl3_chunk_min(t, ch, c, n);
     __syncthreads();
     int tot = n, c1 = 0;
-#ifdef TILER_EXPERIMENTS
-    unsigned long long prof_t = wall_clock64();
-#endif
     while (tot > a.quant_to) {
         // the first entry of minimum error (quantizer.c:610-618) over the chunk minima; none below HUGE_VALF
         // keeps c1
@@ -661,18 +638,12 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
             dl3_mark(ch, tot);  // the removed entry leaves its chunk
         }
         __syncthreads();
-        DL3_PROF(0)
         {
             const Dl3Merge m = sm;
             dl3_merge_pass(t, L, glist, m, ch, a.lcap);
         }
         __syncthreads();
-        DL3_PROF(1)
-#ifdef TILER_EXPERIMENTS
-        if (threadIdx.x == 0 && p < 1024) g_dl3_prof[p][5] += L->n;
-#endif
         dl3_recount_list(t, L, B, glist, L->n, tot, ch, a.lcap, sm);
-        DL3_PROF(2)
         // refresh the marked chunks (every mark above is complete: the list run ends in a barrier)
         const int nd = ch->n;
         for (int q = threadIdx.x >> 6; q < nd; q += DL3_W) dl3_chunk_min(t, ch, ch->dirty[q], tot);
@@ -680,10 +651,6 @@ __global__ __launch_bounds__(DL3_T) void dl3_reduce_kernel(Dl3Args a) {
         for (int q = threadIdx.x; q < nd; q += DL3_T) ch->bits[ch->dirty[q] >> 5] = 0;
         if (threadIdx.x == 0) ch->n = 0;
         __syncthreads();
-        DL3_PROF(3)
-#ifdef TILER_EXPERIMENTS
-        if (threadIdx.x == 0 && p < 1024) g_dl3_prof[p][4]++;
-#endif
     }
     for (int i = threadIdx.x; i < a.quant_to; i += DL3_T)  // set_palette3 + copy_pal (calloc'd beyond tot)
         a.pal[(long)p * a.quant_to + i] = i < tot ? (int32_t)t.QN[i].x : 0;
@@ -924,31 +891,8 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
             ra.list = d_list;
             ra.lcap = std::max(1, std::min(DL3_LCAP, g_dl3_lcap.load()));
             ra.pal = d_pal;
-#ifdef TILER_EXPERIMENTS
-            static unsigned long long zero[1024][8];
-            if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dl3_prof), zero, sizeof(zero), 0, hipMemcpyHostToDevice, stream) !=
-                hipSuccess)
-                break;
-#endif
             hipLaunchKernelGGL(dl3_reduce_kernel, dim3(P), dim3(DL3_T), 0, stream, ra);
             if (hipGetLastError() != hipSuccess) break;
-#ifdef TILER_EXPERIMENTS
-            if (getenv("TILER_DL3_PROF")) {  // the largest pair's phase split
-                static unsigned long long pr[1024][8];
-                if (hipMemcpyFromSymbolAsync(pr, HIP_SYMBOL(g_dl3_prof), sizeof(pr), 0, hipMemcpyDeviceToHost, stream) !=
-                        hipSuccess ||
-                    hipStreamSynchronize(stream) != hipSuccess)
-                    break;
-                int best = 0;
-                for (int q = 0; q < std::min(P, 1024); q++)
-                    if (seg[q + 1] - seg[q] > seg[best + 1] - seg[best]) best = q;
-                fprintf(stderr, "dl3 pair %d colors %d merges %llu list/merge %.2f us: argmin+merge %.1f pass %.1f list %.1f chunks %.1f\n",
-                        best, seg[best + 1] - seg[best], pr[best][4], (double)pr[best][5] / std::max(1ull, pr[best][4]),
-                        pr[best][0] / 100.0, pr[best][1] / 100.0, pr[best][2] / 100.0, pr[best][3] / 100.0);
-                fprintf(stderr, "  recount candidates per merge: past L1 %.1f, past the exact bound %.1f\n",
-                        (double)pr[best][6] / std::max(1ull, pr[best][4]), (double)pr[best][7] / std::max(1ull, pr[best][4]));
-            }
-#endif
         }
         if (hipMemcpyAsync(pal_out, d_pal, 4 * (size_t)P * palsize, hipMemcpyDeviceToHost, stream) != hipSuccess) break;
         if (hipStreamSynchronize(stream) != hipSuccess) break;

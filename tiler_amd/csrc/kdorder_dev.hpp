@@ -130,6 +130,35 @@ __device__ __forceinline__ float kd_root_box(const KdOrder &o, const float *__re
     return dist;
 }
 
+// The same value by a whole wave (every lane returns it): lanes load and square 64 dimensions at a time, the outside
+// terms are then added in dimension order from registers -- the sequential sum without a memory round trip per term
+__device__ __forceinline__ float kd_root_box_wave(const KdOrder &o, const float *__restrict__ q, int lane) {
+    float rb = 0.0f;
+    for (int d0 = 0; d0 < o.dd; d0 += 64) {
+        const int d = d0 + lane;
+        float t = 0.0f;
+        bool outside = false;
+        if (d < o.dd) {
+            const float v = q[d], lo = o.box_lo[d], hi = o.box_hi[d];
+            if (v < lo) {
+                t = lo - v;
+                outside = true;
+            } else if (v > hi) {
+                t = v - hi;
+                outside = true;
+            }
+            t = t * t;
+        }
+        unsigned long long m = __ballot(outside);
+        while (m) {
+            const int src = __builtin_ctzll(m);
+            m &= m - 1;
+            rb = rb + __shfl(t, src, 64);
+        }
+    }
+    return rb;
+}
+
 // The largest box distance ANN computes for a far child on the root-to-leaf path of leaf position p
 // (ANNkd_split::ann_search: box_dist + (cut_diff^2 - box_diff^2), fp32).  The leaf is visited iff every one of
 // these is < the k-th key current at that check; -inf when p lies only in near children.

@@ -338,7 +338,10 @@ __device__ __forceinline__ void vm_wait() {  // s_waitcnt vmcnt(N): all but this
 }
 
 // VAR bit 0: per query block, a wave-uniform test before its 4 per-element list tests, thresholds kept in registers
-// (the same comparisons, so the same lists); bit 1: a 3-buffer LDS ring (two stages in flight instead of one)
+// (the same comparisons, so the same lists); bit 1: a 3-buffer LDS ring (two stages in flight instead of one); bit 2:
+// a software-pipelined stage; bit 3: insertions queued per lane in LDS and applied in bulk
+#define NBUF_OF(VAR) (((VAR) & 2) ? 3 : 2)
+static constexpr int SLQ_SLOTS = 6;  // queue entries per lane and query block (VAR & 8)
 template <int S, int L, int CB, int NW, int QB, bool FLAT, int MODE = 0, int VAR = 0>
 __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag, const float *__restrict__ cseed,
                                                  int nblk, const half8 *__restrict__ qfrag, int nq, int blk_per_split,
@@ -389,9 +392,10 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
         const uint4 *src = reinterpret_cast<const uint4 *>(cfrag) + (long)blk0 * S * 64 + w * 64 + lane;
         char *dst = smem + buf * BUF_BYTES + w * 1024;
         if constexpr (FLAT) {  // wave w: k-step 0 of block w (the last block again past the end: never read)
-            static_assert(CB == NW, "one k-step-0 piece per wave");
-            glds16_asm(reinterpret_cast<const uint4 *>(cfrag) + (long)(blk0 + min(w, nb - 1)) * S * 64 + lane,
-                       smem + buf * BUF_BYTES + w * S * 1024);
+            static_assert(CB <= NW, "one k-step-0 piece per wave");
+            if (CB == NW || w < CB)
+                glds16_asm(reinterpret_cast<const uint4 *>(cfrag) + (long)(blk0 + min(w, nb - 1)) * S * 64 + lane,
+                           smem + buf * BUF_BYTES + w * S * 1024);
         } else if (nb == CB) {
 #pragma unroll
             for (int j = 0; j < PER_T; j++) glds16_asm(src + j * NT, dst + j * NT * 16);
@@ -405,7 +409,7 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
                        smem + buf * BUF_BYTES + FRAG_BYTES);
     };
 
-    constexpr int NBUF = (VAR & 2) ? 3 : 2;
+    constexpr int NBUF = NBUF_OF(VAR);
     // a stage's DMA instructions per wave (the seed piece is wave 0's): the counted wait of the 3-buffer ring
     auto wait_all_but_next = [&]() {
         if (w == 0) vm_wait<(FLAT ? 1 : PER_T) + 1>();
@@ -414,6 +418,28 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
     float th[QB];  // VAR & 1: -0.5 * lk[q][L - 1] (and the window bound), kept current
 #pragma unroll
     for (int q = 0; q < QB; q++) th[q] = -INFINITY;
+    // VAR & 8: the candidates that pass a lane's threshold are queued in LDS (per lane and query block, in scan order)
+    // and inserted into its list in bulk when some lane's queue is nearly full: the SIMT cost of an insertion is paid
+    // per flush of a lane's own entries instead of per (query block, element) that ANY lane of the wave needs.  The
+    // lists are the same (the same entries inserted in the same order; the stale threshold between flushes only
+    // queues entries that the insertion then rejects).  [QB][SLQ_SLOTS][NT] entries {key bits, index} after the ring.
+    constexpr int SLQ = (VAR & 8) ? SLQ_SLOTS : 1;
+    uint2 *qbuf = reinterpret_cast<uint2 *>(smem + NBUF_OF(VAR) * BUF_BYTES);
+    int qcnt[QB];
+#pragma unroll
+    for (int q = 0; q < QB; q++) qcnt[q] = 0;
+    auto flush = [&](int q) {
+#pragma unroll
+        for (int j = 0; j < SLQ; j++)
+            if (__any(j < qcnt[q])) {
+                if (j < qcnt[q]) {
+                    const uint2 e = qbuf[(q * SLQ + j) * NT + tid];
+                    list_insert<L>(lk[q], li[q], __uint_as_float(e.x), (int)e.y);
+                }
+            }
+        qcnt[q] = 0;
+        th[q] = -0.5f * lk[q][L - 1];
+    };
     if (nstage > 0) issue(0, 0);
     if (NBUF == 3 && nstage > 1) {
         issue(1, 1);
@@ -551,7 +577,20 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
                 }
                 if (__builtin_expect(__any(need), 0)) {
                     const int base = blk * 16;
-                    if constexpr ((VAR & 1) != 0) {
+                    if constexpr ((VAR & 8) != 0) {
+#pragma unroll
+                        for (int q = 0; q < QB; q++)
+                            if (__any(m[q] > th[q])) {
+                                if (__any(qcnt[q] > SLQ - 4)) flush(q);  // room for this block's 4 elements
+#pragma unroll
+                                for (int i = 0; i < 4; i++)
+                                    if (acc[q][i] > th[q]) {
+                                        qbuf[(q * SLQ + qcnt[q]) * NT + tid] =
+                                            make_uint2(__float_as_uint(-2.0f * acc[q][i]), (unsigned)(base + rel[i]));
+                                        qcnt[q]++;
+                                    }
+                            }
+                    } else if constexpr ((VAR & 1) != 0) {
 #pragma unroll
                         for (int q = 0; q < QB; q++)
                             if (__any(m[q] > th[q]))
@@ -577,6 +616,10 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
         else
             dma_drain();
         __syncthreads();
+    }
+    if constexpr ((VAR & 8) != 0) {
+#pragma unroll
+        for (int q = 0; q < QB; q++) flush(q);
     }
     // partial lists: [q][split][g][L]
 #pragma unroll
@@ -1168,6 +1211,8 @@ __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int ns
             bi[p] = vi;
         }
     int ptr = 0;
+    int my_c = -1, first = -1;  // lane r keeps result r (the argmin is wave-uniform)
+    float my_d = FLT_MAX, Dk = FLT_MAX;
     for (int r = 0; r < a.k; r++) {
         float v = INFINITY;
         int vi = 0x7fffffff;
@@ -1181,32 +1226,37 @@ __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int ns
         int mi = vi;
         kd_argmin<64>(a.ko, qr, mv, mi);
         if (vi == mi && mi != 0x7fffffff) ptr++;
+        const bool ok = mi != 0x7fffffff;
+        if (lane == r) {
+            my_c = ok ? mi : -1;
+            my_d = ok ? mv : FLT_MAX;
+        }
+        if (r == 0) first = ok ? mi : -1;
+        Dk = ok ? mv : FLT_MAX;
         if (lane == 0) {
-            const bool ok = mi != 0x7fffffff;
             a.out_idx[(long)q * a.k + r] = ok ? mi : -1;
             a.out_err[(long)q * a.k + r] = ok ? mv : FLT_MAX;
             if (r == 0) write_map(a, q, ok ? mi : -1);
         }
     }
-    // ANN's pruning along every result's path (kd_verify_kernel's test, one lane): vouched for, or listed for the
-    // exact replay.  Saves the root-box and verify launches of a coalesced per-tile batch.
-    if (a.kd_count && lane == 0) {
+    // ANN's pruning along every result's path (kd_verify_kernel's test): vouched for, or listed for the exact replay.
+    // Saves the root-box and verify launches of a coalesced per-tile batch: the wave forms the root box distance
+    // from registers, then lane j walks result j's path.
+    if (a.kd_count) {
         const KdOrder o = *a.ko;
-        const float Dk = a.out_err[(long)q * a.k + a.k - 1];
-        if (a.out_idx[(long)q * a.k] >= 0 && Dk < FLT_MAX) {
-            const float rb = kd_root_box(o, qr);
+        if (first >= 0 && Dk < FLT_MAX) {  // uniform
+            const float rb = kd_root_box_wave(o, qr, lane);
             bool vouch = true;
-            for (int j = 0; j < a.k && vouch; j++) {
-                const int c = a.out_idx[(long)q * a.k + j];
-                if ((unsigned)c >= (unsigned)o.n) {
+            if (lane < a.k) {
+                if ((unsigned)my_c >= (unsigned)o.n) {
                     vouch = false;
-                    break;
+                } else {
+                    const float fb = kd_path_far_box(o, qr, o.pos[my_c], rb);
+                    vouch = fb < Dk || (fb <= Dk && my_d == Dk);
                 }
-                const float fb = kd_path_far_box(o, qr, o.pos[c], rb);
-                const float dc = a.out_err[(long)q * a.k + j];
-                vouch = fb < Dk || (fb <= Dk && dc == Dk);
             }
-            if (!vouch || a.force_replay) a.kd_list[atomicAdd(a.kd_count, 1)] = q;
+            const bool all = __all(vouch);
+            if (lane == 0 && (!all || a.force_replay)) a.kd_list[atomicAdd(a.kd_count, 1)] = q;
         }
     }
 }
@@ -1495,6 +1545,23 @@ static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
             case 1: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 1>, 2); break;
             case 2: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 2>, 3); break;
             case 5: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 5>, 2); break;
+            case 9: {  // 4 candidate blocks per stage: the LDS room for the insertion queues
+                const size_t buf4 = 4 * S * 1024 + 4 * 64;
+                const size_t qb = (size_t)SL16_QB * SLQ_SLOTS * SL16_NW * 64 * 8;
+                hipLaunchKernelGGL((nn_shortlist16_kernel<S, L, 4, SL16_NW, SL16_QB, 0, 9>), grid, dim3(SL16_NW * 64),
+                                   2 * buf4 + qb, stream, (const half8 *)ix->d_frag16, ix->d_seed16, ix->nblk16,
+                                   (const half8 *)ix->scratch.qfrag16, nq, bps, nsplit, ix->perm, ix->scratch.key,
+                                   ix->scratch.idx, ix->flat_cnt);
+                break;
+            }
+            case 8: {  // the same with CB = 4 and the list insertion as shipped (VAR 1): the stage size alone
+                const size_t buf4 = 4 * S * 1024 + 4 * 64;
+                hipLaunchKernelGGL((nn_shortlist16_kernel<S, L, 4, SL16_NW, SL16_QB, 0, 1>), grid, dim3(SL16_NW * 64),
+                                   2 * buf4, stream, (const half8 *)ix->d_frag16, ix->d_seed16, ix->nblk16,
+                                   (const half8 *)ix->scratch.qfrag16, nq, bps, nsplit, ix->perm, ix->scratch.key,
+                                   ix->scratch.idx, ix->flat_cnt);
+                break;
+            }
             default: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 3>, 3); break;
         }
     } else

@@ -58,7 +58,9 @@ def main():
     ap.add_argument("--no-encoder", action="store_true", help="skip the sustained 1000-frame encoder lines")
     ap.add_argument("--no-per-call", action="store_true", help="skip the per-tile ann_kdtree_search line")
     ap.add_argument("--per-call-queries", type=int, default=8192)
-    ap.add_argument("--palette-frames", type=int, default=8, help="frames of the palette-generation line")
+    ap.add_argument("--palette-frames", type=int, default=8, help="frames per keyframe of the palette lines")
+    ap.add_argument("--palette-keyframes", type=int, default=8,
+                    help="keyframes of the clip-level palette line (all pairs in one call; <= 1: skip it)")
     ap.add_argument("--clip-frames", type=int, default=1000, help="keyframe-detection clip length (C3: 1000)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI, the product); gloo only to rehearse the N>1 control flow")
@@ -458,6 +460,32 @@ def main():
             palettes_line["parity_palettes"] = len(sel)
             palettes_line["parity_mismatches_vs_cpu"] = mism
 
+    # ---- secondary: the palettes of SEVERAL keyframes in one call, as btnDitherClick runs DoQuantize over every
+    # (keyframe, palette) pair at once (main.pas:901): what a clip pays per keyframe when the pairs share the GPU ----
+    palettes_clip = None
+    if rank == 0 and world == 1 and not args.no_palettes and args.palette_keyframes > 1:
+        from tiler_amd.palette import generate_palettes
+        nk, fpk = args.palette_keyframes, args.palette_frames
+        cf, _ = synth.shot_frames(np.random.default_rng(args.seed + 13), nk * fpk, W // 8, H // 8,
+                                  shot_len=(fpk, fpk), noise=2)
+        kfs = np.arange(0, nk * fpk + 1, fpk)
+        torch.cuda.synchronize(dev)
+        lib.tiler_timing_reset()
+        lib.tiler_timing_enable(1)
+        t0 = time.perf_counter()
+        generate_palettes(cf, kfs, P)
+        tp = time.perf_counter() - t0
+        lib.tiler_timing_enable(0)
+        ph = {}
+        for name in ("kmeans", "dl3_table", "dl3_pass1", "dl3_reduce"):
+            n = ctypes.c_int(0)
+            ph[name] = round(lib.tiler_timing_get(name.encode(), ctypes.byref(n)), 2)
+        palettes_clip = {"value": round(tp / nk, 4), "unit": "s per keyframe (amortised)", "s": round(tp, 3),
+                         "keyframes": nk, "pairs": nk * P, "phases_ms": ph,
+                         "shape": f"{nk} keyframes x {fpk} frames {W}x{H}, {P} palettes x 16 each, DLv3 of all "
+                                  f"{nk * P} (keyframe, palette) pairs in one pass (k-means per keyframe)"}
+        del cf
+
     # ---- secondary: GlobalTiling K-Modes at C4 (BASELINE.json config 4; bench_globaltiling.py) ----
     gtl = None
     if rank == 0 and not args.no_globaltiling:
@@ -510,7 +538,8 @@ def main():
                        "parallelism": f"keyframes sharded, {world} GPU(s)"},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "search_stats": stats, "out_digest": out_digest,
             "secondary": {"prepare": prep, "smooth": smooth, "keyframes": keyframes, "dither": dither,
-                          "palettes": palettes_line, "globaltiling": gtl, "per_tile_calls": per_call,
+                          "palettes": palettes_line, "palettes_clip": palettes_clip, "globaltiling": gtl,
+                          "per_tile_calls": per_call,
                           "encoder_local": enc_local, "encoder_all": enc_all},
         }
         print(json.dumps(res))

@@ -94,7 +94,7 @@ def parser():
     ap.add_argument("--check-kf", type=int, default=1, help="keyframe re-checked against the restatement (-1: none)")
     ap.add_argument("--check-queries", type=int, default=1500)
     ap.add_argument("--check-items", type=int, default=1000, help="items whose k = 8 search is re-checked")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, visible cores)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host cores this process may use (benchutil)")
     ap.add_argument("--seed", type=int, default=20261017)
     return ap
 
@@ -340,7 +340,8 @@ def run(args) -> dict:
     if 0 <= ck < nkf and "kt" in kept:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle as oracle
-        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        from benchutil import host_cores
+        threads = args.cpu_threads or host_cores()["usable"]
         t0 = time.perf_counter()
         say = lambda m: print(f"[bench_encoder] check: {m} ({time.perf_counter() - t0:.1f} s)", file=sys.stderr,
                               flush=True)  # noqa: E731

@@ -42,10 +42,9 @@ def parser():
 
 
 def _cpu_threads() -> int:
-    try:
-        return max(1, min(16, len(os.sched_getaffinity(0))))
-    except AttributeError:
-        return 1
+    """The host cores this process may use (benchutil.host_cores: affinity, cgroup quota, the box's share)."""
+    from benchutil import host_cores
+    return host_cores()["usable"]
 
 
 def run(args) -> dict:
@@ -171,7 +170,7 @@ def run(args) -> dict:
                 work += bw
                 spent = time.perf_counter() - tc
         cpu = {"value": round(done_pts / spent, 1) if spent else None, "unit": "points/s (full K-Modes run per bin)",
-               "cores": workers * per_bin, "kind": "port",
+               "cores": workers * per_bin, "kind": "port", "host_cores": __import__("benchutil").host_cores(),
                "sample": f"{done_bins} smallest bins ({done_pts} points), oracle/tiler_oracle.c restatement "
                          f"(dissimilarity pinned to the reference kmodes.pas asm), {workers} bins at a time x "
                          f"{per_bin} distance threads each (the reference: TKModes(4) per bin, bins on its pool)",

@@ -52,23 +52,16 @@ def test_no_cpu_fallback_without_gpu():
     assert lib.tiler_kmodes_compute(None, 0, 80, 1, 0, 16, None, None, None, None) == -1
 
 
-# env switches of the timing-experiment build (`make EXPERIMENTS=1`): some select kernels whose results are invalid
-EXPERIMENT_SWITCHES = ["TILER_ORBIT", "TILER_ORBIT_QB", "TILER_ORBIT_NW", "TILER_ORBIT_MODE", "TILER_ORBIT_PIPE",
-                       "TILER_ORBIT_PMODE", "TILER_SHORTLIST", "TILER_SL16_MODE", "TILER_SL16_VAR"]
-
-
-def test_shipped_library_ignores_experiment_switches():
-    """The shipped libANN.so never reads an experiment switch: none of their names is in the binary (a getenv of
-    one would carry it), so setting them cannot change a result.  The only environment read left is the
-    result-neutral rescore counter TILER_ORBIT_STATS."""
+def test_shipped_library_reads_no_switches():
+    """The library reads no environment switch that could change a result: the timing-experiment variants of rounds
+    1-4 were removed in round 5 (their measurements are in DESIGN.md), so no TILER_* name but the result-neutral
+    rescore counter TILER_ORBIT_STATS is in the binary (a getenv of one would carry it)."""
     import re
     blob = open(_lib.LIB_PATH, "rb").read()
     names = set(re.findall(rb"TILER_[A-Z0-9_]+", blob))
     assert names <= {b"TILER_ORBIT_STATS"}, names
-    exp = os.path.join(os.path.dirname(_lib.LIB_PATH), "experiments", "libANN.so")
-    if os.path.exists(exp):  # the experiment build carries the switches and their kernel variants
-        eblob = open(exp, "rb").read()
-        assert all(s.encode() in eblob for s in EXPERIMENT_SWITCHES)
+    src = open(os.path.join(os.path.dirname(_lib.HEADER_PATH), "..", "tiler_amd", "csrc", "Makefile")).read()
+    assert "EXPERIMENTS" not in src
 
 
 def test_search_stats_layout_matches_header(tmp_path):

@@ -338,10 +338,10 @@ __device__ __forceinline__ void vm_wait() {  // s_waitcnt vmcnt(N): all but this
 }
 
 // VAR bit 0: per query block, a wave-uniform test before its 4 per-element list tests, thresholds kept in registers
-// (the same comparisons, so the same lists); bit 1: a 3-buffer LDS ring (two stages in flight instead of one); bit 2:
-// a software-pipelined stage; bit 3: insertions queued per lane in LDS and applied in bulk
-#define NBUF_OF(VAR) (((VAR) & 2) ? 3 : 2)
-static constexpr int SLQ_SLOTS = 6;  // queue entries per lane and query block (VAR & 8)
+// (the same comparisons, so the same lists); bit 1: a 3-buffer LDS ring (two stages in flight instead of one).
+// Measured and removed (round 5, DESIGN.md section 4, identical digests): a software-pipelined stage (block cb + 1's
+// MFMAs before block cb's epilogue, one compare per element) +1.5..3 %; 4 blocks per stage +1..3 %; 4 blocks per
+// stage with the insertions queued per lane in LDS and applied in bulk +6 % (commit c152f52 has both).
 template <int S, int L, int CB, int NW, int QB, bool FLAT, int MODE = 0, int VAR = 0>
 __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag, const float *__restrict__ cseed,
                                                  int nblk, const half8 *__restrict__ qfrag, int nq, int blk_per_split,
@@ -409,7 +409,7 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
                        smem + buf * BUF_BYTES + FRAG_BYTES);
     };
 
-    constexpr int NBUF = NBUF_OF(VAR);
+    constexpr int NBUF = (VAR & 2) ? 3 : 2;
     // a stage's DMA instructions per wave (the seed piece is wave 0's): the counted wait of the 3-buffer ring
     auto wait_all_but_next = [&]() {
         if (w == 0) vm_wait<(FLAT ? 1 : PER_T) + 1>();
@@ -418,28 +418,6 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
     float th[QB];  // VAR & 1: -0.5 * lk[q][L - 1] (and the window bound), kept current
 #pragma unroll
     for (int q = 0; q < QB; q++) th[q] = -INFINITY;
-    // VAR & 8: the candidates that pass a lane's threshold are queued in LDS (per lane and query block, in scan order)
-    // and inserted into its list in bulk when some lane's queue is nearly full: the SIMT cost of an insertion is paid
-    // per flush of a lane's own entries instead of per (query block, element) that ANY lane of the wave needs.  The
-    // lists are the same (the same entries inserted in the same order; the stale threshold between flushes only
-    // queues entries that the insertion then rejects).  [QB][SLQ_SLOTS][NT] entries {key bits, index} after the ring.
-    constexpr int SLQ = (VAR & 8) ? SLQ_SLOTS : 1;
-    uint2 *qbuf = reinterpret_cast<uint2 *>(smem + NBUF_OF(VAR) * BUF_BYTES);
-    int qcnt[QB];
-#pragma unroll
-    for (int q = 0; q < QB; q++) qcnt[q] = 0;
-    auto flush = [&](int q) {
-#pragma unroll
-        for (int j = 0; j < SLQ; j++)
-            if (__any(j < qcnt[q])) {
-                if (j < qcnt[q]) {
-                    const uint2 e = qbuf[(q * SLQ + j) * NT + tid];
-                    list_insert<L>(lk[q], li[q], __uint_as_float(e.x), (int)e.y);
-                }
-            }
-        qcnt[q] = 0;
-        th[q] = -0.5f * lk[q][L - 1];
-    };
     if (nstage > 0) issue(0, 0);
     if (NBUF == 3 && nstage > 1) {
         issue(1, 1);
@@ -458,69 +436,6 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
         half8 a0 = A[0], a1 = A[64];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (st + NBUF - 1 < nstage) issue(st + NBUF - 1, (st + NBUF - 1) % NBUF);
-        if constexpr (!FLAT && MODE == 0 && (VAR & 4) != 0) {
-            // Software-pipelined stage: block cb + 1's contraction is issued before block cb's epilogue (two
-            // accumulator sets), so the epilogue's VALU runs beside this wave's own MFMAs; every element is compared
-            // once and its mask both gates the wave-uniform branch and selects the list insertions (the same tests
-            // as VAR 1, so the same lists).
-            const int nb = min(CB, b_end - (b_begin + st * CB));  // >= 1: st < nstage
-            floatx4 acc2[2][QB];
-            auto contract = [&](int cb, floatx4(&ac)[QB]) {  // a0 / a1: block cb's first fragment pair on entry,
-#pragma unroll                                                   // block cb + 1's on exit
-                for (int s = 0; s < S; s += 2) {
-                    half8 n0, n1;
-                    const bool more = s + 2 < S || cb + 1 < CB;
-                    if (s + 2 < S) {
-                        n0 = A[(cb * S + s + 2) * 64];
-                        n1 = A[(cb * S + s + 3) * 64];
-                    } else if (cb + 1 < CB) {
-                        n0 = A[((cb + 1) * S) * 64];
-                        n1 = A[((cb + 1) * S + 1) * 64];
-                    }
-#pragma unroll
-                    for (int q = 0; q < QB; q++)
-                        ac[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bq[q][s], s == 0 ? sd[cb] : ac[q], 0, 0, 0);
-#pragma unroll
-                    for (int q = 0; q < QB; q++)
-                        ac[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bq[q][s + 1], ac[q], 0, 0, 0);
-                    if (more) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, 2 * QB, 0);
-                    if (more) {
-                        a0 = n0;
-                        a1 = n1;
-                    }
-                }
-            };
-            auto epilogue = [&](int cb, const floatx4(&ac)[QB]) {
-                bool p[QB][4], need = false;
-#pragma unroll
-                for (int q = 0; q < QB; q++)
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        p[q][i] = ac[q][i] > th[q];
-                        need |= p[q][i];
-                    }
-                if (__builtin_expect(__any(need), 0)) {
-                    const int base = (b_begin + st * CB + cb) * 16;
-#pragma unroll
-                    for (int q = 0; q < QB; q++)
-                        if (__any(p[q][0] | p[q][1] | p[q][2] | p[q][3])) {
-#pragma unroll
-                            for (int i = 0; i < 4; i++)
-                                if (p[q][i]) list_insert<L>(lk[q], li[q], -2.0f * ac[q][i], base + rel[i]);
-                            th[q] = -0.5f * lk[q][L - 1];
-                        }
-                }
-            };
-            contract(0, acc2[0]);
-#pragma unroll
-            for (int cb = 0; cb < CB; cb++) {
-                if (cb < nb) {
-                    if (cb + 1 < nb) contract(cb + 1, acc2[(cb + 1) & 1]);
-                    epilogue(cb, acc2[cb & 1]);
-                }
-            }
-        } else
 #pragma unroll
         for (int cb = 0; cb < CB; cb++) {
             const int blk = b_begin + st * CB + cb;
@@ -577,20 +492,7 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
                 }
                 if (__builtin_expect(__any(need), 0)) {
                     const int base = blk * 16;
-                    if constexpr ((VAR & 8) != 0) {
-#pragma unroll
-                        for (int q = 0; q < QB; q++)
-                            if (__any(m[q] > th[q])) {
-                                if (__any(qcnt[q] > SLQ - 4)) flush(q);  // room for this block's 4 elements
-#pragma unroll
-                                for (int i = 0; i < 4; i++)
-                                    if (acc[q][i] > th[q]) {
-                                        qbuf[(q * SLQ + qcnt[q]) * NT + tid] =
-                                            make_uint2(__float_as_uint(-2.0f * acc[q][i]), (unsigned)(base + rel[i]));
-                                        qcnt[q]++;
-                                    }
-                            }
-                    } else if constexpr ((VAR & 1) != 0) {
+                    if constexpr ((VAR & 1) != 0) {
 #pragma unroll
                         for (int q = 0; q < QB; q++)
                             if (__any(m[q] > th[q]))
@@ -616,10 +518,6 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
         else
             dma_drain();
         __syncthreads();
-    }
-    if constexpr ((VAR & 8) != 0) {
-#pragma unroll
-        for (int q = 0; q < QB; q++) flush(q);
     }
     // partial lists: [q][split][g][L]
 #pragma unroll
@@ -1458,6 +1356,10 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
     return 0;
 }
 
+// waves per workgroup of the 32x32x16 shortlist on 64-d rows (UseOne's k = 8 preselection, main.pas:3830): two query
+// blocks of 32 per wave, so 64 * NW queries per workgroup
+static constexpr int GEN_NW_S4 = 4;
+
 template <int S, int L, int CB, int NW>
 static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     const int nqblk = (nq + 31) / 32;
@@ -1472,41 +1374,10 @@ static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream
 // D=192 generic shortlist variant (A/B switch TILER_SHORTLIST, datasets without mirror orbits; C3 keyframe,
 // one box): "q16" (default): nn_shortlist16_kernel, 16x16x32 MFMA, L16 = 4 (51.6 ms); "q16l6": L16 = 6
 // (53.4 ms, fewer tier-2 queries); "w8": nn_shortlist_kernel, 32x32x16, 8 waves x 2 query blocks (63.9 ms)
-#ifdef TILER_EXPERIMENTS
-// TILER_SL16_MODE=1..3: timing modes of the 16x16x32 shortlist (shortlist16_body MODE); the search then stops after
-// the shortlist with idx = 0, err = 0 (nothing downstream may use such results)
-static int sl16_mode() {
-    static int m = [] {
-        const char *e = getenv("TILER_SL16_MODE");
-        return e ? atoi(e) : 0;
-    }();
-    return m;
-}
-#endif
 
-#ifdef TILER_EXPERIMENTS
-// TILER_SL16_VAR=1..3: variants of the 16x16x32 shortlist (shortlist16_body VAR), valid results
-static int sl16_var() {  // -1: unset (the shipped VAR)
-    static int v = [] {
-        const char *e = getenv("TILER_SL16_VAR");
-        return e ? atoi(e) : -1;
-    }();
-    return v;
-}
-#endif
 
 static int shortlist_variant() {
-#ifdef TILER_EXPERIMENTS
-    static int v = [] {
-        const char *e = getenv("TILER_SHORTLIST");
-        if (e && !strcmp(e, "w8")) return 8;
-        if (e && !strcmp(e, "q16l6")) return 166;
-        return 16;
-    }();
-    return v;
-#else
     return 16;  // the shipped library: q16 only
-#endif
 }
 
 // 16x16x32 shortlist for D = 161..192 float datasets: TILER_SHORTLIST=q16 (L16 = 4) / q16l6 (L16 = 6);
@@ -1532,40 +1403,6 @@ static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
                            ix->scratch.key, ix->scratch.idx, ix->flat_cnt);
     };
     KTimer tm("nn_shortlist", stream);
-#ifdef TILER_EXPERIMENTS
-    const int mode = sl16_mode();
-    const int var = sl16_var();
-    if (mode) {
-        if (mode == 1) go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 1>, 2);
-        else if (mode == 2) go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 2>, 2);
-        else go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 3>, 2);
-    } else if (var >= 0) {
-        switch (var) {
-            case 0: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 0>, 2); break;
-            case 1: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 1>, 2); break;
-            case 2: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 2>, 3); break;
-            case 5: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 5>, 2); break;
-            case 9: {  // 4 candidate blocks per stage: the LDS room for the insertion queues
-                const size_t buf4 = 4 * S * 1024 + 4 * 64;
-                const size_t qb = (size_t)SL16_QB * SLQ_SLOTS * SL16_NW * 64 * 8;
-                hipLaunchKernelGGL((nn_shortlist16_kernel<S, L, 4, SL16_NW, SL16_QB, 0, 9>), grid, dim3(SL16_NW * 64),
-                                   2 * buf4 + qb, stream, (const half8 *)ix->d_frag16, ix->d_seed16, ix->nblk16,
-                                   (const half8 *)ix->scratch.qfrag16, nq, bps, nsplit, ix->perm, ix->scratch.key,
-                                   ix->scratch.idx, ix->flat_cnt);
-                break;
-            }
-            case 8: {  // the same with CB = 4 and the list insertion as shipped (VAR 1): the stage size alone
-                const size_t buf4 = 4 * S * 1024 + 4 * 64;
-                hipLaunchKernelGGL((nn_shortlist16_kernel<S, L, 4, SL16_NW, SL16_QB, 0, 1>), grid, dim3(SL16_NW * 64),
-                                   2 * buf4, stream, (const half8 *)ix->d_frag16, ix->d_seed16, ix->nblk16,
-                                   (const half8 *)ix->scratch.qfrag16, nq, bps, nsplit, ix->perm, ix->scratch.key,
-                                   ix->scratch.idx, ix->flat_cnt);
-                break;
-            }
-            default: go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, 3>, 3); break;
-        }
-    } else
-#endif
     go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, SL16_VAR>, 2);
     TILER_HIP_CHECK(hipGetLastError());
     if (ix->flat_cnt) {  // flat_queries of the stats: derived from the device count when they are read
@@ -1580,7 +1417,7 @@ static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
 template <int L>
 static int dispatch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     switch (ix->S) {
-        case 4: launch_shortlist<4, L, 6, 4>(ix, nq, nsplit, bps, stream); break;
+        case 4: launch_shortlist<4, L, 6, GEN_NW_S4>(ix, nq, nsplit, bps, stream); break;
         case 8: launch_shortlist<8, L, 3, 4>(ix, nq, nsplit, bps, stream); break;
         case 12: launch_shortlist<12, L, 2, 8>(ix, nq, nsplit, bps, stream); break;
         case 16: launch_shortlist<16, L, 2, 4>(ix, nq, nsplit, bps, stream); break;
@@ -1727,12 +1564,6 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
         }
     }
     if (search_core(ix, ra, d_q, nq, k, stream, orbit_prepared)) return -1;
-#ifdef TILER_EXPERIMENTS
-    if (ix->S16 > 0 && !ix->orbit && sl16_mode()) {  // timing mode: no verify over the invalid results
-        TILER_HIP_CHECK(hipEventRecord(ix->done_event, stream));
-        return 0;
-    }
-#endif
     if (!ix->kd) {
         TILER_HIP_CHECK(hipEventRecord(ix->done_event, stream));
         return 0;
@@ -1819,7 +1650,7 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     const int lpq = v16 ? 4 : 2;
     const int nblk = v16 ? ix->nblk16 : ix->nblk;
     const int max_split = 64 / (lpq * L);
-    const int qpwg = v16 ? SL16_NW * SL16_QB * 16 : (ix->S == 12 ? 512 : 256);
+    const int qpwg = v16 ? SL16_NW * SL16_QB * 16 : (ix->S == 12 ? 512 : ix->S == 4 ? 64 * GEN_NW_S4 : 256);
     const int wgs = (nq + qpwg - 1) / qpwg;
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
     nsplit = std::min(nsplit, nblk);
@@ -1883,24 +1714,12 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
                                dim3(256), 0, stream, p16);
         }
         TILER_HIP_CHECK(hipGetLastError());
-#ifdef TILER_EXPERIMENTS
-        if (v16 == 6) {
-            if (launch_shortlist16<6, 6>(ix, nq, nsplit, bps, stream)) return -1;
-        } else
-#endif
         {
             if (launch_shortlist16<6, 4>(ix, nq, nsplit, bps, stream)) return -1;
         }
     } else if (dispatch_shortlist<8>(ix, nq, nsplit, bps, stream)) {
         return -1;
     }
-#ifdef TILER_EXPERIMENTS
-    if (v16 && sl16_mode()) {
-        TILER_HIP_CHECK(hipMemsetAsync(ra.out_idx, 0, (size_t)nq * k * sizeof(int), stream));
-        TILER_HIP_CHECK(hipMemsetAsync(ra.out_err, 0, (size_t)nq * k * sizeof(float), stream));
-        return 0;
-    }
-#endif
     ra.qstat = s.qstat;
     ra.key = s.key;
     ra.idx = s.idx;
@@ -2066,11 +1885,7 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
     }
     const bool fuse_rb = ix->kd && use_wavelets && ix->kd->dd == 192;
     if (fuse_rb && ensure_scratch(ix, Q, 0)) return -1;
-#ifdef TILER_EXPERIMENTS
-    static const bool noflat = getenv("TILER_NO_FLAT") != nullptr;  // A/B: tiles in their own order
-#else
     constexpr bool noflat = false;
-#endif
     // flat grouping on the generic path (datasets without mirror orbits: real PrepareFrameTiling candidate sets):
     // the 16x16x32 shortlist's flat workgroups contract k-step 0 only (dc_first_dim)
     const bool flat_generic = !ix->orbit && use_wavelets && ix->S16 > 0 && shortlist16_L() > 0 && Q >= 8192;

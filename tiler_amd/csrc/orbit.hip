@@ -1713,7 +1713,7 @@ struct FtQueryArgs {
     OrbitStat *qstat;    // [n]
     const float *box;    // [2][192] or null
     float *rootbox;      // [n] when box
-    int xmode;           // timing experiments only (TILER_EXPERIMENTS build, TILER_FTQ_MODE): results invalid
+    int xmode;           // 0 (timing-experiment modes of round 2 lived here; results invalid when != 0)
     const int *perm;     // query i reads tile perm[i] (null: tile i)
 };
 
@@ -1975,12 +1975,6 @@ int orbit_ft_queries(NNIndex *ix, const int32_t *d_rgb, int Q, int gamma, float 
     fa.rootbox = rootbox;
     fa.xmode = 0;
     fa.perm = perm;
-#ifdef TILER_EXPERIMENTS
-    {
-        const char *e = getenv("TILER_FTQ_MODE");  // 1 no Haar, 2 no transform, 3 no norms, 5 no frag stores (timing only)
-        fa.xmode = e ? atoi(e) : 0;
-    }
-#endif
     const dim3 grid((unsigned)((Q + 63) / 64));
     KTimer tm("psyv", stream);
     // output stores non-temporal (template 1; r03g: plain 0.426 ms, nt 0.396-0.399, sc1 0.414 at C3)
@@ -2025,20 +2019,8 @@ void orbit_destroy(OrbitIndex *o) {
     delete o;
 }
 
-static int orbit_enabled() {
-#ifdef TILER_EXPERIMENTS
-    static int v = [] {
-        const char *e = getenv("TILER_ORBIT");  // 0: generic kernels only (A/B reference)
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return v;
-#else
-    return 1;
-#endif
-}
-
 int orbit_build(NNIndex *ix, hipStream_t stream) {
-    if (!orbit_enabled() || ix->d != OD || ix->S == 0 || ix->exact_int || ix->n < 2) return 1;
+    if (ix->d != OD || ix->S == 0 || ix->exact_int || ix->n < 2) return 1;
     static OrbitMap hmap;
     static int map_ok = -1;
     if (map_ok < 0) map_ok = build_map(hmap) ? 1 : 0;
@@ -2216,35 +2198,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
                  bool queries_prepared) {
     OrbitIndex *o = ix->orbit;
     const int nqblk = (nq + 31) / 32;
-#ifdef TILER_EXPERIMENTS
-    // experiment build only (make EXPERIMENTS=1): shortlist variants and timing modes (MODE / PMODE: results invalid)
-    static const int qb = [] {
-        const char *e = getenv("TILER_ORBIT_QB");  // query blocks of 32 per wave: 2 (default) or 1
-        return (e && e[0] == '1') ? 1 : 2;
-    }();
-    static const int nw = [] {
-        const char *e = getenv("TILER_ORBIT_NW");  // 12 waves x 1 query block (3 waves/SIMD)
-        return (e && atoi(e) == 12) ? 12 : ORB_NW;
-    }();
-    static const int mode = [] {
-        const char *e = getenv("TILER_ORBIT_MODE");  // 2, 3: timing experiments (results invalid)
-        return e ? atoi(e) : 0;
-    }();
-    static const int pipe = [] {
-        const char *e = getenv("TILER_ORBIT_PIPE");  // 0: the block-serial shortlist kernel
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    static const int pmode = [] {
-        const char *e = getenv("TILER_ORBIT_PMODE");  // 1 no list updates, 2 MFMA + loads only (results invalid)
-        return e ? atoi(e) : 0;
-    }();
-    static const bool nomix = getenv("TILER_NO_MIX") != nullptr;  // A/B: uniform candidate splits only
-#else
-    constexpr int qb = 2, nw = ORB_NW, mode = 0, pipe = 1, pmode = 0;
-    constexpr bool nomix = false;
-#endif
-    const bool use_pipe = pipe && qb == 2 && mode == 0 && nw == ORB_NW;
-    const int qpw = pmode == 8 ? 16 : pmode == 9 ? 12 : nw * qb;  // query blocks per workgroup
+    const int qpw = ORB_NW * 2;  // query blocks per workgroup (two per wave)
     const int wgs = (nqblk + qpw - 1) / qpw;
     const int max_split = 32 / (2 * ORB_L);  // rescore: one list entry per lane of a half-wave
     // One 8-wave workgroup fills a CU (2 waves per SIMD), so a launch runs in rounds of n_cu workgroups of
@@ -2273,7 +2227,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     // (C2: 3 rounds of 576 -> 2 x 576 + 2 x 235 block-times).  Lists keep the mix_ns stride for every query;
     // the whole-candidate part's other splits are empty entries.
     int mix_full = 0;
-    if (use_pipe && pmode == 0 && !nomix) {
+    {
         const int R = wgs / n_cu, rem = wgs - R * n_cu;
         for (int ns = 2; R >= 1 && rem > 0 && ns <= max_split && ns <= o->gblk; ns++) {
             const double t = R * (o->gblk + ORB_WG_FIXED) +
@@ -2290,7 +2244,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     // (d_1..d_3 are +-0 for them: the same bounds bit for bit).  The count stays on the device: the kernel derives its
     // first all-flat workgroup from it, with any candidate split (the mixed launch is not used then).
     const int qpw_q = qpw * 32;  // queries per workgroup
-    const int *flat_cnt = (use_pipe && pmode == 0) ? tail.flat_cnt : nullptr;
+    const int *flat_cnt = tail.flat_cnt;
     if (flat_cnt) mix_full = 0;
     const int bps = (o->gblk + nsplit - 1) / nsplit;
     nsplit = (o->gblk + bps - 1) / bps;
@@ -2322,59 +2276,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
                        dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
                        (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id, o->red_end, o->d_bmask,                \
                        0x7fffffff, o->d_bmask0, MD == 0 ? flat_cnt : nullptr)
-#ifdef TILER_EXPERIMENTS
-#define ORB_LAUNCH(NWV, QB, MD)                                                                                   \
-    hipLaunchKernelGGL((nn_orbit_shortlist_kernel<ORB_L, ORB_CB, NWV, QB, MD>), dim3(wgs, nsplit),                  \
-                       dim3(NWV * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
-                       (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id)
-        if (use_pipe && pmode == 1)
-            ORB_PIPE(1);
-        else if (use_pipe && pmode == 2)
-            ORB_PIPE(2);
-        else if (use_pipe && pmode == 3)  // 3 setprio 1 for waves NW/2.., 4 MFMA/VALU interleave groups, 5 both (valid)
-            ORB_PIPE(3);
-        else if (use_pipe && pmode == 4)
-            ORB_PIPE(4);
-        else if (use_pipe && pmode == 5)
-            ORB_PIPE(5);
-        else if (use_pipe && pmode == 11)  // timing: MFMA + loads + independent VALU adds (results invalid)
-            ORB_PIPE(11);
-        else if (use_pipe && pmode == 12)  // timing: MFMA + loads only, every chain live (results invalid)
-            ORB_PIPE(12);
-        else if (use_pipe && pmode == 13)  // |d_2| adds spread over k-steps 9..11 (valid)
-            ORB_PIPE(13);
-        else if (use_pipe && pmode == 14)  // timing: as 12 without the A-fragment LDS reads (results invalid)
-            ORB_PIPE(14);
-        else if (use_pipe && pmode == 15)  // timing: as 1 (bound, no list updates) without the A-fragment LDS reads (invalid)
-            ORB_PIPE(15);
-        else if (use_pipe && pmode == 8)  // one wave per SIMD: 4 waves x 4 query blocks (9: x 3)
-            hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 4, 0>), dim3(wgs, nsplit), dim3(256), lds,
-                               stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
-                               nsplit, o->key, o->id, o->red_end, o->d_bmask, 0x7fffffff, o->d_bmask0, nullptr);
-        else if (use_pipe && pmode == 9)
-            hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, 4, 3, 0>), dim3(wgs, nsplit), dim3(256), lds,
-                               stream, (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, nq, bps,
-                               nsplit, o->key, o->id, o->red_end, o->d_bmask, 0x7fffffff, o->d_bmask0, nullptr);
-        else if (use_pipe && !mix_full)
-            ORB_PIPE(0);
-        else if (use_pipe)
-            ;  // mixed: below
-        else if (qb == 1 && nw == 12)
-            ORB_LAUNCH(12, 1, 0);
-        else if (qb == 1)
-            ORB_LAUNCH(8, 1, 0);
-        else if (mode == 2)
-            ORB_LAUNCH(8, 2, 2);
-        else if (mode == 3)
-            ORB_LAUNCH(8, 2, 3);
-        else
-            ORB_LAUNCH(8, 2, 0);
-#undef ORB_LAUNCH
-#else
-        (void)use_pipe;
-        (void)pmode;
         if (!mix_full) ORB_PIPE(0);
-#endif
         if (mix_full) {
             const int qb_off = mix_full * ORB_NW * 2, q_off = qb_off * 32;  // query blocks / queries of part A
             const size_t per_q = (size_t)nsplit * 2 * ORB_L;

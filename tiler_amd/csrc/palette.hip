@@ -845,42 +845,44 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     t.V = (uint4 *)take(4 * b_keys);
     int *d_list = (int *)k0;  // the sort buffers are free once the table exists
     int32_t *d_pal = (int32_t *)take(4 * (size_t)P * palsize);
-    int rc = -1;
+    int rc = -1, step = 0;  // step: the failing call (error message)
     std::vector<int> seg(P + 1);
     do {
-        if (hipMemsetAsync(d_uc, 0, 4 * (P + 2), stream) != hipSuccess) break;
-        if (hipMemsetAsync(d_nruns, 0, 4, stream) != hipSuccess) break;
+        if (hipMemsetAsync(d_uc, 0, 4 * (P + 2), stream) != hipSuccess) { step = 1; break; }
+        if (hipMemsetAsync(d_nruns, 0, 4, stream) != hipSuccess) { step = 2; break; }
         if (npix > 0) {
             KTimer tk("dl3_table", stream);
             hipLaunchKernelGGL(dl3_keys_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, d_rgb, d_pal_of,
                                d_active, n_tiles, P, bpc, k0, v0, d_uc);
-            if (hipGetLastError() != hipSuccess) break;
+            if (hipGetLastError() != hipSuccess) { step = 3; break; }
             hipcub::DoubleBuffer<uint32_t> kb(k0, k1), vb(v0, v1);
             size_t ts = tmp_sort;
-            if (hipcub::DeviceRadixSort::SortPairs(tmp, ts, kb, vb, npix, 0, end_bit, stream) != hipSuccess) break;
+            if (hipcub::DeviceRadixSort::SortPairs(tmp, ts, kb, vb, npix, 0, end_bit, stream) != hipSuccess) { step = 4; break; }
             hipcub::TransformInputIterator<Dl3Sum, Dl3Expand, const uint32_t *> vin(vb.Current(), Dl3Expand());
             size_t tr = tmp_red;
             if (hipcub::DeviceReduce::ReduceByKey(tmp, tr, (const uint32_t *)kb.Current(), ukeys, vin, agg, d_nruns,
-                                                  Dl3SumOp(), npix, stream) != hipSuccess)
+                                                  Dl3SumOp(), npix, stream) != hipSuccess) {
+                step = 14;
                 break;
+            }
         }
         hipLaunchKernelGGL(dl3_seg_kernel, dim3((P + 256) / 256), dim3(256), 0, stream, ukeys, d_nruns, P, bpc, d_seg);
-        if (hipGetLastError() != hipSuccess) break;
-        if (hipMemcpyAsync(seg.data(), d_seg, 4 * (P + 1), hipMemcpyDeviceToHost, stream) != hipSuccess) break;
-        if (hipMemcpyAsync(use_count, d_uc, 4 * P, hipMemcpyDeviceToHost, stream) != hipSuccess) break;
-        if (hipStreamSynchronize(stream) != hipSuccess) break;
+        if (hipGetLastError() != hipSuccess) { step = 5; break; }
+        if (hipMemcpyAsync(seg.data(), d_seg, 4 * (P + 1), hipMemcpyDeviceToHost, stream) != hipSuccess) { step = 6; break; }
+        if (hipMemcpyAsync(use_count, d_uc, 4 * P, hipMemcpyDeviceToHost, stream) != hipSuccess) { step = 7; break; }
+        if (hipStreamSynchronize(stream) != hipSuccess) { step = 8; break; }
         const int total = seg[P];
         if (total > 0) {
             hipLaunchKernelGGL(dl3_init_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, agg, d_seg, P,
                                t);
-            if (hipGetLastError() != hipSuccess) break;
+            if (hipGetLastError() != hipSuccess) { step = 9; break; }
         }
         {
             KTimer tp("dl3_pass1", stream);
             if (total > 0)
                 hipLaunchKernelGGL(dl3_pass1_kernel, dim3((unsigned)std::min(65536, (total + 3) / 4)), dim3(256), 0, stream,
                                    ukeys, d_seg, P, bpc, t);
-            if (hipGetLastError() != hipSuccess) break;
+            if (hipGetLastError() != hipSuccess) { step = 10; break; }
         }
         {
             KTimer tr("dl3_reduce", stream);
@@ -892,17 +894,21 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
             ra.lcap = std::max(1, std::min(DL3_LCAP, g_dl3_lcap.load()));
             ra.pal = d_pal;
             hipLaunchKernelGGL(dl3_reduce_kernel, dim3(P), dim3(DL3_T), 0, stream, ra);
-            if (hipGetLastError() != hipSuccess) break;
+            if (hipGetLastError() != hipSuccess) { step = 11; break; }
         }
-        if (hipMemcpyAsync(pal_out, d_pal, 4 * (size_t)P * palsize, hipMemcpyDeviceToHost, stream) != hipSuccess) break;
-        if (hipStreamSynchronize(stream) != hipSuccess) break;
+        if (hipMemcpyAsync(pal_out, d_pal, 4 * (size_t)P * palsize, hipMemcpyDeviceToHost, stream) != hipSuccess) { step = 12; break; }
+        if (hipStreamSynchronize(stream) != hipSuccess) { step = 13; break; }
         for (int p = 0; p < P; p++) {
             if (hist) hist[p] = seg[p + 1] - seg[p];
             sort_palette_cmulhs(pal_out + (size_t)p * palsize, palsize);  // CMPal.Sort (main.pas:2413)
         }
         rc = 0;
     } while (0);
-    if (rc) set_error("quantize_palettes: HIP failure");
+    if (rc) {
+        const hipError_t e = hipGetLastError();
+        set_error("quantize_palettes: HIP failure at step " + std::to_string(step) + " (" + hipGetErrorString(e) +
+                  "), " + std::to_string(npix) + " pixels, " + std::to_string(P) + " pairs");
+    }
     (void)hipFree(ws);
     return rc;
 }

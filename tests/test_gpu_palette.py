@@ -39,6 +39,15 @@ def test_quantize_two_keyframes(gpu, oracle):
     assert h.max() > 1000  # textured tiles: the O(n^2) passes are exercised
 
 
+def test_quantize_many_pairs(gpu, oracle):
+    """1024 (keyframe, palette) pairs in one call, the clip-level form: the per-pair arrays of the workspace
+    (use counts, segments, run count) are sized for every pair (an undersized carve once put the palette
+    output past the end of the allocation at P >= 1024)."""
+    rgb, pal_of, pairs = _case(11, (2, 2), 2048, 512)
+    h = _check(oracle, rgb, pal_of, pairs)
+    assert pairs == 1024 and (h > 0).sum() > 1000
+
+
 @pytest.mark.parametrize("bpc", [4, 5, 6, 8])
 def test_quantize_bpc(gpu, oracle, bpc):
     rgb, pal_of, pairs = _case(2 + bpc, (2,), 100, 4)

@@ -821,8 +821,12 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
                                                       stream));
     const size_t np = (size_t)std::max(npix, 1);
     const size_t b_keys = 4 * np, b_sum = sizeof(Dl3Sum) * np, b_tmp = std::max(tmp_sort, tmp_red) + 256;
-    const size_t bytes = 4 * b_keys /* keys, vals x2 */ + b_keys /* ukeys */ + b_sum + b_tmp + 4 * (P + 2) * 2 +
-                         8 * b_keys + 16384 /* table (the list reuses a sort buffer) */ + 4 * (size_t)P * palsize + 4096;
+    const size_t b_pairs = 4 * ((size_t)P + 2), b_table = 2 * b_keys + 8 * 1024;  // + slack for unclamped loads
+    // The workspace is the sum of the carved pieces, each rounded up to 256 bytes (the same rounding as take()).
+    const size_t sizes[] = {b_keys, b_keys, b_keys, b_keys, b_keys, b_sum, b_tmp, b_pairs, b_pairs, b_pairs,
+                            b_table, b_table, 4 * b_keys, 4 * (size_t)P * palsize};
+    size_t bytes = 0;
+    for (size_t b : sizes) bytes += (b + 255) & ~(size_t)255;
     char *ws = nullptr;
     TILER_HIP_CHECK(hipMalloc((void **)&ws, bytes));
     char *cur = ws;
@@ -836,15 +840,20 @@ int quantize_palettes_dev(long n_tiles, const int32_t *d_rgb, const int32_t *d_p
     uint32_t *ukeys = (uint32_t *)take(b_keys);
     Dl3Sum *agg = (Dl3Sum *)take(b_sum);
     void *tmp = take(b_tmp);
-    int *d_nruns = (int *)take(4 * (P + 2));
-    int *d_seg = (int *)take(4 * (P + 2));
-    int *d_uc = (int *)take(4 * (P + 2));
+    int *d_nruns = (int *)take(b_pairs);
+    int *d_seg = (int *)take(b_pairs);
+    int *d_uc = (int *)take(b_pairs);
     Dl3Tab t;
-    t.QN = (uint2 *)take(2 * b_keys + 8 * 1024);  // + slack for the scans' unclamped loads
-    t.EC = (uint2 *)take(2 * b_keys + 8 * 1024);  // + slack for the pass's unclamped loads
+    t.QN = (uint2 *)take(b_table);  // scans
+    t.EC = (uint2 *)take(b_table);  // pass 1
     t.V = (uint4 *)take(4 * b_keys);
     int *d_list = (int *)k0;  // the sort buffers are free once the table exists
     int32_t *d_pal = (int32_t *)take(4 * (size_t)P * palsize);
+    if ((size_t)(cur - ws) != bytes) {
+        hipFree(ws);
+        set_error("quantize_palettes: workspace layout mismatch");
+        return -1;
+    }
     int rc = -1, step = 0;  // step: the failing call (error message)
     std::vector<int> seg(P + 1);
     do {

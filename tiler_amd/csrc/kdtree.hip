@@ -26,7 +26,7 @@
 
 namespace tiler {
 
-static constexpr int KD_CH = 512;  // points per spread chunk of a big node
+static constexpr int KD_CH = 128;  // points per spread chunk (one wave) of a big node
 
 struct KdChunk {
     int node, s, e;  // big-node index, positions [s, e)
@@ -102,21 +102,40 @@ __global__ __launch_bounds__(256) void kd_spread_big_kernel(const float *__restr
                                                             const int *__restrict__ pidx,
                                                             const KdChunk *__restrict__ ch, int nch,
                                                             unsigned *__restrict__ omin, unsigned *__restrict__ omax) {
-    const int lane = threadIdx.x & 63;
-    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= nch) return;
-    const KdChunk k = ch[c];
+    // one wave per chunk; the waves of a workgroup that share a node fold their minima / maxima in LDS first, so each
+    // node dimension takes one pair of atomics per workgroup run of its chunks, not one per chunk
+    __shared__ float smn[4][256], smx[4][256];
+    __shared__ int snode[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 4 + w;
+    const bool valid = c < nch;
+    const KdChunk k = valid ? ch[c] : KdChunk{-1, 0, 0};
+    if (lane == 0) snode[w] = k.node;
     for (int d0 = 0; d0 < dd; d0 += 256) {
         float mn[4], mx[4];
-        kd_minmax(rows, dd, pidx, k.s, k.e, d0, mn, mx);
+        kd_minmax(rows, dd, pidx, k.s, k.e, d0, mn, mx);  // an invalid wave's empty range: +inf / -inf
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const int d = d0 + j * 64 + lane;
-            if (d < dd) {
-                atomicMin(&omin[(long)k.node * dd + d], f2o(mn[j]));
-                atomicMax(&omax[(long)k.node * dd + d], f2o(mx[j]));
+            smn[w][j * 64 + lane] = mn[j];
+            smx[w][j * 64 + lane] = mx[j];
+        }
+        __syncthreads();
+        if (valid && (w == 0 || snode[w - 1] != k.node)) {  // the first wave of its node's run in this workgroup
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int d = d0 + j * 64 + lane;
+                float a = smn[w][j * 64 + lane], b = smx[w][j * 64 + lane];
+                for (int u = w + 1; u < 4 && snode[u] == k.node; u++) {
+                    a = fminf(a, smn[u][j * 64 + lane]);
+                    b = fmaxf(b, smx[u][j * 64 + lane]);
+                }
+                if (d < dd) {
+                    atomicMin(&omin[(long)k.node * dd + d], f2o(a));
+                    atomicMax(&omax[(long)k.node * dd + d], f2o(b));
+                }
             }
         }
+        __syncthreads();
     }
 }
 
@@ -209,7 +228,8 @@ __global__ __launch_bounds__(256) void kd_small_kernel(const float *__restrict__
 // number of right stoppers above L_j is >= j, which each lane decides from the ranks alone.  Per iteration: each wave
 // ranks a contiguous segment by ballots (two passes), writes the stoppers' positions by rank, the J-1 swaps run in
 // parallel (their positions are distinct), then swap(l, k).  Same comparisons, same permutation, same cut value.
-static constexpr int KD_MW = 16;  // waves per big-node workgroup
+static constexpr int KD_MW = 16;    // waves per big-node workgroup
+static constexpr int KD_TAIL = 2048;  // a range this short finishes in LDS by one wave (kd_qselect_wave)
 __device__ __forceinline__ void kd_swap(float *kk, int *ii, int a, int b) {
     const float tk = kk[a];
     kk[a] = kk[b];
@@ -217,6 +237,62 @@ __device__ __forceinline__ void kd_swap(float *kk, int *ii, int a, int b) {
     const int ti = ii[a];
     ii[a] = ii[b];
     ii[b] = ti;
+}
+
+__device__ __forceinline__ void kd_wsync() {  // a wave's LDS writes visible to its other lanes
+    __builtin_amdgcn_s_waitcnt(0xc07f);         // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// annMedianSplit's loop from the state (l, r) with n_lo in [l, r] (the loop's invariant), by one wave
+__device__ __forceinline__ void kd_qselect_wave(float *kk, int *ii, int l, int r, int n_lo, int *Lp, int *Rp) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    while (l < r) {  // l, r, k: wave-uniform
+        if (lane == 0) {
+            const int i = (r + l) / 2;
+            if (kk[i] > kk[r]) kd_swap(kk, ii, i, r);
+            kd_swap(kk, ii, l, i);
+        }
+        kd_wsync();
+        const float c = kk[l];
+        int tot_r = 0;
+        for (int p0 = l; p0 <= r; p0 += 64) {
+            const int p = p0 + lane;
+            const float v = p <= r ? kk[p] : 0.0f;
+            tot_r += __popcll(__ballot(p < r && !(v > c)));
+        }
+        int bl = 0, br = 0, np = 0;
+        for (int p0 = l; p0 <= r; p0 += 64) {
+            const int p = p0 + lane;
+            const float v = p <= r ? kk[p] : 0.0f;
+            // stoppers where the scans' loop tests fail (NaN keys stop both scans, as the sequential comparisons do)
+            const bool isl = p <= r && p > l && !(v < c), isr = p < r && !(v > c);
+            const unsigned long long bL = __ballot(isl), bR = __ballot(isr);
+            const int jl = bl + __popcll(bL & below) + 1;  // rank from the left (1-based)
+            const int rb = br + __popcll(bR & below);      // right stoppers below p
+            if (isl) Lp[jl - 1] = p;
+            if (isr) Rp[tot_r - rb - 1] = p;
+            if (isl && tot_r - rb - (isr ? 1 : 0) >= jl) np++;  // R_jl > p: pair jl is swapped
+            bl += __popcll(bL);
+            br += __popcll(bR);
+        }
+        for (int o = 32; o > 0; o >>= 1) np += __shfl_xor(np, o, 64);
+        kd_wsync();
+        for (int j = lane; j < np; j += 64) kd_swap(kk, ii, Lp[j], Rp[j]);
+        kd_wsync();
+        int k = Rp[np];
+        if (np > 0) k = max(k, Lp[np - 1]);
+        if (lane == 0) kd_swap(kk, ii, l, k);
+        kd_wsync();
+        if (k > n_lo)
+            r = k - 1;
+        else if (k < n_lo)
+            l = k + 1;
+        else
+            break;
+    }
 }
 
 __global__ __launch_bounds__(64 * KD_MW) void kd_median_big_kernel(float *__restrict__ keys, int *__restrict__ pidx,
@@ -228,6 +304,8 @@ __global__ __launch_bounds__(64 * KD_MW) void kd_median_big_kernel(float *__rest
     __shared__ float s_c;
     __shared__ int wl[KD_MW], wr[KD_MW], wp[KD_MW];
     __shared__ float wv[KD_MW];
+    __shared__ float t_k[KD_TAIL];
+    __shared__ int t_i[KD_TAIL], t_l[KD_TAIL], t_r[KD_TAIL];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const KdNodeDev N = nodes[blockIdx.x];
     float *kk = keys + N.s;
@@ -242,6 +320,21 @@ __global__ __launch_bounds__(64 * KD_MW) void kd_median_big_kernel(float *__rest
     for (;;) {
         const int l = s_l, r = s_r;  // uniform: read after the barrier
         if (l >= r) break;
+        if (r - l < KD_TAIL) {  // the rest of the loop on an LDS copy of [l, r] by one wave (no global round trips)
+            for (int p = l + tid; p <= r; p += 64 * KD_MW) {
+                t_k[p - l] = kk[p];
+                t_i[p - l] = ii[p];
+            }
+            __syncthreads();
+            if (w == 0) kd_qselect_wave(t_k, t_i, 0, r - l, n_lo - l, t_l, t_r);
+            __syncthreads();
+            for (int p = l + tid; p <= r; p += 64 * KD_MW) {
+                kk[p] = t_k[p - l];
+                ii[p] = t_i[p - l];
+            }
+            __syncthreads();
+            break;
+        }
         if (tid == 0) {
             const int i = (r + l) / 2;
             if (kk[i] > kk[r]) kd_swap(kk, ii, i, r);
@@ -396,27 +489,102 @@ __global__ __launch_bounds__(256) void kd_pos_kernel(int n, const int *__restric
     if (i < n) pos[pidx ? pidx[i] : i] = i;  // pidx null: the identity (SkeletonTree's pidx[i] = i)
 }
 
-// A whole subtree of <= KD_SUB points per workgroup, entirely on the device: for every node (explicit stack) the
-// annSpread / annMaxSpread cut dimension (threads over dimensions, rows read coalesced), the node's keys into LDS
-// and annMedianSplit's quickselect by one thread on the LDS copy -- the same comparisons, swaps and cut value as
-// kd_median_big_kernel -- so the subtree's permutation, cut dimensions and cut values are ANN's.
+// A whole subtree of <= KD_SUB points per workgroup, entirely on the device: every node's annSpread / annMaxSpread
+// cut dimension, its keys into LDS and annMedianSplit's quickselect on the LDS copy -- the same comparisons, swaps and
+// cut value as kd_median_big_kernel -- so the subtree's permutation, cut dimensions and cut values are ANN's.  Nodes of
+// one level own disjoint ranges of key / idx and distinct output slots, so they run concurrently.
+//   * a level of >= KD_SW nodes: one wave per node (lanes over dimensions, a wave reduction for the first maximum);
+//   * a level of fewer nodes (the subtree's top levels, where one wave per node left most of the workgroup idle):
+//     KD_SW / nn waves per node, each folding every (KD_SW / nn)-th point into per-wave minima / maxima in LDS;
+//   * the quickselect by the node's wave: Hoare's partition ranked by ballots (kd_median_big_kernel's scheme at wave
+//     scale) instead of one lane walking the keys.
 static constexpr int KD_SUB = 1024;
-
-
-// The same subtrees with the nodes of each level spread over the workgroup's 16 waves (round 2): one wave per node --
-// spreads with lanes over dimensions and a wave reduction (annMaxSpread's first maximum), the cut dimension's keys
-// gathered by the lanes, then lane 0's annMedianSplit quickselect on the LDS copy, exactly the operations of
-// the round-1 one-node-per-workgroup kernel.  Nodes of one level own disjoint ranges of key/idx and distinct output slots, so running them
-// concurrently changes nothing; that kernel walked them one at a time with a block barrier per node.
 static constexpr int KD_SW = 16;
+static constexpr int KD_PD = 256;  // dimensions of the multi-wave partials (larger dd: one wave per node)
+
+// min / max over points idx[s], idx[s + step], ... (< e) along dims d0 + lane + 64 j (j < 4); 4 points per round
+__device__ __forceinline__ void kd_minmax_idx(const float *__restrict__ rows, int dd, const int *idx, int s, int e,
+                                              int step, int d0, float (&mn)[4], float (&mx)[4]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        mn[j] = INFINITY;
+        mx[j] = -INFINITY;
+    }
+    int i = s;
+    for (; i + 3 * step < e; i += 4 * step) {
+        const float *r[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) r[u] = rows + (long)idx[i + u * step] * dd;
+        float v[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int d = d0 + j * 64 + lane;
+                v[u][j] = d < dd ? r[u][d] : 0.0f;
+            }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                mn[j] = fminf(mn[j], v[u][j]);
+                mx[j] = fmaxf(mx[j], v[u][j]);
+            }
+    }
+    for (; i < e; i += step) {
+        const float *r = rows + (long)idx[i] * dd;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int d = d0 + j * 64 + lane;
+            const float v = d < dd ? r[d] : 0.0f;
+            mn[j] = fminf(mn[j], v);
+            mx[j] = fmaxf(mx[j], v);
+        }
+    }
+}
+
+// annMedianSplit on kk[0..n) / ii[0..n) (LDS) by one wave; Lp / Rp: n ints of LDS scratch.  Leaves the keys and
+// indices permuted exactly as the sequential quickselect does (kd_median_big_kernel's derivation), the first maximum
+// of kk[0..n_lo) swapped to n_lo - 1.
+__device__ __forceinline__ void kd_median_wave(float *kk, int *ii, int n, int *Lp, int *Rp) {
+    const int lane = threadIdx.x & 63;
+    const int n_lo = n / 2;
+    kd_qselect_wave(kk, ii, 0, n - 1, n_lo, Lp, Rp);
+    // the first maximum of kk[0..n_lo) to n_lo - 1 (NaN keys as in kd_median_big_kernel)
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = lane; i < n_lo; i += 64) {
+        const float v = kk[i];
+        if (v == v && (v > bv || bi == 0x7fffffff)) {
+            bv = v;
+            bi = i;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (oi != 0x7fffffff && (bi == 0x7fffffff || ov > bv || (ov == bv && oi < bi))) {
+            bv = ov;
+            bi = oi;
+        }
+    }
+    if (n_lo > 0 && (bi == 0x7fffffff || kk[0] != kk[0])) bi = 0;
+    if (n_lo > 0 && lane == 0) kd_swap(kk, ii, n_lo - 1, bi);
+    kd_wsync();
+}
+
 __global__ __launch_bounds__(64 * KD_SW) void kd_subtree_waves_kernel(const float *__restrict__ rows, int dd,
                                                                      int *__restrict__ pidx,
                                                                      const KdNodeDev *__restrict__ roots, int bs,
                                                                      int *__restrict__ cd_out, float *__restrict__ cv_out) {
     __shared__ float key[KD_SUB];
     __shared__ int idx[KD_SUB];
+    __shared__ int lpos[KD_SUB], rpos[KD_SUB];
     __shared__ int2 lvl[2][KD_SUB / 2 + 1];
     __shared__ int nlvl[2];
+    __shared__ float pmn[KD_SW][KD_PD], pmx[KD_SW][KD_PD];
+    __shared__ int gcd[KD_SW];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const KdNodeDev R = roots[blockIdx.x];
     const int S = R.s, m_all = R.e - R.s;
@@ -427,97 +595,93 @@ __global__ __launch_bounds__(64 * KD_SW) void kd_subtree_waves_kernel(const floa
         nlvl[1] = 0;
     }
     __syncthreads();
+    // a node's cut dimension known: keys gathered, median, outputs, children (one wave; keys already in LDS)
+    auto split_node = [&](int s, int e, int cd, int nxt) __attribute__((always_inline)) {
+        const int n = e - s, n_lo = n / 2;
+        kd_median_wave(key + s, idx + s, n, lpos + s, rpos + s);
+        if (lane == 0) {
+            const float *kk = key + s;
+            const int m = s + n_lo;
+            cd_out[S + m] = cd;
+            cv_out[S + m] = (float)(((double)(kk[n_lo > 0 ? n_lo - 1 : 0] + kk[n_lo])) / 2.0);
+            if (e - m > bs) lvl[nxt][atomicAdd(&nlvl[nxt], 1)] = make_int2(m, e);
+            if (m - s > bs) lvl[nxt][atomicAdd(&nlvl[nxt], 1)] = make_int2(s, m);
+        }
+    };
     for (int L = 0;; L++) {
         const int cur = L & 1, nxt = cur ^ 1;
         const int nn = nlvl[cur];
         if (nn == 0) break;  // uniform: read after the barrier
-        for (int j = w; j < nn; j += KD_SW) {
-            const int2 nd = lvl[cur][j];
-            const int s = nd.x, e = nd.y;
-            float best = -INFINITY;
-            int bd = 0x7fffffff;
-            for (int d = lane; d < dd; d += 64) {  // this lane's dimensions ascend: strict > keeps the first
-                float mn = INFINITY, mx = -INFINITY;
-#pragma unroll 4
-                for (int i = s; i < e; i++) {
-                    const float v = rows[(long)idx[i] * dd + d];
-                    mn = fminf(mn, v);
-                    mx = fmaxf(mx, v);
-                }
-                const float spr = mx - mn;
-                if (spr > best) {
-                    best = spr;
-                    bd = d;
-                }
-            }
-            for (int o = 32; o > 0; o >>= 1) {
-                const float ob = __shfl_xor(best, o, 64);
-                const int od = __shfl_xor(bd, o, 64);
-                if (ob > best || (ob == best && od < bd)) {
-                    best = ob;
-                    bd = od;
-                }
-            }
-            const int cd = best > 0.0f ? bd : 0;
-            for (int i = s + lane; i < e; i += 64) key[i] = rows[(long)idx[i] * dd + cd];
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the keys are in LDS before lane 0 reads them
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) {  // annMedianSplit on key[s..e) / idx[s..e), as the round-1 kernel did
-                float *kk = key + s;
-                int *ii = idx + s;
-                const int n = e - s, n_lo = n / 2;
-                auto sw = [&](int a, int b) {
-                    const float tk = kk[a];
-                    kk[a] = kk[b];
-                    kk[b] = tk;
-                    const int ti = ii[a];
-                    ii[a] = ii[b];
-                    ii[b] = ti;
-                };
-                int l = 0, r = n - 1;
-                while (l < r) {
-                    int i = (r + l) / 2, k;
-                    if (kk[i] > kk[r]) sw(i, r);
-                    sw(l, i);
-                    const float c = kk[l];
-                    i = l;
-                    k = r;
-                    for (;;) {
-                        while (kk[++i] < c) {
+        if (nn < KD_SW && dd <= KD_PD) {
+            const int gw = KD_SW / nn, j = w / gw, sub = w - j * gw;
+            int s = 0, e = 0;
+            if (j < nn) {
+                const int2 nd = lvl[cur][j];
+                s = nd.x;
+                e = nd.y;
+                for (int d0 = 0; d0 < dd; d0 += 256) {
+                    float mn[4], mx[4];
+                    kd_minmax_idx(rows, dd, idx, s + sub, e, gw, d0, mn, mx);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int d = d0 + q * 64 + lane;
+                        if (d < dd) {
+                            pmn[w][d] = mn[q];
+                            pmx[w][d] = mx[q];
                         }
-                        while (kk[--k] > c) {
-                        }
-                        if (i < k)
-                            sw(i, k);
-                        else
-                            break;
                     }
-                    sw(l, k);
-                    if (k > n_lo)
-                        r = k - 1;
-                    else if (k < n_lo)
-                        l = k + 1;
-                    else
-                        break;
                 }
-                if (n_lo > 0) {
-                    float c = kk[0];
-                    int k = 0;
-                    for (int i = 1; i < n_lo; i++)
-                        if (kk[i] > c) {
-                            c = kk[i];
-                            k = i;
-                        }
-                    sw(n_lo - 1, k);
-                }
-                const int m = s + n_lo;
-                cd_out[S + m] = cd;
-                cv_out[S + m] = (float)(((double)(kk[n_lo > 0 ? n_lo - 1 : 0] + kk[n_lo])) / 2.0);
-                if (e - m > bs) lvl[nxt][atomicAdd(&nlvl[nxt], 1)] = make_int2(m, e);
-                if (m - s > bs) lvl[nxt][atomicAdd(&nlvl[nxt], 1)] = make_int2(s, m);
             }
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
+            if (j < nn && sub == 0) {
+                float best = -INFINITY;
+                int bd = 0x7fffffff;
+                for (int d = lane; d < dd; d += 64) {  // this lane's dimensions ascend: strict > keeps the first
+                    float mn = pmn[w][d], mx = pmx[w][d];
+                    for (int g = 1; g < gw; g++) {
+                        mn = fminf(mn, pmn[w + g][d]);
+                        mx = fmaxf(mx, pmx[w + g][d]);
+                    }
+                    const float spr = mx - mn;
+                    if (spr > best) {
+                        best = spr;
+                        bd = d;
+                    }
+                }
+                const int cd = kd_first_max(best, bd);
+                if (lane == 0) gcd[j] = cd;
+            }
+            __syncthreads();
+            if (j < nn) {
+                const int cd = gcd[j];
+                for (int i = s + sub * 64 + lane; i < e; i += gw * 64) key[i] = rows[(long)idx[i] * dd + cd];
+            }
+            __syncthreads();
+            if (j < nn && sub == 0) split_node(s, e, gcd[j], nxt);
+        } else {
+            for (int j = w; j < nn; j += KD_SW) {
+                const int2 nd = lvl[cur][j];
+                const int s = nd.x, e = nd.y;
+                float best = -INFINITY;
+                int bd = 0x7fffffff;
+                for (int d0 = 0; d0 < dd; d0 += 256) {
+                    float mn[4], mx[4];
+                    kd_minmax_idx(rows, dd, idx, s, e, 1, d0, mn, mx);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {  // this lane's dimensions ascend: strict > keeps the first
+                        const int d = d0 + q * 64 + lane;
+                        const float spr = mx[q] - mn[q];
+                        if (d < dd && spr > best) {
+                            best = spr;
+                            bd = d;
+                        }
+                    }
+                }
+                const int cd = kd_first_max(best, bd);
+                for (int i = s + lane; i < e; i += 64) key[i] = rows[(long)idx[i] * dd + cd];
+                kd_wsync();
+                split_node(s, e, cd, nxt);
+            }
         }
         __syncthreads();
         if (tid == 0) nlvl[cur] = 0;

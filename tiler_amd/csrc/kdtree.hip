@@ -346,11 +346,19 @@ __global__ __launch_bounds__(64 * KD_MW) void kd_median_big_kernel(float *__rest
         const int seg = (r - l + KD_MW) / KD_MW;  // ceil((r - l + 1) / KD_MW)
         const int a0 = l + w * seg, a1 = min(r + 1, a0 + seg);
         int nl = 0, nr = 0;
-        for (int p0 = a0; p0 < a1; p0 += 64) {
-            const int p = p0 + lane;
-            const float v = p < a1 ? kk[p] : 0.0f;
-            nl += __popcll(__ballot(p < a1 && p > l && !(v < c)));
-            nr += __popcll(__ballot(p < a1 && p < r && !(v > c)));
+        for (int p0 = a0; p0 < a1; p0 += 256) {  // 4 loads in flight per lane before their ballots
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = p0 + 64 * u + lane;
+                v[u] = p < a1 ? kk[p] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = p0 + 64 * u + lane;
+                nl += __popcll(__ballot(p < a1 && p > l && !(v[u] < c)));
+                nr += __popcll(__ballot(p < a1 && p < r && !(v[u] > c)));
+            }
         }
         if (lane == 0) {
             wl[w] = nl;
@@ -366,20 +374,29 @@ __global__ __launch_bounds__(64 * KD_MW) void kd_median_big_kernel(float *__rest
             tot_r += wr[x];
         }
         int np = 0;
-        for (int p0 = a0; p0 < a1; p0 += 64) {
-            const int p = p0 + lane;
-            const float v = p < a1 ? kk[p] : 0.0f;
-            // a stopper is where the scan's loop test FAILS: !(key < c) / !(key > c), so a NaN key (or a NaN pivot)
-            // stops both scans exactly as the sequential loop's comparisons do (and position l always stops the k-scan)
-            const bool isl = p < a1 && p > l && !(v < c), isr = p < a1 && p < r && !(v > c);
-            const unsigned long long bL = __ballot(isl), bR = __ballot(isr);
-            const int jl = bl + __popcll(bL & below) + 1;  // rank from the left (1-based)
-            const int rb = br + __popcll(bR & below);      // right stoppers below p
-            if (isl) Lp[jl - 1] = p;
-            if (isr) Rp[tot_r - rb - 1] = p;  // rank from the right: tot_r - rb
-            if (isl && tot_r - rb - (isr ? 1 : 0) >= jl) np++;  // R_jl > p: pair jl is swapped
-            bl += __popcll(bL);
-            br += __popcll(bR);
+        for (int p0 = a0; p0 < a1; p0 += 256) {  // 4 loads in flight, then the 4 pieces in position order
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = p0 + 64 * u + lane;
+                v[u] = p < a1 ? kk[p] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int p = p0 + 64 * u + lane;
+                // a stopper is where the scan's loop test FAILS: !(key < c) / !(key > c), so a NaN key (or a NaN
+                // pivot) stops both scans exactly as the sequential loop's comparisons do (and position l always
+                // stops the k-scan)
+                const bool isl = p < a1 && p > l && !(v[u] < c), isr = p < a1 && p < r && !(v[u] > c);
+                const unsigned long long bL = __ballot(isl), bR = __ballot(isr);
+                const int jl = bl + __popcll(bL & below) + 1;  // rank from the left (1-based)
+                const int rb = br + __popcll(bR & below);      // right stoppers below p
+                if (isl) Lp[jl - 1] = p;
+                if (isr) Rp[tot_r - rb - 1] = p;  // rank from the right: tot_r - rb
+                if (isl && tot_r - rb - (isr ? 1 : 0) >= jl) np++;  // R_jl > p: pair jl is swapped
+                bl += __popcll(bL);
+                br += __popcll(bR);
+            }
         }
         for (int o = 32; o > 0; o >>= 1) np += __shfl_xor(np, o, 64);
         if (lane == 0) wp[w] = np;
@@ -501,6 +518,7 @@ __global__ __launch_bounds__(256) void kd_pos_kernel(int n, const int *__restric
 static constexpr int KD_SUB = 1024;
 static constexpr int KD_SW = 16;
 static constexpr int KD_PD = 256;  // dimensions of the multi-wave partials (larger dd: one wave per node)
+static constexpr int KD_DFS = 32;  // nodes this small are finished depth first by one wave (stack depth <= 6 + 1)
 
 // min / max over points idx[s], idx[s + step], ... (< e) along dims d0 + lane + 64 j (j < 4); 4 points per round
 __device__ __forceinline__ void kd_minmax_idx(const float *__restrict__ rows, int dd, const int *idx, int s, int e,
@@ -585,6 +603,7 @@ __global__ __launch_bounds__(64 * KD_SW) void kd_subtree_waves_kernel(const floa
     __shared__ int nlvl[2];
     __shared__ float pmn[KD_SW][KD_PD], pmx[KD_SW][KD_PD];
     __shared__ int gcd[KD_SW];
+    __shared__ int2 stk[KD_SW][16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const KdNodeDev R = roots[blockIdx.x];
     const int S = R.s, m_all = R.e - R.s;
@@ -596,16 +615,62 @@ __global__ __launch_bounds__(64 * KD_SW) void kd_subtree_waves_kernel(const floa
     }
     __syncthreads();
     // a node's cut dimension known: keys gathered, median, outputs, children (one wave; keys already in LDS)
+    // children of <= KD_DFS points go on the wave's own stack and are finished by that wave, depth first, without the
+    // level barriers (the deep levels are many tiny nodes whose cost is fixed latency)
+    int top = 0;  // wave-uniform depth of this wave's stack
     auto split_node = [&](int s, int e, int cd, int nxt) __attribute__((always_inline)) {
         const int n = e - s, n_lo = n / 2;
         kd_median_wave(key + s, idx + s, n, lpos + s, rpos + s);
+        const int m = s + n_lo;
         if (lane == 0) {
             const float *kk = key + s;
-            const int m = s + n_lo;
             cd_out[S + m] = cd;
             cv_out[S + m] = (float)(((double)(kk[n_lo > 0 ? n_lo - 1 : 0] + kk[n_lo])) / 2.0);
-            if (e - m > bs) lvl[nxt][atomicAdd(&nlvl[nxt], 1)] = make_int2(m, e);
-            if (m - s > bs) lvl[nxt][atomicAdd(&nlvl[nxt], 1)] = make_int2(s, m);
+        }
+        if (e - m > bs) {
+            if (e - m > KD_DFS) {
+                if (lane == 0) lvl[nxt][atomicAdd(&nlvl[nxt], 1)] = make_int2(m, e);
+            } else {
+                if (lane == 0) stk[w][top] = make_int2(m, e);
+                top++;
+            }
+        }
+        if (m - s > bs) {
+            if (m - s > KD_DFS) {
+                if (lane == 0) lvl[nxt][atomicAdd(&nlvl[nxt], 1)] = make_int2(s, m);
+            } else {
+                if (lane == 0) stk[w][top] = make_int2(s, m);
+                top++;
+            }
+        }
+    };
+    // one node by one wave: annSpread / annMaxSpread over its points, keys to LDS, median, children
+    auto wave_node = [&](int s, int e, int nxt) __attribute__((always_inline)) {
+        float best = -INFINITY;
+        int bd = 0x7fffffff;
+        for (int d0 = 0; d0 < dd; d0 += 256) {
+            float mn[4], mx[4];
+            kd_minmax_idx(rows, dd, idx, s, e, 1, d0, mn, mx);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {  // this lane's dimensions ascend: strict > keeps the first
+                const int d = d0 + q * 64 + lane;
+                const float spr = mx[q] - mn[q];
+                if (d < dd && spr > best) {
+                    best = spr;
+                    bd = d;
+                }
+            }
+        }
+        const int cd = kd_first_max(best, bd);
+        for (int i = s + lane; i < e; i += 64) key[i] = rows[(long)idx[i] * dd + cd];
+        kd_wsync();
+        split_node(s, e, cd, nxt);
+    };
+    auto drain_stack = [&](int nxt) __attribute__((always_inline)) {
+        while (top > 0) {
+            kd_wsync();
+            const int2 nd = stk[w][--top];
+            wave_node(nd.x, nd.y, nxt);
         }
     };
     for (int L = 0;; L++) {
@@ -657,30 +722,15 @@ __global__ __launch_bounds__(64 * KD_SW) void kd_subtree_waves_kernel(const floa
                 for (int i = s + sub * 64 + lane; i < e; i += gw * 64) key[i] = rows[(long)idx[i] * dd + cd];
             }
             __syncthreads();
-            if (j < nn && sub == 0) split_node(s, e, gcd[j], nxt);
+            if (j < nn && sub == 0) {
+                split_node(s, e, gcd[j], nxt);
+                drain_stack(nxt);
+            }
         } else {
             for (int j = w; j < nn; j += KD_SW) {
                 const int2 nd = lvl[cur][j];
-                const int s = nd.x, e = nd.y;
-                float best = -INFINITY;
-                int bd = 0x7fffffff;
-                for (int d0 = 0; d0 < dd; d0 += 256) {
-                    float mn[4], mx[4];
-                    kd_minmax_idx(rows, dd, idx, s, e, 1, d0, mn, mx);
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {  // this lane's dimensions ascend: strict > keeps the first
-                        const int d = d0 + q * 64 + lane;
-                        const float spr = mx[q] - mn[q];
-                        if (d < dd && spr > best) {
-                            best = spr;
-                            bd = d;
-                        }
-                    }
-                }
-                const int cd = kd_first_max(best, bd);
-                for (int i = s + lane; i < e; i += 64) key[i] = rows[(long)idx[i] * dd + cd];
-                kd_wsync();
-                split_node(s, e, cd, nxt);
+                wave_node(nd.x, nd.y, nxt);
+                drain_stack(nxt);
             }
         }
         __syncthreads();

@@ -978,6 +978,14 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(RescoreArgs a, int list_n
 // fixed costs (a 512-query workgroup per split, fragment prep, rescore) dominated a call of one query (0.6 ms).
 // ------------------------------------------------------------------------------------------
 static constexpr int SCAN_D_MAX = 256;
+// One term of the reference's sequential sum, d + (q - c)^2 rounded after the product and after the sum (the mode's
+// IEEE single ops, as the compiler's own).  Written as one asm block so that the vectoriser cannot pack the
+// independent per-query sums into v_pk_add_f32 / v_pk_mul_f32 with v_mov shuffles (measured slower here).
+__device__ __forceinline__ float sq_acc(float d, float q, float c) {
+    float t;
+    asm("v_sub_f32 %1, %2, %3\n\tv_mul_f32 %1, %1, %1\n\tv_add_f32 %0, %0, %1" : "+v"(d), "=&v"(t) : "v"(q), "v"(c));
+    return d;
+}
 template <int QN, int K>
 __global__ __launch_bounds__(256) void nn_scan_small_kernel(RescoreArgs a, int nsplit, float *__restrict__ pd,
                                                             int *__restrict__ pi) {
@@ -1006,16 +1014,48 @@ __global__ __launch_bounds__(256) void nn_scan_small_kernel(RescoreArgs a, int n
         float dist[QN];
 #pragma unroll
         for (int q = 0; q < QN; q++) dist[q] = 0.0f;
-        for (int d0 = 0; d0 < d; d0 += 4) {  // d % 4 == 0 (checked on the host)
-            const float4 cv = *reinterpret_cast<const float4 *>(c + d0);
-#pragma unroll
-            for (int q = 0; q < QN; q++) {
-                const float4 qv = *reinterpret_cast<const float4 *>(sq + q * SCAN_D_MAX + d0);
+        if constexpr (QN == 1) {  // one sum per row: the compiler keeps 8 loads in flight by itself
+            for (int d0 = 0; d0 < d; d0 += 4) {  // d % 4 == 0 (checked on the host)
+                const float4 cv = *reinterpret_cast<const float4 *>(c + d0);
+                const float4 qv = *reinterpret_cast<const float4 *>(sq + d0);
                 float t;
-                t = qv.x - cv.x; dist[q] = dist[q] + t * t;
-                t = qv.y - cv.y; dist[q] = dist[q] + t * t;
-                t = qv.z - cv.z; dist[q] = dist[q] + t * t;
-                t = qv.w - cv.w; dist[q] = dist[q] + t * t;
+                t = qv.x - cv.x; dist[0] = dist[0] + t * t;
+                t = qv.y - cv.y; dist[0] = dist[0] + t * t;
+                t = qv.z - cv.z; dist[0] = dist[0] + t * t;
+                t = qv.w - cv.w; dist[0] = dist[0] + t * t;
+            }
+        } else {
+            // QN sums per row: the row in steps of 16 dimensions through two register buffers, the next step's 4
+            // loads in flight while this step is summed (a row is one lane's; one load at a time waited out a memory
+            // latency per 16 bytes)
+            constexpr int SD = 16;
+            float4 ba[SD / 4], bb[SD / 4];
+            // unconditional loads (past the row end: its last 16 bytes again, never summed), so that the wait before a
+            // step's sums counts only that step's loads
+            auto load_step = [&](float4 (&v)[SD / 4], int d0) __attribute__((always_inline)) {
+#pragma unroll
+                for (int u = 0; u < SD / 4; u++) v[u] = *reinterpret_cast<const float4 *>(c + min(d0 + 4 * u, d - 4));
+            };
+            auto sum_step = [&](const float4 (&v)[SD / 4], int d0) __attribute__((always_inline)) {
+#pragma unroll
+                for (int u = 0; u < SD / 4; u++) {
+                    if (d0 + 4 * u >= d) break;
+#pragma unroll
+                    for (int q = 0; q < QN; q++) {
+                        const float4 qv = *reinterpret_cast<const float4 *>(sq + q * SCAN_D_MAX + d0 + 4 * u);
+                        dist[q] = sq_acc(dist[q], qv.x, v[u].x);
+                        dist[q] = sq_acc(dist[q], qv.y, v[u].y);
+                        dist[q] = sq_acc(dist[q], qv.z, v[u].z);
+                        dist[q] = sq_acc(dist[q], qv.w, v[u].w);
+                    }
+                }
+            };
+            load_step(ba, 0);
+            for (int d0 = 0; d0 < d; d0 += 2 * SD) {
+                load_step(bb, d0 + SD);
+                sum_step(ba, d0);
+                load_step(ba, d0 + 2 * SD);
+                sum_step(bb, d0 + SD);
             }
         }
 #pragma unroll

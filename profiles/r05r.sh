@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round 5 pass r: nn_search.hip without SLP packing + a one-step-ahead load in the small-batch scan.  NN GPU tests, then
+# Round 5 pass r: the small-batch scan (per-tile calls) variants against the previous build (r2: scalar sums + pipelined
 # A/B against the previous build: the per-call probe (scan kernel times at 1 / 4 / 16 queries, native 16-thread calls)
 # and the k = 8 preselection kernel (tools/k8_timing.py; its 32x32x16 shortlist lost its packed seed ops too).
 set -eu

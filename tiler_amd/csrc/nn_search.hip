@@ -63,17 +63,36 @@ __device__ __forceinline__ int row_perm(int i) { return (i & ~5) | ((i & 1) << 2
 __global__ __launch_bounds__(256) void prep_rows_kernel(PrepArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
     const long nblk = (a.n + 31) / 32;
+    double t_n2 = 0.0, t_h2 = 0.0, t_e2 = 0.0, t_ab = 0.0;
+    int t_ni = 0, t_bd = 0;
     for (long blk = (long)blockIdx.x * 4 + wave; blk < nblk; blk += (long)gridDim.x * 4) {
         const long r = blk * 32 + (a.perm ? row_perm(lane & 31) : (lane & 31));
         const bool valid = r < a.n;
         double s2 = 0, sh = 0, se = 0, mabs = 0;
         int notint = 0, bad = 0;
+        // the lane's 8 consecutive values of each k-step: two 16-byte loads when the rows allow it (d % 8 == 0, 32-byte
+        // aligned base), each value alone otherwise; the values and everything computed from them are the same
+        const bool vec = (a.d & 7) == 0 && (((uintptr_t)a.rows) & 31) == 0;
         for (int s = 0; s < a.S; s++) {
             half8 hv;
+            float vv[8];
+            const int k0 = s * 16 + 8 * h;
+            if (vec) {
+                float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+                if (valid && k0 < a.d) {
+                    const float4 *src = reinterpret_cast<const float4 *>(a.rows + r * a.d + k0);
+                    x0 = src[0];
+                    x1 = src[1];
+                }
+                vv[0] = x0.x; vv[1] = x0.y; vv[2] = x0.z; vv[3] = x0.w;
+                vv[4] = x1.x; vv[5] = x1.y; vv[6] = x1.z; vv[7] = x1.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; j++) vv[j] = (valid && k0 + j < a.d) ? a.rows[r * a.d + k0 + j] : 0.0f;
+            }
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                const int k = s * 16 + 8 * h + j;
-                const float v = (valid && k < a.d) ? a.rows[r * a.d + k] : 0.0f;
+                const float v = vv[j];
                 const float vs = v * a.scale;
                 _Float16 vh = (_Float16)vs;
                 if (fabsf((float)vh) < 6.103515625e-05f) vh = (_Float16)0.0f;  // no fp16 subnormal operands
@@ -109,18 +128,45 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(PrepArgs a) {
             a.nc[blk * 32 + pos] = valid ? (float)s2 : INFINITY;
             if (a.seed) a.seed[blk * 32 + pos] = valid ? -0.5f * (float)s2 : -INFINITY;
         }
-        if (a.ds) {
-            double m2 = wave_max_d(valid ? s2 : 0.0), mh = wave_max_d(valid ? sh : 0.0);
-            double me = wave_max_d(valid ? se : 0.0), ma = wave_max_d(valid ? mabs : 0.0);
-            int ni = __any(valid && notint), bd = __any(valid && bad);
-            if (lane == 0) {
-                atomicMax(&a.ds->max_n2_bits, (unsigned long long)__double_as_longlong(m2));
-                atomicMax(&a.ds->max_h2_bits, (unsigned long long)__double_as_longlong(mh));
-                atomicMax(&a.ds->max_e2_bits, (unsigned long long)__double_as_longlong(me));
-                atomicMax(&a.ds->max_abs_bits, (unsigned long long)__double_as_longlong(ma));
-                if (ni) atomicOr(&a.ds->not_int, 1u);
-                if (bd) atomicOr(&a.ds->bad, 1u);
+        if (a.ds) {  // this thread's running maxima (all >= 0: the max of the bit patterns is the max of the values)
+            if (valid) {
+                t_n2 = fmax(t_n2, s2);
+                t_h2 = fmax(t_h2, sh);
+                t_e2 = fmax(t_e2, se);
+                t_ab = fmax(t_ab, mabs);
+                t_ni |= notint;
+                t_bd |= bad;
             }
+        }
+    }
+    if (a.ds) {  // one set of dataset atomics per workgroup (per wave and block they serialised on six addresses)
+        __shared__ double r_d[4][4];
+        __shared__ int r_i[4][2];
+        const double m2 = wave_max_d(t_n2), mh = wave_max_d(t_h2), me = wave_max_d(t_e2), ma = wave_max_d(t_ab);
+        const int ni = __any(t_ni), bd = __any(t_bd);
+        if (lane == 0) {
+            r_d[wave][0] = m2;
+            r_d[wave][1] = mh;
+            r_d[wave][2] = me;
+            r_d[wave][3] = ma;
+            r_i[wave][0] = ni;
+            r_i[wave][1] = bd;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double v[4] = {0.0, 0.0, 0.0, 0.0};
+            int f0 = 0, f1 = 0;
+            for (int w = 0; w < 4; w++) {
+                for (int x = 0; x < 4; x++) v[x] = fmax(v[x], r_d[w][x]);
+                f0 |= r_i[w][0];
+                f1 |= r_i[w][1];
+            }
+            atomicMax(&a.ds->max_n2_bits, (unsigned long long)__double_as_longlong(v[0]));
+            atomicMax(&a.ds->max_h2_bits, (unsigned long long)__double_as_longlong(v[1]));
+            atomicMax(&a.ds->max_e2_bits, (unsigned long long)__double_as_longlong(v[2]));
+            atomicMax(&a.ds->max_abs_bits, (unsigned long long)__double_as_longlong(v[3]));
+            if (f0) atomicOr(&a.ds->not_int, 1u);
+            if (f1) atomicOr(&a.ds->bad, 1u);
         }
     }
 }
@@ -129,17 +175,42 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(PrepArgs a) {
 __global__ __launch_bounds__(256) void maxabs_kernel(const float *rows, long total, unsigned int *out) {
     float m = 0.0f;
     int ni = 0;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        const float x = rows[i];
-        float v = fabsf(x);
+    auto fold = [&](float x) __attribute__((always_inline)) {
+        const float v = fabsf(x);
         m = isfinite(v) ? fmaxf(m, v) : m;
         ni |= !(x == rintf(x));
+    };
+    const long stride = (long)gridDim.x * 256, g = (long)blockIdx.x * 256 + threadIdx.x;
+    long i0 = 0;
+    if ((((uintptr_t)rows) & 15) == 0) {  // 16-byte loads, two in flight per thread; the tail below
+        const float4 *r4 = reinterpret_cast<const float4 *>(rows);
+        const long n4 = total >> 2;
+        long i = g;
+        for (; i + stride < n4; i += 2 * stride) {
+            const float4 x = r4[i], y = r4[i + stride];
+            fold(x.x); fold(x.y); fold(x.z); fold(x.w);
+            fold(y.x); fold(y.y); fold(y.z); fold(y.w);
+        }
+        if (i < n4) {
+            const float4 x = r4[i];
+            fold(x.x); fold(x.y); fold(x.z); fold(x.w);
+        }
+        i0 = n4 << 2;
     }
+    for (long i = i0 + g; i < total; i += stride) fold(rows[i]);
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
     const bool any_ni = __any(ni);
+    __shared__ float r_m[4];
+    __shared__ int r_n[4];
     if ((threadIdx.x & 63) == 0) {
-        atomicMax(out, __float_as_uint(m));
-        if (any_ni) atomicOr(out + 1, 1u);
+        r_m[threadIdx.x >> 6] = m;
+        r_n[threadIdx.x >> 6] = any_ni;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one pair of atomics per workgroup (one per wave serialised on the two words)
+        const float mm = fmaxf(fmaxf(r_m[0], r_m[1]), fmaxf(r_m[2], r_m[3]));
+        atomicMax(out, __float_as_uint(mm));
+        if (r_n[0] | r_n[1] | r_n[2] | r_n[3]) atomicOr(out + 1, 1u);
     }
 }
 
@@ -304,13 +375,38 @@ __global__ __launch_bounds__(256) void prep16_kernel(Prep16Args a) {
         const long row = blk * 16 + (a.perm ? perm16(r) : r);
         const bool valid = row < a.n;
         double s2 = 0;
+        const bool vec = (a.d & 7) == 0 && (((uintptr_t)a.rows) & 31) == 0;
         for (int s = 0; s < a.S; s++) {
             half8 hv;
+            float vv[8];
+            const int k0 = s * 32 + 8 * g;
+            if (vec) {  // the piece's 8 consecutive dimensions in two 16-byte loads, then the DC swaps of dc_first_dim
+                float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+                if (valid && k0 < a.d) {
+                    const float4 *src = reinterpret_cast<const float4 *>(a.rows + row * a.d + k0);
+                    x0 = src[0];
+                    x1 = src[1];
+                }
+                vv[0] = x0.x; vv[1] = x0.y; vv[2] = x0.z; vv[3] = x0.w;
+                vv[4] = x1.x; vv[5] = x1.y; vv[6] = x1.z; vv[7] = x1.w;
+                if (a.dcfirst && valid && (k0 == 0 || k0 == 64 || k0 == 128) && k0 < a.d) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const int kd = dc_first_dim(k0 + j);
+                        if (kd != k0 + j) vv[j] = a.rows[row * a.d + kd];
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int k = k0 + j;
+                    const int kd = a.dcfirst ? dc_first_dim(k) : k;
+                    vv[j] = (valid && k < a.d) ? a.rows[row * a.d + kd] : 0.0f;
+                }
+            }
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                const int k = s * 32 + 8 * g + j;
-                const int kd = a.dcfirst ? dc_first_dim(k) : k;
-                const float v = (valid && k < a.d) ? a.rows[row * a.d + kd] : 0.0f;
+                const float v = vv[j];
                 const float vs = v * a.scale;
                 _Float16 vh = (_Float16)vs;
                 if (fabsf((float)vh) < 6.103515625e-05f) vh = (_Float16)0.0f;  // as prep_rows_kernel

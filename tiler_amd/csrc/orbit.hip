@@ -208,8 +208,10 @@ __global__ __launch_bounds__(256) void orbit_eq_kernel(const float *__restrict__
             if (j + t >= n) break;
             for (int m = 0; m < 3; m++) {
                 bool ok = true;
-                for (int i = lane; i < OD; i += 64)
-                    ok &= rows[(j + t) * OD + i] == mp->msgn[m][i] * rows[j * OD + mp->msrc[m][i]];
+                for (int i = lane; i < OD; i += 64) {  // a mismatch in any 64-dimension piece settles it
+                    ok = rows[(j + t) * OD + i] == mp->msgn[m][i] * rows[j * OD + mp->msrc[m][i]];
+                    if (!__all(ok)) break;
+                }
                 if (__all(ok)) b |= 1u << ((t - 1) * 3 + m);
             }
         }
@@ -373,6 +375,8 @@ __global__ __launch_bounds__(64 * ORB_PW) void orbit_prep_kernel(OrbitPrepArgs a
     }
     for (int i = tid; i < OD; i += 64 * ORB_PW) mc[i] = dataset ? a.mp->cs[i] : a.mp->qs[i];
     float *sw = srow[w];
+    double t_n2 = 0.0, t_p2 = 0.0, t_h2 = 0.0, t_e2 = 0.0;  // dataset statistics over this thread's valid rows
+    int t_bd = 0;
     for (long wb = blockIdx.x; wb * ORB_PW < nblk; wb += gridDim.x) {  // uniform trip count per workgroup
         const long blk = wb * ORB_PW + w;
         const long r = blk * 32 + (lane & 31);
@@ -460,15 +464,39 @@ __global__ __launch_bounds__(64 * ORB_PW) void orbit_prep_kernel(OrbitPrepArgs a
             a.seed[blk * 32 + pos] = valid ? -0.5f * (float)n2 : -INFINITY;
             if (valid) a.nc[r] = (float)n2;
         }
-        double mn = wave_max_d(valid ? n2 : 0.0), mp2 = wave_max_d(valid ? p2 : 0.0);
-        double mh = wave_max_d(valid ? h2 : 0.0), me = wave_max_d(valid ? e2 : 0.0);
-        const int bd = __any(valid && bad);
+        if (valid) {  // this thread's running maxima (all >= 0: bit patterns order like the values)
+            t_n2 = fmax(t_n2, n2);
+            t_p2 = fmax(t_p2, p2);
+            t_h2 = fmax(t_h2, h2);
+            t_e2 = fmax(t_e2, e2);
+            t_bd |= bad;
+        }
+    }
+    if (dataset) {  // one set of atomics per workgroup (per wave and block they serialised on five words)
+        __shared__ double r_d[ORB_PW][4];
+        __shared__ int r_b[ORB_PW];
+        const double mn = wave_max_d(t_n2), mp2 = wave_max_d(t_p2), mh = wave_max_d(t_h2), me = wave_max_d(t_e2);
+        const int bd = __any(t_bd);
         if (lane == 0) {
-            atomicMax(&a.ds->max_n2, (unsigned long long)__double_as_longlong(mn));
-            atomicMax(&a.ds->max_p2, (unsigned long long)__double_as_longlong(mp2));
-            atomicMax(&a.ds->max_h2, (unsigned long long)__double_as_longlong(mh));
-            atomicMax(&a.ds->max_e2, (unsigned long long)__double_as_longlong(me));
-            if (bd) atomicOr(&a.ds->bad, 1u);
+            r_d[w][0] = mn;
+            r_d[w][1] = mp2;
+            r_d[w][2] = mh;
+            r_d[w][3] = me;
+            r_b[w] = bd;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double v[4] = {0.0, 0.0, 0.0, 0.0};
+            int b = 0;
+            for (int x = 0; x < ORB_PW; x++) {
+                for (int y = 0; y < 4; y++) v[y] = fmax(v[y], r_d[x][y]);
+                b |= r_b[x];
+            }
+            atomicMax(&a.ds->max_n2, (unsigned long long)__double_as_longlong(v[0]));
+            atomicMax(&a.ds->max_p2, (unsigned long long)__double_as_longlong(v[1]));
+            atomicMax(&a.ds->max_h2, (unsigned long long)__double_as_longlong(v[2]));
+            atomicMax(&a.ds->max_e2, (unsigned long long)__double_as_longlong(v[3]));
+            if (b) atomicOr(&a.ds->bad, 1u);
         }
     }
 }

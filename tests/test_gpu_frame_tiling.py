@@ -173,6 +173,33 @@ def test_frame_tiling_end_to_end_c1(gpu, oracle):
     kt.finish_frame_tiling()
 
 
+def test_frame_tiling_small_batches_on_orbit_index(gpu, oracle):
+    """DoFrameTiling batches of <= 64 tiles on a mirror-orbit index (20 % symmetric tiles, so equal
+    distances among a tile's mirrors) take the small-batch exact scan by default; with the scan disabled
+    (tiler_set_scan_limits(0, 0)) they take the orbit MFMA tiers.  Both must give the restatement's tilemap items,
+    mirror flags and errors bit for bit."""
+    from tiler_amd.frame_tiling import KeyframeTiler
+    wl = synth.make_workload(29, 320, 240, 1, 3000, n_palettes=16)
+    kt = KeyframeTiler(wl.tiles, wl.thm, wl.tvm, wl.palettes, wl.ds)
+    assert kt.kdt.stats()["orbit_groups"] > 0
+    used = synth.used_one_palette(wl.tile_pal, 16)
+    ods, otile, opal, oattr = oracle.build_ft_dataset(used, wl.tiles, wl.thm, wl.tvm, wl.palettes)
+    lib = gpu.load()
+    try:
+        for limits in ((64, 16), (0, 0)):
+            assert lib.tiler_set_scan_limits(*limits) == 0
+            for q0, nq in ((0, 1), (5, 17), (100, 64)):
+                rgb = wl.frame_rgb[0][q0:q0 + nq]
+                g = kt.do_frame_tiling(rgb)
+                o = oracle.frame_tiling(rgb, ods, otile, opal, oattr)
+                for a, b in zip(g[:4], o[:4]):
+                    assert np.array_equal(a, b), (limits, q0, nq)
+                assert np.array_equal(g[4].view(np.uint32), o[4].view(np.uint32)), (limits, q0, nq)
+    finally:
+        lib.tiler_set_scan_limits(64, 16)
+    kt.finish_frame_tiling()
+
+
 def test_frame_tiling_flat_tiles_last_matches_small_batches(gpu):
     """A batch of >= 8192 tiles runs with its flat tiles moved last (their shortlist workgroups compute isotypic block
     0 only, nn_frame_tiling_dev / orbit_search); per-frame batches below that size keep the tile order.  Both must

@@ -237,7 +237,9 @@ __device__ __forceinline__ void scan_keys(const floatx16 &acc, int base, int h, 
     }
 }
 
-template <int S, int L, int CB, int NW>
+// QB query blocks of 32 per wave (2: each A-fragment read feeds two MFMAs; 1: twice the waves for the same queries,
+// for launches too small to give every SIMD more than one wave otherwise -- UseOne's k = 8 preselection)
+template <int S, int L, int CB, int NW, int QB = 2>
 __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *__restrict__ cfrag,
                                                               const float *__restrict__ cnc, int nblk,
                                                               const half8 *__restrict__ qfrag, int nq,
@@ -251,26 +253,28 @@ __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *_
     static_assert((CB * S * 64) % NT == 0, "stage must split evenly over the workgroup");
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
     const int nqblk = (nq + 31) / 32;
-    const int qb0 = (blockIdx.x * NW + w) * 2;
+    const int qb0 = (blockIdx.x * NW + w) * QB;
     const int split = blockIdx.y;
     const int b_begin = split * blk_per_split;
     const int b_end = min(nblk, b_begin + blk_per_split);
 
-    half8 bq0[S], bq1[S];
+    half8 bq[QB][S];
     // query blocks past the end compute on a clamped duplicate and are never written out
-    const long qa = min(qb0, nqblk - 1), qc = min(qb0 + 1, nqblk - 1);
 #pragma unroll
-    for (int s = 0; s < S; s++) {
-        bq0[s] = qfrag[(qa * S + s) * 64 + lane];
-        bq1[s] = qfrag[(qc * S + s) * 64 + lane];
-    }
-    float lk0[L], lk1[L];
-    int li0[L], li1[L];
+    for (int x = 0; x < QB; x++) {
+        const long qa = min(qb0 + x, nqblk - 1);
 #pragma unroll
-    for (int i = 0; i < L; i++) {
-        lk0[i] = lk1[i] = INFINITY;
-        li0[i] = li1[i] = -1;
+        for (int s = 0; s < S; s++) bq[x][s] = qfrag[(qa * S + s) * 64 + lane];
     }
+    float lk[QB][L];
+    int li[QB][L];
+#pragma unroll
+    for (int x = 0; x < QB; x++)
+#pragma unroll
+        for (int i = 0; i < L; i++) {
+            lk[x][i] = INFINITY;
+            li[x][i] = -1;
+        }
 
     const int nstage = (b_end > b_begin) ? (b_end - b_begin + CB - 1) / CB : 0;
     // LDS-DMA staging (global_load_lds_dwordx4): the fragment image is lane-linear, so each wave
@@ -306,34 +310,36 @@ __global__ __launch_bounds__(NW * 64, 2) void nn_shortlist_kernel(const half8 *_
             const int blk = b_begin + st * CB + cb;
             if (blk < b_end) {
                 const float4 n0 = ncr[cb][0], n1 = ncr[cb][1], n2 = ncr[cb][2], n3 = ncr[cb][3];
-                floatx16 acc0 = {-0.5f * n0.x, -0.5f * n0.y, -0.5f * n0.z, -0.5f * n0.w,
-                                 -0.5f * n1.x, -0.5f * n1.y, -0.5f * n1.z, -0.5f * n1.w,
-                                 -0.5f * n2.x, -0.5f * n2.y, -0.5f * n2.z, -0.5f * n2.w,
-                                 -0.5f * n3.x, -0.5f * n3.y, -0.5f * n3.z, -0.5f * n3.w};
-                floatx16 acc1 = acc0;
+                const floatx16 seed = {-0.5f * n0.x, -0.5f * n0.y, -0.5f * n0.z, -0.5f * n0.w,
+                                       -0.5f * n1.x, -0.5f * n1.y, -0.5f * n1.z, -0.5f * n1.w,
+                                       -0.5f * n2.x, -0.5f * n2.y, -0.5f * n2.z, -0.5f * n2.w,
+                                       -0.5f * n3.x, -0.5f * n3.y, -0.5f * n3.z, -0.5f * n3.w};
+                floatx16 acc[QB];
+#pragma unroll
+                for (int x = 0; x < QB; x++) acc[x] = seed;
 #pragma unroll
                 for (int s = 0; s < S; s++) {
                     const half8 av = reinterpret_cast<const half8 *>(B)[(cb * S + s) * 64 + lane];
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq0[s], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq1[s], acc1, 0, 0, 0);
+#pragma unroll
+                    for (int x = 0; x < QB; x++) acc[x] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bq[x][s], acc[x], 0, 0, 0);
                 }
                 const int base = blk * 32;
-                scan_keys<L>(acc0, base, h, perm, lk0, li0);
-                scan_keys<L>(acc1, base, h, perm, lk1, li1);
+#pragma unroll
+                for (int x = 0; x < QB; x++) scan_keys<L>(acc[x], base, h, perm, lk[x], li[x]);
             }
         }
         __syncthreads();  // vmcnt(0) + s_barrier: next stage's DMA landed, this stage's reads done
     }
     // partial lists: [q][split][h][L]
 #pragma unroll
-    for (int qb = 0; qb < 2; qb++) {
-        const int q = (qb0 + qb) * 32 + (lane & 31);
+    for (int x = 0; x < QB; x++) {
+        const int q = (qb0 + x) * 32 + (lane & 31);
         if (q < nq) {
             const long o = (((long)q * nsplit + split) * 2 + h) * L;
 #pragma unroll
             for (int i = 0; i < L; i++) {
-                out_key[o + i] = qb ? lk1[i] : lk0[i];
-                out_idx[o + i] = qb ? li1[i] : li0[i];
+                out_key[o + i] = lk[x][i];
+                out_idx[o + i] = li[x][i];
             }
         }
     }
@@ -1495,14 +1501,15 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
 // waves per workgroup of the 32x32x16 shortlist on 64-d rows (UseOne's k = 8 preselection, main.pas:3830): two query
 // blocks of 32 per wave, so 64 * NW queries per workgroup
 static constexpr int GEN_NW_S4 = 4;
+static constexpr int GEN_QB_S4 = 1;  // query blocks per wave there: 16,384 items x 4 splits fill 2 waves per SIMD
 
-template <int S, int L, int CB, int NW>
+template <int S, int L, int CB, int NW, int QB = 2>
 static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     const int nqblk = (nq + 31) / 32;
-    const dim3 grid((nqblk + 2 * NW - 1) / (2 * NW), nsplit);
+    const dim3 grid((nqblk + QB * NW - 1) / (QB * NW), nsplit);
     const size_t lds = 2 * (CB * S * 1024 + CB * 128);
     KTimer tm("nn_shortlist", stream);
-    hipLaunchKernelGGL((nn_shortlist_kernel<S, L, CB, NW>), grid, dim3(NW * 64), lds, stream, (const half8 *)ix->d_frag,
+    hipLaunchKernelGGL((nn_shortlist_kernel<S, L, CB, NW, QB>), grid, dim3(NW * 64), lds, stream, (const half8 *)ix->d_frag,
                        ix->d_nc, ix->nblk, (const half8 *)ix->scratch.qfrag, nq, bps, nsplit, ix->perm,
                        ix->scratch.key, ix->scratch.idx);
 }
@@ -1553,7 +1560,7 @@ static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, hipStrea
 template <int L>
 static int dispatch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     switch (ix->S) {
-        case 4: launch_shortlist<4, L, 6, GEN_NW_S4>(ix, nq, nsplit, bps, stream); break;
+        case 4: launch_shortlist<4, L, 6, GEN_NW_S4, GEN_QB_S4>(ix, nq, nsplit, bps, stream); break;
         case 8: launch_shortlist<8, L, 3, 4>(ix, nq, nsplit, bps, stream); break;
         case 12: launch_shortlist<12, L, 2, 8>(ix, nq, nsplit, bps, stream); break;
         case 16: launch_shortlist<16, L, 2, 4>(ix, nq, nsplit, bps, stream); break;
@@ -1786,7 +1793,7 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     const int lpq = v16 ? 4 : 2;
     const int nblk = v16 ? ix->nblk16 : ix->nblk;
     const int max_split = 64 / (lpq * L);
-    const int qpwg = v16 ? SL16_NW * SL16_QB * 16 : (ix->S == 12 ? 512 : ix->S == 4 ? 64 * GEN_NW_S4 : 256);
+    const int qpwg = v16 ? SL16_NW * SL16_QB * 16 : (ix->S == 12 ? 512 : ix->S == 4 ? 32 * GEN_QB_S4 * GEN_NW_S4 : 256);
     const int wgs = (nq + qpwg - 1) / qpwg;
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
     nsplit = std::min(nsplit, nblk);

@@ -71,6 +71,8 @@ struct Dl3Tab {
 #endif
 constexpr int DL3_U = DL3_U_V;    // records loaded per lane before any is used
 constexpr int DL3_UM = DL3_UM_V;  // the same in the merge pass (two records per entry)
+// the scans load up to 64 * unroll + 63 records past tot, into the QN / EC tables' 1,024-record slack
+static_assert(64 * (DL3_U + 1) <= 1024 && 64 * (DL3_UM + 1) <= 1024, "DLv3 unroll depth exceeds the table slack");
 
 __device__ __forceinline__ void dl3_set_ec(const Dl3Tab &t, int i, float e, int c) {
     t.EC[i] = make_uint2(__float_as_uint(e), (uint32_t)c);

@@ -25,8 +25,12 @@ def main():
     ap.add_argument("--item-tiles", type=int, default=16384)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--lib", default="")
     args = ap.parse_args()
     import torch
+    import tiler_amd._lib as L
+    if args.lib:
+        L.LIB_PATH = os.path.abspath(args.lib)
     import tiler_amd
     from tiler_amd import frame_tiling as ftm
     from tiler_amd import synth

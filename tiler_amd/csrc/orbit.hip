@@ -2201,7 +2201,7 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     return 0;
 }
 
-static constexpr int ORB_L = 4, ORB_CB = 4, ORB_NW = 8;
+static constexpr int ORB_L = 4, ORB_CB = 4, ORB_NW = 8, ORB_QB = 2;
 
 int orbit_ensure_queries(OrbitIndex *o, int nq) {
     if ((size_t)nq <= o->cap_q) return 0;
@@ -2226,7 +2226,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
                  bool queries_prepared) {
     OrbitIndex *o = ix->orbit;
     const int nqblk = (nq + 31) / 32;
-    const int qpw = ORB_NW * 2;  // query blocks per workgroup (two per wave)
+    const int qpw = ORB_NW * ORB_QB;  // query blocks per workgroup (ORB_QB per wave)
     const int wgs = (nqblk + qpw - 1) / qpw;
     const int max_split = 32 / (2 * ORB_L);  // rescore: one list entry per lane of a half-wave
     // One 8-wave workgroup fills a CU (2 waves per SIMD), so a launch runs in rounds of n_cu workgroups of
@@ -2300,23 +2300,23 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         const size_t lds = 2 * ((size_t)ORB_CB * OS * 1024 + ORB_CB * 128);
         KTimer tm("nn_orbit", stream);
 #define ORB_PIPE(MD)                                                                                              \
-    hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, MD>), dim3(wgs, nsplit),              \
+    hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, ORB_QB, MD>), dim3(wgs, nsplit),              \
                        dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
                        (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id, o->red_end, o->d_bmask,                \
                        0x7fffffff, o->d_bmask0, MD == 0 ? flat_cnt : nullptr)
         if (!mix_full) ORB_PIPE(0);
         if (mix_full) {
-            const int qb_off = mix_full * ORB_NW * 2, q_off = qb_off * 32;  // query blocks / queries of part A
+            const int qb_off = mix_full * ORB_NW * ORB_QB, q_off = qb_off * 32;  // query blocks / queries of part A
             const size_t per_q = (size_t)nsplit * 2 * ORB_L;
             const size_t na = (size_t)std::min(nq, q_off) * per_q;
             TILER_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)o->key, 0x7f800000u, na, stream));  // +inf: empty
             TILER_HIP_CHECK(hipMemsetAsync(o->id, 0xff, na * sizeof(int), stream));
-            hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, 0>), dim3(mix_full, 1),
+            hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, ORB_QB, 0>), dim3(mix_full, 1),
                                dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,
                                (const half8 *)o->qfrag, nq, o->gblk, nsplit, o->key, o->id, o->red_end, o->d_bmask,
                                0x7fffffff, o->d_bmask0, nullptr);
             if (nq > q_off)
-                hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, 2, 0>),
+                hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, ORB_QB, 0>),
                                    dim3(wgs - mix_full, nsplit), dim3(ORB_NW * 64), lds, stream,
                                    (const half8 *)o->d_frag, o->d_seed, o->gblk,
                                    (const half8 *)o->qfrag + (size_t)qb_off * OS * 64, nq - q_off, bps, nsplit,

@@ -56,3 +56,25 @@ def test_scan_small_several_rounds_per_thread(gpu, oracle):
     data = rng.standard_normal((300000, 48)).astype(np.float32)
     q = data[rng.choice(300000, 9, replace=False)] + 0.05
     check_nn(gpu, oracle, data, q)
+
+
+@pytest.mark.parametrize("k", [1, 8])
+def test_scan_small_orbit_index(gpu, oracle, k):
+    """A mirror-orbit dataset (a tileset in its 4 orientations: PsyV rows that are exact signed permutations of their
+    group's base row, 20 % symmetric tiles with identical mirrors): batches of up to 4 queries take nn_scan_orbit_kernel,
+    which reads only the base rows and forms every member's values from them (larger ones the generic scan).  Batches of 1, 3, 16 and 64 queries (16 for k = 8),
+    frame tiles and perturbed candidate rows (exact ties among a tile's mirrors), both tie orders."""
+    from tiler_amd import synth
+    rng = np.random.default_rng(31 + k)
+    P, T = 16, 3000
+    pals = synth.palettes(rng, P)
+    tiles, thm, tvm = synth.tileset(rng, T)
+    ds = synth.ft_dataset_from_used(synth.used_one_palette(rng.integers(0, P, T).astype(np.int32), P), thm, tvm)
+    rows = gpu.psyv_batch(palpix=tiles, tile_of=ds.tile_of, palettes=pals, pal_of=ds.pal_of,
+                          flags_per=ds.psyv_flags, flags=1 | 2, gamma=-1, want32=True)[1]
+    with gpu.KDTree(rows) as kdt:
+        assert kdt.stats()["orbit_groups"] > 0
+    picks = rows[rng.choice(rows.shape[0], 64, replace=False)]
+    qs = np.concatenate([picks[:32], picks[32:] + rng.standard_normal((32, 192)).astype(np.float32) * 0.01])
+    for nq in ((1, 3, 16) if k == 8 else (1, 3, 16, 64)):
+        check_nn(gpu, oracle, rows, qs[:nq], k=k)

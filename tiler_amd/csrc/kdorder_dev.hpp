@@ -134,29 +134,86 @@ __device__ __forceinline__ float kd_root_box(const KdOrder &o, const float *__re
 // terms are then added in dimension order from registers -- the sequential sum without a memory round trip per term
 __device__ __forceinline__ float kd_root_box_wave(const KdOrder &o, const float *__restrict__ q, int lane) {
     float rb = 0.0f;
-    for (int d0 = 0; d0 < o.dd; d0 += 64) {
-        const int d = d0 + lane;
-        float t = 0.0f;
-        bool outside = false;
-        if (d < o.dd) {
-            const float v = q[d], lo = o.box_lo[d], hi = o.box_hi[d];
-            if (v < lo) {
-                t = lo - v;
-                outside = true;
-            } else if (v > hi) {
-                t = v - hi;
-                outside = true;
+    for (int d00 = 0; d00 < o.dd; d00 += 256) {  // 4 pieces of 64 dimensions: their loads in flight together
+        float t[4];
+        bool outside[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int d = d00 + 64 * u + lane;
+            t[u] = 0.0f;
+            outside[u] = false;
+            if (d < o.dd) {
+                const float v = q[d], lo = o.box_lo[d], hi = o.box_hi[d];
+                if (v < lo) {
+                    t[u] = lo - v;
+                    outside[u] = true;
+                } else if (v > hi) {
+                    t[u] = v - hi;
+                    outside[u] = true;
+                }
+                t[u] = t[u] * t[u];
             }
-            t = t * t;
         }
-        unsigned long long m = __ballot(outside);
-        while (m) {
-            const int src = __builtin_ctzll(m);
-            m &= m - 1;
-            rb = rb + __shfl(t, src, 64);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            unsigned long long m = __ballot(outside[u]);
+            while (m) {
+                const int src = __builtin_ctzll(m);
+                m &= m - 1;
+                rb = rb + __shfl(t[u], src, 64);
+            }
         }
     }
     return rb;
+}
+
+// kd_path_far_box by a half-wave (h = lane >> 5; p uniform over the half): lane l of the half loads path level l, all
+// levels in flight together, then every lane of the half adds the far-child terms in path order from shuffles --
+// the same sequential fp32 sum.  Path depth <= 32 (as kd_quad_path_ok).
+__device__ __forceinline__ float kd_half_path_far_box(const KdOrder &o, const float *__restrict__ q, int p,
+                                                      float root_box, int lane) {
+    const int l = lane & 31, base = lane & 32;
+    int S = 0, E = o.n, m = -1;
+    bool in_lo = false;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        if (E - S > o.bs) {
+            const int mm = S + ((E - S) >> 1);
+            const bool lo = p < mm;
+            if (i == l) {
+                m = mm;
+                in_lo = lo;
+            }
+            if (lo)
+                E = mm;
+            else
+                S = mm;
+        }
+    }
+    float term = 0.0f;
+    bool far = false;
+    if (m >= 0) {
+        const float qd = q[o.cd[m]];
+        const float cut_diff = qd - o.cv[m];
+        const bool lo_first = cut_diff < 0.0f;
+        if (in_lo != lo_first) {
+            float box_diff = lo_first ? o.lo[m] - qd : qd - o.hi[m];
+            if (box_diff < 0.0f) box_diff = 0.0f;
+            term = cut_diff * cut_diff - box_diff * box_diff;
+            far = true;
+        }
+    }
+    const unsigned fm = (unsigned)(__ballot(far) >> base);
+    float box = root_box, worst = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        const float t = __shfl(term, base + i, 64);
+        if ((fm >> i) & 1) {
+            box = box + t;
+            worst = fmaxf(worst, box);
+        }
+    }
+    return worst;
 }
 
 // The largest box distance ANN computes for a far child on the root-to-leaf path of leaf position p

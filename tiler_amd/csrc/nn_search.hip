@@ -1222,6 +1222,145 @@ __global__ __launch_bounds__(256) void nn_scan_small_kernel(RescoreArgs a, int n
     }
 }
 
+// The same scan on a mirror-orbit index (orbit.hip: every group holds a base row and up to 3 members that are exact
+// signed permutations of it, S_m c[i] = +-c[src_m(i)], inside each 64-value colour component): a workgroup of 4 waves
+// takes 64 groups per round, a wave 16 of them, one lane per (group, member slot); the wave's 16 base rows are staged
+// one component at a time in LDS (coalesced: a quarter of the bytes of reading every member's row) and each lane sums
+// the reference's sequential distance of its member, whose value of dimension i is +-base[src_m(i)] -- exactly the
+// member's own row value (orbit_eq_kernel checked it with float equality: a -0 / +0 difference squares to the same
+// term) -- so the lists are the row walk's bit for bit.
+template <int QN, int K>
+__global__ __launch_bounds__(256) void nn_scan_orbit_kernel(RescoreArgs a, const int *__restrict__ member, long G,
+                                                            const uint32_t *__restrict__ mtab, int nsplit,
+                                                            float *__restrict__ pd, int *__restrict__ pi) {
+    constexpr int D = 192, SB = 65;  // SB: LDS row stride
+    __shared__ __attribute__((aligned(16))) float sq[QN * D];
+    __shared__ float sb[4][16 * SB];
+    __shared__ uint32_t st[D];
+    __shared__ float rd[4][K];
+    __shared__ int ri[4][K];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lg = lane >> 2, x = lane & 3;
+    const int qg = blockIdx.y * QN;
+    const int nq = min(a.nq - qg, QN);
+    if (a.kd_count && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.kd_count = 0;  // the merge kernel appends
+    for (int i = tid; i < nq * D; i += 256) sq[i] = a.q[(long)qg * D + i];
+    for (int i = tid; i < D; i += 256) st[i] = mtab[i];
+    const long g0 = G * blockIdx.x / nsplit, g1 = G * (blockIdx.x + 1) / nsplit;
+    float bd[QN][K];
+    int bi[QN][K];
+#pragma unroll
+    for (int q = 0; q < QN; q++)
+#pragma unroll
+        for (int r = 0; r < K; r++) {
+            bd[q][r] = INFINITY;
+            bi[q][r] = 0x7fffffff;
+        }
+    float *wb = sb[w];
+    const float *row = wb + lg * SB;
+    for (long gb = g0; gb < g1; gb += 64) {  // uniform over the workgroup
+        const long g = gb + w * 16 + lg;
+        const bool valid = g < g1;
+        const int j = valid ? member[g * 4 + x] : -1;  // this lane's candidate (-1: empty slot)
+        const int base = __shfl(j, lane & ~3, 64);     // slot 0 of the group: its base row
+        float dist[QN];
+#pragma unroll
+        for (int q = 0; q < QN; q++) dist[q] = 0.0f;
+        for (int c = 0; c < 3; c++) {
+            __syncthreads();  // the previous component's reads are done (and, first, the query / table staging)
+#pragma unroll
+            for (int u = 0; u < 4; u++) {  // row r's 16 float4 pieces from 16 consecutive lanes
+                const int p = lane + 64 * u, r = p >> 4, k4 = p & 15;
+                const int br = __shfl(base, r * 4, 64);
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (br >= 0) v = reinterpret_cast<const float4 *>(a.rows + (long)br * D + c * 64)[k4];
+                float *d = wb + r * SB + 4 * k4;
+                d[0] = v.x;
+                d[1] = v.y;
+                d[2] = v.z;
+                d[3] = v.w;
+            }
+            __syncthreads();
+            const int sh = 7 * (x - 1);
+#pragma unroll 8
+            for (int i = 0; i < 64; i++) {
+                float v;
+                if (x == 0) {
+                    v = row[i];
+                } else {
+                    const uint32_t e = (st[c * 64 + i] >> sh) & 127;
+                    const float bv = row[e & 63];
+                    v = (e & 64) ? -bv : bv;
+                }
+#pragma unroll
+                for (int q = 0; q < QN; q++) {
+                    const float t = sq[q * D + c * 64 + i] - v;
+                    dist[q] = dist[q] + t * t;
+                }
+            }
+        }
+        if (j < 0) continue;
+#pragma unroll
+        for (int q = 0; q < QN; q++) {
+            if (q >= nq) break;
+            const float *qr = sq + q * D;
+            if (!kd_less(a.ko, qr, dist[q], j, bd[q][K - 1], bi[q][K - 1])) continue;
+            int p = K - 1;  // a lane's members do not arrive in index order: the insertion compares (distance, tie order)
+            while (p > 0 && kd_less(a.ko, qr, dist[q], j, bd[q][p - 1], bi[q][p - 1])) {
+                bd[q][p] = bd[q][p - 1];
+                bi[q][p] = bi[q][p - 1];
+                p--;
+            }
+            bd[q][p] = dist[q];
+            bi[q][p] = j;
+        }
+    }
+    // per query: the workgroup's K best, K rounds of (distance, tie order) argmin over the lanes' sorted lists
+    for (int q = 0; q < nq; q++) {
+        const float *qr = sq + q * D;
+        int ptr = 0;
+        for (int r = 0; r < K; r++) {
+            float v = INFINITY;
+            int vi = 0x7fffffff;
+#pragma unroll
+            for (int y = 0; y < K; y++)
+                if (y == ptr) {
+                    v = bd[q][y];
+                    vi = bi[q][y];
+                }
+            float mv = v;
+            int mi = vi;
+            kd_argmin<64>(a.ko, qr, mv, mi);
+            if (lane == 0) {
+                rd[w][r] = mv;
+                ri[w][r] = mi;
+            }
+            if (vi == mi && mi != 0x7fffffff) ptr++;  // this wave's winner leaves its list
+        }
+        __syncthreads();
+        if (w == 0) {  // merge the 4 waves' sorted K-lists: lane l < 4 holds wave l's list head
+            int hp = 0;
+            for (int r = 0; r < K; r++) {
+                float v = INFINITY;
+                int vi = 0x7fffffff;
+                if (lane < 4 && hp < K) {
+                    v = rd[lane][hp];
+                    vi = ri[lane][hp];
+                }
+                float mv = v;
+                int mi = vi;
+                kd_argmin<64>(a.ko, qr, mv, mi);
+                if (lane < 4 && vi == mi && mi != 0x7fffffff) hp++;
+                if (lane == 0) {
+                    const long o = ((long)(qg + q) * nsplit + blockIdx.x) * K + r;
+                    pd[o] = mv;
+                    pi[o] = mi;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // one wave per query: the k best of its nsplit * K partials (each split's list sorted) -> out, tilemap item
 template <int K>
 __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int nsplit, const float *__restrict__ pd,
@@ -1236,6 +1375,29 @@ __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int ns
         bd[r] = INFINITY;
         bi[r] = 0x7fffffff;
     }
+    if constexpr (K == 1) {  // one entry per split: 16 loads in flight per lane, then the running minimum
+        constexpr int U = 16;
+        for (int sp0 = lane; sp0 < nsplit; sp0 += 64 * U) {
+            float v[U];
+            int vi[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int sp = sp0 + 64 * u;
+                v[u] = INFINITY;
+                vi[u] = 0x7fffffff;
+                if (sp < nsplit) {
+                    v[u] = pd[(long)q * nsplit + sp];
+                    vi[u] = pi[(long)q * nsplit + sp];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (vi[u] != 0x7fffffff && kd_less(a.ko, qr, v[u], vi[u], bd[0], bi[0])) {
+                    bd[0] = v[u];
+                    bi[0] = vi[u];
+                }
+        }
+    } else
     for (int sp = lane; sp < nsplit; sp += 64)
         for (int r = 0; r < K; r++) {
             const float v = pd[((long)q * nsplit + sp) * K + r];
@@ -1281,19 +1443,19 @@ __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int ns
     }
     // ANN's pruning along every result's path (kd_verify_kernel's test): vouched for, or listed for the exact replay.
     // Saves the root-box and verify launches of a coalesced per-tile batch: the wave forms the root box distance
-    // from registers, then lane j walks result j's path.
+    // from registers, then each half-wave walks one result's path, one level per lane (two results per pass).
     if (a.kd_count) {
         const KdOrder o = *a.ko;
         if (first >= 0 && Dk < FLT_MAX) {  // uniform
             const float rb = kd_root_box_wave(o, qr, lane);
             bool vouch = true;
-            if (lane < a.k) {
-                if ((unsigned)my_c >= (unsigned)o.n) {
-                    vouch = false;
-                } else {
-                    const float fb = kd_path_far_box(o, qr, o.pos[my_c], rb);
-                    vouch = fb < Dk || (fb <= Dk && my_d == Dk);
-                }
+            for (int r0 = 0; r0 < a.k; r0 += 2) {
+                const int r = r0 + (lane >> 5);
+                const int c = __shfl(my_c, r & 63, 64);
+                const float dr = __shfl(my_d, r & 63, 64);
+                const bool valid = r < a.k && (unsigned)c < (unsigned)o.n;
+                const float fb = kd_half_path_far_box(o, qr, valid ? o.pos[c] : 0, rb, lane);
+                if (r < a.k) vouch = vouch && valid && (fb < Dk || (fb <= Dk && dr == Dk));
             }
             const bool all = __all(vouch);
             if (lane == 0 && (!all || a.force_replay)) a.kd_list[atomicAdd(a.kd_count, 1)] = q;
@@ -1747,7 +1909,11 @@ static bool scan_small_takes(const NNIndex *ix, int nq, int k) {
             (k <= 8 && nq <= g_scan_max8.load(std::memory_order_relaxed)));
 }
 static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t stream) {
-    const int nsplit = (int)std::max<long>(1, std::min<long>(1024, ((long)ix->n + 255) / 256));
+    const OrbitIndex *o = ix->orbit;
+    // mirror orbits, groups of <= 4 queries: base rows only (nn_scan_orbit_kernel; 16-query groups measured slower)
+    const bool orb = o && o->d_mtab && o->G > 0 && ix->d == 192 && nq <= 4;
+    const int nsplit = orb ? (int)std::max<long>(1, std::min<long>(1024, ((long)o->G + 63) / 64))
+                           : (int)std::max<long>(1, std::min<long>(1024, ((long)ix->n + 255) / 256));
     const int K = k == 1 ? 1 : 8;
     if (ensure_scratch(ix, nq, (long)nq * nsplit * K)) return -1;
     SearchScratch &s = ix->scratch;
@@ -1760,7 +1926,22 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
     auto scan = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, ra, nsplit, s.key, s.idx);
     };
-    if (K == 1) {
+    auto scan_o = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, ra, (const int *)o->d_member, (long)o->G,
+                           (const uint32_t *)o->d_mtab, nsplit, s.key, s.idx);
+    };
+    if (orb) {
+        if (K == 1) {
+            if (qn == 1) scan_o(nn_scan_orbit_kernel<1, 1>);
+            else if (qn == 4) scan_o(nn_scan_orbit_kernel<4, 1>);
+            else scan_o(nn_scan_orbit_kernel<SCAN_QN1, 1>);
+        } else {
+            if (qn == 1) scan_o(nn_scan_orbit_kernel<1, 8>);
+            else scan_o(nn_scan_orbit_kernel<SCAN_QN8, 8>);
+        }
+        hipLaunchKernelGGL(K == 1 ? nn_scan_merge_kernel<1> : nn_scan_merge_kernel<8>, dim3(nq), dim3(64), 0, stream, ra,
+                           nsplit, (const float *)s.key, (const int *)s.idx);
+    } else if (K == 1) {
         if (qn == 1) scan(nn_scan_small_kernel<1, 1>);
         else if (qn == 4) scan(nn_scan_small_kernel<4, 1>);
         else scan(nn_scan_small_kernel<SCAN_QN1, 1>);

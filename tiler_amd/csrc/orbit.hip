@@ -2037,6 +2037,7 @@ void orbit_destroy(OrbitIndex *o) {
     hipFree(o->d_gorder);
     hipFree(o->d_grp_of);
     hipFree(o->d_map);
+    hipFree(o->d_mtab);
     hipFree(o->qfrag);
     hipFree(o->qstat);
     hipFree(o->pair_cnt);
@@ -2101,6 +2102,25 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     o->G = (int)G;
     o->gblk = (int)((G + 31) / 32);
     o->d_map = d_map;
+    {  // the mirrors as (column in the component, sign) for the small-batch scan (nn_scan_orbit_kernel); build_map
+       // already requires each mirror to stay inside its colour component -- if not, the scan keeps the row walk
+        uint32_t mtab[OD];
+        bool ok = true;
+        for (int i = 0; i < OD; i++) {
+            uint32_t w = 0;
+            for (int m = 0; m < 3; m++) {
+                const int src = hmap.msrc[m][i], c0 = (i / 64) * 64;
+                ok = ok && src >= c0 && src < c0 + 64 && (hmap.msgn[m][i] == 1.0f || hmap.msgn[m][i] == -1.0f);
+                w |= (uint32_t)(((src - c0) & 63) | (hmap.msgn[m][i] < 0.0f ? 64 : 0)) << (7 * m);
+            }
+            mtab[i] = w;
+        }
+        if (ok) {
+            TILER_HIP_CHECK(hipMalloc((void **)&o->d_mtab, sizeof(mtab)));
+            TILER_HIP_CHECK(hipMemcpyAsync(o->d_mtab, mtab, sizeof(mtab), hipMemcpyHostToDevice, stream));
+            TILER_HIP_CHECK(hipStreamSynchronize(stream));  // mtab is this block's
+        }
+    }
     OrbitDsStat *d_ds = nullptr;
     TILER_HIP_CHECK(hipMalloc((void **)&o->d_member, G * 4 * sizeof(int)));
     TILER_HIP_CHECK(hipMemcpyAsync(o->d_member, member.data(), G * 4 * sizeof(int), hipMemcpyHostToDevice, stream));

@@ -47,6 +47,8 @@ struct OrbitIndex {
     GroupOrder *d_gorder = nullptr;  // [G] (kd tie order only)
     int *d_grp_of = nullptr;      // [n] candidate -> g * 4 + slot (kd tie order only; -1: not in a group)
     void *d_map = nullptr;        // OrbitMap
+    uint32_t *d_mtab = nullptr;   // [192] mirror m = 1..3 of dimension i in bits 7(m-1)..: its source column inside i's
+                                  // 64-value component (6 bits) and a sign bit (the small-batch orbit scan)
     // mirror-symmetric groups first (orbit_build): blocks [0, red_end) may have isotypic blocks of c' that are zero
     // for every group in them (bit x of d_bmask[blk] clear), whose k-steps the shortlist skips; the rest are full
     int red_end = 0;

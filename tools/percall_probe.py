@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--lib", default="")
     ap.add_argument("--queries", type=int, default=8192)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--scan-only", action="store_true", help="only the scan-kernel timings on the C3 handle")
     args = ap.parse_args()
     import tiler_amd._lib as L
     if args.lib:
@@ -41,7 +42,8 @@ def main():
     qd = np.ascontiguousarray(qd, np.float32)
     vp = ctypes.c_void_p
     out = {"tag": args.tag}
-    for name, data in (("c3_262144", rows), ("small_12000", rows[rng.choice(rows.shape[0], 12000, replace=False)])):
+    for name, data in (() if args.scan_only else
+                       (("c3_262144", rows), ("small_12000", rows[rng.choice(rows.shape[0], 12000, replace=False)]))):
         with tiler_amd.KDTree(data) as kdt:
             bi, be = kdt.search_batch(qd)
             n_idx = np.zeros(qd.shape[0], np.int32)

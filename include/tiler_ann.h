@@ -20,10 +20,10 @@
  *   - split = TILER_SPLIT_INDEX_ORDER (100): no tree, equal distances resolve to the lowest index;
  *     the other ANN split rules (1..5, never used by the reference) are rejected;
  *   - eps > 0 is accepted and ignored: the exact answer satisfies every eps bound;
- *   - ann_kdtree_pri_search returns ann_kdtree_search's answer: the same exact minimum distance, but among
- *     EQUAL distances annkSearch's first-found candidate, not annkPriSearch's (ANN's priority search visits the
- *     leaves by increasing box distance, so its tie order can differ).  The reference declares it
- *     (extern.pas:66) and never calls it; its tie order is not reproduced;
+ *   - ann_kdtree_pri_search returns annkPriSearch's answer (the priority search replayed on the GPU: its leaf
+ *     visit order by box distance, hence its own choice among equal distances, and its (1 + eps)^2 termination,
+ *     so eps > 0 gives ANN's approximate answer there); the reference declares it (extern.pas:66) and never
+ *     calls it;
  *   - the dataset rows are copied to device memory at create (ANN borrows pa until destroy);
  *   - no process abort: errors return -1 (or NULL) and tiler_last_error() explains;
  *   - every entry point is thread-safe.  Concurrent single-query calls on one handle (ann_kdtree_search /
@@ -64,6 +64,8 @@ ann_kdtree *ann_kdtree_create_dev_ex(const float *d_rows, int n, int dd, int bs,
 int ann_kdtree_search_batch(ann_kdtree *akd, const float *q, int nq, float eps, int *idx, float *err);
 /* k results per query, ascending by (err, index): idxs[nq][k], errs[nq][k] (missing: -1 / FLT_MAX). k <= 32. */
 int ann_kdtree_search_multi_batch(ann_kdtree *akd, const float *q, int nq, int k, float eps, int *idxs, float *errs);
+/* nq ann_kdtree_pri_search calls at once (host arrays; idx / err [nq]) */
+int ann_kdtree_pri_search_batch(ann_kdtree *akd, const float *q, int nq, float eps, int *idx, float *err);
 /* Same with device-resident buffers (HBM) on a HIP stream (NULL = default stream); asynchronous. */
 int ann_kdtree_search_batch_dev(ann_kdtree *akd, const float *d_q, int nq, int k, int *d_idx, float *d_err,
                                 void *stream);

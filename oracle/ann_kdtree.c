@@ -355,3 +355,117 @@ long or_kdtree_search_multi_batch(void *p, const float *q, int nq, int k, int *i
 long or_kdtree_search_batch(void *p, const float *q, int nq, int *idx, float *err, int threads) {
     return or_kdtree_search_multi_batch(p, q, nq, 1, idx, err, threads);
 }
+
+/* annkPriSearch (ANN.dll 0x1800121a0; ann_kdtree_pri_search 0x180003ef0 calls it with k = 1, the caller's eps):
+ * the root enters ANNpr_queue (a 1-based binary min-heap, pr_queue(n_pts) entries) with annBoxDistance; while it is
+ * non-empty the minimum is extracted (inlined at 0x1800122d0) and, unless key * (1 + eps)^2 >= the current best
+ * (max_key), ANNkd_split::ann_pri_search (0x180012580) descends on q's side with the same box, pushing each far child
+ * with (cut_diff^2 - box_diff^2) + box, box_diff = maxss(bound difference, 0); ANNkd_leaf::ann_pri_search
+ * (0x180012670) scans the bucket exactly as annkSearch's leaf does.  k = 1. */
+typedef struct {
+    float key;
+    int node;
+} pq_entry;
+
+/* ANNpr_queue::insert (0x180008fc0): sift up while the parent's key > kv */
+static void pq_insert(pq_entry *pq, int *n, float kv, int node) {
+    int r = ++*n;
+    while (r > 1) {
+        const int p = r / 2;
+        if (pq[p].key <= kv) break;
+        pq[r] = pq[p];
+        r = p;
+    }
+    pq[r].key = kv;
+    pq[r].node = node;
+}
+
+/* ANNpr_queue::extr_min (0x1800122d0-0x180012364) */
+static pq_entry pq_extr_min(pq_entry *pq, int *n) {
+    const pq_entry top = pq[1];
+    const float kn = pq[*n].key;
+    (*n)--;
+    int p = 1, r = 2;
+    while (r <= *n) {
+        if (r < *n && pq[r].key > pq[r + 1].key) r++;
+        if (kn <= pq[r].key) break;
+        pq[p] = pq[r];
+        p = r;
+        r = p << 1;
+    }
+    pq[p] = pq[*n + 1];
+    return top;
+}
+
+static int kd_pri_nn(const kd_tree *t, const float *q, float eps, float *err, pq_entry *pq) {
+    kd_query s;
+    s.t = t;
+    s.q = q;
+    s.k = 1;
+    s.cnt = 0;
+    s.visited = 0;
+    if (t->n > 0) {
+        float max_err = eps + 1.0f;
+        max_err = max_err * max_err;
+        float bd = 0.0f; /* annBoxDistance */
+        for (int dim = 0; dim < t->d; dim++) {
+            float v = 0.0f;
+            if (q[dim] < t->box_lo[dim]) v = t->box_lo[dim] - q[dim];
+            else if (q[dim] > t->box_hi[dim]) v = q[dim] - t->box_hi[dim];
+            bd = bd + v * v;
+        }
+        int hn = 0;
+        pq_insert(pq, &hn, bd, 0);
+        while (hn > 0) {
+            const pq_entry top = pq_extr_min(pq, &hn);
+            if (top.key * max_err >= kd_max_key(&s)) break;
+            const float box = top.key;
+            int id = top.node;
+            for (;;) {
+                const kd_node *nd = &t->nodes[id];
+                if (nd->cut_dim < 0) { /* ANNkd_leaf::ann_pri_search */
+                    float min_dist = kd_max_key(&s);
+                    for (int b = 0; b < nd->child[1]; b++) {
+                        const int j = t->pidx[nd->child[0] + b];
+                        const float *p = t->data + (size_t)j * t->d;
+                        float dist = 0.0f;
+                        int i;
+                        for (i = 0; i < t->d; i++) {
+                            const float tt = q[i] - p[i];
+                            dist = dist + tt * tt;
+                            if (dist > min_dist) break;
+                        }
+                        if (i >= t->d) {
+                            kd_insert(&s, dist, j);
+                            min_dist = kd_max_key(&s);
+                        }
+                    }
+                    break;
+                }
+                const float qd = q[nd->cut_dim];
+                const float cut_diff = qd - nd->cut_val;
+                if (cut_diff < 0) {
+                    float box_diff = nd->lo_bnd - qd;
+                    box_diff = box_diff > 0.0f ? box_diff : 0.0f; /* maxss */
+                    pq_insert(pq, &hn, (cut_diff * cut_diff - box_diff * box_diff) + box, nd->child[1]);
+                    id = nd->child[0];
+                } else {
+                    float box_diff = qd - nd->hi_bnd;
+                    box_diff = box_diff > 0.0f ? box_diff : 0.0f;
+                    pq_insert(pq, &hn, (cut_diff * cut_diff - box_diff * box_diff) + box, nd->child[0]);
+                    id = nd->child[1];
+                }
+            }
+        }
+    }
+    if (err) *err = s.cnt ? s.mk[0] : FLT_MAX;
+    return s.cnt ? s.mi[0] : -1;
+}
+
+/* nq ann_kdtree_pri_search calls (single thread): idx/err [nq] */
+void or_kdtree_pri_search_batch(void *p, const float *q, int nq, float eps, int *idx, float *err) {
+    const kd_tree *t = (const kd_tree *)p;
+    pq_entry *pq = (pq_entry *)malloc(((size_t)t->n + 2) * sizeof(pq_entry));
+    for (int i = 0; i < nq; i++) idx[i] = kd_pri_nn(t, q + (size_t)i * t->d, eps, err + i, pq);
+    free(pq);
+}

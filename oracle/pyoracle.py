@@ -128,6 +128,18 @@ class KDTree:
         self.visited += f(self.h, _p(qs), qs.shape[0], k, _p(idx), _p(err), threads or _threads())
         return (idx[:, 0], err[:, 0]) if k == 1 else (idx, err)
 
+    def pri_search_batch(self, qs, eps: float = 0.0):
+        """annkPriSearch per query (k = 1, ann_kdtree_pri_search): (idx[nq], err[nq])"""
+        qs = np.ascontiguousarray(qs, np.float32).reshape(-1, self.data.shape[1])
+        idx = np.zeros(qs.shape[0], np.int32)
+        err = np.zeros(qs.shape[0], np.float32)
+        f = lib().or_kdtree_pri_search_batch
+        f.restype = None
+        f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p,
+                      ctypes.c_void_p]
+        f(self.h, _p(qs), qs.shape[0], eps, _p(idx), _p(err))
+        return idx, err
+
     def splits(self):
         """split nodes by split position m: (cut_dim, cut_val, lo_bnd, hi_bnd), arrays [n] (index 0 unused)"""
         n = self.data.shape[0]

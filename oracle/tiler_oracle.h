@@ -59,6 +59,7 @@ void *or_kdtree_build_bs(const float *data, int n, int d, int bs);
 void or_kdtree_free(void *t);
 long or_kdtree_search_batch(void *t, const float *q, int nq, int *idx, float *err, int threads);
 long or_kdtree_search_multi_batch(void *t, const float *q, int nq, int k, int *idx, float *err, int threads);
+void or_kdtree_pri_search_batch(void *t, const float *q, int nq, float eps, int *idx, float *err);
 void or_kdtree_positions(void *t, int *pos);
 void or_kdtree_splits(void *t, int *cd, float *cv, float *lo, float *hi);
 

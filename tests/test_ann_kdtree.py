@@ -207,3 +207,115 @@ def test_kd_result_is_first_in_dfs_order(oracle, name, k):
             assert np.array_equal(ke[qi].view(np.uint32), d[want].view(np.uint32))
     assert vouched == len(qs)  # these exactly representable datasets never need the replay
     assert ties >= 3  # and they do exercise the tie rule
+
+
+def py_pri_search(data, pidx, cd, cv, lo_b, hi_b, bs, q, eps):
+    """annkPriSearch (ANN.dll 0x1800121a0, k = 1) in Python on the implicit tree of np_kdtree (node = leaf positions
+    [s, e), split at m = s + (e - s) // 2), with ANNpr_queue's own binary heap (its tie behaviour is part of the
+    order), fp32 op by op -- independent of oracle/ann_kdtree.c's explicit-node restatement."""
+    f = np.float32
+    n, dd = data.shape
+    max_err = f(f(eps) + f(1))
+    max_err = f(max_err * max_err)
+    lo, hi = data.min(0), data.max(0)
+    box = f(0)
+    for d in range(dd):
+        if q[d] < lo[d]:
+            t = f(lo[d] - q[d])
+            box = f(box + f(t * t))
+        elif q[d] > hi[d]:
+            t = f(q[d] - hi[d])
+            box = f(box + f(t * t))
+    pq = [None]  # 1-based
+
+    def insert(kv, node):
+        pq.append(None)
+        r = len(pq) - 1
+        while r > 1:
+            p = r // 2
+            if pq[p][0] <= kv:
+                break
+            pq[r] = pq[p]
+            r = p
+        pq[r] = (kv, node)
+
+    def extr_min():
+        top = pq[1]
+        kn = pq[-1][0]
+        last = pq[-1]
+        nn = len(pq) - 2
+        p, r = 1, 2
+        while r <= nn:
+            if r < nn and pq[r][0] > pq[r + 1][0]:
+                r += 1
+            if kn <= pq[r][0]:
+                break
+            pq[p] = pq[r]
+            p, r = r, 2 * r
+        pq[p] = last
+        pq.pop()
+        return top
+
+    best, best_i = None, -1
+    insert(box, (0, n))
+    while len(pq) > 1:
+        kv, (s, e) = extr_min()
+        if f(kv * max_err) >= (best if best is not None else f(np.finfo(np.float32).max)):
+            break
+        while e - s > bs:
+            m = s + (e - s) // 2
+            qd = f(q[cd[m]])
+            cut = f(qd - cv[m])
+            if cut < 0:
+                bd = f(lo_b[m] - qd)
+                bd = bd if bd > 0 else f(0)
+                insert(f(f(f(cut * cut) - f(bd * bd)) + kv), (m, e))
+                e = m
+            else:
+                bd = f(qd - hi_b[m])
+                bd = bd if bd > 0 else f(0)
+                insert(f(f(f(cut * cut) - f(bd * bd)) + kv), (s, m))
+                s = m
+        min_dist = best if best is not None else f(np.finfo(np.float32).max)
+        for lp in range(s, e):
+            j = int(pidx[lp])
+            dist = f(0)
+            done = True
+            for d in range(dd):
+                t = f(q[d] - data[j, d])
+                dist = f(dist + f(t * t))
+                if dist > min_dist:
+                    done = False
+                    break
+            if done:
+                if best is None or best > dist:
+                    best, best_i = dist, j
+                min_dist = best
+    return best_i, (best if best is not None else f(np.finfo(np.float32).max))
+
+
+@pytest.mark.parametrize("name", ["dup", "ints", "flat"])
+@pytest.mark.parametrize("bs", [1, 3])
+@pytest.mark.parametrize("eps", [0.0, 0.5])
+def test_oracle_pri_search_matches_python_restatement(oracle, name, bs, eps):
+    """or_kdtree_pri_search_batch (ann_kdtree_pri_search's checker) == the Python restatement above, index and
+    distance bits; with eps = 0 the distance is the exact minimum (only the choice among ties is the search's)."""
+    data = _datasets()[name]
+    rng = np.random.default_rng(17)
+    n = data.shape[0]
+    qs = np.concatenate([data[rng.integers(0, n, 30)], data[rng.integers(0, n, 30)] + rng.integers(-1, 2, (30, data.shape[1])),
+                         rng.normal(0, 2, (30, data.shape[1]))]).astype(np.float32)
+    pidx, cd, cv, lo_b, hi_b = np_kdtree(data, bs)
+    kd = oracle.KDTree(data, bs=bs)
+    oi, oe = kd.pri_search_batch(qs, eps)
+    si, se = kd.search_batch(qs)
+    kd.close()
+    differ = 0
+    for qi, q in enumerate(qs):
+        pi_, pe_ = py_pri_search(data, pidx, cd, cv, lo_b, hi_b, bs, q, eps)
+        assert oi[qi] == pi_ and np.float32(oe[qi]).view(np.uint32) == np.float32(pe_).view(np.uint32), qi
+        if eps == 0.0:
+            assert oe[qi] == exact_dists(data, q).min()
+            differ += int(oi[qi] != si[qi])
+    if eps == 0.0 and name == "ints":
+        assert differ > 0  # the priority search's tie order is its own (ann_kdtree_search would answer otherwise)

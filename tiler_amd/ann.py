@@ -87,6 +87,14 @@ class KDTree:
         check(idx if idx >= 0 or self.n == 0 else -1, "ann_kdtree_search")
         return int(idx), float(err[0])
 
+    def pri_search(self, q, eps: float = 0.0):
+        """ann_kdtree_pri_search (extern.pas:66): annkPriSearch's answer, its own tie order"""
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        err = np.zeros(1, np.float32)
+        idx = self._lib.ann_kdtree_pri_search(self.handle, _ptr(q), eps, _ptr(err))
+        check(idx if idx >= 0 or self.n == 0 else -1, "ann_kdtree_pri_search")
+        return int(idx), float(err[0])
+
     def search_multi(self, q, cnt: int, eps: float = 0.0):
         q = np.ascontiguousarray(q, dtype=np.float32)
         idxs = np.zeros(cnt, np.int32)
@@ -104,6 +112,15 @@ class KDTree:
         check(self._lib.ann_kdtree_search_multi_batch(self.handle, _ptr(qs), nq, k, eps, _ptr(idx), _ptr(err)),
               "ann_kdtree_search_multi_batch")
         return (idx[:, 0], err[:, 0]) if k == 1 else (idx, err)
+
+    def pri_search_batch(self, qs, eps: float = 0.0):
+        qs = np.ascontiguousarray(qs, dtype=np.float32).reshape(-1, self.dd)
+        nq = qs.shape[0]
+        idx = np.zeros(nq, np.int32)
+        err = np.zeros(nq, np.float32)
+        check(self._lib.ann_kdtree_pri_search_batch(self.handle, _ptr(qs), nq, eps, _ptr(idx), _ptr(err)),
+              "ann_kdtree_pri_search_batch")
+        return idx, err
 
     def search_batch_dev(self, q_ptr: int, nq: int, k: int, idx_ptr: int, err_ptr: int, stream: int = 0):
         check(self._lib.ann_kdtree_search_batch_dev(self.handle, ctypes.c_void_p(q_ptr), nq, k,

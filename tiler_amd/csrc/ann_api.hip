@@ -314,6 +314,8 @@ struct ann_kdtree {
     int32_t *d_rgb = nullptr, *d_mt = nullptr, *d_mp = nullptr;
     uint8_t *d_mh = nullptr, *d_mv = nullptr;
     size_t cap_ft = 0;
+    void *d_pri = nullptr;        // kd_pri_search heap scratch (ann_kdtree_pri_search)
+    size_t cap_pri = 0;
     PrepScratch *prep = nullptr;  // tiler_prepare_frame_tiling_dev scratch (on the global dataset's handle)
     int dev = 0;                  // the device the handle's index, stream and buffers live on
     hipEvent_t maps_ev = nullptr; // recorded after tiler_prepare_frame_tiling_dev wrote the TRTo maps (on its stream)
@@ -500,6 +502,7 @@ static void handle_free(ann_kdtree *t) {
     (void)hipFree(t->d_mp);
     (void)hipFree(t->d_mh);
     (void)hipFree(t->d_mv);
+    (void)hipFree(t->d_pri);
     if (t->prep) {
         prep_scratch_free(t->prep);
         delete t->prep;
@@ -847,7 +850,57 @@ int ann_kdtree_search(ann_kdtree *t, float *q, float eps, float *err) {
     return idx;
 }
 
-int ann_kdtree_pri_search(ann_kdtree *t, float *q, float eps, float *err) { return ann_kdtree_search(t, q, eps, err); }
+// annkPriSearch's answer (ann_kdtree_pri_search, extern.pas:66 -> ANN.dll 0x180003ef0, which calls annkPriSearch
+// 0x1800121a0 with k = 1 and the caller's eps): the priority search replayed on the GPU (kd_pri_search), its own tie
+// order and its (1 + eps)^2 termination included.  Queries in chunks that keep the heap scratch <= 1 GiB.  A handle
+// without a tree (TILER_SPLIT_INDEX_ORDER) answers as ann_kdtree_search does.
+int ann_kdtree_pri_search_batch(ann_kdtree *t, const float *q, int nq, float eps, int *idx, float *err) {
+    if (!t || !t->ix || nq < 0 || (nq > 0 && (!q || !idx || !err))) {
+        set_error("ann_kdtree_pri_search: invalid arguments");
+        return -1;
+    }
+    if (!ensure_init()) return -1;
+    if (!t->ix->kd) return ann_kdtree_search_multi_batch(t, q, nq, 1, eps, idx, err);
+    DevScope ds(t->dev);
+    NNIndex *ix = t->ix;
+    std::lock_guard<std::mutex> lk(ix->mu);
+    if (nq == 0) return 0;
+    if (ix->n == 0) {
+        for (int i = 0; i < nq; i++) {
+            idx[i] = -1;
+            err[i] = FLT_MAX;
+        }
+        return 0;
+    }
+    const size_t per = kd_pri_heap_bytes(ix->kd, 1);
+    const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)nq, ((size_t)1 << 30) / per));
+    if (ensure_io(t, chunk, ix->d, 1)) return -1;
+    if (per * chunk > t->cap_pri) {
+        (void)hipFree(t->d_pri);
+        t->d_pri = nullptr;
+        t->cap_pri = 0;
+        TILER_HIP_CHECK(hipMalloc(&t->d_pri, per * chunk));
+        t->cap_pri = per * chunk;
+    }
+    for (int q0 = 0; q0 < nq; q0 += chunk) {
+        const int c = std::min(chunk, nq - q0);
+        TILER_HIP_CHECK(hipMemcpyAsync(t->d_q, q + (size_t)q0 * ix->d, (size_t)c * ix->d * sizeof(float),
+                                       hipMemcpyHostToDevice, t->stream));
+        if (kd_pri_search(ix->kd, ix->d_rows, t->d_q, c, eps, t->d_pri, t->d_idx, t->d_err, t->stream)) return -1;
+        TILER_HIP_CHECK(hipMemcpyAsync(idx + q0, t->d_idx, (size_t)c * sizeof(int), hipMemcpyDeviceToHost, t->stream));
+        TILER_HIP_CHECK(hipMemcpyAsync(err + q0, t->d_err, (size_t)c * sizeof(float), hipMemcpyDeviceToHost, t->stream));
+        TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
+    }
+    return 0;
+}
+
+int ann_kdtree_pri_search(ann_kdtree *t, float *q, float eps, float *err) {
+    int idx = -1;
+    float e = 0.0f;
+    if (ann_kdtree_pri_search_batch(t, q, 1, eps, &idx, &e)) return -1;
+    if (err) *err = e;
+    return idx;
+}
 
 int ann_kdtree_search_multi(ann_kdtree *t, int *idxs, float *errs, int cnt, float *q, float eps) {
     (void)eps;

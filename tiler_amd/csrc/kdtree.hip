@@ -1115,6 +1115,116 @@ __global__ __launch_bounds__(64) void kd_replay_kernel(KdOrder o, KdFixArgs a) {
     }
 }
 
+// annkPriSearch replayed exactly (ANN.dll 0x1800121a0-0x18001257f, ANNkd_split::ann_pri_search 0x180012580,
+// ANNkd_leaf::ann_pri_search 0x180012670, ANNpr_queue::insert 0x180008fc0; extr_min inlined at 0x1800122d0): the
+// root enters a binary min-heap with its box distance; each extracted node whose key * (1 + eps)^2 is below the
+// current best descends to a leaf on q's side, pushing every far child with key (cut_diff^2 - box_diff^2) + box
+// (box_diff = maxss(bound difference, 0)); the leaf scan and the k = 1 ANNmin_k insertion are annkSearch's.  One
+// thread per query; the heap lives in global scratch (n + 1 entries per query, ANN's pr_queue(n_pts) size).
+struct PriEntry {
+    float key;
+    int s, e;  // the node: leaf positions [s, e)
+};
+
+__global__ __launch_bounds__(64) void kd_pri_kernel(KdOrder o, const float *__restrict__ rows,
+                                                    const float *__restrict__ q, int nq, float eps,
+                                                    PriEntry *__restrict__ heap, int *__restrict__ out_idx,
+                                                    float *__restrict__ out_err) {
+    const int qi = blockIdx.x * 64 + threadIdx.x;
+    if (qi >= nq) return;
+    PriEntry *pq = heap + (size_t)qi * ((size_t)o.n + 1);  // pq[1..n]
+    const float *qr = q + (long)qi * o.dd;
+    float max_err = eps + 1.0f;
+    max_err = max_err * max_err;
+    int hn = 0;
+    auto insert = [&](float kv, int s, int e) {  // ANNpr_queue::insert: sift up while the parent's key > kv
+        int r = ++hn;
+        while (r > 1) {
+            const int p = r >> 1;
+            if (pq[p].key <= kv) break;
+            pq[r] = pq[p];
+            r = p;
+        }
+        pq[r] = PriEntry{kv, s, e};
+    };
+    int cnt = 0, best_i = -1;
+    float best = FLT_MAX;
+    insert(kd_root_box(o, qr), 0, o.n);
+    while (hn > 0) {
+        const PriEntry top = pq[1];  // extr_min
+        const float kn = pq[hn].key;
+        hn--;
+        int p = 1, r = 2;
+        while (r <= hn) {
+            if (r < hn && pq[r].key > pq[r + 1].key) r++;
+            if (kn <= pq[r].key) break;
+            pq[p] = pq[r];
+            p = r;
+            r = p << 1;
+        }
+        pq[p] = pq[hn + 1];
+        if (top.key * max_err >= (cnt ? best : FLT_MAX)) break;
+        const float box = top.key;
+        int s = top.s, e = top.e;
+        while (e - s > o.bs) {  // ANNkd_split::ann_pri_search: push the far child, continue on q's side (same box)
+            const int m = s + ((e - s) >> 1);
+            const float qd = qr[o.cd[m]];
+            const float cut_diff = qd - o.cv[m];
+            if (cut_diff < 0.0f) {
+                float box_diff = o.lo[m] - qd;
+                box_diff = box_diff > 0.0f ? box_diff : 0.0f;  // maxss(box_diff, 0)
+                insert((cut_diff * cut_diff - box_diff * box_diff) + box, m, e);
+                e = m;
+            } else {
+                float box_diff = qd - o.hi[m];
+                box_diff = box_diff > 0.0f ? box_diff : 0.0f;
+                insert((cut_diff * cut_diff - box_diff * box_diff) + box, s, m);
+                s = m;
+            }
+        }
+        float min_dist = cnt ? best : FLT_MAX;  // ANNkd_leaf::ann_pri_search
+        for (int lp = s; lp < e; lp++) {
+            const int pt = o.pidx[lp];
+            const float *pp = rows + (long)pt * o.dd;
+            float dist = 0.0f;
+            int d;
+            for (d = 0; d < o.dd; d++) {
+                const float t = qr[d] - pp[d];
+                dist = dist + t * t;
+                if (dist > min_dist) break;
+            }
+            if (d >= o.dd) {  // ANNmin_k::insert with k = 1: an equal key lands in slot 1 and is dropped
+                if (!cnt || best > dist) {
+                    best = dist;
+                    best_i = pt;
+                }
+                cnt = 1;
+                min_dist = best;
+            }
+        }
+    }
+    out_idx[qi] = cnt ? best_i : -1;
+    out_err[qi] = cnt ? best : FLT_MAX;
+}
+
+size_t kd_pri_heap_bytes(const KdTree *t, int nq) {
+    return t ? (size_t)std::max(nq, 0) * ((size_t)t->n + 1) * sizeof(PriEntry) : 0;
+}
+
+int kd_pri_search(const KdTree *t, const float *d_rows, const float *d_q, int nq, float eps, void *heap, int *d_idx,
+                  float *d_err, hipStream_t stream) {
+    if (!t || nq <= 0) return 0;
+    if (!heap) {
+        set_error("kd_pri_search: no heap scratch");
+        return -1;
+    }
+    KTimer tm("kd_pri", stream);
+    hipLaunchKernelGGL(kd_pri_kernel, dim3((unsigned)((nq + 63) / 64)), dim3(64), 0, stream, t->view(), d_rows, d_q,
+                       nq, eps, (PriEntry *)heap, d_idx, d_err);
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 // one wave per query: coalesced row read, the outside-the-box terms in parallel, then their sequential fp32 sum
 // in dimension order (a term inside the box is +0 and leaves the running sum unchanged, so only the others are
 // added, by one lane, in order)

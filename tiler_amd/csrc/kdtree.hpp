@@ -66,5 +66,11 @@ int kd_root_boxes(const KdTree *t, const float *d_q, int nq, float *rootbox, hip
 int kd_verify_and_replay(const KdTree *t, const KdFixArgs &a, hipStream_t stream);
 // the exact replay of the queries already listed in a.list / *a.count (the small-batch merge checks them itself)
 int kd_replay_listed(const KdTree *t, const KdFixArgs &a, hipStream_t stream);
+// annkPriSearch (ANN.dll 0x1800121a0, k = 1 as ann_kdtree_pri_search 0x180003ef0 calls it) replayed exactly for nq
+// queries, one thread each: box-distance priority queue (ANNpr_queue, 1-based binary heap of at most n entries),
+// leaf scans as annkSearch's, (1 + eps)^2 termination.  heap: kd_pri_heap_bytes(t, nq) of device scratch.
+size_t kd_pri_heap_bytes(const KdTree *t, int nq);
+int kd_pri_search(const KdTree *t, const float *d_rows, const float *d_q, int nq, float eps, void *heap, int *d_idx,
+                  float *d_err, hipStream_t stream);
 
 }  // namespace tiler

@@ -28,6 +28,7 @@
 #include "kdorder_dev.hpp"
 #include "nn_dev.hpp"
 #include "orbit.hpp"
+#include "orbit_map_gen.hpp"
 #include "psyv.hpp"
 
 #pragma clang fp contract(off)
@@ -1223,141 +1224,108 @@ __global__ __launch_bounds__(256) void nn_scan_small_kernel(RescoreArgs a, int n
 }
 
 // The same scan on a mirror-orbit index (orbit.hip: every group holds a base row and up to 3 members that are exact
-// signed permutations of it, S_m c[i] = +-c[src_m(i)], inside each 64-value colour component): a workgroup of 4 waves
-// takes 64 groups per round, a wave 16 of them, one lane per (group, member slot); the wave's 16 base rows are staged
-// one component at a time in LDS (coalesced: a quarter of the bytes of reading every member's row) and each lane sums
-// the reference's sequential distance of its member, whose value of dimension i is +-base[src_m(i)] -- exactly the
-// member's own row value (orbit_eq_kernel checked it with float equality: a -0 / +0 difference squares to the same
-// term) -- so the lists are the row walk's bit for bit.
-template <int QN, int K>
-__global__ __launch_bounds__(256) void nn_scan_orbit_kernel(RescoreArgs a, const int *__restrict__ member, long G,
-                                                            const uint32_t *__restrict__ mtab, int nsplit,
-                                                            float *__restrict__ pd, int *__restrict__ pi) {
-    constexpr int D = 192, SB = 65;  // SB: LDS row stride
-    __shared__ __attribute__((aligned(16))) float sq[QN * D];
-    __shared__ float sb[4][16 * SB];
-    __shared__ uint32_t st[D];
-    __shared__ float rd[4][K];
-    __shared__ int ri[4][K];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lg = lane >> 2, x = lane & 3;
-    const int qg = blockIdx.y * QN;
-    const int nq = min(a.nq - qg, QN);
-    if (a.kd_count && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.kd_count = 0;  // the merge kernel appends
-    for (int i = tid; i < nq * D; i += 256) sq[i] = a.q[(long)qg * D + i];
-    for (int i = tid; i < D; i += 256) st[i] = mtab[i];
-    const long g0 = G * blockIdx.x / nsplit, g1 = G * (blockIdx.x + 1) / nsplit;
-    float bd[QN][K];
-    int bi[QN][K];
+// signed permutations of it, (S_m c)[i] = +-c[src_m(i)] inside each 64-value colour component, the same map in all
+// three): one wave takes 64 groups per round, one lane per group, and holds its group's base row in registers (from
+// OrbitIndex::d_base, the fp32 base rows interleaved per 64-group block so every load is 1 KB contiguous).  The mirror
+// tables are compile-time (orbitgen::MSRC / MNEG, checked against build_map when the index is built), so each member's
+// value at dimension i is a fixed register, its sign a fixed add-or-subtract ((q - (-b)) == (q + b) bit for bit) and
+// the query value a scalar operand: 3 VALU per (member, dimension).  Each member's sum runs in dimension order --
+// the reference's sequential distance of its own row (orbit_eq_kernel checked row == S_m base with float equality; a
+// -0 / +0 difference squares to the same term) -- so the lists are the row walk's bit for bit.
+template <int K>
+__global__ __launch_bounds__(64) void nn_scan_orbit_kernel(RescoreArgs a, const float *__restrict__ qs,
+                                                           const int4 *__restrict__ member,
+                                                           const float4 *__restrict__ base, long G, int nsplit,
+                                                           float *__restrict__ pd, int *__restrict__ pi) {
+    constexpr int D = 192;
+    // workgroup = (64-group block, query), nsplit = the block count.  XCD-aware order: workgroups are dispatched
+    // round-robin over the 8 XCDs (id % 8), so the nq workgroups of block b take ids on b's XCD, consecutively --
+    // the block's rows are read from HBM once and from that XCD's L2 by the other queries
+    const int lane = threadIdx.x, id = blockIdx.x, xcd = id & 7, slot = id >> 3, q = slot % a.nq;
+    const long b = (long)(slot / a.nq) * 8 + xcd, g = b * 64 + lane;
+    if (b >= nsplit) return;  // the padding of the block count to a multiple of 8
+    if (a.kd_count && b == 0 && q == 0 && lane == 0) *a.kd_count = 0;  // the merge kernel appends
+    const float *qr = qs + (long)q * D;  // uniform, restrict: the query values are scalar operands
+    const int4 mj = g < G ? member[g] : make_int4(-1, -1, -1, -1);
+    float cur[64];
+    auto load = [&](int c, float *r) {
 #pragma unroll
-    for (int q = 0; q < QN; q++)
-#pragma unroll
-        for (int r = 0; r < K; r++) {
-            bd[q][r] = INFINITY;
-            bi[q][r] = 0x7fffffff;
+        for (int k = 0; k < 16; k++) {
+            const float4 v = base[(b * 48 + c * 16 + k) * 64 + lane];
+            r[4 * k] = v.x;
+            r[4 * k + 1] = v.y;
+            r[4 * k + 2] = v.z;
+            r[4 * k + 3] = v.w;
         }
-    float *wb = sb[w];
-    const float *row = wb + lg * SB;
-    for (long gb = g0; gb < g1; gb += 64) {  // uniform over the workgroup
-        const long g = gb + w * 16 + lg;
-        const bool valid = g < g1;
-        const int j = valid ? member[g * 4 + x] : -1;  // this lane's candidate (-1: empty slot)
-        const int base = __shfl(j, lane & ~3, 64);     // slot 0 of the group: its base row
-        float dist[QN];
+    };
+    load(0, cur);
+    float dist[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    // components in a (not unrolled) loop: its 64 query values per component in scalar registers, the next
+    // component's row values loading while this one is summed
+    for (int c = 0; c < 3; c++) {
+        float nxt[64];
+        if (c < 2) load(c + 1, nxt);
+        const float *qc = qr + c * 64;
 #pragma unroll
-        for (int q = 0; q < QN; q++) dist[q] = 0.0f;
-        for (int c = 0; c < 3; c++) {
-            __syncthreads();  // the previous component's reads are done (and, first, the query / table staging)
+        for (int i = 0; i < 64; i++) {
+            const float qv = qc[i];
+            const float t0 = qv - cur[i];
+            dist[0] = dist[0] + t0 * t0;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {  // row r's 16 float4 pieces from 16 consecutive lanes
-                const int p = lane + 64 * u, r = p >> 4, k4 = p & 15;
-                const int br = __shfl(base, r * 4, 64);
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (br >= 0) v = reinterpret_cast<const float4 *>(a.rows + (long)br * D + c * 64)[k4];
-                float *d = wb + r * SB + 4 * k4;
-                d[0] = v.x;
-                d[1] = v.y;
-                d[2] = v.z;
-                d[3] = v.w;
-            }
-            __syncthreads();
-            const int sh = 7 * (x - 1);
-#pragma unroll 8
-            for (int i = 0; i < 64; i++) {
-                float v;
-                if (x == 0) {
-                    v = row[i];
-                } else {
-                    const uint32_t e = (st[c * 64 + i] >> sh) & 127;
-                    const float bv = row[e & 63];
-                    v = (e & 64) ? -bv : bv;
-                }
-#pragma unroll
-                for (int q = 0; q < QN; q++) {
-                    const float t = sq[q * D + c * 64 + i] - v;
-                    dist[q] = dist[q] + t * t;
-                }
+            for (int m = 0; m < 3; m++) {
+                const float bv = cur[orbitgen::MSRC[m][i]];
+                const float t = orbitgen::MNEG[m][i] ? qv + bv : qv - bv;
+                dist[m + 1] = dist[m + 1] + t * t;
             }
         }
-        if (j < 0) continue;
+        if (c < 2)
 #pragma unroll
-        for (int q = 0; q < QN; q++) {
-            if (q >= nq) break;
-            const float *qr = sq + q * D;
-            if (!kd_less(a.ko, qr, dist[q], j, bd[q][K - 1], bi[q][K - 1])) continue;
-            int p = K - 1;  // a lane's members do not arrive in index order: the insertion compares (distance, tie order)
-            while (p > 0 && kd_less(a.ko, qr, dist[q], j, bd[q][p - 1], bi[q][p - 1])) {
-                bd[q][p] = bd[q][p - 1];
-                bi[q][p] = bi[q][p - 1];
-                p--;
-            }
-            bd[q][p] = dist[q];
-            bi[q][p] = j;
-        }
+            for (int i = 0; i < 64; i++) cur[i] = nxt[i];
     }
-    // per query: the workgroup's K best, K rounds of (distance, tie order) argmin over the lanes' sorted lists
-    for (int q = 0; q < nq; q++) {
-        const float *qr = sq + q * D;
-        int ptr = 0;
-        for (int r = 0; r < K; r++) {
-            float v = INFINITY;
-            int vi = 0x7fffffff;
+    // the lane's (up to 4) members sorted by (distance, tie order) with a 4-input network (absent slots: the
+    // (inf, 0x7fffffff) sentinel, which kd_less puts after every candidate), then K rounds of argmin over the wave
+    float bd[4] = {dist[0], dist[1], dist[2], dist[3]};
+    int bi[4] = {mj.x, mj.y, mj.z, mj.w};
 #pragma unroll
-            for (int y = 0; y < K; y++)
-                if (y == ptr) {
-                    v = bd[q][y];
-                    vi = bi[q][y];
-                }
-            float mv = v;
-            int mi = vi;
-            kd_argmin<64>(a.ko, qr, mv, mi);
-            if (lane == 0) {
-                rd[w][r] = mv;
-                ri[w][r] = mi;
-            }
-            if (vi == mi && mi != 0x7fffffff) ptr++;  // this wave's winner leaves its list
+    for (int x = 0; x < 4; x++)
+        if (bi[x] < 0) {
+            bd[x] = INFINITY;
+            bi[x] = 0x7fffffff;
         }
-        __syncthreads();
-        if (w == 0) {  // merge the 4 waves' sorted K-lists: lane l < 4 holds wave l's list head
-            int hp = 0;
-            for (int r = 0; r < K; r++) {
-                float v = INFINITY;
-                int vi = 0x7fffffff;
-                if (lane < 4 && hp < K) {
-                    v = rd[lane][hp];
-                    vi = ri[lane][hp];
-                }
-                float mv = v;
-                int mi = vi;
-                kd_argmin<64>(a.ko, qr, mv, mi);
-                if (lane < 4 && vi == mi && mi != 0x7fffffff) hp++;
-                if (lane == 0) {
-                    const long o = ((long)(qg + q) * nsplit + blockIdx.x) * K + r;
-                    pd[o] = mv;
-                    pi[o] = mi;
-                }
-            }
+    auto cx = [&](int u, int w) {
+        if (kd_less(a.ko, qr, bd[w], bi[w], bd[u], bi[u])) {
+            const float td = bd[u];
+            const int ti = bi[u];
+            bd[u] = bd[w];
+            bi[u] = bi[w];
+            bd[w] = td;
+            bi[w] = ti;
         }
-        __syncthreads();
+    };
+    cx(0, 1);
+    cx(2, 3);
+    cx(0, 2);
+    cx(1, 3);
+    cx(1, 2);
+    int ptr = 0;
+    for (int r = 0; r < K; r++) {
+        float v = INFINITY;
+        int vi = 0x7fffffff;
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+            if (y == ptr) {
+                v = bd[y];
+                vi = bi[y];
+            }
+        float mv = v;
+        int mi = vi;
+        kd_argmin<64>(a.ko, qr, mv, mi);
+        if (vi == mi && mi != 0x7fffffff) ptr++;  // this lane's winner leaves its list
+        if (lane == 0) {
+            const long o = ((long)q * nsplit + b) * K + r;
+            pd[o] = mv;
+            pi[o] = mi;
+        }
     }
 }
 
@@ -1896,6 +1864,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
 // the small-batch path (nn_scan_small_kernel): groups of up to 16 queries (k = 1) or 4 (k <= 8) per workgroup row,
 // batches of up to SCAN_MAX1 / SCAN_MAX8 queries
 static constexpr int SCAN_QN1 = 16, SCAN_QN8 = 4;
+static constexpr long SCAN_ORB_MAXBLK = 4096;  // the orbit scan's splits (64-group blocks) at most: merge length
 static std::atomic<int> g_scan_max1{64}, g_scan_max8{16};  // tiler_set_scan_limits
 void nn_set_scan_limits(int max_k1, int max_k8) {
     g_scan_max1.store(std::max(0, max_k1));
@@ -1910,10 +1879,10 @@ static bool scan_small_takes(const NNIndex *ix, int nq, int k) {
 }
 static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t stream) {
     const OrbitIndex *o = ix->orbit;
-    // mirror orbits, groups of <= 4 queries: base rows only (nn_scan_orbit_kernel; 16-query groups measured slower)
-    const bool orb = o && o->d_mtab && o->G > 0 && ix->d == 192 && nq <= 4;
-    const int nsplit = orb ? (int)std::max<long>(1, std::min<long>(1024, ((long)o->G + 63) / 64))
-                           : (int)std::max<long>(1, std::min<long>(1024, ((long)ix->n + 255) / 256));
+    // mirror orbits: base rows only (nn_scan_orbit_kernel), one wave per (64-group block, query)
+    const long nblk = o ? ((long)o->G + 63) / 64 : 0;
+    const bool orb = o && o->d_base && o->G > 0 && ix->d == 192 && nblk <= SCAN_ORB_MAXBLK;
+    const int nsplit = orb ? (int)nblk : (int)std::max<long>(1, std::min<long>(1024, ((long)ix->n + 255) / 256));
     const int K = k == 1 ? 1 : 8;
     if (ensure_scratch(ix, nq, (long)nq * nsplit * K)) return -1;
     SearchScratch &s = ix->scratch;
@@ -1926,19 +1895,13 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
     auto scan = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, ra, nsplit, s.key, s.idx);
     };
-    auto scan_o = [&](auto kern) {
-        hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, ra, (const int *)o->d_member, (long)o->G,
-                           (const uint32_t *)o->d_mtab, nsplit, s.key, s.idx);
+    auto scan_o = [&](auto kern) {  // one wave per (64-group block, query), the block count padded to 8 XCDs
+        hipLaunchKernelGGL(kern, dim3((unsigned)(((nsplit + 7) / 8) * 8 * nq)), dim3(64), 0, stream, ra, ra.q, (const int4 *)o->d_member,
+                           (const float4 *)o->d_base, (long)o->G, nsplit, s.key, s.idx);
     };
     if (orb) {
-        if (K == 1) {
-            if (qn == 1) scan_o(nn_scan_orbit_kernel<1, 1>);
-            else if (qn == 4) scan_o(nn_scan_orbit_kernel<4, 1>);
-            else scan_o(nn_scan_orbit_kernel<SCAN_QN1, 1>);
-        } else {
-            if (qn == 1) scan_o(nn_scan_orbit_kernel<1, 8>);
-            else scan_o(nn_scan_orbit_kernel<SCAN_QN8, 8>);
-        }
+        if (K == 1) scan_o(nn_scan_orbit_kernel<1>);
+        else scan_o(nn_scan_orbit_kernel<8>);
         hipLaunchKernelGGL(K == 1 ? nn_scan_merge_kernel<1> : nn_scan_merge_kernel<8>, dim3(nq), dim3(64), 0, stream, ra,
                            nsplit, (const float *)s.key, (const int *)s.idx);
     } else if (K == 1) {

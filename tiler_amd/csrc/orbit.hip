@@ -2023,6 +2023,21 @@ static double bits2d(unsigned long long b) {
     return v;
 }
 
+// base = the groups' base rows rows[member[g][0]] in OrbitIndex::d_base's interleaved layout, zero past G
+__global__ __launch_bounds__(256) void orbit_base_kernel(const float *__restrict__ rows, const int *__restrict__ member,
+                                                         long G, float4 *__restrict__ base) {
+    constexpr int W = OD / 4;
+    const long total = (G + 63) / 64 * 64 * W;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const long blk = t / (64 * W);
+        const int k = (int)(t / 64 % W), l = (int)(t % 64);
+        const long g = blk * 64 + l;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (g < G) v = reinterpret_cast<const float4 *>(rows)[(long)member[g * 4] * W + k];
+        base[t] = v;
+    }
+}
+
 void orbit_destroy(OrbitIndex *o) {
     if (!o) return;
     hipFree(o->d_bmask);
@@ -2037,7 +2052,7 @@ void orbit_destroy(OrbitIndex *o) {
     hipFree(o->d_gorder);
     hipFree(o->d_grp_of);
     hipFree(o->d_map);
-    hipFree(o->d_mtab);
+    hipFree(o->d_base);
     hipFree(o->qfrag);
     hipFree(o->qstat);
     hipFree(o->pair_cnt);
@@ -2102,25 +2117,6 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     o->G = (int)G;
     o->gblk = (int)((G + 31) / 32);
     o->d_map = d_map;
-    {  // the mirrors as (column in the component, sign) for the small-batch scan (nn_scan_orbit_kernel); build_map
-       // already requires each mirror to stay inside its colour component -- if not, the scan keeps the row walk
-        uint32_t mtab[OD];
-        bool ok = true;
-        for (int i = 0; i < OD; i++) {
-            uint32_t w = 0;
-            for (int m = 0; m < 3; m++) {
-                const int src = hmap.msrc[m][i], c0 = (i / 64) * 64;
-                ok = ok && src >= c0 && src < c0 + 64 && (hmap.msgn[m][i] == 1.0f || hmap.msgn[m][i] == -1.0f);
-                w |= (uint32_t)(((src - c0) & 63) | (hmap.msgn[m][i] < 0.0f ? 64 : 0)) << (7 * m);
-            }
-            mtab[i] = w;
-        }
-        if (ok) {
-            TILER_HIP_CHECK(hipMalloc((void **)&o->d_mtab, sizeof(mtab)));
-            TILER_HIP_CHECK(hipMemcpyAsync(o->d_mtab, mtab, sizeof(mtab), hipMemcpyHostToDevice, stream));
-            TILER_HIP_CHECK(hipStreamSynchronize(stream));  // mtab is this block's
-        }
-    }
     OrbitDsStat *d_ds = nullptr;
     TILER_HIP_CHECK(hipMalloc((void **)&o->d_member, G * 4 * sizeof(int)));
     TILER_HIP_CHECK(hipMemcpyAsync(o->d_member, member.data(), G * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
@@ -2209,6 +2205,22 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
             TILER_HIP_CHECK(hipGetLastError());
             TILER_HIP_CHECK(hipStreamSynchronize(stream));  // (pm, bm) stay alive until the copies are done
             hipFree(d_ds);
+        }
+    }
+    {  // the base rows in (final) group order for the small-batch orbit scan, whose mirror tables are compiled in
+        bool ok = true;
+        for (int m = 0; m < 3; m++)
+            for (int i = 0; i < OD; i++) {
+                const int c0 = (i / 64) * 64;
+                ok = ok && hmap.msrc[m][i] == c0 + orbitgen::MSRC[m][i % 64] &&
+                     hmap.msgn[m][i] == (orbitgen::MNEG[m][i % 64] ? -1.0f : 1.0f);
+            }
+        if (ok) {
+            const long nb = (G + 63) / 64;
+            TILER_HIP_CHECK(hipMalloc((void **)&o->d_base, (size_t)nb * 64 * OD * sizeof(float)));
+            hipLaunchKernelGGL(orbit_base_kernel, dim3((unsigned)std::min<long>(8192, (nb * 64 * (OD / 4) + 255) / 256)),
+                               dim3(256), 0, stream, ix->d_rows, (const int *)o->d_member, G, (float4 *)o->d_base);
+            TILER_HIP_CHECK(hipGetLastError());
         }
     }
     {  // block 0 only, every block: the flat query tiles' shortlist (orbit_search)

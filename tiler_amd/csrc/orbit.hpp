@@ -47,8 +47,9 @@ struct OrbitIndex {
     GroupOrder *d_gorder = nullptr;  // [G] (kd tie order only)
     int *d_grp_of = nullptr;      // [n] candidate -> g * 4 + slot (kd tie order only; -1: not in a group)
     void *d_map = nullptr;        // OrbitMap
-    uint32_t *d_mtab = nullptr;   // [192] mirror m = 1..3 of dimension i in bits 7(m-1)..: its source column inside i's
-                                  // 64-value component (6 bits) and a sign bit (the small-batch orbit scan)
+    float *d_base = nullptr;      // [ceil(G / 64)][48][64] float4: fp32 base row (member slot 0) of every group, float4
+                                  // piece k of group g at [g / 64][k][g % 64] (zero padding); null when the compiled
+                                  // mirror tables (orbitgen::MSRC / MNEG) do not match build_map (small-batch orbit scan)
     // mirror-symmetric groups first (orbit_build): blocks [0, red_end) may have isotypic blocks of c' that are zero
     // for every group in them (bit x of d_bmask[blk] clear), whose k-steps the shortlist skips; the rest are full
     int red_end = 0;

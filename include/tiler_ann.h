@@ -27,8 +27,8 @@
  *   - the dataset rows are copied to device memory at create (ANN borrows pa until destroy);
  *   - no process abort: errors return -1 (or NULL) and tiler_last_error() explains;
  *   - every entry point is thread-safe.  Concurrent single-query calls on one handle (ann_kdtree_search /
- *     _pri_search / _search_multi from many threads: the reference's ProcThreadPool pattern, main.pas:972, 4027,
- *     3830) are coalesced: callers that arrive while a batch is in flight are searched together as the next batch,
+ *     _search_multi from many threads: the reference's ProcThreadPool pattern, main.pas:972, 4027, 3830) are
+ *     coalesced: callers that arrive while a batch is in flight are searched together as the next batch,
  *     each woken with its own answer (identical to a lone call's); other calls on one handle are serialised.
  * The search runs on the GPU only.  There is no CPU fallback: if the HIP runtime or a gfx950
  * device is missing every call fails with -1 / NULL.

@@ -1232,9 +1232,22 @@ __global__ __launch_bounds__(256) void nn_scan_small_kernel(RescoreArgs a, int n
 // the query value a scalar operand: 3 VALU per (member, dimension).  Each member's sum runs in dimension order --
 // the reference's sequential distance of its own row (orbit_eq_kernel checked row == S_m base with float equality; a
 // -0 / +0 difference squares to the same term) -- so the lists are the row walk's bit for bit.
+// ANN's order of two different present slots x, y of one group for query q (orbit.hip group_before)
+__device__ __forceinline__ bool group_order_before(const GroupOrder *__restrict__ go, const float *__restrict__ q, int x,
+                                                   int y) {
+    const int lo = min(x, y), hi = max(x, y);
+    const int pi = lo == 0 ? hi - 1 : lo == 1 ? hi + 1 : 5;  // (0,1)(0,2)(0,3)(1,2)(1,3)(2,3)
+    const unsigned code = (go->pairs >> (3 * pi)) & 7u;
+    const int node = code & 3;
+    const bool lo_first = (q[go->cd[node]] - go->cv[node]) < 0.0f;
+    const bool low_slot_first = ((code >> 2) & 1) == (unsigned)lo_first;
+    return (x == lo) == low_slot_first;
+}
+
 template <int K>
 __global__ __launch_bounds__(64) void nn_scan_orbit_kernel(RescoreArgs a, const float *__restrict__ qs,
                                                            const int4 *__restrict__ member,
+                                                           const GroupOrder *__restrict__ gorder,
                                                            const float4 *__restrict__ base, long G, int nsplit,
                                                            float *__restrict__ pd, int *__restrict__ pi) {
     constexpr int D = 192;
@@ -1284,22 +1297,33 @@ __global__ __launch_bounds__(64) void nn_scan_orbit_kernel(RescoreArgs a, const 
     }
     // the lane's (up to 4) members sorted by (distance, tie order) with a 4-input network (absent slots: the
     // (inf, 0x7fffffff) sentinel, which kd_less puts after every candidate), then K rounds of argmin over the wave
+    // An exact tie between two members of the group is decided by the group's cached separating node
+    // (GroupOrder, orbit.hip group_before: one compare) instead of kd_before's root-to-leaf walk.
     float bd[4] = {dist[0], dist[1], dist[2], dist[3]};
     int bi[4] = {mj.x, mj.y, mj.z, mj.w};
+    int sl[4] = {0, 1, 2, 3};  // member slots, carried through the swaps
 #pragma unroll
     for (int x = 0; x < 4; x++)
         if (bi[x] < 0) {
             bd[x] = INFINITY;
             bi[x] = 0x7fffffff;
         }
+    const GroupOrder *go = gorder && g < G ? gorder + g : nullptr;
     auto cx = [&](int u, int w) {
-        if (kd_less(a.ko, qr, bd[w], bi[w], bd[u], bi[u])) {
+        bool less;
+        if (bd[w] != bd[u] || bi[w] == 0x7fffffff || bi[u] == 0x7fffffff || !go)
+            less = kd_less(a.ko, qr, bd[w], bi[w], bd[u], bi[u]);
+        else
+            less = group_order_before(go, qr, sl[w], sl[u]);
+        if (less) {
             const float td = bd[u];
-            const int ti = bi[u];
+            const int ti = bi[u], ts = sl[u];
             bd[u] = bd[w];
             bi[u] = bi[w];
+            sl[u] = sl[w];
             bd[w] = td;
             bi[w] = ti;
+            sl[w] = ts;
         }
     };
     cx(0, 1);
@@ -1896,7 +1920,8 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
         hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, ra, nsplit, s.key, s.idx);
     };
     auto scan_o = [&](auto kern) {  // one wave per (64-group block, query), the block count padded to 8 XCDs
-        hipLaunchKernelGGL(kern, dim3((unsigned)(((nsplit + 7) / 8) * 8 * nq)), dim3(64), 0, stream, ra, ra.q, (const int4 *)o->d_member,
+        hipLaunchKernelGGL(kern, dim3((unsigned)(((nsplit + 7) / 8) * 8 * nq)), dim3(64), 0, stream, ra, ra.q,
+                           (const int4 *)o->d_member, ra.ko && ix->kd && ix->kd->bs == 1 ? (const GroupOrder *)o->d_gorder : nullptr,
                            (const float4 *)o->d_base, (long)o->G, nsplit, s.key, s.idx);
     };
     if (orb) {

@@ -1353,6 +1353,81 @@ __global__ __launch_bounds__(64) void nn_scan_orbit_kernel(RescoreArgs a, const 
     }
 }
 
+// The k = 1 scan of a plain index, one wave per (candidate split, query): lane = row, the rows from the index's
+// row-interleaved copy (NNIndex::d_rowsT, float4 piece k of row b * 64 + l at [b][k][l]: each load instruction reads
+// 1 KB contiguous), the query values scalar operands (restrict pointer: scalar loads), 64 dimensions per step (d is a
+// multiple of 64), the reference's sequential sum per row; each lane keeps its best (distance, tie order) over its rows, the wave's best
+// goes to the merge.  XCD-aware order as nn_scan_orbit_kernel's (a split's queries on its XCD, consecutively).
+__global__ __launch_bounds__(64) void nn_scan_rows_kernel(RescoreArgs a, const float *__restrict__ qs,
+                                                          const float4 *__restrict__ rowsT, int nsplit,
+                                                          float *__restrict__ pd, int *__restrict__ pi) {
+    const int lane = threadIdx.x, id = blockIdx.x, xcd = id & 7, slot = id >> 3, q = slot % a.nq;
+    const long sp = (long)(slot / a.nq) * 8 + xcd;
+    if (sp >= nsplit) return;  // the padding of the split count to a multiple of 8
+    if (a.kd_count && sp == 0 && q == 0 && lane == 0) *a.kd_count = 0;  // the merge kernel appends
+    const int d4 = a.d >> 2, nch = a.d >> 6;  // a.d % 64 == 0
+    const long nb = ((long)a.n + 63) / 64;
+    const long b0 = nb * sp / nsplit, b1 = nb * (sp + 1) / nsplit;
+    const float *qr = qs + (long)q * a.d;
+    float best = INFINITY;
+    int bi = 0x7fffffff;
+    for (long b = b0; b < b1; b++) {
+        const float4 *rb = rowsT + b * d4 * 64 + lane;
+        float dist = 0.0f;
+        float4 cur[16];
+        auto load = [&](int c, float4 *r) {
+#pragma unroll
+            for (int u = 0; u < 16; u++) r[u] = rb[(long)(c * 16 + u) * 64];
+        };
+        load(0, cur);
+        // 64-dimension chunks in a (not unrolled) loop: the chunk's 64 query values in scalar registers, the next
+        // chunk's 16 loads in flight while this one is summed
+        for (int c = 0; c < nch; c++) {
+            float4 nxt[16];
+            if (c + 1 < nch) load(c + 1, nxt);
+            const float *qk = qr + 64 * c;
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                float t = qk[4 * u] - cur[u].x;
+                dist = dist + t * t;
+                t = qk[4 * u + 1] - cur[u].y;
+                dist = dist + t * t;
+                t = qk[4 * u + 2] - cur[u].z;
+                dist = dist + t * t;
+                t = qk[4 * u + 3] - cur[u].w;
+                dist = dist + t * t;
+            }
+            if (c + 1 < nch)
+#pragma unroll
+                for (int u = 0; u < 16; u++) cur[u] = nxt[u];
+        }
+        const int j = (int)(b * 64 + lane);
+        if (j < a.n && kd_less(a.ko, qr, dist, j, best, bi)) {
+            best = dist;
+            bi = j;
+        }
+    }
+    float mv = best;
+    int mi = bi;
+    kd_argmin<64>(a.ko, qr, mv, mi);
+    if (lane == 0) {
+        pd[(long)q * nsplit + sp] = mv;
+        pi[(long)q * nsplit + sp] = mi;
+    }
+}
+
+// rowsT = the row-interleaved copy of rows[n][d] (d % 4 == 0), zero past n
+__global__ __launch_bounds__(256) void rows_interleave_kernel(const float4 *__restrict__ rows, long n, int d4,
+                                                             float4 *__restrict__ rowsT) {
+    const long total = (n + 63) / 64 * 64 * d4;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+        const long blk = t / (64L * d4);
+        const int k = (int)(t / 64 % d4), l = (int)(t % 64);
+        const long r = blk * 64 + l;
+        rowsT[t] = r < n ? rows[r * d4 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
 // one wave per query: the k best of its nsplit * K partials (each split's list sorted) -> out, tilemap item
 template <int K>
 __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int nsplit, const float *__restrict__ pd,
@@ -1586,6 +1661,7 @@ void nn_index_destroy(NNIndex *ix) {
     orbit_destroy(ix->orbit);
     kd_tree_destroy(ix->kd);
     hipFree(ix->d_rows);
+    hipFree(ix->d_rowsT);
     hipFree(ix->d_frag);
     hipFree(ix->d_nc);
     hipFree(ix->d_seed);
@@ -1888,6 +1964,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
 // the small-batch path (nn_scan_small_kernel): groups of up to 16 queries (k = 1) or 4 (k <= 8) per workgroup row,
 // batches of up to SCAN_MAX1 / SCAN_MAX8 queries
 static constexpr int SCAN_QN1 = 16, SCAN_QN8 = 4;
+static constexpr long SCAN_ROWS_MAXN = 65536;   // nn_scan_rows_kernel up to this many candidates
 static constexpr long SCAN_ORB_MAXBLK = 4096;  // the orbit scan's splits (64-group blocks) at most: merge length
 static std::atomic<int> g_scan_max1{64}, g_scan_max8{16};  // tiler_set_scan_limits
 void nn_set_scan_limits(int max_k1, int max_k8) {
@@ -1906,8 +1983,23 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
     // mirror orbits: base rows only (nn_scan_orbit_kernel), one wave per (64-group block, query)
     const long nblk = o ? ((long)o->G + 63) / 64 : 0;
     const bool orb = o && o->d_base && o->G > 0 && ix->d == 192 && nblk <= SCAN_ORB_MAXBLK;
-    const int nsplit = orb ? (int)nblk : (int)std::max<long>(1, std::min<long>(1024, ((long)ix->n + 255) / 256));
     const int K = k == 1 ? 1 : 8;
+    // k = 1 on a plain index: the row-interleaved scan (nn_scan_rows_kernel); its copy is made on first use and waited
+    // for (a concurrent slot's scan may be queued on another stream as soon as this call releases the index)
+    // (at larger n the split-per-thread scan reads each row once for the batch's queries at near HBM peak: r05w2, the
+    // shuffled 262,144-row handle, 1 query 73 vs 77 us, batches slower)
+    const bool rows_scan = !orb && K == 1 && ix->d % 64 == 0 && ix->n <= SCAN_ROWS_MAXN;
+    if (rows_scan && !ix->d_rowsT) {
+        const long nb = ((long)ix->n + 63) / 64;
+        TILER_HIP_CHECK(hipMalloc((void **)&ix->d_rowsT, (size_t)nb * 64 * ix->d * sizeof(float)));
+        hipLaunchKernelGGL(rows_interleave_kernel, dim3((unsigned)std::min<long>(8192, (nb * 64 * (ix->d / 4) + 255) / 256)),
+                           dim3(256), 0, stream, (const float4 *)ix->d_rows, (long)ix->n, ix->d / 4, (float4 *)ix->d_rowsT);
+        TILER_HIP_CHECK(hipGetLastError());
+        TILER_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+    const int nsplit = orb ? (int)nblk
+                           : rows_scan ? (int)std::max<long>(1, ((long)ix->n + 63) / 64)
+                                       : (int)std::max<long>(1, std::min<long>(1024, ((long)ix->n + 255) / 256));
     if (ensure_scratch(ix, nq, (long)nq * nsplit * K)) return -1;
     SearchScratch &s = ix->scratch;
     ix->last_splits = 0;  // the stats report no tier-2 / tier-3 queries for a scan (fb_count is not read)
@@ -1929,6 +2021,11 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
         else scan_o(nn_scan_orbit_kernel<8>);
         hipLaunchKernelGGL(K == 1 ? nn_scan_merge_kernel<1> : nn_scan_merge_kernel<8>, dim3(nq), dim3(64), 0, stream, ra,
                            nsplit, (const float *)s.key, (const int *)s.idx);
+    } else if (rows_scan) {
+        hipLaunchKernelGGL(nn_scan_rows_kernel, dim3((unsigned)(((nsplit + 7) / 8) * 8 * nq)), dim3(64), 0, stream, ra,
+                           ra.q, (const float4 *)ix->d_rowsT, nsplit, s.key, s.idx);
+        hipLaunchKernelGGL(nn_scan_merge_kernel<1>, dim3(nq), dim3(64), 0, stream, ra, nsplit, (const float *)s.key,
+                           (const int *)s.idx);
     } else if (K == 1) {
         if (qn == 1) scan(nn_scan_small_kernel<1, 1>);
         else if (qn == 4) scan(nn_scan_small_kernel<4, 1>);

@@ -66,6 +66,8 @@ struct NNIndex {
     int perm = 0;               // 1: candidate rows spread over accumulator lanes (row_perm), float data
     const int *flat_cnt = nullptr; // FrameTiling call in progress: device count of non-flat queries (flat ones last)
     float *d_rows = nullptr;    // [n][d] fp32 (exact rescoring)
+    float *d_rowsT = nullptr;   // [ceil(n/64)][d/4][64] float4 row-interleaved copy (k = 1 small-batch scan, built on
+                                // first use; null on mirror-orbit indexes, which scan their base rows)
     void *d_frag = nullptr;     // [nblk][S][64][8] fp16, MFMA A-operand fragment order
     float *d_nc = nullptr;      // [nblk][32] ||c||^2 in accumulator-row order (+inf on padding rows)
     float *d_seed = nullptr;    // [nblk][32] -||c||^2/2, same order (-inf on padding rows)

@@ -2,7 +2,8 @@
 """Study script: the reference's per-tile call pattern (ann_kdtree_search once per frame tile from 16 threads on one
 handle, main.pas:972 / 4027) through libANN.so's native harness (tiler_debug_percall_bench): calls/s, the median lone
 call, batches, and mismatches against the batched search -- on the C3 keyframe handle (262,144 PsyV rows) and on a
-12,000-row handle.  --lib selects a library build (A/B)."""
+12,000-row handle and on the C3 rows shuffled (plain_262144: the same candidates, no mirror orbits, as a real
+PrepareFrameTiling set).  --lib selects a library build (A/B)."""
 import argparse
 import ctypes
 import json
@@ -43,7 +44,9 @@ def main():
     vp = ctypes.c_void_p
     out = {"tag": args.tag}
     for name, data in (() if args.scan_only else
-                       (("c3_262144", rows), ("small_12000", rows[rng.choice(rows.shape[0], 12000, replace=False)]))):
+                       (("c3_262144", rows), ("small_12000", rows[rng.choice(rows.shape[0], 12000, replace=False)]),
+                        ("plain_262144", rows[rng.permutation(rows.shape[0])]),
+                        ("plain_65536", rows[rng.permutation(rows.shape[0])[:65536]]))):
         with tiler_amd.KDTree(data) as kdt:
             bi, be = kdt.search_batch(qd)
             n_idx = np.zeros(qd.shape[0], np.int32)

@@ -2,7 +2,8 @@
 # Round 5 pass w2: the k = 1 small-batch scan of plain indexes from a row-interleaved copy (nn_scan_rows_kernel).
 # NN / FT / orbit / per-call GPU tests, then the per-call probe against the previous commit's build (libANN_h.so):
 # plain_262144 / plain_65536 / small_12000 are non-orbit handles (c3_262144 is a mirror-orbit index).  w3: only up
-# to 65,536 candidates.
+# to 65,536 candidates.  w4: the merge kernel replays in place and writes the results to host-visible memory
+# (no replay launch, no copy back); libANN_h.so = the previous commit.
 set -eu
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r05w2}

@@ -755,7 +755,9 @@ static int combine_run(ann_kdtree *t, CombineSlot &cs, std::vector<CombineReq *>
         cs.h_res = nullptr;
         cs.d_res = nullptr;
         cs.cap_r = 0;
-        TILER_HIP_CHECK(hipHostMalloc((void **)&cs.h_res, 2 * nr * sizeof(int), hipHostMallocPortable));
+        // fine-grained (coherent) pinned memory: a small-batch scan's merge kernel writes the results here itself
+        TILER_HIP_CHECK(hipHostMalloc((void **)&cs.h_res, 2 * nr * sizeof(int),
+                                      hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
         TILER_HIP_CHECK(hipMalloc((void **)&cs.d_res, 2 * nr * sizeof(int)));
         cs.cap_r = 2 * nr;
     }
@@ -764,11 +766,15 @@ static int combine_run(ann_kdtree *t, CombineSlot &cs, std::vector<CombineReq *>
     float *r_err = reinterpret_cast<float *>(cs.d_res + nr);
     TILER_HIP_CHECK(hipMemcpyAsync(cs.d_q, cs.h_q, (size_t)nq * d * sizeof(float), hipMemcpyHostToDevice, cs.stream));
     const bool small = nn_search_is_small(ix, nq, k);
+    int *hd_res = nullptr;  // the device's view of h_res (a small-batch scan writes its results there: no copy back)
+    TILER_HIP_CHECK(hipHostGetDevicePointer((void **)&hd_res, cs.h_res, 0));
     std::swap(ix->scratch, cs.scratch);  // this batch's scratch
-    const int rc = nn_search_dev(ix, cs.d_q, nq, k, r_idx, r_err, nullptr, cs.stream);
+    const int rc = nn_search_dev(ix, cs.d_q, nq, k, r_idx, r_err, nullptr, cs.stream, false, false,
+                                 small ? hd_res : nullptr, small ? reinterpret_cast<float *>(hd_res + nr) : nullptr);
     std::swap(ix->scratch, cs.scratch);
     if (rc) return -1;
-    TILER_HIP_CHECK(hipMemcpyAsync(cs.h_res, cs.d_res, 2 * nr * sizeof(int), hipMemcpyDeviceToHost, cs.stream));
+    if (!small)
+        TILER_HIP_CHECK(hipMemcpyAsync(cs.h_res, cs.d_res, 2 * nr * sizeof(int), hipMemcpyDeviceToHost, cs.stream));
     // a small-batch scan is queued: the other slot may queue its batch while this one runs; any other search keeps
     // the index (its orbit / tier buffers) until it has finished
     if (small) lk.unlock();

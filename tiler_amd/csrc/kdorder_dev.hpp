@@ -1,6 +1,7 @@
 // kdorder_dev.hpp -- device side of the ANN tie order (kdtree.hpp): which of two equal-distance candidates
 // annkSearch finds first, and ANN's box-distance pruning replayed along one candidate's path.
 #pragma once
+#include <float.h>
 #include <hip/hip_runtime.h>
 
 #include "kdtree.hpp"
@@ -289,6 +290,86 @@ __device__ __forceinline__ bool kd_quad_path_ok(const KdOrder *__restrict__ op, 
         }
     }
     return ok;
+}
+
+// annkSearch replayed exactly for one query (kd_search.cpp; ANN.dll 0x1800128e0, ANNkd_split::ann_search 0x180012b60,
+// ANNkd_leaf::ann_search 0x180012cf0): depth-first, near child first, far child iff its box distance < the current
+// k-th key (eps = 0), leaf scans with the early break, ANNmin_k insertion (equal keys keep the first found).  One
+// thread; the explicit stack holds pending nodes and pending far checks.  Writes idx[0..k) / err[0..k) (missing:
+// -1 / FLT_MAX) and returns the best index (-1: none).  K >= k.
+template <int K>
+__device__ int kd_replay_query(const KdOrder &o, const float *__restrict__ rows, const float *__restrict__ qr, int k,
+                               int *__restrict__ idx, float *__restrict__ err) {
+    float mk[K + 1];
+    int mi[K + 1];
+    int cnt = 0;
+    auto max_key = [&]() { return cnt == k ? mk[k - 1] : FLT_MAX; };
+    // stack frames: kind 0 = visit node [s, e) with box b; kind 1 = far check of node [s, e)'s child
+    struct Fr {
+        int s, e, kind;
+        float b;
+    };
+    Fr st[96];
+    int sp = 0;
+    st[sp++] = Fr{0, o.n, 0, kd_root_box(o, qr)};
+    while (sp > 0) {
+        const Fr f = st[--sp];
+        if (f.kind == 0) {
+            if (f.e - f.s <= o.bs) {  // ANNkd_leaf::ann_search
+                float min_dist = max_key();
+                for (int p = f.s; p < f.e; p++) {
+                    const int pt = o.pidx[p];
+                    const float *pp = rows + (long)pt * o.dd;
+                    float dist = 0.0f;
+                    int d;
+                    for (d = 0; d < o.dd; d++) {
+                        const float t = qr[d] - pp[d];
+                        dist = dist + t * t;
+                        if (dist > min_dist) break;
+                    }
+                    if (d >= o.dd) {  // ANNmin_k::insert
+                        int i;
+                        for (i = cnt; i > 0; i--) {
+                            if (mk[i - 1] > dist) {
+                                mk[i] = mk[i - 1];
+                                mi[i] = mi[i - 1];
+                            } else {
+                                break;
+                            }
+                        }
+                        mk[i] = dist;
+                        mi[i] = pt;
+                        if (cnt < k) cnt++;
+                        min_dist = max_key();
+                    }
+                }
+                continue;
+            }
+            const int m = f.s + ((f.e - f.s) >> 1);
+            const float cut_diff = qr[o.cd[m]] - o.cv[m];
+            // near child now, far check after it returns (pushed first, popped after the near subtree)
+            st[sp++] = Fr{f.s, f.e, 1, f.b};
+            if (cut_diff < 0.0f)
+                st[sp++] = Fr{f.s, m, 0, f.b};
+            else
+                st[sp++] = Fr{m, f.e, 0, f.b};
+        } else {
+            const int m = f.s + ((f.e - f.s) >> 1);
+            const float qd = qr[o.cd[m]];
+            const float cut_diff = qd - o.cv[m];
+            const bool lo_first = cut_diff < 0.0f;
+            float box_diff = lo_first ? o.lo[m] - qd : qd - o.hi[m];
+            if (box_diff < 0.0f) box_diff = 0.0f;
+            const float b = f.b + (cut_diff * cut_diff - box_diff * box_diff);
+            if (b * 1.0f < max_key()) st[sp++] = lo_first ? Fr{m, f.e, 0, b} : Fr{f.s, m, 0, b};
+        }
+    }
+    for (int j = 0; j < k; j++) {
+        const bool ok = j < cnt;
+        idx[j] = ok ? mi[j] : -1;
+        err[j] = ok ? mk[j] : FLT_MAX;
+    }
+    return cnt > 0 ? mi[0] : -1;
 }
 
 }  // namespace tiler

@@ -1025,87 +1025,14 @@ __global__ __launch_bounds__(256) void kd_verify_kernel(KdOrder o, KdFixArgs a) 
     if (!ok || a.force_replay) a.list[atomicAdd(a.count, 1)] = (int)q;
 }
 
-// annkSearch replayed exactly (kd_search.cpp): depth-first, near child first, far child iff its box distance
-// < the current k-th key (eps = 0), leaf scans with the early break, ANNmin_k insertion (equal keys keep the
-// first found).  One thread per listed query; the explicit stack holds pending nodes and pending far checks.
+// annkSearch replayed exactly: kd_replay_query (kdorder_dev.hpp), one thread per listed query
 template <int K>
 __global__ __launch_bounds__(64) void kd_replay_kernel(KdOrder o, KdFixArgs a) {
     const int count = *a.count;
     for (int li = blockIdx.x * 64 + threadIdx.x; li < count; li += gridDim.x * 64) {
         const long q = a.list[li];
-        const float *qr = a.q + q * o.dd;
-        const int k = a.k;
-        float mk[K + 1];
-        int mi[K + 1];
-        int cnt = 0;
-        auto max_key = [&]() { return cnt == k ? mk[k - 1] : FLT_MAX; };
-        // stack frames: kind 0 = visit node [s, e) with box b; kind 1 = far check of node [s, e)'s child
-        struct Fr {
-            int s, e, kind;
-            float b;
-        };
-        Fr st[96];
-        int sp = 0;
-        st[sp++] = Fr{0, o.n, 0, kd_root_box(o, qr)};
-        while (sp > 0) {
-            const Fr f = st[--sp];
-            if (f.kind == 0) {
-                if (f.e - f.s <= o.bs) {  // ANNkd_leaf::ann_search
-                    float min_dist = max_key();
-                    for (int p = f.s; p < f.e; p++) {
-                        const int pt = o.pidx[p];
-                        const float *pp = a.rows + (long)pt * o.dd;
-                        float dist = 0.0f;
-                        int d;
-                        for (d = 0; d < o.dd; d++) {
-                            const float t = qr[d] - pp[d];
-                            dist = dist + t * t;
-                            if (dist > min_dist) break;
-                        }
-                        if (d >= o.dd) {  // ANNmin_k::insert
-                            int i;
-                            for (i = cnt; i > 0; i--) {
-                                if (mk[i - 1] > dist) {
-                                    mk[i] = mk[i - 1];
-                                    mi[i] = mi[i - 1];
-                                } else {
-                                    break;
-                                }
-                            }
-                            mk[i] = dist;
-                            mi[i] = pt;
-                            if (cnt < k) cnt++;
-                            min_dist = max_key();
-                        }
-                    }
-                    continue;
-                }
-                const int m = f.s + ((f.e - f.s) >> 1);
-                const float cut_diff = qr[o.cd[m]] - o.cv[m];
-                // near child now, far check after it returns (pushed first, popped after the near subtree)
-                st[sp++] = Fr{f.s, f.e, 1, f.b};
-                if (cut_diff < 0.0f)
-                    st[sp++] = Fr{f.s, m, 0, f.b};
-                else
-                    st[sp++] = Fr{m, f.e, 0, f.b};
-            } else {
-                const int m = f.s + ((f.e - f.s) >> 1);
-                const float qd = qr[o.cd[m]];
-                const float cut_diff = qd - o.cv[m];
-                const bool lo_first = cut_diff < 0.0f;
-                float box_diff = lo_first ? o.lo[m] - qd : qd - o.hi[m];
-                if (box_diff < 0.0f) box_diff = 0.0f;
-                const float b = f.b + (cut_diff * cut_diff - box_diff * box_diff);
-                if (b * 1.0f < max_key()) st[sp++] = lo_first ? Fr{m, f.e, 0, b} : Fr{f.s, m, 0, b};
-            }
-        }
-        for (int j = 0; j < k; j++) {
-            const bool ok = j < cnt;
-            a.idx[q * k + j] = ok ? mi[j] : -1;
-            a.err[q * k + j] = ok ? mk[j] : FLT_MAX;
-        }
+        const int best = kd_replay_query<K>(o, a.rows, a.q + q * o.dd, a.k, a.idx + q * a.k, a.err + q * a.k);
         if (a.m_tile) {
-            const int best = cnt > 0 ? mi[0] : -1;
             a.m_tile[q] = best >= 0 ? a.tr_tile[best] : -1;
             a.m_pal[q] = best >= 0 ? a.tr_pal[best] : -1;
             const int at = best >= 0 ? a.tr_attr[best] : 0;

@@ -781,9 +781,12 @@ struct RescoreArgs {
     int32_t *m_tile, *m_pal;
     uint8_t *m_hm, *m_vm;
     const KdOrder *ko;   // tie order: ANN's kd-tree first-found (device view) or nullptr = the lowest index
-    int *kd_list, *kd_count;  // small-batch scan with a kd-tree of > bs points: the merge kernel runs ANN's pruning
-                              // check itself (kd_verify_kernel's test) and lists the queries for kd_replay_kernel
+    int *kd_list, *kd_count;  // (unused by the small-batch scan since round 5: its merge replays in place)
     int force_replay;         // test hook (tiler_debug_force_replay): the check vouches for nothing
+    int prune;                // small-batch scan with a kd-tree of > bs points: the merge kernel runs ANN's pruning
+                              // check (kd_verify_kernel's test) and replays a query it cannot vouch for itself
+    int *h_idx;               // small-batch scan: host-visible copies of the final results (null: none)
+    float *h_err;
 };
 
 __device__ __forceinline__ void write_map(const RescoreArgs &a, long q, int best) {
@@ -1098,7 +1101,6 @@ __global__ __launch_bounds__(256) void nn_scan_small_kernel(RescoreArgs a, int n
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int qg = blockIdx.y * QN;  // this workgroup's group of queries
     const int nq = min(a.nq - qg, QN), d = a.d;
-    if (a.kd_count && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.kd_count = 0;  // the merge kernel appends
     for (int i = tid; i < nq * d; i += 256)
         sq[(i / d) * SCAN_D_MAX + i % d] = a.q[(long)(qg + i / d) * d + i % d];
     __syncthreads();
@@ -1257,7 +1259,6 @@ __global__ __launch_bounds__(64) void nn_scan_orbit_kernel(RescoreArgs a, const 
     const int lane = threadIdx.x, id = blockIdx.x, xcd = id & 7, slot = id >> 3, q = slot % a.nq;
     const long b = (long)(slot / a.nq) * 8 + xcd, g = b * 64 + lane;
     if (b >= nsplit) return;  // the padding of the block count to a multiple of 8
-    if (a.kd_count && b == 0 && q == 0 && lane == 0) *a.kd_count = 0;  // the merge kernel appends
     const float *qr = qs + (long)q * D;  // uniform, restrict: the query values are scalar operands
     const int4 mj = g < G ? member[g] : make_int4(-1, -1, -1, -1);
     float cur[64];
@@ -1364,7 +1365,6 @@ __global__ __launch_bounds__(64) void nn_scan_rows_kernel(RescoreArgs a, const f
     const int lane = threadIdx.x, id = blockIdx.x, xcd = id & 7, slot = id >> 3, q = slot % a.nq;
     const long sp = (long)(slot / a.nq) * 8 + xcd;
     if (sp >= nsplit) return;  // the padding of the split count to a multiple of 8
-    if (a.kd_count && sp == 0 && q == 0 && lane == 0) *a.kd_count = 0;  // the merge kernel appends
     const int d4 = a.d >> 2, nch = a.d >> 6;  // a.d % 64 == 0
     const long nb = ((long)a.n + 63) / 64;
     const long b0 = nb * sp / nsplit, b1 = nb * (sp + 1) / nsplit;
@@ -1505,13 +1505,18 @@ __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int ns
         if (lane == 0) {
             a.out_idx[(long)q * a.k + r] = ok ? mi : -1;
             a.out_err[(long)q * a.k + r] = ok ? mv : FLT_MAX;
+            if (a.h_idx) {
+                a.h_idx[(long)q * a.k + r] = ok ? mi : -1;
+                a.h_err[(long)q * a.k + r] = ok ? mv : FLT_MAX;
+            }
             if (r == 0) write_map(a, q, ok ? mi : -1);
         }
     }
-    // ANN's pruning along every result's path (kd_verify_kernel's test): vouched for, or listed for the exact replay.
-    // Saves the root-box and verify launches of a coalesced per-tile batch: the wave forms the root box distance
-    // from registers, then each half-wave walks one result's path, one level per lane (two results per pass).
-    if (a.kd_count) {
+    // ANN's pruning along every result's path (kd_verify_kernel's test): vouched for, or replayed exactly here by
+    // lane 0 (kd_replay_query), which then rewrites the query's results and tilemap item.  Saves the root-box, verify
+    // and replay launches of a coalesced per-tile batch: the wave forms the root box distance from registers, then
+    // each half-wave walks one result's path, one level per lane (two results per pass).
+    if (a.prune) {
         const KdOrder o = *a.ko;
         if (first >= 0 && Dk < FLT_MAX) {  // uniform
             const float rb = kd_root_box_wave(o, qr, lane);
@@ -1525,7 +1530,17 @@ __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int ns
                 if (r < a.k) vouch = vouch && valid && (fb < Dk || (fb <= Dk && dr == Dk));
             }
             const bool all = __all(vouch);
-            if (lane == 0 && (!all || a.force_replay)) a.kd_list[atomicAdd(a.kd_count, 1)] = q;
+            if ((!all || a.force_replay) && lane == 0) {
+                int *oi = a.out_idx + (long)q * a.k;
+                float *oe = a.out_err + (long)q * a.k;
+                const int best = kd_replay_query<K>(o, a.rows, qr, a.k, oi, oe);
+                write_map(a, q, best);
+                if (a.h_idx)
+                    for (int r = 0; r < a.k; r++) {
+                        a.h_idx[(long)q * a.k + r] = oi[r];
+                        a.h_err[(long)q * a.k + r] = oe[r];
+                    }
+            }
         }
     }
 }
@@ -1870,7 +1885,7 @@ static bool scan_small_takes(const NNIndex *ix, int nq, int k);
 static std::atomic<int> g_force_replay{0};  // tiler_debug_force_replay
 
 int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
-                  hipStream_t stream, bool rootbox_ready, bool orbit_prepared) {
+                  hipStream_t stream, bool rootbox_ready, bool orbit_prepared, int *h_idx, float *h_err) {
     if (nq <= 0) return 0;
     if (k < 1 || k > 32) {
         set_error("nn: k must be in 1..32");
@@ -1891,6 +1906,8 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     ra.out_idx = d_idx;
     ra.out_err = d_err;
     ra.ko = ix->kd ? ix->kd->d_view : nullptr;
+    ra.h_idx = h_idx;
+    ra.h_err = h_idx ? h_err : nullptr;
     if (maps && k == 1 && ix->d_tr_tile) {
         ra.tr_tile = ix->d_tr_tile;
         ra.tr_pal = ix->d_tr_pal;
@@ -1906,24 +1923,9 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
     if (!ix->done_event) TILER_HIP_CHECK(hipEventCreateWithFlags(&ix->done_event, hipEventDisableTiming));
     if (ix->kd && scan_small_takes(ix, nq, k)) {  // the coalesced per-tile batches: scan, merge + pruning check, replay
         if (ensure_scratch(ix, nq, 0)) return -1;
-        const bool prune = ix->kd->n > ix->kd->bs;  // a single bucket: no pruning, position order is exact
-        ra.kd_list = prune ? s.kd_list : nullptr;
-        ra.kd_count = prune ? s.kd_count : nullptr;
+        ra.prune = ix->kd->n > ix->kd->bs;  // a single bucket: no pruning, position order is exact
         ra.force_replay = g_force_replay.load(std::memory_order_relaxed);
         if (search_core(ix, ra, d_q, nq, k, stream, orbit_prepared)) return -1;
-        if (prune) {
-            KdFixArgs fa{ix->d_rows, d_q, nq, k, d_idx, d_err};
-            fa.tr_tile = ra.tr_tile;
-            fa.tr_pal = ra.tr_pal;
-            fa.tr_attr = ra.tr_attr;
-            fa.m_tile = ra.m_tile;
-            fa.m_pal = ra.m_pal;
-            fa.m_hm = ra.m_hm;
-            fa.m_vm = ra.m_vm;
-            fa.list = s.kd_list;
-            fa.count = s.kd_count;
-            if (kd_replay_listed(ix->kd, fa, stream)) return -1;
-        }
         TILER_HIP_CHECK(hipEventRecord(ix->done_event, stream));
         return 0;
     }

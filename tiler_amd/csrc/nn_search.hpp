@@ -110,8 +110,11 @@ struct FtMaps {
 
 // k nearest neighbours of nq fp32 query rows in HBM; results [nq][k] in HBM; async on stream.
 // If maps is non-null (k == 1) the FrameTiling tilemap items are written too.
+// h_idx / h_err (host-visible, fine-grained pinned memory, or null): a small-batch scan (nn_search_is_small) also
+// writes its final results there from the device, so the caller needs no copy back; any other search leaves them.
 int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, float *d_err, const FtMaps *maps,
-                  hipStream_t stream, bool rootbox_ready = false, bool orbit_prepared = false);
+                  hipStream_t stream, bool rootbox_ready = false, bool orbit_prepared = false, int *h_idx = nullptr,
+                  float *h_err = nullptr);
 
 // batches of at most max_k1 queries (k = 1) / max_k8 (k <= 8) take the exhaustive small-batch scan; 0 disables it
 void nn_set_scan_limits(int max_k1, int max_k8);

@@ -319,3 +319,59 @@ def test_oracle_pri_search_matches_python_restatement(oracle, name, bs, eps):
             differ += int(oi[qi] != si[qi])
     if eps == 0.0 and name == "ints":
         assert differ > 0  # the priority search's tie order is its own (ann_kdtree_search would answer otherwise)
+
+
+@pytest.mark.parametrize("name", ["dup", "ints", "flat"])
+@pytest.mark.parametrize("bs", [1, 3])
+def test_pri_search_entry_key_rule(oracle, name, bs):
+    """The GPU's fast priority-search answer (kdtree.hip kd_pri_resolve_kernel), checked on the oracle: with D the
+    exact minimum and S the points at D, annkPriSearch returns the point of S with the smallest leaf entry key
+    (the box value after the last far step on its path) below D, bucket order inside one leaf -- whenever that
+    minimum is below D and held by a single leaf (otherwise the GPU replays)."""
+    data = _datasets()[name]
+    rng = np.random.default_rng(23)
+    n = data.shape[0]
+    qs = np.concatenate([data[rng.integers(0, n, 40)], data[rng.integers(0, n, 40)] + rng.integers(-1, 2, (40, data.shape[1])),
+                         rng.normal(0, 2, (40, data.shape[1]))]).astype(np.float32)
+    kd = oracle.KDTree(data, bs=bs)
+    oi, oe = kd.pri_search_batch(qs)
+    pos = kd.positions()
+    kd.close()
+    pidx, cd, cv, lo_b, hi_b = np_kdtree(data, bs)
+    box_lo, box_hi = data.min(0), data.max(0)
+
+    def leaf_start(p):
+        s, e = 0, n
+        while e - s > bs:
+            m = s + (e - s) // 2
+            s, e = (s, m) if p < m else (m, e)
+        return s
+
+    decided = 0
+    for qi, q in enumerate(qs):
+        d = exact_dists(data, q)
+        dm = d.min()
+        S = np.nonzero(d == dm)[0]
+        f = np.float32
+        rbv = f(0)  # annBoxDistance: the root's own entry key
+        for dd in range(q.size):
+            if q[dd] < box_lo[dd]:
+                t = f(box_lo[dd] - q[dd])
+                rbv = f(rbv + f(t * t))
+            elif q[dd] > box_hi[dd]:
+                t = f(q[dd] - box_hi[dd])
+                rbv = f(rbv + f(t * t))
+        eks = []
+        for p in S:
+            w = far_box(pos, cd, cv, lo_b, hi_b, n, bs, q, int(pos[p]), box_lo, box_hi)
+            eks.append(rbv if w == f(-np.inf) else w)  # no far step on the path: the root's chain
+        eks = np.array(eks, np.float32)
+        ekm = eks.min()
+        cand = S[eks == ekm]
+        leaves = {leaf_start(int(pos[p])) for p in cand}
+        if not (ekm < dm and len(leaves) == 1):
+            continue
+        decided += 1
+        want = cand[np.argmin(pos[cand])]
+        assert oi[qi] == want and oe[qi] == dm, qi
+    assert decided >= len(qs) // 2

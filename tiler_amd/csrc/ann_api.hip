@@ -316,6 +316,8 @@ struct ann_kdtree {
     size_t cap_ft = 0;
     void *d_pri = nullptr;        // kd_pri_search heap scratch (ann_kdtree_pri_search)
     size_t cap_pri = 0;
+    void *d_pri_aux = nullptr;    // kd_pri_resolve scratch + the replay flags
+    size_t cap_pri_aux = 0;
     PrepScratch *prep = nullptr;  // tiler_prepare_frame_tiling_dev scratch (on the global dataset's handle)
     int dev = 0;                  // the device the handle's index, stream and buffers live on
     hipEvent_t maps_ev = nullptr; // recorded after tiler_prepare_frame_tiling_dev wrote the TRTo maps (on its stream)
@@ -503,6 +505,7 @@ static void handle_free(ann_kdtree *t) {
     (void)hipFree(t->d_mh);
     (void)hipFree(t->d_mv);
     (void)hipFree(t->d_pri);
+    (void)hipFree(t->d_pri_aux);
     if (t->prep) {
         prep_scratch_free(t->prep);
         delete t->prep;
@@ -888,11 +891,30 @@ int ann_kdtree_pri_search_batch(ann_kdtree *t, const float *q, int nq, float eps
         TILER_HIP_CHECK(hipMalloc(&t->d_pri, per * chunk));
         t->cap_pri = per * chunk;
     }
+    // eps = 0: annkSearch's answer and the exact tie set decide almost every query (kd_pri_resolve); the rest, and
+    // every query of eps > 0, replay the priority search
+    const size_t aux = kd_pri_aux_bytes(chunk) + (size_t)chunk;
+    if (eps == 0.0f && aux > t->cap_pri_aux) {
+        (void)hipFree(t->d_pri_aux);
+        t->d_pri_aux = nullptr;
+        t->cap_pri_aux = 0;
+        TILER_HIP_CHECK(hipMalloc(&t->d_pri_aux, aux));
+        t->cap_pri_aux = aux;
+    }
     for (int q0 = 0; q0 < nq; q0 += chunk) {
         const int c = std::min(chunk, nq - q0);
         TILER_HIP_CHECK(hipMemcpyAsync(t->d_q, q + (size_t)q0 * ix->d, (size_t)c * ix->d * sizeof(float),
                                        hipMemcpyHostToDevice, t->stream));
-        if (kd_pri_search(ix->kd, ix->d_rows, t->d_q, c, eps, t->d_pri, t->d_idx, t->d_err, t->stream)) return -1;
+        uint8_t *flag = nullptr;
+        if (eps == 0.0f) {
+            flag = (uint8_t *)t->d_pri_aux + kd_pri_aux_bytes(chunk);
+            if (nn_search_dev(ix, t->d_q, c, 1, t->d_idx, t->d_err, nullptr, t->stream)) return -1;
+            if (kd_pri_resolve(ix->kd, ix->d_rows, t->d_q, c, t->d_err, t->d_pri_aux, t->d_idx, t->d_err, flag,
+                               t->stream))
+                return -1;
+        }
+        if (kd_pri_search(ix->kd, ix->d_rows, t->d_q, c, eps, t->d_pri, t->d_idx, t->d_err, t->stream, flag))
+            return -1;
         TILER_HIP_CHECK(hipMemcpyAsync(idx + q0, t->d_idx, (size_t)c * sizeof(int), hipMemcpyDeviceToHost, t->stream));
         TILER_HIP_CHECK(hipMemcpyAsync(err + q0, t->d_err, (size_t)c * sizeof(float), hipMemcpyDeviceToHost, t->stream));
         TILER_HIP_CHECK(hipStreamSynchronize(t->stream));

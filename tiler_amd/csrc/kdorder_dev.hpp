@@ -292,6 +292,36 @@ __device__ __forceinline__ bool kd_quad_path_ok(const KdOrder *__restrict__ op, 
     return ok;
 }
 
+// ANNkd_leaf's distance with its early break: the sequential fp32 sum of (q_d - p_d)^2 into dist, false once it
+// exceeds lim (never inserted).  Summed 8 terms per step with the step's loads issued together and the test after
+// the step: the partial sums only grow, so this is false exactly when ANN's per-term test breaks (a NaN sum never
+// breaks there either), and the sum is the same.
+__device__ __forceinline__ bool kd_leaf_dist(const float *__restrict__ qr, const float *__restrict__ pp, int dd,
+                                             float lim, float &dist) {
+    dist = 0.0f;
+    int d = 0;
+    for (; d + 8 <= dd; d += 8) {
+        float v[8], w[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            v[u] = pp[d + u];
+            w[u] = qr[d + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const float t = w[u] - v[u];
+            dist = dist + t * t;
+        }
+        if (dist > lim) return false;
+    }
+    for (; d < dd; d++) {
+        const float t = qr[d] - pp[d];
+        dist = dist + t * t;
+        if (dist > lim) return false;
+    }
+    return true;
+}
+
 // annkSearch replayed exactly for one query (kd_search.cpp; ANN.dll 0x1800128e0, ANNkd_split::ann_search 0x180012b60,
 // ANNkd_leaf::ann_search 0x180012cf0): depth-first, near child first, far child iff its box distance < the current
 // k-th key (eps = 0), leaf scans with the early break, ANNmin_k insertion (equal keys keep the first found).  One
@@ -320,14 +350,8 @@ __device__ int kd_replay_query(const KdOrder &o, const float *__restrict__ rows,
                 for (int p = f.s; p < f.e; p++) {
                     const int pt = o.pidx[p];
                     const float *pp = rows + (long)pt * o.dd;
-                    float dist = 0.0f;
-                    int d;
-                    for (d = 0; d < o.dd; d++) {
-                        const float t = qr[d] - pp[d];
-                        dist = dist + t * t;
-                        if (dist > min_dist) break;
-                    }
-                    if (d >= o.dd) {  // ANNmin_k::insert
+                    float dist;
+                    if (kd_leaf_dist(qr, pp, o.dd, min_dist, dist)) {  // ANNmin_k::insert
                         int i;
                         for (i = cnt; i > 0; i--) {
                             if (mk[i - 1] > dist) {

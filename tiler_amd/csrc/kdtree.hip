@@ -1056,9 +1056,10 @@ struct PriEntry {
 __global__ __launch_bounds__(64) void kd_pri_kernel(KdOrder o, const float *__restrict__ rows,
                                                     const float *__restrict__ q, int nq, float eps,
                                                     PriEntry *__restrict__ heap, int *__restrict__ out_idx,
-                                                    float *__restrict__ out_err) {
+                                                    float *__restrict__ out_err, const uint8_t *__restrict__ only) {
     const int qi = blockIdx.x * 64 + threadIdx.x;
     if (qi >= nq) return;
+    if (only && !only[qi]) return;  // resolved by kd_pri_resolve_kernel
     PriEntry *pq = heap + (size_t)qi * ((size_t)o.n + 1);  // pq[1..n]
     const float *qr = q + (long)qi * o.dd;
     float max_err = eps + 1.0f;
@@ -1113,14 +1114,8 @@ __global__ __launch_bounds__(64) void kd_pri_kernel(KdOrder o, const float *__re
         for (int lp = s; lp < e; lp++) {
             const int pt = o.pidx[lp];
             const float *pp = rows + (long)pt * o.dd;
-            float dist = 0.0f;
-            int d;
-            for (d = 0; d < o.dd; d++) {
-                const float t = qr[d] - pp[d];
-                dist = dist + t * t;
-                if (dist > min_dist) break;
-            }
-            if (d >= o.dd) {  // ANNmin_k::insert with k = 1: an equal key lands in slot 1 and is dropped
+            float dist;
+            if (kd_leaf_dist(qr, pp, o.dd, min_dist, dist)) {  // ANNmin_k::insert with k = 1: an equal key lands in slot 1 and is dropped
                 if (!cnt || best > dist) {
                     best = dist;
                     best_i = pt;
@@ -1134,12 +1129,139 @@ __global__ __launch_bounds__(64) void kd_pri_kernel(KdOrder o, const float *__re
     out_err[qi] = cnt ? best : FLT_MAX;
 }
 
+// The priority search's answer without the replay (eps = 0, k = 1).  Leaves leave the heap in ascending order of
+// their entry key -- the box value after the last far step on the leaf's root path, i.e. kd_path_far_box's maximum
+// (the root box without a far step): a node's entry is pushed by a chain whose key is <= its own, so it is in the
+// heap before any larger key is extracted.  Let D be the exact minimum distance and S the points at D.  A point of S
+// whose entry key is < D is visited (termination needs an extracted key >= the best so far >= D) and inserted; every
+// point of S with a larger entry key comes later and cannot replace it (ANNmin_k keeps the first of equal keys).  So
+// the answer is the point of S with the smallest entry key below D, the bucket order deciding inside one leaf.  A
+// query falls back to the replay when that is not decided this way: no point of S below D, two leaves with the same
+// smallest key (the heap's own tie order), or more than KD_PRI_CAP points within the annkSearch distance.
+static constexpr int KD_PRI_CAP = 64;
+
+// every point within d0[q] (annkSearch's distance, >= D) of query q -> list[q][.] with its exact distance
+__global__ __launch_bounds__(256) void kd_pri_ties_kernel(const float *__restrict__ rows, int n, int dd,
+                                                         const float *__restrict__ q, int nq,
+                                                         const float *__restrict__ d0, int *__restrict__ cnt,
+                                                         int *__restrict__ list, float *__restrict__ ldist) {
+    for (long r = (long)blockIdx.x * 256 + threadIdx.x; r < n; r += (long)gridDim.x * 256)
+        for (int qi = blockIdx.y; qi < nq; qi += gridDim.y) {
+            const float lim = d0[qi];
+            const float *qr = q + (long)qi * dd;
+            const float *pr = rows + r * dd;
+            float dist = 0.0f;
+            int d;
+            for (d = 0; d < dd; d++) {
+                const float t = qr[d] - pr[d];
+                dist = dist + t * t;
+                if (dist > lim) break;  // partial sums only grow
+            }
+            if (d < dd) continue;
+            const int slot = atomicAdd(cnt + qi, 1);
+            if (slot < KD_PRI_CAP) {
+                list[(long)qi * KD_PRI_CAP + slot] = (int)r;
+                ldist[(long)qi * KD_PRI_CAP + slot] = dist;
+            }
+        }
+}
+
+// one wave per query: the rule above, or the query flagged for kd_pri_kernel
+__global__ __launch_bounds__(64) void kd_pri_resolve_kernel(KdOrder o, const float *__restrict__ q, int nq,
+                                                            const int *__restrict__ cnt, const int *__restrict__ list,
+                                                            const float *__restrict__ ldist, int *__restrict__ out_idx,
+                                                            float *__restrict__ out_err, uint8_t *__restrict__ flag) {
+    const int qi = blockIdx.x, lane = threadIdx.x;
+    const float *qr = q + (long)qi * o.dd;
+    const int c = cnt[qi];
+    if (c <= 0 || c > KD_PRI_CAP) {  // uniform
+        if (lane == 0) flag[qi] = 1;
+        return;
+    }
+    const int my_i = lane < c ? list[(long)qi * KD_PRI_CAP + lane] : -1;
+    const float my_d = lane < c ? ldist[(long)qi * KD_PRI_CAP + lane] : INFINITY;
+    float dm = my_d;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dm = fminf(dm, __shfl_xor(dm, off, 64));
+    const bool in_s = lane < c && my_d == dm;
+    const float rb = kd_root_box_wave(o, qr, lane);
+    // entry keys of S's members, two per pass (one half-wave each)
+    float my_ek = INFINITY;
+    unsigned long long m = __ballot(in_s);
+    while (m) {  // uniform
+        const int a0 = __builtin_ctzll(m);
+        m &= m - 1;
+        int a1 = -1;
+        if (m) {
+            a1 = __builtin_ctzll(m);
+            m &= m - 1;
+        }
+        const int mine = (lane >> 5) ? a1 : a0;
+        const int ci = __shfl(my_i, mine < 0 ? 0 : mine, 64);
+        const float w = kd_half_path_far_box(o, qr, mine < 0 ? 0 : o.pos[ci], rb, lane);
+        const float ek = w == -INFINITY ? rb : w;
+        const float e0 = __shfl(ek, 0, 64), e1 = __shfl(ek, 32, 64);
+        if (lane == a0) my_ek = e0;
+        if (a1 >= 0 && lane == a1) my_ek = e1;
+    }
+    // the smallest entry key, then its members' leaves (start positions, from the positions alone)
+    float ekm = my_ek;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ekm = fminf(ekm, __shfl_xor(ekm, off, 64));
+    const bool cand = in_s && my_ek == ekm;
+    int leaf = 0x7fffffff, p = 0x7fffffff;
+    if (cand) {
+        p = o.pos[my_i];
+        int s = 0, e = o.n;
+        while (e - s > o.bs) {
+            const int mm = s + ((e - s) >> 1);
+            if (p < mm)
+                e = mm;
+            else
+                s = mm;
+        }
+        leaf = s;
+    }
+    int lmin = leaf, lmax = cand ? leaf : -1, pmin = p;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lmin = min(lmin, __shfl_xor(lmin, off, 64));
+        lmax = max(lmax, __shfl_xor(lmax, off, 64));
+        pmin = min(pmin, __shfl_xor(pmin, off, 64));
+    }
+    const bool decided = ekm < dm && lmin == lmax;  // uniform
+    if (lane == 0) flag[qi] = decided ? 0 : 1;
+    if (decided && cand && p == pmin) {
+        out_idx[qi] = my_i;
+        out_err[qi] = dm;
+    }
+}
+
+int kd_pri_resolve(const KdTree *t, const float *d_rows, const float *d_q, int nq, const float *d_err0, void *aux,
+                   int *d_idx, float *d_err, uint8_t *flag, hipStream_t stream) {
+    if (!t || nq <= 0) return 0;
+    int *cnt = (int *)aux;
+    int *list = cnt + nq;
+    float *ldist = (float *)(list + (size_t)nq * KD_PRI_CAP);
+    KTimer tm("kd_pri_resolve", stream);
+    TILER_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)nq * sizeof(int), stream));
+    const dim3 grid((unsigned)std::min<long>(((long)t->n + 255) / 256, 2048), (unsigned)std::min(nq, 64));
+    hipLaunchKernelGGL(kd_pri_ties_kernel, grid, dim3(256), 0, stream, d_rows, t->n, t->dd, d_q, nq, d_err0, cnt, list,
+                       ldist);
+    hipLaunchKernelGGL(kd_pri_resolve_kernel, dim3((unsigned)nq), dim3(64), 0, stream, t->view(), d_q, nq,
+                       (const int *)cnt, (const int *)list, (const float *)ldist, d_idx, d_err, flag);
+    TILER_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+size_t kd_pri_aux_bytes(int nq) { return (size_t)std::max(nq, 0) * (1 + 2 * KD_PRI_CAP) * 4; }
+
 size_t kd_pri_heap_bytes(const KdTree *t, int nq) {
     return t ? (size_t)std::max(nq, 0) * ((size_t)t->n + 1) * sizeof(PriEntry) : 0;
 }
 
 int kd_pri_search(const KdTree *t, const float *d_rows, const float *d_q, int nq, float eps, void *heap, int *d_idx,
-                  float *d_err, hipStream_t stream) {
+                  float *d_err, hipStream_t stream, const uint8_t *only) {
     if (!t || nq <= 0) return 0;
     if (!heap) {
         set_error("kd_pri_search: no heap scratch");
@@ -1147,7 +1269,7 @@ int kd_pri_search(const KdTree *t, const float *d_rows, const float *d_q, int nq
     }
     KTimer tm("kd_pri", stream);
     hipLaunchKernelGGL(kd_pri_kernel, dim3((unsigned)((nq + 63) / 64)), dim3(64), 0, stream, t->view(), d_rows, d_q,
-                       nq, eps, (PriEntry *)heap, d_idx, d_err);
+                       nq, eps, (PriEntry *)heap, d_idx, d_err, only);
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }

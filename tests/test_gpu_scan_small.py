@@ -78,3 +78,18 @@ def test_scan_small_orbit_index(gpu, oracle, k):
     qs = np.concatenate([picks[:32], picks[32:] + rng.standard_normal((32, 192)).astype(np.float32) * 0.01])
     for nq in ((1, 3, 16) if k == 8 else (1, 3, 16, 64)):
         check_nn(gpu, oracle, rows, qs[:nq], k=k)
+
+
+def test_scan_small_k8_ties(gpu, oracle):
+    """k = 8 small batches on a plain index whose rows come in groups of 4 identical copies at scattered positions
+    (a flat tile's 4 orientations in a shuffled PrepareFrameTiling set): every copy must survive the per-thread,
+    per-workgroup and merge lists in ANN's tie order.  These lists lost a
+    copy (tools/k8_plain_check.py: 28 of 256 frame tiles on the shuffled C3 rows); since round 5 a tie at or inside the
+    k-th result sends the query to the exact replay in the merge kernel."""
+    rng = np.random.default_rng(77)
+    base = rng.standard_normal((6000, 192)).astype(np.float32)
+    rows = np.concatenate([base, np.repeat(base[:1500], 3, axis=0)])[rng.permutation(6000 + 4500)]
+    picks = base[rng.choice(1500, 16, replace=False)]
+    qs = np.concatenate([picks[:8], picks[8:] + rng.standard_normal((8, 192)).astype(np.float32) * 0.05])
+    for nq in (1, 3, 16):
+        check_nn(gpu, oracle, rows, qs[:nq], k=8)

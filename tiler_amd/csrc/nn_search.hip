@@ -1429,11 +1429,60 @@ __global__ __launch_bounds__(256) void rows_interleave_kernel(const float4 *__re
 }
 
 // one wave per query: the k best of its nsplit * K partials (each split's list sorted) -> out, tilemap item
-template <int K>
-__global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int nsplit, const float *__restrict__ pd,
-                                                           const int *__restrict__ pi) {
-    const int q = blockIdx.x, lane = threadIdx.x;
+// WIDE (K > 1, nsplit <= 1024): one 1024-thread workgroup per query, one split per thread: the k best come from k
+// rounds of (distance, tie order) argmin over the splits' sorted list heads, across lanes and waves only.  The
+// one-wave form keeps up to 16 splits per lane in a per-lane K-list; those lists mis-ordered exact ties between a
+// lane's splits (tools/k8_plain_check.py: on the shuffled C3 rows 28 of 256 frame tiles lost one of a flat tile's
+// 4 identical rows), so the k = 8 small batches take this form.  Wave 0 then runs the common tail.
+template <int K, bool WIDE = false>
+__global__ __launch_bounds__(WIDE ? 1024 : 64) void nn_scan_merge_kernel(RescoreArgs a, int nsplit,
+                                                                         const float *__restrict__ pd,
+                                                                         const int *__restrict__ pi) {
+    const int q = blockIdx.x, lane = threadIdx.x & 63;
     const float *qr = a.q + (long)q * a.d;
+    __shared__ float wd[WIDE ? 16 : 1], rdw[WIDE ? 32 : 1];
+    __shared__ int wi[WIDE ? 16 : 1], riw[WIDE ? 32 : 1];
+    if constexpr (WIDE) {
+        const int tid = threadIdx.x, w = tid >> 6;
+        float hd[K];
+        int hx[K];
+#pragma unroll
+        for (int r = 0; r < K; r++) {
+            hd[r] = tid < nsplit ? pd[((long)q * nsplit + tid) * K + r] : INFINITY;
+            hx[r] = tid < nsplit ? pi[((long)q * nsplit + tid) * K + r] : 0x7fffffff;
+        }
+        int hp = 0;
+        for (int r = 0; r < a.k; r++) {
+            float v = INFINITY;
+            int vi = 0x7fffffff;
+#pragma unroll
+            for (int x = 0; x < K; x++)
+                if (x == hp) {
+                    v = hd[x];
+                    vi = hx[x];
+                }
+            float mv = v;
+            int mi = vi;
+            kd_argmin<64>(a.ko, qr, mv, mi);
+            if (lane == 0) {
+                wd[w] = mv;
+                wi[w] = mi;
+            }
+            __syncthreads();
+            if (w == 0) {
+                float v2 = lane < 16 ? wd[lane] : INFINITY;
+                int i2 = lane < 16 ? wi[lane] : 0x7fffffff;
+                kd_argmin<64>(a.ko, qr, v2, i2);
+                if (lane == 0) {
+                    rdw[r] = v2;
+                    riw[r] = i2;
+                }
+            }
+            __syncthreads();
+            if (riw[r] != 0x7fffffff && vi == riw[r]) hp++;  // the winner's split moves to its next entry
+        }
+        if (w != 0) return;
+    }
     // each lane owns the splits lane, lane + 64, ...: its running K best of their entries
     float bd[K];
     int bi[K];
@@ -1442,7 +1491,8 @@ __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int ns
         bd[r] = INFINITY;
         bi[r] = 0x7fffffff;
     }
-    if constexpr (K == 1) {  // one entry per split: 16 loads in flight per lane, then the running minimum
+    if constexpr (WIDE) {
+    } else if constexpr (K == 1) {  // one entry per split: 16 loads in flight per lane, then the running minimum
         constexpr int U = 16;
         for (int sp0 = lane; sp0 < nsplit; sp0 += 64 * U) {
             float v[U];
@@ -1483,18 +1533,23 @@ __global__ __launch_bounds__(64) void nn_scan_merge_kernel(RescoreArgs a, int ns
     int my_c = -1, first = -1;  // lane r keeps result r (the argmin is wave-uniform)
     float my_d = FLT_MAX, Dk = FLT_MAX;
     for (int r = 0; r < a.k; r++) {
-        float v = INFINITY;
-        int vi = 0x7fffffff;
+        float mv, v = INFINITY;
+        int mi, vi = 0x7fffffff;
+        if constexpr (WIDE) {
+            mv = rdw[r];
+            mi = riw[r];
+        } else {
 #pragma unroll
-        for (int x = 0; x < K; x++)
-            if (x == ptr) {
-                v = bd[x];
-                vi = bi[x];
-            }
-        float mv = v;
-        int mi = vi;
-        kd_argmin<64>(a.ko, qr, mv, mi);
-        if (vi == mi && mi != 0x7fffffff) ptr++;
+            for (int x = 0; x < K; x++)
+                if (x == ptr) {
+                    v = bd[x];
+                    vi = bi[x];
+                }
+            mv = v;
+            mi = vi;
+            kd_argmin<64>(a.ko, qr, mv, mi);
+            if (vi == mi && mi != 0x7fffffff) ptr++;
+        }
         const bool ok = mi != 0x7fffffff;
         if (lane == r) {
             my_c = ok ? mi : -1;
@@ -2021,6 +2076,10 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
     if (orb) {
         if (K == 1) scan_o(nn_scan_orbit_kernel<1>);
         else scan_o(nn_scan_orbit_kernel<8>);
+        if (K == 8 && nsplit <= 1024)
+            hipLaunchKernelGGL((nn_scan_merge_kernel<8, true>), dim3(nq), dim3(1024), 0, stream, ra, nsplit,
+                               (const float *)s.key, (const int *)s.idx);
+        else
         hipLaunchKernelGGL(K == 1 ? nn_scan_merge_kernel<1> : nn_scan_merge_kernel<8>, dim3(nq), dim3(64), 0, stream, ra,
                            nsplit, (const float *)s.key, (const int *)s.idx);
     } else if (rows_scan) {
@@ -2037,7 +2096,7 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
     } else {
         if (qn == 1) scan(nn_scan_small_kernel<1, 8>);
         else scan(nn_scan_small_kernel<SCAN_QN8, 8>);
-        hipLaunchKernelGGL(nn_scan_merge_kernel<8>, dim3(nq), dim3(64), 0, stream, ra, nsplit, (const float *)s.key,
+        hipLaunchKernelGGL((nn_scan_merge_kernel<8, true>), dim3(nq), dim3(1024), 0, stream, ra, nsplit, (const float *)s.key,
                            (const int *)s.idx);
     }
     TILER_HIP_CHECK(hipGetLastError());

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--queries", type=int, default=8192)
     ap.add_argument("--tag", default="")
     ap.add_argument("--scan-only", action="store_true", help="only the scan-kernel timings on the C3 handle")
+    ap.add_argument("--k", type=int, default=1, help="results per call (ann_kdtree_search_multi's cnt for k > 1)")
     args = ap.parse_args()
     import tiler_amd._lib as L
     if args.lib:
@@ -42,18 +43,19 @@ def main():
     _, qd = tiler_amd.psyv_batch(rgb=fr, flags=2, want64=False, want32=True)
     qd = np.ascontiguousarray(qd, np.float32)
     vp = ctypes.c_void_p
-    out = {"tag": args.tag}
+    out = {"tag": args.tag, "k": args.k}
     for name, data in (() if args.scan_only else
                        (("c3_262144", rows), ("small_12000", rows[rng.choice(rows.shape[0], 12000, replace=False)]),
                         ("plain_262144", rows[rng.permutation(rows.shape[0])]),
                         ("plain_65536", rows[rng.permutation(rows.shape[0])[:65536]]))):
         with tiler_amd.KDTree(data) as kdt:
-            bi, be = kdt.search_batch(qd)
-            n_idx = np.zeros(qd.shape[0], np.int32)
-            n_err = np.zeros(qd.shape[0], np.float32)
+            bi, be = kdt.search_batch(qd, k=args.k)
+            n_idx = np.zeros(qd.shape[0] * args.k, np.int32)
+            n_err = np.zeros(qd.shape[0] * args.k, np.float32)
+            bi, be = bi.reshape(-1), be.reshape(-1)
             wall, lone = ctypes.c_double(0), ctypes.c_double(0)
             c0 = kdt.combine_stats()
-            L.check(lib.tiler_debug_percall_bench(kdt.handle, qd.ctypes.data_as(vp), qd.shape[0], 1, 16,
+            L.check(lib.tiler_debug_percall_bench(kdt.handle, qd.ctypes.data_as(vp), qd.shape[0], args.k, 16,
                                                   n_idx.ctypes.data_as(vp), n_err.ctypes.data_as(vp),
                                                   ctypes.byref(wall), ctypes.byref(lone)), "percall")
             c1 = kdt.combine_stats()

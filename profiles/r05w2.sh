@@ -3,7 +3,7 @@
 # NN / FT / orbit / per-call GPU tests, then the per-call probe against the previous commit's build (libANN_h.so):
 # plain_262144 / plain_65536 / small_12000 are non-orbit handles (c3_262144 is a mirror-orbit index).  w3: only up
 # to 65,536 candidates.  w4: the merge kernel replays in place and writes the results to host-visible memory
-# (no replay launch, no copy back); libANN_h.so = the previous commit.
+# (no replay launch, no copy back); libANN_h.so = the previous commit.  w9: the k = 1 merge in the wide form too.
 set -eu
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r05w2}

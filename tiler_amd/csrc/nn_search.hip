@@ -2073,32 +2073,37 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
                            (const int4 *)o->d_member, ra.ko && ix->kd && ix->kd->bs == 1 ? (const GroupOrder *)o->d_gorder : nullptr,
                            (const float4 *)o->d_base, (long)o->G, nsplit, s.key, s.idx);
     };
+    // the merge: one split per thread (cross-lane selection only) when the splits fit one workgroup
+    auto merge = [&]() {
+        const float *pk = s.key;
+        const int *pj = s.idx;
+        if (nsplit <= 1024) {
+            if (K == 1)
+                hipLaunchKernelGGL((nn_scan_merge_kernel<1, true>), dim3(nq), dim3(1024), 0, stream, ra, nsplit, pk, pj);
+            else
+                hipLaunchKernelGGL((nn_scan_merge_kernel<8, true>), dim3(nq), dim3(1024), 0, stream, ra, nsplit, pk, pj);
+        } else {
+            if (K == 1)
+                hipLaunchKernelGGL(nn_scan_merge_kernel<1>, dim3(nq), dim3(64), 0, stream, ra, nsplit, pk, pj);
+            else
+                hipLaunchKernelGGL(nn_scan_merge_kernel<8>, dim3(nq), dim3(64), 0, stream, ra, nsplit, pk, pj);
+        }
+    };
     if (orb) {
         if (K == 1) scan_o(nn_scan_orbit_kernel<1>);
         else scan_o(nn_scan_orbit_kernel<8>);
-        if (K == 8 && nsplit <= 1024)
-            hipLaunchKernelGGL((nn_scan_merge_kernel<8, true>), dim3(nq), dim3(1024), 0, stream, ra, nsplit,
-                               (const float *)s.key, (const int *)s.idx);
-        else
-        hipLaunchKernelGGL(K == 1 ? nn_scan_merge_kernel<1> : nn_scan_merge_kernel<8>, dim3(nq), dim3(64), 0, stream, ra,
-                           nsplit, (const float *)s.key, (const int *)s.idx);
     } else if (rows_scan) {
         hipLaunchKernelGGL(nn_scan_rows_kernel, dim3((unsigned)(((nsplit + 7) / 8) * 8 * nq)), dim3(64), 0, stream, ra,
                            ra.q, (const float4 *)ix->d_rowsT, nsplit, s.key, s.idx);
-        hipLaunchKernelGGL(nn_scan_merge_kernel<1>, dim3(nq), dim3(64), 0, stream, ra, nsplit, (const float *)s.key,
-                           (const int *)s.idx);
     } else if (K == 1) {
         if (qn == 1) scan(nn_scan_small_kernel<1, 1>);
         else if (qn == 4) scan(nn_scan_small_kernel<4, 1>);
         else scan(nn_scan_small_kernel<SCAN_QN1, 1>);
-        hipLaunchKernelGGL(nn_scan_merge_kernel<1>, dim3(nq), dim3(64), 0, stream, ra, nsplit, (const float *)s.key,
-                           (const int *)s.idx);
     } else {
         if (qn == 1) scan(nn_scan_small_kernel<1, 8>);
         else scan(nn_scan_small_kernel<SCAN_QN8, 8>);
-        hipLaunchKernelGGL((nn_scan_merge_kernel<8, true>), dim3(nq), dim3(1024), 0, stream, ra, nsplit, (const float *)s.key,
-                           (const int *)s.idx);
     }
+    merge();
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }

@@ -2022,7 +2022,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
 // batches of up to SCAN_MAX1 / SCAN_MAX8 queries
 static constexpr int SCAN_QN1 = 16, SCAN_QN8 = 4;
 static constexpr long SCAN_ROWS_MAXN = 65536;   // nn_scan_rows_kernel up to this many candidates
-static constexpr long SCAN_ORB_MAXBLK = 4096;  // the orbit scan's splits (64-group blocks) at most: merge length
+static constexpr long SCAN_ORB_MAXBLK = 1024;  // the orbit scan's splits (64-group blocks) at most: the wide merge's
 static std::atomic<int> g_scan_max1{64}, g_scan_max8{16};  // tiler_set_scan_limits
 void nn_set_scan_limits(int max_k1, int max_k8) {
     g_scan_max1.store(std::max(0, max_k1));

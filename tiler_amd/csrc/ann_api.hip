@@ -913,7 +913,8 @@ int ann_kdtree_pri_search_batch(ann_kdtree *t, const float *q, int nq, float eps
                                t->stream))
                 return -1;
         }
-        if (kd_pri_search(ix->kd, ix->d_rows, t->d_q, c, eps, t->d_pri, t->d_idx, t->d_err, t->stream, flag))
+        if (kd_pri_search(ix->kd, ix->d_rows, t->d_q, c, eps, t->d_pri, t->d_idx, t->d_err, t->stream, flag,
+                          flag ? t->d_pri_aux : nullptr))
             return -1;
         TILER_HIP_CHECK(hipMemcpyAsync(idx + q0, t->d_idx, (size_t)c * sizeof(int), hipMemcpyDeviceToHost, t->stream));
         TILER_HIP_CHECK(hipMemcpyAsync(err + q0, t->d_err, (size_t)c * sizeof(float), hipMemcpyDeviceToHost, t->stream));

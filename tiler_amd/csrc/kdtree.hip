@@ -1056,10 +1056,12 @@ struct PriEntry {
 __global__ __launch_bounds__(64) void kd_pri_kernel(KdOrder o, const float *__restrict__ rows,
                                                     const float *__restrict__ q, int nq, float eps,
                                                     PriEntry *__restrict__ heap, int *__restrict__ out_idx,
-                                                    float *__restrict__ out_err, const uint8_t *__restrict__ only) {
+                                                    float *__restrict__ out_err, const uint8_t *__restrict__ only,
+                                                    const int *__restrict__ tcnt, const int *__restrict__ tlist) {
     const int qi = blockIdx.x * 64 + threadIdx.x;
     if (qi >= nq) return;
     if (only && !only[qi]) return;  // resolved by kd_pri_resolve_kernel
+    const bool sim = only && only[qi] == 2;  // heap order only: the first extracted leaf holding a target wins
     PriEntry *pq = heap + (size_t)qi * ((size_t)o.n + 1);  // pq[1..n]
     const float *qr = q + (long)qi * o.dd;
     float max_err = eps + 1.0f;
@@ -1078,6 +1080,12 @@ __global__ __launch_bounds__(64) void kd_pri_kernel(KdOrder o, const float *__re
     int cnt = 0, best_i = -1;
     float best = FLT_MAX;
     insert(kd_root_box(o, qr), 0, o.n);
+    int nt = 0;
+    const int *tl = nullptr;
+    if (sim) {
+        nt = tcnt[qi];
+        tl = tlist + (long)qi * 64;  // KD_PRI_CAP
+    }
     while (hn > 0) {
         const PriEntry top = pq[1];  // extr_min
         const float kn = pq[hn].key;
@@ -1091,7 +1099,7 @@ __global__ __launch_bounds__(64) void kd_pri_kernel(KdOrder o, const float *__re
             r = p << 1;
         }
         pq[p] = pq[hn + 1];
-        if (top.key * max_err >= (cnt ? best : FLT_MAX)) break;
+        if (!sim && top.key * max_err >= (cnt ? best : FLT_MAX)) break;
         const float box = top.key;
         int s = top.s, e = top.e;
         while (e - s > o.bs) {  // ANNkd_split::ann_pri_search: push the far child, continue on q's side (same box)
@@ -1109,6 +1117,21 @@ __global__ __launch_bounds__(64) void kd_pri_kernel(KdOrder o, const float *__re
                 insert((cut_diff * cut_diff - box_diff * box_diff) + box, s, m);
                 s = m;
             }
+        }
+        if (sim) {  // the leaf [s, e): its lowest-position target, if any, is the answer
+            int win = -1, wp = 0x7fffffff;
+            for (int j = 0; j < nt; j++) {
+                const int t = tl[j], pt = o.pos[t];
+                if (pt >= s && pt < e && pt < wp) {
+                    wp = pt;
+                    win = t;
+                }
+            }
+            if (win >= 0) {
+                out_idx[qi] = win;  // out_err: the minimum, written by kd_pri_resolve_kernel
+                return;
+            }
+            continue;
         }
         float min_dist = cnt ? best : FLT_MAX;  // ANNkd_leaf::ann_pri_search
         for (int lp = s; lp < e; lp++) {
@@ -1168,7 +1191,7 @@ __global__ __launch_bounds__(256) void kd_pri_ties_kernel(const float *__restric
 
 // one wave per query: the rule above, or the query flagged for kd_pri_kernel
 __global__ __launch_bounds__(64) void kd_pri_resolve_kernel(KdOrder o, const float *__restrict__ q, int nq,
-                                                            const int *__restrict__ cnt, const int *__restrict__ list,
+                                                            int *__restrict__ cnt, int *__restrict__ list,
                                                             const float *__restrict__ ldist, int *__restrict__ out_idx,
                                                             float *__restrict__ out_err, uint8_t *__restrict__ flag) {
     const int qi = blockIdx.x, lane = threadIdx.x;
@@ -1230,10 +1253,25 @@ __global__ __launch_bounds__(64) void kd_pri_resolve_kernel(KdOrder o, const flo
         pmin = min(pmin, __shfl_xor(pmin, off, 64));
     }
     const bool decided = ekm < dm && lmin == lmax;  // uniform
-    if (lane == 0) flag[qi] = decided ? 0 : 1;
+    // smallest key below D but held by several leaves: the heap's order among them decides -- kd_pri_kernel simulates
+    // the heap alone (flag 2: no leaf scans; every entry below D is extracted before the search could stop) up to the
+    // first of these leaves; the candidates go to the front of the query's list, their count to cnt[qi]
+    const bool heap_tie = ekm < dm && lmin != lmax;
+    if (lane == 0) flag[qi] = decided ? 0 : heap_tie ? 2 : 1;
     if (decided && cand && p == pmin) {
         out_idx[qi] = my_i;
         out_err[qi] = dm;
+    }
+    if (heap_tie) {  // uniform; every lane read its list entry above
+        const unsigned long long cm = __ballot(cand);
+        if (cand) {
+            const int rank = __popcll(cm & ((1ull << lane) - 1));
+            list[(long)qi * KD_PRI_CAP + rank] = my_i;
+        }
+        if (lane == 0) {
+            cnt[qi] = __popcll(cm);
+            out_err[qi] = dm;
+        }
     }
 }
 
@@ -1249,7 +1287,7 @@ int kd_pri_resolve(const KdTree *t, const float *d_rows, const float *d_q, int n
     hipLaunchKernelGGL(kd_pri_ties_kernel, grid, dim3(256), 0, stream, d_rows, t->n, t->dd, d_q, nq, d_err0, cnt, list,
                        ldist);
     hipLaunchKernelGGL(kd_pri_resolve_kernel, dim3((unsigned)nq), dim3(64), 0, stream, t->view(), d_q, nq,
-                       (const int *)cnt, (const int *)list, (const float *)ldist, d_idx, d_err, flag);
+                       cnt, list, (const float *)ldist, d_idx, d_err, flag);
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }
@@ -1261,7 +1299,7 @@ size_t kd_pri_heap_bytes(const KdTree *t, int nq) {
 }
 
 int kd_pri_search(const KdTree *t, const float *d_rows, const float *d_q, int nq, float eps, void *heap, int *d_idx,
-                  float *d_err, hipStream_t stream, const uint8_t *only) {
+                  float *d_err, hipStream_t stream, const uint8_t *only, const void *aux) {
     if (!t || nq <= 0) return 0;
     if (!heap) {
         set_error("kd_pri_search: no heap scratch");
@@ -1269,7 +1307,8 @@ int kd_pri_search(const KdTree *t, const float *d_rows, const float *d_q, int nq
     }
     KTimer tm("kd_pri", stream);
     hipLaunchKernelGGL(kd_pri_kernel, dim3((unsigned)((nq + 63) / 64)), dim3(64), 0, stream, t->view(), d_rows, d_q,
-                       nq, eps, (PriEntry *)heap, d_idx, d_err, only);
+                       nq, eps, (PriEntry *)heap, d_idx, d_err, only, aux ? (const int *)aux : nullptr,
+                       aux ? (const int *)aux + nq : nullptr);
     TILER_HIP_CHECK(hipGetLastError());
     return 0;
 }

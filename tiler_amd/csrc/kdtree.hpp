@@ -71,8 +71,9 @@ int kd_replay_listed(const KdTree *t, const KdFixArgs &a, hipStream_t stream);
 // leaf scans as annkSearch's, (1 + eps)^2 termination.  heap: kd_pri_heap_bytes(t, nq) of device scratch.
 size_t kd_pri_heap_bytes(const KdTree *t, int nq);
 // only (device flags [nq], or null = all): the queries to replay (kd_pri_resolve's fallbacks)
+// (flag 2: the heap alone up to the first leaf holding one of kd_pri_resolve's targets, read from aux)
 int kd_pri_search(const KdTree *t, const float *d_rows, const float *d_q, int nq, float eps, void *heap, int *d_idx,
-                  float *d_err, hipStream_t stream, const uint8_t *only = nullptr);
+                  float *d_err, hipStream_t stream, const uint8_t *only = nullptr, const void *aux = nullptr);
 // eps = 0: the priority search's answer from annkSearch's (d_err0 = its distances) and the exact tie set (every point
 // within that distance, then the entry keys of the points at the minimum); writes d_idx / d_err of the queries it
 // decides and flag[q] = 1 for the others (to kd_pri_search).  aux: kd_pri_aux_bytes(nq) of device scratch.

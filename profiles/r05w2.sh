@@ -4,6 +4,7 @@
 # plain_262144 / plain_65536 / small_12000 are non-orbit handles (c3_262144 is a mirror-orbit index).  w3: only up
 # to 65,536 candidates.  w4: the merge kernel replays in place and writes the results to host-visible memory
 # (no replay launch, no copy back); libANN_h.so = the previous commit.  w9: the k = 1 merge in the wide form too.
+# w10: the query row staged in LDS for the merge tail.
 set -eu
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r05w2}

@@ -185,6 +185,31 @@ def main():
     got = [x.cpu().numpy() for x in o]
     out["replica_ft_mismatches"] = int(sum(np.count_nonzero(a != b) for a, b in zip(got[:4], ref[:4])) +
                                        np.count_nonzero(got[4].view(np.uint32) != ref[4].view(np.uint32)))
+    # a device create on a caller's stream that is still busy, copied at once with no host sync in between: the copy
+    # must wait for the rows copy and index build queued on that stream (replica_of's ready_ev)
+    ods1 = dss[1][0]
+    src = torch.from_numpy(ods1).to(dev)
+    torch.cuda.synchronize(dev)
+    side = torch.cuda.Stream(dev)
+    with torch.cuda.stream(side):
+        busy = torch.rand(4096, 4096, device=dev)
+        for _ in range(24):
+            busy = busy @ busy * (1.0 / 4096)
+        rows_late = src * 1.0  # the dataset is written on `side` only after the busy work
+    kt1 = tiler_amd.KDTree(dev_ptr=rows_late.data_ptr(), n=ods1.shape[0], dd=ods1.shape[1], stream=side.cuda_stream)
+    kt1.replicate(-1)
+    q1 = torch.from_numpy(qs[1]).to(dev)
+    di1 = torch.empty(qs[1].shape[0], dtype=torch.int32, device=dev)
+    de1 = torch.empty(qs[1].shape[0], dtype=torch.float32, device=dev)
+    kt1.search_batch_dev(q1.data_ptr(), qs[1].shape[0], 1, di1.data_ptr(), de1.data_ptr())
+    torch.cuda.synchronize(dev)
+    okd = pyoracle.KDTree(ods1)
+    oi1, oe1 = okd.search_batch(qs[1])
+    okd.close()
+    out["stream_replica_mismatches"] = int(np.count_nonzero(di1.cpu().numpy() != oi1) +
+                                           np.count_nonzero(de1.cpu().numpy().view(np.uint32) != oe1.view(np.uint32)))
+    kt1.close()
+    del busy, rows_late
     lib.tiler_debug_force_replicas(0)
     for k in kdts:
         k.close()

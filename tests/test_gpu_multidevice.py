@@ -47,3 +47,4 @@ def test_all_devices_one_process():
     assert res["replica_search_mismatches"] == 0
     assert res["prepare_same"] and res["ft_dev_same"] and res["ft_host_same"]
     assert res["replica_ft_mismatches"] == 0
+    assert res["stream_replica_mismatches"] == 0

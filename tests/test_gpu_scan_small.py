@@ -83,9 +83,11 @@ def test_scan_small_orbit_index(gpu, oracle, k):
 def test_scan_small_k8_ties(gpu, oracle):
     """k = 8 small batches on a plain index whose rows come in groups of 4 identical copies at scattered positions
     (a flat tile's 4 orientations in a shuffled PrepareFrameTiling set): every copy must survive the per-thread,
-    per-workgroup and merge lists in ANN's tie order.  These lists lost a
-    copy (tools/k8_plain_check.py: 28 of 256 frame tiles on the shuffled C3 rows); since round 5 a tie at or inside the
-    k-th result sends the query to the exact replay in the merge kernel."""
+    per-workgroup and merge lists in ANN's tie order.  The round-4 merge lost a copy (tools/k8_plain_check.py: 28 of
+    256 frame tiles on the shuffled C3 rows): its per-lane K-lists over up to 16 splits were miscompiled on exact ties.
+    The merge is now the wide cross-lane one (nn_scan_merge_kernel: one split per thread, k rounds of argmin over the
+    split heads, no per-lane list), and the per-thread lists of the scan insert through kd_list_insert
+    (test_gpu_list_ties.py places the copies in one old merge lane and in one scan thread on purpose)."""
     rng = np.random.default_rng(77)
     base = rng.standard_normal((6000, 192)).astype(np.float32)
     rows = np.concatenate([base, np.repeat(base[:1500], 3, axis=0)])[rng.permutation(6000 + 4500)]

@@ -321,6 +321,8 @@ struct ann_kdtree {
     PrepScratch *prep = nullptr;  // tiler_prepare_frame_tiling_dev scratch (on the global dataset's handle)
     int dev = 0;                  // the device the handle's index, stream and buffers live on
     hipEvent_t maps_ev = nullptr; // recorded after tiler_prepare_frame_tiling_dev wrote the TRTo maps (on its stream)
+    hipEvent_t ready_ev = nullptr; // recorded after the rows copy and index build of ann_kdtree_create_dev_ex, on the
+                                   // caller's stream when one was passed (replica_of waits for it before a peer copy)
     long long placed = 0;         // dataset bytes counted in g_dev_load[dev]
     // copies of this handle's index on other devices (tiler_kdtree_replicate, or made on first use by a device entry
     // point whose buffers live there): rows peer-copied over xGMI, the same index built there
@@ -474,14 +476,26 @@ ann_kdtree *ann_kdtree_create_dev_ex(const float *d_rows_in, int n, int dd, int 
         std::lock_guard<std::mutex> lk(g_place_mu);
         g_dev_load[dev] += t->placed;
     }
-    TILER_HIP_CHECK_NULL(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking));
-    hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+    // every failure below releases the handle (handle_free also takes its bytes back out of g_dev_load)
     float *d_rows = nullptr;
     const size_t bytes = (size_t)n * dd * sizeof(float);
-    TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_rows, std::max<size_t>(4, bytes)));
-    if (n > 0) TILER_HIP_CHECK_NULL(hipMemcpyAsync(d_rows, d_rows_in, bytes, hipMemcpyDeviceToDevice, s));
+    const bool ok_stream = hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) == hipSuccess;
+    hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+    if (!ok_stream || hipMalloc((void **)&d_rows, std::max<size_t>(4, bytes)) != hipSuccess ||
+        (n > 0 && hipMemcpyAsync(d_rows, d_rows_in, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)) {
+        set_error("ann_kdtree_create_dev: device allocation or copy failed");
+        if (d_rows) (void)hipFree(d_rows);
+        handle_free(t);
+        return nullptr;
+    }
     t->ix = nn_index_create_dev(d_rows, n, dd, bs, split, s);
     if (!t->ix) {
+        handle_free(t);
+        return nullptr;
+    }
+    // the rows copy and the index build are queued on s: a replica made from another device must wait for them
+    if (hipEventCreateWithFlags(&t->ready_ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(t->ready_ev, s) != hipSuccess) {
+        set_error("ann_kdtree_create_dev: event record failed");
         handle_free(t);
         return nullptr;
     }
@@ -520,6 +534,7 @@ static void handle_free(ann_kdtree *t) {
         if (cs.stream) (void)hipStreamDestroy(cs.stream);
     }
     if (t->maps_ev) (void)hipEventDestroy(t->maps_ev);
+    if (t->ready_ev) (void)hipEventDestroy(t->ready_ev);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     unplace_handle(t->dev, t->placed);
     delete t;
@@ -550,8 +565,11 @@ static ann_kdtree *replica_of(ann_kdtree *t, int dev) {
     }
     float *d_rows = nullptr;
     const size_t bytes = (size_t)src->n * src->d * sizeof(float);
-    // the source's own stream has finished building it (creates return with the index queued on it)
-    if (hipStreamSynchronize(t->stream) != hipSuccess || (src->done_event && hipEventSynchronize(src->done_event) != hipSuccess) ||
+    // the source is complete before it is copied: its own stream (creates return with the index queued on it), the
+    // caller's stream of a device create (ready_ev) and of the Prepare that wrote its TRTo maps (maps_ev), its searches
+    if (hipStreamSynchronize(t->stream) != hipSuccess || (t->ready_ev && hipEventSynchronize(t->ready_ev) != hipSuccess) ||
+        (t->maps_ev && hipEventSynchronize(t->maps_ev) != hipSuccess) ||
+        (src->done_event && hipEventSynchronize(src->done_event) != hipSuccess) ||
         hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void **)&d_rows, std::max<size_t>(4, bytes)) != hipSuccess ||
         (bytes && hipMemcpyPeerAsync(d_rows, dev, src->d_rows, t->dev, bytes, r->stream) != hipSuccess)) {

@@ -101,6 +101,38 @@ __device__ __forceinline__ bool kd_less(const KdOrder *op, const float *__restri
     return da < db || (da == db && kd_before(op, q, a, b));
 }
 
+// Insert (x, xi) into a lane's K-list (bd, bi) sorted by (distance, ANN order), as the shifting insertion
+//     p = n;  while (p > 0 && kd_less(x, list[p-1])) { list[p] = list[p-1]; p--; }  list[p] = x;
+// does (n = the slot that receives the last entry: K - 1 for a full list, the count while it fills; the caller has
+// already checked that x enters the list) -- in two phases.  First the position: the test of every slot below n,
+// the tie walk only on an equal distance, no list register written.  Then the move: straight-line selects on the
+// known position, no call and no branch.  The shifting loop itself is miscompiled by this toolchain (ROCm 7.2, gfx950)
+// when its tie test is more than one block (the kd_before_tree call, inlined or not): the shifted copy of the list is
+// formed ahead of the divergent tie test, and the join's phi copies -- the unshifted list, for the lanes whose test
+// fails -- are placed in the structurizer's flow block, which the lanes whose tie test succeeds execute too, into the
+// same registers; such a lane then keeps an unshifted slot, so one entry is lost and its neighbour listed twice.  The
+// optimised LLVM IR is correct, the ISA is not (DESIGN §4 "A k = 8 correctness fix", tools/merge_tie_repro.hip,
+// profiles/r06/tie_repro.txt: 53-57 of 64 lanes corrupted; 0 with the tie test a single compare, 0 in this form).
+template <int K>
+__device__ __forceinline__ void kd_list_insert(const KdOrder *op, const float *__restrict__ q, float (&bd)[K],
+                                               int (&bi)[K], float x, int xi, int n = K - 1) {
+    bool f[K];
+#pragma unroll
+    for (int i = 0; i < K - 1; i++) f[i] = i < n && kd_less(op, q, x, xi, bd[i], bi[i]);
+    int p = n;  // the loop's stop: the lowest slot of the run of passed tests that ends at slot n - 1
+#pragma unroll
+    for (int i = K - 2; i >= 0; i--)
+        if (f[i] && p == i + 1) p = i;
+#pragma unroll
+    for (int i = K - 1; i > 0; i--) {
+        const bool sh = i > p && i <= n;
+        bd[i] = sh ? bd[i - 1] : (i == p ? x : bd[i]);
+        bi[i] = sh ? bi[i - 1] : (i == p ? xi : bi[i]);
+    }
+    bd[0] = p == 0 ? x : bd[0];
+    bi[0] = p == 0 ? xi : bi[0];
+}
+
 // (dist, kd order) minimum over lanes xor-reachable below `width` (64: the wave, 32: a half-wave, 4: a quad)
 template <int WIDTH>
 __device__ __forceinline__ void kd_argmin(const KdOrder *o, const float *__restrict__ q, float &v, int &i) {

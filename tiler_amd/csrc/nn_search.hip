@@ -952,14 +952,7 @@ __global__ __launch_bounds__(256) void nn_rescore2_kernel(RescoreArgs a, int jba
             const int idx = a.cbuf[j * a.cap + e];
             const float dist = exact_dist(qrow, a.rows + (long)idx * a.d, a.d);
             if (!kd_less(a.ko, qrow, dist, idx, bd[7], bi[7])) continue;
-            int p = 7;  // (dist, tie order) insertion (entries arrive in no particular order)
-            while (p > 0 && kd_less(a.ko, qrow, dist, idx, bd[p - 1], bi[p - 1])) {
-                bd[p] = bd[p - 1];
-                bi[p] = bi[p - 1];
-                p--;
-            }
-            bd[p] = dist;
-            bi[p] = idx;
+            kd_list_insert<8>(a.ko, qrow, bd, bi, dist, idx);  // (dist, tie order); entries arrive in no order
         }
         int ptr = 0;
         for (int r = 0; r < a.k; r++) {
@@ -1020,18 +1013,10 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(RescoreArgs a, int list_n
             }
             if (i < a.d) continue;
             if (cnt == K && !kd_less(a.ko, sq, dist, j, bd[K - 1], bi[K - 1])) continue;
-            if (!a.ko) {
+            if (!a.ko)
                 list_insert<K>(bd, bi, dist, j);  // j ascends: an equal key stays behind, as index order wants
-            } else {
-                int p = (cnt < K) ? cnt : K - 1;
-                while (p > 0 && kd_less(a.ko, sq, dist, j, bd[p - 1], bi[p - 1])) {
-                    bd[p] = bd[p - 1];
-                    bi[p] = bi[p - 1];
-                    p--;
-                }
-                bd[p] = dist;
-                bi[p] = j;
-            }
+            else
+                kd_list_insert<K>(a.ko, sq, bd, bi, dist, j, cnt < K ? cnt : K - 1);
             if (cnt < K) cnt++;
         }
 #pragma unroll
@@ -1168,14 +1153,7 @@ __global__ __launch_bounds__(256) void nn_scan_small_kernel(RescoreArgs a, int n
             if (q >= nq) break;
             const float *qr = sq + q * SCAN_D_MAX;
             if (!kd_less(a.ko, qr, dist[q], (int)j, bd[q][K - 1], bi[q][K - 1])) continue;
-            int p = K - 1;  // j ascends in this thread: insertion keeps (distance, tie order)
-            while (p > 0 && kd_less(a.ko, qr, dist[q], (int)j, bd[q][p - 1], bi[q][p - 1])) {
-                bd[q][p] = bd[q][p - 1];
-                bi[q][p] = bi[q][p - 1];
-                p--;
-            }
-            bd[q][p] = dist[q];
-            bi[q][p] = (int)j;
+            kd_list_insert<K>(a.ko, qr, bd[q], bi[q], dist[q], (int)j);  // keeps (distance, tie order)
         }
     }
     // per query: the workgroup's K best, K rounds of (distance, tie order) argmin over the threads' sorted lists
@@ -1428,21 +1406,20 @@ __global__ __launch_bounds__(256) void rows_interleave_kernel(const float4 *__re
     }
 }
 
-// one wave per query: the k best of its nsplit * K partials (each split's list sorted) -> out, tilemap item
-// WIDE (K > 1, nsplit <= 1024): one 1024-thread workgroup per query, one split per thread: the k best come from k
-// rounds of (distance, tie order) argmin over the splits' sorted list heads, across lanes and waves only.  The
-// one-wave form keeps up to 16 splits per lane in a per-lane K-list; those lists mis-ordered exact ties between a
-// lane's splits (tools/k8_plain_check.py: on the shuffled C3 rows 28 of 256 frame tiles lost one of a flat tile's
-// 4 identical rows), so the k = 8 small batches take this form.  Wave 0 then runs the common tail.
-template <int K, bool WIDE = false>
-__global__ __launch_bounds__(WIDE ? 1024 : 64) void nn_scan_merge_kernel(RescoreArgs a, int nsplit,
-                                                                         const float *__restrict__ pd,
-                                                                         const int *__restrict__ pi) {
+// one 1024-thread workgroup per query (nsplit <= 1024, checked on the host), one split per thread: the k best of the
+// query's nsplit * K partials (each split's list sorted) come from k rounds of (distance, tie order) argmin over the
+// splits' list heads, across lanes and waves only -- no per-lane list.  Wave 0 then runs the common tail (results,
+// tilemap item, ANN's pruning check, in-place replay).  Until round 5 a one-wave form kept up to 16 splits per lane in
+// a per-lane K-list; its shifting insertion was miscompiled on exact ties (kdorder_dev.hpp kd_list_insert, DESIGN §4
+// "A k = 8 correctness fix") and it was removed.
+template <int K>
+__global__ __launch_bounds__(1024) void nn_scan_merge_kernel(RescoreArgs a, int nsplit, const float *__restrict__ pd,
+                                                             const int *__restrict__ pi) {
     const int q = blockIdx.x, lane = threadIdx.x & 63;
     const float *qr = a.q + (long)q * a.d;
-    __shared__ float wd[WIDE ? 16 : 1], rdw[WIDE ? 32 : 1];
-    __shared__ int wi[WIDE ? 16 : 1], riw[WIDE ? 32 : 1];
-    if constexpr (WIDE) {
+    __shared__ float wd[16], rdw[32];
+    __shared__ int wi[16], riw[32];
+    {
         const int tid = threadIdx.x, w = tid >> 6;
         float hd[K];
         int hx[K];
@@ -1483,73 +1460,11 @@ __global__ __launch_bounds__(WIDE ? 1024 : 64) void nn_scan_merge_kernel(Rescore
         }
         if (w != 0) return;
     }
-    // each lane owns the splits lane, lane + 64, ...: its running K best of their entries
-    float bd[K];
-    int bi[K];
-#pragma unroll
-    for (int r = 0; r < K; r++) {
-        bd[r] = INFINITY;
-        bi[r] = 0x7fffffff;
-    }
-    if constexpr (WIDE) {
-    } else if constexpr (K == 1) {  // one entry per split: 16 loads in flight per lane, then the running minimum
-        constexpr int U = 16;
-        for (int sp0 = lane; sp0 < nsplit; sp0 += 64 * U) {
-            float v[U];
-            int vi[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int sp = sp0 + 64 * u;
-                v[u] = INFINITY;
-                vi[u] = 0x7fffffff;
-                if (sp < nsplit) {
-                    v[u] = pd[(long)q * nsplit + sp];
-                    vi[u] = pi[(long)q * nsplit + sp];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                if (vi[u] != 0x7fffffff && kd_less(a.ko, qr, v[u], vi[u], bd[0], bi[0])) {
-                    bd[0] = v[u];
-                    bi[0] = vi[u];
-                }
-        }
-    } else
-    for (int sp = lane; sp < nsplit; sp += 64)
-        for (int r = 0; r < K; r++) {
-            const float v = pd[((long)q * nsplit + sp) * K + r];
-            const int vi = pi[((long)q * nsplit + sp) * K + r];
-            if (vi == 0x7fffffff || !kd_less(a.ko, qr, v, vi, bd[K - 1], bi[K - 1])) break;  // the split's list is sorted
-            int p = K - 1;
-            while (p > 0 && kd_less(a.ko, qr, v, vi, bd[p - 1], bi[p - 1])) {
-                bd[p] = bd[p - 1];
-                bi[p] = bi[p - 1];
-                p--;
-            }
-            bd[p] = v;
-            bi[p] = vi;
-        }
-    int ptr = 0;
     int my_c = -1, first = -1;  // lane r keeps result r (the argmin is wave-uniform)
     float my_d = FLT_MAX, Dk = FLT_MAX;
     for (int r = 0; r < a.k; r++) {
-        float mv, v = INFINITY;
-        int mi, vi = 0x7fffffff;
-        if constexpr (WIDE) {
-            mv = rdw[r];
-            mi = riw[r];
-        } else {
-#pragma unroll
-            for (int x = 0; x < K; x++)
-                if (x == ptr) {
-                    v = bd[x];
-                    vi = bi[x];
-                }
-            mv = v;
-            mi = vi;
-            kd_argmin<64>(a.ko, qr, mv, mi);
-            if (vi == mi && mi != 0x7fffffff) ptr++;
-        }
+        const float mv = rdw[r];
+        const int mi = riw[r];
         const bool ok = mi != 0x7fffffff;
         if (lane == r) {
             my_c = ok ? mi : -1;
@@ -2057,6 +1972,10 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
     const int nsplit = orb ? (int)nblk
                            : rows_scan ? (int)std::max<long>(1, ((long)ix->n + 63) / 64)
                                        : (int)std::max<long>(1, std::min<long>(1024, ((long)ix->n + 255) / 256));
+    if (nsplit > 1024) {  // the merge holds one split per thread of one workgroup (the caps above keep this)
+        set_error("scan_small: " + std::to_string(nsplit) + " candidate splits exceed the merge's 1024");
+        return -1;
+    }
     if (ensure_scratch(ix, nq, (long)nq * nsplit * K)) return -1;
     SearchScratch &s = ix->scratch;
     ix->last_splits = 0;  // the stats report no tier-2 / tier-3 queries for a scan (fb_count is not read)
@@ -2073,21 +1992,14 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
                            (const int4 *)o->d_member, ra.ko && ix->kd && ix->kd->bs == 1 ? (const GroupOrder *)o->d_gorder : nullptr,
                            (const float4 *)o->d_base, (long)o->G, nsplit, s.key, s.idx);
     };
-    // the merge: one split per thread (cross-lane selection only) when the splits fit one workgroup
+    // the merge: one split per thread (cross-lane selection only)
     auto merge = [&]() {
         const float *pk = s.key;
         const int *pj = s.idx;
-        if (nsplit <= 1024) {
-            if (K == 1)
-                hipLaunchKernelGGL((nn_scan_merge_kernel<1, true>), dim3(nq), dim3(1024), 0, stream, ra, nsplit, pk, pj);
-            else
-                hipLaunchKernelGGL((nn_scan_merge_kernel<8, true>), dim3(nq), dim3(1024), 0, stream, ra, nsplit, pk, pj);
-        } else {
-            if (K == 1)
-                hipLaunchKernelGGL(nn_scan_merge_kernel<1>, dim3(nq), dim3(64), 0, stream, ra, nsplit, pk, pj);
-            else
-                hipLaunchKernelGGL(nn_scan_merge_kernel<8>, dim3(nq), dim3(64), 0, stream, ra, nsplit, pk, pj);
-        }
+        if (K == 1)
+            hipLaunchKernelGGL(nn_scan_merge_kernel<1>, dim3(nq), dim3(1024), 0, stream, ra, nsplit, pk, pj);
+        else
+            hipLaunchKernelGGL(nn_scan_merge_kernel<8>, dim3(nq), dim3(1024), 0, stream, ra, nsplit, pk, pj);
     };
     if (orb) {
         if (K == 1) scan_o(nn_scan_orbit_kernel<1>);

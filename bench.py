@@ -90,7 +90,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # TILER_BENCH_ONE_DEVICE=1: every rank on cuda:0 (rehearsal of the N>1 path on a one-GPU box, gloo)
     devi = 0 if os.environ.get("TILER_BENCH_ONE_DEVICE") == "1" else local
-    if world > 1:
+    # under a launcher the process group is made even at WORLD_SIZE=1, so the RCCL branch (broadcast, barriers, the
+    # max-over-ranks all-reduce) is the one that runs; a bare `python bench.py` stays single-process
+    use_dist = env_world is not None
+    if use_dist:
         torch.cuda.set_device(devi)
         dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", devi)
@@ -118,7 +121,7 @@ def main():
         t_packed = torch.from_numpy(packed).to(cdev)
     else:
         t_packed = torch.empty(TS * 64 + 3 * TS + P * 16, dtype=torch.int32, device=cdev)
-    if world > 1:
+    if use_dist:
         dist.broadcast(t_packed, 0)
     packed = t_packed.cpu().numpy()
     o = 0
@@ -179,14 +182,14 @@ def main():
     torch.cuda.synchronize(dev)
     lib.tiler_timing_reset()
     lib.tiler_timing_enable(1)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     print(f"[bench] {args.steps} steps in {elapsed:.3f} s", file=sys.stderr, flush=True)
@@ -205,11 +208,11 @@ def main():
         kernels[name] = {"ms_total": round(ms, 4), "launches": n.value,
                          "ms_avg": round(ms / n.value, 4) if n.value else None}
     stats = kdt.stats()
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ranks_seen = dist.get_world_size() if world > 1 else 1
+    ranks_seen = dist.get_world_size() if use_dist else 1
     total_tiles = QK * args.steps * ranks_seen
     value = total_tiles / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
@@ -529,6 +532,7 @@ def main():
     if rank == 0:
         res = {
             "metric": METRIC, "value": round(value, 4), "unit": "Mtiles/s", "n_gpus": world, "ranks_seen": ranks_seen,
+            "process_group": dist.get_backend() if use_dist else None,
             "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded, SURVEY.md 8(d))",
@@ -544,7 +548,7 @@ def main():
         }
         print(json.dumps(res))
     kdt.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -137,12 +137,16 @@ def test_run_all_chain_bit_exact(gpu, oracle, quality):
         assert np.array_equal(items[live, 0], t[live]) and np.array_equal(items[live, 1], attrs[live])
 
 
-def _dist_worker(rank, world, port, out, quality):
+def _dist_worker(rank, world, port, out, quality, backend="gloo"):
     import os
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)  # RCCL: the collective tensors live in this rank's HBM (dist.comm_device)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     import tiler_amd
+    from tiler_amd import dist as td
     from tiler_amd._lib import check
     from tiler_amd.encoder import DistributedEncoder
     check(tiler_amd.load().tiler_init(0), "tiler_init")  # every rank on the one GPU of the test box
@@ -150,9 +154,15 @@ def _dist_worker(rank, world, port, out, quality):
     e = DistributedEncoder(v, device=0)
     sm = e.run_all(700, quality, 0.2)
     data = e.save_stream(320, 240, 24.0)  # a collective: every rank calls it, rank 0 gets the bytes
-    assert e.frames == e.frame_idx.size < v.frames  # only this rank's keyframes are held
+    assert e.frames == e.frame_idx.size
+    if world > 1:
+        assert e.frame_idx.size < v.frames  # only this rank's keyframes are held
+    # the reduced tileset from rank 0 (the north star's tileset exchange), through the backend's device
+    tiles = td.broadcast_array(e.palpix if rank == 0 else None, e.palpix.shape, e.palpix.dtype)
+    assert np.array_equal(tiles, e.palpix)
     np.savez(out + f".{rank}.npz", frame_idx=e.frame_idx, palpix=e.palpix, tile=e.tile, pal=e.pal, hm=e.hm, vm=e.vm,
-             sm_tile=sm["tile"], sm_smoothed=sm["smoothed"],
+             sm_tile=sm["tile"], sm_smoothed=sm["smoothed"], comm_device=str(td.comm_device()),
+             backend=dist.get_backend(),
              gtm=np.frombuffer(data, np.uint8) if data is not None else np.zeros(0, np.uint8))
     dist.barrier()
     dist.destroy_process_group()
@@ -189,6 +199,35 @@ def test_run_all_chain_two_ranks_match_single_process(gpu, tmp_path):
         else:
             assert got["gtm"].size == 0
     assert seen.all()
+
+
+@pytest.mark.gpu
+def test_run_all_chain_nccl_world1_matches_single_process(gpu, tmp_path):
+    """The product's RCCL branch executed: DistributedEncoder at world size 1 on the nccl
+    backend -- the merge-map MAX and UseCount SUM all-reduces, gather_units' stream lengths and the tileset broadcast
+    run as device tensors through RCCL (dist.comm_device = the rank's GPU) -- ends in exactly the single-process state
+    and .gtm bytes."""
+    import socket
+    import torch.multiprocessing as mp
+    from tiler_amd.encoder import Encoder
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "n.npz")
+    mp.spawn(_dist_worker, args=(1, port, out, FT_MEDIUM, "nccl"), nprocs=1, join=True)
+    v = synth.video(61, 320, 240, kf_frames=(3, 2, 3), n_palettes=8)
+    e = Encoder(v)
+    sm = e.run_all(700, FT_MEDIUM, 0.2)
+    data = e.save_stream(320, 240, 24.0)
+    got = np.load(out + ".0.npz")
+    assert str(got["backend"]) == "nccl" and str(got["comm_device"]).startswith("cuda")
+    assert np.array_equal(got["frame_idx"], np.arange(v.frames))
+    assert np.array_equal(got["palpix"], e.palpix)
+    for k, a in (("tile", e.tile), ("pal", e.pal), ("hm", e.hm), ("vm", e.vm), ("sm_tile", sm["tile"]),
+                 ("sm_smoothed", sm["smoothed"])):
+        assert np.array_equal(got[k], a), k
+    assert got["gtm"].tobytes() == data
 
 
 @pytest.mark.gpu

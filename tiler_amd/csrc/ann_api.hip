@@ -938,6 +938,10 @@ int ann_kdtree_pri_search_batch(ann_kdtree *t, const float *q, int nq, float eps
         TILER_HIP_CHECK(hipMemcpyAsync(err + q0, t->d_err, (size_t)c * sizeof(float), hipMemcpyDeviceToHost, t->stream));
         TILER_HIP_CHECK(hipStreamSynchronize(t->stream));
     }
+    // the heap scratch (up to 1 GiB) is not kept on the handle: several keyframe handles would each pin it
+    (void)hipFree(t->d_pri);
+    t->d_pri = nullptr;
+    t->cap_pri = 0;
     return 0;
 }
 

@@ -1094,12 +1094,30 @@ __global__ __launch_bounds__(32 * (KM_A / NSLICE)) void kmb_seq_apply(KmBatch B,
 // is re-initialised), so a result never depends on residency.  Same updates, same partition-independent argmax
 // (value, then the largest index), so the centres are those of the per-launch rounds.
 static constexpr int KM_FF_NT = 512;
+static constexpr int KM_FF_SUBMAX = 512;  // farthest-first items (subs) per bin at most
 
-__device__ __forceinline__ bool km_grid_sync(unsigned *bar, unsigned epoch, unsigned *fail) {
+// Study build only (-DTILER_KM_STAMPS, tools/ff_stamps.py; never in the shipped library): thread 0 of every workgroup
+// stamps the 100 MHz real-time counter at 8 points of two windows of 64 rounds (rounds 64..127, and the 64 rounds
+// from Kmax - 128 on, when only the largest bin is alive).  The stamp at "row landed" waits for the centre row.
+#ifdef TILER_KM_STAMPS
+__device__ unsigned long long g_km_stamps[2][64][256][8];
+__device__ __forceinline__ void km_stamp(int j, int Kmax, int pt) {
+    if (threadIdx.x != 0 || blockIdx.x >= 256) return;
+    const int w = (j >= 64 && j < 128) ? 0 : (j >= Kmax - 128 && j < Kmax - 64) ? 1 : -1;
+    if (w >= 0) g_km_stamps[w][j - (w ? Kmax - 128 : 64)][blockIdx.x][pt] = __builtin_amdgcn_s_memrealtime();
+}
+#define KM_STAMP(j, Kmax, pt) km_stamp(j, Kmax, pt)
+#else
+#define KM_STAMP(j, Kmax, pt) ((void)0)
+#endif
+
+__device__ __forceinline__ bool km_grid_sync(unsigned *bar, unsigned epoch, unsigned *fail, int Kmax = 0) {
     __shared__ int s_ok;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores have left (R1 drain)
     __syncthreads();
+    (void)Kmax;
     if (threadIdx.x == 0) {
+        KM_STAMP((int)epoch - 1, Kmax, 5);
         const int G = (int)gridDim.x, g = (int)(blockIdx.x & 7);
         const unsigned ng = (unsigned)((G - g + 7) >> 3), ngroups = (unsigned)min(G, 8);
         int ok = 1;
@@ -1107,6 +1125,7 @@ __device__ __forceinline__ bool km_grid_sync(unsigned *bar, unsigned epoch, unsi
         if (__hip_atomic_fetch_add(bar + 32 * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch * ng - 1u &&
             __hip_atomic_fetch_add(bar + 256, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch * ngroups - 1u)
             for (int x = 0; x < 8; x++) __hip_atomic_store(bar + 288 + 32 * x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        KM_STAMP((int)epoch - 1, Kmax, 6);
         for (unsigned spins = 0; __hip_atomic_load(bar + 288 + 32 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch;) {
             if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || ++spins > (1u << 20)) {
                 __hip_atomic_store(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1115,6 +1134,7 @@ __device__ __forceinline__ bool km_grid_sync(unsigned *bar, unsigned epoch, unsi
             }
             __builtin_amdgcn_s_sleep(2);
         }
+        KM_STAMP((int)epoch - 1, Kmax, 7);
         s_ok = ok;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below the poll
@@ -1122,39 +1142,52 @@ __device__ __forceinline__ bool km_grid_sync(unsigned *bar, unsigned epoch, unsi
     return s_ok != 0;
 }
 
-// (value, largest index) maximum of a packed u64 over the workgroup; red[] holds one word per wave
-__device__ __forceinline__ unsigned long long km_block_max(unsigned long long v, unsigned long long *red) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long ov = ((unsigned long long)__shfl_xor((unsigned)(v >> 32), o, 64) << 32) |
-                                      (unsigned)__shfl_xor((unsigned)v, o, 64);
-        v = ov > v ? ov : v;
-    }
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    unsigned long long m = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); w++) m = red[w] > m ? red[w] : m;
-    __syncthreads();  // red[] is reused
-    return m;
-}
-
-// Farthest-first with the selection after the barrier (round 3, r03zo): every item of round j stores its candidate
+// The farthest-first protocol (round 3, r03zo; kmb_ff_persist2 until round 6, now kmb_ff_persist3 below): every item of round j stores its candidate
 // (sc1) into the round's parity half of the part slots and arrives; after the barrier EVERY item of a bin reduces
 // that bin's candidates itself (the same partition-independent maximum, so the same centre) instead of the last item
 // to finish selecting and publishing it.  Gone per round: the ffdone count, the selector's candidate loads, the
 // centre's sc1 publication and its load -- three dependent device-scope round trips of the ~11 on a round's
 // critical path.  The slots alternate halves by round parity: round j + 1's stores cannot reach a half that a slow
 // workgroup still reads for round j (it has not arrived at barrier j + 1 yet).  The used flag of a point is written
-// and read only by the thread that scans it (item u always on workgroup u % G, point i on lane i % KM_FF_NT), centres
-// and their rows for the later kernels by the bin's sub-0 item (plain stores: nothing in this launch reads them).
-__global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist2(KmBatch B, const KmFfItem *items, const int *ff_end,
+// and read only by the lane that scans it, centres and their rows for the later kernels by the bin's sub-0 item
+// (plain stores: nothing in this launch reads them).
+
+// (value, largest index) maximum of a packed u64 over the wave
+__device__ __forceinline__ unsigned long long km_wave_max(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long ov = ((unsigned long long)__shfl_xor((unsigned)(v >> 32), o, 64) << 32) |
+                                      (unsigned)__shfl_xor((unsigned)v, o, 64);
+        v = ov > v ? ov : v;
+    }
+    return v;
+}
+
+// Farthest-first with WAVE work items (round 6).  Round stamps of kmb_ff_persist2 (tools/ff_stamps.py,
+// profiles/r06/ff_stamps_persist2.json) put the time in the items, not the barrier: a round with only the largest bin
+// alive took 7.4 us (barrier ~2.5 us of it), but rounds with every bin alive took 60 us, because each workgroup ran its
+// ~13 (bin, sub) items one after another, each a dependent chain (candidate slots -> centre -> its row -> scan ->
+// reduce) of ~4.6 us over only ~2 points per thread.  Here an item is one wave's: lane l of sub s owns the points
+// s * 64 + l + k * nsub * 64 (the slot layout, used flags and candidate protocol of kmb_ff_persist2 per item, the
+// reductions wave shuffles with no workgroup barrier), item u always on wave slot u % (8 G) -- wave u / G of workgroup
+// u % G, so consecutive items sit on different CUs and a point's min-distance word stays with one lane -- so a
+// workgroup's 8 waves run 8 items concurrently.  Items hold ~256 points (4 per lane, loaded together): a bin has
+// min(512, n / 256) subs.  The same partition-independent maximum, so the same centres.  C4 (r06f, one box): 101 ms
+// (persist2) -> 79 ms (wave items, one load at a time) -> 56 ms (slot and point loads in flight together); rounds with
+// every bin alive 60 -> 21 us, with the largest bin alone 7.4 -> 7.9 us (profiles/r06/ff_stamps_*.json).  Measured and
+// not kept: two items per wave carried together (256 VGPRs, 111 spilled) and ~512-point items (59.5 ms: the early
+// rounds stream 80 MB of rows each and fewer, longer items lose more to latency than they save in slots).
+__global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist3(KmBatch B, const KmFfItem *items, const int *ff_end,
                                                             int Kmax, unsigned *bar, unsigned *fail) {
-    __shared__ unsigned long long red[KM_FF_NT / 64];
+    constexpr int NWV = KM_FF_NT / 64;
+    const int lane = threadIdx.x & 63, G = (int)gridDim.x, NWS = G * NWV;
+    const int ws = (int)(threadIdx.x >> 6) * G + (int)blockIdx.x;
     int alive = B.nb;
     const long half = B.poff[B.nb];
     for (int j = 0; j < Kmax; j++) {
+        KM_STAMP(j, Kmax, 0);
         while (alive > 0 && B.koff[alive] - B.koff[alive - 1] <= j) alive--;
         const int nit = ff_end[alive];
-        for (int u = blockIdx.x; u < nit; u += gridDim.x) {
+        for (int u = ws; u < nit; u += NWS) {
             const KmFfItem it = items[u];
             KmState s = bin_state(B, it.bin);
             int c;
@@ -1162,56 +1195,92 @@ __global__ __launch_bounds__(KM_FF_NT) void kmb_ff_persist2(KmBatch B, const KmF
                 c = s.center[0];  // kmb_ff_start (an earlier launch)
             } else {
                 const unsigned long long *pp = s.part + ((j - 1) & 1) * half;
+                unsigned long long v[KM_FF_SUBMAX / 64];  // every slot of the bin in flight at once
+#pragma unroll
+                for (int k = 0; k < KM_FF_SUBMAX / 64; k++)
+                    v[k] = lane + 64 * k < it.nsub
+                               ? __hip_atomic_load(&pp[lane + 64 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : 0ull;
                 unsigned long long bb = 0;
-                for (int i = threadIdx.x; i < it.nsub; i += KM_FF_NT)
-                    bb = max(bb, __hip_atomic_load(&pp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                const unsigned long long w = km_block_max(bb, red);
+#pragma unroll
+                for (int k = 0; k < KM_FF_SUBMAX / 64; k++) bb = max(bb, v[k]);
+                const unsigned long long w = km_wave_max(bb);
                 c = (w == 0) ? -1 : (int)(w & 0xFFFFFFFFull) - 1;
                 if (c < 0) {
-                    if (it.sub == 0 && threadIdx.x == 0) *s.err = 1;
+                    if (it.sub == 0 && lane == 0) *s.err = 1;
                     c = 0;  // the call fails (host checks err); keep the rounds well-defined
                 } else {
                     if (it.sub == 0) {
-                        if (threadIdx.x < KM_A) s.cent[(long)j * KM_A + threadIdx.x] = s.X[(long)c * KM_A + threadIdx.x];
-                        if (threadIdx.x == 0) s.center[j] = c;
+                        for (int a = lane; a < KM_A; a += 64) s.cent[(long)j * KM_A + a] = s.X[(long)c * KM_A + a];
+                        if (lane == 0) s.center[j] = c;
                     }
-                    if ((c / KM_FF_NT) % it.nsub == it.sub && c % KM_FF_NT == (int)threadIdx.x) s.used[c] = 1;
+                    if ((c >> 6) % it.nsub == it.sub && (c & 63) == lane) s.used[c] = 1;
                 }
             }
+            KM_STAMP(j, Kmax, 1);
             uint32_t item[20];
             load_row(s.X + (long)c * KM_A, item);
+#ifdef TILER_KM_STAMPS
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            KM_STAMP(j, Kmax, 2);
+#endif
             unsigned long long bv = 0;
             int bi = -1;
-            for (long i = (long)it.sub * KM_FF_NT + threadIdx.x; i < s.n; i += (long)it.nsub * KM_FF_NT) {
-                uint32_t row[20];
-                load_row(s.X + i * KM_A, row);
-                const unsigned long long d = km_dissim(row, item);
-                unsigned long long m = s.mind[i];
-                if (d < m) {  // cmovb: strict-less (kmodes.pas:555-558)
-                    m = d;
-                    s.mind[i] = m;
+            // the lane's points 4 at a time: their rows, min-distances and used flags loaded before any is compared
+            const long stride = (long)it.nsub * 64;
+            for (long i0 = (long)it.sub * 64 + lane; i0 < s.n; i0 += 4 * stride) {
+                uint32_t row[4][20];
+                unsigned long long mv[4];
+                uint8_t uf[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const long i = i0 + k * stride;
+                    if (i < s.n) {
+                        load_row(s.X + i * KM_A, row[k]);
+                        mv[k] = s.mind[i];
+                        uf[k] = s.used[i];
+                    }
                 }
-                if (!s.used[i] && m >= bv) {  // ascending i within a thread: '>=' keeps the last
-                    bv = m;
-                    bi = (int)i;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const long i = i0 + k * stride;
+                    if (i >= s.n) break;
+                    const unsigned long long d = km_dissim(row[k], item);
+                    unsigned long long m = mv[k];
+                    if (d < m) {  // cmovb: strict-less (kmodes.pas:555-558)
+                        m = d;
+                        s.mind[i] = m;
+                    }
+                    if (!uf[k] && m >= bv) {  // ascending i within a lane: '>=' keeps the last
+                        bv = m;
+                        bi = (int)i;
+                    }
                 }
             }
+            KM_STAMP(j, Kmax, 3);
             const unsigned long long v32 = bv > 0xFFFFFFFFull ? 0xFFFFFFFFull : bv;
-            const unsigned long long best = km_block_max(bi < 0 ? 0ull : ((v32 << 32) | (unsigned)(bi + 1)), red);
+            const unsigned long long best = km_wave_max(bi < 0 ? 0ull : ((v32 << 32) | (unsigned)(bi + 1)));
+            KM_STAMP(j, Kmax, 4);
             if (j + 1 >= s.K) continue;  // the bin's last round: no selection (uniform)
-            if (threadIdx.x == 0) __hip_atomic_store(s.part + (j & 1) * half + it.sub, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(s.part + (j & 1) * half + it.sub, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (j + 1 < Kmax && !km_grid_sync(bar, (unsigned)(j + 1), fail)) return;
+        if (j + 1 < Kmax && !km_grid_sync(bar, (unsigned)(j + 1), fail, Kmax)) return;
     }
 }
 
-// resident workgroups for kmb_ff_persist2: one per CU (0: not placeable -> per-launch rounds)
+#ifdef TILER_KM_STAMPS
+extern "C" int tiler_debug_km_stamps(void *out) {  // study build: the stamps of the last farthest-first launch
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_km_stamps), sizeof(g_km_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+// resident workgroups for kmb_ff_persist3: one per CU (0: not placeable -> per-launch rounds)
 static int ff_persist_grid() {
     static const int g = [] {
         int dev = 0, ncu = 0, per = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)kmb_ff_persist2, KM_FF_NT, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)kmb_ff_persist3, KM_FF_NT, 0) != hipSuccess ||
             per <= 0 || ncu <= 0)
             return 0;
         return ncu;
@@ -1284,7 +1353,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
         start[r] = h_start[b];
         boff[r + 1] = boff[r] + nv[r];
         koff[r + 1] = koff[r] + Kv[r];
-        poff[r + 1] = poff[r] + std::min(256, (nv[r] + 255) / 256);
+        poff[r + 1] = poff[r] + std::min(KM_FF_SUBMAX, (nv[r] + 255) / 256);  // kmb_ff_persist3's wave items
     }
     const long N = boff[nb], Ktot = koff[nb];
     const int M = n_modalities;
@@ -1318,7 +1387,7 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     }
     const size_t item_bytes = (max_items + (size_t)poff[nb] + 64) * sizeof(KmAsgItem) +
                               (size_t)(nb + 1) * 4 + 256;
-    // farthest-first: one persistent launch for every round (kmb_ff_persist2) unless it cannot be placed
+    // farthest-first: one persistent launch for every round (kmb_ff_persist3) unless it cannot be placed
     const int g_ff = ff_persist_grid();
     TILER_HIP_CHECK(hipMalloc((void **)&buf, off + item_bytes));
     char *items = buf + o_items;
@@ -1414,8 +1483,8 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     goto fail;
                 {
                     KTimer tm("kmodes_init", st);
-                    // every item selects the centre after the barrier (r03zo: C4 122 -> 102 ms)
-                    hipLaunchKernelGGL(kmb_ff_persist2, dim3(g_ff), dim3(KM_FF_NT), 0, st, B, (const KmFfItem *)items,
+                    // every item selects the centre after the barrier (r03zo: C4 122 -> 102 ms); wave items (r06)
+                    hipLaunchKernelGGL(kmb_ff_persist3, dim3(g_ff), dim3(KM_FF_NT), 0, st, B, (const KmFfItem *)items,
                                        (const int *)(items + fb), Kv[0], bar, ffail);
                 }
                 unsigned hf = 1;

@@ -102,6 +102,10 @@ int tiler_set_scan_limits(int max_k1, int max_k8);
 /* Test hook (process-wide): on != 0 makes ANN's pruning check vouch for no result, so every query of every kd-order
  * search takes the exact replay of annkSearch (kd_replay_kernel); answers are identical either way.  0. */
 int tiler_debug_force_replay(int on);
+/* Test / bench hook (process-wide): on = 0 switches off the k = 1 generic shortlist's exact insertion gate (the query's
+ * best key so far bounds what its lists may need), for A/B timing; answers are identical either
+ * way.  Default 1.  0. */
+int tiler_debug_shortlist_gate(int on);
 /* Coalescing counters of the single-query entry points on this handle: calls, batches searched, largest batch. */
 int tiler_combine_stats(ann_kdtree *akd, int64_t *calls, int64_t *batches, int32_t *max_batch);
 /* Test / bench hook: the reference's per-call pattern timed natively (no interpreter between the calls): the first

@@ -60,6 +60,7 @@ _SIGS = {
     "tiler_debug_percall_bench": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, P(c_double),
                                           P(c_double)]),
     "tiler_debug_force_replay": (c_int, [c_int]),
+    "tiler_debug_shortlist_gate": (c_int, [c_int]),
     "tiler_combine_stats": (c_int, [c_void_p, P(ctypes.c_int64), P(ctypes.c_int64), P(ctypes.c_int32)]),
     "tiler_init": (c_int, [c_int]),
     "tiler_device_count": (c_int, []),

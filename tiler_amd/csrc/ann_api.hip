@@ -972,6 +972,11 @@ int tiler_debug_force_replay(int on) {
     return 0;
 }
 
+int tiler_debug_shortlist_gate(int on) {
+    nn_set_shortlist_gate(on);
+    return 0;
+}
+
 int tiler_combine_stats(ann_kdtree *t, int64_t *calls, int64_t *batches, int32_t *max_batch) {
     if (!t) {
         set_error("tiler_combine_stats: null handle");

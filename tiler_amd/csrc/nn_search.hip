@@ -445,11 +445,19 @@ __device__ __forceinline__ void vm_wait() {  // s_waitcnt vmcnt(N): all but this
 // Measured and removed (round 5, DESIGN.md section 4, identical digests): a software-pipelined stage (block cb + 1's
 // MFMAs before block cb's epilogue, one compare per element) +1.5..3 %; 4 blocks per stage +1..3 %; 4 blocks per
 // stage with the insertions queued per lane in LDS and applied in bulk +6 % (commit c152f52 has both).
+// gate (VAR bit 0 only; nullptr: off): the k = 1 search's exact insertion gate (round 6).  The rescore needs every
+// candidate whose key can reach T(kk), kk the smallest key of the query (nn_rescore_kernel; T increasing in kk), and
+// T(kk) <= T(b) for every key b the query has already seen.  So a lane may skip any candidate whose key exceeds
+// T(best key of the query so far, over its 4 lanes): gate[q] = (x, y) with T(b) <= (b + x) * gb + y up to the
+// fp32 slack added here (gate16_kernel).  Each lane's own L-th key still gates its list as before; the tighter of the
+// two is kept current in th[] whenever the wave takes the insertion branch (the 4 lanes' bests by two xor shuffles).
+// A lane's list keeps every candidate the rescore can need, so the overflow rule and tiers 2 / 3 are unchanged.
 template <int S, int L, int CB, int NW, int QB, bool FLAT, int MODE = 0, int VAR = 0>
 __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag, const float *__restrict__ cseed,
                                                  int nblk, const half8 *__restrict__ qfrag, int nq, int blk_per_split,
                                                  int nsplit, int perm, float *__restrict__ out_key,
-                                                 int *__restrict__ out_idx) {
+                                                 int *__restrict__ out_idx, const float2 *__restrict__ gate,
+                                                 float gb) {
     typedef float floatx4 __attribute__((ext_vector_type(4)));
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * S * 1024;
@@ -518,9 +526,14 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
         if (w == 0) vm_wait<(FLAT ? 1 : PER_T) + 1>();
         else vm_wait<(FLAT ? 1 : PER_T)>();
     };
-    float th[QB];  // VAR & 1: -0.5 * lk[q][L - 1] (and the window bound), kept current
+    float th[QB];  // VAR & 1: max(-0.5 * lk[q][L - 1], the gate's bound), kept current
+    float2 gq[QB];  // the gate of this lane's query of block q (x = +inf: none)
 #pragma unroll
-    for (int q = 0; q < QB; q++) th[q] = -INFINITY;
+    for (int q = 0; q < QB; q++) {
+        th[q] = -INFINITY;
+        const int qq = (qb0 + q) * 16 + (lane & 15);
+        gq[q] = (gate && qq < nq) ? gate[qq] : make_float2(INFINITY, INFINITY);
+    }
     if (nstage > 0) issue(0, 0);
     if (NBUF == 3 && nstage > 1) {
         issue(1, 1);
@@ -603,8 +616,22 @@ __device__ __forceinline__ void shortlist16_body(const half8 *__restrict__ cfrag
                                 for (int i = 0; i < 4; i++)
                                     if (acc[q][i] > th[q]) {
                                         list_insert<L>(lk[q], li[q], -2.0f * acc[q][i], base + rel[i]);
-                                        th[q] = -0.5f * lk[q][L - 1];
+                                        th[q] = fmaxf(th[q], -0.5f * lk[q][L - 1]);
                                     }
+                        if (gate) {  // wave-uniform: the query's best key over its 4 lanes -> its gate
+#pragma unroll
+                            for (int q = 0; q < QB; q++) {
+                                float b = lk[q][0];
+                                b = fminf(b, __shfl_xor(b, 16, 64));
+                                b = fminf(b, __shfl_xor(b, 32, 64));
+                                if (gq[q].x < INFINITY && b < INFINITY) {
+                                    const float X = b + gq[q].x, T1 = X * gb, T2 = T1 + gq[q].y;
+                                    // every rounding of the three ops, and the rescore's 1e-12 |kk| term, inside
+                                    const float T = T2 + (fabsf(T1) + fabsf(gq[q].y)) * 9.5367431640625e-07f + 1e-30f;
+                                    th[q] = fmaxf(th[q], -0.5f * T);
+                                }
+                            }
+                        }
                     } else {
 #pragma unroll
                         for (int q = 0; q < QB; q++)
@@ -644,13 +671,37 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_shortlist16_kernel(const half8 
                                                                 const half8 *__restrict__ qfrag, int nq,
                                                                 int blk_per_split, int nsplit, int perm,
                                                                 float *__restrict__ out_key,
-                                                                int *__restrict__ out_idx, const int *flat_cnt) {
+                                                                int *__restrict__ out_idx, const int *flat_cnt,
+                                                                const float2 *__restrict__ gate, float gb) {
     if (flat_cnt && (long)blockIdx.x * (NW * QB * 16) >= (long)*flat_cnt)
         shortlist16_body<S, L, CB, NW, QB, true, MODE, VAR>(cfrag, cseed, nblk, qfrag, nq, blk_per_split, nsplit, perm,
-                                                            out_key, out_idx);
+                                                            out_key, out_idx, gate, gb);
     else
         shortlist16_body<S, L, CB, NW, QB, false, MODE, VAR>(cfrag, cseed, nblk, qfrag, nq, blk_per_split, nsplit,
-                                                             perm, out_key, out_idx);
+                                                             perm, out_key, out_idx, gate, gb);
+}
+
+// The k = 1 gate of nn_shortlist16_kernel: T(kk) <= (kk + x) * gb + y for the rescore's threshold
+//     T(kk) = (n2 + kk + Ek)(1 + g)/(1 - g) - n2 + Ek + 1e-12 (n2 + |kk|) + 1e-30     (nn_rescore_kernel)
+// x = n2 + Ek and y = -n2 + Ek + 1e-12 n2 + 1e-30 rounded up to fp32, gb = (1 + g)/(1 - g) rounded up (host); the
+// kernel's fp32 slack covers its own roundings and the 1e-12 |kk| term.  Queries the rescore sends to tier 3: no gate.
+__global__ __launch_bounds__(256) void gate16_kernel(const QStat *__restrict__ qs, int nq, int d, double N, double H,
+                                                     double Ec, float2 *__restrict__ gate) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= nq) return;
+    const QStat st = qs[q];
+    if (st.flags & QF_BAD) {
+        gate[q] = make_float2(INFINITY, INFINITY);
+        return;
+    }
+    const double u = 5.9604644775390625e-08;  // 2^-24
+    const double gam = 2.0 * (d + 1) * u;
+    const double Ek = 1.05 * (2.0 * u * N * N + gam * (N * N + 2.0 * st.hn * H) + 2.0 * (st.en * N + st.hn * Ec)) + 1e-30;
+    const double x = st.n2 + Ek, y = -st.n2 + Ek + 1e-12 * st.n2 + 1e-30;
+    float xf = (float)x, yf = (float)y;
+    if ((double)xf < x) xf = nextafterf(xf, INFINITY);
+    if ((double)yf < y) yf = nextafterf(yf, INFINITY);
+    gate[q] = make_float2(xf, yf);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1620,6 +1671,7 @@ void nn_scratch_free(SearchScratch &s) {
     hipFree(s.fb_count);
     hipFree(s.qrows);
     hipFree(s.thr);
+    hipFree(s.gate);
     hipFree(s.ex_list);
     hipFree(s.ccnt);
     hipFree(s.cbuf);
@@ -1673,6 +1725,7 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         hipFree(s.fb_list);
         hipFree(s.fb_count);
         hipFree(s.thr);
+        hipFree(s.gate);
         hipFree(s.ex_list);
         hipFree(s.kd_list);
         hipFree(s.kd_rootbox);
@@ -1682,6 +1735,7 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         s.qstat = nullptr;
         s.fb_list = s.fb_count = s.ex_list = s.kd_list = nullptr;
         s.thr = s.kd_rootbox = nullptr;
+        s.gate = nullptr;
         s.kd_done = nullptr;
         s.t2best = nullptr;
         s.cap_q = 0;
@@ -1692,6 +1746,7 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         TILER_HIP_CHECK(hipMalloc((void **)&s.fb_list, (size_t)nq * sizeof(int)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.fb_count, 16));
         TILER_HIP_CHECK(hipMalloc((void **)&s.thr, (size_t)nq * sizeof(float)));
+        TILER_HIP_CHECK(hipMalloc((void **)&s.gate, (size_t)nq * sizeof(float2)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.ex_list, (size_t)nq * sizeof(int)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.kd_list, (size_t)nq * sizeof(int)));
         TILER_HIP_CHECK(hipMalloc((void **)&s.kd_rootbox, (size_t)nq * sizeof(float)));
@@ -1745,20 +1800,32 @@ static constexpr int SL16_NW = 8, SL16_QB = 4, SL16_CB = 8;
 // shortlist16_body VAR of the shipped kernel: the per-query-block insertion gate (r04c/r04e: -2..-3 % shortlist time,
 // same digests; the 3-buffer ring, VAR 2, measured no gain)
 static constexpr int SL16_VAR = 1;
+static std::atomic<int> g_gate16{1};  // tiler_debug_shortlist_gate: the k = 1 insertion gate (A/B timing hook)
 static int shortlist16_L() {
     const int v = shortlist_variant();
     return v == 16 ? 4 : v == 166 ? 6 : 0;
 }
 
 template <int S, int L>
-static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
+static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, bool gated, hipStream_t stream) {
     const int nqblk = (nq + 15) / 16;
     const dim3 grid((nqblk + SL16_NW * SL16_QB - 1) / (SL16_NW * SL16_QB), nsplit);
     const size_t buf = SL16_CB * S * 1024 + SL16_CB * 64;
+    float gb = 0.0f;
+    if (gated) {  // the k = 1 gate (gate16_kernel): per query (x, y) from the query statistics, gb = (1 + g)/(1 - g)
+        const double u = 5.9604644775390625e-08;
+        const double g = (double)(ix->d + 4) * u / (1.0 - (double)(ix->d + 4) * u) * 1.05;
+        const double b = (1.0 + g) / (1.0 - g);
+        gb = (float)b;
+        if ((double)gb < b) gb = nextafterf(gb, INFINITY);
+        hipLaunchKernelGGL(gate16_kernel, dim3((nq + 255) / 256), dim3(256), 0, stream, ix->scratch.qstat, nq, ix->d,
+                           ix->maxN, ix->maxH, ix->maxE, ix->scratch.gate);
+    }
     auto go = [&](auto kern, int nbuf) {
         hipLaunchKernelGGL(kern, grid, dim3(SL16_NW * 64), nbuf * buf, stream, (const half8 *)ix->d_frag16,
                            ix->d_seed16, ix->nblk16, (const half8 *)ix->scratch.qfrag16, nq, bps, nsplit, ix->perm,
-                           ix->scratch.key, ix->scratch.idx, ix->flat_cnt);
+                           ix->scratch.key, ix->scratch.idx, ix->flat_cnt, gated ? (const float2 *)ix->scratch.gate : nullptr,
+                           gb);
     };
     KTimer tm("nn_shortlist", stream);
     go(nn_shortlist16_kernel<S, L, SL16_CB, SL16_NW, SL16_QB, 0, SL16_VAR>, 2);
@@ -1944,6 +2011,7 @@ void nn_set_scan_limits(int max_k1, int max_k8) {
     g_scan_max8.store(std::max(0, max_k8));
 }
 void nn_set_force_replay(int on) { g_force_replay.store(on != 0); }
+void nn_set_shortlist_gate(int on) { g_gate16.store(on != 0); }
 bool nn_search_is_small(const NNIndex *ix, int nq, int k) { return scan_small_takes(ix, nq, k); }
 static bool scan_small_takes(const NNIndex *ix, int nq, int k) {
     return ix->d <= SCAN_D_MAX && ix->d % 4 == 0 &&
@@ -2102,7 +2170,8 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
         }
         TILER_HIP_CHECK(hipGetLastError());
         {
-            if (launch_shortlist16<6, 4>(ix, nq, nsplit, bps, stream)) return -1;
+            if (launch_shortlist16<6, 4>(ix, nq, nsplit, bps, k == 1 && g_gate16.load(std::memory_order_relaxed), stream))
+                return -1;
         }
     } else if (dispatch_shortlist<8>(ix, nq, nsplit, bps, stream)) {
         return -1;

@@ -40,6 +40,7 @@ struct SearchScratch {
     float *qrows = nullptr;   // fp32 query rows (frame-tiling path: descriptors)
     void *qfrag16 = nullptr;  // query fragments, 16-row layout
     float *thr = nullptr;     // tier-2 thresholds [nq]
+    float2 *gate = nullptr;   // [nq] the generic k = 1 shortlist's insertion gate: T(kk) = (kk + x) * b + y (gate16_kernel)
     int *ex_list = nullptr;   // tier-3 list [nq]
     int *ccnt = nullptr;      // generic tier-2 collect counts [TIER2_MAX] (one chunk)
     int *cbuf = nullptr;      // generic tier-2 collect buffers [TIER2_MAX][TIER2_CAP]
@@ -120,6 +121,7 @@ int nn_search_dev(NNIndex *ix, const float *d_q, int nq, int k, int *d_idx, floa
 void nn_set_scan_limits(int max_k1, int max_k8);
 // test hook: every kd pruning check lists its query for the exact replay (results unchanged)
 void nn_set_force_replay(int on);
+void nn_set_shortlist_gate(int on);
 
 // frame tiling: RGB tiles -> descriptors (fp32) -> search -> tilemap items
 int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavelets, int gamma, int *d_idx,

@@ -34,6 +34,18 @@ static constexpr int OS = 12;   // k-steps of 16 (4 isotypic blocks x 3)
 #ifndef ORB_XBATCH
 #define ORB_XBATCH 3
 #endif
+#ifndef ORB_RS_WAVES
+#define ORB_RS_WAVES 6  // nn_orbit_rescore_kernel: waves per SIMD it is compiled for
+#endif
+#ifndef ORB_STG_ROWS
+#define ORB_STG_ROWS 4  // nn_orbit_rescore_kernel: candidate rows staged in LDS per pass
+#endif
+#ifndef ORB_PR_WAVES
+#define ORB_PR_WAVES 0  // nn_orbit_pairs_kernel: waves per SIMD it is compiled for (0: the compiler's choice)
+#endif
+#ifndef ORB_PR_UNROLL
+#define ORB_PR_UNROLL 8  // nn_orbit_pairs_kernel: 16-byte load pairs in flight per lane
+#endif
 #ifndef ORB_DU
 #define ORB_DU 4
 #endif
@@ -1145,7 +1157,7 @@ struct OrbitRescoreArgs {
 __device__ __forceinline__ float exact_dist192_lean(const float *__restrict__ q, const float *__restrict__ c) {
     const float4 *q4 = reinterpret_cast<const float4 *>(q), *c4 = reinterpret_cast<const float4 *>(c);
     float dist = 0.0f;
-#pragma unroll 8
+#pragma unroll ORB_PR_UNROLL
     for (int i = 0; i < OD / 4; i++) {
         const float4 x = q4[i], y = c4[i];
         float t;
@@ -1257,7 +1269,7 @@ __device__ __forceinline__ void orbit_argmin(const OrbitRescoreArgs &a, const fl
 // reference distances), so two independent chains per wave double the work in flight.  Every cross-lane
 // operation below stays inside the half (xor offsets < 32, ballots masked to the half).
 static constexpr int ORB_QCAP = 64;  // rescore queue per query
-static constexpr int ORB_STG = 4;    // candidate rows staged in LDS per pass
+static constexpr int ORB_STG = ORB_STG_ROWS;  // candidate rows staged in LDS per pass
 static constexpr int ORB_PSLOTS = 4; // candidates per query handed to the pair pass
 
 __device__ __forceinline__ float half_min_f(float v) {
@@ -1277,7 +1289,7 @@ __device__ __forceinline__ unsigned half_ballot(bool p) {
     return (unsigned)(__ballot(p) >> (32 * ((threadIdx.x >> 5) & 1)));
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void nn_orbit_rescore_kernel(OrbitRescoreArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_RS_WAVES))) void nn_orbit_rescore_kernel(OrbitRescoreArgs a) {
     const int l = threadIdx.x & 31, hq = threadIdx.x >> 5;  // lane in the half, query slot of the block
     const int hbase = threadIdx.x & 32;                     // first lane of this half in the wave
     const long q = (long)blockIdx.x * 8 + hq;
@@ -1467,7 +1479,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void n
 // these 192-step chains here instead of one lane per candidate inside the half-wave rescore keeps the
 // rescore's instruction stream short (it is latency-bound) and fills the lanes.  r03zr: staging the rows through LDS in
 // coalesced 32-float column chunks (12 barriers, every slot's row loaded) took 1.00 ms vs 0.50 ms for this per-lane walk.
+#if ORB_PR_WAVES
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_PR_WAVES))) void nn_orbit_pairs_kernel(OrbitRescoreArgs a) {
+#else
 __global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a) {
+#endif
     const long gid = (long)blockIdx.x * 256 + threadIdx.x;
     const long q = gid / ORB_PSLOTS;
     const int s = (int)(gid % ORB_PSLOTS);

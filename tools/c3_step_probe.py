@@ -74,11 +74,17 @@ def main():
     lib.tiler_timing_enable(0)
     n = ctypes.c_int(0)
     ms = lib.tiler_timing_get(b"nn_orbit", ctypes.byref(n))
+    kern = {}
+    for name in ("psyv", "nn_rescore", "nn_pairs", "nn_collect", "kd_verify"):
+        c = ctypes.c_int(0)
+        t_ = lib.tiler_timing_get(name.encode(), ctypes.byref(c))
+        kern[name] = round(t_ / max(1, c.value), 4) if c.value else None
     h = hashlib.sha256()
     for x in out:
         h.update(x.cpu().numpy().tobytes())
     print(json.dumps({"tag": args.tag, "ms_per_step": round(1e3 * el / args.steps, 3),
-                      "orbit_ms": round(ms / max(1, n.value), 3), "mtiles_s": round(QK * args.steps / el / 1e6, 2),
+                      "orbit_ms": round(ms / max(1, n.value), 3), "kernels_ms": kern,
+                      "mtiles_s": round(QK * args.steps / el / 1e6, 2),
                       "digest": h.hexdigest()[:16]}), flush=True)
     kdt.close()
 

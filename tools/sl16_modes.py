@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tag", default="")
     ap.add_argument("--lib", default="")
+    ap.add_argument("--gate", type=int, default=1, help="the k = 1 insertion gate (tiler_debug_shortlist_gate)")
     args = ap.parse_args()
     import torch
     import tiler_amd._lib as L
@@ -39,6 +40,8 @@ def main():
 
     lib = tiler_amd.load()
     check(lib.tiler_init(0), "tiler_init")
+    if hasattr(lib, "tiler_debug_shortlist_gate"):
+        lib.tiler_debug_shortlist_gate(args.gate)
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(20261017)
     P, T, W, H, F = 128, 65536, 1920, 1080, 24
@@ -82,7 +85,8 @@ def main():
     m0 = info["candidates"]
     flops = 2.0 * (-(-m0 // 16) * 16) * 32 * (6 * (n - st["flat_queries"]) + st["flat_queries"])
     best = min(ms)
-    print(json.dumps({"tag": args.tag, "mode": os.environ.get("TILER_SL16_MODE", "0"), "shortlist_ms": ms,
+    print(json.dumps({"tag": args.tag, "gate": args.gate, "mode": os.environ.get("TILER_SL16_MODE", "0"),
+                      "shortlist_ms": ms, "tier2_queries": st["fallback_queries"], "tier3_queries": st["exhaustive_queries"],
                       "candidates": m0, "flat_queries": st["flat_queries"],
                       "frac": round(flops / (best * 1e-3) / 1e12 / 2500.0, 4), "digest": h.hexdigest()[:16]}),
           flush=True)

@@ -90,6 +90,9 @@ def parser():
     ap.add_argument("--item-tiles", type=int, default=0,
                     help="tiles a keyframe's items are drawn from (0: the whole tileset, uniformly)")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--prep-priority", type=int, default=1,
+                    help="1: the next keyframe's Prepare on a high-priority stream (its short kernels and host syncs "
+                         "then get CUs as FrameTiling's workgroups retire instead of after the whole grid); 0: normal")
     ap.add_argument("--no-smooth", action="store_true")
     ap.add_argument("--check-kf", type=int, default=1, help="keyframe re-checked against the restatement (-1: none)")
     ap.add_argument("--check-queries", type=int, default=1500)
@@ -142,7 +145,8 @@ def run(args) -> dict:
     print(f"[bench_encoder] {args.frames} frames x {Q} tiles in HBM, {nkf} keyframes", file=sys.stderr, flush=True)
 
     s_ft = torch.cuda.Stream(dev)     # FrameTiling + Smooth
-    s_prep = torch.cuda.Stream(dev)   # PrepareFrameTiling of the next keyframe
+    # PrepareFrameTiling of the next keyframe; high priority (torch: negative = higher) by default
+    s_prep = torch.cuda.Stream(dev, priority=-1) if args.prep_priority else torch.cuda.Stream(dev)
     outs = []
     for k in range(nkf):
         n = (starts[k + 1] - starts[k]) * Q
@@ -150,7 +154,7 @@ def run(args) -> dict:
                      (("tile", torch.int32), ("pal", torch.int32), ("hm", torch.uint8), ("vm", torch.uint8),
                       ("err", torch.float32))})
     sm = [None] * nkf
-    times = {"prepare": [], "ft_smooth": []}
+    times = {"prepare": [], "ft_smooth": [], "close": [], "join": [], "prep_call": []}
     stats_kf = {}
     info_all = []
 
@@ -160,6 +164,7 @@ def run(args) -> dict:
                                                 d_tiles.data_ptr(), d_thm.data_ptr(), d_tvm.data_ptr(), T,
                                                 d_pals.data_ptr(), P, args.quality, near, True, -1,
                                                 stream.cuda_stream)
+        times["prep_call"].append(time.perf_counter() - t0)
         stream.synchronize()
         times["prepare"].append(time.perf_counter() - t0)
         info_all.append(info)
@@ -191,8 +196,8 @@ def run(args) -> dict:
     kept = {}
 
     def run_clip(keep=False):
-        times["prepare"].clear()
-        times["ft_smooth"].clear()
+        for v in times.values():
+            v.clear()
         info_all.clear()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -212,10 +217,14 @@ def run(args) -> dict:
             worker.start()
             prev = None
             for k in range(nkf):
+                tj = time.perf_counter()
                 worker.join()
+                times["join"].append(time.perf_counter() - tj)
                 kt = box.pop(k)
+                tc = time.perf_counter()
                 if prev is not None and prev is not kept.get("kt"):
                     prev.close()  # keyframe k-1 is finished and nothing else is in flight: its frees cost nothing
+                times["close"].append(time.perf_counter() - tc)
                 if k + 1 < nkf:
                     worker = threading.Thread(target=lambda k1=k + 1: box.__setitem__(k1, prepare(k1, gds, s_prep)))
                     worker.start()
@@ -283,10 +292,11 @@ def run(args) -> dict:
     res = {"metric": "sustained FrameTiling Mtiles/s over a clip incl. PrepareGlobalFT + per-keyframe "
                      "PrepareFrameTiling + Smooth", "value": round(value, 3), "unit": "Mtiles/s",
            "wall_s": round(wall, 4), "frames": args.frames, "keyframes": nkf, "tiles": tiles_total,
-           "overlap": not args.no_overlap, "quality": ["fast", "medium", "slow"][args.quality],
+           "overlap": not args.no_overlap, "prep_priority": args.prep_priority, "quality": ["fast", "medium", "slow"][args.quality],
            "prepare_global_ms": round(t_global * 1e3, 2),
            "prepare_ms_avg": round(1e3 * float(np.mean(times["prepare"])), 3),
            "ft_smooth_ms_avg": round(1e3 * float(np.mean(times["ft_smooth"])), 3),
+           "loop_ms_avg": {k: round(1e3 * float(np.mean(times[k])), 3) for k in ("join", "close", "prep_call") if times[k]},
            "items_avg": round(float(np.mean([i["items"] for i in info_all])), 1),
            "candidates_avg": round(float(np.mean(cand)), 1), "candidates_min": int(min(cand)),
            "candidates_max": int(max(cand)), "search_stats_one_keyframe": stats_kf,

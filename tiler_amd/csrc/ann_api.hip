@@ -440,11 +440,11 @@ ann_kdtree *ann_kdtree_create(float **pa, int n, int dd, int bs, int split) {
     t->placed = bytes;
     float *d_rows = nullptr;
     if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void **)&d_rows, std::max<size_t>(1, h.size()) * sizeof(float)) != hipSuccess ||
+        dmalloc((void **)&d_rows, std::max<size_t>(1, h.size()) * sizeof(float)) != hipSuccess ||
         (n > 0 && hipMemcpyAsync(d_rows, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, t->stream) !=
                       hipSuccess)) {
         set_error("ann_kdtree_create: device allocation or copy failed");
-        if (d_rows) (void)hipFree(d_rows);
+        if (d_rows) dfree_sync(d_rows);
         handle_free(t);
         return nullptr;
     }
@@ -481,10 +481,10 @@ ann_kdtree *ann_kdtree_create_dev_ex(const float *d_rows_in, int n, int dd, int 
     const size_t bytes = (size_t)n * dd * sizeof(float);
     const bool ok_stream = hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) == hipSuccess;
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
-    if (!ok_stream || hipMalloc((void **)&d_rows, std::max<size_t>(4, bytes)) != hipSuccess ||
+    if (!ok_stream || dmalloc((void **)&d_rows, std::max<size_t>(4, bytes)) != hipSuccess ||
         (n > 0 && hipMemcpyAsync(d_rows, d_rows_in, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)) {
         set_error("ann_kdtree_create_dev: device allocation or copy failed");
-        if (d_rows) (void)hipFree(d_rows);
+        if (d_rows) dfree_sync(d_rows);
         handle_free(t);
         return nullptr;
     }
@@ -571,10 +571,10 @@ static ann_kdtree *replica_of(ann_kdtree *t, int dev) {
         (t->maps_ev && hipEventSynchronize(t->maps_ev) != hipSuccess) ||
         (src->done_event && hipEventSynchronize(src->done_event) != hipSuccess) ||
         hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void **)&d_rows, std::max<size_t>(4, bytes)) != hipSuccess ||
+        dmalloc((void **)&d_rows, std::max<size_t>(4, bytes)) != hipSuccess ||
         (bytes && hipMemcpyPeerAsync(d_rows, dev, src->d_rows, t->dev, bytes, r->stream) != hipSuccess)) {
         set_error("tiler: replica allocation or peer copy failed");
-        if (d_rows) (void)hipFree(d_rows);
+        if (d_rows) dfree_sync(d_rows);
         handle_free(r);
         return nullptr;
     }
@@ -586,8 +586,8 @@ static ann_kdtree *replica_of(ann_kdtree *t, int dev) {
     if (src->d_tr_tile) {
         const size_t n = std::max(1, src->n);
         NNIndex *ix = r->ix;
-        if (hipMalloc((void **)&ix->d_tr_tile, n * 4) != hipSuccess || hipMalloc((void **)&ix->d_tr_pal, n * 4) != hipSuccess ||
-            hipMalloc((void **)&ix->d_tr_attr, n) != hipSuccess ||
+        if (dmalloc((void **)&ix->d_tr_tile, n * 4) != hipSuccess || dmalloc((void **)&ix->d_tr_pal, n * 4) != hipSuccess ||
+            dmalloc((void **)&ix->d_tr_attr, n) != hipSuccess ||
             hipMemcpyPeerAsync(ix->d_tr_tile, dev, src->d_tr_tile, t->dev, (size_t)src->n * 4, r->stream) != hipSuccess ||
             hipMemcpyPeerAsync(ix->d_tr_pal, dev, src->d_tr_pal, t->dev, (size_t)src->n * 4, r->stream) != hipSuccess ||
             hipMemcpyPeerAsync(ix->d_tr_attr, dev, src->d_tr_attr, t->dev, (size_t)src->n, r->stream) != hipSuccess) {
@@ -1183,12 +1183,13 @@ static int set_maps_one(ann_kdtree *t, const int32_t *tr_tile, const int32_t *tr
     NNIndex *ix = t->ix;
     std::lock_guard<std::mutex> lk(ix->mu);
     const size_t n = std::max(1, ix->n);
-    hipFree(ix->d_tr_tile);
-    hipFree(ix->d_tr_pal);
-    hipFree(ix->d_tr_attr);
-    TILER_HIP_CHECK(hipMalloc((void **)&ix->d_tr_tile, n * 4));
-    TILER_HIP_CHECK(hipMalloc((void **)&ix->d_tr_pal, n * 4));
-    TILER_HIP_CHECK(hipMalloc((void **)&ix->d_tr_attr, n));
+    (void)hipDeviceSynchronize();  // a search may still read the old maps (dfree: hipFree's rule made explicit)
+    dfree(ix->d_tr_tile);
+    dfree(ix->d_tr_pal);
+    dfree(ix->d_tr_attr);
+    TILER_HIP_CHECK(dmalloc((void **)&ix->d_tr_tile, n * 4));
+    TILER_HIP_CHECK(dmalloc((void **)&ix->d_tr_pal, n * 4));
+    TILER_HIP_CHECK(dmalloc((void **)&ix->d_tr_attr, n));
     TILER_HIP_CHECK(hipMemcpy(ix->d_tr_tile, tr_tile, (size_t)ix->n * 4, hipMemcpyHostToDevice));
     TILER_HIP_CHECK(hipMemcpy(ix->d_tr_pal, tr_pal, (size_t)ix->n * 4, hipMemcpyHostToDevice));
     TILER_HIP_CHECK(hipMemcpy(ix->d_tr_attr, tr_attr, (size_t)ix->n, hipMemcpyHostToDevice));

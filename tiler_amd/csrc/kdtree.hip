@@ -758,14 +758,15 @@ KdOrder KdTree::view() const {
 
 void kd_tree_destroy(KdTree *t) {
     if (!t) return;
-    hipFree(t->d_pos);
-    hipFree(t->d_pidx);
-    hipFree(t->d_cd);
-    hipFree(t->d_cv);
-    hipFree(t->d_lo);
-    hipFree(t->d_hi);
-    hipFree(t->d_box);
-    hipFree(t->d_view);
+    (void)hipDeviceSynchronize();  // dfree files the blocks for reuse: nothing may still read them (hipFree's rule)
+    dfree(t->d_pos);
+    dfree(t->d_pidx);
+    dfree(t->d_cd);
+    dfree(t->d_cv);
+    dfree(t->d_lo);
+    dfree(t->d_hi);
+    dfree(t->d_box);
+    dfree(t->d_view);
     delete t;
 }
 
@@ -797,12 +798,15 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
     t->n = n;
     t->dd = dd;
     t->bs = std::max(1, bs);
-    struct Guard {  // frees the build's device scratch on every exit path
+    struct Guard {  // returns the build's device scratch to the block cache on every exit path, once idle
         std::vector<void *> dev;
+        hipStream_t s;
         ~Guard() {
-            for (void *p : dev) (void)hipFree(p);
+            if (!dev.empty()) (void)hipStreamSynchronize(s);  // an error exit may leave work queued on it
+            for (void *p : dev) dfree(p);
         }
     } g;
+    g.s = stream;
     auto fail = [&]() -> KdTree * {
         kd_tree_destroy(t);
         return nullptr;
@@ -824,14 +828,14 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
         }                                                              \
     } while (0)
     const size_t nn1 = (size_t)std::max(n, 1);
-    KD_CHECK(hipMalloc((void **)&t->d_pos, nn1 * 4));
-    KD_CHECK(hipMalloc((void **)&t->d_pidx, nn1 * 4));
-    KD_CHECK(hipMalloc((void **)&t->d_cd, nn1 * 4));
-    KD_CHECK(hipMalloc((void **)&t->d_cv, nn1 * 4));
-    KD_CHECK(hipMalloc((void **)&t->d_lo, nn1 * 4));
-    KD_CHECK(hipMalloc((void **)&t->d_hi, nn1 * 4));
-    KD_CHECK(hipMalloc((void **)&t->d_box, (size_t)2 * std::max(dd, 1) * 4));
-    KD_CHECK(hipMalloc((void **)&t->d_view, sizeof(KdOrder)));
+    KD_CHECK(dmalloc((void **)&t->d_pos, nn1 * 4));
+    KD_CHECK(dmalloc((void **)&t->d_pidx, nn1 * 4));
+    KD_CHECK(dmalloc((void **)&t->d_cd, nn1 * 4));
+    KD_CHECK(dmalloc((void **)&t->d_cv, nn1 * 4));
+    KD_CHECK(dmalloc((void **)&t->d_lo, nn1 * 4));
+    KD_CHECK(dmalloc((void **)&t->d_hi, nn1 * 4));
+    KD_CHECK(dmalloc((void **)&t->d_box, (size_t)2 * std::max(dd, 1) * 4));
+    KD_CHECK(dmalloc((void **)&t->d_view, sizeof(KdOrder)));
     KD_CHECK(hipMemsetAsync(t->d_cd, 0, nn1 * 4, stream));
     KD_CHECK(hipMemsetAsync(t->d_cv, 0, nn1 * 4, stream));
     KD_CHECK(hipMemsetAsync(t->d_lo, 0, nn1 * 4, stream));
@@ -898,23 +902,23 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
         int *d_cut = nullptr, *d_lpos = nullptr, *d_rpos = nullptr;
         KdChunk *d_ch = nullptr;
         KdNodeDev *d_nodes = nullptr;
-        KD_CHECK(hipMalloc((void **)&d_nodes, (size_t)std::max(n_nodes, 1) * sizeof(KdNodeDev)));
+        KD_CHECK(dmalloc((void **)&d_nodes, (size_t)std::max(n_nodes, 1) * sizeof(KdNodeDev)));
         g.dev.push_back(d_nodes);
         KD_CHECK(hipMemcpyAsync(d_nodes, h_nodes, (size_t)n_nodes * sizeof(KdNodeDev), hipMemcpyHostToDevice, stream));
         if (nlev > 0) {
-            KD_CHECK(hipMalloc((void **)&d_keys, nn1 * 4));
+            KD_CHECK(dmalloc((void **)&d_keys, nn1 * 4));
             g.dev.push_back(d_keys);
-            KD_CHECK(hipMalloc((void **)&d_lpos, nn1 * 4));
+            KD_CHECK(dmalloc((void **)&d_lpos, nn1 * 4));
             g.dev.push_back(d_lpos);
-            KD_CHECK(hipMalloc((void **)&d_rpos, nn1 * 4));
+            KD_CHECK(dmalloc((void **)&d_rpos, nn1 * 4));
             g.dev.push_back(d_rpos);
-            KD_CHECK(hipMalloc((void **)&d_omin, (size_t)max_big * dd * 4));
+            KD_CHECK(dmalloc((void **)&d_omin, (size_t)max_big * dd * 4));
             g.dev.push_back(d_omin);
-            KD_CHECK(hipMalloc((void **)&d_omax, (size_t)max_big * dd * 4));
+            KD_CHECK(dmalloc((void **)&d_omax, (size_t)max_big * dd * 4));
             g.dev.push_back(d_omax);
-            KD_CHECK(hipMalloc((void **)&d_cut, (size_t)max_nn * 4));
+            KD_CHECK(dmalloc((void **)&d_cut, (size_t)max_nn * 4));
             g.dev.push_back(d_cut);
-            KD_CHECK(hipMalloc((void **)&d_ch, (size_t)std::max(n_ch, 1) * sizeof(KdChunk)));
+            KD_CHECK(dmalloc((void **)&d_ch, (size_t)std::max(n_ch, 1) * sizeof(KdChunk)));
             g.dev.push_back(d_ch);
             if (n_ch > 0)
                 KD_CHECK(hipMemcpyAsync(d_ch, h_ch, (size_t)n_ch * sizeof(KdChunk), hipMemcpyHostToDevice, stream));
@@ -953,9 +957,9 @@ KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t st
             if (nlev == 0) {  // the whole tree is one subtree: the enclosing box comes from a root spread
                 int *d_cut1 = nullptr;
                 float *d_keys1 = nullptr;
-                KD_CHECK(hipMalloc((void **)&d_cut1, 4));
+                KD_CHECK(dmalloc((void **)&d_cut1, 4));
                 g.dev.push_back(d_cut1);
-                KD_CHECK(hipMalloc((void **)&d_keys1, nn1 * 4));
+                KD_CHECK(dmalloc((void **)&d_keys1, nn1 * 4));
                 g.dev.push_back(d_keys1);
                 hipLaunchKernelGGL(kd_small_kernel, dim3(1), dim3(256), 0, stream, d_rows, dd, (const int *)t->d_pidx,
                                    dn, 1, d_cut1, d_keys1, t->d_box);

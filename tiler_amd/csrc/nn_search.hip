@@ -1601,8 +1601,8 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hip
     // scale: power of two so that max|v| * scale <= 16384
     unsigned int *d_m = nullptr;
     DsStat *d_ds = nullptr;
-    TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_m, 2 * sizeof(unsigned int)));
-    TILER_HIP_CHECK_NULL(hipMalloc((void **)&d_ds, sizeof(DsStat)));
+    TILER_HIP_CHECK_NULL(dmalloc((void **)&d_m, 2 * sizeof(unsigned int)));
+    TILER_HIP_CHECK_NULL(dmalloc((void **)&d_ds, sizeof(DsStat)));
     TILER_HIP_CHECK_NULL(hipMemsetAsync(d_m, 0, 2 * sizeof(unsigned int), stream));
     TILER_HIP_CHECK_NULL(hipMemsetAsync(d_ds, 0, sizeof(DsStat), stream));
     const long total = (long)n * d;
@@ -1622,9 +1622,9 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hip
     }
     ix->scale = scale;
     ix->perm = all_int ? 0 : 1;
-    TILER_HIP_CHECK_NULL(hipMalloc(&ix->d_frag, (size_t)ix->nblk * ix->S * 64 * 16));
-    TILER_HIP_CHECK_NULL(hipMalloc((void **)&ix->d_nc, (size_t)ix->nblk * 32 * sizeof(float)));
-    TILER_HIP_CHECK_NULL(hipMalloc((void **)&ix->d_seed, (size_t)ix->nblk * 32 * sizeof(float)));
+    TILER_HIP_CHECK_NULL(dmalloc(&ix->d_frag, (size_t)ix->nblk * ix->S * 64 * 16));
+    TILER_HIP_CHECK_NULL(dmalloc((void **)&ix->d_nc, (size_t)ix->nblk * 32 * sizeof(float)));
+    TILER_HIP_CHECK_NULL(dmalloc((void **)&ix->d_seed, (size_t)ix->nblk * 32 * sizeof(float)));
     PrepArgs pa{d_rows, n, d, ix->S, scale, (half8 *)ix->d_frag, ix->d_nc, ix->d_seed, nullptr, d_ds, ix->perm};
     hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)std::min<long>(4096, (ix->nblk + 3) / 4)), dim3(256), 0,
                        stream, pa);
@@ -1632,8 +1632,8 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hip
     DsStat ds;
     TILER_HIP_CHECK_NULL(hipMemcpyAsync(&ds, d_ds, sizeof(ds), hipMemcpyDeviceToHost, stream));
     TILER_HIP_CHECK_NULL(hipStreamSynchronize(stream));
-    hipFree(d_m);
-    hipFree(d_ds);
+    dfree(d_m);
+    dfree(d_ds);
     auto bits2d = [](unsigned long long b) {
         double v;
         memcpy(&v, &b, 8);
@@ -1649,8 +1649,8 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hip
     if (ix->S > 0 && ix->perm && (d + 31) / 32 == 6) {
         ix->S16 = 6;
         ix->nblk16 = (int)((n + 15) / 16);
-        TILER_HIP_CHECK_NULL(hipMalloc(&ix->d_frag16, (size_t)ix->nblk16 * ix->S16 * 1024));
-        TILER_HIP_CHECK_NULL(hipMalloc((void **)&ix->d_seed16, (size_t)ix->nblk16 * 16 * sizeof(float)));
+        TILER_HIP_CHECK_NULL(dmalloc(&ix->d_frag16, (size_t)ix->nblk16 * ix->S16 * 1024));
+        TILER_HIP_CHECK_NULL(dmalloc((void **)&ix->d_seed16, (size_t)ix->nblk16 * 16 * sizeof(float)));
         Prep16Args p16{d_rows, n, d, ix->S16, scale, (half8 *)ix->d_frag16, ix->d_seed16, 1, d == 192 ? 1 : 0};
         hipLaunchKernelGGL(prep16_kernel, dim3((unsigned)std::min<long>(4096, (ix->nblk16 + 3) / 4)), dim3(256), 0,
                            stream, p16);
@@ -1662,51 +1662,53 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hip
 }
 
 void nn_scratch_free(SearchScratch &s) {
-    hipFree(s.qfrag);
-    hipFree(s.qfrag16);
-    hipFree(s.qstat);
-    hipFree(s.key);
-    hipFree(s.idx);
-    hipFree(s.fb_list);
-    hipFree(s.fb_count);
-    hipFree(s.qrows);
-    hipFree(s.thr);
-    hipFree(s.gate);
-    hipFree(s.ex_list);
-    hipFree(s.ccnt);
-    hipFree(s.cbuf);
-    hipFree(s.kd_list);
-    hipFree(s.kd_count);
-    hipFree(s.kd_rootbox);
-    hipFree(s.kd_done);
-    hipFree(s.t2best);
-    hipFree(s.fperm);
-    hipFree(s.fbcnt);
-    hipFree(s.fcnt);
-    hipFree(s.fflag);
-    hipFree(s.fidx);
-    hipFree(s.ferr);
-    hipFree(s.ftile);
-    hipFree(s.fpal);
-    hipFree(s.fhm);
-    hipFree(s.fvm);
+    (void)hipDeviceSynchronize();  // dfree files the blocks for reuse: nothing may still read them (hipFree's rule)
+    dfree(s.qfrag);
+    dfree(s.qfrag16);
+    dfree(s.qstat);
+    dfree(s.key);
+    dfree(s.idx);
+    dfree(s.fb_list);
+    dfree(s.fb_count);
+    dfree(s.qrows);
+    dfree(s.thr);
+    dfree(s.gate);
+    dfree(s.ex_list);
+    dfree(s.ccnt);
+    dfree(s.cbuf);
+    dfree(s.kd_list);
+    dfree(s.kd_count);
+    dfree(s.kd_rootbox);
+    dfree(s.kd_done);
+    dfree(s.t2best);
+    dfree(s.fperm);
+    dfree(s.fbcnt);
+    dfree(s.fcnt);
+    dfree(s.fflag);
+    dfree(s.fidx);
+    dfree(s.ferr);
+    dfree(s.ftile);
+    dfree(s.fpal);
+    dfree(s.fhm);
+    dfree(s.fvm);
     s = SearchScratch();
 }
 
 void nn_index_destroy(NNIndex *ix) {
     if (!ix) return;
+    (void)hipDeviceSynchronize();  // once for the whole index (dfree: hipFree's rule made explicit)
     orbit_destroy(ix->orbit);
     kd_tree_destroy(ix->kd);
-    hipFree(ix->d_rows);
-    hipFree(ix->d_rowsT);
-    hipFree(ix->d_frag);
-    hipFree(ix->d_nc);
-    hipFree(ix->d_seed);
-    hipFree(ix->d_frag16);
-    hipFree(ix->d_seed16);
-    hipFree(ix->d_tr_tile);
-    hipFree(ix->d_tr_pal);
-    hipFree(ix->d_tr_attr);
+    dfree(ix->d_rows);
+    dfree(ix->d_rowsT);
+    dfree(ix->d_frag);
+    dfree(ix->d_nc);
+    dfree(ix->d_seed);
+    dfree(ix->d_frag16);
+    dfree(ix->d_seed16);
+    dfree(ix->d_tr_tile);
+    dfree(ix->d_tr_pal);
+    dfree(ix->d_tr_attr);
     nn_scratch_free(ix->scratch);
     hipHostFree(ix->h_fb_count);
     if (ix->done_event) hipEventDestroy(ix->done_event);
@@ -1718,19 +1720,21 @@ static constexpr int TIER2_CAP = 1024;   // generic tier 2: collected candidates
 
 static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
     SearchScratch &s = ix->scratch;
+    if ((size_t)nq > s.cap_q || (size_t)nkeys > s.cap_keys)
+        (void)hipDeviceSynchronize();  // the outgrown buffers go back to the block cache: earlier searches must be done
     if ((size_t)nq > s.cap_q) {
-        hipFree(s.qfrag);
-        hipFree(s.qfrag16);
-        hipFree(s.qstat);
-        hipFree(s.fb_list);
-        hipFree(s.fb_count);
-        hipFree(s.thr);
-        hipFree(s.gate);
-        hipFree(s.ex_list);
-        hipFree(s.kd_list);
-        hipFree(s.kd_rootbox);
-        hipFree(s.kd_done);
-        hipFree(s.t2best);
+        dfree(s.qfrag);
+        dfree(s.qfrag16);
+        dfree(s.qstat);
+        dfree(s.fb_list);
+        dfree(s.fb_count);
+        dfree(s.thr);
+        dfree(s.gate);
+        dfree(s.ex_list);
+        dfree(s.kd_list);
+        dfree(s.kd_rootbox);
+        dfree(s.kd_done);
+        dfree(s.t2best);
         s.qfrag = s.qfrag16 = nullptr;
         s.qstat = nullptr;
         s.fb_list = s.fb_count = s.ex_list = s.kd_list = nullptr;
@@ -1740,29 +1744,29 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
         s.t2best = nullptr;
         s.cap_q = 0;
         const long nqblk = (nq + 31) / 32 + 2;
-        TILER_HIP_CHECK(hipMalloc(&s.qfrag, (size_t)nqblk * 16 * 64 * 16));
-        TILER_HIP_CHECK(hipMalloc(&s.qfrag16, (size_t)((nq + 15) / 16 + 2) * 8 * 64 * 16));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.qstat, (size_t)nq * sizeof(QStat)));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.fb_list, (size_t)nq * sizeof(int)));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.fb_count, 16));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.thr, (size_t)nq * sizeof(float)));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.gate, (size_t)nq * sizeof(float2)));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.ex_list, (size_t)nq * sizeof(int)));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.kd_list, (size_t)nq * sizeof(int)));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.kd_rootbox, (size_t)nq * sizeof(float)));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.kd_done, (size_t)nq));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.t2best, (size_t)nq * sizeof(unsigned long long)));
+        TILER_HIP_CHECK(dmalloc(&s.qfrag, (size_t)nqblk * 16 * 64 * 16));
+        TILER_HIP_CHECK(dmalloc(&s.qfrag16, (size_t)((nq + 15) / 16 + 2) * 8 * 64 * 16));
+        TILER_HIP_CHECK(dmalloc((void **)&s.qstat, (size_t)nq * sizeof(QStat)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.fb_list, (size_t)nq * sizeof(int)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.fb_count, 16));
+        TILER_HIP_CHECK(dmalloc((void **)&s.thr, (size_t)nq * sizeof(float)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.gate, (size_t)nq * sizeof(float2)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.ex_list, (size_t)nq * sizeof(int)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.kd_list, (size_t)nq * sizeof(int)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.kd_rootbox, (size_t)nq * sizeof(float)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.kd_done, (size_t)nq));
+        TILER_HIP_CHECK(dmalloc((void **)&s.t2best, (size_t)nq * sizeof(unsigned long long)));
         s.cap_q = nq;
     }
-    if (!s.kd_count) TILER_HIP_CHECK(hipMalloc((void **)&s.kd_count, 16));
+    if (!s.kd_count) TILER_HIP_CHECK(dmalloc((void **)&s.kd_count, 16));
     if ((size_t)nkeys > s.cap_keys) {
-        hipFree(s.key);
-        hipFree(s.idx);
+        dfree(s.key);
+        dfree(s.idx);
         s.key = nullptr;
         s.idx = nullptr;
         s.cap_keys = 0;
-        TILER_HIP_CHECK(hipMalloc((void **)&s.key, (size_t)nkeys * sizeof(float)));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.idx, (size_t)nkeys * sizeof(int)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.key, (size_t)nkeys * sizeof(float)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.idx, (size_t)nkeys * sizeof(int)));
         s.cap_keys = nkeys;
     }
     return 0;
@@ -2031,7 +2035,7 @@ static int scan_small(NNIndex *ix, RescoreArgs &ra, int nq, int k, hipStream_t s
     const bool rows_scan = !orb && K == 1 && ix->d % 64 == 0 && ix->n <= SCAN_ROWS_MAXN;
     if (rows_scan && !ix->d_rowsT) {
         const long nb = ((long)ix->n + 63) / 64;
-        TILER_HIP_CHECK(hipMalloc((void **)&ix->d_rowsT, (size_t)nb * 64 * ix->d * sizeof(float)));
+        TILER_HIP_CHECK(dmalloc((void **)&ix->d_rowsT, (size_t)nb * 64 * ix->d * sizeof(float)));
         hipLaunchKernelGGL(rows_interleave_kernel, dim3((unsigned)std::min<long>(8192, (nb * 64 * (ix->d / 4) + 255) / 256)),
                            dim3(256), 0, stream, (const float4 *)ix->d_rows, (long)ix->n, ix->d / 4, (float4 *)ix->d_rowsT);
         TILER_HIP_CHECK(hipGetLastError());
@@ -2188,8 +2192,8 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     ra.ex_count = s.fb_count + 1;
     ra.thr = s.thr;
     if (!s.ccnt) {  // the generic tier 2's collect buffers (256 MB), on the first search that can need them
-        TILER_HIP_CHECK(hipMalloc((void **)&s.ccnt, (size_t)TIER2_MAX * sizeof(int)));
-        TILER_HIP_CHECK(hipMalloc((void **)&s.cbuf, (size_t)TIER2_MAX * TIER2_CAP * sizeof(int)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.ccnt, (size_t)TIER2_MAX * sizeof(int)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.cbuf, (size_t)TIER2_MAX * TIER2_CAP * sizeof(int)));
     }
     ra.ccnt = s.ccnt;
     ra.cbuf = s.cbuf;
@@ -2333,10 +2337,11 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
     }
     SearchScratch &s = ix->scratch;
     if ((size_t)Q > s.cap_rows) {
-        hipFree(s.qrows);
+        (void)hipDeviceSynchronize();  // the outgrown buffer goes back to the block cache: earlier searches must be done
+        dfree(s.qrows);
         s.qrows = nullptr;
         s.cap_rows = 0;
-        TILER_HIP_CHECK(hipMalloc((void **)&s.qrows, (size_t)Q * 192 * sizeof(float)));
+        TILER_HIP_CHECK(dmalloc((void **)&s.qrows, (size_t)Q * 192 * sizeof(float)));
         s.cap_rows = Q;
     }
     const bool fuse_rb = ix->kd && use_wavelets && ix->kd->dd == 192;
@@ -2352,30 +2357,31 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
         if (!noflat && Q >= 8192 && (flat_generic || ((const OrbitIndex *)ix->orbit)->gblk >= 1024)) {
             const int nb = (Q + 255) / 256;
             if ((size_t)Q > s.cap_flat) {
-                hipFree(s.fperm);
-                hipFree(s.fbcnt);
-                hipFree(s.fflag);
-                hipFree(s.fidx);
-                hipFree(s.ferr);
-                hipFree(s.ftile);
-                hipFree(s.fpal);
-                hipFree(s.fhm);
-                hipFree(s.fvm);
+                (void)hipDeviceSynchronize();  // (as above)
+                dfree(s.fperm);
+                dfree(s.fbcnt);
+                dfree(s.fflag);
+                dfree(s.fidx);
+                dfree(s.ferr);
+                dfree(s.ftile);
+                dfree(s.fpal);
+                dfree(s.fhm);
+                dfree(s.fvm);
                 s.fperm = s.fbcnt = s.fidx = nullptr;  // a failed allocation below leaves nothing dangling
                 s.fflag = s.fhm = s.fvm = nullptr;
                 s.ferr = nullptr;
                 s.ftile = s.fpal = nullptr;
                 s.cap_flat = 0;
-                if (!s.fcnt) TILER_HIP_CHECK(hipMalloc((void **)&s.fcnt, sizeof(int)));
-                TILER_HIP_CHECK(hipMalloc((void **)&s.fperm, (size_t)Q * sizeof(int)));
-                TILER_HIP_CHECK(hipMalloc((void **)&s.fbcnt, (size_t)nb * sizeof(int)));
-                TILER_HIP_CHECK(hipMalloc((void **)&s.fflag, (size_t)Q));
-                TILER_HIP_CHECK(hipMalloc((void **)&s.fidx, (size_t)Q * sizeof(int)));
-                TILER_HIP_CHECK(hipMalloc((void **)&s.ferr, (size_t)Q * sizeof(float)));
-                TILER_HIP_CHECK(hipMalloc((void **)&s.ftile, (size_t)Q * sizeof(int32_t)));
-                TILER_HIP_CHECK(hipMalloc((void **)&s.fpal, (size_t)Q * sizeof(int32_t)));
-                TILER_HIP_CHECK(hipMalloc((void **)&s.fhm, (size_t)Q));
-                TILER_HIP_CHECK(hipMalloc((void **)&s.fvm, (size_t)Q));
+                if (!s.fcnt) TILER_HIP_CHECK(dmalloc((void **)&s.fcnt, sizeof(int)));
+                TILER_HIP_CHECK(dmalloc((void **)&s.fperm, (size_t)Q * sizeof(int)));
+                TILER_HIP_CHECK(dmalloc((void **)&s.fbcnt, (size_t)nb * sizeof(int)));
+                TILER_HIP_CHECK(dmalloc((void **)&s.fflag, (size_t)Q));
+                TILER_HIP_CHECK(dmalloc((void **)&s.fidx, (size_t)Q * sizeof(int)));
+                TILER_HIP_CHECK(dmalloc((void **)&s.ferr, (size_t)Q * sizeof(float)));
+                TILER_HIP_CHECK(dmalloc((void **)&s.ftile, (size_t)Q * sizeof(int32_t)));
+                TILER_HIP_CHECK(dmalloc((void **)&s.fpal, (size_t)Q * sizeof(int32_t)));
+                TILER_HIP_CHECK(dmalloc((void **)&s.fhm, (size_t)Q));
+                TILER_HIP_CHECK(dmalloc((void **)&s.fvm, (size_t)Q));
                 s.cap_flat = Q;
             }
             hipLaunchKernelGGL(ft_flat_flag_kernel, dim3(nb), dim3(256), 0, stream, d_rgb, Q, s.fflag, s.fbcnt);

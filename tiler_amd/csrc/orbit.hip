@@ -2056,26 +2056,27 @@ __global__ __launch_bounds__(256) void orbit_base_kernel(const float *__restrict
 
 void orbit_destroy(OrbitIndex *o) {
     if (!o) return;
-    hipFree(o->d_bmask);
-    hipFree(o->d_bmask0);
-    hipFree(o->d_frag);
-    hipFree(o->d_rowh);
-    hipFree(o->d_seed);
-    hipFree(o->d_nc);
-    hipFree(o->d_member);
-    hipFree(o->d_dup);
-    hipFree(o->d_rep);
-    hipFree(o->d_gorder);
-    hipFree(o->d_grp_of);
-    hipFree(o->d_map);
-    hipFree(o->d_base);
-    hipFree(o->qfrag);
-    hipFree(o->qstat);
-    hipFree(o->pair_cnt);
-    hipFree(o->pair_cand);
-    hipFree(o->d_stats);
-    hipFree(o->key);
-    hipFree(o->id);
+    (void)hipDeviceSynchronize();  // dfree files the blocks for reuse: nothing may still read them (hipFree's rule)
+    dfree(o->d_bmask);
+    dfree(o->d_bmask0);
+    dfree(o->d_frag);
+    dfree(o->d_rowh);
+    dfree(o->d_seed);
+    dfree(o->d_nc);
+    dfree(o->d_member);
+    dfree(o->d_dup);
+    dfree(o->d_rep);
+    dfree(o->d_gorder);
+    dfree(o->d_grp_of);
+    dfree(o->d_map);
+    dfree(o->d_base);
+    dfree(o->qfrag);
+    dfree(o->qstat);
+    dfree(o->pair_cnt);
+    dfree(o->pair_cand);
+    dfree(o->d_stats);
+    dfree(o->key);
+    dfree(o->id);
     delete o;
 }
 
@@ -2088,16 +2089,16 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     const long n = ix->n;
     OrbitMap *d_map = nullptr;
     uint16_t *d_bits = nullptr;
-    TILER_HIP_CHECK(hipMalloc((void **)&d_map, sizeof(OrbitMap)));
+    TILER_HIP_CHECK(dmalloc((void **)&d_map, sizeof(OrbitMap)));
     TILER_HIP_CHECK(hipMemcpyAsync(d_map, &hmap, sizeof(OrbitMap), hipMemcpyHostToDevice, stream));
-    TILER_HIP_CHECK(hipMalloc((void **)&d_bits, n * sizeof(uint16_t)));
+    TILER_HIP_CHECK(dmalloc((void **)&d_bits, n * sizeof(uint16_t)));
     hipLaunchKernelGGL(orbit_eq_kernel, dim3((unsigned)std::min<long>(8192, (n + 3) / 4)), dim3(256), 0, stream,
                        ix->d_rows, n, d_map, d_bits);
     TILER_HIP_CHECK(hipGetLastError());
     std::vector<uint16_t> bits(n);
     TILER_HIP_CHECK(hipMemcpyAsync(bits.data(), d_bits, n * sizeof(uint16_t), hipMemcpyDeviceToHost, stream));
     TILER_HIP_CHECK(hipStreamSynchronize(stream));
-    hipFree(d_bits);
+    dfree(d_bits);
     // greedy grouping in index order: candidate j joins the open group (base s) in a free mirror slot m
     // if row_j == S_m row_s (checked on the device above); otherwise it opens a new group
     std::vector<int> member;
@@ -2126,7 +2127,7 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     }
     const long G = (long)member.size() / 4;
     if (G * 10 > n * 7) {  // < ~1.43 candidates per orbit: the generic kernels are as fast
-        hipFree(d_map);
+        dfree(d_map);
         return 1;
     }
     OrbitIndex *o = new OrbitIndex();
@@ -2134,25 +2135,25 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     o->gblk = (int)((G + 31) / 32);
     o->d_map = d_map;
     OrbitDsStat *d_ds = nullptr;
-    TILER_HIP_CHECK(hipMalloc((void **)&o->d_member, G * 4 * sizeof(int)));
+    TILER_HIP_CHECK(dmalloc((void **)&o->d_member, G * 4 * sizeof(int)));
     TILER_HIP_CHECK(hipMemcpyAsync(o->d_member, member.data(), G * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
-    TILER_HIP_CHECK(hipMalloc((void **)&o->d_dup, G));
-    TILER_HIP_CHECK(hipMalloc((void **)&o->d_rep, G));
+    TILER_HIP_CHECK(dmalloc((void **)&o->d_dup, G));
+    TILER_HIP_CHECK(dmalloc((void **)&o->d_rep, G));
     hipLaunchKernelGGL(orbit_dup_kernel, dim3((unsigned)std::min<long>(8192, (G + 3) / 4)), dim3(256), 0, stream,
                        ix->d_rows, o->d_member, G, o->d_dup, o->d_rep);
     if (ix->kd) {  // ANN's order inside every group (the tree exists: nn_index_create_dev builds it first)
-        TILER_HIP_CHECK(hipMalloc((void **)&o->d_gorder, G * sizeof(GroupOrder)));
-        TILER_HIP_CHECK(hipMalloc((void **)&o->d_grp_of, n * sizeof(int)));
+        TILER_HIP_CHECK(dmalloc((void **)&o->d_gorder, G * sizeof(GroupOrder)));
+        TILER_HIP_CHECK(dmalloc((void **)&o->d_grp_of, n * sizeof(int)));
         TILER_HIP_CHECK(hipMemsetAsync(o->d_grp_of, 0xff, n * sizeof(int), stream));
         hipLaunchKernelGGL(orbit_gorder_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, stream, ix->kd->view(),
                            o->d_member, G, o->d_gorder, o->d_grp_of);
     }
     TILER_HIP_CHECK(hipGetLastError());
-    TILER_HIP_CHECK(hipMalloc(&o->d_frag, (size_t)o->gblk * OS * 1024));
-    TILER_HIP_CHECK(hipMalloc(&o->d_rowh, (size_t)G * OD * 2));
-    TILER_HIP_CHECK(hipMalloc((void **)&o->d_seed, (size_t)o->gblk * 32 * sizeof(float)));
-    TILER_HIP_CHECK(hipMalloc((void **)&o->d_nc, (size_t)G * sizeof(float)));
-    TILER_HIP_CHECK(hipMalloc((void **)&d_ds, sizeof(OrbitDsStat)));
+    TILER_HIP_CHECK(dmalloc(&o->d_frag, (size_t)o->gblk * OS * 1024));
+    TILER_HIP_CHECK(dmalloc(&o->d_rowh, (size_t)G * OD * 2));
+    TILER_HIP_CHECK(dmalloc((void **)&o->d_seed, (size_t)o->gblk * 32 * sizeof(float)));
+    TILER_HIP_CHECK(dmalloc((void **)&o->d_nc, (size_t)G * sizeof(float)));
+    TILER_HIP_CHECK(dmalloc((void **)&d_ds, sizeof(OrbitDsStat)));
     TILER_HIP_CHECK(hipMemsetAsync(d_ds, 0, sizeof(OrbitDsStat), stream));
     OrbitPrepArgs pa{ix->d_rows, o->d_member, G, (const OrbitMap *)d_map, ix->scale, (half8 *)o->d_frag,
                      (_Float16 *)o->d_rowh, o->d_seed, o->d_nc, d_ds, nullptr};
@@ -2162,7 +2163,7 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     OrbitDsStat ds;
     TILER_HIP_CHECK(hipMemcpyAsync(&ds, d_ds, sizeof(ds), hipMemcpyDeviceToHost, stream));
     TILER_HIP_CHECK(hipStreamSynchronize(stream));
-    hipFree(d_ds);
+    dfree(d_ds);
     if (ds.bad) {
         orbit_destroy(o);
         return 1;
@@ -2179,13 +2180,13 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     // Every other structure is indexed by the group number and rebuilt for the new order (member drives them all).
     {
         uint8_t *d_mask = nullptr;
-        TILER_HIP_CHECK(hipMalloc((void **)&d_mask, G));
+        TILER_HIP_CHECK(dmalloc((void **)&d_mask, G));
         hipLaunchKernelGGL(orbit_zmask_kernel, dim3((unsigned)std::min<long>(8192, (G + 3) / 4)), dim3(256), 0, stream,
                            (const _Float16 *)o->d_rowh, G, d_mask);
         std::vector<uint8_t> mask(G);
         TILER_HIP_CHECK(hipMemcpyAsync(mask.data(), d_mask, G, hipMemcpyDeviceToHost, stream));
         TILER_HIP_CHECK(hipStreamSynchronize(stream));
-        hipFree(d_mask);
+        dfree(d_mask);
         auto key = [](unsigned m) { return (m & ~1u) == 0 ? 0 : (m & ~5u) == 0 ? 1 : (m & ~3u) == 0 ? 2 : 3; };
         long cnt[5] = {0, 0, 0, 0, 0};  // stable counting sort by class (4 keys)
         for (long g = 0; g < G; g++) cnt[key(mask[g]) + 1]++;
@@ -2202,7 +2203,7 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
             for (long g = 0; g < (long)o->red_end * 32 && g < G; g++) bm[g / 32] |= mask[order[g]] | 1u;
             o->ksteps = 12 * (o->gblk - o->red_end);
             for (int b = 0; b < o->red_end; b++) o->ksteps += 3 * __builtin_popcount(bm[b]);
-            TILER_HIP_CHECK(hipMalloc((void **)&o->d_bmask, o->red_end));
+            TILER_HIP_CHECK(dmalloc((void **)&o->d_bmask, o->red_end));
             TILER_HIP_CHECK(hipMemcpyAsync(o->d_bmask, bm.data(), o->red_end, hipMemcpyHostToDevice, stream));
             TILER_HIP_CHECK(hipMemcpyAsync(o->d_member, pm.data(), G * 4 * sizeof(int), hipMemcpyHostToDevice, stream));
             hipLaunchKernelGGL(orbit_dup_kernel, dim3((unsigned)std::min<long>(8192, (G + 3) / 4)), dim3(256), 0, stream,
@@ -2212,7 +2213,7 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
                 hipLaunchKernelGGL(orbit_gorder_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, stream,
                                    ix->kd->view(), o->d_member, G, o->d_gorder, o->d_grp_of);
             }
-            TILER_HIP_CHECK(hipMalloc((void **)&d_ds, sizeof(OrbitDsStat)));
+            TILER_HIP_CHECK(dmalloc((void **)&d_ds, sizeof(OrbitDsStat)));
             TILER_HIP_CHECK(hipMemsetAsync(d_ds, 0, sizeof(OrbitDsStat), stream));
             OrbitPrepArgs pb{ix->d_rows, o->d_member, G, (const OrbitMap *)d_map, ix->scale, (half8 *)o->d_frag,
                              (_Float16 *)o->d_rowh, o->d_seed, o->d_nc, d_ds, nullptr};
@@ -2220,7 +2221,7 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
                                dim3(64 * ORB_PW), 0, stream, pb);
             TILER_HIP_CHECK(hipGetLastError());
             TILER_HIP_CHECK(hipStreamSynchronize(stream));  // (pm, bm) stay alive until the copies are done
-            hipFree(d_ds);
+            dfree(d_ds);
         }
     }
     {  // the base rows in (final) group order for the small-batch orbit scan, whose mirror tables are compiled in
@@ -2233,7 +2234,7 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
             }
         if (ok) {
             const long nb = (G + 63) / 64;
-            TILER_HIP_CHECK(hipMalloc((void **)&o->d_base, (size_t)nb * 64 * OD * sizeof(float)));
+            TILER_HIP_CHECK(dmalloc((void **)&o->d_base, (size_t)nb * 64 * OD * sizeof(float)));
             hipLaunchKernelGGL(orbit_base_kernel, dim3((unsigned)std::min<long>(8192, (nb * 64 * (OD / 4) + 255) / 256)),
                                dim3(256), 0, stream, ix->d_rows, (const int *)o->d_member, G, (float4 *)o->d_base);
             TILER_HIP_CHECK(hipGetLastError());
@@ -2241,7 +2242,7 @@ int orbit_build(NNIndex *ix, hipStream_t stream) {
     }
     {  // block 0 only, every block: the flat query tiles' shortlist (orbit_search)
         std::vector<uint8_t> ones(o->gblk, 1);
-        TILER_HIP_CHECK(hipMalloc((void **)&o->d_bmask0, o->gblk));
+        TILER_HIP_CHECK(dmalloc((void **)&o->d_bmask0, o->gblk));
         TILER_HIP_CHECK(hipMemcpyAsync(o->d_bmask0, ones.data(), o->gblk, hipMemcpyHostToDevice, stream));
         TILER_HIP_CHECK(hipStreamSynchronize(stream));
     }
@@ -2254,18 +2255,19 @@ static constexpr int ORB_L = 4, ORB_CB = 4, ORB_NW = 8, ORB_QB = 2;
 int orbit_ensure_queries(OrbitIndex *o, int nq) {
     if ((size_t)nq <= o->cap_q) return 0;
     const long nqblk = (nq + 31) / 32;
-    hipFree(o->qfrag);
-    hipFree(o->qstat);
-    hipFree(o->pair_cnt);
-    hipFree(o->pair_cand);
+    (void)hipDeviceSynchronize();  // the smaller buffers go back to the block cache: earlier searches must be done
+    dfree(o->qfrag);
+    dfree(o->qstat);
+    dfree(o->pair_cnt);
+    dfree(o->pair_cand);
     o->qfrag = nullptr;  // a failed allocation below leaves nothing dangling
     o->qstat = nullptr;
     o->pair_cnt = o->pair_cand = nullptr;
     o->cap_q = 0;
-    TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cnt, (size_t)nq * sizeof(int)));
-    TILER_HIP_CHECK(hipMalloc((void **)&o->pair_cand, (size_t)nq * ORB_PSLOTS * sizeof(int)));
-    TILER_HIP_CHECK(hipMalloc(&o->qfrag, (size_t)(nqblk + 1) * OS * 1024));
-    TILER_HIP_CHECK(hipMalloc((void **)&o->qstat, (size_t)nq * sizeof(OrbitStat)));
+    TILER_HIP_CHECK(dmalloc((void **)&o->pair_cnt, (size_t)nq * sizeof(int)));
+    TILER_HIP_CHECK(dmalloc((void **)&o->pair_cand, (size_t)nq * ORB_PSLOTS * sizeof(int)));
+    TILER_HIP_CHECK(dmalloc(&o->qfrag, (size_t)(nqblk + 1) * OS * 1024));
+    TILER_HIP_CHECK(dmalloc((void **)&o->qstat, (size_t)nq * sizeof(OrbitStat)));
     o->cap_q = nq;
     return 0;
 }
@@ -2327,13 +2329,14 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     if (orbit_ensure_queries(o, nq)) return -1;
     const size_t nkeys = (size_t)nq * nsplit * 2 * ORB_L;
     if (nkeys > o->cap_keys) {
-        hipFree(o->key);
-        hipFree(o->id);
+        (void)hipDeviceSynchronize();  // (as orbit_ensure_queries)
+        dfree(o->key);
+        dfree(o->id);
         o->key = nullptr;
         o->id = nullptr;
         o->cap_keys = 0;
-        TILER_HIP_CHECK(hipMalloc((void **)&o->key, nkeys * sizeof(float)));
-        TILER_HIP_CHECK(hipMalloc((void **)&o->id, nkeys * sizeof(int)));
+        TILER_HIP_CHECK(dmalloc((void **)&o->key, nkeys * sizeof(float)));
+        TILER_HIP_CHECK(dmalloc((void **)&o->id, nkeys * sizeof(int)));
         o->cap_keys = nkeys;
     }
     if (!queries_prepared) {  // (the FrameTiling path prepares them inside its descriptor kernel, orbit_ft_queries)
@@ -2406,7 +2409,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         return e && e[0] == '1';
     }();
     if (want_stats) {
-        if (!o->d_stats) TILER_HIP_CHECK(hipMalloc((void **)&o->d_stats, 2 * sizeof(int)));
+        if (!o->d_stats) TILER_HIP_CHECK(dmalloc((void **)&o->d_stats, 2 * sizeof(int)));
         TILER_HIP_CHECK(hipMemsetAsync(o->d_stats, 0, 2 * sizeof(int), stream));
         ra.t.n_expand = o->d_stats;
     }

@@ -276,7 +276,7 @@ NNIndex *prepare_frame_tiling_dev(NNIndex *global, PrepScratch &s, const int32_t
     TILER_HIP_CHECK_NULL(hipGetLastError());
     // 4. DoPsyV: the candidates' descriptors (fp64 -> fp32 rows), then the keyframe's index
     float *rows = nullptr;
-    TILER_HIP_CHECK_NULL(hipMalloc((void **)&rows, (size_t)std::max<long>(M, 1) * 192 * sizeof(float)));
+    TILER_HIP_CHECK_NULL(dmalloc((void **)&rows, (size_t)std::max<long>(M, 1) * 192 * sizeof(float)));  // the index owns it
     PsyvArgs pa;
     pa.n = M;
     pa.palpix = d_palpix;
@@ -295,8 +295,8 @@ NNIndex *prepare_frame_tiling_dev(NNIndex *global, PrepScratch &s, const int32_t
     NNIndex *ix = nn_index_create_dev(rows, (int)M, 192, 1, KD_SPLIT_STD, stream);  // owns rows
     if (!ix) return nullptr;
     const size_t n1 = std::max<long>(M, 1);
-    if (hipMalloc((void **)&ix->d_tr_tile, n1 * 4) != hipSuccess || hipMalloc((void **)&ix->d_tr_pal, n1 * 4) != hipSuccess ||
-        hipMalloc((void **)&ix->d_tr_attr, n1) != hipSuccess ||
+    if (dmalloc((void **)&ix->d_tr_tile, n1 * 4) != hipSuccess || dmalloc((void **)&ix->d_tr_pal, n1 * 4) != hipSuccess ||
+        dmalloc((void **)&ix->d_tr_attr, n1) != hipSuccess ||
         hipMemcpyAsync(ix->d_tr_tile, s.tile_of, (size_t)M * 4, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
         hipMemcpyAsync(ix->d_tr_pal, s.pal_of, (size_t)M * 4, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
         hipMemcpyAsync(ix->d_tr_attr, s.attrs, (size_t)M, hipMemcpyDeviceToDevice, stream) != hipSuccess) {

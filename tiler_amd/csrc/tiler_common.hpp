@@ -27,6 +27,13 @@ struct Luts {
 };
 const Luts &luts();
 
+// Device blocks of the search indexes (devmem.hip): dmalloc hands out an idle cached block of about the size, else
+// hipMalloc; dfree files the block for reuse -- the caller guarantees that no GPU work still uses it (hipFree's
+// implicit device synchronisation made explicit: the destroy paths synchronise once); dfree_sync synchronises first.
+hipError_t dmalloc(void **p, size_t bytes);
+void dfree(void *p);
+void dfree_sync(void *p);
+
 // Kernel timing (tiler_timing_*): RAII scope that records a HIP event pair on the launch stream.
 bool timing_enabled();
 struct KTimer {

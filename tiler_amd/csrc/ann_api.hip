@@ -439,7 +439,7 @@ ann_kdtree *ann_kdtree_create(float **pa, int n, int dd, int bs, int split) {
     t->dev = dev;
     t->placed = bytes;
     float *d_rows = nullptr;
-    if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
+    if (stream_get(&t->stream) != hipSuccess ||
         dmalloc((void **)&d_rows, std::max<size_t>(1, h.size()) * sizeof(float)) != hipSuccess ||
         (n > 0 && hipMemcpyAsync(d_rows, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, t->stream) !=
                       hipSuccess)) {
@@ -479,7 +479,7 @@ ann_kdtree *ann_kdtree_create_dev_ex(const float *d_rows_in, int n, int dd, int 
     // every failure below releases the handle (handle_free also takes its bytes back out of g_dev_load)
     float *d_rows = nullptr;
     const size_t bytes = (size_t)n * dd * sizeof(float);
-    const bool ok_stream = hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) == hipSuccess;
+    const bool ok_stream = stream_get(&t->stream) == hipSuccess;
     hipStream_t s = stream ? (hipStream_t)stream : t->stream;
     if (!ok_stream || dmalloc((void **)&d_rows, std::max<size_t>(4, bytes)) != hipSuccess ||
         (n > 0 && hipMemcpyAsync(d_rows, d_rows_in, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)) {
@@ -531,11 +531,11 @@ static void handle_free(ann_kdtree *t) {
         (void)hipFree(cs.d_res);
         (void)hipHostFree(cs.h_q);
         (void)hipHostFree(cs.h_res);
-        if (cs.stream) (void)hipStreamDestroy(cs.stream);
+        stream_put(cs.stream);
     }
     if (t->maps_ev) (void)hipEventDestroy(t->maps_ev);
     if (t->ready_ev) (void)hipEventDestroy(t->ready_ev);
-    if (t->stream) (void)hipStreamDestroy(t->stream);
+    stream_put(t->stream);  // (synchronised first) back to the device's pool
     unplace_handle(t->dev, t->placed);
     delete t;
 }
@@ -570,7 +570,7 @@ static ann_kdtree *replica_of(ann_kdtree *t, int dev) {
     if (hipStreamSynchronize(t->stream) != hipSuccess || (t->ready_ev && hipEventSynchronize(t->ready_ev) != hipSuccess) ||
         (t->maps_ev && hipEventSynchronize(t->maps_ev) != hipSuccess) ||
         (src->done_event && hipEventSynchronize(src->done_event) != hipSuccess) ||
-        hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
+        stream_get(&r->stream) != hipSuccess ||
         dmalloc((void **)&d_rows, std::max<size_t>(4, bytes)) != hipSuccess ||
         (bytes && hipMemcpyPeerAsync(d_rows, dev, src->d_rows, t->dev, bytes, r->stream) != hipSuccess)) {
         set_error("tiler: replica allocation or peer copy failed");
@@ -676,7 +676,7 @@ ann_kdtree *tiler_prepare_frame_tiling_dev(ann_kdtree *global_ds, const int32_t 
     DevScope ds(dev);
     ann_kdtree *t = new ann_kdtree();
     t->dev = dev;
-    if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (stream_get(&t->stream) != hipSuccess) {
         set_error("tiler_prepare_frame_tiling_dev: stream creation failed");
         delete t;
         return nullptr;
@@ -759,7 +759,7 @@ static int combine_run(ann_kdtree *t, CombineSlot &cs, std::vector<CombineReq *>
             }
         return 0;
     }
-    if (!cs.stream) TILER_HIP_CHECK(hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+    if (!cs.stream) TILER_HIP_CHECK(stream_get(&cs.stream));
     if ((size_t)nq * d > cs.cap_q) {
         (void)hipHostFree(cs.h_q);
         (void)hipFree(cs.d_q);

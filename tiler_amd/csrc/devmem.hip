@@ -15,6 +15,7 @@
 #include <map>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 
 #include "tiler_common.hpp"
 
@@ -102,6 +103,61 @@ void dfree_sync(void *p) {
     if (!p) return;
     (void)hipDeviceSynchronize();
     dfree(p);
+}
+
+// Streams and pinned count slots of the per-keyframe handles, reused the same way (a stream create / destroy pair and
+// a small pinned allocation + free are further driver calls per keyframe).
+namespace {
+std::vector<hipStream_t> g_streams[DM_MAX_DEV];
+std::vector<int *> g_slots;  // free 16-byte pinned slots
+}  // namespace
+
+hipError_t stream_get(hipStream_t *s) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    {
+        std::lock_guard<std::mutex> lk(g_dm_mu);
+        if (dev >= 0 && dev < DM_MAX_DEV && !g_streams[dev].empty()) {
+            *s = g_streams[dev].back();
+            g_streams[dev].pop_back();
+            return hipSuccess;
+        }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
+void stream_put(hipStream_t s) {
+    if (!s) return;
+    int dev = 0;
+    if (hipStreamSynchronize(s) != hipSuccess || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= DM_MAX_DEV) {
+        (void)hipStreamDestroy(s);
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_dm_mu);
+    if (g_streams[dev].size() >= 64) {
+        (void)hipStreamDestroy(s);
+        return;
+    }
+    g_streams[dev].push_back(s);
+}
+
+int *pinned_slot() {
+    std::lock_guard<std::mutex> lk(g_dm_mu);
+    if (g_slots.empty()) {  // one 64 KiB pinned page, carved into 4,096 slots (never returned)
+        void *page = nullptr;
+        if (hipHostMalloc(&page, 65536, hipHostMallocPortable) != hipSuccess) return nullptr;
+        for (int i = 4095; i >= 0; i--) g_slots.push_back(reinterpret_cast<int *>(static_cast<char *>(page) + 16 * i));
+    }
+    int *p = g_slots.back();
+    g_slots.pop_back();
+    return p;
+}
+
+void pinned_slot_free(int *p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_dm_mu);
+    g_slots.push_back(p);
 }
 
 }  // namespace tiler

@@ -756,9 +756,9 @@ KdOrder KdTree::view() const {
     return o;
 }
 
-void kd_tree_destroy(KdTree *t) {
+void kd_tree_destroy(KdTree *t, bool synced) {
     if (!t) return;
-    (void)hipDeviceSynchronize();  // dfree files the blocks for reuse: nothing may still read them (hipFree's rule)
+    if (!synced) (void)hipDeviceSynchronize();  // dfree files the blocks for reuse: nothing may still read them (hipFree's rule)
     dfree(t->d_pos);
     dfree(t->d_pidx);
     dfree(t->d_cd);

@@ -38,7 +38,7 @@ struct KdTree {
 
 // Builds the tree of d_rows[n][dd] (fp32, HBM) exactly as ANN's kd_tree constructor does; synchronous.
 KdTree *kd_tree_build(const float *d_rows, int n, int dd, int bs, hipStream_t stream);
-void kd_tree_destroy(KdTree *t);
+void kd_tree_destroy(KdTree *t, bool synced = false);  // synced: the caller already synchronised the device
 // leaf position of every point (host copy), for tests
 int kd_tree_positions(const KdTree *t, int32_t *pos);
 

@@ -1594,7 +1594,12 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hip
     }
     ix->S = pick_S(d);
     ix->nblk = (n + 31) / 32;
-    TILER_HIP_CHECK_NULL(hipHostMalloc((void **)&ix->h_fb_count, sizeof(int) * 2, hipHostMallocPortable));
+    ix->h_fb_count = pinned_slot();
+    if (!ix->h_fb_count) {
+        set_error("nn_index_create_dev: pinned host allocation failed");
+        nn_index_destroy(ix);
+        return nullptr;
+    }
     ix->h_fb_count[0] = 1 << 30;  // first call: full tier-2 grid
     ix->h_fb_count[1] = 0;
     if (ix->S == 0 || n == 0) return ix;
@@ -1661,8 +1666,9 @@ NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hip
     return ix;
 }
 
-void nn_scratch_free(SearchScratch &s) {
-    (void)hipDeviceSynchronize();  // dfree files the blocks for reuse: nothing may still read them (hipFree's rule)
+void nn_scratch_free(SearchScratch &s, bool synced) {
+    if (!synced && (s.qfrag || s.key || s.qrows || s.ccnt || s.fperm || s.kd_count))
+        (void)hipDeviceSynchronize();  // dfree files the blocks for reuse: nothing may still read them (hipFree's rule)
     dfree(s.qfrag);
     dfree(s.qfrag16);
     dfree(s.qstat);
@@ -1697,8 +1703,8 @@ void nn_scratch_free(SearchScratch &s) {
 void nn_index_destroy(NNIndex *ix) {
     if (!ix) return;
     (void)hipDeviceSynchronize();  // once for the whole index (dfree: hipFree's rule made explicit)
-    orbit_destroy(ix->orbit);
-    kd_tree_destroy(ix->kd);
+    orbit_destroy(ix->orbit, true);
+    kd_tree_destroy(ix->kd, true);
     dfree(ix->d_rows);
     dfree(ix->d_rowsT);
     dfree(ix->d_frag);
@@ -1709,8 +1715,8 @@ void nn_index_destroy(NNIndex *ix) {
     dfree(ix->d_tr_tile);
     dfree(ix->d_tr_pal);
     dfree(ix->d_tr_attr);
-    nn_scratch_free(ix->scratch);
-    hipHostFree(ix->h_fb_count);
+    nn_scratch_free(ix->scratch, true);
+    pinned_slot_free(ix->h_fb_count);
     if (ix->done_event) hipEventDestroy(ix->done_event);
     delete ix;
 }

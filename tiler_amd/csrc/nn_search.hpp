@@ -99,7 +99,7 @@ struct NNIndex {
 NNIndex *nn_index_create_dev(float *d_rows, int n, int d, int bs, int split, hipStream_t stream);
 void nn_index_destroy(NNIndex *ix);
 // release a SearchScratch's device buffers (an index's own, or a coalescer slot's)
-void nn_scratch_free(SearchScratch &s);
+void nn_scratch_free(SearchScratch &s, bool synced = false);
 // the search nn_search_dev runs for nq queries of k: the small-batch scan (true), which touches nothing of the index
 // but its read-only data and the scratch, or the shortlist path
 bool nn_search_is_small(const NNIndex *ix, int nq, int k);

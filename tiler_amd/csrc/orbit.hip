@@ -2054,9 +2054,9 @@ __global__ __launch_bounds__(256) void orbit_base_kernel(const float *__restrict
     }
 }
 
-void orbit_destroy(OrbitIndex *o) {
+void orbit_destroy(OrbitIndex *o, bool synced) {
     if (!o) return;
-    (void)hipDeviceSynchronize();  // dfree files the blocks for reuse: nothing may still read them (hipFree's rule)
+    if (!synced) (void)hipDeviceSynchronize();  // dfree files the blocks for reuse: nothing may still read them (hipFree's rule)
     dfree(o->d_bmask);
     dfree(o->d_bmask0);
     dfree(o->d_frag);

@@ -91,7 +91,7 @@ struct OrbitTail {
 
 // 0: orbit index built (ix->orbit), 1: dataset has no exploitable mirror structure, -1: HIP error
 int orbit_build(NNIndex *ix, hipStream_t stream);
-void orbit_destroy(OrbitIndex *o);
+void orbit_destroy(OrbitIndex *o, bool synced = false);
 inline long long orbit_groups(const NNIndex *ix) { return ix->orbit ? ((const OrbitIndex *)ix->orbit)->G : 0; }
 inline int orbit_ksteps(const NNIndex *ix) { return ix->orbit ? ((const OrbitIndex *)ix->orbit)->ksteps : 0; }
 // rescore counters of the last search (TILER_ORBIT_STATS=1, else 0): 4-entry expansion passes, candidates rescored

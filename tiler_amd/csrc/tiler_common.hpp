@@ -33,6 +33,12 @@ const Luts &luts();
 hipError_t dmalloc(void **p, size_t bytes);
 void dfree(void *p);
 void dfree_sync(void *p);
+// non-blocking streams of the current device, reused (stream_put synchronises the stream first)
+hipError_t stream_get(hipStream_t *s);
+void stream_put(hipStream_t s);
+// 16-byte pinned host slots (per-index tier-2 counters), reused
+int *pinned_slot();
+void pinned_slot_free(int *p);
 
 // Kernel timing (tiler_timing_*): RAII scope that records a HIP event pair on the launch stream.
 bool timing_enabled();

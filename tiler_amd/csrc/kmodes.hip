@@ -1306,10 +1306,65 @@ __global__ __launch_bounds__(256) void kmb_medoid(const uint8_t *X, const int32_
     }
 }
 
-// ---- host driver ----
 // centroid splits of an assignment block: ~64 centroids per block, so a chunk of the largest bin alone
 // still spreads over the chip (results merge by atomicMin)
-static int csplit_of(int K) { return std::max(1, std::min(128, (K + 63) / 64)); }
+__host__ __device__ inline int csplit_of(int K) {
+    const int c = (K + 63) / 64;
+    return c < 1 ? 1 : (c > 128 ? 128 : c);
+}
+
+// One iteration's work list, written on the device, one workgroup per chunk step c: every active bin's assignment
+// items (256 points x one centroid split each, in the active order), then one seq item per bin present at the step --
+// the list the host used to build and upload whenever the active set changed (up to 1.3 ms of GPU idle each time on
+// C4, profiles/r06/kt_kmodes_gaps_r06o.json).  step_off[c]: the first item of step c.
+static constexpr int KM_GEN_MAXB = 4096;  // active bins the generator takes (beyond: the host builds the list)
+__global__ __launch_bounds__(256) void kmb_gen_items(KmBatch B, const int *act, int nact, const int *step_off,
+                                                     KmAsgItem *out) {
+    __shared__ int s_off[KM_GEN_MAXB + 1];
+    const int c = blockIdx.x, p0 = c * KM_BIN;
+    if (threadIdx.x == 0) {
+        int o = 0;
+        for (int j = 0; j < nact; j++) {
+            const int r = act[j], n = B.boff[r + 1] - B.boff[r];
+            s_off[j] = o;
+            if (p0 < n) o += ((min(n - p0, KM_BIN) + 255) / 256) * csplit_of(B.koff[r + 1] - B.koff[r]);
+        }
+        s_off[nact] = o;
+    }
+    __syncthreads();
+    KmAsgItem *dst = out + step_off[c];
+    for (int j = 0; j < nact; j++) {
+        const int cnt = s_off[j + 1] - s_off[j];
+        if (cnt == 0) continue;  // bin absent at this step (uniform)
+        const int r = act[j], n = B.boff[r + 1] - B.boff[r], K = B.koff[r + 1] - B.koff[r];
+        const int p1 = min(n, p0 + KM_BIN), cs = csplit_of(K), per = (K + cs - 1) / cs;
+        for (int e = threadIdx.x; e < cnt; e += 256) {
+            const int qi = e / cs, cc = e - qi * cs, q0 = p0 + qi * 256;
+            KmAsgItem it;
+            it.bin = r;
+            it.p0 = q0;
+            it.p1 = min(p1, q0 + 256);
+            it.c0 = cc * per;
+            it.c1 = min(K, (cc + 1) * per);
+            it.pad[0] = it.pad[1] = it.pad[2] = 0;
+            dst[s_off[j] + e] = it;
+        }
+    }
+    if (threadIdx.x == 0) {  // the seq items, in the active order
+        int k = s_off[nact];
+        for (int j = 0; j < nact; j++) {
+            const int r = act[j], n = B.boff[r + 1] - B.boff[r];
+            if (p0 >= n) continue;
+            KmAsgItem it{};
+            it.bin = r;  // KmSeqItem view: bin, p0, p1
+            it.p0 = p0;
+            it.p1 = min(n, p0 + KM_BIN);
+            dst[k++] = it;
+        }
+    }
+}
+
+// ---- host driver ----
 
 // counters of the last batch (tiler_kmodes_last_stats): assignment (point, centroid) pairs and dependent chunk steps
 static std::atomic<long long> g_km_last_pairs{0}, g_km_last_steps{0};
@@ -1385,8 +1440,10 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
         max_items += (size_t)nch * ((KM_BIN + 255) / 256) * csplit_of(Kv[r]) + nch;
         max_items += (size_t)((nv[r] + 255) / 256) * csplit_of(Kv[r]);
     }
+    int max_steps = 0;  // chunk steps of the largest bin (the device work list's per-step offsets)
+    for (int r = 0; r < nb; r++) max_steps = std::max(max_steps, (nv[r] + KM_BIN - 1) / KM_BIN);
     const size_t item_bytes = (max_items + (size_t)poff[nb] + 64) * sizeof(KmAsgItem) +
-                              (size_t)(nb + 1) * 4 + 256;
+                              (size_t)(nb + 1 + max_steps) * 4 + 256;
     // farthest-first: one persistent launch for every round (kmb_ff_persist3) unless it cannot be placed
     const int g_ff = ff_persist_grid();
     TILER_HIP_CHECK(hipMalloc((void **)&buf, off + item_bytes));
@@ -1418,11 +1475,12 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
     int32_t *rand_rows = (int32_t *)(buf + o_rand);
     int rc = -1;
     std::vector<char> hitems;
-    auto upload = [&](const void *src, size_t bytes) -> int {  // work list -> device (synchronous: the
-        TILER_HIP_CHECK(hipMemcpyAsync(items, src, bytes, hipMemcpyHostToDevice, st));  // host buffer is reused)
+    auto upload_at = [&](size_t at, const void *src, size_t bytes) -> int {  // work list -> device (synchronous:
+        TILER_HIP_CHECK(hipMemcpyAsync(items + at, src, bytes, hipMemcpyHostToDevice, st));  // the host buffer is reused)
         TILER_HIP_CHECK(hipStreamSynchronize(st));
         return 0;
     };
+    auto upload = [&](const void *src, size_t bytes) -> int { return upload_at(0, src, bytes); };
     do {
         // permuted copy of X (bins contiguous in K order) + metadata
         for (int r = 0; r < nb; r++)
@@ -1538,48 +1596,91 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
             for (int r = 0; r < nb; r++) active[r] = r;
             std::vector<unsigned long long> best_cost(nb, ~0ull), hcost(nb);
             std::vector<int> hmoves(nb), herr(nb), iters(nb, 0);
+            // the work list depends only on the active bins: an iteration whose set is unchanged (from iteration ~13
+            // on at C4 only the largest bin is left) reuses the list already on the device.  Rebuilding and uploading
+            // the largest bin's ~73k items took 0.5-1.1 ms of GPU idle per iteration, 21 ms per C4 call
+            // (profiles/r06/kt_kmodes_gaps.json)
+            std::vector<int> prev_active;
+            std::vector<char> hstat(o_err + (size_t)nb * 4 - o_cost);
+            std::vector<std::pair<int, int>> steps;  // (assign items, seq items) per chunk step
+            size_t wb = 0;
+            long long it_pairs = 0;
             while (!active.empty()) {
-                // work list of this iteration: per chunk step c, the assign items then the seq items
-                std::vector<KmAsgItem> wl;
-                std::vector<std::pair<int, int>> steps;  // (assign items, seq items) per chunk step
-                const int qstep = 256;  // points per assignment item
-                int maxch = 0;
-                for (int r : active) maxch = std::max(maxch, (nv[r] + KM_BIN - 1) / KM_BIN);
-                for (int c = 0; c < maxch; c++) {
-                    int na = 0, ns = 0;
-                    for (int r : active) {
-                        const int p0 = c * KM_BIN;
-                        if (p0 >= nv[r]) continue;
-                        const int p1 = std::min(nv[r], p0 + KM_BIN), cs = csplit_of(Kv[r]), per = (Kv[r] + cs - 1) / cs;
-                        for (int q0 = p0; q0 < p1; q0 += qstep)
-                            for (int cc = 0; cc < cs; cc++, na++)
-                                wl.push_back({r, q0, std::min(p1, q0 + qstep), cc * per, std::min(Kv[r], (cc + 1) * per), {0, 0, 0}});
+                if (active != prev_active && (int)active.size() <= KM_GEN_MAXB) {
+                    // work list of this iteration (per chunk step c, the assign items then the seq items), written by
+                    // kmb_gen_items from the active bins and the per-step offsets computed here
+                    steps.clear();
+                    std::vector<int> hdr(active);
+                    int maxch = 0;
+                    for (int r : active) maxch = std::max(maxch, (nv[r] + KM_BIN - 1) / KM_BIN);
+                    size_t total = 0;
+                    it_pairs = 0;
+                    for (int c = 0; c < maxch; c++) {
+                        int na = 0, ns = 0;
+                        for (int r : active) {
+                            const int p0 = c * KM_BIN;
+                            if (p0 >= nv[r]) continue;
+                            const int pts = std::min(nv[r] - p0, KM_BIN);
+                            na += ((pts + 255) / 256) * csplit_of(Kv[r]);
+                            ns++;
+                            it_pairs += (long long)pts * Kv[r];  // (point, centroid) pairs the assignment evaluates
+                        }
+                        steps.push_back({na, ns});
+                        hdr.push_back((int)total);
+                        total += (size_t)na + ns;
                     }
-                    for (int r : active) {
-                        const int p0 = c * KM_BIN;
-                        if (p0 >= nv[r]) continue;
-                        KmAsgItem e{};
-                        reinterpret_cast<KmSeqItem &>(e) = {r, p0, std::min(nv[r], p0 + KM_BIN), 0};
-                        wl.push_back(e);
-                        ns++;
+                    wb = total * sizeof(KmAsgItem);  // the active bins follow the list (kmb_iter_reset), then the offsets
+                    if (upload_at(wb, hdr.data(), hdr.size() * 4)) goto fail;
+                    hipLaunchKernelGGL(kmb_gen_items, dim3((unsigned)maxch), dim3(256), 0, st, B, (const int *)(items + wb),
+                                       (int)active.size(), (const int *)(items + wb) + active.size(), (KmAsgItem *)items);
+                    if (hipGetLastError() != hipSuccess) goto fail;
+                    prev_active = active;
+                } else if (active != prev_active) {  // more bins than the generator takes: built here
+                    std::vector<KmAsgItem> wl;
+                    steps.clear();
+                    const int qstep = 256;  // points per assignment item
+                    int maxch = 0;
+                    for (int r : active) maxch = std::max(maxch, (nv[r] + KM_BIN - 1) / KM_BIN);
+                    for (int c = 0; c < maxch; c++) {
+                        int na = 0, ns = 0;
+                        for (int r : active) {
+                            const int p0 = c * KM_BIN;
+                            if (p0 >= nv[r]) continue;
+                            const int p1 = std::min(nv[r], p0 + KM_BIN), cs = csplit_of(Kv[r]), per = (Kv[r] + cs - 1) / cs;
+                            for (int q0 = p0; q0 < p1; q0 += qstep)
+                                for (int cc = 0; cc < cs; cc++, na++)
+                                    wl.push_back({r, q0, std::min(p1, q0 + qstep), cc * per, std::min(Kv[r], (cc + 1) * per), {0, 0, 0}});
+                        }
+                        for (int r : active) {
+                            const int p0 = c * KM_BIN;
+                            if (p0 >= nv[r]) continue;
+                            KmAsgItem e{};
+                            reinterpret_cast<KmSeqItem &>(e) = {r, p0, std::min(nv[r], p0 + KM_BIN), 0};
+                            wl.push_back(e);
+                            ns++;
+                        }
+                        steps.push_back({na, ns});
                     }
-                    steps.push_back({na, ns});
-                }
-                {
-                    size_t q = 0;
-                    for (const auto &sp : steps) {  // (point, centroid) pairs the assignment launches evaluate
-                        for (int i = 0; i < sp.first; i++, q++)
-                            km_pairs += (long long)(wl[q].p1 - wl[q].p0) * (wl[q].c1 - wl[q].c0);
-                        q += sp.second;
-                        km_steps++;
+                    {
+                        size_t q = 0;
+                        it_pairs = 0;
+                        for (const auto &sp : steps) {  // (point, centroid) pairs the assignment launches evaluate
+                            for (int i = 0; i < sp.first; i++, q++)
+                                it_pairs += (long long)(wl[q].p1 - wl[q].p0) * (wl[q].c1 - wl[q].c0);
+                            q += sp.second;
+                        }
                     }
-                }
-                {  // the work list, then the active bins (one reset launch, not three memsets per bin)
-                    const size_t wb = wl.size() * sizeof(KmAsgItem);
+                    // the work list, then the active bins (one reset launch, not three memsets per bin)
+                    wb = wl.size() * sizeof(KmAsgItem);
                     hitems.resize(wb + active.size() * 4);
                     memcpy(hitems.data(), wl.data(), wb);
                     memcpy(hitems.data() + wb, active.data(), active.size() * 4);
                     if (upload(hitems.data(), hitems.size())) goto fail;
+                    prev_active = active;
+                }
+                km_pairs += it_pairs;
+                km_steps += (long long)steps.size();
+                {
                     int maxn = 0;
                     for (int r : active) {
                         iters[r]++;
@@ -1617,11 +1718,13 @@ int kmodes_batch_dev(const uint8_t *d_X, const int32_t *h_boff, int nb, const in
                     }
                 }
                 if (hipGetLastError() != hipSuccess) goto fail;
-                if (hipMemcpyAsync(hcost.data(), B.cost, nb * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                    hipMemcpyAsync(hmoves.data(), B.moves, nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                    hipMemcpyAsync(herr.data(), B.err, nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                // cost, moves and err are consecutive in the workspace: one read-back per iteration
+                if (hipMemcpyAsync(hstat.data(), buf + o_cost, hstat.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
                     hipStreamSynchronize(st) != hipSuccess)
                     goto fail;
+                memcpy(hcost.data(), hstat.data(), nb * 8);
+                memcpy(hmoves.data(), hstat.data() + (o_moves - o_cost), nb * 4);
+                memcpy(herr.data(), hstat.data() + (o_err - o_cost), nb * 4);
                 std::vector<int> still;
                 for (int r : active) {
                     if (herr[r]) {

@@ -49,6 +49,9 @@ static constexpr int OS = 12;   // k-steps of 16 (4 isotypic blocks x 3)
 #ifndef ORB_DU
 #define ORB_DU 4
 #endif
+#ifndef ORB_PR_QUAD
+#define ORB_PR_QUAD 1  // nn_orbit_pairs_kernel: the query row loaded once per quad of slot lanes, broadcast by DPP (r06o: 0.50 -> 0.42 ms)
+#endif
 
 // device copy of the transform: output coordinate o (block x = o / 48) = coef[o] * sum_t w[o][t] * v[src[o][t]]
 struct OrbitMap {
@@ -1169,6 +1172,35 @@ __device__ __forceinline__ float exact_dist192_lean(const float *__restrict__ q,
     return dist;
 }
 
+// exact_dist192_lean for the 4 slot lanes of one query (a lane quad, every lane active): lane s loads 16-byte
+// piece 4k + s of the query row and the quad broadcasts it by DPP, so each piece is requested once per quad
+// instead of once per lane; the same values in the same order, so the same sum bit for bit
+template <int J>
+__device__ __forceinline__ float quad_bcast(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), J * 0x55, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float exact_dist192_quad(const float *__restrict__ q, const float *__restrict__ c, int s) {
+    const float4 *q4 = reinterpret_cast<const float4 *>(q), *c4 = reinterpret_cast<const float4 *>(c);
+    float dist = 0.0f;
+    auto step = [&](const float4 &x, const float4 &y) __attribute__((always_inline)) {
+        float t;
+        t = x.x - y.x; dist = dist + t * t;
+        t = x.y - y.y; dist = dist + t * t;
+        t = x.z - y.z; dist = dist + t * t;
+        t = x.w - y.w; dist = dist + t * t;
+    };
+#pragma unroll 2
+    for (int k = 0; k < OD / 16; k++) {
+        const float4 m = q4[4 * k + s];
+        const float4 y0 = c4[4 * k], y1 = c4[4 * k + 1], y2 = c4[4 * k + 2], y3 = c4[4 * k + 3];
+        step(make_float4(quad_bcast<0>(m.x), quad_bcast<0>(m.y), quad_bcast<0>(m.z), quad_bcast<0>(m.w)), y0);
+        step(make_float4(quad_bcast<1>(m.x), quad_bcast<1>(m.y), quad_bcast<1>(m.z), quad_bcast<1>(m.w)), y1);
+        step(make_float4(quad_bcast<2>(m.x), quad_bcast<2>(m.y), quad_bcast<2>(m.z), quad_bcast<2>(m.w)), y2);
+        step(make_float4(quad_bcast<3>(m.x), quad_bcast<3>(m.y), quad_bcast<3>(m.z), quad_bcast<3>(m.w)), y3);
+    }
+    return dist;
+}
+
 __device__ __forceinline__ float wave_min_f(float v) {
     for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
     return v;
@@ -1479,6 +1511,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_RS_WAVE
 // these 192-step chains here instead of one lane per candidate inside the half-wave rescore keeps the
 // rescore's instruction stream short (it is latency-bound) and fills the lanes.  r03zr: staging the rows through LDS in
 // coalesced 32-float column chunks (12 barriers, every slot's row loaded) took 1.00 ms vs 0.50 ms for this per-lane walk.
+// r06o (`profiles/r06/o_pairs_ab.txt`): the query row's 16-byte pieces requested once per quad and broadcast by DPP
+// (exact_dist192_quad) 0.50 -> 0.42 ms at C3, output digest unchanged; the load requests, not HBM, bound this pass.
 #if ORB_PR_WAVES
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_PR_WAVES))) void nn_orbit_pairs_kernel(OrbitRescoreArgs a) {
 #else
@@ -1492,9 +1526,19 @@ __global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a)
     const int n = a.pair_cnt[q];
     if (n == 0) return;  // uniform over the group
     int bi = 0x7fffffff, bg = -1;
+#if ORB_PR_QUAD
+    static_assert(ORB_PSLOTS == 4, "one lane quad per query");
+    {  // every lane of the quad takes part in the broadcasts; a lane past the count re-reads slot 0's row
+        const int c = a.pair_cand[q * ORB_PSLOTS + (s < n ? s : 0)];
+        const float d = exact_dist192_quad(a.q + q * OD, a.rows + (long)c * OD, s);
+        if (s < n) bd = d;
+    }
+#endif
     if (s < n) {
         int c = a.pair_cand[q * ORB_PSLOTS + s];
+#if !ORB_PR_QUAD
         bd = exact_dist192_lean(a.q + q * OD, a.rows + (long)c * OD);
+#endif
         if (a.grp_of) {
             bg = a.grp_of[c];
             class_first(a, a.q + q * OD, c, bg);  // same row, same distance

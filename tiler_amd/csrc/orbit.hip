@@ -49,6 +49,9 @@ static constexpr int OS = 12;   // k-steps of 16 (4 isotypic blocks x 3)
 #ifndef ORB_DU
 #define ORB_DU 4
 #endif
+#ifndef ORB_RS_DPP
+#define ORB_RS_DPP 1  // rescore / pair pass reductions: DPP lane moves inside each row of 16, one ds_bpermute across rows
+#endif
 #ifndef ORB_PR_QUAD
 #define ORB_PR_QUAD 1  // nn_orbit_pairs_kernel: the query row loaded once per quad of slot lanes, broadcast by DPP (r06o: 0.50 -> 0.42 ms)
 #endif
@@ -1175,9 +1178,13 @@ __device__ __forceinline__ float exact_dist192_lean(const float *__restrict__ q,
 // exact_dist192_lean for the 4 slot lanes of one query (a lane quad, every lane active): lane s loads 16-byte
 // piece 4k + s of the query row and the quad broadcasts it by DPP, so each piece is requested once per quad
 // instead of once per lane; the same values in the same order, so the same sum bit for bit
+template <int CTRL>  // a DPP lane move (row_mask / bank_mask all rows, every lane written)
+__device__ __forceinline__ int dpp_mov(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
 template <int J>
 __device__ __forceinline__ float quad_bcast(float v) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), J * 0x55, 0xf, 0xf, false));
+    return __int_as_float(dpp_mov<J * 0x55>(__float_as_int(v)));
 }
 __device__ __forceinline__ float exact_dist192_quad(const float *__restrict__ q, const float *__restrict__ c, int s) {
     const float4 *q4 = reinterpret_cast<const float4 *>(q), *c4 = reinterpret_cast<const float4 *>(c);
@@ -1218,7 +1225,15 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
     const int g = (id >> 2) * 32 + 8 * (id & 3) + 4 * h + j;
     const bool gv = id >= 0 && g < a.G;
     float d = 0.0f;
+    int cand = -1;
+    unsigned dupb = 0;
+    float ncg = 0.0f;
     if (gv) {  // fp16 products, fp32 sums (any order is inside the bound's gamma_{D+1} allowance)
+        // the slot's member, the group's duplicate flags and norm travel with its fp16 row: one round trip where
+        // the dependent loads after the butterfly took three more (r06q, `profiles/r06/q_rescore_ab.txt`: rescore 0.61 -> 0.55 ms)
+        cand = a.member[(long)g * 4 + x];
+        dupb = a.dup[g];
+        ncg = a.nc[g];
         const uint4 *cr = reinterpret_cast<const uint4 *>(a.rowh + (long)g * OD + x * 48);
         // q' of block x from the MFMA B fragments: 16-byte piece t = (k-step 3x + t/2, half t%2) of query q
         const uint4 *qf = reinterpret_cast<const uint4 *>(a.qfrag) + ((q >> 5) * OS + 3 * x) * 64 + (q & 31);
@@ -1244,10 +1259,8 @@ __device__ __forceinline__ int orbit_expand4(const OrbitRescoreArgs &a, long q, 
     o = __shfl_xor(d, 2, 64);
     d = (x & 2) ? (o - d) : (d + o);
     key = INFINITY;
-    if (!gv) return -1;
-    int cand = a.member[(long)g * 4 + x];
-    if (cand < 0 || ((a.dup[g] >> x) & 1)) return -1;
-    key = (double)a.nc[g] - 2.0 * (double)d;
+    if (!gv || cand < 0 || ((dupb >> x) & 1)) return -1;
+    key = (double)ncg - 2.0 * (double)d;
     return cand;  // the lowest-index copy of its row; the final pick resolves the copies (class_first)
 }
 
@@ -1287,8 +1300,17 @@ __device__ __forceinline__ void orbit_argmin(const OrbitRescoreArgs &a, const fl
                                              int &gs) {
 #pragma unroll
     for (int off = WIDTH / 2; off > 0; off >>= 1) {
-        const float ov = __shfl_xor(v, off, 64);
-        const int oi = __shfl_xor(i, off, 64), og = __shfl_xor(gs, off, 64);
+        float ov;
+        int oi, og;
+        if (WIDTH == 4 && ORB_RS_DPP) {  // the pair pass: one lane quad per query, every lane active
+            ov = __int_as_float(off == 2 ? dpp_mov<0x4E>(__float_as_int(v)) : dpp_mov<0xB1>(__float_as_int(v)));
+            oi = off == 2 ? dpp_mov<0x4E>(i) : dpp_mov<0xB1>(i);
+            og = off == 2 ? dpp_mov<0x4E>(gs) : dpp_mov<0xB1>(gs);
+        } else {
+            ov = __shfl_xor(v, off, 64);
+            oi = __shfl_xor(i, off, 64);
+            og = __shfl_xor(gs, off, 64);
+        }
         if (ov < v || (ov == v && orbit_before(a, q, oi, og, i, gs))) {
             v = ov;
             i = oi;
@@ -1304,18 +1326,46 @@ static constexpr int ORB_QCAP = 64;  // rescore queue per query
 static constexpr int ORB_STG = ORB_STG_ROWS;  // candidate rows staged in LDS per pass
 static constexpr int ORB_PSLOTS = 4; // candidates per query handed to the pair pass
 
+// Lane moves of the half-wave reductions.  A minimum (of values, or of (value, index) pairs) is symmetric and
+// associative, so any pairing that doubles the reduced span each step works: lane ^ 1 and lane ^ 2 (quad_perm), lane
+// <-> 7 - lane and lane <-> 15 - lane (row half-mirror, row mirror) by DPP -- VALU lane moves, no LDS round trip --
+// then lane ^ 16 by ds_bpermute.  Every lane of the half is active at each call site (the branches around them are
+// uniform over the half-wave).  ORB_RS_DPP 0: five ds_bpermute steps (xor 16, 8, 4, 2, 1) as before (r06r,
+// `profiles/r06/r_rescore_dpp_ab.txt`: rescore 0.540 -> 0.533 ms).
+template <int STEP>  // STEP 0..4: the partner lane of the step
+__device__ __forceinline__ int half_partner(int v) {
+#if ORB_RS_DPP
+    if (STEP == 0) return dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+    if (STEP == 1) return dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+    if (STEP == 2) return dpp_mov<0x141>(v);  // row_half_mirror: 7 - lane within 8
+    if (STEP == 3) return dpp_mov<0x140>(v);  // row_mirror: 15 - lane within 16
+    return __shfl_xor(v, 16, 64);
+#else
+    return __shfl_xor(v, 16 >> STEP, 64);
+#endif
+}
 __device__ __forceinline__ float half_min_f(float v) {
-    for (int o = 16; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    v = fminf(v, __int_as_float(half_partner<0>(__float_as_int(v))));
+    v = fminf(v, __int_as_float(half_partner<1>(__float_as_int(v))));
+    v = fminf(v, __int_as_float(half_partner<2>(__float_as_int(v))));
+    v = fminf(v, __int_as_float(half_partner<3>(__float_as_int(v))));
+    v = fminf(v, __int_as_float(half_partner<4>(__float_as_int(v))));
     return v;
 }
+template <int STEP>
+__device__ __forceinline__ void half_argmin_step(float &v, int &i) {
+    const float ov = __int_as_float(half_partner<STEP>(__float_as_int(v)));
+    const int oi = half_partner<STEP>(i);
+    const bool take = (ov < v) || (ov == v && (unsigned)oi < (unsigned)i);
+    v = take ? ov : v;
+    i = take ? oi : i;
+}
 __device__ __forceinline__ void half_argmin(float &v, int &i) {
-    for (int o = 16; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(v, o, 64);
-        const int oi = __shfl_xor(i, o, 64);
-        const bool take = (ov < v) || (ov == v && (unsigned)oi < (unsigned)i);
-        v = take ? ov : v;
-        i = take ? oi : i;
-    }
+    half_argmin_step<0>(v, i);
+    half_argmin_step<1>(v, i);
+    half_argmin_step<2>(v, i);
+    half_argmin_step<3>(v, i);
+    half_argmin_step<4>(v, i);
 }
 __device__ __forceinline__ unsigned half_ballot(bool p) {
     return (unsigned)(__ballot(p) >> (32 * ((threadIdx.x >> 5) & 1)));
@@ -1328,17 +1378,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_RS_WAVE
     if (q >= a.nq) return;
     const OrbitTail &t = a.t;
     const OrbitStat st = a.ostat[q];
+    const int E = a.nsplit * 2 * a.L;  // <= 32 (orbit_search limits nsplit)
+    float ek = INFINITY;
+    int eid = -1;
+    if (l < E) {  // issued with the stat: the two loads do not wait for each other
+        ek = a.key[q * E + l];
+        eid = a.id[q * E + l];
+    }
     if (l == 0) a.pair_cnt[q] = 0;  // the pair pass skips queries settled here or by tiers 2/3
     if (st.flags & 2) {
         if (l == 0) t.ex_list[atomicAdd(t.ex_count, 1)] = (int)q;
         return;
-    }
-    const int E = a.nsplit * 2 * a.L;  // <= 32 (orbit_search limits nsplit)
-    float ek = INFINITY;
-    int eid = -1;
-    if (l < E) {
-        ek = a.key[q * E + l];
-        eid = a.id[q * E + l];
     }
     const int eh = (l / a.L) & 1;
     if (eid < 0) ek = INFINITY;

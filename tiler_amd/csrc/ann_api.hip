@@ -293,8 +293,12 @@ struct CombineSlot {
     SearchScratch scratch;
     bool busy = false;
 };
+#ifndef ANN_COMBINE_SLOTS
+#define ANN_COMBINE_SLOTS 3  // batches of one handle in flight at once (r06t, profiles/r06/t_percall_slots_ab.txt: 2 -> 3
+                             // C3 per-tile calls 89k -> 95k/s, 65k-row plain handle 106k -> 120k; 4 slower)
+#endif
 struct Combiner {
-    static constexpr int SLOTS = 2;
+    static constexpr int SLOTS = ANN_COMBINE_SLOTS;
     std::mutex m;
     std::condition_variable cv;
     std::deque<CombineReq *> pending;

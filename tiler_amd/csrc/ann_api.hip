@@ -277,7 +277,8 @@ struct CombineReq {
     int *idx = nullptr;
     float *err = nullptr;
     int rc = 0;
-    bool done = false;
+    bool taken = false;             // in a batch (set by its leader under Combiner::m)
+    std::atomic<bool> done{false};  // answered: idx / err / rc / msg written before the release store
     std::string msg;
 };
 // One batch in flight: its own stream, pinned staging, device buffers and search scratch, so that two batches can be
@@ -293,6 +294,10 @@ struct CombineSlot {
     SearchScratch scratch;
     bool busy = false;
 };
+#ifndef ANN_COMBINE_SPIN_US
+#define ANN_COMBINE_SPIN_US 200  // a caller whose query is in a batch in flight spins this long before sleeping
+                                 // (r06v, profiles/r06/v_percall_spin_ab.txt: C3 per-tile calls 85k -> 98k/s, 0 vs 200 us)
+#endif
 #ifndef ANN_COMBINE_SLOTS
 #define ANN_COMBINE_SLOTS 3  // batches of one handle in flight at once (r06t, profiles/r06/t_percall_slots_ab.txt: 2 -> 3
                              // C3 per-tile calls 89k -> 95k/s, 65k-row plain handle 106k -> 120k; 4 slower)
@@ -831,11 +836,22 @@ static int combined_search(ann_kdtree *t, const float *q, int k, int *idx, float
     std::unique_lock<std::mutex> lk(c.m);
     c.pending.push_back(&me);
     c.calls++;
-    while (!me.done) {
+    while (!me.done.load(std::memory_order_acquire)) {
         int si = -1;
         for (int i = 0; i < Combiner::SLOTS && si < 0; i++)
             if (!c.slot[i].busy) si = i;
-        if (si < 0 || c.pending.empty()) {  // both slots leading, or this caller's query is in a batch already
+        if (si < 0 || c.pending.empty()) {  // every slot leading, or this caller's query is in a batch already
+            if (me.taken && ANN_COMBINE_SPIN_US > 0) {
+                // its batch is in flight (~40 us): spin on the answer for a while before sleeping -- a condition
+                // variable wake-up of 16 waiting callers costs several microseconds each
+                lk.unlock();
+                const auto t0 = std::chrono::steady_clock::now();
+                while (!me.done.load(std::memory_order_acquire) &&
+                       std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(ANN_COMBINE_SPIN_US))
+                    __builtin_ia32_pause();
+                lk.lock();
+                if (me.done.load(std::memory_order_acquire)) break;
+            }
             c.cv.wait(lk);
             continue;
         }
@@ -846,6 +862,7 @@ static int combined_search(ann_kdtree *t, const float *q, int k, int *idx, float
             const int bk = c.pending.front()->k;
             for (auto it = c.pending.begin(); it != c.pending.end() && (int)b.size() < COMBINE_MAX;) {
                 if ((*it)->k == bk) {
+                    (*it)->taken = true;
                     b.push_back(*it);
                     it = c.pending.erase(it);
                 } else {
@@ -861,7 +878,7 @@ static int combined_search(ann_kdtree *t, const float *q, int k, int *idx, float
             for (CombineReq *r : b) {
                 r->rc = rc;
                 r->msg = msg;
-                r->done = true;
+                r->done.store(true, std::memory_order_release);
             }
             c.cv.notify_all();
         }

@@ -281,7 +281,7 @@ struct CombineReq {
     std::atomic<bool> done{false};  // answered: idx / err / rc / msg written before the release store
     std::string msg;
 };
-// One batch in flight: its own stream, pinned staging, device buffers and search scratch, so that two batches can be
+// One batch in flight: its own stream, pinned staging, device buffers and search scratch, so that several batches can be
 // in flight on one handle (the second one's upload and kernels overlap the first one's; only small-batch scans run
 // concurrently: they touch nothing of the index but its read-only data and the scratch swapped in for them).
 struct CombineSlot {

@@ -127,6 +127,28 @@ def test_kmodes_batch_matches_per_bin(gpu, oracle):
         assert np.array_equal(med[koff[b]:koff[b + 1]], m1) and np.array_equal(cnt[koff[b]:koff[b + 1]], c1), b
 
 
+def test_kmodes_batch_many_bins_host_list(gpu, oracle):
+    """More active bins than the device work-list generator takes (kmodes.hip KM_GEN_MAXB = 4,096): the iteration's
+    list is built on the host instead, and bins leave the active set at different iterations; 4,500 small bins, every
+    one bit-identical to its own ComputeKModes run."""
+    from tiler_amd.kmodes import compute_kmodes_batch
+    rng = np.random.default_rng(4500)
+    sizes = rng.integers(3, 13, 4500)
+    ks = [int(rng.integers(1, n)) for n in sizes]
+    Xs = [_dataset(rng, int(n), 3, 0.3) for n in sizes]
+    X = np.concatenate(Xs)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    starts = [int(n - 1 - np.argmin(x.astype(np.int64).sum(1)[::-1])) for n, x in zip(sizes, Xs)]
+    labels, cent, iters, costs = compute_kmodes_batch(X, off, ks, starts)
+    koff = np.concatenate([[0], np.cumsum(ks)])
+    assert len(set(int(i) for i in iters)) > 1  # the active set shrinks over the iterations
+    for b, (x, k, st) in enumerate(zip(Xs, ks, starts)):
+        ol, oc, oi, ocost = oracle.kmodes(x, k, st)
+        assert (int(iters[b]), int(costs[b])) == (oi, ocost), b
+        assert np.array_equal(labels[off[b]:off[b + 1]], ol), b
+        assert np.array_equal(cent[koff[b]:koff[b + 1]], oc), b
+
+
 def _oracle_threads():
     try:
         return max(1, min(16, len(os.sched_getaffinity(0))))

@@ -817,6 +817,15 @@ static int combine_run(ann_kdtree *t, CombineSlot &cs, std::vector<CombineReq *>
     return 0;
 }
 
+// Slots a handle's coalescer uses: the third pays where a small batch's scan is short (C3's 65,536 orbit base rows,
+// plain handles up to ~65k rows: 89k -> 95k calls/s), and costs where each scan streams much more (262k plain rows,
+// C5's 262k base rows: 16.6k -> 13.9k calls/s at C5) -- r06w, profiles/r06/w_percall_slots_c5_ab.txt
+static int comb_slots(const ann_kdtree *t) {
+    const NNIndex *ix = t->ix;
+    const long rows = ix->orbit ? (long)ix->orbit->G : (long)ix->n;
+    return rows * (long)ix->d * 4 > (96l << 20) ? std::min(2, Combiner::SLOTS) : Combiner::SLOTS;
+}
+
 static int combined_search(ann_kdtree *t, const float *q, int k, int *idx, float *err) {
     if (!t || !t->ix || !q || !idx || !err) {
         set_error("ann_kdtree_search: invalid arguments");
@@ -838,7 +847,8 @@ static int combined_search(ann_kdtree *t, const float *q, int k, int *idx, float
     c.calls++;
     while (!me.done.load(std::memory_order_acquire)) {
         int si = -1;
-        for (int i = 0; i < Combiner::SLOTS && si < 0; i++)
+        const int ns = comb_slots(t);
+        for (int i = 0; i < ns && si < 0; i++)
             if (!c.slot[i].busy) si = i;
         if (si < 0 || c.pending.empty()) {  // every slot leading, or this caller's query is in a batch already
             if (me.taken && ANN_COMBINE_SPIN_US > 0) {

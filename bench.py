@@ -412,6 +412,29 @@ def main():
             dither["parity_mismatches_vs_cpu"] = int(np.sum(np.any(gpx != opx, axis=1)) +
                                                      np.sum(d_dhm[:ns].cpu().numpy() != ohm) +
                                                      np.sum(d_dvm[:ns].cpu().numpy() != ovm))
+        # the non-default branch (chkUseTK off): Yliluoma mixing at the form's default cbxYilMix = 4
+        yl_call = lambda: dither_tiles_dev(QK, d_rgb.data_ptr(), d_pal_of.data_ptr(), d_pals.data_ptr(), P, 16,  # noqa: E731
+                                           d_px.data_ptr(), d_dhm.data_ptr(), d_dvm.data_ptr(), stream, yliluoma_mix=4)
+        yl_call()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        yl_call()
+        torch.cuda.synchronize(dev)
+        ty = time.perf_counter() - t0
+        yl = {"value": round(QK / ty / 1e6, 4), "unit": "Mtiles/s", "ms": round(ty * 1e3, 3),
+              "shape": "the same tiles and palettes, Yliluoma mixing (DeviseBestMixingPlanYliluoma's ASM_DBMP form, "
+                       "Y2MixedColors 4) + luma QuickSort + PrepareTileMirrors"}
+        if world == 1 and not args.no_cpu:
+            ns = 400
+            t0 = time.perf_counter()
+            opx, ohm, ovm = pyoracle.dither_tiles_yl(sample, pal_of[:ns], pals, 4)
+            tc = time.perf_counter() - t0
+            yl["cpu_baseline"] = {"value": round(ns / tc / 1e6, 6), "unit": "Mtiles/s", "cores": 1, "kind": "port",
+                                  "sample": f"the first {ns} tiles (oracle/dither_tk.c or_dither_tiles_yl, no colour cache)"}
+            yl["parity_mismatches_vs_cpu"] = int(np.sum(np.any(d_px[:ns].cpu().numpy() != opx, axis=1)) +
+                                                 np.sum(d_dhm[:ns].cpu().numpy() != ohm) +
+                                                 np.sum(d_dvm[:ns].cpu().numpy() != ovm))
+        dither["yliluoma"] = yl
         del d_px, d_dhm, d_dvm, d_pal_of
 
     # ---- secondary: the Dither step's palette generation over one keyframe (btnDitherClick main.pas:886-907):

@@ -271,6 +271,16 @@ int tiler_dither_tiles(int n, const int32_t *rgb, const int32_t *pal_of, const i
 /* Same with every array in HBM; asynchronous on stream. */
 int tiler_dither_tiles_dev(int n, const int32_t *d_rgb, const int32_t *d_pal_of, const int32_t *d_palettes,
                            int n_palettes, int palsize, uint8_t *d_palpix, uint8_t *d_hm, uint8_t *d_vm, void *stream);
+/* The same step with Yliluoma mixing instead (chkUseTK unchecked, main.lfm:272-282): DitherTile's other branch
+ * (main.pas:2055-2067) with DeviseBestMixingPlanYliluoma (main.pas:1573-1826, the ASM_DBMP form the reference build
+ * compiles), mixed_colors = FY2MixedColors (cbxYilMix: 1, 2, 4 (the form's default), 8, 16; here 1..64), palsize
+ * 1..16 (any size).  Then PrepareTileMirrors as above.  0 / -1. */
+int tiler_dither_tiles_yliluoma(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes,
+                                int n_palettes, int palsize, int mixed_colors, uint8_t *palpix, uint8_t *hm,
+                                uint8_t *vm);
+int tiler_dither_tiles_yliluoma_dev(int n, const int32_t *d_rgb, const int32_t *d_pal_of, const int32_t *d_palettes,
+                                    int n_palettes, int palsize, int mixed_colors, uint8_t *d_palpix, uint8_t *d_hm,
+                                    uint8_t *d_vm, void *stream);
 
 /* ---- Dither step, palette generation (QuantizePalette / FinishQuantizePalette) ------------
  * QuantizePalette with the default Dennis Lee v3 quantizer (chkUseDL3, main.pas:2154-2254 -> dl3quant,

@@ -8,6 +8,9 @@
  *   ColorCompare                                                                            main.pas:1557-1571
  *   QuickSort (the reference's own, kmodes.pas:89-136) with PlanCompareLuma                  main.pas:1540-1551
  *   PrepareTileMirrors (canonical orientation)                                              main.pas:4049-4069
+ * and the non-default branch (chkUseTK unchecked):
+ *   DeviseBestMixingPlanYliluoma, the ASM_DBMP x86-64 form (main.pas:5 defines ASM_DBMP)    main.pas:1573-1826
+ *   DitherTile's Yliluoma branch (map_value * count shr 6)                                  main.pas:2055-2067
  * The colour cache of the reference (CountCache / ListCache) only memoises the per-colour list: not restated.
  * Parity: no reference fixture exists (no FPC, no palettes in the reference): pinned by known-answer tests and an
  * independent Python restatement (tests/test_dither.py) -- "parity unpinned" against the binary.
@@ -109,18 +112,85 @@ void or_tk_plan(const int32_t *pal, int palsize, int32_t col, uint8_t *list) {
     quicksort_bytes(list, 0, DITHER_LEN - 1, luma);
 }
 
+/* DeviseBestMixingPlanYliluoma main.pas:1573-1826 as the reference build runs it: main.pas:5 defines ASM_DBMP, so on
+ * x86-64 the SSE block (1602-1752) replaces the Pascal loop.  Its arithmetic, lane by lane over (r, g, b, luma):
+ * xmm4 = the colour (r, g, b, (r*cRedMul + g*cGreenMul + b*cBlueMul) div cLumaDiv), xmm5 = 1s, xmm6 = (13, 13, 13,
+ * 32); per palette entry sum = so_far, add = Y2Palette[index] (r, g, b, LumaPal div cLumaDiv); per t sum += add and
+ * add += 1 in all four lanes (the Pascal form leaves the luma lane alone), then
+ * pen = sum_k w_k * (((gVecInv[t] * sum_k) shr 16) - x_k)^2, gVecInv[t] = 65536 div t, every product the low 32 bits
+ * (pmulld), the shift logical (psrld), the four lanes added mod 2^32 (phaddd) and compared zero-extended, strict
+ * '<' against the least so far (jae).  The chosen amount is t - plan_count, capped by the list (256 entries). */
+#define YL_LIST 256
+int or_yl_plan(const int32_t *pal, int palsize, int mixed, int32_t col, uint8_t *list) {
+    uint32_t y2[256][4];
+    int32_t luma[256];
+    for (int i = 0; i < palsize; i++) { /* PreparePlan main.pas:1514-1525 */
+        const uint32_t r = pal[i] & 0xff, g = (pal[i] >> 8) & 0xff, b = (pal[i] >> 16) & 0xff;
+        luma[i] = (int32_t)(r * RED_MUL + g * GREEN_MUL + b * BLUE_MUL);
+        y2[i][0] = r;
+        y2[i][1] = g;
+        y2[i][2] = b;
+        y2[i][3] = (uint32_t)luma[i] / LUMA_DIV;
+    }
+    const uint32_t r = col & 0xff, g = (col >> 8) & 0xff, b = (col >> 16) & 0xff;
+    const uint32_t x[4] = {r, g, b, (r * RED_MUL + g * GREEN_MUL + b * BLUE_MUL) / LUMA_DIV};
+    const uint32_t w[4] = {RGBW, RGBW, RGBW, 32};
+    uint32_t so_far[4] = {0, 0, 0, 0};
+    int plan_count = 0;
+    while (plan_count < mixed) {
+        const int max_test = plan_count == 0 ? 1 : plan_count;
+        uint64_t least = 0x7fffffffffffffffull;
+        int chosen = 0, chosen_t = plan_count + 1;
+        for (int idx = 0; idx < palsize; idx++) {
+            uint32_t sum[4], add[4];
+            for (int k = 0; k < 4; k++) {
+                sum[k] = so_far[k];
+                add[k] = y2[idx][k];
+            }
+            for (int t = plan_count + 1; t <= plan_count + max_test; t++) {
+                const uint32_t inv = 65536u / (uint32_t)t;
+                uint32_t pen = 0;
+                for (int k = 0; k < 4; k++) {
+                    sum[k] += add[k];
+                    add[k] += 1u;
+                    const uint32_t q = (inv * sum[k]) >> 16;
+                    const uint32_t d = q - x[k];
+                    pen += (d * d) * w[k];
+                }
+                if ((uint64_t)pen < least) {
+                    least = pen;
+                    chosen = idx;
+                    chosen_t = t;
+                }
+            }
+        }
+        int amount = chosen_t - plan_count;
+        if (amount > YL_LIST - plan_count) amount = YL_LIST - plan_count;
+        memset(list + plan_count, chosen, (size_t)amount);
+        plan_count += amount;
+        for (int k = 0; k < 4; k++) so_far[k] += y2[chosen][k] * (uint32_t)amount;
+    }
+    quicksort_bytes(list, 0, plan_count - 1, luma);
+    return plan_count;
+}
+
 /* FinishDitherTiles' per-tile work (main.pas:2507-2524): DitherTile (Thomas Knoll) with the tile's
  * DitheringPalIndex palette, then PrepareTileMirrors.  rgb[n][64] 0x00BBGGRR, pal_of[n], palettes[P][palsize]. */
-void or_dither_tiles_tk(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int palsize,
-                        uint8_t *palpix, uint8_t *hm, uint8_t *vm) {
-    uint8_t list[DITHER_LEN];
+static void dither_tiles(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int palsize,
+                         int yl_mixed, uint8_t *palpix, uint8_t *hm, uint8_t *vm) {
+    uint8_t list[YL_LIST];
     for (int i = 0; i < n; i++) {
         const int32_t *pal = palettes + (long)pal_of[i] * palsize;
         uint8_t px[64];
         for (int y = 0; y < 8; y++)
             for (int x = 0; x < 8; x++) {
-                or_tk_plan(pal, palsize, rgb[(long)i * 64 + y * 8 + x], list);
-                px[y * 8 + x] = list[k_dither_map[y * 8 + x]];
+                if (yl_mixed > 0) { /* DitherTile's Yliluoma branch main.pas:2057-2066 */
+                    const int count = or_yl_plan(pal, palsize, yl_mixed, rgb[(long)i * 64 + y * 8 + x], list);
+                    px[y * 8 + x] = list[(k_dither_map[y * 8 + x] * count) >> 6];
+                } else {
+                    or_tk_plan(pal, palsize, rgb[(long)i * 64 + y * 8 + x], list);
+                    px[y * 8 + x] = list[k_dither_map[y * 8 + x]];
+                }
             }
         /* PrepareTileMirrors: quadrant sums, v outer / h inner, strict '>' (first max) */
         int best = -1, bh = 0, bv = 0;
@@ -141,4 +211,14 @@ void or_dither_tiles_tk(int n, const int32_t *rgb, const int32_t *pal_of, const 
         hm[i] = (uint8_t)bh;
         vm[i] = (uint8_t)bv;
     }
+}
+
+void or_dither_tiles_tk(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int palsize,
+                        uint8_t *palpix, uint8_t *hm, uint8_t *vm) {
+    dither_tiles(n, rgb, pal_of, palettes, palsize, 0, palpix, hm, vm);
+}
+
+void or_dither_tiles_yl(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int palsize,
+                        int mixed, uint8_t *palpix, uint8_t *hm, uint8_t *vm) {
+    dither_tiles(n, rgb, pal_of, palettes, palsize, mixed, palpix, hm, vm);
 }

@@ -346,6 +346,27 @@ def dither_tiles_tk(rgb, pal_of, palettes):
     return palpix, hm, vm
 
 
+def yl_plan(pal, col, mixed):
+    """DeviseBestMixingPlanYliluoma (main.pas:1573-1826, the ASM_DBMP form): the luma-sorted list for one colour."""
+    pal = np.ascontiguousarray(pal, np.int32)
+    out = np.zeros(256, np.uint8)
+    n = lib().or_yl_plan(_p(pal), pal.size, int(mixed), int(np.int32(col)), _p(out))
+    return out[:n]
+
+
+def dither_tiles_yl(rgb, pal_of, palettes, mixed):
+    """FinishDitherTiles per tile with Yliluoma mixing (chkUseTK off) + PrepareTileMirrors: (palpix, hm, vm)."""
+    rgb = np.ascontiguousarray(rgb, np.int32).reshape(-1, 64)
+    palettes = np.ascontiguousarray(palettes, np.int32)
+    n = rgb.shape[0]
+    palpix = np.zeros((n, 64), np.uint8)
+    hm = np.zeros(n, np.uint8)
+    vm = np.zeros(n, np.uint8)
+    lib().or_dither_tiles_yl(n, _p(rgb), _p(np.ascontiguousarray(pal_of, np.int32)), _p(palettes),
+                             palettes.shape[1], int(mixed), _p(palpix), _p(hm), _p(vm))
+    return palpix, hm, vm
+
+
 def ref_kmodes_lib():
     """The reference's own asm (kmodes.pas:316-596) if oracle/_ref was built here; else None."""
     if not os.path.exists(REF_LIB):

@@ -112,6 +112,11 @@ const uint8_t *or_dither_map(void);
 void or_tk_plan(const int32_t *pal, int palsize, int32_t col, uint8_t *list);
 void or_dither_tiles_tk(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int palsize,
                         uint8_t *palpix, uint8_t *hm, uint8_t *vm);
+/* the Yliluoma branch (chkUseTK off; DeviseBestMixingPlanYliluoma main.pas:1573-1826, ASM_DBMP form): the sorted list
+ * of one colour (returns its length), and the tiles */
+int or_yl_plan(const int32_t *pal, int palsize, int mixed, int32_t col, uint8_t *list);
+void or_dither_tiles_yl(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int palsize,
+                        int mixed, uint8_t *palpix, uint8_t *hm, uint8_t *vm);
 
 
 /* palette generation (palette.c): QuantizePalette / DLv3 / FinishQuantizePalette, main.pas:2154-2480 */

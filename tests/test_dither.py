@@ -131,3 +131,109 @@ def test_video_from_frames_host_logic(oracle):
     px, thm, tvm = oracle.dither_tiles_tk(frames.reshape(-1, 64), (np.repeat(kf_of, tm_w * tm_h) * 4 + v.dith_pal),
                                           pals.reshape(-1, 16))
     assert np.array_equal(px, v.palpix) and np.array_equal(thm, v.thm) and np.array_equal(tvm, v.tvm)
+
+
+# ---- the Yliluoma branch (chkUseTK unchecked): DeviseBestMixingPlanYliluoma main.pas:1573-1826, ASM_DBMP form ----
+
+def _qs(a, first, last, luma):
+    """kmodes.pas:89-136 QuickSort with PlanCompareLuma, in Python (restated again, apart from _py_plan's)."""
+    if last <= first:
+        return
+    while True:
+        i, j, p = first, last, (first + last) >> 1
+        while True:
+            while luma[a[i]] < luma[a[p]]:
+                i += 1
+            while luma[a[j]] > luma[a[p]]:
+                j -= 1
+            if i <= j:
+                a[i], a[j] = a[j], a[i]
+                if p == i:
+                    p = j
+                elif p == j:
+                    p = i
+                i += 1
+                j -= 1
+            if i > j:
+                break
+        if first < j:
+            _qs(a, first, j, luma)
+        first = i
+        if i >= last:
+            break
+
+
+def _py_yl_plan(pal, col, mixed):
+    """The SSE block of main.pas:1602-1752 lane by lane in Python ints: per t, sum += add and add += 1 in all four
+    lanes (r, g, b, luma), q = (gVecInv[t] * sum) & 0xffffffff >> 16, pen = sum_k w_k (q_k - x_k)^2 mod 2^32
+    (pmulld / psrld / psubd / phaddd), strict '<'; amount = t - plan_count capped by the 256-entry list."""
+    M = 0xFFFFFFFF
+    rgb = [(c & 255, (c >> 8) & 255, (c >> 16) & 255) for c in pal]
+    luma = [r * 2126 + g * 7152 + b * 722 for r, g, b in rgb]
+    y2 = [(r, g, b, lu // 10000) for (r, g, b), lu in zip(rgb, luma)]
+    r, g, b = col & 255, (col >> 8) & 255, (col >> 16) & 255
+    x = (r, g, b, (r * 2126 + g * 7152 + b * 722) // 10000)
+    w = (13, 13, 13, 32)
+    so, lst, pc = [0, 0, 0, 0], [], 0
+    while pc < mixed:
+        mt = 1 if pc == 0 else pc
+        least, chosen, ct = (1 << 63) - 1, 0, pc + 1
+        for idx, yv in enumerate(y2):
+            s, a = list(so), list(yv)
+            for t in range(pc + 1, pc + mt + 1):
+                inv = 65536 // t
+                pen = 0
+                for k in range(4):
+                    s[k] = (s[k] + a[k]) & M
+                    a[k] = (a[k] + 1) & M
+                    q = ((inv * s[k]) & M) >> 16
+                    d = (q - x[k]) & M
+                    pen = (pen + (((d * d) & M) * w[k] & M)) & M
+                if pen < least:
+                    least, chosen, ct = pen, idx, t
+        amount = min(ct - pc, 256 - pc)
+        lst += [chosen] * amount
+        pc += amount
+        so = [(so[k] + y2[chosen][k] * amount) & M for k in range(4)]
+    _qs(lst, 0, pc - 1, luma)
+    return np.asarray(lst, np.uint8), luma
+
+
+@pytest.mark.parametrize("mixed", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("ties", [False, True])
+def test_yl_plan_matches_python(oracle, mixed, ties):
+    rng = np.random.default_rng(31 + mixed + 100 * ties)
+    for _ in range(3):
+        pal = _palette(rng, ties=ties)
+        for col in synth.rgb_pack(*rng.integers(0, 256, (3, 12))):
+            o = oracle.yl_plan(pal, int(col), mixed)
+            p, luma = _py_yl_plan([int(c) for c in pal], int(col), mixed)
+            assert np.array_equal(o, p)
+            assert mixed <= o.size <= max(1, 2 * (mixed - 1))
+            assert all(luma[a] <= luma[b] for a, b in zip(o[:-1], o[1:]))   # sorted by luma
+
+
+def test_yl_plan_known_answers(oracle):
+    pal = _palette(np.random.default_rng(5))
+    for i in (0, 9, 15):
+        lst = oracle.yl_plan(pal, int(pal[i]), 4)
+        assert np.all(lst == i) and lst.size >= 4   # an exact palette colour: mixing it with itself wins
+    gray = synth.rgb_pack(*([np.arange(16) * 17] * 3)).astype(np.int32)
+    lst = oracle.yl_plan(gray, int(synth.rgb_pack(25, 25, 25)), 8)  # between entries 1 (17) and 2 (34)
+    assert set(lst.tolist()) <= {1, 2}
+
+
+def test_dither_tiles_yl_composition(oracle):
+    """or_dither_tiles_yl = per-pixel plan -> list[cDitheringMap * count shr 6] -> PrepareTileMirrors."""
+    rng = np.random.default_rng(9)
+    pals = np.stack([_palette(rng, ties=k % 2 == 1) for k in range(3)])
+    rgb = synth.frame_tiles(rng, 6)
+    pal_of = rng.integers(0, 3, 6).astype(np.int32)
+    px, hm, vm = oracle.dither_tiles_yl(rgb, pal_of, pals, 4)
+    raw = np.zeros((6, 64), np.uint8)
+    for t in range(6):
+        for k in range(64):
+            lst = oracle.yl_plan(pals[pal_of[t]], int(rgb[t, k]), 4)
+            raw[t, k] = lst[(MAP[k] * lst.size) >> 6]
+    cpx, chm, cvm = synth.prepare_tile_mirrors(raw)
+    assert np.array_equal(px, cpx.reshape(6, 64)) and np.array_equal(hm, chm) and np.array_equal(vm, cvm)

@@ -52,3 +52,43 @@ def test_dither_rejects_bad_input(gpu):
         dither_tiles(rgb, np.array([0, 5], np.int32), np.zeros((2, 16), np.int32))   # palette index out of range
     with pytest.raises(TilerError):
         dither_tiles(rgb, np.array([0, 0], np.int32), np.zeros((2, 12), np.int32))   # palsize not a power of two
+
+
+@pytest.mark.parametrize("mixed", [1, 2, 4, 8, 16])
+def test_dither_yliluoma_bit_exact(gpu, oracle, mixed):
+    """The Yliluoma branch (chkUseTK off; DeviseBestMixingPlanYliluoma's ASM_DBMP form, main.pas:1573-1826) at every
+    cbxYilMix setting: palette indices and mirror flags equal to the restatement, tie palettes included."""
+    rng = np.random.default_rng(500 + mixed)
+    n, P = 400, 6
+    rgb = synth.frame_tiles(rng, n)
+    pal_of = rng.integers(0, P, n).astype(np.int32)
+    pals = _palettes(rng, P, 16)
+    g = dither_tiles(rgb, pal_of, pals, yliluoma_mix=mixed)
+    o = oracle.dither_tiles_yl(rgb, pal_of, pals, mixed)
+    for a, b in zip(g, o):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("size,mixed", [(5, 4), (8, 64), (1, 3), (16, 33)])
+def test_dither_yliluoma_sizes(gpu, oracle, size, mixed):
+    """Palette sizes that are not powers of two (the Yliluoma plan has no `c and (palsize - 1)` default), one entry,
+    and mixed counts beyond the form's choices up to the 64 supported (lists of up to 126 entries)."""
+    rng = np.random.default_rng(size * 100 + mixed)
+    n, P = 64, 3
+    rgb = synth.frame_tiles(rng, n)
+    pal_of = rng.integers(0, P, n).astype(np.int32)
+    pals = synth.rgb_pack(*rng.integers(0, 256, (3, P, size))).astype(np.int32)
+    g = dither_tiles(rgb, pal_of, pals, yliluoma_mix=mixed)
+    o = oracle.dither_tiles_yl(rgb, pal_of, pals, mixed)
+    for a, b in zip(g, o):
+        assert np.array_equal(a, b)
+
+
+def test_dither_yliluoma_rejects_bad_input(gpu):
+    rgb = np.zeros((2, 64), np.int32)
+    pal_of = np.array([0, 0], np.int32)
+    for mixed in (-1, 65):
+        with pytest.raises(TilerError):
+            dither_tiles(rgb, pal_of, np.zeros((1, 16), np.int32), yliluoma_mix=mixed)
+    with pytest.raises(TilerError):
+        dither_tiles(rgb, pal_of, np.zeros((1, 17), np.int32), yliluoma_mix=4)   # more than 16 palette entries

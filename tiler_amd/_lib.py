@@ -104,6 +104,10 @@ _SIGS = {
     "tiler_kmodes_compute": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
     "tiler_dither_tiles": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "tiler_dither_tiles_yliluoma": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                            c_void_p]),
+    "tiler_dither_tiles_yliluoma_dev": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                                c_void_p, c_void_p, c_void_p]),
     "tiler_dither_tiles_dev": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                        c_void_p]),
     "tiler_quantize_palettes": (c_int, [c_long, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,

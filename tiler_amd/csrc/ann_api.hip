@@ -1344,15 +1344,39 @@ int tiler_smooth_keyframe_dev(int F, int Q, int32_t *d_tile, int32_t *d_tmpidx, 
 int tiler_dither_tiles(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes, int n_palettes,
                        int palsize, uint8_t *palpix, uint8_t *hm, uint8_t *vm) {
     if (!ensure_init()) return -1;
-    return dither_tiles_tk_host(n, rgb, pal_of, palettes, n_palettes, palsize, palpix, hm, vm);
+    return dither_tiles_host(n, rgb, pal_of, palettes, n_palettes, palsize, 0, palpix, hm, vm);
 }
 
 int tiler_dither_tiles_dev(int n, const int32_t *d_rgb, const int32_t *d_pal_of, const int32_t *d_palettes,
                            int n_palettes, int palsize, uint8_t *d_palpix, uint8_t *d_hm, uint8_t *d_vm, void *stream) {
     if (!ensure_init()) return -1;
     DevScope ds(ptr_device(d_rgb));
-    return dither_tiles_tk_dev(n, d_rgb, d_pal_of, d_palettes, n_palettes, palsize, d_palpix, d_hm, d_vm,
-                               (hipStream_t)stream);
+    return dither_tiles_dev(n, d_rgb, d_pal_of, d_palettes, n_palettes, palsize, 0, d_palpix, d_hm, d_vm,
+                            (hipStream_t)stream);
+}
+
+int tiler_dither_tiles_yliluoma(int n, const int32_t *rgb, const int32_t *pal_of, const int32_t *palettes,
+                                int n_palettes, int palsize, int mixed_colors, uint8_t *palpix, uint8_t *hm,
+                                uint8_t *vm) {
+    if (!ensure_init()) return -1;
+    if (mixed_colors < 1) {
+        set_error("dither: Yliluoma mixed colours must be 1..64");
+        return -1;
+    }
+    return dither_tiles_host(n, rgb, pal_of, palettes, n_palettes, palsize, mixed_colors, palpix, hm, vm);
+}
+
+int tiler_dither_tiles_yliluoma_dev(int n, const int32_t *d_rgb, const int32_t *d_pal_of, const int32_t *d_palettes,
+                                    int n_palettes, int palsize, int mixed_colors, uint8_t *d_palpix, uint8_t *d_hm,
+                                    uint8_t *d_vm, void *stream) {
+    if (!ensure_init()) return -1;
+    if (mixed_colors < 1) {
+        set_error("dither: Yliluoma mixed colours must be 1..64");
+        return -1;
+    }
+    DevScope ds(ptr_device(d_rgb));
+    return dither_tiles_dev(n, d_rgb, d_pal_of, d_palettes, n_palettes, palsize, mixed_colors, d_palpix, d_hm, d_vm,
+                            (hipStream_t)stream);
 }
 
 int tiler_quantize_palettes(long n_tiles, const int32_t *rgb, const int32_t *pal_of, const uint8_t *active,

@@ -221,6 +221,9 @@ def main():
     orbit = kernels["nn_orbit"]["launches"] > 0
     sl = kernels["nn_orbit"] if orbit else kernels["nn_shortlist"]
     sec = sl["ms_avg"] * 1e-3 if sl["ms_avg"] else None
+    # launches of the dominant kernel per step: 2 when the search runs its query halves as two launches (orbit.hip
+    # ORB_SPLIT_TAILS); the flops below are per launch, like the HIP-event and rocprofv3 per-dispatch times
+    lps = max(1, round(sl["launches"] / args.steps)) if sl["launches"] else 1
     # the contraction this algorithm performs: the orbit kernel scores a tile's 4 mirrors with ONE 192-deep
     # fp16 contraction (2*G*D flops per query, G = tile orbits); the brute-force form is 2*M*D (M = candidates)
     # the MFMA work actually issued: k-steps of 16 dims x 32 groups per query (12 per block of groups; the blocks of
@@ -228,9 +231,9 @@ def main():
     ksteps = stats.get("orbit_ksteps") or 0
     nflat = stats.get("flat_queries") or 0  # flat tiles, grouped last: 3 k-steps per candidate block
     gblk = ((stats["orbit_groups"] or 0) + 31) // 32
-    issued_launch = (2.0 * 32 * 16 * (ksteps * (QK - nflat) + 3 * gblk * nflat)) if (orbit and ksteps) else \
-        2.0 * (stats["orbit_groups"] if orbit else M) * 192 * QK
-    bruteforce_launch = 2.0 * M * 192 * QK
+    issued_launch = ((2.0 * 32 * 16 * (ksteps * (QK - nflat) + 3 * gblk * nflat)) if (orbit and ksteps) else
+                     2.0 * (stats["orbit_groups"] if orbit else M) * 192 * QK) / lps
+    bruteforce_launch = 2.0 * M * 192 * QK / lps
     issued = issued_launch / sec / 1e12 if sec else None
     effective = bruteforce_launch / sec / 1e12 if sec else None
     kname = "nn_orbit_shortlist_pipe_kernel" if orbit else "nn_shortlist16_kernel"
@@ -243,7 +246,7 @@ def main():
                 "unit": "TFLOP/s", "frac": round(issued / PEAK_F16_TFLOPS, 4) if issued else None,
                 "traffic": traffic, "traffic_unit": "bytes/launch (HBM, FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": traffic_src, "kernel": ORBIT_KERNEL if orbit else GENERIC_KERNEL,
-                "kernel_ms_avg": sl["ms_avg"],
+                "kernel_ms_avg": sl["ms_avg"], "launches_per_step": lps,
                 "flops_per_launch": issued_launch,
                 "effective_tflops": round(effective, 2) if effective else None,
                 "effective_speedup": round(bruteforce_launch / issued_launch, 4),
@@ -255,7 +258,9 @@ def main():
                          "12 per block of 32 mirror orbits, fewer on the blocks of mirror-symmetric tiles whose zero "
                          "isotypic blocks are skipped, 3 per block for the flat query tiles grouped last; = 2*G*D "
                          "without them) / its "
-                         "average launch time (HIP events on the launch stream) vs the dense fp16 peak; "
+                         "average launch time (HIP events on the launch stream) vs the dense fp16 peak -- per launch: "
+                         "a step's search runs two query halves as two launches, the first half's rescore and pair "
+                         "pass on a second stream beside the second launch, whose time includes that; "
                          "effective_tflops = the brute-force 2*M*D per query over the same time (effective_speedup = "
                          "brute-force / issued flops: the exact 4-mirror orbit algebra and the skipped zero blocks). hbm = the metric's '% HBM roofline': SURVEY.md 8(d) "
                          "bytes per matched tile x tiles / ms_per_step -- small by construction, the search is "

@@ -66,7 +66,7 @@ static std::vector<TimedPair> g_times;
 static bool g_timing = false;
 bool timing_enabled() { return g_timing; }
 KTimer::KTimer(const char *n, hipStream_t s) : name(n), stream(s) {
-    if (!g_timing) return;
+    if (!g_timing || !n) return;  // a null name: no timer
     hipEvent_t a, b;
     if (hipEventCreate(&a) != hipSuccess) return;
     if (hipEventCreate(&b) != hipSuccess) {

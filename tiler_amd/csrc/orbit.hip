@@ -52,6 +52,14 @@ static constexpr int OS = 12;   // k-steps of 16 (4 isotypic blocks x 3)
 #ifndef ORB_RS_DPP
 #define ORB_RS_DPP 1  // rescore / pair pass reductions: DPP lane moves inside each row of 16, one ds_bpermute across rows
 #endif
+#ifndef ORB_SPLIT_TAILS
+// 1: the shortlist in two query halves, the first half's rescore + pair pass on a second stream beside the second
+// launch.  Measured (r06z, profiles/r06/z_split_tails_ab.txt, same box, same digest): C3 step 14.75 -> 14.61 ms, but the
+// second launch absorbs the overlapped tails (shortlist 13.07 -> 13.40 ms, roofline.frac 0.458 -> 0.44) and the
+// tails' own event times stop meaning their cost; a 1 % step gain does not pay for measurements that no longer
+// isolate the kernels, so it stays off (an A/B switch)
+#define ORB_SPLIT_TAILS 0
+#endif
 #ifndef ORB_PR_QUAD
 #define ORB_PR_QUAD 1  // nn_orbit_pairs_kernel: the query row loaded once per quad of slot lanes, broadcast by DPP (r06o: 0.50 -> 0.42 ms)
 #endif
@@ -722,7 +730,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
                                                                          int *__restrict__ out_id, int red_end,
                                                                          const uint8_t *__restrict__ bmask,
                                                                          int flat_wg0, const uint8_t *__restrict__ bmask0,
-                                                                         const int *__restrict__ flat_cnt) {
+                                                                         const int *__restrict__ flat_cnt,
+                                                                         int flat_base) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int FRAG_BYTES = CB * OS * 1024;
     constexpr int BUF_BYTES = FRAG_BYTES + CB * 128;
@@ -768,7 +777,8 @@ __global__ __launch_bounds__(NW * 64, 1) void nn_orbit_shortlist_pipe_kernel(con
     // workgroups from flat_wg0 on hold flat query tiles only (q' block 0): every candidate block block-serially with
     // k-steps 0..2, only those streamed
     // (flat_cnt: the device count of non-flat queries -> first all-flat workgroup; flat_wg0 bounds it)
-    if (flat_cnt) flat_wg0 = min(flat_wg0, (*flat_cnt + NW * QB * 32 - 1) / (NW * QB * 32));
+    // (flat_base: the launch's first query, when it covers a later part of the batch)
+    if (flat_cnt) flat_wg0 = min(flat_wg0, (max(0, *flat_cnt - flat_base) + NW * QB * 32 - 1) / (NW * QB * 32));
     const bool flat = (int)blockIdx.x >= flat_wg0;
     const int nks = flat ? 3 : OS;
     if (flat) {
@@ -1150,6 +1160,7 @@ struct OrbitRescoreArgs {
     const float *key;
     const int *id;
     int G, nq, L, nsplit;
+    int q0;                         // first query of the launch (the launch covers [q0, nq))
     int p1;                         // entries re-keyed in the first pass (1..4)
     int *pair_cnt;                  // [nq] candidates handed to the pair pass (0: settled here or by tiers 2/3)
     int *pair_cand;                 // [nq][ORB_PSLOTS]
@@ -1374,7 +1385,7 @@ __device__ __forceinline__ unsigned half_ballot(bool p) {
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_RS_WAVES))) void nn_orbit_rescore_kernel(OrbitRescoreArgs a) {
     const int l = threadIdx.x & 31, hq = threadIdx.x >> 5;  // lane in the half, query slot of the block
     const int hbase = threadIdx.x & 32;                     // first lane of this half in the wave
-    const long q = (long)blockIdx.x * 8 + hq;
+    const long q = (long)blockIdx.x * 8 + hq + a.q0;
     if (q >= a.nq) return;
     const OrbitTail &t = a.t;
     const OrbitStat st = a.ostat[q];
@@ -1569,7 +1580,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_PR_WAVE
 __global__ __launch_bounds__(256) void nn_orbit_pairs_kernel(OrbitRescoreArgs a) {
 #endif
     const long gid = (long)blockIdx.x * 256 + threadIdx.x;
-    const long q = gid / ORB_PSLOTS;
+    const long q = gid / ORB_PSLOTS + a.q0;
     const int s = (int)(gid % ORB_PSLOTS);
     float bd = INFINITY;
     if (q >= a.nq) return;  // whole groups: 256 % ORB_PSLOTS == 0
@@ -2171,6 +2182,9 @@ void orbit_destroy(OrbitIndex *o, bool synced) {
     dfree(o->d_stats);
     dfree(o->key);
     dfree(o->id);
+    if (o->tail_stream) stream_put(o->tail_stream);
+    if (o->ev_half) (void)hipEventDestroy(o->ev_half);
+    if (o->ev_tail) (void)hipEventDestroy(o->ev_tail);
     delete o;
 }
 
@@ -2420,6 +2434,18 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     if (flat_cnt) mix_full = 0;
     const int bps = (o->gblk + nsplit - 1) / nsplit;
     nsplit = (o->gblk + bps - 1) / bps;
+    // Two query halves (whole rounds of n_cu workgroups first): the first half's rescore and pair pass -- latency-bound
+    // kernels -- run on the index's second stream while the second half's shortlist runs, instead of after it.
+    int split_q = 0;
+    if (ORB_SPLIT_TAILS && !mix_full && wgs >= 2 * n_cu) {
+        const int wa = std::max(1, (wgs / 2 + n_cu / 2) / n_cu) * n_cu;
+        if (wa < wgs && (long)wa * qpw_q < nq) {
+            if (!o->tail_stream) TILER_HIP_CHECK(stream_get(&o->tail_stream));
+            if (!o->ev_half) TILER_HIP_CHECK(hipEventCreateWithFlags(&o->ev_half, hipEventDisableTiming));
+            if (!o->ev_tail) TILER_HIP_CHECK(hipEventCreateWithFlags(&o->ev_tail, hipEventDisableTiming));
+            split_q = wa * qpw_q;
+        }
+    }
     if (orbit_ensure_queries(o, nq)) return -1;
     const size_t nkeys = (size_t)nq * nsplit * 2 * ORB_L;
     if (nkeys > o->cap_keys) {
@@ -2443,13 +2469,33 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     }
     {
         const size_t lds = 2 * ((size_t)ORB_CB * OS * 1024 + ORB_CB * 128);
-        KTimer tm("nn_orbit", stream);
+        // one timer per launch (the query-half split makes two per search: their per-dispatch times match a trace's)
+        KTimer tm(split_q > 0 ? nullptr : "nn_orbit", stream);
 #define ORB_PIPE(MD)                                                                                              \
     hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, ORB_QB, MD>), dim3(wgs, nsplit),              \
                        dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,                   \
                        (const half8 *)o->qfrag, nq, bps, nsplit, o->key, o->id, o->red_end, o->d_bmask,                \
-                       0x7fffffff, o->d_bmask0, MD == 0 ? flat_cnt : nullptr)
-        if (!mix_full) ORB_PIPE(0);
+                       0x7fffffff, o->d_bmask0, MD == 0 ? flat_cnt : nullptr, 0)
+        if (!mix_full && split_q == 0) ORB_PIPE(0);
+        if (split_q > 0) {  // two launches over query halves; the end of the first one is the tails' start
+            const int qb_off = split_q / 32;
+            const size_t per_q = (size_t)nsplit * 2 * ORB_L;
+            {
+                KTimer ta("nn_orbit", stream);
+                hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, ORB_QB, 0>),
+                                   dim3(split_q / qpw_q, nsplit), dim3(ORB_NW * 64), lds, stream,
+                                   (const half8 *)o->d_frag, o->d_seed, o->gblk, (const half8 *)o->qfrag, split_q, bps,
+                                   nsplit, o->key, o->id, o->red_end, o->d_bmask, 0x7fffffff, o->d_bmask0, flat_cnt, 0);
+            }
+            TILER_HIP_CHECK(hipEventRecord(o->ev_half, stream));
+            KTimer tb("nn_orbit", stream);
+            hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, ORB_QB, 0>),
+                               dim3(wgs - split_q / qpw_q, nsplit), dim3(ORB_NW * 64), lds, stream,
+                               (const half8 *)o->d_frag, o->d_seed, o->gblk,
+                               (const half8 *)o->qfrag + (size_t)qb_off * OS * 64, nq - split_q, bps, nsplit,
+                               o->key + (size_t)split_q * per_q, o->id + (size_t)split_q * per_q, o->red_end,
+                               o->d_bmask, 0x7fffffff, o->d_bmask0, flat_cnt, split_q);
+        }
         if (mix_full) {
             const int qb_off = mix_full * ORB_NW * ORB_QB, q_off = qb_off * 32;  // query blocks / queries of part A
             const size_t per_q = (size_t)nsplit * 2 * ORB_L;
@@ -2459,14 +2505,14 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
             hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, ORB_QB, 0>), dim3(mix_full, 1),
                                dim3(ORB_NW * 64), lds, stream, (const half8 *)o->d_frag, o->d_seed, o->gblk,
                                (const half8 *)o->qfrag, nq, o->gblk, nsplit, o->key, o->id, o->red_end, o->d_bmask,
-                               0x7fffffff, o->d_bmask0, nullptr);
+                               0x7fffffff, o->d_bmask0, nullptr, 0);
             if (nq > q_off)
                 hipLaunchKernelGGL((nn_orbit_shortlist_pipe_kernel<ORB_L, ORB_CB, ORB_NW, ORB_QB, 0>),
                                    dim3(wgs - mix_full, nsplit), dim3(ORB_NW * 64), lds, stream,
                                    (const half8 *)o->d_frag, o->d_seed, o->gblk,
                                    (const half8 *)o->qfrag + (size_t)qb_off * OS * 64, nq - q_off, bps, nsplit,
                                    o->key + (size_t)q_off * per_q, o->id + (size_t)q_off * per_q, o->red_end,
-                                   o->d_bmask, 0x7fffffff, o->d_bmask0, nullptr);
+                                   o->d_bmask, 0x7fffffff, o->d_bmask0, nullptr, 0);
         }
 #undef ORB_PIPE
     }
@@ -2487,6 +2533,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     ra.id = o->id;
     ra.G = o->G;
     ra.nq = nq;
+    ra.q0 = 0;
     ra.L = ORB_L;
     ra.nsplit = nsplit;
     ra.p1 = 2;
@@ -2507,18 +2554,34 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
         TILER_HIP_CHECK(hipMemsetAsync(o->d_stats, 0, 2 * sizeof(int), stream));
         ra.t.n_expand = o->d_stats;
     }
-    {
-        KTimer tm("nn_rescore", stream);
-        hipLaunchKernelGGL(nn_orbit_rescore_kernel, dim3((nq + 7) / 8), dim3(256), 0, stream, ra);
+    // the rescore and pair pass of queries [q0, q1) on stream s
+    auto tails = [&](int q0, int q1, hipStream_t s) -> int {
+        OrbitRescoreArgs r = ra;
+        r.q0 = q0;
+        r.nq = q1;
+        {
+            KTimer tm("nn_rescore", s);
+            hipLaunchKernelGGL(nn_orbit_rescore_kernel, dim3((unsigned)((q1 - q0 + 7) / 8)), dim3(256), 0, s, r);
+        }
+        TILER_HIP_CHECK(hipGetLastError());
+        {
+            static_assert(256 % ORB_PSLOTS == 0, "pair groups must not straddle blocks");
+            KTimer tm("nn_pairs", s);
+            const long lanes = (long)(q1 - q0) * ORB_PSLOTS;
+            hipLaunchKernelGGL(nn_orbit_pairs_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, s, r);
+        }
+        TILER_HIP_CHECK(hipGetLastError());
+        return 0;
+    };
+    if (split_q > 0) {
+        TILER_HIP_CHECK(hipStreamWaitEvent(o->tail_stream, o->ev_half, 0));
+        if (tails(0, split_q, o->tail_stream)) return -1;
+        TILER_HIP_CHECK(hipEventRecord(o->ev_tail, o->tail_stream));
+        if (tails(split_q, nq, stream)) return -1;
+        TILER_HIP_CHECK(hipStreamWaitEvent(stream, o->ev_tail, 0));  // tier 2 / 3 and the caller after both halves
+    } else if (tails(0, nq, stream)) {
+        return -1;
     }
-    TILER_HIP_CHECK(hipGetLastError());
-    {
-        static_assert(256 % ORB_PSLOTS == 0, "pair groups must not straddle blocks");
-        KTimer tm("nn_pairs", stream);
-        const long lanes = (long)nq * ORB_PSLOTS;
-        hipLaunchKernelGGL(nn_orbit_pairs_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, ra);
-    }
-    TILER_HIP_CHECK(hipGetLastError());
     if (want_stats) {
         int h[2];
         TILER_HIP_CHECK(hipMemcpyAsync(h, o->d_stats, sizeof(h), hipMemcpyDeviceToHost, stream));

@@ -67,6 +67,9 @@ struct OrbitIndex {
     size_t cap_keys = 0;
     int *d_stats = nullptr;         // [2] expansion passes, candidates rescored (TILER_ORBIT_STATS=1)
     long long last_expansions = 0, last_rescored = 0;
+    // the first query half's rescore and pair pass run on their own stream beside the second half's shortlist
+    hipStream_t tail_stream = nullptr;
+    hipEvent_t ev_half = nullptr, ev_tail = nullptr;
 };
 
 // generic tier-2 / tier-3 plumbing the orbit rescore feeds (owned by nn_search.hip)

@@ -99,6 +99,7 @@ def parser():
     ap.add_argument("--check-items", type=int, default=1000, help="items whose k = 8 search is re-checked")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host cores this process may use (benchutil)")
     ap.add_argument("--seed", type=int, default=20261017)
+    ap.add_argument("--lib", default="", help="a libANN.so build to load instead of tiler_amd/lib/libANN.so (A/B)")
     return ap
 
 
@@ -111,6 +112,9 @@ def run(args) -> dict:
     from tiler_amd import synth
     from tiler_amd._lib import check
 
+    if getattr(args, "lib", ""):
+        import tiler_amd._lib as _l
+        _l.LIB_PATH = os.path.abspath(args.lib)
     lib = tiler_amd.load()
     devi = torch.cuda.current_device() if torch.cuda.is_initialized() else 0
     check(lib.tiler_init(devi), "tiler_init")

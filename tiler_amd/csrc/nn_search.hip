@@ -1782,6 +1782,11 @@ static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
 // blocks of 32 per wave, so 64 * NW queries per workgroup
 static constexpr int GEN_NW_S4 = 4;
 static constexpr int GEN_QB_S4 = 1;  // query blocks per wave there: 16,384 items x 4 splits fill 2 waves per SIMD
+#ifndef GEN_QB_S4_BIG
+#define GEN_QB_S4_BIG 2  // ... and from 32,768 items (whole-tileset keyframes: ~64k) two, each A fragment feeding 2 MFMAs
+                         // (r06qb, profiles/r06/qb_preselect_qb2_encoder_ab.txt: whole-tileset loop 9.51 -> 9.59 Mtiles/s)
+#endif
+static int gen_qb_s4(int nq) { return nq >= 32768 ? GEN_QB_S4_BIG : GEN_QB_S4; }
 
 template <int S, int L, int CB, int NW, int QB = 2>
 static void launch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
@@ -1852,7 +1857,12 @@ static int launch_shortlist16(NNIndex *ix, int nq, int nsplit, int bps, bool gat
 template <int L>
 static int dispatch_shortlist(NNIndex *ix, int nq, int nsplit, int bps, hipStream_t stream) {
     switch (ix->S) {
-        case 4: launch_shortlist<4, L, 6, GEN_NW_S4, GEN_QB_S4>(ix, nq, nsplit, bps, stream); break;
+        case 4:
+            if (gen_qb_s4(nq) == 2)
+                launch_shortlist<4, L, 6, GEN_NW_S4, 2>(ix, nq, nsplit, bps, stream);
+            else
+                launch_shortlist<4, L, 6, GEN_NW_S4, GEN_QB_S4>(ix, nq, nsplit, bps, stream);
+            break;
         case 8: launch_shortlist<8, L, 3, 4>(ix, nq, nsplit, bps, stream); break;
         case 12: launch_shortlist<12, L, 2, 8>(ix, nq, nsplit, bps, stream); break;
         case 16: launch_shortlist<16, L, 2, 4>(ix, nq, nsplit, bps, stream); break;
@@ -2115,7 +2125,7 @@ static int search_core(NNIndex *ix, RescoreArgs &ra, const float *d_q, int nq, i
     const int lpq = v16 ? 4 : 2;
     const int nblk = v16 ? ix->nblk16 : ix->nblk;
     const int max_split = 64 / (lpq * L);
-    const int qpwg = v16 ? SL16_NW * SL16_QB * 16 : (ix->S == 12 ? 512 : ix->S == 4 ? 32 * GEN_QB_S4 * GEN_NW_S4 : 256);
+    const int qpwg = v16 ? SL16_NW * SL16_QB * 16 : (ix->S == 12 ? 512 : ix->S == 4 ? 32 * gen_qb_s4(nq) * GEN_NW_S4 : 256);
     const int wgs = (nq + qpwg - 1) / qpwg;
     int nsplit = std::max(1, std::min(max_split, (1024 + wgs - 1) / wgs));
     nsplit = std::min(nsplit, nblk);

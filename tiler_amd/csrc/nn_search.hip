@@ -1726,8 +1726,13 @@ static constexpr int TIER2_CAP = 1024;   // generic tier 2: collected candidates
 
 static int ensure_scratch(NNIndex *ix, long nq, long nkeys) {
     SearchScratch &s = ix->scratch;
-    if ((size_t)nq > s.cap_q || (size_t)nkeys > s.cap_keys)
-        (void)hipDeviceSynchronize();  // the outgrown buffers go back to the block cache: earlier searches must be done
+    // the outgrown buffers go back to the block cache: earlier searches must be done.  A handle's first call has
+    // nothing to file, and a device-wide wait there would also wait for other streams' work (the encoder's next
+    // Prepare, running beside this FrameTiling)
+    const bool q_held = s.qfrag || s.qfrag16 || s.qstat || s.fb_list || s.fb_count || s.thr || s.gate || s.ex_list ||
+                        s.kd_list || s.kd_rootbox || s.kd_done || s.t2best;
+    if (((size_t)nq > s.cap_q && q_held) || ((size_t)nkeys > s.cap_keys && (s.key || s.idx)))
+        (void)hipDeviceSynchronize();
     if ((size_t)nq > s.cap_q) {
         dfree(s.qfrag);
         dfree(s.qfrag16);
@@ -2353,7 +2358,7 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
     }
     SearchScratch &s = ix->scratch;
     if ((size_t)Q > s.cap_rows) {
-        (void)hipDeviceSynchronize();  // the outgrown buffer goes back to the block cache: earlier searches must be done
+        if (s.qrows) (void)hipDeviceSynchronize();  // the outgrown buffer goes back to the block cache (ensure_scratch)
         dfree(s.qrows);
         s.qrows = nullptr;
         s.cap_rows = 0;
@@ -2373,7 +2378,8 @@ int nn_frame_tiling_dev(NNIndex *ix, const int32_t *d_rgb, int Q, int use_wavele
         if (!noflat && Q >= 8192 && (flat_generic || ((const OrbitIndex *)ix->orbit)->gblk >= 1024)) {
             const int nb = (Q + 255) / 256;
             if ((size_t)Q > s.cap_flat) {
-                (void)hipDeviceSynchronize();  // (as above)
+                if (s.fperm || s.fbcnt || s.fflag || s.fidx || s.ferr || s.ftile || s.fpal || s.fhm || s.fvm)
+                    (void)hipDeviceSynchronize();  // (as above)
                 dfree(s.fperm);
                 dfree(s.fbcnt);
                 dfree(s.fflag);

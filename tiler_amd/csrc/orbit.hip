@@ -2385,7 +2385,8 @@ static constexpr int ORB_L = 4, ORB_CB = 4, ORB_NW = 8, ORB_QB = 2;
 int orbit_ensure_queries(OrbitIndex *o, int nq) {
     if ((size_t)nq <= o->cap_q) return 0;
     const long nqblk = (nq + 31) / 32;
-    (void)hipDeviceSynchronize();  // the smaller buffers go back to the block cache: earlier searches must be done
+    if (o->qfrag || o->qstat || o->pair_cnt || o->pair_cand)  // (a first call has nothing to file: ensure_scratch)
+        (void)hipDeviceSynchronize();  // the smaller buffers go back to the block cache: earlier searches must be done
     dfree(o->qfrag);
     dfree(o->qstat);
     dfree(o->pair_cnt);
@@ -2471,7 +2472,7 @@ int orbit_search(NNIndex *ix, const float *d_q, int nq, const OrbitTail &tail, h
     if (orbit_ensure_queries(o, nq)) return -1;
     const size_t nkeys = (size_t)nq * nsplit * 2 * ORB_L;
     if (nkeys > o->cap_keys) {
-        (void)hipDeviceSynchronize();  // (as orbit_ensure_queries)
+        if (o->key || o->id) (void)hipDeviceSynchronize();  // (as orbit_ensure_queries)
         dfree(o->key);
         dfree(o->id);
         o->key = nullptr;

@@ -94,6 +94,10 @@ def parser():
                     help="1: the next keyframe's Prepare on a high-priority stream (its short kernels and host syncs "
                          "then get CUs as FrameTiling's workgroups retire instead of after the whole grid); 0: normal")
     ap.add_argument("--no-smooth", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1: keyframe k + 1's FrameTiling queued behind k's as soon as its Prepare ends, Smooth on a third "
+                         "stream, handles closed by a closer thread (A/B study: whole tileset +1 %%, shot-local -4 %%, "
+                         "profiles/r06/pp_encoder_pipeline_ab.txt); 0: the host waits for each keyframe before the next")
     ap.add_argument("--check-kf", type=int, default=1, help="keyframe re-checked against the restatement (-1: none)")
     ap.add_argument("--check-queries", type=int, default=1500)
     ap.add_argument("--check-items", type=int, default=1000, help="items whose k = 8 search is re-checked")
@@ -198,6 +202,103 @@ def run(args) -> dict:
             stats_kf.update(kt.stats())
 
     kept = {}
+    s_sm = torch.cuda.Stream(dev)  # --pipeline: keyframe k's Smooth, beside keyframe k + 1's FrameTiling
+
+    def run_pipelined(gds, keep):
+        """FrameTiling k + 1 is queued on its stream behind FrameTiling k as soon as Prepare k + 1 has ended, so the GPU
+        does not wait for the host between keyframes; Smooth k runs on a third stream once FrameTiling k's event has
+        fired (its host sync then waits for k alone); a finished keyframe's handle is closed by a closer thread (the
+        close synchronises the device before filing the handle's blocks, which would otherwise hold up the queueing)."""
+        nonlocal_ft = {}
+        box = {}
+        closing = []
+        closer_go = threading.Event()
+        closer_stop = [False]
+
+        def closer():
+            while True:
+                closer_go.wait()
+                closer_go.clear()
+                while closing:
+                    closing.pop(0).close()
+                if closer_stop[0] and not closing:
+                    return
+
+        ct = threading.Thread(target=closer)
+        ct.start()
+
+        def launch_ft(k, kt):
+            o = outs[k]
+            n = (starts[k + 1] - starts[k]) * Q
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(s_ft)
+            check(lib.tiler_frame_tiling_dev(kt.handle, vp(frames[k].data_ptr()), n, 1, -1, vp(o["tile"].data_ptr()),
+                                             vp(o["pal"].data_ptr()), vp(o["hm"].data_ptr()), vp(o["vm"].data_ptr()),
+                                             vp(o["err"].data_ptr()), vp(s_ft.cuda_stream)), "tiler_frame_tiling_dev")
+            e1.record(s_ft)
+            nonlocal_ft[k] = (e0, e1)
+
+        def smooth(k):
+            F = starts[k + 1] - starts[k]
+            o = outs[k]
+            e0, e1 = nonlocal_ft[k]
+            s_sm.wait_event(e1)
+            es0 = torch.cuda.Event(enable_timing=True)
+            es1 = torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(s_sm):
+                es0.record(s_sm)
+                st = {nm: o[nm].view(F, Q).clone() for nm in ("tile", "pal", "hm", "vm")}
+                st["smoothed"] = torch.zeros((F, Q), dtype=torch.uint8, device=dev)
+            check(lib.tiler_smooth_keyframe_dev(F, Q, vp(st["tile"].data_ptr()), None, vp(st["pal"].data_ptr()),
+                                                vp(st["hm"].data_ptr()), vp(st["vm"].data_ptr()),
+                                                vp(st["smoothed"].data_ptr()), vp(d_tiles.data_ptr()),
+                                                vp(d_pals.data_ptr()), 0.02, vp(s_sm.cuda_stream)),
+                  "tiler_smooth_keyframe_dev")
+            es1.record(s_sm)
+            sm[k] = st
+            return es0, es1
+
+        def start_prep(k1):
+            if k1 < nkf:
+                w = threading.Thread(target=lambda: box.__setitem__(k1, prepare(k1, gds, s_prep)))
+                w.start()
+                return w
+            return None
+
+        w = start_prep(0)
+        w.join()
+        kts = {0: box.pop(0)}
+        w = start_prep(1)
+        launch_ft(0, kts[0])
+        for k in range(nkf):
+            if k + 1 < nkf:
+                tj = time.perf_counter()
+                w.join()
+                times["join"].append(time.perf_counter() - tj)
+                kts[k + 1] = box.pop(k + 1)
+                w = start_prep(k + 2)  # before the launch: FrameTiling k + 1 may wait on the host for k's end
+                launch_ft(k + 1, kts[k + 1])
+            if not args.no_smooth:
+                es = smooth(k)
+            e0, e1 = nonlocal_ft[k]
+            e1.synchronize()
+            t_ft = e0.elapsed_time(e1)
+            if not args.no_smooth:
+                es[1].synchronize()
+                t_ft += es[0].elapsed_time(es[1])
+            times["ft_smooth"].append(t_ft * 1e-3)
+            kt = kts.pop(k)
+            if k == args.check_kf or (k == 0 and args.check_kf < 0):
+                stats_kf.update(kt.stats())
+            if k == args.check_kf and keep:
+                kept["kt"] = kt
+            else:
+                closing.append(kt)
+                closer_go.set()
+        closer_stop[0] = True
+        closer_go.set()
+        ct.join()
 
     def run_clip(keep=False):
         for v in times.values():
@@ -215,6 +316,8 @@ def run(args) -> dict:
                     kept["kt"] = kt
                 else:
                     kt.close()
+        elif args.pipeline:
+            run_pipelined(gds, keep)
         else:
             box = {}
             worker = threading.Thread(target=lambda: box.__setitem__(0, prepare(0, gds, s_prep)))

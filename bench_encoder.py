@@ -98,6 +98,10 @@ def parser():
                     help="1: keyframe k + 1's FrameTiling queued behind k's as soon as its Prepare ends, Smooth on a third "
                          "stream, handles closed by a closer thread (A/B study: whole tileset +1 %%, shot-local -4 %%, "
                          "profiles/r06/pp_encoder_pipeline_ab.txt); 0: the host waits for each keyframe before the next")
+    ap.add_argument("--async-close", type=int, default=1,
+                    help="1: the previous keyframe's handle is closed by a closer thread (its device-wide synchronisation "
+                         "and block filing off the host path between two keyframes: +0.7 %% both item modes, "
+                         "profiles/r06/ac_encoder_async_close_ab.txt); 0: closed before the next launch")
     ap.add_argument("--check-kf", type=int, default=1, help="keyframe re-checked against the restatement (-1: none)")
     ap.add_argument("--check-queries", type=int, default=1500)
     ap.add_argument("--check-items", type=int, default=1000, help="items whose k = 8 search is re-checked")
@@ -323,6 +327,7 @@ def run(args) -> dict:
             worker = threading.Thread(target=lambda: box.__setitem__(0, prepare(0, gds, s_prep)))
             worker.start()
             prev = None
+            closers = []
             for k in range(nkf):
                 tj = time.perf_counter()
                 worker.join()
@@ -330,7 +335,11 @@ def run(args) -> dict:
                 kt = box.pop(k)
                 tc = time.perf_counter()
                 if prev is not None and prev is not kept.get("kt"):
-                    prev.close()  # keyframe k-1 is finished and nothing else is in flight: its frees cost nothing
+                    if args.async_close:  # the close waits for the device, so not on the launching thread
+                        closers.append(threading.Thread(target=prev.close))
+                        closers[-1].start()
+                    else:
+                        prev.close()  # keyframe k-1 is finished and nothing else is in flight: its frees cost nothing
                 times["close"].append(time.perf_counter() - tc)
                 if k + 1 < nkf:
                     worker = threading.Thread(target=lambda k1=k + 1: box.__setitem__(k1, prepare(k1, gds, s_prep)))
@@ -339,6 +348,8 @@ def run(args) -> dict:
                 if k == args.check_kf and keep:
                     kept["kt"] = kt  # the re-checked keyframe's candidate set is read back after the timed region
                 prev = kt
+            for c in closers:
+                c.join()
             if prev is not kept.get("kt"):
                 prev.close()
         torch.cuda.synchronize(dev)
